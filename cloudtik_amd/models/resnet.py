@@ -1,0 +1,131 @@
+"""ResNet-50 (v1.5) for the reference's image-recognition workloads.
+
+Parity targets: torchvision ``resnet50`` trained with SGD + DDP, channels_last + bf16
+(applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296,317,
+585-586) and the synthetic benchmark
+(examples/runtime/ai/basics/pytorch/imagenet-resnet50-synthetic-pytorch-distributed.py).
+
+MI355X layout: NHWC (channels_last) bf16 activations and weights; convolutions go to
+MIOpen; every BatchNorm is fused with its ReLU -- and, at the end of a bottleneck, with the
+residual add -- in ONE HIP kernel pair (csrc/batchnorm.hip: per-channel statistics with a
+Chan-merged parallel variance, then normalise+add+ReLU), instead of BN / add / ReLU as
+three separate memory passes.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from cloudtik_amd import ops
+
+
+class BatchNormAct(nn.Module):
+    """BatchNorm2d (+ optional residual add) (+ optional ReLU), NHWC, fused on GPU."""
+
+    def __init__(self, C, relu=True, eps=1e-5, momentum=0.1, zero_init=False, device=None,
+                 dtype=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.full((C,), 0.0 if zero_init else 1.0, device=device, dtype=dtype))
+        self.bias = nn.Parameter(torch.zeros(C, device=device, dtype=dtype))
+        self.register_buffer("running_mean", torch.zeros(C, device=device))
+        self.register_buffer("running_var", torch.ones(C, device=device))
+        self.relu, self.eps, self.momentum = relu, eps, momentum
+
+    def forward(self, x, residual=None):
+        return ops.batch_norm_act(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                  residual=residual, relu=self.relu, training=self.training,
+                                  momentum=self.momentum, eps=self.eps)
+
+
+def _conv(cin, cout, k, stride=1, device=None, dtype=None):
+    c = nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False, device=device, dtype=torch.float32)
+    nn.init.kaiming_normal_(c.weight, mode="fan_out", nonlinearity="relu")
+    return c.to(dtype) if dtype is not None else c
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, downsample=False, device=None, dtype=None):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        cout = width * self.expansion
+        self.conv1 = _conv(cin, width, 1, **kw)
+        self.bn1 = BatchNormAct(width, **kw)
+        self.conv2 = _conv(width, width, 3, stride, **kw)   # v1.5: stride on the 3x3
+        self.bn2 = BatchNormAct(width, **kw)
+        self.conv3 = _conv(width, cout, 1, **kw)
+        self.bn3 = BatchNormAct(cout, relu=True, zero_init=True, **kw)  # fused add + ReLU
+        self.down = None
+        if downsample:
+            self.down = _conv(cin, cout, 1, stride, **kw)
+            self.down_bn = BatchNormAct(cout, relu=False, **kw)
+
+    def forward(self, x):
+        idt = self.down_bn(self.down(x)) if self.down is not None else x
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), residual=idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        self.conv1 = _conv(3, 64, 7, 2, **kw)
+        self.bn1 = BatchNormAct(64, **kw)
+        cin = 64
+        stages = []
+        for i, (n, w) in enumerate(zip(layers, (64, 128, 256, 512))):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(Bottleneck(cin, w, stride, downsample=(j == 0), **kw))
+                cin = w * 4
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        fc = nn.Linear(cin, num_classes, device=device)
+        bound = 1.0 / math.sqrt(cin)
+        nn.init.uniform_(fc.weight, -bound, bound)
+        nn.init.uniform_(fc.bias, -bound, bound)
+        self.fc = fc.to(dtype)
+        if device is not None and torch.device(device).type == "cuda":
+            self.to(memory_format=torch.channels_last)
+
+    def forward(self, x):
+        x = self.bn1(self.conv1(x))
+        x = F.max_pool2d(x, 3, 2, 1)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000, device=None, dtype=torch.bfloat16):
+    return ResNet((3, 4, 6, 3), num_classes, device=device, dtype=dtype)
+
+
+def resnet18_like_small(num_classes=10, device=None, dtype=torch.float32):
+    """Tiny bottleneck ResNet for CPU tests."""
+    return ResNet((1, 1, 1, 1), num_classes, device=device, dtype=dtype)
+
+
+class ResNetTrainStep:
+    """forward -> CE loss -> backward (overlapped bucketed all-reduce) -> fused SGD."""
+
+    def __init__(self, model, optimizer, bucketer=None, scheduler=None):
+        self.model, self.opt, self.ddp, self.sched = model, optimizer, bucketer, scheduler
+
+    def __call__(self, x, y):
+        logits = self.model(x)
+        loss = F.cross_entropy(logits.float(), y)
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.finish()
+        self.opt.step()
+        if self.sched is not None:
+            self.sched.step()
+        self.opt.zero_grad()
+        return loss

@@ -1,0 +1,90 @@
+"""cloudtik_amd op library: hand-written CDNA4 (gfx950) HIP kernels + autograd wrappers.
+
+Dispatch rule (no silent fallback on the GPU path):
+
+* tensors on a ROCm device  -> the HIP kernel in ``_C`` is REQUIRED; if the extension
+  is missing the call raises (build it with ``python -m cloudtik_amd.ops.build``).
+* CPU tensors               -> a plain PyTorch reference implementation
+  (``cloudtik_amd.ops.reference``), used by the CPU test-suite and by gloo-only
+  configs (north-star config #1: MNIST MLP on CPU).
+
+The reference implementations double as the fp32 oracle the GPU numerics tests compare
+against.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+import torch
+
+from . import reference as ref
+
+_C_ERR = None
+try:  # the extension is built in-tree (see ops/build.py)
+    _C = importlib.import_module(__name__ + "._C")
+except Exception as e:  # pragma: no cover - depends on build state
+    _C = None
+    _C_ERR = e
+
+
+def native_available() -> bool:
+    return _C is not None
+
+
+def require_native():
+    if _C is None:
+        raise RuntimeError(
+            "cloudtik_amd HIP op library (_C) is not built or failed to load: %r. "
+            "Run `python -m cloudtik_amd.ops.build`." % (_C_ERR,))
+    return _C
+
+
+def _use_native(*tensors) -> bool:
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            require_native()
+            return True
+    return False
+
+
+# --------------------------------------------------------------------------- RNG streams
+class _DropoutRNG(threading.local):
+    """(seed, offset) pairs for the counter-based Philox dropout kernels.
+
+    Each dropout site draws a fresh 64-bit offset; the kernels regenerate the mask in
+    backward from the same pair, so no mask is ever stored."""
+
+    def __init__(self):
+        self.seed = int(os.environ.get("CLOUDTIK_AMD_SEED", "24301"))
+        self.offset = 0
+
+    def next(self, n_elements: int = 1):
+        off = self.offset
+        self.offset += max(1, (n_elements + 7) // 8)
+        return self.seed, off
+
+
+_rng = _DropoutRNG()
+
+
+def manual_seed(seed: int):
+    _rng.seed = int(seed) & ((1 << 63) - 1)
+    _rng.offset = 0
+
+
+def rng_state():
+    return {"seed": _rng.seed, "offset": _rng.offset}
+
+
+def set_rng_state(state):
+    _rng.seed = int(state["seed"])
+    _rng.offset = int(state["offset"])
+
+
+from .functional import (  # noqa: E402,F401
+    layer_norm, bias_act, bias_gelu, dropout, embedding3, cross_entropy_fused,
+    ACT_NONE, ACT_GELU, ACT_RELU,
+)
+from .attention import attention, attention_packed  # noqa: E402,F401

@@ -1,0 +1,529 @@
+// Fused multi-head attention (forward + backward) on CDNA4 MFMA, head_dim 64, bf16 I/O.
+//
+// Hot op of the reference's BERT-large pretraining: HF BertSelfAttention, 16 heads x 64,
+// S = 128 (phase-1 shards) / 512, padding mask + attention-prob dropout 0.1
+// (run_pretrain_mlperf.py:449-471).  There is no attention kernel in the reference tree --
+// it reaches this through PyTorch/IPEX -- so this is designed for MI355X from scratch:
+//
+// Forward (flash-style, never materialises S x S):
+//   * workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32 queries.
+//   * S^T = K . Q^T with v_mfma_f32_32x32x16_bf16: the query sits on the MFMA lane and the
+//     keys in the 16 accumulator registers, so a query's softmax row is lane-local except
+//     for one xor-32 shuffle (no LDS round trip for the softmax).
+//   * the P^T accumulator feeds the next MFMA directly as its B operand
+//     (O^T += V^T . P^T, cdna_hip_programming.md §3 "accumulator as next operand"); V^T
+//     fragments come from ds_read_b64_tr_b16 transposed LDS reads of the row-major V tile.
+//   * K/V tiles of 64 keys, double-buffered in LDS, register-staged (global loads for tile
+//     t+1 issued before the MFMAs of tile t, LDS write after: T14).
+//   * every 128-byte LDS row is XOR-swizzled at 16-byte granularity with
+//     rev3((row >> 1) & 7): conflict-free for both the ds_read_b128 row reads and the
+//     ds_read_b64_tr_b16 column reads (see swz()).
+//   * online softmax in the exp2 domain; stores O and the per-row log2-sum-exp.
+// Backward (FlashAttention-2 structure, "key on the lane"):
+//   * workgroup = 4 waves = 128 keys; each wave keeps K, V fragments of its 32 keys in
+//     VGPRs and accumulates dK^T, dV^T in registers over all query tiles.
+//   * S = Q.K^T and dP = dO.V^T are computed with the key on the lane, so P and dS are
+//     already the B operands of dV^T += dO^T.P and dK^T += Q^T.dS (Q^T, dO^T by
+//     transposed LDS reads); only dS crosses LDS (once) for dQ = dS.K.
+//   * dQ: reduced across the workgroup's waves in LDS; stored directly (bf16) when one
+//     workgroup covers all keys (S <= 128, the BERT phase-1 case), otherwise accumulated
+//     with fp32 atomics in the full-rate 2x128-byte shape and converted by a tiny kernel.
+//   * attention-prob dropout regenerated from a counter hash (nothing stored).
+#include "common.h"
+
+namespace ct {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int rev3(int x) { return ((x & 1) << 2) | (x & 2) | ((x >> 2) & 1); }
+// byte offset of 16-byte chunk c of `row` inside a [rows][64 x bf16] LDS tile
+__device__ __forceinline__ int swz(int row, int c) { return row * 128 + ((c ^ rev3((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int swz_e(int row, int col) { return swz(row, col >> 3) + ((col & 7) << 1); }
+
+__device__ __forceinline__ bf16x8_t lds_b128(const char* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(p));
+}
+__device__ __forceinline__ s16x4 lds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+__device__ __forceinline__ bf16x8_t cat_tr(s16x4 lo, s16x4 hi) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+__device__ __forceinline__ bf16x8_t gload_frag(const bf16_t* p, bool valid) {
+  u16x8 v = valid ? *reinterpret_cast<const u16x8*>(p) : u16x8(0);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+// 16-bit uniform pair for element pair `pair` (elements 2*pair, 2*pair+1)
+__device__ __forceinline__ uint32_t drop_pair(uint32_t base, uint64_t pair) {
+  return hash_u32((uint32_t)pair ^ base);
+}
+
+struct AttnFwdArgs {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; bf16_t* o;
+  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;
+  const float* kbias; long kb_sb;  // additive per-key bias [B, Sk] (natural-log units)
+  float* lse;                      // [B*H, Sq] log2-domain log-sum-exp
+  int B, H, Sq, Sk;
+  float scale_log2;                // softmax scale * log2(e)
+  uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
+};
+
+template <bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K,V][64][128B]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qi = blockIdx.x * 128 + w * 32 + r;
+  const bool qvalid = qi < a.Sq;
+  const float LOG2E = 1.4426950408889634f;
+
+  const bf16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (long)qi * a.q_ss;
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = gload_frag(qp + 16 * s + 8 * hh, qvalid);
+
+  const bf16_t* kp = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vp = a.v + b * a.v_sb + h * a.v_sh;
+  const float* kbp = a.kbias ? a.kbias + b * a.kb_sb : nullptr;
+  const int srow = tid >> 3, sch = tid & 7;
+  u16x8 stK[2], stV[2];
+
+  f32x16 O0, O1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { O0[i] = 0.f; O1[i] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  const int nt = (a.Sk + 63) / 64;
+
+#define FWD_GLOAD(kt_)                                                               \
+  _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                 \
+    const int key_ = (kt_) * 64 + srow + 32 * i_;                                    \
+    const bool ok_ = key_ < a.Sk;                                                    \
+    stK[i_] = ok_ ? *reinterpret_cast<const u16x8*>(kp + (long)key_ * a.k_ss + sch * 8) : u16x8(0); \
+    stV[i_] = ok_ ? *reinterpret_cast<const u16x8*>(vp + (long)key_ * a.v_ss + sch * 8) : u16x8(0); \
+  }
+#define FWD_SWRITE(buf_)                                                             \
+  _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                 \
+    char* kb_ = smem + (buf_) * 16384;                                               \
+    *reinterpret_cast<u16x8*>(kb_ + swz(srow + 32 * i_, sch)) = stK[i_];             \
+    *reinterpret_cast<u16x8*>(kb_ + 8192 + swz(srow + 32 * i_, sch)) = stV[i_];      \
+  }
+
+  FWD_GLOAD(0);
+  FWD_SWRITE(0);
+  __syncthreads();
+
+  const int trow = (lane >> 2) & 3;
+  const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nt) { FWD_GLOAD(kt + 1); }
+    const char* Kb = smem + buf * 16384;
+    const char* Vb = Kb + 8192;
+    f32x16 S0, S1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { S0[i] = 0.f; S1[i] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      S0 = mfma32(lds_b128(Kb + swz(r, 2 * s + hh)), qf[s], S0);
+      S1 = mfma32(lds_b128(Kb + swz(32 + r, 2 * s + hh)), qf[s], S1);
+    }
+    // scale, key bias, masking; reg i <-> key kt*64 + t*32 + (i&3) + 8(i>>2) + 4hh
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key0 = kt * 64 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      const int key1 = key0 + 32;
+      float x0 = S0[i] * a.scale_log2, x1 = S1[i] * a.scale_log2;
+      if (kbp) {
+        x0 += (key0 < a.Sk ? kbp[key0] : 0.f) * LOG2E;
+        x1 += (key1 < a.Sk ? kbp[key1] : 0.f) * LOG2E;
+      }
+      if (key0 >= a.Sk || (a.causal && key0 > qi)) x0 = -INFINITY;
+      if (key1 >= a.Sk || (a.causal && key1 > qi)) x1 = -INFINITY;
+      S0[i] = x0; S1[i] = x1;
+      mx = fmaxf(mx, fmaxf(x0, x1));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float msub = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m - msub);
+    m = m_new;
+    float ps = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      S0[i] = exp2f(S0[i] - msub);
+      S1[i] = exp2f(S1[i] - msub);
+      ps += S0[i] + S1[i];
+    }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { O0[i] *= alpha; O1[i] *= alpha; }
+    if (DROP) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {  // (i&3) in {0,2}: an even key and its odd partner
+          const int key = kt * 64 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const uint64_t idx = ((uint64_t)bh * a.Sq + qi) * a.Sk + key;
+          const uint32_t rr = drop_pair(a.hash_base, idx >> 1);
+          const bool k0 = (rr & 0xFFFFu) >= a.thr16, k1 = (rr >> 16) >= a.thr16;
+          if (t == 0) { S0[i] = k0 ? S0[i] * a.inv_keep : 0.f; S0[i + 1] = k1 ? S0[i + 1] * a.inv_keep : 0.f; }
+          else { S1[i] = k0 ? S1[i] * a.inv_keep : 0.f; S1[i + 1] = k1 ? S1[i + 1] * a.inv_keep : 0.f; }
+        }
+      }
+    }
+    // P^T registers -> bf16 B fragments (k-step s2 of tile t = registers 8*s2 .. 8*s2+7)
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pf[0][s2][j] = (__bf16)S0[8 * s2 + j];
+        pf[1][s2][j] = (__bf16)S1[8 * s2 + j];
+      }
+    // O^T[d][q] += V^T[d][key] . P^T[key][q]; V^T fragments by transposed LDS reads
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kb = t * 32 + 16 * s2 + 4 * hh + trow;
+        const bf16x8_t a0 = cat_tr(lds_tr(Vb + swz_e(kb, tcol)), lds_tr(Vb + swz_e(kb + 8, tcol)));
+        const bf16x8_t a1 = cat_tr(lds_tr(Vb + swz_e(kb, 32 + tcol)), lds_tr(Vb + swz_e(kb + 8, 32 + tcol)));
+        O0 = mfma32(a0, pf[t][s2], O0);
+        O1 = mfma32(a1, pf[t][s2], O1);
+      }
+    if (kt + 1 < nt) { FWD_SWRITE(buf ^ 1); }
+    __syncthreads();
+  }
+#undef FWD_GLOAD
+#undef FWD_SWRITE
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qvalid) {
+    bf16_t* op = a.o + b * a.o_sb + h * a.o_sh + (long)qi * a.o_ss;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * hh;
+      u16x4 v0 = {f2bf(O0[4 * g] * inv), f2bf(O0[4 * g + 1] * inv), f2bf(O0[4 * g + 2] * inv), f2bf(O0[4 * g + 3] * inv)};
+      u16x4 v1 = {f2bf(O1[4 * g] * inv), f2bf(O1[4 * g + 1] * inv), f2bf(O1[4 * g + 2] * inv), f2bf(O1[4 * g + 3] * inv)};
+      *reinterpret_cast<u16x4*>(op + d) = v0;
+      *reinterpret_cast<u16x4*>(op + 32 + d) = v1;
+    }
+    if (hh == 0 && a.lse) a.lse[(long)bh * a.Sq + qi] = l > 0.f ? m + log2f(l) : INFINITY;
+  }
+}
+
+// delta[bh, q] = sum_d O[q,d] * dO[q,d]   (one thread per (b, q, h) row of 64)
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, long o_sb,
+                                                         long o_ss, long o_sh, const bf16_t* __restrict__ dO,
+                                                         long d_sb, long d_ss, long d_sh,
+                                                         float* __restrict__ delta, int B, int H, int Sq) {
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t >= (long)B * H * Sq) return;
+  const int q = t % Sq;
+  const int bh = t / Sq;
+  const int b = bh / H, h = bh % H;
+  const u16x8* op = reinterpret_cast<const u16x8*>(o + b * o_sb + h * o_sh + (long)q * o_ss);
+  const u16x8* dp = reinterpret_cast<const u16x8*>(dO + b * d_sb + h * d_sh + (long)q * d_ss);
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const u16x8 x = op[c], y = dp[c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += bf2f(x[j]) * bf2f(y[j]);
+  }
+  delta[t] = acc;
+}
+
+struct AttnBwdArgs {
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dO;
+  bf16_t* dq; bf16_t* dk; bf16_t* dv; float* dq_acc;
+  long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, do_sb, do_ss, do_sh;
+  long dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
+  const float* kbias; long kb_sb;
+  const float* lse; const float* delta;
+  int B, H, Sq, Sk;
+  float scale_log2, scale;
+  uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
+};
+
+template <bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
+  // LDS: Q tile 4K | dO tile 4K | K block 16K | dS 8K | dQ pair-reduce 8K | lse, delta
+  __shared__ __attribute__((aligned(16))) char smem[4096 + 4096 + 16384 + 8192 + 8192 + 256];
+  char* Qs = smem;
+  char* dOs = smem + 4096;
+  char* Ks = smem + 8192;
+  char* dSs = smem + 24576;
+  float* red = reinterpret_cast<float*>(smem + 32768);
+  float* lse_s = reinterpret_cast<float*>(smem + 40960);
+  float* delta_s = lse_s + 32;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int k0 = blockIdx.x * 128;
+  const int key_l = k0 + w * 32 + r;  // this lane's key (MFMA column)
+  const bool kvalid = key_l < a.Sk;
+  const float LOG2E = 1.4426950408889634f;
+
+  const bf16_t* kp = a.k + b * a.k_sb + h * a.k_sh;
+  const bf16_t* vp = a.v + b * a.v_sb + h * a.v_sh;
+  bf16x8_t Kf[4], Vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    Kf[s] = gload_frag(kp + (long)key_l * a.k_ss + 16 * s + 8 * hh, kvalid);
+    Vf[s] = gload_frag(vp + (long)key_l * a.v_ss + 16 * s + 8 * hh, kvalid);
+  }
+  // K block (128 keys) into LDS for the dQ product's transposed reads
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c >> 3, ch = c & 7;
+    const int key = k0 + row;
+    const u16x8 val = key < a.Sk ? *reinterpret_cast<const u16x8*>(kp + (long)key * a.k_ss + ch * 8) : u16x8(0);
+    *reinterpret_cast<u16x8*>(Ks + swz(row, ch)) = val;
+  }
+  float kb2 = 0.f;
+  if (a.kbias && kvalid) kb2 = a.kbias[b * a.kb_sb + key_l] * LOG2E;
+  if (!kvalid) kb2 = -INFINITY;
+
+  f32x16 dV0, dV1, dK0, dK1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dV0[i] = 0.f; dV1[i] = 0.f; dK0[i] = 0.f; dK1[i] = 0.f; }
+
+  const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
+  const bf16_t* dobase = a.dO + b * a.do_sb + h * a.do_sh;
+  const int trow = (lane >> 2) & 3;
+  const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
+  const int nq = (a.Sq + 31) / 32;
+  const bool single_block = gridDim.x == 1;
+  const int dt_q = w & 1, kh = w >> 1;  // this wave's share of the dQ product
+
+  for (int qt = 0; qt < nq; ++qt) {
+    const int qb = qt * 32;
+    {
+      const int row = tid >> 3, ch = tid & 7, q = qb + row;
+      const bool ok = q < a.Sq;
+      *reinterpret_cast<u16x8*>(Qs + swz(row, ch)) = ok ? *reinterpret_cast<const u16x8*>(qbase + (long)q * a.q_ss + ch * 8) : u16x8(0);
+      *reinterpret_cast<u16x8*>(dOs + swz(row, ch)) = ok ? *reinterpret_cast<const u16x8*>(dobase + (long)q * a.do_ss + ch * 8) : u16x8(0);
+      if (tid < 32) {
+        const bool ok2 = qb + tid < a.Sq;
+        lse_s[tid] = ok2 ? a.lse[(long)bh * a.Sq + qb + tid] : INFINITY;
+        delta_s[tid] = ok2 ? a.delta[(long)bh * a.Sq + qb + tid] : 0.f;
+      }
+    }
+    __syncthreads();
+    f32x16 S, dP;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { S[i] = 0.f; dP[i] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      S = mfma32(lds_b128(Qs + swz(r, 2 * s + hh)), Kf[s], S);
+      dP = mfma32(lds_b128(dOs + swz(r, 2 * s + hh)), Vf[s], dP);
+    }
+    // reg i <-> query row qrow(i) = (i&3) + 8(i>>2) + 4hh of this tile; column = key_l
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qrow = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      float x = S[i] * a.scale_log2 + kb2;
+      if (a.causal && key_l > qb + qrow) x = -INFINITY;
+      const float p = exp2f(x - lse_s[qrow]);
+      float pd = p, dpv = dP[i];
+      if (DROP) {
+        const uint64_t idx = ((uint64_t)bh * a.Sq + qb + qrow) * a.Sk + key_l;
+        const uint32_t rr = drop_pair(a.hash_base, idx >> 1);
+        const uint32_t r16 = (idx & 1) ? (rr >> 16) : (rr & 0xFFFFu);
+        const bool keep = r16 >= a.thr16;
+        pd = keep ? p * a.inv_keep : 0.f;
+        dpv = keep ? dpv * a.inv_keep : 0.f;
+      }
+      S[i] = pd;                             // P (after dropout) for dV
+      dP[i] = p * (dpv - delta_s[qrow]);     // dS (unscaled) for dK, dQ
+    }
+    bf16x8_t pf[2], dsf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { pf[s2][j] = (__bf16)S[8 * s2 + j]; dsf[s2][j] = (__bf16)dP[8 * s2 + j]; }
+    // dV^T += dO^T . P ; dK^T += Q^T . dS   (A operands by transposed reads of the tiles)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int qr = 16 * s2 + 4 * hh + trow;
+      const bf16x8_t ado0 = cat_tr(lds_tr(dOs + swz_e(qr, tcol)), lds_tr(dOs + swz_e(qr + 8, tcol)));
+      const bf16x8_t ado1 = cat_tr(lds_tr(dOs + swz_e(qr, 32 + tcol)), lds_tr(dOs + swz_e(qr + 8, 32 + tcol)));
+      const bf16x8_t aq0 = cat_tr(lds_tr(Qs + swz_e(qr, tcol)), lds_tr(Qs + swz_e(qr + 8, tcol)));
+      const bf16x8_t aq1 = cat_tr(lds_tr(Qs + swz_e(qr, 32 + tcol)), lds_tr(Qs + swz_e(qr + 8, 32 + tcol)));
+      dV0 = mfma32(ado0, pf[s2], dV0);
+      dV1 = mfma32(ado1, pf[s2], dV1);
+      dK0 = mfma32(aq0, dsf[s2], dK0);
+      dK1 = mfma32(aq1, dsf[s2], dK1);
+    }
+    // dS -> LDS [32 q][128 keys] (256-byte rows, chunk ^= row & 15)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      const int col = w * 32 + r;
+      *reinterpret_cast<bf16_t*>(dSs + row * 256 + ((((col >> 3) ^ (row & 15))) << 4) + ((col & 7) << 1)) = f2bf(dP[i]);
+    }
+    __syncthreads();
+    // dQ[q][d] partial = dS[q][kh*64 .. +64] . K[kh*64 .. +64][dt_q*32 .. +32]
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int cc = kh * 8 + 2 * s + hh;
+      const bf16x8_t aa = lds_b128(dSs + r * 256 + ((cc ^ (r & 15)) << 4));
+      const int kr = kh * 64 + 16 * s + 8 * hh + trow;
+      const bf16x8_t bb = cat_tr(lds_tr(Ks + swz_e(kr, dt_q * 32 + tcol)), lds_tr(Ks + swz_e(kr + 4, dt_q * 32 + tcol)));
+      acc = mfma32(aa, bb, acc);
+    }
+    if (kh == 1) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[(dt_q * 16 + i) * 64 + lane] = acc[i];
+    }
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        const int d = dt_q * 32 + r;
+        const float val = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
+        if (q < a.Sq) {
+          if (single_block) a.dq[b * a.dq_sb + h * a.dq_sh + (long)q * a.dq_ss + d] = f2bf(val);
+          else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (kvalid) {
+    bf16_t* dkp = a.dk + b * a.dk_sb + h * a.dk_sh + (long)key_l * a.dk_ss;
+    bf16_t* dvp = a.dv + b * a.dv_sb + h * a.dv_sh + (long)key_l * a.dv_ss;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * hh;
+      u16x4 k0v = {f2bf(dK0[4 * g] * a.scale), f2bf(dK0[4 * g + 1] * a.scale), f2bf(dK0[4 * g + 2] * a.scale), f2bf(dK0[4 * g + 3] * a.scale)};
+      u16x4 k1v = {f2bf(dK1[4 * g] * a.scale), f2bf(dK1[4 * g + 1] * a.scale), f2bf(dK1[4 * g + 2] * a.scale), f2bf(dK1[4 * g + 3] * a.scale)};
+      u16x4 v0v = {f2bf(dV0[4 * g]), f2bf(dV0[4 * g + 1]), f2bf(dV0[4 * g + 2]), f2bf(dV0[4 * g + 3])};
+      u16x4 v1v = {f2bf(dV1[4 * g]), f2bf(dV1[4 * g + 1]), f2bf(dV1[4 * g + 2]), f2bf(dV1[4 * g + 3])};
+      *reinterpret_cast<u16x4*>(dkp + d) = k0v;
+      *reinterpret_cast<u16x4*>(dkp + 32 + d) = k1v;
+      *reinterpret_cast<u16x4*>(dvp + d) = v0v;
+      *reinterpret_cast<u16x4*>(dvp + 32 + d) = v1v;
+    }
+  }
+}
+
+// dq (bf16, strided) = dq_acc (fp32 [B*H, Sq, 64])
+__global__ void attn_dq_convert_kernel(const float* __restrict__ acc, bf16_t* __restrict__ dq,
+                                       long sb, long ss, long sh, int B, int H, int Sq) {
+  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (t >= (long)B * H * Sq * 64) return;
+  const int d = t & 63;
+  const long row = t >> 6;
+  const int q = row % Sq;
+  const int bh = row / Sq;
+  const int b = bh / H, h = bh % H;
+  dq[b * sb + h * sh + (long)q * ss + d] = f2bf(acc[t]);
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+static uint32_t host_hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+static void drop_params(float p, uint64_t seed, uint64_t offset, uint32_t* thr16, float* inv_keep,
+                        uint32_t* base) {
+  long t = (long)(p * 65536.0f + 0.5f);
+  *thr16 = (uint32_t)(t > 65535 ? 65535 : t);
+  *inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t s_lo = (uint32_t)seed, s_hi = (uint32_t)(seed >> 32), o_lo = (uint32_t)offset;
+  *base = host_hash_u32(s_lo ^ (s_hi * 0x85EBCA6Bu) ^ (o_lo * 0xC2B2AE35u));
+}
+
+// strides: [batch, seq, head] in elements for each tensor; head_dim must be 64 (contiguous)
+extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const long* ks,
+                           const void* v, const long* vs, void* o, const long* os,
+                           const float* kbias, long kb_sb, float* lse, int B, int H, int Sq,
+                           int Sk, float scale, float p_drop, uint64_t seed, uint64_t offset,
+                           int causal, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return -1;
+  if (p_drop > 0.f && (Sk % 2)) return -2;
+  AttnFwdArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
+  a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
+  a.k_sb = ks[0]; a.k_ss = ks[1]; a.k_sh = ks[2];
+  a.v_sb = vs[0]; a.v_ss = vs[1]; a.v_sh = vs[2];
+  a.o_sb = os[0]; a.o_ss = os[1]; a.o_sh = os[2];
+  a.kbias = kbias; a.kb_sb = kb_sb; a.lse = lse;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  drop_params(p_drop, seed, offset, &a.thr16, &a.inv_keep, &a.hash_base);
+  a.causal = causal;
+  dim3 grid((Sq + 127) / 128, B * H);
+  if (p_drop > 0.f) attn_fwd_d64_kernel<true><<<grid, 256, 0, stream>>>(a);
+  else attn_fwd_d64_kernel<false><<<grid, 256, 0, stream>>>(a);
+  return 0;
+}
+
+// delta workspace: float[B*H*Sq]; dq_acc workspace: float[B*H*Sq*64] zeroed (only used
+// when Sk > 128)
+extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const long* ks,
+                           const void* v, const long* vs, const void* o, const long* os,
+                           const void* dO, const long* dos, void* dq, const long* dqs, void* dk,
+                           const long* dks, void* dv, const long* dvs, const float* kbias,
+                           long kb_sb, const float* lse, float* delta, float* dq_acc, int B, int H,
+                           int Sq, int Sk, float scale, float p_drop, uint64_t seed,
+                           uint64_t offset, int causal, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return -1;
+  if (p_drop > 0.f && (Sk % 2)) return -2;
+  const long rows = (long)B * H * Sq;
+  attn_delta_kernel<<<(int)((rows + 255) / 256), 256, 0, stream>>>(
+      (const bf16_t*)o, os[0], os[1], os[2], (const bf16_t*)dO, dos[0], dos[1], dos[2], delta, B, H, Sq);
+  AttnBwdArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.dO = (const bf16_t*)dO;
+  a.dq = (bf16_t*)dq; a.dk = (bf16_t*)dk; a.dv = (bf16_t*)dv; a.dq_acc = dq_acc;
+  a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
+  a.k_sb = ks[0]; a.k_ss = ks[1]; a.k_sh = ks[2];
+  a.v_sb = vs[0]; a.v_ss = vs[1]; a.v_sh = vs[2];
+  a.do_sb = dos[0]; a.do_ss = dos[1]; a.do_sh = dos[2];
+  a.dq_sb = dqs[0]; a.dq_ss = dqs[1]; a.dq_sh = dqs[2];
+  a.dk_sb = dks[0]; a.dk_ss = dks[1]; a.dk_sh = dks[2];
+  a.dv_sb = dvs[0]; a.dv_ss = dvs[1]; a.dv_sh = dvs[2];
+  a.kbias = kbias; a.kb_sb = kb_sb; a.lse = lse; a.delta = delta;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  a.scale = scale; a.scale_log2 = scale * 1.4426950408889634f;
+  drop_params(p_drop, seed, offset, &a.thr16, &a.inv_keep, &a.hash_base);
+  a.causal = causal;
+  const int nkb = (Sk + 127) / 128;
+  if (nkb > 1 && !dq_acc) return -3;
+  if (nkb > 1) hipMemsetAsync(dq_acc, 0, sizeof(float) * rows * 64, stream);
+  dim3 grid(nkb, B * H);
+  if (p_drop > 0.f) attn_bwd_d64_kernel<true><<<grid, 256, 0, stream>>>(a);
+  else attn_bwd_d64_kernel<false><<<grid, 256, 0, stream>>>(a);
+  if (nkb > 1)
+    attn_dq_convert_kernel<<<(int)((rows * 64 + 255) / 256), 256, 0, stream>>>(
+        dq_acc, (bf16_t*)dq, dqs[0], dqs[1], dqs[2], B, H, Sq);
+  return 0;
+}
+
+extern "C" uint32_t ct_attn_hash_base(uint64_t seed, uint64_t offset) {
+  uint32_t t, b; float f;
+  drop_params(0.f, seed, offset, &t, &f, &b);
+  return b;
+}

@@ -1,0 +1,304 @@
+// Training BatchNorm for NHWC (channels_last) bf16 activations, fused with the residual
+// add and ReLU that follow it in every ResNet bottleneck.
+//
+// Reference hot path: torchvision resnet50 trained channels_last + bf16 under DDP
+// (applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296) and
+// the synthetic ResNet-50 benchmark (examples/runtime/ai/basics/pytorch/
+// imagenet-resnet50-synthetic-pytorch-distributed.py).  In PyTorch eager that is three
+// memory passes per BN (batch_norm, add, relu); here it is:
+//   forward : stats kernel (per-block sum/sumsq -> (mean, M2)), finalize (Chan merge of
+//             block partials, running-stat update), apply kernel y = relu(x*a + b + res)
+//   backward: reduce kernel (sum dy', sum dy'*xhat with dy' = dy * [y > 0]), finalize
+//             (dgamma, dbeta, per-channel affine coefficients), apply kernel
+//             dx = a*dy' + c1*x + c0 and d(residual) = dy' in the same pass.
+// Channels are the contiguous dimension: a thread owns 8 channels (one 16-byte vector) and
+// walks rows, so every load is a full coalesced 16-byte-per-lane access.
+#include "common.h"
+
+namespace ct {
+
+struct BnLayout { int M, C, CV, RPI, rows_per_blk; };
+
+__device__ __forceinline__ void bn_thread(const BnLayout& L, int& cv, int& rl) {
+  cv = threadIdx.x % L.CV;
+  rl = threadIdx.x / L.CV;
+}
+
+// per-block (mean, M2) over rows [b*R, (b+1)*R)
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, BnLayout L,
+                                                       float* __restrict__ pmean,
+                                                       float* __restrict__ pm2) {
+  __shared__ float ls[256 * 8];
+  __shared__ float lq[256 * 8];
+  int cv, rl;
+  bn_thread(L, cv, rl);
+  const int r0 = blockIdx.x * L.rows_per_blk;
+  const int r1 = min(L.M, r0 + L.rows_per_blk);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  if (rl < L.RPI) {
+    for (int r = r0 + rl; r < r1; r += L.RPI) {
+      const u16x8 v = reinterpret_cast<const u16x8*>(x + (size_t)r * L.C)[cv];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float f = bf2f(v[j]); s[j] += f; q[j] += f * f; }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { ls[threadIdx.x * 8 + j] = s[j]; lq[threadIdx.x * 8 + j] = q[j]; }
+  __syncthreads();
+  if (rl == 0) {
+    for (int k = 1; k < L.RPI; ++k) {
+      const int t = k * L.CV + cv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += ls[t * 8 + j]; q[j] += lq[t * 8 + j]; }
+    }
+    const float n = (float)max(0, r1 - r0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cv * 8 + j;
+      const float mean = n > 0.f ? s[j] / n : 0.f;
+      pmean[(size_t)blockIdx.x * L.C + c] = mean;
+      pm2[(size_t)blockIdx.x * L.C + c] = n > 0.f ? fmaxf(q[j] - s[j] * mean, 0.f) : 0.f;
+    }
+  }
+}
+
+// Chan-merge of block partials; writes save_mean/save_invstd, affine (a, b) and updates
+// running statistics.
+__global__ void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                   int nblk, BnLayout L, const bf16_t* __restrict__ gamma,
+                                   const bf16_t* __restrict__ beta, float eps, float momentum,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var,
+                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                   float* __restrict__ coef_a, float* __restrict__ coef_b) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= L.C) return;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int b = 0; b < nblk; ++b) {
+    const int r0 = b * L.rows_per_blk;
+    const float nb = (float)max(0, min(L.M, r0 + L.rows_per_blk) - r0);
+    if (nb <= 0.f) continue;
+    const float mb = pmean[(size_t)b * L.C + c], qb = pm2[(size_t)b * L.C + c];
+    const float nn = n + nb;
+    const float d = mb - mean;
+    mean += d * nb / nn;
+    m2 += qb + d * d * n * nb / nn;
+    n = nn;
+  }
+  const float var = n > 0.f ? m2 / n : 0.f;
+  const float invstd = rsqrtf(var + eps);
+  const float g = gamma ? bf2f(gamma[c]) : 1.f, bt = beta ? bf2f(beta[c]) : 0.f;
+  save_mean[c] = mean;
+  save_invstd[c] = invstd;
+  coef_a[c] = g * invstd;
+  coef_b[c] = bt - mean * g * invstd;
+  if (run_mean) {
+    const float unb = n > 1.f ? m2 / (n - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
+// y = act(x * a[c] + b[c] (+ res))
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x,
+                                                       const bf16_t* __restrict__ res,
+                                                       const float* __restrict__ a,
+                                                       const float* __restrict__ b,
+                                                       bf16_t* __restrict__ y, long total_vec,
+                                                       int CV, int relu) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
+       v += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(v % CV);
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
+    u16x8 rv = u16x8(0);
+    if (res) rv = reinterpret_cast<const u16x8*>(res)[v];
+    const f32x4 a0 = reinterpret_cast<const f32x4*>(a)[2 * cv], a1 = reinterpret_cast<const f32x4*>(a)[2 * cv + 1];
+    const f32x4 b0 = reinterpret_cast<const f32x4*>(b)[2 * cv], b1 = reinterpret_cast<const f32x4*>(b)[2 * cv + 1];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float aj = j < 4 ? a0[j] : a1[j - 4], bj = j < 4 ? b0[j] : b1[j - 4];
+      float t = bf2f(xv[j]) * aj + bj + bf2f(rv[j]);
+      if (relu) t = fmaxf(t, 0.f);
+      o[j] = f2bf(t);
+    }
+    reinterpret_cast<u16x8*>(y)[v] = o;
+  }
+}
+
+// per-block sums of dy' and dy'*xhat
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ invstd, BnLayout L, int relu,
+    float* __restrict__ p1, float* __restrict__ p2) {
+  __shared__ float l1[256 * 8];
+  __shared__ float l2[256 * 8];
+  int cv, rl;
+  bn_thread(L, cv, rl);
+  const int r0 = blockIdx.x * L.rows_per_blk;
+  const int r1 = min(L.M, r0 + L.rows_per_blk);
+  float s1[8], s2[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1[j] = 0.f; s2[j] = 0.f;
+    mu[j] = mean[cv * 8 + j]; is[j] = invstd[cv * 8 + j];
+  }
+  if (rl < L.RPI) {
+    for (int r = r0 + rl; r < r1; r += L.RPI) {
+      const size_t o = (size_t)r * L.CV + cv;
+      const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
+      const u16x8 xv = reinterpret_cast<const u16x8*>(x)[o];
+      u16x8 yv = u16x8(1);
+      if (relu) yv = reinterpret_cast<const u16x8*>(y)[o];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (relu && !(bf2f(yv[j]) > 0.f)) ? 0.f : bf2f(g[j]);
+        s1[j] += d;
+        s2[j] += d * (bf2f(xv[j]) - mu[j]) * is[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { l1[threadIdx.x * 8 + j] = s1[j]; l2[threadIdx.x * 8 + j] = s2[j]; }
+  __syncthreads();
+  if (rl == 0) {
+    for (int k = 1; k < L.RPI; ++k) {
+      const int t = k * L.CV + cv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s1[j] += l1[t * 8 + j]; s2[j] += l2[t * 8 + j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      p1[(size_t)blockIdx.x * L.C + cv * 8 + j] = s1[j];
+      p2[(size_t)blockIdx.x * L.C + cv * 8 + j] = s2[j];
+    }
+  }
+}
+
+// dgamma, dbeta and dx = a*dy' + c1*x + c0 coefficients
+template <typename PT>
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ p1, const float* __restrict__ p2,
+                                       int nblk, int M, int C, const bf16_t* __restrict__ gamma,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, PT* __restrict__ dgamma,
+                                       PT* __restrict__ dbeta, float* __restrict__ ca,
+                                       float* __restrict__ c1, float* __restrict__ c0) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sdy = 0.f, sdx = 0.f;
+  for (int b = 0; b < nblk; ++b) { sdy += p1[(size_t)b * C + c]; sdx += p2[(size_t)b * C + c]; }
+  if (dgamma) dgamma[c] = from_f<PT>(sdx);
+  if (dbeta) dbeta[c] = from_f<PT>(sdy);
+  const float g = gamma ? bf2f(gamma[c]) : 1.f;
+  const float is = invstd[c];
+  const float a = g * is;
+  const float k = -a * sdx / M;  // coefficient of xhat
+  ca[c] = a;
+  c1[c] = k * is;
+  c0[c] = -a * sdy / M - k * is * mean[c];
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ ca, const float* __restrict__ c1, const float* __restrict__ c0,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long total_vec, int CV, int relu) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
+       v += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(v % CV);
+    const u16x8 g = reinterpret_cast<const u16x8*>(dy)[v];
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
+    u16x8 yv = u16x8(1);
+    if (relu) yv = reinterpret_cast<const u16x8*>(y)[v];
+    u16x8 o, od;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cv * 8 + j;
+      const float d = (relu && !(bf2f(yv[j]) > 0.f)) ? 0.f : bf2f(g[j]);
+      o[j] = f2bf(ca[c] * d + c1[c] * bf2f(xv[j]) + c0[c]);
+      od[j] = f2bf(d);
+    }
+    reinterpret_cast<u16x8*>(dx)[v] = o;
+    if (dres) reinterpret_cast<u16x8*>(dres)[v] = od;
+  }
+}
+
+inline BnLayout bn_layout(int M, int C, int target_blocks) {
+  BnLayout L;
+  L.M = M; L.C = C; L.CV = C / 8;
+  L.RPI = 256 / L.CV;
+  if (L.RPI < 1) L.RPI = 1;
+  int nblk = target_blocks;
+  const int min_rows = L.RPI * 8;
+  if ((long)nblk * min_rows > M) nblk = (M + min_rows - 1) / min_rows;
+  if (nblk < 1) nblk = 1;
+  L.rows_per_blk = (M + nblk - 1) / nblk;
+  return L;
+}
+inline int bn_nblk(const BnLayout& L) { return (L.M + L.rows_per_blk - 1) / L.rows_per_blk; }
+
+inline int ew_grid(long work) {
+  long g = (work + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+extern "C" int ct_bn_max_blocks() { return 1024; }
+
+// workspace: part = float[2 * 1024 * C]; stat = float[4 * C] (save_mean, save_invstd, a, b)
+extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma, const void* beta,
+                               float* run_mean, float* run_var, void* y, float* part, float* stat,
+                               int M, int C, float eps, float momentum, int relu,
+                               hipStream_t stream) {
+  if (C % 8 || C / 8 > 256 || M <= 0) return -1;
+  BnLayout L = bn_layout(M, C, 1024);
+  const int nblk = bn_nblk(L);
+  bn_stats_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)1024 * C);
+  bn_finalize_kernel<<<ceil_div(C, 256), 256, 0, stream>>>(part, part + (size_t)1024 * C, nblk, L,
+                                                           (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                           eps, momentum, run_mean, run_var, stat,
+                                                           stat + C, stat + 2 * C, stat + 3 * C);
+  const long tv = (long)M * (C / 8);
+  bn_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)res, stat + 2 * C,
+                                                   stat + 3 * C, (bf16_t*)y, tv, C / 8, relu);
+  return 0;
+}
+
+// inference-mode forward with given affine coefficients a, b (float[C] each)
+extern "C" int ct_bn_apply(const void* x, const void* res, const float* a, const float* b, void* y,
+                           int M, int C, int relu, hipStream_t stream) {
+  if (C % 8) return -1;
+  const long tv = (long)M * (C / 8);
+  bn_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)res, a, b,
+                                                   (bf16_t*)y, tv, C / 8, relu);
+  return 0;
+}
+
+// workspace: part = float[2 * 1024 * C]; coef = float[3 * C]
+extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const void* gamma,
+                         const float* save_mean, const float* save_invstd, void* dx, void* dres,
+                         void* dgamma, void* dbeta, int param_fp32, float* part, float* coef, int M,
+                         int C, int relu, hipStream_t stream) {
+  if (C % 8 || C / 8 > 256 || M <= 0) return -1;
+  BnLayout L = bn_layout(M, C, 1024);
+  const int nblk = bn_nblk(L);
+  bn_bwd_reduce_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
+                                                 (const bf16_t*)x, save_mean, save_invstd, L, relu,
+                                                 part, part + (size_t)1024 * C);
+  if (param_fp32)
+    bn_bwd_finalize_kernel<float><<<ceil_div(C, 256), 256, 0, stream>>>(
+        part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
+        (float*)dgamma, (float*)dbeta, coef, coef + C, coef + 2 * C);
+  else
+    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 256), 256, 0, stream>>>(
+        part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
+        (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C);
+  const long tv = (long)M * (C / 8);
+  bn_bwd_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
+                                                       (const bf16_t*)x, coef, coef + C, coef + 2 * C,
+                                                       (bf16_t*)dx, (bf16_t*)dres, tv, C / 8, relu);
+  return 0;
+}

@@ -1,0 +1,342 @@
+// Thin PyTorch bindings for the cloudtik_amd CDNA4 op library.
+// Every function validates shapes/dtypes on the host (a mis-shaped launch of a hand-written
+// kernel can fault the GPU), fetches the current HIP stream and calls the extern "C"
+// launcher.  No allocation happens inside the launchers; workspaces come from the caller.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int ct_layernorm_fwd(const void*, const void*, const void*, const void*, const void*, void*, void*,
+                     float*, float*, int, int, float, int, float, uint64_t, uint64_t, hipStream_t);
+int ct_layernorm_bwd_grid(int M);
+int ct_layernorm_bwd(const void*, const void*, const void*, const float*, const float*,
+                     const void*, void*, void*, float*, void*, void*, void*, int, int, int, int,
+                     int, float, uint64_t, uint64_t, hipStream_t);
+int ct_colsum(const float*, void*, int, int, int, int, hipStream_t);
+int ct_bias_act_fwd(const void*, const void*, void*, long, int, int, hipStream_t);
+int ct_bias_act_bwd_grid(long M);
+int ct_bias_act_bwd(const void*, const void*, const void*, void*, float*, void*, long, int, int,
+                    int, int, hipStream_t);
+int ct_dropout(const void*, void*, long, float, uint64_t, uint64_t, hipStream_t);
+int ct_embed3_fwd(const int64_t*, const int64_t*, const void*, const void*, const void*, void*, int,
+                  int, int, hipStream_t);
+int ct_embed3_bwd(const int64_t*, const int64_t*, const void*, float*, float*, float*, int, int,
+                  int, hipStream_t);
+int ct_cast(const void*, int, void*, int, long, float, int, hipStream_t);
+int ct_lamb(const void*, int, float*, float*, float*, void*, int, const int*, const long*,
+            const int*, int, const int*, int, const float*, const float*, float, float, float, int,
+            int, float*, float*, int, hipStream_t);
+int ct_adam(const void*, int, float*, float*, float*, void*, int, const int*, const long*,
+            const int*, int, const float*, const float*, float, float, float, int, hipStream_t);
+int ct_sgd(const void*, int, float*, float*, void*, int, const int*, const long*, const int*, int,
+           const float*, const float*, float, float, int, int, hipStream_t);
+int ct_sumsq(const void*, int, long, float*, hipStream_t);
+int ct_clip_coef(const float*, float*, float, float, hipStream_t);
+int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, const float*, int, int,
+                float, hipStream_t);
+int ct_attn_fwd(const void*, const long*, const void*, const long*, const void*, const long*, void*,
+                const long*, const float*, long, float*, int, int, int, int, float, float, uint64_t,
+                uint64_t, int, hipStream_t);
+int ct_attn_bwd(const void*, const long*, const void*, const long*, const void*, const long*,
+                const void*, const long*, const void*, const long*, void*, const long*, void*,
+                const long*, void*, const long*, const float*, long, const float*, float*, float*,
+                int, int, int, int, float, float, uint64_t, uint64_t, int, hipStream_t);
+}
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be fp32")
+#define CHECK_IN(x) do { CHECK_CUDA(x); CHECK_CONTIG(x); } while (0)
+
+static inline hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+static inline const void* optr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+static inline void* optr_mut(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+static inline int dt_code(const at::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return 0;
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  TORCH_CHECK(false, "only fp32 / bf16 supported");
+  return -1;
+}
+
+// ---------------------------------------------------------------- layernorm
+// returns (y, s, mean, rstd); s is undefined when no bias/residual/dropout was applied
+std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> bias,
+                                      c10::optional<at::Tensor> res, at::Tensor gamma,
+                                      c10::optional<at::Tensor> beta, double eps, bool rms,
+                                      double p_drop, int64_t seed, int64_t offset) {
+  CHECK_IN(x); CHECK_BF16(x); CHECK_IN(gamma); CHECK_BF16(gamma);
+  const int N = x.size(-1);
+  const int M = x.numel() / N;
+  TORCH_CHECK(gamma.numel() == N, "gamma size");
+  if (bias.has_value() && bias->defined()) { CHECK_IN(*bias); CHECK_BF16(*bias); TORCH_CHECK(bias->numel() == N); }
+  if (res.has_value() && res->defined()) { CHECK_IN(*res); CHECK_BF16(*res); TORCH_CHECK(res->numel() == x.numel()); }
+  if (beta.has_value() && beta->defined()) { CHECK_IN(*beta); CHECK_BF16(*beta); TORCH_CHECK(beta->numel() == N); }
+  auto y = at::empty_like(x);
+  const bool need_s = optr(bias) || optr(res) || p_drop > 0.0;
+  at::Tensor s = need_s ? at::empty_like(x) : at::Tensor();
+  auto fo = x.options().dtype(at::kFloat);
+  auto mean = at::empty({M}, fo);
+  auto rstd = at::empty({M}, fo);
+  int rc = ct_layernorm_fwd(x.data_ptr(), optr(bias), optr(res), gamma.data_ptr(), optr(beta),
+                            y.data_ptr(), need_s ? s.data_ptr() : nullptr, mean.data_ptr<float>(),
+                            rstd.data_ptr<float>(), M, N, (float)eps, rms ? 1 : 0, (float)p_drop,
+                            (uint64_t)seed, (uint64_t)offset, cur_stream());
+  TORCH_CHECK(rc == 0, "layernorm_fwd: unsupported shape N=", N);
+  return {y, s, mean, rstd};
+}
+
+// returns (ds, dx, dgamma, dbeta, dbias)
+std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor s, at::Tensor gamma, at::Tensor mean,
+                                      at::Tensor rstd, c10::optional<at::Tensor> dextra, bool rms,
+                                      bool has_beta, bool has_bias, bool need_dx, double p_drop,
+                                      int64_t seed, int64_t offset) {
+  CHECK_IN(dy); CHECK_BF16(dy); CHECK_IN(s); CHECK_BF16(s); CHECK_IN(gamma);
+  const int N = s.size(-1);
+  const int M = s.numel() / N;
+  TORCH_CHECK(dy.numel() == s.numel());
+  auto ds = at::empty_like(s);
+  at::Tensor dx = need_dx ? at::empty_like(s) : at::Tensor();
+  auto dgamma = at::empty_like(gamma);
+  at::Tensor dbeta = has_beta ? at::empty_like(gamma) : at::Tensor();
+  at::Tensor dbias = has_bias ? at::empty_like(gamma) : at::Tensor();
+  const int grid = ct_layernorm_bwd_grid(M);
+  auto part = at::empty({3 * (long)grid * N}, s.options().dtype(at::kFloat));
+  int rc = ct_layernorm_bwd(dy.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+                            rstd.data_ptr<float>(), optr(dextra), ds.data_ptr(),
+                            need_dx ? dx.data_ptr() : nullptr, part.data_ptr<float>(),
+                            dgamma.data_ptr(), has_beta ? dbeta.data_ptr() : nullptr,
+                            has_bias ? dbias.data_ptr() : nullptr, M, N, rms ? 1 : 0,
+                            gamma.scalar_type() == at::kFloat ? 1 : 0, 0, (float)p_drop,
+                            (uint64_t)seed, (uint64_t)offset, cur_stream());
+  TORCH_CHECK(rc == 0, "layernorm_bwd: unsupported shape N=", N);
+  return {ds, dx, dgamma, dbeta, dbias};
+}
+
+// ---------------------------------------------------------------- bias + activation
+at::Tensor bias_act_fwd(at::Tensor z, c10::optional<at::Tensor> bias, int64_t act) {
+  CHECK_IN(z); CHECK_BF16(z);
+  const int N = z.size(-1);
+  auto y = at::empty_like(z);
+  int rc = ct_bias_act_fwd(z.data_ptr(), optr(bias), y.data_ptr(), z.numel() / N, N, (int)act, cur_stream());
+  TORCH_CHECK(rc == 0, "bias_act_fwd: N % 8 != 0");
+  return y;
+}
+
+std::vector<at::Tensor> bias_act_bwd(at::Tensor dy, at::Tensor z, c10::optional<at::Tensor> bias,
+                                     int64_t act, bool need_dbias) {
+  CHECK_IN(dy); CHECK_IN(z); CHECK_BF16(z); CHECK_BF16(dy);
+  const int N = z.size(-1);
+  const long M = z.numel() / N;
+  auto dz = at::empty_like(z);
+  at::Tensor dbias, part;
+  if (need_dbias) {
+    dbias = at::empty({N}, z.options());
+    part = at::empty({(long)ct_bias_act_bwd_grid(M) * N}, z.options().dtype(at::kFloat));
+  }
+  int rc = ct_bias_act_bwd(dy.data_ptr(), z.data_ptr(), optr(bias), dz.data_ptr(),
+                           need_dbias ? part.data_ptr<float>() : nullptr,
+                           need_dbias ? dbias.data_ptr() : nullptr, M, N, (int)act, 0, 0, cur_stream());
+  TORCH_CHECK(rc == 0, "bias_act_bwd: N % 8 != 0");
+  return {dz, dbias};
+}
+
+at::Tensor dropout_fwd(at::Tensor x, double p, int64_t seed, int64_t offset) {
+  CHECK_IN(x); CHECK_BF16(x);
+  auto y = at::empty_like(x);
+  int rc = ct_dropout(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset, cur_stream());
+  TORCH_CHECK(rc == 0, "dropout: numel % 8 != 0");
+  return y;
+}
+
+// ---------------------------------------------------------------- embeddings
+at::Tensor embed3_fwd(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor W,
+                      c10::optional<at::Tensor> P, c10::optional<at::Tensor> T) {
+  CHECK_IN(ids); CHECK_IN(W); CHECK_BF16(W);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "ids must be int64");
+  TORCH_CHECK(ids.dim() == 2, "ids must be [B, S]");
+  const int S = ids.size(1), N = W.size(1), ntok = ids.numel();
+  if (P.has_value() && P->defined()) TORCH_CHECK(P->size(0) >= S && P->size(1) == N);
+  if (tt.has_value() && tt->defined()) TORCH_CHECK(tt->numel() == ntok && tt->scalar_type() == at::kLong);
+  auto out = at::empty({ids.size(0), S, N}, W.options());
+  int rc = ct_embed3_fwd(ids.data_ptr<int64_t>(),
+                         (tt.has_value() && tt->defined()) ? tt->data_ptr<int64_t>() : nullptr,
+                         W.data_ptr(), optr(P), optr(T), out.data_ptr(), ntok, S, N, cur_stream());
+  TORCH_CHECK(rc == 0, "embed3_fwd: N % 8 != 0");
+  return out;
+}
+
+void embed3_bwd(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor g,
+                c10::optional<at::Tensor> dW, c10::optional<at::Tensor> dP,
+                c10::optional<at::Tensor> dT) {
+  CHECK_IN(ids); CHECK_IN(g); CHECK_BF16(g);
+  const int S = ids.size(1), N = g.size(-1), ntok = ids.numel();
+  for (auto* t : {&dW, &dP, &dT}) if (t->has_value() && (*t)->defined()) { CHECK_F32(**t); CHECK_IN(**t); TORCH_CHECK((*t)->size(1) == N); }
+  ct_embed3_bwd(ids.data_ptr<int64_t>(), (tt.has_value() && tt->defined()) ? tt->data_ptr<int64_t>() : nullptr,
+                g.data_ptr(), (float*)optr_mut(dW), (float*)optr_mut(dP), (float*)optr_mut(dT), ntok, S,
+                N, cur_stream());
+}
+
+void cast_into(at::Tensor x, at::Tensor y, double scale, bool accumulate) {
+  CHECK_IN(x); CHECK_IN(y);
+  TORCH_CHECK(x.numel() == y.numel());
+  ct_cast(x.data_ptr(), dt_code(x), y.data_ptr(), dt_code(y), x.numel(), (float)scale, accumulate ? 1 : 0, cur_stream());
+}
+
+// ---------------------------------------------------------------- optimizers
+void lamb_step(at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor w, c10::optional<at::Tensor> w_model,
+               at::Tensor seg_tensor, at::Tensor seg_start, at::Tensor seg_len, at::Tensor tensor_first_seg,
+               at::Tensor tensor_wd, at::Tensor dyn, double beta1, double beta2, double eps,
+               bool bias_corr, bool trust_all, at::Tensor seg_part, at::Tensor tensor_part, int64_t stage) {
+  for (auto* t : {&g, &m, &v, &w, &seg_tensor, &seg_start, &seg_len, &tensor_first_seg, &tensor_wd, &dyn, &seg_part, &tensor_part}) CHECK_IN(*t);
+  CHECK_F32(m); CHECK_F32(v); CHECK_F32(w);
+  TORCH_CHECK(g.numel() >= w.numel() && m.numel() == w.numel() && v.numel() == w.numel());
+  const int nseg = seg_len.numel(), T = tensor_wd.numel();
+  TORCH_CHECK(seg_part.numel() >= 2 * nseg && tensor_part.numel() >= 2 * T && tensor_first_seg.numel() == T + 1);
+  int pdt = 0;
+  if (w_model.has_value() && w_model->defined()) { CHECK_IN(*w_model); pdt = dt_code(*w_model); TORCH_CHECK(w_model->numel() >= w.numel()); }
+  ct_lamb(g.data_ptr(), dt_code(g), m.data_ptr<float>(), v.data_ptr<float>(), w.data_ptr<float>(),
+          optr_mut(w_model), pdt, seg_tensor.data_ptr<int>(), seg_start.data_ptr<int64_t>(),
+          seg_len.data_ptr<int>(), nseg, tensor_first_seg.data_ptr<int>(), T,
+          tensor_wd.data_ptr<float>(), dyn.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps,
+          bias_corr ? 1 : 0, trust_all ? 1 : 0, seg_part.data_ptr<float>(), tensor_part.data_ptr<float>(),
+          (int)stage, cur_stream());
+}
+
+void adam_step(at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor w, c10::optional<at::Tensor> w_model,
+               at::Tensor seg_tensor, at::Tensor seg_start, at::Tensor seg_len, at::Tensor tensor_wd,
+               at::Tensor dyn, double beta1, double beta2, double eps, bool adamw) {
+  for (auto* t : {&g, &m, &v, &w, &seg_tensor, &seg_start, &seg_len, &tensor_wd, &dyn}) CHECK_IN(*t);
+  CHECK_F32(m); CHECK_F32(v); CHECK_F32(w);
+  TORCH_CHECK(g.numel() >= w.numel() && m.numel() == w.numel() && v.numel() == w.numel());
+  int pdt = 0;
+  if (w_model.has_value() && w_model->defined()) { CHECK_IN(*w_model); pdt = dt_code(*w_model); }
+  ct_adam(g.data_ptr(), dt_code(g), m.data_ptr<float>(), v.data_ptr<float>(), w.data_ptr<float>(),
+          optr_mut(w_model), pdt, seg_tensor.data_ptr<int>(), seg_start.data_ptr<int64_t>(),
+          seg_len.data_ptr<int>(), seg_len.numel(), tensor_wd.data_ptr<float>(), dyn.data_ptr<float>(),
+          (float)beta1, (float)beta2, (float)eps, adamw ? 1 : 0, cur_stream());
+}
+
+void sgd_step(at::Tensor g, c10::optional<at::Tensor> buf, at::Tensor w, c10::optional<at::Tensor> w_model,
+              at::Tensor seg_tensor, at::Tensor seg_start, at::Tensor seg_len, at::Tensor tensor_wd,
+              at::Tensor dyn, double momentum, double dampening, bool nesterov, bool first) {
+  for (auto* t : {&g, &w, &seg_tensor, &seg_start, &seg_len, &tensor_wd, &dyn}) CHECK_IN(*t);
+  CHECK_F32(w);
+  TORCH_CHECK(g.numel() >= w.numel());
+  if (momentum != 0.0) TORCH_CHECK(buf.has_value() && buf->defined() && buf->numel() == w.numel(), "momentum buffer");
+  int pdt = 0;
+  if (w_model.has_value() && w_model->defined()) { CHECK_IN(*w_model); pdt = dt_code(*w_model); }
+  ct_sgd(g.data_ptr(), dt_code(g), (float*)optr_mut(buf), w.data_ptr<float>(), optr_mut(w_model), pdt,
+         seg_tensor.data_ptr<int>(), seg_start.data_ptr<int64_t>(), seg_len.data_ptr<int>(), seg_len.numel(),
+         tensor_wd.data_ptr<float>(), dyn.data_ptr<float>(), (float)momentum, (float)dampening,
+         nesterov ? 1 : 0, first ? 1 : 0, cur_stream());
+}
+
+void sumsq_into(at::Tensor x, at::Tensor out) {
+  CHECK_IN(x); CHECK_IN(out); CHECK_F32(out);
+  TORCH_CHECK(x.numel() % 4 == 0, "sumsq: numel % 4");
+  ct_sumsq(x.data_ptr(), dt_code(x), x.numel(), out.data_ptr<float>(), cur_stream());
+}
+
+void clip_coef(at::Tensor sumsq, at::Tensor dyn, double base_scale, double max_norm) {
+  ct_clip_coef(sumsq.data_ptr<float>(), dyn.data_ptr<float>(), (float)base_scale, (float)max_norm, cur_stream());
+}
+
+// ---------------------------------------------------------------- cross entropy
+// logits [R, ld] bf16 (ld % 8 == 0); gradient written into `dlogits` (may be logits itself)
+std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor dlogits, int64_t V, at::Tensor labels,
+                                 c10::optional<at::Tensor> scale, int64_t ignore_index,
+                                 double label_smoothing) {
+  CHECK_IN(logits); CHECK_BF16(logits); CHECK_IN(dlogits); CHECK_BF16(dlogits); CHECK_IN(labels);
+  TORCH_CHECK(logits.dim() == 2 && dlogits.sizes() == logits.sizes());
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0));
+  const int R = logits.size(0), ld = logits.size(1);
+  TORCH_CHECK(V <= ld && ld % 8 == 0, "xent: ld must be a multiple of 8 and >= V");
+  auto fo = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({R}, fo), lse = at::empty({R}, fo);
+  const float* sp = nullptr;
+  if (scale.has_value() && scale->defined()) { CHECK_F32(*scale); sp = scale->data_ptr<float>(); }
+  ct_xent_fwd(logits.data_ptr(), dlogits.data_ptr(), ld, (int)V, labels.data_ptr<int64_t>(),
+              loss.data_ptr<float>(), lse.data_ptr<float>(), sp, R, (int)ignore_index,
+              (float)label_smoothing, cur_stream());
+  return {loss, lse};
+}
+
+// ---------------------------------------------------------------- attention (head_dim 64)
+// q, k, v, o: 4-D [B, S, H, 64] views with unit stride on the last dim (e.g. slices of a
+// packed [B, S, 3, H, 64] QKV projection output); key_bias: fp32 [B, Sk] additive.
+static void bshd_strides(const at::Tensor& t, long* st, const char* name) {
+  TORCH_CHECK(t.dim() == 4 && t.size(3) == 64 && t.stride(3) == 1, name, " must be [B,S,H,64] with unit last stride");
+  CHECK_CUDA(t); CHECK_BF16(t);
+  st[0] = t.stride(0); st[1] = t.stride(1); st[2] = t.stride(2);
+}
+
+at::Tensor attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o,
+                    c10::optional<at::Tensor> key_bias, double scale, double p, int64_t seed,
+                    int64_t offset, bool causal) {
+  long qs[3], ks[3], vs[3], os[3];
+  bshd_strides(q, qs, "q"); bshd_strides(k, ks, "k"); bshd_strides(v, vs, "v"); bshd_strides(o, os, "o");
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(2) == H && v.size(2) == H && v.size(1) == Sk);
+  TORCH_CHECK(o.size(0) == B && o.size(1) == Sq && o.size(2) == H);
+  const float* kb = nullptr; long kb_sb = 0;
+  if (key_bias.has_value() && key_bias->defined()) {
+    CHECK_F32(*key_bias); CHECK_CUDA(*key_bias);
+    TORCH_CHECK(key_bias->dim() == 2 && key_bias->size(0) == B && key_bias->size(1) == Sk && key_bias->stride(1) == 1);
+    kb = key_bias->data_ptr<float>(); kb_sb = key_bias->stride(0);
+  }
+  auto lse = at::empty({(long)B * H, Sq}, q.options().dtype(at::kFloat));
+  int rc = ct_attn_fwd(q.data_ptr(), qs, k.data_ptr(), ks, v.data_ptr(), vs, o.data_ptr(), os, kb, kb_sb,
+                       lse.data_ptr<float>(), B, H, Sq, Sk, (float)scale, (float)p, (uint64_t)seed,
+                       (uint64_t)offset, causal ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "attn_fwd failed rc=", rc);
+  return lse;
+}
+
+void attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor dO, at::Tensor dq,
+              at::Tensor dk, at::Tensor dv, c10::optional<at::Tensor> key_bias, at::Tensor lse,
+              double scale, double p, int64_t seed, int64_t offset, bool causal) {
+  long qs[3], ks[3], vs[3], os[3], dos[3], dqs[3], dks[3], dvs[3];
+  bshd_strides(q, qs, "q"); bshd_strides(k, ks, "k"); bshd_strides(v, vs, "v"); bshd_strides(o, os, "o");
+  bshd_strides(dO, dos, "dO"); bshd_strides(dq, dqs, "dq"); bshd_strides(dk, dks, "dk"); bshd_strides(dv, dvs, "dv");
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1);
+  TORCH_CHECK(dO.sizes() == o.sizes() && dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes());
+  TORCH_CHECK(lse.numel() == (long)B * H * Sq);
+  const float* kb = nullptr; long kb_sb = 0;
+  if (key_bias.has_value() && key_bias->defined()) { kb = key_bias->data_ptr<float>(); kb_sb = key_bias->stride(0); }
+  auto fo = q.options().dtype(at::kFloat);
+  auto delta = at::empty({(long)B * H * Sq}, fo);
+  at::Tensor dq_acc;
+  if (Sk > 128) dq_acc = at::empty({(long)B * H * Sq * 64}, fo);
+  int rc = ct_attn_bwd(q.data_ptr(), qs, k.data_ptr(), ks, v.data_ptr(), vs, o.data_ptr(), os, dO.data_ptr(), dos,
+                       dq.data_ptr(), dqs, dk.data_ptr(), dks, dv.data_ptr(), dvs, kb, kb_sb,
+                       lse.data_ptr<float>(), delta.data_ptr<float>(), Sk > 128 ? dq_acc.data_ptr<float>() : nullptr,
+                       B, H, Sq, Sk, (float)scale, (float)p, (uint64_t)seed, (uint64_t)offset,
+                       causal ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "attn_bwd failed rc=", rc);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "cloudtik_amd CDNA4 (gfx950) op library";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("bias_act_fwd", &bias_act_fwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("embed3_fwd", &embed3_fwd);
+  m.def("embed3_bwd", &embed3_bwd);
+  m.def("cast_into", &cast_into);
+  m.def("lamb_step", &lamb_step);
+  m.def("adam_step", &adam_step);
+  m.def("sgd_step", &sgd_step);
+  m.def("sumsq_into", &sumsq_into);
+  m.def("clip_coef", &clip_coef);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+}

@@ -1,0 +1,136 @@
+// Shared device helpers for the cloudtik_amd CDNA4 (gfx950) op library.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes; blocks are multiples of 64 threads.
+//   * bf16 tensors are moved as 16-byte vectors (8 x bf16) per lane (Guideline 13:
+//     hipcc does not auto-vectorise 16-bit loads).
+//   * statistics / reductions are carried in fp32.
+//   * every launch function takes an explicit hipStream_t and performs no
+//     allocation or synchronisation, so callers may capture it into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+namespace ct {
+
+typedef unsigned short bf16_t;  // raw storage type for bf16
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;   // MFMA operand (8 x bf16)
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// Round-to-nearest-even; a plain __bf16 cast lowers to v_cvt_pk_bf16_f32 on gfx950
+// and keeps NaNs NaN (MI355X_MICROARCH.md correctness table).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+template <typename T>
+__device__ __forceinline__ float to_f(T v);
+template <>
+__device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+
+template <typename T>
+__device__ __forceinline__ T from_f(float v);
+template <>
+__device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `scratch` must hold blockDim.x/64 floats. Result broadcast to all threads.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  return r;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): consecutive logical tiles land on the same XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace ct
+
+#define CT_HIP_CHECK(expr)                                                              \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+    }                                                                                   \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG (Philox-4x32, 7 rounds) for dropout: the mask is a pure function of
+// (seed, offset, element index), so backward regenerates it instead of storing it.
+// ---------------------------------------------------------------------------------------
+namespace ct {
+struct u32x4 { uint32_t x, y, z, w; };
+__device__ __forceinline__ u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                           uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+// 8 keep-bits (bit j set = keep element 8*v+j) for the 8-element vector number `v`
+// of a stream identified by (seed, offset).
+__device__ __forceinline__ uint32_t dropout_bits8(uint64_t seed, uint64_t offset, uint64_t v,
+                                                 uint32_t thresh) {
+  const u32x4 a = philox4x32((uint32_t)(2 * v), (uint32_t)(v >> 31), (uint32_t)offset,
+                             (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const u32x4 b = philox4x32((uint32_t)(2 * v + 1), (uint32_t)(v >> 31), (uint32_t)offset,
+                             (uint32_t)(offset >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (uint32_t)(a.x >= thresh) | ((uint32_t)(a.y >= thresh) << 1) |
+         ((uint32_t)(a.z >= thresh) << 2) | ((uint32_t)(a.w >= thresh) << 3) |
+         ((uint32_t)(b.x >= thresh) << 4) | ((uint32_t)(b.y >= thresh) << 5) |
+         ((uint32_t)(b.z >= thresh) << 6) | ((uint32_t)(b.w >= thresh) << 7);
+}
+__host__ __device__ inline uint32_t dropout_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+}  // namespace ct

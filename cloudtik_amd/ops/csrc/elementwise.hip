@@ -1,0 +1,231 @@
+// Memory-bound fused elementwise kernels (bf16, 16-byte vectors per lane):
+//   * bias + activation (GELU-erf / ReLU / identity) forward, and its backward with the
+//     bias gradient column-sum fused in (FFN1 of BERT: the hipBLASLt GEMM runs bias-free,
+//     this kernel adds the bias, applies GELU and keeps the pre-activation for backward).
+//   * dropout forward/backward with a regenerated Philox mask (nothing stored).
+//   * word + position + token-type embedding gather-sum and its atomic backward
+//     (HF BertEmbeddings used by the reference BERT-large pretraining,
+//     run_pretrain_mlperf.py:449-471).
+//   * fp32 <-> bf16 casts, scaled adds.
+#include "common.h"
+
+namespace ct {
+
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2 };
+
+__device__ __forceinline__ float act_f(float x, int act) {
+  return act == ACT_GELU ? gelu_erf(x) : (act == ACT_RELU ? fmaxf(x, 0.f) : x);
+}
+__device__ __forceinline__ float act_g(float x, int act) {
+  return act == ACT_GELU ? gelu_erf_grad(x) : (act == ACT_RELU ? (x > 0.f ? 1.f : 0.f) : 1.f);
+}
+
+// y[m, n] = act(z[m, n] + bias[n]); rows x N, N % 8 == 0.
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ z,
+                                                           const bf16_t* __restrict__ bias,
+                                                           bf16_t* __restrict__ y, long total_vec,
+                                                           int nvec_row, int act) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
+       v += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(v % nvec_row);
+    const u16x8 zv = reinterpret_cast<const u16x8*>(z)[v];
+    u16x8 bv = u16x8(0);
+    if (bias) bv = reinterpret_cast<const u16x8*>(bias)[c];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(act_f(bf2f(zv[j]) + bf2f(bv[j]), act));
+    reinterpret_cast<u16x8*>(y)[v] = o;
+  }
+}
+
+// dz = dy * act'(z + bias); dbias partials [grid, N] (each block owns a fixed set of
+// column-vectors so its partial stays in registers across its grid-stride rows).
+// Block: 256 threads = (256 / cols_per_block) rows-in-flight x cols_per_block vectors.
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ z, const bf16_t* __restrict__ bias,
+    bf16_t* __restrict__ dz, float* __restrict__ part, int M, int nvec_row, int act) {
+  // blockIdx.y selects a 64-vector column slice; threads: 64 column vectors x 4 row lanes
+  const int cv = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  __shared__ float red[4][64 * 8];
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (cv < nvec_row) {
+    u16x8 bv = u16x8(0);
+    if (bias) bv = reinterpret_cast<const u16x8*>(bias)[cv];
+    for (int row = blockIdx.x * 4 + rl; row < M; row += gridDim.x * 4) {
+      const long idx = (long)row * nvec_row + cv;
+      const u16x8 zv = reinterpret_cast<const u16x8*>(z)[idx];
+      const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[idx];
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = bf2f(gv[j]) * act_g(bf2f(zv[j]) + bf2f(bv[j]), act);
+        o[j] = f2bf(d);
+        acc[j] += d;
+      }
+      reinterpret_cast<u16x8*>(dz)[idx] = o;
+    }
+  }
+  if (!part) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][(threadIdx.x & 63) * 8 + j] = acc[j];
+  __syncthreads();
+  const int N = nvec_row * 8;
+  for (int t = threadIdx.x; t < 64 * 8; t += 256) {
+    const int col = blockIdx.y * 512 + t;
+    if (col < N) part[(long)blockIdx.x * N + col] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+  }
+}
+
+// y = dropout(x) (keep-scale 1/(1-p)), mask from Philox(seed, offset, vector index)
+__global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__ x,
+                                                      bf16_t* __restrict__ y, long total_vec,
+                                                      uint32_t thresh, float scale, uint64_t seed,
+                                                      uint64_t offset) {
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
+       v += (long)gridDim.x * blockDim.x) {
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
+    const uint32_t keep = dropout_bits8(seed, offset, (uint64_t)v, thresh);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = ((keep >> j) & 1u) ? f2bf(bf2f(xv[j]) * scale) : (bf16_t)0;
+    reinterpret_cast<u16x8*>(y)[v] = o;
+  }
+}
+
+// out[t, :] = W[ids[t]] + P[pos(t)] + T[tt[t]]   (pos(t) = t % S), row width N
+__global__ __launch_bounds__(256) void embed3_fwd_kernel(
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ tt, const bf16_t* __restrict__ W,
+    const bf16_t* __restrict__ P, const bf16_t* __restrict__ T, bf16_t* __restrict__ out, int ntok,
+    int S, int N) {
+  const int nvec = N >> 3;
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < ntok; t += gridDim.x * 4) {
+    const long wi = ids[t];
+    const long ti = tt ? tt[t] : 0;
+    const int pi = t % S;
+    for (int c = lane; c < nvec; c += 64) {
+      const u16x8 a = reinterpret_cast<const u16x8*>(W + wi * N)[c];
+      u16x8 b = u16x8(0), d = u16x8(0);
+      if (P) b = reinterpret_cast<const u16x8*>(P + (long)pi * N)[c];
+      if (T) d = reinterpret_cast<const u16x8*>(T + ti * N)[c];
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(a[j]) + bf2f(b[j]) + bf2f(d[j]));
+      reinterpret_cast<u16x8*>(out + (long)t * N)[c] = o;
+    }
+  }
+}
+
+// Scatter-add rows of g into fp32 tables with float atomics (chip-wide ~1.3 TB/s of added
+// bytes; each wave-instruction adds 256 contiguous bytes of one row: the full-rate shape).
+__global__ __launch_bounds__(256) void embed3_bwd_kernel(
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ tt, const bf16_t* __restrict__ g,
+    float* __restrict__ dW, float* __restrict__ dP, float* __restrict__ dT, int ntok, int S, int N) {
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < ntok; t += gridDim.x * 4) {
+    const long wi = ids[t];
+    const long ti = tt ? tt[t] : 0;
+    const int pi = t % S;
+    const bf16_t* gr = g + (long)t * N;
+    for (int c = lane; c < N; c += 64) {
+      const float v = bf2f(gr[c]);
+      if (dW) atomicAdd(dW + wi * N + c, v);
+      if (dP) atomicAdd(dP + (long)pi * N + c, v);
+      if (dT) atomicAdd(dT + ti * N + c, v);
+    }
+  }
+}
+
+template <typename IN, typename OUT>
+__global__ void cast_kernel(const IN* __restrict__ x, OUT* __restrict__ y, long n, float scale,
+                            int accumulate) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = to_f<IN>(x[i]) * scale;
+    if (accumulate) v += to_f<OUT>(y[i]);
+    y[i] = from_f<OUT>(v);
+  }
+}
+
+inline int grid_for(long work, int block = 256) {
+  long g = (work + block - 1) / block;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+extern "C" int ct_bias_act_fwd(const void* z, const void* bias, void* y, long M, int N, int act,
+                               hipStream_t stream) {
+  if (N % 8) return -1;
+  const long tv = M * (N / 8);
+  bias_act_fwd_kernel<<<grid_for(tv), 256, 0, stream>>>((const bf16_t*)z, (const bf16_t*)bias,
+                                                         (bf16_t*)y, tv, N / 8, act);
+  return 0;
+}
+
+extern "C" int ct_bias_act_bwd_grid(long M) {
+  long g = (M + 3) / 4;
+  return (int)(g > 256 ? 256 : g);
+}
+
+// part: float[ct_bias_act_bwd_grid(M) * N] workspace (may be null if no dbias wanted)
+extern "C" int ct_bias_act_bwd(const void* dy, const void* z, const void* bias, void* dz,
+                               float* part, void* dbias, long M, int N, int act, int param_fp32,
+                               int accumulate, hipStream_t stream);
+extern "C" int ct_colsum(const float* part, void* out, int P, int N, int out_fp32, int accumulate,
+                         hipStream_t stream);
+extern "C" int ct_bias_act_bwd(const void* dy, const void* z, const void* bias, void* dz,
+                               float* part, void* dbias, long M, int N, int act, int param_fp32,
+                               int accumulate, hipStream_t stream) {
+  if (N % 8) return -1;
+  const int gx = ct_bias_act_bwd_grid(M);
+  dim3 grid(gx, ceil_div(N / 8, 64));
+  bias_act_bwd_kernel<<<grid, 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)z,
+                                                (const bf16_t*)bias, (bf16_t*)dz,
+                                                dbias ? part : nullptr, (int)M, N / 8, act);
+  if (dbias) ct_colsum(part, dbias, gx, N, param_fp32, accumulate, stream);
+  return 0;
+}
+
+extern "C" int ct_dropout(const void* x, void* y, long n, float p, uint64_t seed, uint64_t offset,
+                          hipStream_t stream) {
+  if (n % 8) return -1;
+  const long tv = n / 8;
+  dropout_kernel<<<grid_for(tv), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, tv,
+                                                   dropout_threshold(p), 1.f / (1.f - p), seed,
+                                                   offset);
+  return 0;
+}
+
+extern "C" int ct_embed3_fwd(const int64_t* ids, const int64_t* tt, const void* W, const void* P,
+                             const void* T, void* out, int ntok, int S, int N, hipStream_t stream) {
+  if (N % 8) return -1;
+  embed3_fwd_kernel<<<grid_for(ntok, 4), 256, 0, stream>>>(ids, tt, (const bf16_t*)W,
+                                                           (const bf16_t*)P, (const bf16_t*)T,
+                                                           (bf16_t*)out, ntok, S, N);
+  return 0;
+}
+
+extern "C" int ct_embed3_bwd(const int64_t* ids, const int64_t* tt, const void* g, float* dW,
+                             float* dP, float* dT, int ntok, int S, int N, hipStream_t stream) {
+  embed3_bwd_kernel<<<grid_for(ntok, 4), 256, 0, stream>>>(ids, tt, (const bf16_t*)g, dW, dP, dT,
+                                                           ntok, S, N);
+  return 0;
+}
+
+// dtype codes: 0 = fp32, 1 = bf16
+extern "C" int ct_cast(const void* x, int xdt, void* y, int ydt, long n, float scale, int accumulate,
+                       hipStream_t stream) {
+  const int g = grid_for(n);
+  if (xdt == 0 && ydt == 1) cast_kernel<float, bf16_t><<<g, 256, 0, stream>>>((const float*)x, (bf16_t*)y, n, scale, accumulate);
+  else if (xdt == 1 && ydt == 0) cast_kernel<bf16_t, float><<<g, 256, 0, stream>>>((const bf16_t*)x, (float*)y, n, scale, accumulate);
+  else if (xdt == 0 && ydt == 0) cast_kernel<float, float><<<g, 256, 0, stream>>>((const float*)x, (float*)y, n, scale, accumulate);
+  else cast_kernel<bf16_t, bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, n, scale, accumulate);
+  return 0;
+}

@@ -1,0 +1,292 @@
+// LayerNorm / RMSNorm forward + backward with a fused "bias + dropout + residual" prologue:
+//
+//     s = residual + dropout(x + bias)          (each part optional)
+//     y = LN(s) * gamma + beta
+//
+// This is the post-LN block epilogue of HF BERT (BertSelfOutput / BertOutput) that the
+// reference's BERT-large pretraining runs 48x per step
+// (applications/ai/quickstart/models/language_modeling/pytorch/bert_large/training/
+// run_pretrain_mlperf.py:449-471, hidden 1024).  MI355X design:
+//   * one wave64 per row, the row held in VGPRs (N <= 2048), bf16 moved as 16-byte
+//     vectors, fp32 statistics from registers -> exactly one HBM read of each input.
+//   * the projection GEMM runs WITHOUT bias (plain hipBLASLt); its bias, the dropout and
+//     the residual add are folded in here, and backward folds d(bias) = colsum(dx) into
+//     the same pass as dgamma/dbeta -> no separate bias-grad reduction kernel.
+//   * dropout mask regenerated from Philox(seed, offset, index) in backward: nothing stored.
+//   * backward keeps per-lane dgamma/dbeta/dbias partials across a grid-stride row loop;
+//     cross-row reduction = [grid x N] fp32 partials + one column-sum kernel (no atomics,
+//     bitwise reproducible).
+#include "common.h"
+
+namespace ct {
+
+struct LnFwdArgs {
+  const bf16_t* x; const bf16_t* bias; const bf16_t* res;
+  const bf16_t* gamma; const bf16_t* beta;
+  bf16_t* y; bf16_t* s_out; float* mean_out; float* rstd_out;
+  int M, N; float eps; uint32_t thresh; float scale; uint64_t seed, offset;
+};
+
+template <int MAXV, bool RMS>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  const int N = a.N, nvec = N >> 3;
+  const bool has_bias = a.bias != nullptr, has_res = a.res != nullptr, drop = a.thresh != 0;
+  const bool write_s = a.s_out != nullptr;
+  for (int row = blockIdx.x * wpb + (threadIdx.x >> 6); row < a.M; row += gridDim.x * wpb) {
+    const u16x8* xr = reinterpret_cast<const u16x8*>(a.x + (size_t)row * N);
+    const u16x8* rr = reinterpret_cast<const u16x8*>(a.res + (size_t)row * N);
+    const u16x8* br = reinterpret_cast<const u16x8*>(a.bias);
+    float v[MAXV][8];
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        const u16x8 xv = xr[c];
+        u16x8 bv = u16x8(0), rv = u16x8(0);
+        if (has_bias) bv = br[c];
+        if (has_res) rv = rr[c];
+        uint32_t keep = 0xFFu;
+        if (drop) keep = dropout_bits8(a.seed, a.offset, (uint64_t)row * nvec + c, a.thresh);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = bf2f(xv[j]) + bf2f(bv[j]);
+          if (drop) t = ((keep >> j) & 1u) ? t * a.scale : 0.f;
+          t += bf2f(rv[j]);
+          o[j] = f2bf(t);
+          v[i][j] = bf2f(o[j]);  // normalise the rounded sum: backward sees the same s
+          sum += v[i][j];
+        }
+        if (write_s) reinterpret_cast<u16x8*>(a.s_out + (size_t)row * N)[c] = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+      }
+    }
+    sum = wave_sum(sum);
+    const float mean = RMS ? 0.f : sum / N;
+    float var = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      if (lane + i * 64 < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; var += d * d; }
+      }
+    }
+    var = wave_sum(var) / N;
+    const float rstd = rsqrtf(var + a.eps);
+    if (lane == 0) {
+      if (a.mean_out) a.mean_out[row] = mean;
+      a.rstd_out[row] = rstd;
+    }
+    u16x8* yr = reinterpret_cast<u16x8*>(a.y + (size_t)row * N);
+    const u16x8* g8 = reinterpret_cast<const u16x8*>(a.gamma);
+    const u16x8* b8 = reinterpret_cast<const u16x8*>(a.beta);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        const u16x8 g = g8[c];
+        u16x8 bb = u16x8(0);
+        if (!RMS && a.beta) bb = b8[c];
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf((v[i][j] - mean) * rstd * bf2f(g[j]) + bf2f(bb[j]));
+        yr[c] = o;
+      }
+    }
+  }
+}
+
+struct LnBwdArgs {
+  const bf16_t* dy; const bf16_t* s; const bf16_t* gamma; const float* mean; const float* rstd;
+  const bf16_t* dextra;  // optional extra gradient added to ds (e.g. a skip path)
+  bf16_t* ds;            // grad wrt s (= grad of the residual input)
+  bf16_t* dx;            // grad wrt x (after dropout backward); may alias nothing / be null
+  float* dg_part; float* db_part; float* dbias_part;
+  int M, N; uint32_t thresh; float scale; uint64_t seed, offset;
+};
+
+template <int MAXV, bool RMS>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  const int N = a.N, nvec = N >> 3;
+  const bool drop = a.thresh != 0;
+  const bool want_dbias = a.dbias_part != nullptr;
+  float dg[MAXV][8], db[MAXV][8], dbi[MAXV][8], g[MAXV][8];
+  const u16x8* g8 = reinterpret_cast<const u16x8*>(a.gamma);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = lane + i * 64;
+    const u16x8 gv = c < nvec ? g8[c] : u16x8(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; g[i][j] = bf2f(gv[j]); }
+  }
+  for (int row = blockIdx.x * wpb + wid; row < a.M; row += gridDim.x * wpb) {
+    const u16x8* sr = reinterpret_cast<const u16x8*>(a.s + (size_t)row * N);
+    const u16x8* dyr = reinterpret_cast<const u16x8*>(a.dy + (size_t)row * N);
+    const float mean = RMS ? 0.f : a.mean[row];
+    const float rstd = a.rstd[row];
+    float xh[MAXV][8], dyg[MAXV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        const u16x8 sv = sr[c], dv = dyr[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xhat = (bf2f(sv[j]) - mean) * rstd;
+          const float d = bf2f(dv[j]);
+          xh[i][j] = xhat;
+          dyg[i][j] = d * g[i][j];
+          dg[i][j] += d * xhat;
+          db[i][j] += d;
+          s1 += dyg[i][j];
+          s2 += dyg[i][j] * xhat;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { xh[i][j] = 0.f; dyg[i][j] = 0.f; }
+      }
+    }
+    s1 = wave_sum(s1) / N;
+    s2 = wave_sum(s2) / N;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nvec) {
+        u16x8 ev = u16x8(0);
+        if (a.dextra) ev = reinterpret_cast<const u16x8*>(a.dextra + (size_t)row * N)[c];
+        uint32_t keep = 0xFFu;
+        if (drop) keep = dropout_bits8(a.seed, a.offset, (uint64_t)row * nvec + c, a.thresh);
+        u16x8 o, od;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = RMS ? rstd * (dyg[i][j] - xh[i][j] * s2) : rstd * (dyg[i][j] - s1 - xh[i][j] * s2);
+          t += bf2f(ev[j]);
+          o[j] = f2bf(t);
+          float tx = drop ? (((keep >> j) & 1u) ? t * a.scale : 0.f) : t;
+          od[j] = f2bf(tx);
+          dbi[i][j] += tx;
+        }
+        if (a.ds) reinterpret_cast<u16x8*>(a.ds + (size_t)row * N)[c] = o;
+        if (a.dx) reinterpret_cast<u16x8*>(a.dx + (size_t)row * N)[c] = od;
+      }
+    }
+  }
+  // reduce the block's waves through LDS, 512 columns at a time
+  const int nparts = want_dbias ? 3 : 2;
+  for (int base = 0; base < N; base += 512) {
+    for (int pass = 0; pass < nparts; ++pass) {
+#pragma unroll
+      for (int i = 0; i < MAXV; ++i) {
+        const int c = lane + i * 64;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = c * 8 + j;
+          if (c < nvec && col >= base && col < base + 512)
+            red[wid][col - base] = pass == 0 ? dg[i][j] : (pass == 1 ? db[i][j] : dbi[i][j]);
+        }
+      }
+      __syncthreads();
+      float* dst = pass == 0 ? a.dg_part : (pass == 1 ? a.db_part : a.dbias_part);
+      for (int col = threadIdx.x; col < 512 && base + col < N; col += blockDim.x) {
+        float t = 0.f;
+        for (int w = 0; w < wpb; ++w) t += red[w][col];
+        if (dst) dst[(size_t)blockIdx.x * N + base + col] = t;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// out[col] (+)= sum_p part[p, col]
+template <typename OUT>
+__global__ void colsum_kernel(const float* __restrict__ part, OUT* __restrict__ out, int P, int N,
+                              int accumulate) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  float t = 0.f;
+  for (int p = 0; p < P; ++p) t += part[(size_t)p * N + col];
+  if (accumulate) t += to_f<OUT>(out[col]);
+  out[col] = from_f<OUT>(t);
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+extern "C" int ct_colsum(const float* part, void* out, int P, int N, int out_fp32, int accumulate,
+                         hipStream_t stream) {
+  const int cb = ceil_div(N, 256);
+  if (out_fp32) colsum_kernel<float><<<cb, 256, 0, stream>>>(part, (float*)out, P, N, accumulate);
+  else colsum_kernel<bf16_t><<<cb, 256, 0, stream>>>(part, (bf16_t*)out, P, N, accumulate);
+  return 0;
+}
+
+extern "C" int ct_layernorm_fwd(const void* x, const void* bias, const void* res, const void* g,
+                                const void* b, void* y, void* s_out, float* mean, float* rstd,
+                                int M, int N, float eps, int rms, float p_drop, uint64_t seed,
+                                uint64_t offset, hipStream_t stream) {
+  if (N % 8 != 0 || N > 2048 || M <= 0) return -1;
+  LnFwdArgs a;
+  a.x = (const bf16_t*)x; a.bias = (const bf16_t*)bias; a.res = (const bf16_t*)res;
+  a.gamma = (const bf16_t*)g; a.beta = (const bf16_t*)b; a.y = (bf16_t*)y; a.s_out = (bf16_t*)s_out;
+  a.mean_out = mean; a.rstd_out = rstd; a.M = M; a.N = N; a.eps = eps;
+  a.thresh = p_drop > 0.f ? dropout_threshold(p_drop) : 0u;
+  a.scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed; a.offset = offset;
+  const int mv = (N / 8 + 63) / 64;
+  int grid = ceil_div(M, 4);
+  if (grid > 16384) grid = 16384;
+#define CT_LNF(MV) case MV: if (rms) ln_fwd_kernel<MV, true><<<grid, 256, 0, stream>>>(a); \
+                            else ln_fwd_kernel<MV, false><<<grid, 256, 0, stream>>>(a); break;
+  switch (mv) {
+    CT_LNF(1) CT_LNF(2) CT_LNF(3) CT_LNF(4)
+    default: return -1;
+  }
+#undef CT_LNF
+  return 0;
+}
+
+extern "C" int ct_layernorm_bwd_grid(int M) {
+  const int grid = ceil_div(M, 4);
+  return grid > 512 ? 512 : grid;
+}
+
+// Workspace: part = float[3 * grid * N] (grid = ct_layernorm_bwd_grid(M)).
+extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, const float* mean,
+                                const float* rstd, const void* dextra, void* ds, void* dx,
+                                float* part, void* dgamma, void* dbeta, void* dbias, int M, int N,
+                                int rms, int param_fp32, int accumulate, float p_drop,
+                                uint64_t seed, uint64_t offset, hipStream_t stream) {
+  if (N % 8 != 0 || N > 2048 || M <= 0) return -1;
+  const int grid = ct_layernorm_bwd_grid(M);
+  LnBwdArgs a;
+  a.dy = (const bf16_t*)dy; a.s = (const bf16_t*)s; a.gamma = (const bf16_t*)g; a.mean = mean;
+  a.rstd = rstd; a.dextra = (const bf16_t*)dextra; a.ds = (bf16_t*)ds; a.dx = (bf16_t*)dx;
+  a.dg_part = part; a.db_part = (rms || !dbeta) ? nullptr : part + (size_t)grid * N;
+  a.dbias_part = dbias ? part + (size_t)2 * grid * N : nullptr;
+  a.M = M; a.N = N;
+  a.thresh = p_drop > 0.f ? dropout_threshold(p_drop) : 0u;
+  a.scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed; a.offset = offset;
+  const int mv = (N / 8 + 63) / 64;
+#define CT_LNB(MV) case MV: if (rms) ln_bwd_kernel<MV, true><<<grid, 256, 0, stream>>>(a); \
+                            else ln_bwd_kernel<MV, false><<<grid, 256, 0, stream>>>(a); break;
+  switch (mv) {
+    CT_LNB(1) CT_LNB(2) CT_LNB(3) CT_LNB(4)
+    default: return -1;
+  }
+#undef CT_LNB
+  ct_colsum(a.dg_part, dgamma, grid, N, param_fp32, accumulate, stream);
+  if (a.db_part) ct_colsum(a.db_part, dbeta, grid, N, param_fp32, accumulate, stream);
+  if (a.dbias_part) ct_colsum(a.dbias_part, dbias, grid, N, param_fp32, accumulate, stream);
+  return 0;
+}

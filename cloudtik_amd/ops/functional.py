@@ -1,0 +1,186 @@
+"""Autograd front-ends for the HIP op library (GPU) with reference fallbacks (CPU)."""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+
+ACT_NONE, ACT_GELU, ACT_RELU = ref.ACT_NONE, ref.ACT_GELU, ref.ACT_RELU
+
+
+def _pkg():
+    from cloudtik_amd import ops
+    return ops
+
+
+def _native(*ts):
+    return _pkg()._use_native(*ts)
+
+
+def _C():
+    return _pkg().require_native()
+
+
+def _opt(t):
+    return t if (t is not None and isinstance(t, torch.Tensor)) else None
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bias, residual, eps, p, seed, offset, rms):
+        y, s, mean, rstd = _C().layernorm_fwd(x, bias, residual, gamma, beta, eps, rms, p, seed, offset)
+        s_saved = s if s is not None and s.numel() > 0 else x
+        ctx.save_for_backward(s_saved, gamma, mean, rstd)
+        ctx.cfg = (p, seed, offset, rms, beta is not None, bias is not None, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, gamma, mean, rstd = ctx.saved_tensors
+        p, seed, offset, rms, has_beta, has_bias, has_res = ctx.cfg
+        need_dx = p > 0.0
+        ds, dx, dgamma, dbeta, dbias = _C().layernorm_bwd(
+            dy.contiguous(), s, gamma, mean, rstd, None, rms, has_beta, has_bias, need_dx, p, seed, offset)
+        dx_out = dx if need_dx else ds
+        return (dx_out, dgamma, dbeta if has_beta else None, dbias if has_bias else None,
+                ds if has_res else None, None, None, None, None, None)
+
+
+def layer_norm(x, gamma, beta=None, eps=1e-12, bias=None, residual=None, p=0.0,
+               training=True, rms=False):
+    """y = LayerNorm(residual + dropout(x + bias)) * gamma + beta  (all parts optional)."""
+    p = float(p) if training else 0.0
+    ops = _pkg()
+    if _native(x):
+        seed, offset = ops._rng.next(x.numel()) if p > 0 else (0, 0)
+        N = x.shape[-1]
+        if N % 8 == 0 and N <= 2048 and x.dtype == torch.bfloat16:
+            return _LayerNormFn.apply(x.contiguous(), gamma, beta, bias,
+                                      residual.contiguous() if residual is not None else None,
+                                      float(eps), p, seed, offset, bool(rms))
+    else:
+        seed, offset = ops._rng.next(x.numel()) if p > 0 else (0, 0)
+    y, _ = ref.layer_norm(x, gamma, beta, eps, bias, residual, p, seed, offset, rms)
+    return y
+
+
+# ----------------------------------------------------------------------------- bias + act
+class _BiasActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, bias, act):
+        ctx.save_for_backward(z, bias)
+        ctx.act = act
+        ctx.has_bias = bias is not None
+        return _C().bias_act_fwd(z, bias, act)
+
+    @staticmethod
+    def backward(ctx, dy):
+        z, bias = ctx.saved_tensors
+        dz, dbias = _C().bias_act_bwd(dy.contiguous(), z, bias, ctx.act, ctx.has_bias)
+        return dz, (dbias if ctx.has_bias else None), None
+
+
+def bias_act(z, bias=None, act=ACT_GELU):
+    if _native(z) and z.dtype == torch.bfloat16 and z.shape[-1] % 8 == 0:
+        return _BiasActFn.apply(z.contiguous(), bias, int(act))
+    return ref.bias_act(z, bias, act)
+
+
+def bias_gelu(z, bias=None):
+    return bias_act(z, bias, ACT_GELU)
+
+
+# ----------------------------------------------------------------------------- dropout
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed, offset):
+        ctx.cfg = (p, seed, offset)
+        return _C().dropout_fwd(x, p, seed, offset)
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, seed, offset = ctx.cfg
+        return _C().dropout_fwd(dy.contiguous(), p, seed, offset), None, None, None
+
+
+def dropout(x, p=0.1, training=True):
+    if not training or p <= 0.0:
+        return x
+    seed, offset = _pkg()._rng.next(x.numel())
+    if _native(x) and x.dtype == torch.bfloat16 and x.numel() % 8 == 0:
+        return _DropoutFn.apply(x.contiguous(), float(p), seed, offset)
+    if x.numel() % 8 == 0:
+        return ref.dropout(x, p, seed, offset)
+    return torch.nn.functional.dropout(x, p, True)
+
+
+# ----------------------------------------------------------------------------- embeddings
+class _Embed3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, tt, W, P, T):
+        ctx.save_for_backward(ids, tt)
+        ctx.shapes = (W.shape, None if P is None else P.shape, None if T is None else T.shape)
+        ctx.dtypes = (W.dtype,)
+        ctx.has = (P is not None, T is not None)
+        return _C().embed3_fwd(ids, tt, W, P, T)
+
+    @staticmethod
+    def backward(ctx, g):
+        ids, tt = ctx.saved_tensors
+        ws, ps, ts = ctx.shapes
+        f32 = dict(dtype=torch.float32, device=g.device)
+        dW = torch.zeros(ws, **f32)
+        dP = torch.zeros(ps, **f32) if ctx.has[0] else None
+        dT = torch.zeros(ts, **f32) if ctx.has[1] else None
+        _C().embed3_bwd(ids, tt, g.contiguous(), dW, dP, dT)
+        dt = ctx.dtypes[0]
+        return (None, None, dW.to(dt), dP.to(dt) if dP is not None else None,
+                dT.to(dt) if dT is not None else None)
+
+
+def embedding3(ids, token_type_ids, W, P=None, T=None):
+    """word[ids] + position[arange(S)] + token_type[tt] (sum of up to three tables)."""
+    if _native(W) and W.dtype == torch.bfloat16 and W.shape[1] % 8 == 0:
+        tt = token_type_ids.contiguous() if (token_type_ids is not None and T is not None) else None
+        return _Embed3Fn.apply(ids.contiguous(), tt, W, P, T)
+    return ref.embedding3(ids, token_type_ids, W, P, T)
+
+
+# ----------------------------------------------------------------------------- linear + CE
+class _LinearXentFn(torch.autograd.Function):
+    """loss = CE(x @ W[:ld].T + b, labels) over valid labels; gradient built in forward."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, labels, V, ignore_index, label_smoothing):
+        logits = torch.nn.functional.linear(x, W, b)
+        valid = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+        inv = (1.0 / valid).reshape(1)
+        loss_rows, _ = _C().xent_fwd(logits, logits, V, labels, inv, ignore_index, label_smoothing)
+        ctx.save_for_backward(x, W, logits)   # `logits` now holds d(loss)/d(logits)
+        ctx.has_b = b is not None
+        return loss_rows.sum() * inv[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W, dlogits = ctx.saved_tensors
+        dx = torch.matmul(dlogits, W) * g.to(dlogits.dtype)
+        dW = torch.matmul(dlogits.t(), x) * g.to(dlogits.dtype)
+        db = dlogits.sum(0, dtype=torch.float32).mul_(g).to(dlogits.dtype) if ctx.has_b else None
+        return dx, dW, db, None, None, None, None
+
+
+def cross_entropy_fused(x, W, b, labels, V=None, ignore_index=-100, label_smoothing=0.0):
+    """Mean cross entropy of ``x @ W.T + b`` against ``labels``.
+
+    ``W`` may have rows padded beyond the true class count ``V`` (rows >= V are masked out
+    of the softmax); on the GPU the softmax/NLL/gradient run in one HIP kernel whose
+    gradient overwrites the logits buffer in place."""
+    V = int(V or W.shape[0])
+    if _native(x) and x.dtype == torch.bfloat16 and W.shape[0] % 8 == 0:
+        return _LinearXentFn.apply(x.contiguous(), W, b, labels.contiguous(), V, int(ignore_index),
+                                   float(label_smoothing))
+    logits = torch.nn.functional.linear(x, W, b)
+    return ref.cross_entropy(logits, labels, V, ignore_index, label_smoothing)
+
+

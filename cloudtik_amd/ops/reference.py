@@ -1,0 +1,158 @@
+"""Plain-PyTorch reference implementations of every cloudtik_amd HIP op.
+
+Used (a) as the CPU execution path and (b) as the fp32 oracle in the GPU numerics
+tests.  The dropout masks are bit-identical to the kernels': both evaluate the same
+counter-based Philox-4x32-7 stream (``common.h: dropout_bits8``), so a CPU run and a GPU
+run of the same model with the same seed drop the same elements.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+M32 = np.uint64(0xFFFFFFFF)
+ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
+
+
+def _philox4x32_7(c0, c1, c2, c3, k0, k1):
+    for _ in range(7):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & M32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & M32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0), lo1, (hi0 ^ c3 ^ k1), lo0
+        k0 = (k0 + np.uint64(0x9E3779B9)) & M32
+        k1 = (k1 + np.uint64(0xBB67AE85)) & M32
+    return c0, c1, c2, c3
+
+
+def dropout_threshold(p: float) -> int:
+    t = float(p) * 4294967296.0
+    return 0xFFFFFFFF if t >= 4294967295.0 else int(t)
+
+
+def dropout_keep_mask(n: int, p: float, seed: int, offset: int) -> torch.Tensor:
+    """Boolean keep-mask of ``n`` elements (n % 8 == 0), identical to the HIP kernels."""
+    assert n % 8 == 0
+    v = np.arange(n // 8, dtype=np.uint64)
+    seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+    offset = np.uint64(offset & 0xFFFFFFFFFFFFFFFF)
+    k0 = np.full_like(v, seed & M32)
+    k1 = np.full_like(v, seed >> np.uint64(32))
+    c2 = np.full_like(v, offset & M32)
+    c3 = np.full_like(v, offset >> np.uint64(32))
+    c1 = (v >> np.uint64(31)) & M32
+    thr = np.uint64(dropout_threshold(p))
+    out = np.empty((n // 8, 8), dtype=bool)
+    for half in range(2):
+        c0 = (np.uint64(2) * v + np.uint64(half)) & M32
+        r = _philox4x32_7(c0, c1.copy(), c2.copy(), c3.copy(), k0.copy(), k1.copy())
+        for j in range(4):
+            out[:, half * 4 + j] = r[j] >= thr
+    return torch.from_numpy(out.reshape(-1))
+
+
+def dropout(x: torch.Tensor, p: float, seed: int, offset: int) -> torch.Tensor:
+    if p <= 0.0:
+        return x
+    keep = dropout_keep_mask(x.numel(), p, seed, offset).to(x.device).view_as(x)
+    return torch.where(keep, x * (1.0 / (1.0 - p)), torch.zeros_like(x))
+
+
+def _round(x: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    return x.to(like.dtype).to(torch.float32) if like.dtype != torch.float32 else x
+
+
+def layer_norm(x, gamma, beta=None, eps=1e-12, bias=None, residual=None, p=0.0, seed=0,
+               offset=0, rms=False):
+    """y = LN(residual + dropout(x + bias)); returns (y, s) with s the LN input."""
+    xf = x.float()
+    if bias is not None:
+        xf = xf + bias.float()
+    if p > 0.0:
+        xf = dropout(xf, p, seed, offset)
+    if residual is not None:
+        xf = xf + residual.float()
+    s = _round(xf, x)
+    if rms:
+        var = (s * s).mean(-1, keepdim=True)
+        y = s * torch.rsqrt(var + eps) * gamma.float()
+    else:
+        mean = s.mean(-1, keepdim=True)
+        var = ((s - mean) ** 2).mean(-1, keepdim=True)
+        y = (s - mean) * torch.rsqrt(var + eps) * gamma.float()
+        if beta is not None:
+            y = y + beta.float()
+    return y.to(x.dtype), s.to(x.dtype)
+
+
+def bias_act(z, bias=None, act=ACT_GELU):
+    t = z.float()
+    if bias is not None:
+        t = t + bias.float()
+    if act == ACT_GELU:
+        t = F.gelu(t)
+    elif act == ACT_RELU:
+        t = F.relu(t)
+    return t.to(z.dtype)
+
+
+def embedding3(ids, tt, W, P=None, T=None):
+    out = W.float()[ids]
+    if P is not None:
+        out = out + P.float()[: ids.shape[1]].unsqueeze(0)
+    if T is not None:
+        out = out + T.float()[tt if tt is not None else torch.zeros_like(ids)]
+    return out.to(W.dtype)
+
+
+def cross_entropy(logits, labels, V=None, ignore_index=-100, label_smoothing=0.0):
+    """Mean CE over valid rows of logits[:, :V] (fp32 math)."""
+    V = V or logits.shape[-1]
+    return F.cross_entropy(logits[:, :V].float(), labels, ignore_index=ignore_index,
+                           label_smoothing=label_smoothing)
+
+
+def _hash_u32(x):
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x = x ^ (x >> 16)
+    return x
+
+
+def attn_dropout_keep(B, H, Sq, Sk, p, seed, offset):
+    """Keep mask [B, H, Sq, Sk] identical to the attention kernels' hash-based stream."""
+    idx = np.arange(B * H * Sq * Sk, dtype=np.uint64).reshape(B, H, Sq, Sk)
+    pair = idx >> np.uint64(1)
+    half = (idx & np.uint64(1)).astype(np.uint64)
+    s_lo = np.uint64(seed & 0xFFFFFFFF)
+    s_hi = np.uint64((seed >> 32) & 0xFFFFFFFF)
+    off = np.uint64(offset & 0xFFFFFFFF)
+    base = _hash_u32((s_lo ^ (s_hi * np.uint64(0x85EBCA6B) & M32) ^ (off * np.uint64(0xC2B2AE35) & M32)) & M32)
+    r = _hash_u32(((pair & M32) ^ base) & M32)
+    r16 = (r >> (half * np.uint64(16))) & np.uint64(0xFFFF)
+    thr = np.uint64(min(65535, int(round(p * 65536.0))))
+    return torch.from_numpy(r16 >= thr)
+
+
+def attention(q, k, v, key_bias=None, p=0.0, seed=0, offset=0, scale=None, causal=False):
+    """q,k,v: [B, H, S, D]; key_bias: additive [B, Sk] (fp32). Returns [B, H, Sq, D]."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    if key_bias is not None:
+        s = s + key_bias.float()[:, None, None, :]
+    if causal:
+        Sq, Sk = s.shape[-2:]
+        m = torch.ones(Sq, Sk, dtype=torch.bool, device=s.device).triu(1)
+        s = s.masked_fill(m, float("-inf"))
+    pr = torch.softmax(s, -1)
+    if p > 0.0:
+        keep = attn_dropout_keep(*s.shape, p, seed, offset).to(s.device)
+        pr = torch.where(keep, pr / (1.0 - p), torch.zeros_like(pr))
+    return torch.matmul(pr, v.float()).to(q.dtype)

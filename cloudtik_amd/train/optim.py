@@ -1,0 +1,418 @@
+"""Fused multi-tensor optimizers over a flat parameter space.
+
+``FlatParamSpace`` re-homes every parameter of a model into ONE contiguous buffer per
+role -- bf16 model weights, fp32 master weights, gradients -- and points each
+``nn.Parameter.data`` / ``.grad`` at a view of it.  Consequences that matter on MI355X:
+
+* the optimizer step is one (LAMB: two) kernel launch(es) for the whole model
+  (csrc/optim.hip) instead of ~400 per-tensor launches;
+* the gradient buffer IS the data-parallel communication buffer: buckets are plain
+  slices, so RCCL all-reduces / reduce-scatters need no pack/unpack copies
+  (cloudtik_amd.parallel.ddp);
+* with ``shard=(rank, world)`` each rank owns 1/world of the flat space (ZeRO-1): the
+  optimizer state is sharded, gradients are reduce-scattered and parameters all-gathered
+  -- the same bytes on the wire as an all-reduce, 1/world of the optimizer HBM traffic.
+
+Reference optimizers reproduced: LAMB (bert_large/training/lamb.py:61-139 -- bf16 params
+with fp32 master copy, no bias correction, trust ratio only where weight_decay != 0),
+Adam/AdamW (transfer-learning Trainer, GraphSAGE), SGD+momentum (ResNet-50 main.py:317,
+DLRM split-SGD).  On CPU the identical math runs in PyTorch.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+SEG = 8192
+ALIGN = 64
+
+
+class FlatParamSpace:
+    def __init__(self, params: Sequence[torch.nn.Parameter], names: Optional[Sequence[str]] = None,
+                 grad_dtype: Optional[torch.dtype] = None, shard: Tuple[int, int] = (0, 1),
+                 align: int = ALIGN, reverse: bool = True):
+        params = [p for p in params if p.requires_grad]
+        assert params, "no trainable parameters"
+        names = list(names) if names is not None else [f"p{i}" for i in range(len(params))]
+        if reverse:  # backward produces late-layer grads first: put them first in the buffer
+            params, names = params[::-1], names[::-1]
+        self.params: List[torch.nn.Parameter] = params
+        self.names = names
+        self.dtype = params[0].dtype
+        self.device = params[0].device
+        for p in params:
+            assert p.dtype == self.dtype and p.device == self.device, "mixed dtype/device params"
+        self.grad_dtype = grad_dtype or self.dtype
+        self.offsets, self.numels = [], []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            self.numels.append(p.numel())
+            off += ((p.numel() + align - 1) // align) * align
+        rank, world = shard
+        self.rank, self.world = rank, world
+        # pad total so every shard is an aligned equal slice
+        unit = align * world
+        self.total = ((off + unit - 1) // unit) * unit
+        self.shard_size = self.total // world
+        self.shard_lo = rank * self.shard_size
+        self.shard_hi = self.shard_lo + self.shard_size
+
+        dev = self.device
+        self.model = torch.zeros(self.total, dtype=self.dtype, device=dev)
+        self.grad = torch.zeros(self.total, dtype=self.grad_dtype, device=dev)
+        with torch.no_grad():
+            for p, o, n in zip(params, self.offsets, self.numels):
+                self.model[o:o + n].copy_(p.data.reshape(-1))
+                p.data = self.model[o:o + n].view_as(p)
+                p.grad = self.grad[o:o + n].view_as(p)
+        # fp32 master copy of THIS rank's shard only
+        self.master = self.model[self.shard_lo:self.shard_hi].float().clone() \
+            if self.dtype != torch.float32 else None
+        self._build_segments()
+
+    # ------------------------------------------------------------------ segments
+    def _build_segments(self):
+        seg_tensor, seg_start, seg_len, first = [], [], [], []
+        lo, hi = self.shard_lo, self.shard_hi
+        for t, (o, n) in enumerate(zip(self.offsets, self.numels)):
+            first.append(len(seg_tensor))
+            padded = ((n + ALIGN - 1) // ALIGN) * ALIGN
+            a, b = max(o, lo), min(o + padded, hi)
+            s = a
+            while s < b:
+                e = min(s + SEG, b)
+                seg_tensor.append(t)
+                seg_start.append(s - lo)      # relative to the shard
+                seg_len.append(e - s)
+                s = e
+        first.append(len(seg_tensor))
+        dev = self.device
+        self.nseg = len(seg_tensor)
+        self.seg_tensor = torch.tensor(seg_tensor or [0], dtype=torch.int32, device=dev)
+        self.seg_start = torch.tensor(seg_start or [0], dtype=torch.int64, device=dev)
+        self.seg_len = torch.tensor(seg_len or [0], dtype=torch.int32, device=dev)
+        self.tensor_first_seg = torch.tensor(first, dtype=torch.int32, device=dev)
+        self._seg_cpu = (seg_tensor, seg_start, seg_len)
+
+    # ------------------------------------------------------------------ views
+    @property
+    def shard_params(self) -> torch.Tensor:
+        """fp32 weights owned by this rank (master copy, or the model buffer if fp32)."""
+        return self.master if self.master is not None else self.model[self.shard_lo:self.shard_hi]
+
+    @property
+    def shard_model(self) -> torch.Tensor:
+        return self.model[self.shard_lo:self.shard_hi]
+
+    @property
+    def shard_grad(self) -> torch.Tensor:
+        return self.grad[self.shard_lo:self.shard_hi]
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def tensor_wd(self, wd_fn: Callable[[str, torch.nn.Parameter], float]) -> torch.Tensor:
+        return torch.tensor([float(wd_fn(n, p)) for n, p in zip(self.names, self.params)],
+                            dtype=torch.float32, device=self.device)
+
+    def sync_master_from_model(self):
+        if self.master is not None:
+            self.master.copy_(self.shard_model.float())
+
+
+def _is_native(t: torch.Tensor) -> bool:
+    if not t.is_cuda:
+        return False
+    from cloudtik_amd import ops
+    ops.require_native()
+    return True
+
+
+class _FlatOptimizer(torch.optim.Optimizer):
+    """Base: keeps torch.optim.Optimizer's param_groups (so LR schedulers work) but steps
+    the whole flat space with one fused kernel."""
+
+    def __init__(self, params, defaults, space: Optional[FlatParamSpace] = None,
+                 no_decay: Optional[Callable[[str], bool]] = None, names=None):
+        if isinstance(params, FlatParamSpace):
+            space, params = params, params.params
+        params = list(params)
+        if params and isinstance(params[0], dict):
+            groups = params
+        else:
+            groups = [{"params": params}]
+        super().__init__(groups, defaults)
+        if space is None:
+            flat = [p for g in self.param_groups for p in g["params"]]
+            space = FlatParamSpace(flat, names=names)
+        self.space = space
+        # per-tensor weight decay from the group each param belongs to
+        gwd = {}
+        for g in self.param_groups:
+            for p in g["params"]:
+                gwd[id(p)] = g.get("weight_decay", 0.0)
+        self._wd = torch.tensor(
+            [0.0 if (no_decay is not None and no_decay(n)) else gwd.get(id(p), defaults.get("weight_decay", 0.0))
+             for n, p in zip(space.names, space.params)], dtype=torch.float32, device=space.device)
+        self.dyn = torch.zeros(4, dtype=torch.float32, device=space.device)
+        self._dyn_host = torch.zeros(4, dtype=torch.float32, pin_memory=space.device.type == "cuda")
+        self.grad_scale = 1.0
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none: bool = False):  # grads live in the flat buffer
+        self.space.zero_grad()
+
+    def _lr(self):
+        lrs = {g["lr"] for g in self.param_groups}
+        if len(lrs) != 1:
+            raise ValueError("fused flat optimizers need one learning rate across groups")
+        return float(next(iter(lrs)))
+
+    def _push_dyn(self, b1=None, b2=None):
+        t = self.step_count
+        bc1 = 1.0 / (1.0 - b1 ** t) if b1 is not None else 1.0
+        bc2 = 1.0 / (1.0 - b2 ** t) if b2 is not None else 1.0
+        self._dyn_host.copy_(torch.tensor([self._lr(), self.grad_scale, bc1, bc2]))
+        self.dyn.copy_(self._dyn_host, non_blocking=True)
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["flat"] = {k: v for k, v in self._flat_state().items()}
+        sd["step_count"] = self.step_count
+        return sd
+
+    def load_state_dict(self, sd):
+        flat = sd.pop("flat", {})
+        self.step_count = sd.pop("step_count", 0)
+        super().load_state_dict(sd)
+        for k, v in flat.items():
+            getattr(self, k).copy_(v)
+
+    def _flat_state(self):
+        return {}
+
+
+class FusedLAMB(_FlatOptimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01,
+                 bias_correction=False, trust_all=False, max_grad_norm=None, space=None,
+                 no_decay=None, names=None):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay),
+                         space, no_decay, names)
+        sp = self.space
+        n = sp.shard_size
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=sp.device)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=sp.device)
+        self.betas, self.eps = betas, eps
+        self.bias_correction, self.trust_all = bias_correction, trust_all
+        self.max_grad_norm = max_grad_norm
+        self.seg_part = torch.zeros(max(1, 2 * sp.nseg), dtype=torch.float32, device=sp.device)
+        self.tensor_part = torch.zeros(2 * len(sp.params), dtype=torch.float32, device=sp.device)
+        self._sumsq = torch.zeros(1, dtype=torch.float32, device=sp.device)
+        self.norm_allreduce: Optional[Callable[[torch.Tensor], None]] = None  # set by ZeRO wrapper
+
+    def _flat_state(self):
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        sp = self.space
+        b1, b2 = self.betas
+        self._push_dyn(b1 if self.bias_correction else None, b2 if self.bias_correction else None)
+        g = sp.shard_grad
+        if _is_native(g):
+            from cloudtik_amd import ops
+            C = ops.require_native()
+            if self.max_grad_norm:
+                self._sumsq.zero_()
+                C.sumsq_into(g, self._sumsq)
+                if self.norm_allreduce is not None:
+                    self.norm_allreduce(self._sumsq)
+                C.clip_coef(self._sumsq, self.dyn, float(self.grad_scale), float(self.max_grad_norm))
+            wm = sp.shard_model if sp.master is not None else None
+            C.lamb_step(g, self.exp_avg, self.exp_avg_sq, sp.shard_params, wm, sp.seg_tensor,
+                        sp.seg_start, sp.seg_len, sp.tensor_first_seg, self._wd, self.dyn, b1, b2,
+                        self.eps, self.bias_correction, self.trust_all, self.seg_part, self.tensor_part, 1)
+            if self.norm_allreduce is not None:
+                self.norm_allreduce(self.tensor_part)
+            C.lamb_step(g, self.exp_avg, self.exp_avg_sq, sp.shard_params, wm, sp.seg_tensor,
+                        sp.seg_start, sp.seg_len, sp.tensor_first_seg, self._wd, self.dyn, b1, b2,
+                        self.eps, self.bias_correction, self.trust_all, self.seg_part, self.tensor_part, 2)
+        else:
+            self._step_torch(g)
+        return loss
+
+    def _step_torch(self, g):
+        sp = self.space
+        b1, b2 = self.betas
+        lr, gs = self._lr(), self.grad_scale
+        t = self.step_count
+        bc1 = 1.0 / (1.0 - b1 ** t) if self.bias_correction else 1.0
+        bc2 = 1.0 / (1.0 - b2 ** t) if self.bias_correction else 1.0
+        gf = g.float() * gs
+        if self.max_grad_norm:
+            nrm = gf.pow(2).sum()
+            if self.norm_allreduce is not None:
+                buf = nrm.reshape(1).clone()
+                self.norm_allreduce(buf)
+                nrm = buf[0]
+            coef = torch.clamp(self.max_grad_norm / (nrm.sqrt() + 1e-6), max=1.0)
+            gf = gf * coef
+        m, v, w = self.exp_avg, self.exp_avg_sq, sp.shard_params
+        m.mul_(b1).add_(gf, alpha=1 - b1)
+        v.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+        wd = self._per_elem(self._wd)
+        u = (m * bc1) / ((v * bc2).sqrt() + self.eps) + wd * w
+        T = len(sp.params)
+        tid = self._per_elem(torch.arange(T, dtype=torch.float32, device=w.device)).long()
+        valid = self._valid_mask()
+        tp = torch.zeros(2 * T, dtype=torch.float32, device=w.device)
+        tp[0::2].index_add_(0, tid[valid], (w * w)[valid])
+        tp[1::2].index_add_(0, tid[valid], (u * u)[valid])
+        if self.norm_allreduce is not None:
+            self.norm_allreduce(tp)
+        wn, un = tp[0::2].sqrt(), tp[1::2].sqrt()
+        ratio = torch.where((wn > 0) & (un > 0), wn / un.clamp_min(1e-30), torch.ones_like(wn))
+        if not self.trust_all:
+            ratio = torch.where(self._wd != 0, ratio, torch.ones_like(ratio))
+        w.sub_(lr * self._per_elem(ratio) * u)
+        if sp.master is not None:
+            sp.shard_model.copy_(w)
+
+    def _per_elem(self, per_tensor: torch.Tensor) -> torch.Tensor:
+        sp = self.space
+        if not hasattr(self, "_elem_tid"):
+            tid = torch.zeros(sp.shard_size, dtype=torch.long)
+            seg_t, seg_s, seg_l = sp._seg_cpu
+            valid = torch.zeros(sp.shard_size, dtype=torch.bool)
+            for t, s, l in zip(seg_t, seg_s, seg_l):
+                tid[s:s + l] = t
+                valid[s:s + l] = True
+            self._elem_tid = tid.to(sp.device)
+            self._elem_valid = valid.to(sp.device)
+        return per_tensor[self._elem_tid]
+
+    def _valid_mask(self):
+        self._per_elem(self._wd)
+        return self._elem_valid
+
+
+class FusedAdam(_FlatOptimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 adamw=True, space=None, no_decay=None, names=None):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay),
+                         space, no_decay, names)
+        sp = self.space
+        self.exp_avg = torch.zeros(sp.shard_size, dtype=torch.float32, device=sp.device)
+        self.exp_avg_sq = torch.zeros(sp.shard_size, dtype=torch.float32, device=sp.device)
+        self.betas, self.eps, self.adamw = betas, eps, adamw
+
+    def _flat_state(self):
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        sp = self.space
+        b1, b2 = self.betas
+        self._push_dyn(b1, b2)
+        g = sp.shard_grad
+        if _is_native(g):
+            from cloudtik_amd import ops
+            wm = sp.shard_model if sp.master is not None else None
+            ops.require_native().adam_step(g, self.exp_avg, self.exp_avg_sq, sp.shard_params, wm,
+                                           sp.seg_tensor, sp.seg_start, sp.seg_len, self._wd, self.dyn,
+                                           b1, b2, self.eps, self.adamw)
+        else:
+            t = self.step_count
+            lr, gs = self._lr(), self.grad_scale
+            w = sp.shard_params
+            wd = LAMBHelper.per_elem(self, self._wd)
+            gf = g.float() * gs
+            if not self.adamw:
+                gf = gf + wd * w
+            self.exp_avg.mul_(b1).add_(gf, alpha=1 - b1)
+            self.exp_avg_sq.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+            upd = (self.exp_avg / (1 - b1 ** t)) / ((self.exp_avg_sq / (1 - b2 ** t)).sqrt() + self.eps)
+            if self.adamw:
+                upd = upd + wd * w
+            w.sub_(lr * upd)
+            if sp.master is not None:
+                sp.shard_model.copy_(w)
+        return loss
+
+
+class FusedSGD(_FlatOptimizer):
+    def __init__(self, params, lr=0.1, momentum=0.9, dampening=0.0, weight_decay=0.0,
+                 nesterov=False, space=None, no_decay=None, names=None):
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay),
+                         space, no_decay, names)
+        sp = self.space
+        self.momentum, self.dampening, self.nesterov = momentum, dampening, nesterov
+        self.momentum_buffer = torch.zeros(sp.shard_size, dtype=torch.float32, device=sp.device) \
+            if momentum else None
+
+    def _flat_state(self):
+        return {"momentum_buffer": self.momentum_buffer} if self.momentum_buffer is not None else {}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        sp = self.space
+        self._push_dyn()
+        g = sp.shard_grad
+        first = self.step_count == 1
+        if _is_native(g):
+            from cloudtik_amd import ops
+            wm = sp.shard_model if sp.master is not None else None
+            ops.require_native().sgd_step(g, self.momentum_buffer, sp.shard_params, wm, sp.seg_tensor,
+                                          sp.seg_start, sp.seg_len, self._wd, self.dyn,
+                                          self.momentum, self.dampening, self.nesterov, first)
+        else:
+            w = sp.shard_params
+            wd = LAMBHelper.per_elem(self, self._wd)
+            gf = g.float() * self.grad_scale + wd * w
+            if self.momentum:
+                b = self.momentum_buffer
+                if first:
+                    b.copy_(gf)
+                else:
+                    b.mul_(self.momentum).add_(gf, alpha=1 - self.dampening)
+                gf = gf + self.momentum * b if self.nesterov else b
+            w.sub_(self._lr() * gf)
+            if sp.master is not None:
+                sp.shard_model.copy_(w)
+        return loss
+
+
+class LAMBHelper:
+    per_elem = FusedLAMB._per_elem
+    valid = FusedLAMB._valid_mask
+
+
+def param_groups_for(model: torch.nn.Module, weight_decay: float,
+                     no_decay: Callable[[str], bool]) -> Tuple[list, list]:
+    """Reference grouping (run_pretrain_mlperf.py:491-497): decay vs. no-decay groups."""
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    decay = [p for n, p in named if not no_decay(n)]
+    nodecay = [p for n, p in named if no_decay(n)]
+    return ([{"params": decay, "weight_decay": weight_decay},
+             {"params": nodecay, "weight_decay": 0.0}], [n for n, _ in named])
+
+
+def build_optimizer(name: str, model: torch.nn.Module, lr: float, weight_decay: float = 0.0,
+                    no_decay: Optional[Callable[[str], bool]] = None, shard: Tuple[int, int] = (0, 1),
+                    **kw):
+    named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named], shard=shard)
+    nd = no_decay or (lambda n: False)
+    cls = {"lamb": FusedLAMB, "adam": FusedAdam, "adamw": FusedAdam, "sgd": FusedSGD}[name.lower()]
+    if name.lower() == "adam":
+        kw.setdefault("adamw", False)
+    return cls(space, lr=lr, weight_decay=weight_decay, space=space, no_decay=nd, **kw)

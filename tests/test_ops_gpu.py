@@ -1,0 +1,183 @@
+"""Numerics of every HIP kernel vs a plain-PyTorch fp32 reference of the same op (GPU)."""
+import math
+
+import pytest
+import torch
+
+from cloudtik_amd import ops
+from cloudtik_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("N", [64, 768, 1024, 2048])
+@pytest.mark.parametrize("fused", [False, True])
+def test_layernorm_fwd_bwd(cuda, N, fused):
+    torch.manual_seed(0)
+    M = 333
+    x = torch.randn(M, N, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    res = torch.randn(M, N, device=cuda, dtype=torch.bfloat16, requires_grad=True) if fused else None
+    bias = (torch.randn(N, device=cuda) * 0.1).bfloat16().requires_grad_(fused) if fused else None
+    g = (1 + 0.1 * torch.randn(N, device=cuda)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(N, device=cuda)).bfloat16().requires_grad_()
+    p = 0.1 if fused else 0.0
+    ops.manual_seed(7)
+    y = ops.layer_norm(x, g, b, 1e-12, bias=bias, residual=res, p=p, training=True)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    grads = [t.grad.clone() for t in (x, g, b) + ((res, bias) if fused else ())]
+    # reference with identical dropout stream
+    xs = [t.detach().float().requires_grad_() for t in (x, g, b) + ((res, bias) if fused else ())]
+    ops.manual_seed(7)
+    seed, off = ops._rng.next(x.numel()) if p > 0 else (0, 0)
+    yr, _ = ref.layer_norm(xs[0], xs[1], xs[2], 1e-12, xs[4] if fused else None,
+                           xs[3] if fused else None, p, seed, off)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    for gk, xr in zip(grads, xs):
+        assert _rel(gk, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("act", [ops.ACT_GELU, ops.ACT_RELU])
+def test_bias_act(cuda, act):
+    torch.manual_seed(0)
+    z = torch.randn(257, 4096, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    bias = (0.1 * torch.randn(4096, device=cuda)).bfloat16().requires_grad_()
+    y = ops.bias_act(z, bias, act)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    zr, br = z.detach().float().requires_grad_(), bias.detach().float().requires_grad_()
+    yr = ref.bias_act(zr, br, act)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(z.grad, zr.grad) < 1e-2
+    assert _rel(bias.grad, br.grad) < 1e-2
+
+
+def test_dropout_matches_reference_mask(cuda):
+    x = torch.randn(64, 1024, device=cuda, dtype=torch.bfloat16)
+    ops.manual_seed(3)
+    y = ops.dropout(x, 0.1, True)
+    ops.manual_seed(3)
+    seed, off = ops._rng.next(x.numel())
+    yr = ref.dropout(x.float(), 0.1, seed, off)
+    assert torch.equal((y == 0), (yr == 0))
+    frac = (y == 0).float().mean().item()
+    assert abs(frac - 0.1) < 0.01
+
+
+def test_embedding3(cuda):
+    torch.manual_seed(0)
+    V, P, T, H, B, S = 1000, 128, 2, 256, 4, 64
+    W = torch.randn(V, H, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    Pe = torch.randn(P, H, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    Te = torch.randn(T, H, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    ids = torch.randint(0, V, (B, S), device=cuda)
+    tt = torch.randint(0, T, (B, S), device=cuda)
+    y = ops.embedding3(ids, tt, W, Pe, Te)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    Wr, Pr, Tr = (t.detach().float().requires_grad_() for t in (W, Pe, Te))
+    yr = ref.embedding3(ids, tt, Wr, Pr, Tr)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    for a, b in ((W, Wr), (Pe, Pr), (Te, Tr)):
+        assert _rel(a.grad, b.grad) < 2e-2
+
+
+def test_linear_cross_entropy(cuda):
+    torch.manual_seed(0)
+    R, H, V, Vp = 300, 256, 1000, 1024
+    x = torch.randn(R, H, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    W = (0.05 * torch.randn(Vp, H, device=cuda)).bfloat16().requires_grad_()
+    b = (0.05 * torch.randn(Vp, device=cuda)).bfloat16().requires_grad_()
+    labels = torch.randint(0, V, (R,), device=cuda)
+    labels[::7] = -100
+    loss = ops.cross_entropy_fused(x, W, b, labels, V=V)
+    loss.backward()
+    xr, Wr, br = (t.detach().float().requires_grad_() for t in (x, W, b))
+    lr_ = torch.nn.functional.cross_entropy((xr @ Wr.t() + br)[:, :V], labels, ignore_index=-100)
+    lr_.backward()
+    assert abs(loss.item() - lr_.item()) < 2e-2 * abs(lr_.item())
+    assert _rel(x.grad, xr.grad) < 3e-2
+    assert _rel(W.grad[:V], Wr.grad[:V]) < 3e-2
+    assert W.grad[V:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("S", [128, 64, 200, 512])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_packed(cuda, S, p):
+    torch.manual_seed(0)
+    B, H, D = 2, 4, 64
+    qkv = (torch.randn(B, S, 3 * H * D, device=cuda) * 0.5).bfloat16().requires_grad_()
+    mask = torch.ones(B, S, device=cuda)
+    mask[1, S - S // 4:] = 0
+    kb = (1.0 - mask) * -10000.0
+    ops.manual_seed(11)
+    o = ops.attention_packed(qkv, H, kb, p=p, training=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr = qkv.detach().float().requires_grad_()
+    v5 = qr.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+    ops.manual_seed(11)
+    seed, off = ops._rng.next(B * H * S * S) if p > 0 else (0, 0)
+    orf = ref.attention(v5[0], v5[1], v5[2], kb, p, seed, off).permute(0, 2, 1, 3).reshape(B, S, H * D)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 2e-2
+    assert _rel(qkv.grad, qr.grad) < 3e-2
+
+
+def test_attention_bhsd_causal(cuda):
+    torch.manual_seed(1)
+    B, H, S, D = 2, 3, 96, 64
+    q, k, v = (torch.randn(B, H, S, D, device=cuda).bfloat16().requires_grad_() for _ in range(3))
+    o = ops.attention(q, k, v, causal=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = ref.attention(qr, kr, vr, causal=True)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 2e-2
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        assert _rel(a.grad, b.grad) < 3e-2
+
+
+@pytest.mark.parametrize("name", ["lamb", "adamw", "sgd"])
+def test_fused_optimizers_match_torch_path(cuda, name):
+    from cloudtik_amd.train.optim import FlatParamSpace, FusedLAMB, FusedAdam, FusedSGD
+    torch.manual_seed(0)
+
+    def make(dev):
+        m = torch.nn.Sequential(torch.nn.Linear(64, 96), torch.nn.LayerNorm(96), torch.nn.Linear(96, 8))
+        return m.to(dev).to(torch.bfloat16)
+
+    torch.manual_seed(0)
+    mg = make(cuda)
+    torch.manual_seed(0)
+    mc = make("cpu")
+    outs = []
+    for m in (mg, mc):
+        named = list(m.named_parameters())
+        sp = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+        nd = lambda n: n.endswith("bias")  # noqa: E731
+        if name == "lamb":
+            opt = FusedLAMB(sp, lr=1e-2, weight_decay=0.01, no_decay=nd, space=sp)
+        elif name == "adamw":
+            opt = FusedAdam(sp, lr=1e-2, weight_decay=0.01, no_decay=nd, space=sp)
+        else:
+            opt = FusedSGD(sp, lr=1e-2, momentum=0.9, weight_decay=1e-4, space=sp)
+        dev = next(m.parameters()).device
+        for it in range(3):
+            torch.manual_seed(100 + it)
+            x = torch.randn(16, 64).to(dev).bfloat16()
+            loss = m(x).float().pow(2).mean()
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+        outs.append(sp.shard_params.detach().float().cpu())
+    assert _rel(outs[0], outs[1]) < 2e-2
