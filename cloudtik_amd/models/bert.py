@@ -112,15 +112,15 @@ class BertLayer(nn.Module):
     def forward(self, x, key_bias):
         cfg = self.cfg
         tr = self.training
-        qkv = F.linear(x, self.qkv_weight, self.qkv_bias)
+        qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
         ctx = ops.attention_packed(qkv, cfg.num_attention_heads, key_bias,
                                    p=cfg.attention_probs_dropout_prob, training=tr)
-        a = F.linear(ctx, self.out_weight)
+        a = ops.linear(ctx, self.out_weight)
         x1 = ops.layer_norm(a, self.ln1_weight, self.ln1_bias, cfg.layer_norm_eps,
                             bias=self.out_bias, residual=x, p=cfg.hidden_dropout_prob, training=tr)
-        z = F.linear(x1, self.ffn1_weight)
+        z = ops.linear(x1, self.ffn1_weight)
         h = ops.bias_gelu(z, self.ffn1_bias)
-        f = F.linear(h, self.ffn2_weight)
+        f = ops.linear(h, self.ffn2_weight)
         return ops.layer_norm(f, self.ln2_weight, self.ln2_bias, cfg.layer_norm_eps,
                               bias=self.ffn2_bias, residual=x1, p=cfg.hidden_dropout_prob, training=tr)
 
@@ -185,7 +185,7 @@ class BertForPreTraining(nn.Module):
         else:
             rows = seq.reshape(B * S, H)
             labels = masked_lm_labels.reshape(-1)
-        t = F.linear(rows, self.mlm_dense_weight)
+        t = ops.linear(rows, self.mlm_dense_weight)
         t = ops.bias_gelu(t, self.mlm_dense_bias)
         t = ops.layer_norm(t, self.mlm_ln_weight, self.mlm_ln_bias, cfg.layer_norm_eps)
         return ops.cross_entropy_fused(t, self.bert.word_embeddings, self.mlm_decoder_bias, labels,

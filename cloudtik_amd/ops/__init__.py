@@ -84,7 +84,8 @@ def set_rng_state(state):
 
 
 from .functional import (  # noqa: E402,F401
-    layer_norm, bias_act, bias_gelu, dropout, embedding3, cross_entropy_fused,
+    layer_norm, bias_act, bias_gelu, dropout, embedding3, cross_entropy_fused, batch_norm_act,
     ACT_NONE, ACT_GELU, ACT_RELU,
 )
 from .attention import attention, attention_packed  # noqa: E402,F401
+from .linear import linear  # noqa: E402,F401

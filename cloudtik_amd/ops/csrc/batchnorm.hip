@@ -65,25 +65,39 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
 }
 
 // Chan-merge of block partials; writes save_mean/save_invstd, affine (a, b) and updates
-// running statistics.
-__global__ void bn_finalize_kernel(const float* __restrict__ pmean, const float* __restrict__ pm2,
-                                   int nblk, BnLayout L, const bf16_t* __restrict__ gamma,
-                                   const bf16_t* __restrict__ beta, float eps, float momentum,
-                                   float* __restrict__ run_mean, float* __restrict__ run_var,
-                                   float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                   float* __restrict__ coef_a, float* __restrict__ coef_b) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= L.C) return;
+// running statistics.  Block = 64 channels x 16 partial-lanes; each lane Chan-merges a
+// strided subset of the block partials, then the 16 lane results merge through LDS.
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(
+    const float* __restrict__ pmean, const float* __restrict__ pm2, int nblk, BnLayout L,
+    const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta, float eps, float momentum,
+    float* __restrict__ run_mean, float* __restrict__ run_var, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ coef_a, float* __restrict__ coef_b) {
+  __shared__ float sn[16][64], sm[16][64], sq[16][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    const int r0 = b * L.rows_per_blk;
-    const float nb = (float)max(0, min(L.M, r0 + L.rows_per_blk) - r0);
+  if (c < L.C) {
+    for (int b = pl; b < nblk; b += 16) {
+      const int r0 = b * L.rows_per_blk;
+      const float nb = (float)max(0, min(L.M, r0 + L.rows_per_blk) - r0);
+      if (nb <= 0.f) continue;
+      const float mb = pmean[(size_t)b * L.C + c], qb = pm2[(size_t)b * L.C + c];
+      const float nn = n + nb;
+      const float d = mb - mean;
+      mean += d * nb / nn;
+      m2 += qb + d * d * n * nb / nn;
+      n = nn;
+    }
+  }
+  sn[pl][cl] = n; sm[pl][cl] = mean; sq[pl][cl] = m2;
+  __syncthreads();
+  if (pl != 0 || c >= L.C) return;
+  for (int k = 1; k < 16; ++k) {
+    const float nb = sn[k][cl];
     if (nb <= 0.f) continue;
-    const float mb = pmean[(size_t)b * L.C + c], qb = pm2[(size_t)b * L.C + c];
-    const float nn = n + nb;
-    const float d = mb - mean;
+    const float nn = n + nb, d = sm[k][cl] - mean;
     mean += d * nb / nn;
-    m2 += qb + d * d * n * nb / nn;
+    m2 += sq[k][cl] + d * d * n * nb / nn;
     n = nn;
   }
   const float var = n > 0.f ? m2 / n : 0.f;
@@ -176,18 +190,23 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   }
 }
 
-// dgamma, dbeta and dx = a*dy' + c1*x + c0 coefficients
+// dgamma, dbeta and dx = a*dy' + c1*x + c0 coefficients (64 channels x 16 lanes per block)
 template <typename PT>
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ p1, const float* __restrict__ p2,
-                                       int nblk, int M, int C, const bf16_t* __restrict__ gamma,
-                                       const float* __restrict__ mean,
-                                       const float* __restrict__ invstd, PT* __restrict__ dgamma,
-                                       PT* __restrict__ dbeta, float* __restrict__ ca,
-                                       float* __restrict__ c1, float* __restrict__ c0) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
+    const float* __restrict__ p1, const float* __restrict__ p2, int nblk, int M, int C,
+    const bf16_t* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ invstd, PT* __restrict__ dgamma, PT* __restrict__ dbeta,
+    float* __restrict__ ca, float* __restrict__ c1, float* __restrict__ c0) {
+  __shared__ float s1[16][64], s2[16][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float sdy = 0.f, sdx = 0.f;
-  for (int b = 0; b < nblk; ++b) { sdy += p1[(size_t)b * C + c]; sdx += p2[(size_t)b * C + c]; }
+  if (c < C)
+    for (int b = pl; b < nblk; b += 16) { sdy += p1[(size_t)b * C + c]; sdx += p2[(size_t)b * C + c]; }
+  s1[pl][cl] = sdy; s2[pl][cl] = sdx;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  for (int k = 1; k < 16; ++k) { sdy += s1[k][cl]; sdx += s2[k][cl]; }
   if (dgamma) dgamma[c] = from_f<PT>(sdx);
   if (dbeta) dbeta[c] = from_f<PT>(sdy);
   const float g = gamma ? bf2f(gamma[c]) : 1.f;
@@ -210,12 +229,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
     u16x8 yv = u16x8(1);
     if (relu) yv = reinterpret_cast<const u16x8*>(y)[v];
+    const f32x4* a4 = reinterpret_cast<const f32x4*>(ca) + 2 * cv;
+    const f32x4* k4 = reinterpret_cast<const f32x4*>(c1) + 2 * cv;
+    const f32x4* z4 = reinterpret_cast<const f32x4*>(c0) + 2 * cv;
+    const f32x4 aa[2] = {a4[0], a4[1]}, kk[2] = {k4[0], k4[1]}, zz[2] = {z4[0], z4[1]};
     u16x8 o, od;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = cv * 8 + j;
       const float d = (relu && !(bf2f(yv[j]) > 0.f)) ? 0.f : bf2f(g[j]);
-      o[j] = f2bf(ca[c] * d + c1[c] * bf2f(xv[j]) + c0[c]);
+      o[j] = f2bf(aa[j >> 2][j & 3] * d + kk[j >> 2][j & 3] * bf2f(xv[j]) + zz[j >> 2][j & 3]);
       od[j] = f2bf(d);
     }
     reinterpret_cast<u16x8*>(dx)[v] = o;
@@ -254,10 +276,10 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
                                int M, int C, float eps, float momentum, int relu,
                                hipStream_t stream) {
   if (C % 8 || C / 8 > 256 || M <= 0) return -1;
-  BnLayout L = bn_layout(M, C, 1024);
+  BnLayout L = bn_layout(M, C, 512);
   const int nblk = bn_nblk(L);
   bn_stats_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)1024 * C);
-  bn_finalize_kernel<<<ceil_div(C, 256), 256, 0, stream>>>(part, part + (size_t)1024 * C, nblk, L,
+  bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)1024 * C, nblk, L,
                                                            (const bf16_t*)gamma, (const bf16_t*)beta,
                                                            eps, momentum, run_mean, run_var, stat,
                                                            stat + C, stat + 2 * C, stat + 3 * C);
@@ -283,17 +305,17 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
                          void* dgamma, void* dbeta, int param_fp32, float* part, float* coef, int M,
                          int C, int relu, hipStream_t stream) {
   if (C % 8 || C / 8 > 256 || M <= 0) return -1;
-  BnLayout L = bn_layout(M, C, 1024);
+  BnLayout L = bn_layout(M, C, 512);
   const int nblk = bn_nblk(L);
   bn_bwd_reduce_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
                                                  (const bf16_t*)x, save_mean, save_invstd, L, relu,
                                                  part, part + (size_t)1024 * C);
   if (param_fp32)
-    bn_bwd_finalize_kernel<float><<<ceil_div(C, 256), 256, 0, stream>>>(
+    bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
         part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
         (float*)dgamma, (float*)dbeta, coef, coef + C, coef + 2 * C);
   else
-    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 256), 256, 0, stream>>>(
+    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
         part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
         (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C);
   const long tv = (long)M * (C / 8);

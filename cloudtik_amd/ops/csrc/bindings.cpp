@@ -35,6 +35,11 @@ int ct_sumsq(const void*, int, long, float*, hipStream_t);
 int ct_clip_coef(const float*, float*, float, float, hipStream_t);
 int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, const float*, int, int,
                 float, hipStream_t);
+int ct_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, float*,
+                    float*, int, int, float, float, int, hipStream_t);
+int ct_bn_apply(const void*, const void*, const float*, const float*, void*, int, int, int, hipStream_t);
+int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*,
+              void*, void*, void*, int, float*, float*, int, int, int, hipStream_t);
 int ct_attn_fwd(const void*, const long*, const void*, const long*, const void*, const long*, void*,
                 const long*, const float*, long, float*, int, int, int, int, float, float, uint64_t,
                 uint64_t, int, hipStream_t);
@@ -321,6 +326,70 @@ void attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor
   TORCH_CHECK(rc == 0, "attn_bwd failed rc=", rc);
 }
 
+// ---------------------------------------------------------------- batchnorm (NHWC)
+static void check_nhwc(const at::Tensor& x, const char* name) {
+  CHECK_CUDA(x); CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 4 ? x.is_contiguous(at::MemoryFormat::ChannelsLast) : x.is_contiguous(),
+              name, " must be channels_last (4-D) or contiguous [M, C]");
+}
+static int64_t nhwc_rows(const at::Tensor& x) { return x.numel() / x.size(1); }
+
+// returns (y, save_mean, save_invstd)
+std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma,
+                                     at::Tensor beta, at::Tensor run_mean, at::Tensor run_var,
+                                     double eps, double momentum, bool relu) {
+  check_nhwc(x, "x");
+  const int C = x.size(1);
+  const long M = nhwc_rows(x);
+  if (res.has_value() && res->defined()) { check_nhwc(*res, "residual"); TORCH_CHECK(res->sizes() == x.sizes()); }
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  CHECK_F32(run_mean); CHECK_F32(run_var);
+  auto y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  auto part = at::empty({2 * 1024 * (long)C}, fo);
+  auto stat = at::empty({4 * (long)C}, fo);
+  int rc = ct_bn_fwd_train(x.data_ptr(), optr(res), gamma.data_ptr(), beta.data_ptr(),
+                           run_mean.data_ptr<float>(), run_var.data_ptr<float>(), y.data_ptr(),
+                           part.data_ptr<float>(), stat.data_ptr<float>(), (int)M, C, (float)eps,
+                           (float)momentum, relu ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_fwd_train: unsupported C=", C);
+  return {y, stat.narrow(0, 0, C), stat.narrow(0, C, C)};
+}
+
+at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, at::Tensor b, bool relu) {
+  check_nhwc(x, "x");
+  const int C = x.size(1);
+  CHECK_F32(a); CHECK_F32(b); TORCH_CHECK(a.numel() == C && b.numel() == C);
+  auto y = at::empty_like(x);
+  int rc = ct_bn_apply(x.data_ptr(), optr(res), a.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
+                       (int)nhwc_rows(x), C, relu ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_apply: unsupported C");
+  return y;
+}
+
+// returns (dx, dres, dgamma, dbeta)
+std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor gamma,
+                               at::Tensor save_mean, at::Tensor save_invstd, bool relu, bool need_dres) {
+  check_nhwc(x, "x");
+  at::Tensor dyc = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
+  check_nhwc(dyc, "dy"); check_nhwc(y, "y");
+  const int C = x.size(1);
+  const long M = nhwc_rows(x);
+  auto dx = at::empty_like(x);
+  at::Tensor dres = need_dres ? at::empty_like(x) : at::Tensor();
+  auto dgamma = at::empty_like(gamma), dbeta = at::empty_like(gamma);
+  auto fo = x.options().dtype(at::kFloat);
+  auto part = at::empty({2 * 1024 * (long)C}, fo);
+  auto coef = at::empty({3 * (long)C}, fo);
+  int rc = ct_bn_bwd(dyc.data_ptr(), y.data_ptr(), x.data_ptr(), gamma.data_ptr(),
+                     save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr(),
+                     need_dres ? dres.data_ptr() : nullptr, dgamma.data_ptr(), dbeta.data_ptr(),
+                     gamma.scalar_type() == at::kFloat ? 1 : 0, part.data_ptr<float>(),
+                     coef.data_ptr<float>(), (int)M, C, relu ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_bwd: unsupported C=", C);
+  return {dx, dres, dgamma, dbeta};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "cloudtik_amd CDNA4 (gfx950) op library";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -337,6 +406,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_into", &sumsq_into);
   m.def("clip_coef", &clip_coef);
   m.def("xent_fwd", &xent_fwd);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
 }

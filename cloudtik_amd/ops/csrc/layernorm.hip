@@ -206,16 +206,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
-// out[col] (+)= sum_p part[p, col]
+// out[col] (+)= sum_p part[p, col].  Block = 64 columns x 16 row-lanes (1024 threads):
+// every wave reads 64 consecutive floats of one partial row (coalesced), 16 waves per CU
+// keep enough loads in flight; the 16 lanes per column are merged through LDS.
 template <typename OUT>
-__global__ void colsum_kernel(const float* __restrict__ part, OUT* __restrict__ out, int P, int N,
-                              int accumulate) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part,
+                                                      OUT* __restrict__ out, int P, int N,
+                                                      int accumulate) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
   float t = 0.f;
-  for (int p = 0; p < P; ++p) t += part[(size_t)p * N + col];
-  if (accumulate) t += to_f<OUT>(out[col]);
-  out[col] = from_f<OUT>(t);
+  if (col < N) {
+    int p = rl;
+    for (; p + 48 < P; p += 64) {
+      const float a = part[(size_t)p * N + col], b = part[(size_t)(p + 16) * N + col];
+      const float c = part[(size_t)(p + 32) * N + col], d = part[(size_t)(p + 48) * N + col];
+      t += (a + b) + (c + d);
+    }
+    for (; p < P; p += 16) t += part[(size_t)p * N + col];
+  }
+  red[rl][cl] = t;
+  __syncthreads();
+  if (rl == 0 && col < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][cl];
+    if (accumulate) s += to_f<OUT>(out[col]);
+    out[col] = from_f<OUT>(s);
+  }
 }
 
 }  // namespace ct
@@ -224,9 +243,9 @@ using namespace ct;
 
 extern "C" int ct_colsum(const float* part, void* out, int P, int N, int out_fp32, int accumulate,
                          hipStream_t stream) {
-  const int cb = ceil_div(N, 256);
-  if (out_fp32) colsum_kernel<float><<<cb, 256, 0, stream>>>(part, (float*)out, P, N, accumulate);
-  else colsum_kernel<bf16_t><<<cb, 256, 0, stream>>>(part, (bf16_t*)out, P, N, accumulate);
+  const int cb = ceil_div(N, 64);
+  if (out_fp32) colsum_kernel<float><<<cb, 1024, 0, stream>>>(part, (float*)out, P, N, accumulate);
+  else colsum_kernel<bf16_t><<<cb, 1024, 0, stream>>>(part, (bf16_t*)out, P, N, accumulate);
   return 0;
 }
 

@@ -184,3 +184,54 @@ def cross_entropy_fused(x, W, b, labels, V=None, ignore_index=-100, label_smooth
     return ref.cross_entropy(logits, labels, V, ignore_index, label_smoothing)
 
 
+
+
+# ----------------------------------------------------------------------------- batchnorm
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, run_mean, run_var, relu, momentum, eps):
+        y, mean, invstd = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu)
+        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        ctx.cfg = (relu, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, gamma, mean, invstd = ctx.saved_tensors
+        relu, has_res = ctx.cfg
+        dx, dres, dg, db = _C().bn_bwd(dy, y, x, gamma, mean, invstd, relu, has_res)
+        return dx, dg, db, (dres if has_res else None), None, None, None, None, None
+
+
+def _bn_native_ok(x):
+    if x.dtype != torch.bfloat16 or x.dim() not in (2, 4):
+        return False
+    C = x.shape[1]
+    if C % 8 or C > 2048:
+        return False
+    return x.is_contiguous(memory_format=torch.channels_last) if x.dim() == 4 else x.is_contiguous()
+
+
+def batch_norm_act(x, weight, bias, running_mean, running_var, residual=None, relu=True,
+                   training=True, momentum=0.1, eps=1e-5):
+    """relu(BatchNorm(x) + residual) over NHWC/channels_last bf16 (training: batch stats)."""
+    if _native(x) and _bn_native_ok(x) and training and (
+            residual is None or residual.is_contiguous(memory_format=torch.channels_last)
+            or (x.dim() == 2 and residual.is_contiguous())):
+        return _BNActFn.apply(x, weight, bias, residual, running_mean, running_var, bool(relu),
+                              float(momentum), float(eps))
+    if _native(x) and _bn_native_ok(x) and not training and not torch.is_grad_enabled():
+        a = weight.float() * torch.rsqrt(running_var + eps)
+        b = bias.float() - running_mean * a
+        res = residual.contiguous(memory_format=torch.channels_last) if (residual is not None and x.dim() == 4) else residual
+        return _C().bn_apply(x, res, a.contiguous(), b.contiguous(), bool(relu))
+    if x.dtype != running_mean.dtype:
+        y = torch.nn.functional.batch_norm(x.float(), running_mean, running_var, weight.float(), bias.float(),
+                                           training, momentum, eps).to(x.dtype)
+        if residual is not None:
+            y = y + residual
+        return torch.relu(y) if relu else y
+    y = torch.nn.functional.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y

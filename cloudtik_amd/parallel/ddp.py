@@ -69,6 +69,7 @@ class GradBucketer:
         if self.overlap:
             for p in space.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                p._ct_grad_ready = self._on_grad   # fused-wgrad GEMMs (ops.linear) report here
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
@@ -128,6 +129,9 @@ class GradBucketer:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+        for p in self.space.params:
+            if getattr(p, "_ct_grad_ready", None) == self._on_grad:
+                p._ct_grad_ready = None
 
 
 def broadcast_flat_params(space, src: int = 0, group=None):

@@ -68,6 +68,7 @@ class FlatParamSpace:
                 self.model[o:o + n].copy_(p.data.reshape(-1))
                 p.data = self.model[o:o + n].view_as(p)
                 p.grad = self.grad[o:o + n].view_as(p)
+                p._ct_flat_grad = True   # ops.linear may accumulate dW straight into it
         # fp32 master copy of THIS rank's shard only
         self.master = self.model[self.shard_lo:self.shard_hi].float().clone() \
             if self.dtype != torch.float32 else None

@@ -181,3 +181,55 @@ def test_fused_optimizers_match_torch_path(cuda, name):
             opt.zero_grad()
         outs.append(sp.shard_params.detach().float().cpu())
     assert _rel(outs[0], outs[1]) < 2e-2
+
+
+@pytest.mark.parametrize("C,HW", [(64, 56), (256, 14), (2048, 7)])
+@pytest.mark.parametrize("res", [False, True])
+def test_batchnorm_act(cuda, C, HW, res):
+    torch.manual_seed(0)
+    N = 8
+    x = (torch.randn(N, C, HW, HW, device=cuda) * 2 + 0.5).bfloat16().contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    r = torch.randn(N, C, HW, HW, device=cuda).bfloat16().contiguous(
+        memory_format=torch.channels_last).requires_grad_() if res else None
+    g = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=cuda)).bfloat16().requires_grad_()
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y = ops.batch_norm_act(x, g, b, rm, rv, residual=r, relu=True, training=True)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    ts = [t.detach().float().requires_grad_() for t in ((x, g, b, r) if res else (x, g, b))]
+    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yr = torch.nn.functional.batch_norm(ts[0], rm2, rv2, ts[1], ts[2], True, 0.1, 1e-5)
+    if res:
+        yr = yr + ts[3]
+    yr = torch.relu(yr)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(rm, rm2) < 1e-3 and _rel(rv, rv2) < 1e-3
+    grads = [x.grad, g.grad, b.grad] + ([r.grad] if res else [])
+    for a, t in zip(grads, ts):
+        assert _rel(a, t.grad) < 2e-2
+
+
+def test_linear_fused_wgrad(cuda):
+    from cloudtik_amd.train.optim import FlatParamSpace
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(256, 512, device=cuda, dtype=torch.bfloat16)
+    sp = FlatParamSpace([lin.weight, lin.bias], names=["w", "b"])
+    seen = []
+    lin.weight._ct_grad_ready = lambda p: seen.append(p)
+    x = torch.randn(4, 33, 256, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.linear(x, lin.weight, lin.bias)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, lin.weight, lin.bias))
+    yr = torch.nn.functional.linear(xr, wr, br)
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2
+    assert _rel(lin.weight.grad, wr.grad) < 1e-2
+    assert _rel(lin.bias.grad, br.grad) < 1e-2
+    assert len(seen) == 1
+    # the weight grad must live in the flat buffer
+    assert lin.weight.grad.data_ptr() == sp.grad[sp.offsets[sp.params.index(lin.weight)]:].data_ptr()
