@@ -45,7 +45,34 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--tunableop", default="use", choices=["off", "use", "tune"],
+                    help="hipBLASLt solution selection via PyTorch TunableOp (results shipped in-tree)")
     return ap.parse_args()
+
+
+TUNE_FILE = os.path.join(REPO, "cloudtik_amd", "ops", "tunableop", "gfx950_tunableop.csv")
+
+
+def setup_tunableop(mode, rank):
+    """Library GEMMs: let TunableOp pick the fastest hipBLASLt solution per shape.  The tuned
+    table (gfx950) is committed in-tree; `--tunableop tune` regenerates it."""
+    if mode == "off":
+        return
+    import torch.cuda.tunable as tn
+    if mode == "use" and not os.path.exists(TUNE_FILE):
+        return
+    os.makedirs(os.path.dirname(TUNE_FILE), exist_ok=True)
+    tn.enable(True)
+    tn.set_filename(TUNE_FILE if rank == 0 or mode == "use" else TUNE_FILE + f".rank{rank}")
+    tn.tuning_enable(mode == "tune")
+    if mode == "tune":
+        tn.set_max_tuning_duration(60)
+        tn.set_max_tuning_iterations(30)
+
+
+def finish_tunableop(mode, rank):
+    # TunableOp writes the results file itself when the process exits
+    return None
 
 
 def bench_bert(args, rank, world, device):
@@ -128,6 +155,7 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.backends.cuda.matmul.allow_tf32 = False
+    setup_tunableop(args.tunableop, rank)
     fn = bench_bert if args.model.startswith("bert") else bench_resnet
     step, info = fn(args, rank, world, device)
 
@@ -162,6 +190,7 @@ def main():
                "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16",
                "data": "synthetic (random tokens/images, random-init weights)", "config": cfg}
         print(json.dumps(out), flush=True)
+    finish_tunableop(args.tunableop, rank)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 

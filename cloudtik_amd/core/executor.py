@@ -1,0 +1,448 @@
+"""Command executors: how the control plane runs commands on (and syncs files to) nodes.
+
+Contract: reference ``core/command_executor.py:27-186``.  Implementations:
+
+* ``LocalCommandExecutor``  -- the node is this host (local provider head = CLI host).
+* ``SSHCommandExecutor``    -- ssh with ControlMaster/ControlPersist multiplexing, optional
+                               proxy command, rsync over ssh (ssh_command_executor.py:25-268).
+* ``DockerCommandExecutor`` -- wraps a host executor and runs everything inside the node's
+                               container.  ROCm-first: ``run_init`` starts the container with
+                               ``--device=/dev/kfd --device=/dev/dri --group-add video
+                               --ipc=host`` when the host has AMD GPUs (replacing the
+                               reference's nvidia-container-runtime detection,
+                               docker_command_executor.py:475-497), plus auto shm sizing.
+* ``KubernetesCommandExecutor`` -- ``kubectl exec`` / ``kubectl cp``.
+
+All executors route process creation through an injectable ``process_runner`` (the
+``subprocess`` module by default) so tests can substitute a recording fake runner, as the
+reference test-suite does with MockProcessRunner.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import logging
+import os
+import shlex
+import socket
+import subprocess
+import time
+from typing import Any, Dict, List, Optional
+
+logger = logging.getLogger(__name__)
+
+CHECK_DOCKER_RUNTIME_NUMBER_OF_RETRIES = 5
+SSH_CONTROL_PATH_MAX = 70
+
+
+class CallContext:
+    """Per-invocation output settings (reference core/_private/call_context.py)."""
+
+    def __init__(self, verbosity: int = 0, output_redirected: bool = False, allow_interactive: bool = False):
+        self.verbosity = verbosity
+        self.output_redirected = output_redirected
+        self.allow_interactive = allow_interactive
+
+    def is_output_redirected(self):
+        return self.output_redirected
+
+    def new_call_context(self):
+        return CallContext(self.verbosity, self.output_redirected, self.allow_interactive)
+
+
+class ProcessRunnerError(Exception):
+    def __init__(self, msg, msg_type, code=None, command=None, special_case=None):
+        super().__init__(f"{msg} (type={msg_type}, code={code}, cmd={command})")
+        self.msg_type = msg_type
+        self.code = code
+        self.command = command
+        self.special_case = special_case
+
+
+def with_environment_variables(cmd: str, env: Optional[Dict[str, Any]]) -> str:
+    if not env:
+        return cmd
+    parts = []
+    for k, v in env.items():
+        if not isinstance(v, str):
+            v = json.dumps(v, separators=(",", ":"))
+        parts.append(f"export {k}={shlex.quote(v)};")
+    return " ".join(parts) + " " + cmd
+
+
+def run_cmd_with_runner(process_runner, final_cmd, with_output=False, silent=False, timeout=None,
+                        shell=False):
+    try:
+        if with_output:
+            return process_runner.check_output(final_cmd, shell=shell, timeout=timeout) \
+                if timeout else process_runner.check_output(final_cmd, shell=shell)
+        kw = {}
+        if silent:
+            kw["stdout"] = subprocess.DEVNULL
+            kw["stderr"] = subprocess.DEVNULL
+        if timeout:
+            kw["timeout"] = timeout
+        return process_runner.check_call(final_cmd, shell=shell, **kw)
+    except subprocess.CalledProcessError as e:
+        raise ProcessRunnerError("Command failed", "cmd_failed", code=e.returncode, command=final_cmd)
+
+
+class CommandExecutor:
+    def __init__(self, call_context: CallContext = None):
+        self.call_context = call_context or CallContext()
+
+    def run(self, cmd: str = None, timeout: int = 120, exit_on_fail: bool = False,
+            port_forward=None, with_output: bool = False, environment_variables=None,
+            run_env: str = "auto", ssh_options_override_ssh_key: str = "",
+            shutdown_after_run: bool = False, cmd_to_print: str = None, silent: bool = False):
+        raise NotImplementedError
+
+    def run_with_retry(self, cmd: str = None, timeout: int = 120, exit_on_fail=False,
+                       port_forward=None, with_output=False, environment_variables=None,
+                       run_env="auto", ssh_options_override_ssh_key="",
+                       shutdown_after_run=False, cmd_to_print=None, silent=False,
+                       number_of_retries=30, retry_interval=1):
+        last = None
+        for i in range(max(1, number_of_retries)):
+            try:
+                return self.run(cmd, timeout=timeout, exit_on_fail=exit_on_fail,
+                                port_forward=port_forward, with_output=with_output,
+                                environment_variables=environment_variables, run_env=run_env,
+                                ssh_options_override_ssh_key=ssh_options_override_ssh_key,
+                                shutdown_after_run=shutdown_after_run, cmd_to_print=cmd_to_print,
+                                silent=silent)
+            except Exception as e:  # noqa: BLE001
+                last = e
+                if i + 1 < number_of_retries:
+                    time.sleep(retry_interval)
+        raise last
+
+    def run_rsync_up(self, source: str, target: str, options: Optional[Dict[str, Any]] = None):
+        raise NotImplementedError
+
+    def run_rsync_down(self, source: str, target: str, options: Optional[Dict[str, Any]] = None):
+        raise NotImplementedError
+
+    def remote_shell_command_str(self) -> str:
+        return "true"
+
+    def run_init(self, *, as_head: bool, file_mounts: Dict[str, str], shared_memory_ratio: float,
+                 sync_run_yet: bool) -> Optional[bool]:
+        return None
+
+    def run_terminate(self):
+        return None
+
+    def bootstrap_data_disks(self) -> None:
+        return None
+
+
+# ---------------------------------------------------------------------------------- local
+class LocalCommandExecutor(CommandExecutor):
+    def __init__(self, call_context, log_prefix, auth_config, cluster_name, process_runner,
+                 node_id=None, provider=None, use_internal_ip=True):
+        super().__init__(call_context)
+        self.log_prefix = log_prefix
+        self.process_runner = process_runner
+        self.node_id = node_id
+        self.provider = provider
+
+    def run(self, cmd=None, timeout=120, exit_on_fail=False, port_forward=None, with_output=False,
+            environment_variables=None, run_env="auto", ssh_options_override_ssh_key="",
+            shutdown_after_run=False, cmd_to_print=None, silent=False):
+        if not cmd:
+            return None
+        cmd = with_environment_variables(cmd, environment_variables)
+        final = ["bash", "-c", cmd]
+        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent)
+
+    def run_rsync_up(self, source, target, options=None):
+        target = os.path.expanduser(target)
+        os.makedirs(os.path.dirname(target.rstrip("/")) or ".", exist_ok=True)
+        self._copy(source, target)
+
+    def run_rsync_down(self, source, target, options=None):
+        self._copy(os.path.expanduser(source), target)
+
+    def _copy(self, source, target):
+        if os.path.abspath(source.rstrip("/")) == os.path.abspath(target.rstrip("/")):
+            return
+        if os.path.isdir(source):
+            src = source.rstrip("/") + "/."
+            os.makedirs(target, exist_ok=True)
+            run_cmd_with_runner(self.process_runner, ["cp", "-a", src, target])
+        else:
+            run_cmd_with_runner(self.process_runner, ["cp", "-a", source, target])
+
+    def remote_shell_command_str(self):
+        return "bash"
+
+
+# ---------------------------------------------------------------------------------- ssh
+class SSHOptions:
+    def __init__(self, ssh_key, control_path=None, **kwargs):
+        self.ssh_key = ssh_key
+        self.arg_dict = {
+            "StrictHostKeyChecking": "no",
+            "UserKnownHostsFile": os.devnull,
+            "IdentitiesOnly": "yes",
+            "ExitOnForwardFailure": "yes",
+            "ServerAliveInterval": 5,
+            "ServerAliveCountMax": 3,
+        }
+        if control_path:
+            self.arg_dict.update({"ControlMaster": "auto", "ControlPath": f"{control_path}/%C",
+                                  "ControlPersist": "10s"})
+        self.arg_dict.update(kwargs)
+
+    def to_ssh_options_list(self, *, timeout=60):
+        self.arg_dict["ConnectTimeout"] = f"{timeout}s"
+        opts = ["-i", self.ssh_key] if self.ssh_key else []
+        return opts + [x for y in (["-o", f"{k}={v}"] for k, v in self.arg_dict.items() if v is not None) for x in y]
+
+
+class SSHCommandExecutor(CommandExecutor):
+    def __init__(self, call_context, log_prefix, node_id, provider, auth_config, cluster_name,
+                 process_runner, use_internal_ip):
+        super().__init__(call_context)
+        ssh_control_hash = hashlib.md5(cluster_name.encode()).hexdigest()
+        ssh_user_hash = hashlib.md5(os.environ.get("USER", "user").encode()).hexdigest()
+        self.ssh_control_path = f"/tmp/cloudtik_ssh_{ssh_user_hash[:10]}/{ssh_control_hash[:10]}"
+        self.log_prefix = log_prefix
+        self.node_id = node_id
+        self.provider = provider
+        self.use_internal_ip = use_internal_ip
+        self.ssh_user = auth_config.get("ssh_user", "ubuntu")
+        self.ssh_private_key = auth_config.get("ssh_private_key")
+        self.ssh_proxy_command = auth_config.get("ssh_proxy_command")
+        self.ssh_port = auth_config.get("ssh_port")
+        self.process_runner = process_runner
+        self.ssh_options = SSHOptions(self.ssh_private_key, self.ssh_control_path,
+                                      ProxyCommand=self.ssh_proxy_command)
+        self._ip = None
+
+    def _get_node_ip(self):
+        if self.use_internal_ip:
+            return self.provider.internal_ip(self.node_id)
+        return self.provider.external_ip(self.node_id)
+
+    def _wait_for_ip(self, deadline=60):
+        ip = self._get_node_ip()
+        t0 = time.time()
+        while ip is None and time.time() - t0 < deadline:
+            time.sleep(2)
+            ip = self._get_node_ip()
+        if ip is None:
+            raise RuntimeError(f"node {self.node_id} has no ip")
+        return ip
+
+    def _set_ssh_ip_if_required(self):
+        if self._ip is None:
+            self._ip = self._wait_for_ip()
+            os.makedirs(self.ssh_control_path, mode=0o700, exist_ok=True)
+
+    def _ssh_base(self, timeout=120):
+        port = ["-p", str(self.ssh_port)] if self.ssh_port else []
+        return ["ssh", "-tt" if self.call_context.allow_interactive else "-T"] + port + \
+            self.ssh_options.to_ssh_options_list(timeout=timeout) + [f"{self.ssh_user}@{self._ip}"]
+
+    def run(self, cmd=None, timeout=120, exit_on_fail=False, port_forward=None, with_output=False,
+            environment_variables=None, run_env="auto", ssh_options_override_ssh_key="",
+            shutdown_after_run=False, cmd_to_print=None, silent=False):
+        self._set_ssh_ip_if_required()
+        final = self._ssh_base(timeout)
+        if port_forward:
+            pf = port_forward if isinstance(port_forward, list) else [port_forward]
+            for local, remote in pf:
+                final += ["-L", f"{local}:localhost:{remote}"]
+        if cmd:
+            cmd = with_environment_variables(cmd, environment_variables)
+            if shutdown_after_run:
+                cmd += "; sudo shutdown -h now"
+            final += ["bash", "--login", "-c", "-i", shlex.quote("set -i || true; " + cmd)]
+        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent)
+
+    def _rsync(self, src, dst, options):
+        self._set_ssh_ip_if_required()
+        ssh = " ".join(["ssh"] + self.ssh_options.to_ssh_options_list(timeout=120) +
+                       (["-p", str(self.ssh_port)] if self.ssh_port else []))
+        cmd = ["rsync", "--rsh", ssh, "-avz"]
+        for ex in (options or {}).get("rsync_exclude", []) or []:
+            cmd += ["--exclude", ex]
+        for fl in (options or {}).get("rsync_filter", []) or []:
+            cmd += ["--filter", f"dir-merge,- {fl}"]
+        cmd += [src, dst]
+        run_cmd_with_runner(self.process_runner, cmd)
+
+    def run_rsync_up(self, source, target, options=None):
+        self.run(f"mkdir -p {shlex.quote(os.path.dirname(target.rstrip('/')))}", silent=True)
+        self._rsync(source, f"{self.ssh_user}@{self._ip}:{target}", options)
+
+    def run_rsync_down(self, source, target, options=None):
+        self._rsync(f"{self.ssh_user}@{self._ip}:{source}", target, options)
+
+    def remote_shell_command_str(self):
+        self._set_ssh_ip_if_required()
+        key = f"-i {self.ssh_private_key} " if self.ssh_private_key else ""
+        return f"ssh -o IdentitiesOnly=yes {key}{self.ssh_user}@{self._ip}\n"
+
+    def bootstrap_data_disks(self):
+        """Format and mount unmounted NVMe data disks under /mnt/cloudtik/data_disk_N."""
+        script = (
+            "i=1; for d in $(lsblk -dpno NAME,TYPE,MOUNTPOINT | awk '$2==\"disk\" && $3==\"\" {print $1}'); do "
+            "  if ! lsblk -no MOUNTPOINT $d | grep -q .; then "
+            "    (sudo blkid $d >/dev/null || sudo mkfs -t ext4 -q $d) && "
+            "    sudo mkdir -p /mnt/cloudtik/data_disk_$i && sudo mount -o defaults,noatime $d /mnt/cloudtik/data_disk_$i && "
+            "    sudo chmod a+w /mnt/cloudtik/data_disk_$i; i=$((i+1)); fi; done")
+        self.run(script, silent=True)
+
+
+# ---------------------------------------------------------------------------------- docker
+class DockerCommandExecutor(CommandExecutor):
+    def __init__(self, call_context, host_executor: CommandExecutor, docker_config: Dict[str, Any]):
+        super().__init__(call_context)
+        self.host = host_executor
+        self.docker_config = docker_config or {}
+        self.container_name = self.docker_config.get("container_name", "cloudtik-ai")
+        self.docker_cmd = self.docker_config.get("docker_cmd", "docker")
+        self.initialized = False
+
+    def run(self, cmd=None, timeout=120, exit_on_fail=False, port_forward=None, with_output=False,
+            environment_variables=None, run_env="auto", ssh_options_override_ssh_key="",
+            shutdown_after_run=False, cmd_to_print=None, silent=False):
+        if run_env == "host" or not cmd:
+            return self.host.run(cmd, timeout, exit_on_fail, port_forward, with_output,
+                                 environment_variables, "auto", ssh_options_override_ssh_key,
+                                 shutdown_after_run, cmd_to_print, silent)
+        cmd = with_environment_variables(cmd, environment_variables)
+        inner = f"{self.docker_cmd} exec {'-it' if self.call_context.allow_interactive else ''} " \
+                f"{self.container_name} /bin/bash -c {shlex.quote(cmd)}"
+        return self.host.run(inner, timeout, exit_on_fail, port_forward, with_output, None, "host",
+                             ssh_options_override_ssh_key, shutdown_after_run, cmd_to_print, silent)
+
+    def run_rsync_up(self, source, target, options=None):
+        staging = f"/tmp/cloudtik_docker_staging{target}"
+        self.host.run_rsync_up(source, staging, options)
+        self.host.run(f"{self.docker_cmd} exec {self.container_name} mkdir -p {shlex.quote(os.path.dirname(target.rstrip('/')))} && "
+                      f"{self.docker_cmd} cp {shlex.quote(staging)} {self.container_name}:{shlex.quote(target)}",
+                      run_env="host", silent=True)
+
+    def run_rsync_down(self, source, target, options=None):
+        staging = f"/tmp/cloudtik_docker_staging{source}"
+        self.host.run(f"mkdir -p {shlex.quote(os.path.dirname(staging.rstrip('/')))} && "
+                      f"{self.docker_cmd} cp {self.container_name}:{shlex.quote(source)} {shlex.quote(staging)}",
+                      run_env="host", silent=True)
+        self.host.run_rsync_down(staging, target, options)
+
+    def remote_shell_command_str(self):
+        return self.host.remote_shell_command_str().strip() + f" -tt -- {self.docker_cmd} exec -it {self.container_name} /bin/bash\n"
+
+    def rocm_run_options(self, as_head: bool) -> List[str]:
+        """GPU pass-through flags when the host exposes /dev/kfd (AMD ROCm)."""
+        if self.docker_config.get("disable_automatic_runtime_detection"):
+            return []
+        try:
+            out = self.host.run("ls /dev/kfd /dev/dri 2>/dev/null | head -1", with_output=True, run_env="host")
+            has = bool(out and out.strip())
+        except Exception:  # noqa: BLE001
+            has = False
+        if not has:
+            return []
+        return ["--device=/dev/kfd", "--device=/dev/dri", "--group-add=video",
+                "--cap-add=SYS_PTRACE", "--security-opt=seccomp=unconfined"]
+
+    def shm_run_options(self, shared_memory_ratio: float) -> List[str]:
+        if self.docker_config.get("disable_shm_size_detection") or shared_memory_ratio <= 0:
+            return []
+        try:
+            out = self.host.run("cat /proc/meminfo || true", with_output=True, run_env="host").decode()
+            kb = int([ln for ln in out.split("\n") if "MemAvailable" in ln][0].split()[1])
+            return [f"--shm-size={int(kb * 1024 * shared_memory_ratio * 1.1)}b"]
+        except Exception:  # noqa: BLE001
+            return []
+
+    def run_init(self, *, as_head, file_mounts, shared_memory_ratio, sync_run_yet):
+        image = self.docker_config.get("head_image" if as_head else "worker_image") or self.docker_config.get("image")
+        if not image:
+            return None
+        running = self.host.run(f"{self.docker_cmd} inspect -f '{{{{.State.Running}}}}' {self.container_name} || true",
+                                with_output=True, run_env="host")
+        if running and running.strip() == b"true":
+            self.initialized = True
+            return True
+        opts = list(self.docker_config.get("run_options", [])) + \
+            list(self.docker_config.get("head_run_options" if as_head else "worker_run_options", []))
+        opts += ["--ipc=host", "--net=host", "--cap-add=NET_ADMIN", "--cap-add=SYS_NICE"]
+        opts += self.rocm_run_options(as_head) + self.shm_run_options(shared_memory_ratio)
+        mounts = " ".join(f"-v {shlex.quote(d)}:{shlex.quote(d)}" for d in (file_mounts or {}))
+        cmd = f"{self.docker_cmd} run --rm --name {self.container_name} -d -it {mounts} " \
+              f"{' '.join(opts)} {image} bash"
+        self.host.run(cmd, run_env="host")
+        self.initialized = True
+        return True
+
+    def run_terminate(self):
+        self.host.run(f"{self.docker_cmd} stop {self.container_name} || true", run_env="host", silent=True)
+
+    def bootstrap_data_disks(self):
+        return self.host.bootstrap_data_disks()
+
+
+# ---------------------------------------------------------------------------------- kubernetes
+class KubernetesCommandExecutor(CommandExecutor):
+    def __init__(self, call_context, log_prefix, namespace, node_id, auth_config, process_runner):
+        super().__init__(call_context)
+        self.namespace = namespace
+        self.node_id = node_id
+        self.process_runner = process_runner
+        self.kubectl = ["kubectl"]
+
+    def run(self, cmd=None, timeout=120, exit_on_fail=False, port_forward=None, with_output=False,
+            environment_variables=None, run_env="auto", ssh_options_override_ssh_key="",
+            shutdown_after_run=False, cmd_to_print=None, silent=False):
+        if not cmd:
+            return None
+        cmd = with_environment_variables(cmd, environment_variables)
+        final = self.kubectl + ["exec", "-i", "-n", self.namespace, self.node_id, "--", "bash", "-c", cmd]
+        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent)
+
+    def run_rsync_up(self, source, target, options=None):
+        run_cmd_with_runner(self.process_runner, self.kubectl + ["cp", source, f"{self.namespace}/{self.node_id}:{target}"])
+
+    def run_rsync_down(self, source, target, options=None):
+        run_cmd_with_runner(self.process_runner, self.kubectl + ["cp", f"{self.namespace}/{self.node_id}:{source}", target])
+
+    def remote_shell_command_str(self):
+        return f"kubectl -n {self.namespace} exec -it {self.node_id} -- bash\n"
+
+
+def local_ips() -> List[str]:
+    ips = {"127.0.0.1", "localhost"}
+    try:
+        host = socket.gethostname()
+        ips.add(host)
+        for a in socket.getaddrinfo(host, None):
+            ips.add(a[4][0])
+    except OSError:
+        pass
+    try:
+        out = subprocess.run(["hostname", "-I"], capture_output=True, text=True, timeout=5).stdout
+        ips.update(out.split())
+    except Exception:  # noqa: BLE001
+        pass
+    return sorted(ips)
+
+
+def create_default_command_executor(call_context, log_prefix, node_id, provider, auth_config,
+                                    cluster_name, process_runner, use_internal_ip,
+                                    docker_config=None):
+    ip = provider.internal_ip(node_id) if use_internal_ip else provider.external_ip(node_id)
+    if ip is not None and (ip in local_ips() or provider.provider_config.get("type") == "mock-local"):
+        host = LocalCommandExecutor(call_context, log_prefix, auth_config, cluster_name, process_runner,
+                                    node_id, provider, use_internal_ip)
+    else:
+        host = SSHCommandExecutor(call_context, log_prefix, node_id, provider, auth_config,
+                                  cluster_name, process_runner, use_internal_ip)
+    if docker_config and docker_config.get("enabled") and docker_config.get("image"):
+        return DockerCommandExecutor(call_context, host, docker_config)
+    return host

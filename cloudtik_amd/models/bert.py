@@ -112,6 +112,16 @@ class BertLayer(nn.Module):
     def forward(self, x, key_bias):
         cfg = self.cfg
         tr = self.training
+        from cloudtik_amd.ops import transformer as T
+        if T.blocks_supported(x, cfg.hidden_size, cfg.num_attention_heads):
+            # hand-scheduled blocks: one autograd node each, fused residual/bias/wgrad grads
+            x1 = T.attention_block(x, self.qkv_weight, self.qkv_bias, self.out_weight, self.out_bias,
+                                   self.ln1_weight, self.ln1_bias, key_bias, cfg.num_attention_heads,
+                                   cfg.attention_probs_dropout_prob, cfg.hidden_dropout_prob,
+                                   cfg.layer_norm_eps, tr)
+            return T.ffn_block(x1, self.ffn1_weight, self.ffn1_bias, self.ffn2_weight, self.ffn2_bias,
+                               self.ln2_weight, self.ln2_bias, cfg.hidden_dropout_prob,
+                               cfg.layer_norm_eps, tr)
         qkv = ops.linear(x, self.qkv_weight, self.qkv_bias)
         ctx = ops.attention_packed(qkv, cfg.num_attention_heads, key_bias,
                                    p=cfg.attention_probs_dropout_prob, training=tr)

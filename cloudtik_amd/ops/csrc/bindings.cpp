@@ -123,6 +123,34 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor s, at::Tensor ga
   return {ds, dx, dgamma, dbeta, dbias};
 }
 
+// Same as layernorm_bwd but parameter grads are ACCUMULATED into caller-provided tensors
+// (views of the flat gradient buffer) and the activation grads may go to given outputs.
+// returns (ds, dx); dx is undefined when need_dx is false.
+std::vector<at::Tensor> layernorm_bwd_into(at::Tensor dy, at::Tensor s, at::Tensor gamma,
+                                           at::Tensor mean, at::Tensor rstd, bool rms,
+                                           at::Tensor dgamma, c10::optional<at::Tensor> dbeta,
+                                           c10::optional<at::Tensor> dbias, bool need_dx,
+                                           double p_drop, int64_t seed, int64_t offset) {
+  CHECK_IN(dy); CHECK_BF16(dy); CHECK_IN(s); CHECK_BF16(s); CHECK_IN(gamma); CHECK_IN(dgamma);
+  const int N = s.size(-1);
+  const int M = s.numel() / N;
+  TORCH_CHECK(dy.numel() == s.numel() && dgamma.numel() == N);
+  if (dbeta.has_value() && dbeta->defined()) { CHECK_IN(*dbeta); TORCH_CHECK(dbeta->numel() == N && dbeta->scalar_type() == dgamma.scalar_type()); }
+  if (dbias.has_value() && dbias->defined()) { CHECK_IN(*dbias); TORCH_CHECK(dbias->numel() == N && dbias->scalar_type() == dgamma.scalar_type()); }
+  auto ds = at::empty_like(s);
+  at::Tensor dx = need_dx ? at::empty_like(s) : at::Tensor();
+  const int grid = ct_layernorm_bwd_grid(M);
+  auto part = at::empty({3 * (long)grid * N}, s.options().dtype(at::kFloat));
+  int rc = ct_layernorm_bwd(dy.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+                            rstd.data_ptr<float>(), nullptr, ds.data_ptr(),
+                            need_dx ? dx.data_ptr() : nullptr, part.data_ptr<float>(),
+                            dgamma.data_ptr(), optr_mut(dbeta), optr_mut(dbias), M, N, rms ? 1 : 0,
+                            dgamma.scalar_type() == at::kFloat ? 1 : 0, 1, (float)p_drop,
+                            (uint64_t)seed, (uint64_t)offset, cur_stream());
+  TORCH_CHECK(rc == 0, "layernorm_bwd_into: unsupported shape N=", N);
+  return {ds, dx};
+}
+
 // ---------------------------------------------------------------- bias + activation
 at::Tensor bias_act_fwd(at::Tensor z, c10::optional<at::Tensor> bias, int64_t act) {
   CHECK_IN(z); CHECK_BF16(z);
@@ -149,6 +177,23 @@ std::vector<at::Tensor> bias_act_bwd(at::Tensor dy, at::Tensor z, c10::optional<
                            need_dbias ? dbias.data_ptr() : nullptr, M, N, (int)act, 0, 0, cur_stream());
   TORCH_CHECK(rc == 0, "bias_act_bwd: N % 8 != 0");
   return {dz, dbias};
+}
+
+// dz = dy * act'(z + bias) (skipped when want_dz is false: pure bias-gradient reduction);
+// d(bias) accumulated into `dbias` (a view of the flat gradient buffer).
+at::Tensor bias_act_bwd_into(at::Tensor dy, at::Tensor z, c10::optional<at::Tensor> bias, int64_t act,
+                             at::Tensor dbias, bool want_dz) {
+  CHECK_IN(dy); CHECK_IN(z); CHECK_BF16(z); CHECK_BF16(dy); CHECK_IN(dbias);
+  const int N = z.size(-1);
+  const long M = z.numel() / N;
+  TORCH_CHECK(dbias.numel() == N && dy.numel() == z.numel());
+  at::Tensor dz = want_dz ? at::empty_like(z) : at::Tensor();
+  auto part = at::empty({(long)ct_bias_act_bwd_grid(M) * N}, z.options().dtype(at::kFloat));
+  int rc = ct_bias_act_bwd(dy.data_ptr(), z.data_ptr(), optr(bias), want_dz ? dz.data_ptr() : nullptr,
+                           part.data_ptr<float>(), dbias.data_ptr(), M, N, (int)act,
+                           dbias.scalar_type() == at::kFloat ? 1 : 0, 1, cur_stream());
+  TORCH_CHECK(rc == 0, "bias_act_bwd_into: N % 8 != 0");
+  return dz;
 }
 
 at::Tensor dropout_fwd(at::Tensor x, double p, int64_t seed, int64_t offset) {
@@ -396,6 +441,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("bias_act_bwd_into", &bias_act_bwd_into);
+  m.def("layernorm_bwd_into", &layernorm_bwd_into);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("embed3_fwd", &embed3_fwd);
   m.def("embed3_bwd", &embed3_bwd);

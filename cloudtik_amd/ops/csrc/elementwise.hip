@@ -56,8 +56,8 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(
     if (bias) bv = reinterpret_cast<const u16x8*>(bias)[cv];
     for (int row = blockIdx.x * 4 + rl; row < M; row += gridDim.x * 4) {
       const long idx = (long)row * nvec_row + cv;
-      const u16x8 zv = reinterpret_cast<const u16x8*>(z)[idx];
       const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[idx];
+      const u16x8 zv = act != ACT_NONE ? reinterpret_cast<const u16x8*>(z)[idx] : u16x8(0);
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(
         o[j] = f2bf(d);
         acc[j] += d;
       }
-      reinterpret_cast<u16x8*>(dz)[idx] = o;
+      if (dz) reinterpret_cast<u16x8*>(dz)[idx] = o;
     }
   }
   if (!part) return;

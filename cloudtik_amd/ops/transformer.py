@@ -1,0 +1,185 @@
+"""Hand-scheduled post-LN transformer encoder blocks (forward + backward).
+
+Each block is ONE autograd node with a hand-written backward, so that
+
+* the residual branch's gradient is added inside a GEMM epilogue
+  (``dx = addmm(d_residual, d_qkv, W_qkv)``: hipBLASLt beta=1) instead of by the autograd
+  engine's separate elementwise add (2 x [tokens, hidden] per layer);
+* weight gradients are accumulated by the wgrad GEMMs straight into the flat gradient
+  buffer (``grad.addmm_``) and every LayerNorm / bias gradient is accumulated by the
+  LayerNorm / bias-GELU backward kernels into the same buffer -- no AccumulateGrad kernels;
+* the data-parallel bucketer is told the moment a parameter's gradient has been issued
+  (``param._ct_grad_ready``), so RCCL all-reduces overlap the rest of backward.
+
+Block structure (BERT / HF BertLayer, reference run_pretrain_mlperf.py:449-471):
+
+  attention block:  x -> qkv = x Wqkv^T + b -> MFMA flash attention -> a = ctx Wo^T
+                      -> x1 = LN(x + dropout(a + bo))
+  FFN block:        x1 -> z = x1 W1^T -> h = gelu(z + b1) -> f = h W2^T
+                      -> x2 = LN(x1 + dropout(f + b2))
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def _C():
+    from cloudtik_amd import ops
+    return ops.require_native()
+
+
+def _flat(p) -> bool:
+    return p.grad is not None and getattr(p, "_ct_flat_grad", False)
+
+
+def _ready(*params):
+    for p in params:
+        cb = getattr(p, "_ct_grad_ready", None)
+        if cb is not None:
+            cb(p)
+
+
+def _wgrad(p, dy2, x2):
+    """dW = dy2^T x2, accumulated into the flat buffer when possible."""
+    if _flat(p):
+        p.grad.addmm_(dy2.t(), x2)
+        _ready(p)
+        return None
+    return dy2.t() @ x2
+
+
+def _vec_grad_out(p):
+    """(target tensor for an accumulating kernel, whether it is the flat grad)."""
+    if _flat(p):
+        return p.grad, True
+    return torch.zeros_like(p), False
+
+
+class _AttnBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, Wqkv, bqkv, Wo, bo, g1, b1, key_bias, nh, p_attn, p_hid, eps,
+                seed_a, off_a, seed_h, off_h):
+        C = _C()
+        B, S, H = x.shape
+        D = H // nh
+        x2 = x.reshape(B * S, H)
+        qkv = torch.addmm(bqkv, x2, Wqkv.t())
+        v5 = qkv.view(B, S, 3, nh, D)
+        o = torch.empty(B, S, nh, D, dtype=x.dtype, device=x.device)
+        scale = 1.0 / math.sqrt(D)
+        lse = C.attn_fwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, key_bias, scale, p_attn,
+                         seed_a, off_a, False)
+        a = torch.mm(o.view(B * S, H), Wo.t())
+        y, s, mean, rstd = C.layernorm_fwd(a, bo, x2, g1, b1, eps, False, p_hid, seed_h, off_h)
+        ctx.save_for_backward(x2, qkv, o, lse, s, mean, rstd,
+                              key_bias if key_bias is not None else torch.empty(0))
+        ctx.params = (Wqkv, bqkv, Wo, bo, g1, b1)
+        ctx.cfg = (B, S, H, nh, D, scale, p_attn, p_hid, seed_a, off_a, seed_h, off_h,
+                   key_bias is not None)
+        return y.view(B, S, H)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x2, qkv, o, lse, s, mean, rstd, kb = ctx.saved_tensors
+        Wqkv, bqkv, Wo, bo, g1, b1 = ctx.params
+        B, S, H, nh, D, scale, p_attn, p_hid, seed_a, off_a, seed_h, off_h, has_kb = ctx.cfg
+        dy2 = dy.reshape(B * S, H).contiguous()
+        dg1, fg1 = _vec_grad_out(g1)
+        db1, fb1 = _vec_grad_out(b1)
+        dbo, fbo = _vec_grad_out(bo)
+        need_dx = p_hid > 0.0
+        ds, da = C.layernorm_bwd_into(dy2, s, g1, mean, rstd, False, dg1, db1, dbo, need_dx,
+                                      p_hid, seed_h, off_h)
+        if not need_dx:
+            da = ds
+        _ready(*[p for p, f in ((g1, fg1), (b1, fb1), (bo, fbo)) if f])
+        o2 = o.view(B * S, H)
+        dWo = _wgrad(Wo, da, o2)
+        do = torch.mm(da, Wo).view(B, S, nh, D)
+        dqkv = torch.empty_like(qkv)
+        v5 = qkv.view(B, S, 3, nh, D)
+        d5 = dqkv.view(B, S, 3, nh, D)
+        C.attn_bwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, do, d5[:, :, 0], d5[:, :, 1], d5[:, :, 2],
+                   kb if has_kb else None, lse, scale, p_attn, seed_a, off_a, False)
+        dbq, fbq = _vec_grad_out(bqkv)
+        C.bias_act_bwd_into(dqkv, dqkv, None, 0, dbq, False)   # column sum of dqkv
+        if fbq:
+            _ready(bqkv)
+        dWqkv = _wgrad(Wqkv, dqkv, x2)
+        dx = torch.addmm(ds, dqkv, Wqkv)                         # residual grad fused (beta=1)
+        return (dx.view(B, S, H), dWqkv, None if fbq else dbq, dWo, None if fbo else dbo,
+                None if fg1 else dg1, None if fb1 else db1, None, None, None, None, None,
+                None, None, None, None)
+
+
+class _FFNBlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x1, W1, b1f, W2, b2f, g2, b2, p_hid, eps, seed_h, off_h):
+        C = _C()
+        B, S, H = x1.shape
+        x2 = x1.reshape(B * S, H)
+        z = torch.mm(x2, W1.t())
+        h = C.bias_act_fwd(z, b1f, 1)
+        f = torch.mm(h, W2.t())
+        y, s, mean, rstd = C.layernorm_fwd(f, b2f, x2, g2, b2, eps, False, p_hid, seed_h, off_h)
+        ctx.save_for_backward(x2, z, h, s, mean, rstd)
+        ctx.params = (W1, b1f, W2, b2f, g2, b2)
+        ctx.cfg = (B, S, H, p_hid, seed_h, off_h)
+        return y.view(B, S, H)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x2, z, h, s, mean, rstd = ctx.saved_tensors
+        W1, b1f, W2, b2f, g2, b2 = ctx.params
+        B, S, H, p_hid, seed_h, off_h = ctx.cfg
+        dy2 = dy.reshape(B * S, H).contiguous()
+        dg2, fg2 = _vec_grad_out(g2)
+        db2, fb2 = _vec_grad_out(b2)
+        db2f, fb2f = _vec_grad_out(b2f)
+        need_dx = p_hid > 0.0
+        ds, df = C.layernorm_bwd_into(dy2, s, g2, mean, rstd, False, dg2, db2, db2f, need_dx,
+                                      p_hid, seed_h, off_h)
+        if not need_dx:
+            df = ds
+        _ready(*[p for p, f in ((g2, fg2), (b2, fb2), (b2f, fb2f)) if f])
+        dW2 = _wgrad(W2, df, h)
+        dh = torch.mm(df, W2)
+        db1f, fb1f = _vec_grad_out(b1f)
+        dz = C.bias_act_bwd_into(dh, z, b1f, 1, db1f, True)
+        if fb1f:
+            _ready(b1f)
+        dW1 = _wgrad(W1, dz, x2)
+        dx = torch.addmm(ds, dz, W1)
+        return (dx.view(B, S, H), dW1, None if fb1f else db1f, dW2, None if fb2f else db2f,
+                None if fg2 else dg2, None if fb2 else db2, None, None, None, None)
+
+
+def attention_block(x, Wqkv, bqkv, Wo, bo, g1, b1, key_bias, num_heads, p_attn, p_hidden, eps,
+                    training=True):
+    from cloudtik_amd import ops
+    B, S, H = x.shape
+    p_attn = float(p_attn) if training else 0.0
+    p_hidden = float(p_hidden) if training else 0.0
+    sa, oa = ops._rng.next(B * num_heads * S * S) if p_attn > 0 else (0, 0)
+    sh, oh = ops._rng.next(x.numel()) if p_hidden > 0 else (0, 0)
+    if key_bias is not None:
+        key_bias = key_bias.float().contiguous()
+    return _AttnBlockFn.apply(x.contiguous(), Wqkv, bqkv, Wo, bo, g1, b1, key_bias, num_heads,
+                              p_attn, p_hidden, float(eps), sa, oa, sh, oh)
+
+
+def ffn_block(x1, W1, b1f, W2, b2f, g2, b2, p_hidden, eps, training=True):
+    from cloudtik_amd import ops
+    p_hidden = float(p_hidden) if training else 0.0
+    sh, oh = ops._rng.next(x1.numel()) if p_hidden > 0 else (0, 0)
+    return _FFNBlockFn.apply(x1.contiguous(), W1, b1f, W2, b2f, g2, b2, p_hidden, float(eps), sh, oh)
+
+
+def blocks_supported(x, H, nh) -> bool:
+    from cloudtik_amd import ops
+    return (x.is_cuda and ops.native_available() and x.dtype == torch.bfloat16 and H // nh == 64
+            and H % 8 == 0 and H <= 2048 and torch.is_grad_enabled() is not None)

@@ -232,4 +232,42 @@ def test_linear_fused_wgrad(cuda):
     assert _rel(lin.bias.grad, br.grad) < 1e-2
     assert len(seen) == 1
     # the weight grad must live in the flat buffer
-    assert lin.weight.grad.data_ptr() == sp.grad[sp.offsets[sp.params.index(lin.weight)]:].data_ptr()
+    idx = [i for i, q in enumerate(sp.params) if q is lin.weight][0]
+    assert lin.weight.grad.data_ptr() == sp.grad[sp.offsets[idx]:].data_ptr()
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_bert_layer_blocks_match_composed(cuda, p):
+    """Hand-scheduled block backward == composed-op autograd (same dropout streams)."""
+    from cloudtik_amd.models.bert import BertConfig, BertLayer
+    from cloudtik_amd.train.optim import FlatParamSpace
+    cfg = BertConfig.tiny(hidden_size=256, num_attention_heads=4, intermediate_size=1024,
+                          hidden_dropout_prob=p, attention_probs_dropout_prob=p)
+    torch.manual_seed(0)
+    lay = BertLayer(cfg, device=cuda, dtype=torch.bfloat16)
+    named = list(lay.named_parameters())
+    sp = FlatParamSpace([q for _, q in named], names=[n for n, _ in named])
+    x = torch.randn(4, 64, 256, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    kb = torch.zeros(4, 64, device=cuda)
+    kb[1, 50:] = -10000.0
+    dy = torch.randn(4, 64, 256, device=cuda, dtype=torch.bfloat16)
+    ops.manual_seed(5)
+    y = lay(x, kb)
+    y.backward(dy)
+    g_blocks = sp.grad.clone().float()
+    gx_blocks = x.grad.clone()
+    # composed path (disable blocks)
+    from cloudtik_amd.ops import transformer as T
+    orig = T.blocks_supported
+    T.blocks_supported = lambda *a, **k: False
+    try:
+        sp.zero_grad()
+        x.grad = None
+        ops.manual_seed(5)
+        y2 = lay(x, kb)
+        y2.backward(dy)
+    finally:
+        T.blocks_supported = orig
+    assert _rel(y, y2) < 1e-2
+    assert _rel(gx_blocks, x.grad) < 2e-2
+    assert _rel(g_blocks, sp.grad.float()) < 2e-2
