@@ -78,9 +78,11 @@ struct AttnFwdArgs {
   uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
 };
 
-template <bool DROP>
+template <bool DROP, bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128];  // [buf][K,V][64][128B]
+  // [buf][K,V][64 rows][128 B] then [buf][64] fp32 log2-domain key bias (-inf past Sk)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + 2 * 64 * 4];
+  float* kbias_lds = reinterpret_cast<float*>(smem + 32768);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qi = blockIdx.x * 128 + w * 32 + r;
@@ -97,6 +99,9 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   const float* kbp = a.kbias ? a.kbias + b * a.kb_sb : nullptr;
   const int srow = tid >> 3, sch = tid & 7;
   u16x8 stK[2], stV[2];
+  float stB = 0.f;
+  // element pair index base of this lane's query row (dropout stream); Sk even
+  const uint32_t rb2 = (uint32_t)((((uint64_t)bh * a.Sq + qi) * (uint64_t)a.Sk) >> 1);
 
   f32x16 O0, O1;
 #pragma unroll
@@ -110,13 +115,18 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
     const bool ok_ = key_ < a.Sk;                                                    \
     stK[i_] = ok_ ? *reinterpret_cast<const u16x8*>(kp + (long)key_ * a.k_ss + sch * 8) : u16x8(0); \
     stV[i_] = ok_ ? *reinterpret_cast<const u16x8*>(vp + (long)key_ * a.v_ss + sch * 8) : u16x8(0); \
+  }                                                                                  \
+  if (tid < 64) {                                                                    \
+    const int kk_ = (kt_) * 64 + tid;                                                \
+    stB = kk_ < a.Sk ? (kbp ? kbp[kk_] * LOG2E : 0.f) : -INFINITY;                   \
   }
 #define FWD_SWRITE(buf_)                                                             \
   _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                 \
     char* kb_ = smem + (buf_) * 16384;                                               \
     *reinterpret_cast<u16x8*>(kb_ + swz(srow + 32 * i_, sch)) = stK[i_];             \
     *reinterpret_cast<u16x8*>(kb_ + 8192 + swz(srow + 32 * i_, sch)) = stV[i_];      \
-  }
+  }                                                                                  \
+  if (tid < 64) kbias_lds[(buf_) * 64 + tid] = stB;
 
   FWD_GLOAD(0);
   FWD_SWRITE(0);
@@ -138,45 +148,51 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
       S0 = mfma32(lds_b128(Kb + swz(r, 2 * s + hh)), qf[s], S0);
       S1 = mfma32(lds_b128(Kb + swz(32 + r, 2 * s + hh)), qf[s], S1);
     }
-    // scale, key bias, masking; reg i <-> key kt*64 + t*32 + (i&3) + 8(i>>2) + 4hh
+    // reg i <-> key kt*64 + t*32 + 8(i>>2) + 4hh + (i&3): 4 consecutive keys per group,
+    // so the bias comes in as float4 LDS reads; -inf bias masks keys past Sk
+    const float* kbt = kbias_lds + buf * 64 + 4 * hh;
     float mx = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key0 = kt * 64 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      const int key1 = key0 + 32;
-      float x0 = S0[i] * a.scale_log2, x1 = S1[i] * a.scale_log2;
-      if (kbp) {
-        x0 += (key0 < a.Sk ? kbp[key0] : 0.f) * LOG2E;
-        x1 += (key1 < a.Sk ? kbp[key1] : 0.f) * LOG2E;
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(kbt + 8 * g);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(kbt + 32 + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * g + j;
+        float x0 = fmaf(S0[i], a.scale_log2, b0[j]);
+        float x1 = fmaf(S1[i], a.scale_log2, b1[j]);
+        if (CAUSAL) {
+          const int key0 = kt * 64 + 8 * g + 4 * hh + j;
+          if (key0 > qi) x0 = -INFINITY;
+          if (key0 + 32 > qi) x1 = -INFINITY;
+        }
+        S0[i] = x0; S1[i] = x1;
+        mx = fmaxf(mx, fmaxf(x0, x1));
       }
-      if (key0 >= a.Sk || (a.causal && key0 > qi)) x0 = -INFINITY;
-      if (key1 >= a.Sk || (a.causal && key1 > qi)) x1 = -INFINITY;
-      S0[i] = x0; S1[i] = x1;
-      mx = fmaxf(mx, fmaxf(x0, x1));
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m, mx);
     const float msub = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m - msub);
+    const float alpha = __builtin_amdgcn_exp2f(m - msub);
     m = m_new;
     float ps = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      S0[i] = exp2f(S0[i] - msub);
-      S1[i] = exp2f(S1[i] - msub);
+      S0[i] = __builtin_amdgcn_exp2f(S0[i] - msub);
+      S1[i] = __builtin_amdgcn_exp2f(S1[i] - msub);
       ps += S0[i] + S1[i];
     }
     l = l * alpha + ps;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { O0[i] *= alpha; O1[i] *= alpha; }
     if (DROP) {
+      const uint32_t pbase = rb2 + (uint32_t)(kt * 32 + 2 * hh);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {  // (i&3) in {0,2}: an even key and its odd partner
-          const int key = kt * 64 + t * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const uint64_t idx = ((uint64_t)bh * a.Sq + qi) * a.Sk + key;
-          const uint32_t rr = drop_pair(a.hash_base, idx >> 1);
+          const uint32_t pair = pbase + (uint32_t)(t * 16 + 4 * (i >> 2) + ((i & 3) >> 1));
+          const uint32_t rr = hash_u32(pair ^ a.hash_base);
           const bool k0 = (rr & 0xFFFFu) >= a.thr16, k1 = (rr >> 16) >= a.thr16;
           if (t == 0) { S0[i] = k0 ? S0[i] * a.inv_keep : 0.f; S0[i + 1] = k1 ? S0[i + 1] * a.inv_keep : 0.f; }
           else { S1[i] = k0 ? S1[i] * a.inv_keep : 0.f; S1[i + 1] = k1 ? S1[i + 1] * a.inv_keep : 0.f; }
@@ -259,15 +275,17 @@ struct AttnBwdArgs {
 };
 
 template <bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   // LDS: Q tile 4K | dO tile 4K | K block 16K | dS 8K | dQ pair-reduce 8K | lse, delta
-  __shared__ __attribute__((aligned(16))) char smem[4096 + 4096 + 16384 + 8192 + 8192 + 256];
+  // LDS: Q tile 4K | dO tile 4K | K block 16K | V block 16K | dS^T 8K | dQ pair-reduce 8K | lse, delta
+  __shared__ __attribute__((aligned(16))) char smem[4096 + 4096 + 16384 + 16384 + 8192 + 8192 + 256];
   char* Qs = smem;
   char* dOs = smem + 4096;
   char* Ks = smem + 8192;
-  char* dSs = smem + 24576;
-  float* red = reinterpret_cast<float*>(smem + 32768);
-  float* lse_s = reinterpret_cast<float*>(smem + 40960);
+  char* Vs = smem + 24576;
+  char* dSs = smem + 40960;
+  float* red = reinterpret_cast<float*>(smem + 49152);
+  float* lse_s = reinterpret_cast<float*>(smem + 57344);
   float* delta_s = lse_s + 32;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -279,21 +297,21 @@ __global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
 
   const bf16_t* kp = a.k + b * a.k_sb + h * a.k_sh;
   const bf16_t* vp = a.v + b * a.v_sb + h * a.v_sh;
-  bf16x8_t Kf[4], Vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    Kf[s] = gload_frag(kp + (long)key_l * a.k_ss + 16 * s + 8 * hh, kvalid);
-    Vf[s] = gload_frag(vp + (long)key_l * a.v_ss + 16 * s + 8 * hh, kvalid);
-  }
-  // K block (128 keys) into LDS for the dQ product's transposed reads
+  // K and V blocks (128 keys) into LDS: row reads give the B operands of S = Q K^T and
+  // dP = dO V^T (re-read per q-tile instead of pinning 32 VGPRs), transposed reads of K
+  // give dQ's B operand
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i;
     const int row = c >> 3, ch = c & 7;
     const int key = k0 + row;
-    const u16x8 val = key < a.Sk ? *reinterpret_cast<const u16x8*>(kp + (long)key * a.k_ss + ch * 8) : u16x8(0);
-    *reinterpret_cast<u16x8*>(Ks + swz(row, ch)) = val;
+    const bool ok = key < a.Sk;
+    const u16x8 kv = ok ? *reinterpret_cast<const u16x8*>(kp + (long)key * a.k_ss + ch * 8) : u16x8(0);
+    const u16x8 vv = ok ? *reinterpret_cast<const u16x8*>(vp + (long)key * a.v_ss + ch * 8) : u16x8(0);
+    *reinterpret_cast<u16x8*>(Ks + swz(row, ch)) = kv;
+    *reinterpret_cast<u16x8*>(Vs + swz(row, ch)) = vv;
   }
+  const int krow = w * 32 + r;   // this lane's key row inside the block
   float kb2 = 0.f;
   if (a.kbias && kvalid) kb2 = a.kbias[b * a.kb_sb + key_l] * LOG2E;
   if (!kvalid) kb2 = -INFINITY;
@@ -310,46 +328,85 @@ __global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   const bool single_block = gridDim.x == 1;
   const int dt_q = w & 1, kh = w >> 1;  // this wave's share of the dQ product
 
+  // Q / dO / lse / delta tiles are register-prefetched one q-tile ahead (issued before the
+  // tile's MFMAs, written to LDS after the mid barrier): 2 barriers per q-tile, and the
+  // global-load latency of tile t+1 hides under the compute of tile t.
+  const int prow = tid >> 3, pch = tid & 7;
+  u16x8 pQ, pdO;
+  float pL = INFINITY, pD = 0.f;
+#define BWD_PREFETCH(qb_)                                                                   \
+  {                                                                                         \
+    const int q_ = (qb_) + prow;                                                            \
+    const bool ok_ = q_ < a.Sq;                                                             \
+    pQ = ok_ ? *reinterpret_cast<const u16x8*>(qbase + (long)q_ * a.q_ss + pch * 8) : u16x8(0); \
+    pdO = ok_ ? *reinterpret_cast<const u16x8*>(dobase + (long)q_ * a.do_ss + pch * 8) : u16x8(0); \
+    if (tid < 32) {                                                                         \
+      const bool ok2_ = (qb_) + tid < a.Sq;                                                 \
+      pL = ok2_ ? a.lse[(long)bh * a.Sq + (qb_) + tid] : INFINITY;                          \
+      pD = ok2_ ? a.delta[(long)bh * a.Sq + (qb_) + tid] : 0.f;                             \
+    }                                                                                       \
+  }
+#define BWD_STAGE()                                                                         \
+  {                                                                                         \
+    *reinterpret_cast<u16x8*>(Qs + swz(prow, pch)) = pQ;                                    \
+    *reinterpret_cast<u16x8*>(dOs + swz(prow, pch)) = pdO;                                  \
+    if (tid < 32) { lse_s[tid] = pL; delta_s[tid] = pD; }                                   \
+  }
+  BWD_PREFETCH(0);
+  BWD_STAGE();
+  __syncthreads();
+
   for (int qt = 0; qt < nq; ++qt) {
     const int qb = qt * 32;
-    {
-      const int row = tid >> 3, ch = tid & 7, q = qb + row;
-      const bool ok = q < a.Sq;
-      *reinterpret_cast<u16x8*>(Qs + swz(row, ch)) = ok ? *reinterpret_cast<const u16x8*>(qbase + (long)q * a.q_ss + ch * 8) : u16x8(0);
-      *reinterpret_cast<u16x8*>(dOs + swz(row, ch)) = ok ? *reinterpret_cast<const u16x8*>(dobase + (long)q * a.do_ss + ch * 8) : u16x8(0);
-      if (tid < 32) {
-        const bool ok2 = qb + tid < a.Sq;
-        lse_s[tid] = ok2 ? a.lse[(long)bh * a.Sq + qb + tid] : INFINITY;
-        delta_s[tid] = ok2 ? a.delta[(long)bh * a.Sq + qb + tid] : 0.f;
-      }
-    }
-    __syncthreads();
+    if (qt + 1 < nq) BWD_PREFETCH(qb + 32);
     f32x16 S, dP;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { S[i] = 0.f; dP[i] = 0.f; }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      S = mfma32(lds_b128(Qs + swz(r, 2 * s + hh)), Kf[s], S);
-      dP = mfma32(lds_b128(dOs + swz(r, 2 * s + hh)), Vf[s], dP);
+      S = mfma32(lds_b128(Qs + swz(r, 2 * s + hh)), lds_b128(Ks + swz(krow, 2 * s + hh)), S);
+      dP = mfma32(lds_b128(dOs + swz(r, 2 * s + hh)), lds_b128(Vs + swz(krow, 2 * s + hh)), dP);
+    }
+    // dropout keep bits: the pair (even key, odd key) shares one hash; the two lanes of a
+    // pair (lane ^ 1) each hash 8 of the 16 query rows and swap halves with one DPP move
+    // packed into one register: bit i = keep decision of register i
+    uint32_t keepbits = 0xFFFFu;
+    if (DROP) {
+      const uint32_t T0 = (uint32_t)(((uint64_t)bh * a.Sq + qb) * (uint64_t)(a.Sk >> 1));
+      const uint32_t half_sk = (uint32_t)(a.Sk >> 1);
+      const int hsel = r & 1;                // == key_l & 1 (k0, w*32 even)
+      uint32_t mine = 0, theirs = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * hsel + j;
+        const int qrow = (i & 3) + 8 * (i >> 2) + 4 * hh;
+        const uint32_t rr = hash_u32((T0 + (uint32_t)qrow * half_sk + (uint32_t)(key_l >> 1)) ^ a.hash_base);
+        const uint32_t klo = (rr & 0xFFFFu) >= a.thr16, khi = (rr >> 16) >= a.thr16;
+        mine |= (hsel ? khi : klo) << i;
+        theirs |= (hsel ? klo : khi) << i;
+      }
+      keepbits = mine | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)theirs, 0xB1, 0xF, 0xF, false);
     }
     // reg i <-> query row qrow(i) = (i&3) + 8(i>>2) + 4hh of this tile; column = key_l
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qrow = (i & 3) + 8 * (i >> 2) + 4 * hh;
-      float x = S[i] * a.scale_log2 + kb2;
-      if (a.causal && key_l > qb + qrow) x = -INFINITY;
-      const float p = exp2f(x - lse_s[qrow]);
-      float pd = p, dpv = dP[i];
-      if (DROP) {
-        const uint64_t idx = ((uint64_t)bh * a.Sq + qb + qrow) * a.Sk + key_l;
-        const uint32_t rr = drop_pair(a.hash_base, idx >> 1);
-        const uint32_t r16 = (idx & 1) ? (rr >> 16) : (rr & 0xFFFFu);
-        const bool keep = r16 >= a.thr16;
-        pd = keep ? p * a.inv_keep : 0.f;
-        dpv = keep ? dpv * a.inv_keep : 0.f;
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_s + 8 * g + 4 * hh);
+      const f32x4 D4 = *reinterpret_cast<const f32x4*>(delta_s + 8 * g + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * g + j;
+        float x = fmaf(S[i], a.scale_log2, kb2);
+        if (a.causal && key_l > qb + 8 * g + 4 * hh + j) x = -INFINITY;
+        const float p = __builtin_amdgcn_exp2f(x - L4[j]);
+        float pd = p, dpv = dP[i];
+        if (DROP) {
+          const bool keep = (keepbits >> i) & 1u;
+          pd = keep ? p * a.inv_keep : 0.f;
+          dpv = keep ? dpv * a.inv_keep : 0.f;
+        }
+        S[i] = pd;                        // P (after dropout) for dV
+        dP[i] = p * (dpv - D4[j]);        // dS (unscaled) for dK, dQ
       }
-      S[i] = pd;                             // P (after dropout) for dV
-      dP[i] = p * (dpv - delta_s[qrow]);     // dS (unscaled) for dK, dQ
     }
     bf16x8_t pf[2], dsf[2];
 #pragma unroll
@@ -369,23 +426,33 @@ __global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
       dK0 = mfma32(aq0, dsf[s2], dK0);
       dK1 = mfma32(aq1, dsf[s2], dK1);
     }
-    // dS -> LDS [32 q][128 keys] (256-byte rows, chunk ^= row & 15)
+    // dS^T -> LDS [128 keys][32 q] (64-byte rows, 8-byte chunks XOR ((key >> 1) & 7)):
+    // each lane owns one key row and 4 runs of 4 consecutive queries -> 4 ds_write_b64
+    {
+      const int key = w * 32 + r;
+      char* rowp = dSs + key * 64;
+      const int sw = (key >> 1) & 7;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-      const int col = w * 32 + r;
-      *reinterpret_cast<bf16_t*>(dSs + row * 256 + ((((col >> 3) ^ (row & 15))) << 4) + ((col & 7) << 1)) = f2bf(dP[i]);
+      for (int g = 0; g < 4; ++g) {
+        const int c = 2 * g + hh;     // 8-byte chunk = queries 8g + 4hh .. +3
+        u16x4 v = {f2bf(dP[4 * g]), f2bf(dP[4 * g + 1]), f2bf(dP[4 * g + 2]), f2bf(dP[4 * g + 3])};
+        *reinterpret_cast<u16x4*>(rowp + ((c ^ sw) << 3)) = v;
+      }
     }
-    __syncthreads();
+    __syncthreads();   // (B1) every wave is done reading Qs / dOs / lse / delta of this tile
+    if (qt + 1 < nq) BWD_STAGE();
     // dQ[q][d] partial = dS[q][kh*64 .. +64] . K[kh*64 .. +64][dt_q*32 .. +32]
+    // A (dS, q on the lane) by transposed reads of dS^T; B (K columns) by transposed reads
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const int qcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;   // 4 queries this lane addresses
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int cc = kh * 8 + 2 * s + hh;
-      const bf16x8_t aa = lds_b128(dSs + r * 256 + ((cc ^ (r & 15)) << 4));
       const int kr = kh * 64 + 16 * s + 8 * hh + trow;
+      const int r0 = kr, r1 = kr + 4;
+      const bf16x8_t aa = cat_tr(lds_tr(dSs + r0 * 64 + ((((qcol >> 2)) ^ ((r0 >> 1) & 7)) << 3)),
+                                 lds_tr(dSs + r1 * 64 + ((((qcol >> 2)) ^ ((r1 >> 1) & 7)) << 3)));
       const bf16x8_t bb = cat_tr(lds_tr(Ks + swz_e(kr, dt_q * 32 + tcol)), lds_tr(Ks + swz_e(kr + 4, dt_q * 32 + tcol)));
       acc = mfma32(aa, bb, acc);
     }
@@ -393,7 +460,7 @@ __global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) red[(dt_q * 16 + i) * 64 + lane] = acc[i];
     }
-    __syncthreads();
+    __syncthreads();   // (B2) red visible; staged tile t+1 visible for the next iteration
     if (kh == 0) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -406,8 +473,11 @@ __global__ __launch_bounds__(256) void attn_bwd_d64_kernel(AttnBwdArgs a) {
         }
       }
     }
-    __syncthreads();
+    // no trailing barrier: the next tile's dS / red writes happen after its (B1), which
+    // every wave reaches only after finishing these reads
   }
+#undef BWD_PREFETCH
+#undef BWD_STAGE
   if (kvalid) {
     bf16_t* dkp = a.dk + b * a.dk_sb + h * a.dk_sh + (long)key_l * a.dk_ss;
     bf16_t* dvp = a.dv + b * a.dv_sb + h * a.dv_sh + (long)key_l * a.dv_ss;
@@ -476,8 +546,11 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
   drop_params(p_drop, seed, offset, &a.thr16, &a.inv_keep, &a.hash_base);
   a.causal = causal;
   dim3 grid((Sq + 127) / 128, B * H);
-  if (p_drop > 0.f) attn_fwd_d64_kernel<true><<<grid, 256, 0, stream>>>(a);
-  else attn_fwd_d64_kernel<false><<<grid, 256, 0, stream>>>(a);
+  const bool drop = p_drop > 0.f;
+  if (drop && causal) attn_fwd_d64_kernel<true, true><<<grid, 256, 0, stream>>>(a);
+  else if (drop) attn_fwd_d64_kernel<true, false><<<grid, 256, 0, stream>>>(a);
+  else if (causal) attn_fwd_d64_kernel<false, true><<<grid, 256, 0, stream>>>(a);
+  else attn_fwd_d64_kernel<false, false><<<grid, 256, 0, stream>>>(a);
   return 0;
 }
 

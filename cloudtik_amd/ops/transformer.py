@@ -109,7 +109,7 @@ class _AttnBlockFn(torch.autograd.Function):
         if fbq:
             _ready(bqkv)
         dWqkv = _wgrad(Wqkv, dqkv, x2)
-        dx = torch.addmm(ds, dqkv, Wqkv)                         # residual grad fused (beta=1)
+        dx = ds.addmm_(dqkv, Wqkv)        # residual grad fused: in-place beta=1 epilogue, no C copy
         return (dx.view(B, S, H), dWqkv, None if fbq else dbq, dWo, None if fbo else dbo,
                 None if fg1 else dg1, None if fb1 else db1, None, None, None, None, None,
                 None, None, None, None)
@@ -153,7 +153,7 @@ class _FFNBlockFn(torch.autograd.Function):
         if fb1f:
             _ready(b1f)
         dW1 = _wgrad(W1, dz, x2)
-        dx = torch.addmm(ds, dz, W1)
+        dx = ds.addmm_(dz, W1)
         return (dx.view(B, S, H), dW1, None if fb1f else db1f, dW2, None if fb2f else db2f,
                 None if fg2 else dg2, None if fb2 else db2, None, None, None, None)
 
