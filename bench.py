@@ -3,7 +3,8 @@
 
 Metric / config from BASELINE.json ("samples/sec ResNet-50 + tokens/sec BERT-large, whole
 node, 1/2/4/8 MI355X").  Default run = BERT-large (24 x 1024, 16 heads, vocab 30522),
-seq 128, 20 masked-LM slots per sequence, LAMB (lr 3.5e-4, wd 0.01, betas 0.9/0.999 --
+seq 128, 76 masked-LM slots per sequence (max_predictions_per_seq of the reference's
+run_ddp_bert_pretrain_phase1.sh:72), per-GPU batch 256, LAMB (lr 3.5e-4, wd 0.01, betas 0.9/0.999 --
 the reference's run_ddp_bert_pretrain_phase1.sh:63 hyper-parameters), bf16 compute with
 fp32 master weights, dropout 0.1, random-init weights, synthetic token data.
 Data-parallel over RCCL with one process per GPU (weak scaling: fixed per-GPU batch).
@@ -41,7 +42,8 @@ def parse():
     ap.add_argument("--model", default="bert-large", choices=["bert-large", "bert-base", "resnet50"])
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default per model)")
     ap.add_argument("--seq", type=int, default=128)
-    ap.add_argument("--max-pred", type=int, default=20)
+    ap.add_argument("--max-pred", type=int, default=76,
+                    help="masked-LM slots per sequence (reference phase-1: max_predictions_per_seq=76)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -98,7 +100,7 @@ def bench_bert(args, rank, world, device):
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=args.bucket_mb)
     opt.grad_scale = ddp.grad_scale
-    B = args.batch or 64
+    B = args.batch or 256
     gen = torch.Generator().manual_seed(42 + rank)
     batch = synthetic_pretraining_batch(cfg, B, args.seq, args.max_pred, device=device, generator=gen)
 

@@ -219,6 +219,43 @@ extern "C" int ct_embed3_bwd(const int64_t* ids, const int64_t* tt, const void* 
   return 0;
 }
 
+// ---------------------------------------------------------------- split-K weight-grad reduce
+// g[i] = bf16( (accumulate ? g[i] : 0) + sum_s P[s*n + i] ) -- the second half of a split-K
+// weight-gradient GEMM (the partials come from one batched hipBLASLt GEMM with fp32 output).
+// One pass: 8 elements per thread, S fp32 float4 pairs + one bf16x8 load/store.
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, int S, long nv,
+                                                            bf16_t* __restrict__ g, int accumulate) {
+  const long n = nv * 8;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nv; v += (long)gridDim.x * blockDim.x) {
+    float acc[8];
+    if (accumulate) {
+      const u16x8 gv = *reinterpret_cast<const u16x8*>(g + v * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = bf2f(gv[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    }
+    for (int s = 0; s < S; ++s) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(P + s * n + v * 8);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(P + s * n + v * 8 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += b[j]; }
+    }
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+    *reinterpret_cast<u16x8*>(g + v * 8) = o;
+  }
+}
+
+extern "C" int ct_splitk_reduce(const float* P, int S, long n, void* g, int accumulate, hipStream_t stream) {
+  if (n % 8) return -1;
+  const long nv = n / 8;
+  splitk_reduce_kernel<<<grid_for(nv), 256, 0, stream>>>(P, S, nv, (bf16_t*)g, accumulate);
+  return 0;
+}
+
 // dtype codes: 0 = fp32, 1 = bf16
 extern "C" int ct_cast(const void* x, int xdt, void* y, int ydt, long n, float scale, int accumulate,
                        hipStream_t stream) {

@@ -11,8 +11,44 @@ then never sees a weight gradient, the data-parallel bucketer is notified explic
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
+
+# split-K for weight-gradient GEMMs: 0 disables, otherwise the maximum split factor
+_SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
+
+
+def splitk_factor(T: int, N: int, K: int) -> int:
+    """Split factor for dW[N,K] = dY[T,N]^T X[T,K].  hipBLASLt's 256x256 macro-tiles give only
+    ceil(N/256)*ceil(K/256) workgroups (16..192 for BERT-large), far fewer than the 256 CUs;
+    splitting the T reduction S ways multiplies the workgroup count (measured on MI355X,
+    bench/gemm_bench.py: 1024x1024 wgrad 0.51 -> 0.81 PF/s at S=8, 3072x1024 0.67 -> 0.89)."""
+    tiles = -(-N // 256) * -(-K // 256)
+    S = 1
+    while tiles * S < 256 and S < _SPLITK_MAX:
+        S *= 2
+    while S > 1 and (T % S or T // S < 2048):
+        S //= 2
+    return S
+
+
+def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    """g += dy2^T x2 (bf16 g, fp32 accumulation).  Split-K as one batched GEMM with fp32
+    partials + one fused reduce-accumulate HIP kernel when the plain GEMM under-fills the
+    GPU; otherwise hipBLASLt's beta=1 epilogue does the accumulation."""
+    T, N = dy2.shape
+    K = x2.shape[1]
+    S = splitk_factor(T, N, K) if (g.is_cuda and g.dtype == torch.bfloat16 and g.is_contiguous()) else 1
+    if S == 1:
+        g.addmm_(dy2.t(), x2)
+        return
+    from cloudtik_amd import ops
+    dy2 = dy2.contiguous()
+    x2 = x2.contiguous()
+    P = torch.bmm(dy2.view(S, T // S, N).transpose(1, 2), x2.view(S, T // S, K), out_dtype=torch.float32)
+    ops.require_native().splitk_reduce(P, g, True)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -35,7 +71,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             g = Wp.grad
             if g is not None and getattr(Wp, "_ct_flat_grad", False) and g.dtype == dy.dtype:
-                g.addmm_(dy2.t(), x2)
+                wgrad_accumulate(g, dy2, x2)
                 cb = getattr(Wp, "_ct_grad_ready", None)
                 if cb is not None:
                     cb(Wp)

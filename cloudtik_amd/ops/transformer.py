@@ -24,6 +24,8 @@ import math
 
 import torch
 
+from cloudtik_amd.ops.linear import wgrad_accumulate
+
 
 def _C():
     from cloudtik_amd import ops
@@ -44,7 +46,7 @@ def _ready(*params):
 def _wgrad(p, dy2, x2):
     """dW = dy2^T x2, accumulated into the flat buffer when possible."""
     if _flat(p):
-        p.grad.addmm_(dy2.t(), x2)
+        wgrad_accumulate(p.grad, dy2, x2)
         _ready(p)
         return None
     return dy2.t() @ x2

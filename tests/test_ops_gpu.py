@@ -236,6 +236,25 @@ def test_linear_fused_wgrad(cuda):
     assert lin.weight.grad.data_ptr() == sp.grad[sp.offsets[idx]:].data_ptr()
 
 
+@pytest.mark.parametrize("N,K", [(1024, 1024), (3072, 1024), (512, 768)])
+def test_wgrad_splitk_accumulate(cuda, N, K):
+    from cloudtik_amd.ops.linear import splitk_factor, wgrad_accumulate
+    T = 16384
+    assert splitk_factor(T, N, K) > 1
+    torch.manual_seed(0)
+    dy = torch.randn(T, N, device=cuda, dtype=torch.bfloat16)
+    x = torch.randn(T, K, device=cuda, dtype=torch.bfloat16)
+    g0 = torch.randn(N, K, device=cuda, dtype=torch.bfloat16)
+    g = g0.clone()
+    wgrad_accumulate(g, dy, x)
+    ref = g0.float() + dy.float().t() @ x.float()
+    assert _rel(g, ref) < 5e-3
+    # the non-split path agrees too
+    g2 = g0.clone()
+    g2.addmm_(dy.t(), x)
+    assert _rel(g2, ref) < 5e-3
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_bert_layer_blocks_match_composed(cuda, p):
     """Hand-scheduled block backward == composed-op autograd (same dropout streams)."""
