@@ -67,6 +67,9 @@ def with_environment_variables(cmd: str, env: Optional[Dict[str, Any]]) -> str:
         if not isinstance(v, str):
             v = json.dumps(v, separators=(",", ":"))
         parts.append(f"export {k}={shlex.quote(v)};")
+    if "CLOUDTIK_BIN_DIR" in env:
+        # same-host nodes run this checkout's `cloudtik` / `cloudtik-run` wrappers
+        parts.append('export PATH="$CLOUDTIK_BIN_DIR:$PATH";')
     return " ".join(parts) + " " + cmd
 
 

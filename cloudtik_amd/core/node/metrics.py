@@ -1,0 +1,106 @@
+"""Node resource metrics for heartbeats and ``cloudtik resource-metrics`` (reference
+core/_private/node/node_monitor.py + resource_spec.py, which sample psutil and NVIDIA GPUs
+through GPUtil).  AMD GPUs are sampled from the amdgpu sysfs files of each card
+(``gpu_busy_percent``, ``mem_info_vram_used/total``, hwmon temperature / power), which
+cost microseconds and need no SMI library; ``amdsmi`` is used when importable for fields
+sysfs lacks.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import time
+from typing import Any, Dict, List, Optional
+
+import psutil
+
+DRM_ROOT = "/sys/class/drm"
+AMD_VENDOR = "0x1002"
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _read_int(path: str) -> Optional[int]:
+    v = _read(path)
+    try:
+        return int(v) if v is not None else None
+    except ValueError:
+        return None
+
+
+def amd_gpu_cards(root: str = DRM_ROOT) -> List[str]:
+    out = []
+    for card in sorted(glob.glob(os.path.join(root, "card[0-9]*")), key=lambda p: int(p.rsplit("card", 1)[1])
+                       if p.rsplit("card", 1)[1].isdigit() else 1 << 30):
+        if not os.path.basename(card)[4:].isdigit():
+            continue
+        if _read(os.path.join(card, "device", "vendor")) == AMD_VENDOR and \
+                os.path.exists(os.path.join(card, "device", "mem_info_vram_total")):
+            out.append(card)
+    return out
+
+
+def gpu_metrics(root: str = DRM_ROOT) -> List[Dict[str, Any]]:
+    gpus = []
+    for i, card in enumerate(amd_gpu_cards(root)):
+        dev = os.path.join(card, "device")
+        g: Dict[str, Any] = {
+            "index": i,
+            "card": os.path.basename(card),
+            "busy_percent": _read_int(os.path.join(dev, "gpu_busy_percent")),
+            "vram_used": _read_int(os.path.join(dev, "mem_info_vram_used")),
+            "vram_total": _read_int(os.path.join(dev, "mem_info_vram_total")),
+            "pci": os.path.basename(os.path.realpath(dev)),
+        }
+        hw = sorted(glob.glob(os.path.join(dev, "hwmon", "hwmon*")))
+        if hw:
+            t = _read_int(os.path.join(hw[0], "temp1_input"))
+            pw = _read_int(os.path.join(hw[0], "power1_average")) or _read_int(os.path.join(hw[0], "power1_input"))
+            g["temperature_c"] = t / 1000.0 if t is not None else None
+            g["power_w"] = pw / 1e6 if pw is not None else None
+        gpus.append(g)
+    return gpus
+
+
+class NodeMetricsCollector:
+    def __init__(self, drm_root: str = DRM_ROOT):
+        self.drm_root = drm_root
+        self._last_net = None
+        psutil.cpu_percent(interval=None)
+
+    def collect(self) -> Dict[str, Any]:
+        vm = psutil.virtual_memory()
+        now = time.time()
+        net = psutil.net_io_counters()
+        rx_rate = tx_rate = 0.0
+        if self._last_net is not None:
+            dt = max(1e-3, now - self._last_net[0])
+            rx_rate = (net.bytes_recv - self._last_net[1]) / dt
+            tx_rate = (net.bytes_sent - self._last_net[2]) / dt
+        self._last_net = (now, net.bytes_recv, net.bytes_sent)
+        try:
+            load = os.getloadavg()
+        except OSError:
+            load = (0.0, 0.0, 0.0)
+        disk = psutil.disk_usage(os.path.expanduser("~"))
+        gpus = gpu_metrics(self.drm_root)
+        return {
+            "time": now,
+            "cpu_count": psutil.cpu_count(),
+            "cpu_percent": psutil.cpu_percent(interval=None),
+            "load_avg": list(load),
+            "memory_total": vm.total,
+            "memory_used": vm.total - vm.available,
+            "disk_total": disk.total,
+            "disk_used": disk.used,
+            "network_rx_bytes_per_s": rx_rate,
+            "network_tx_bytes_per_s": tx_rate,
+            "gpus": gpus,
+            "gpu_busy_percent_avg": (sum(g["busy_percent"] or 0 for g in gpus) / len(gpus)) if gpus else None,
+        }

@@ -179,6 +179,7 @@ class NodeUpdater:
     def exec_commands(self, action: str, commands: List[str], env: Dict[str, Any]):
         for cmd in commands:
             logger.info("%s[%s] %s", self.log_prefix, action, cmd)
+
             try:
                 self.executor.run(cmd, environment_variables=env, timeout=self.command_timeout,
                                   run_env="auto")

@@ -1,0 +1,60 @@
+"""``cloudtik-run``: launch a (distributed) training program, one process per MI355X GPU
+(reference runtime/ai/runner/launch.py:1-330).
+
+    cloudtik-run train.py --epochs 3                       # all local GPUs, 1 rank each
+    cloudtik-run --nproc-per-node 4 train.py               # 4 ranks
+    cloudtik-run --hosts 10.0.0.1,10.0.0.2 train.py        # 2 nodes x all GPUs
+    cloudtik-run --hostfile hosts --launcher mpi train.py
+    cloudtik-run -m package.module args                    # python -m
+    cloudtik-run --no-python ./binary args
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+
+from cloudtik_amd.runner.distributor import Distributor
+from cloudtik_amd.runner.launchers import create_launcher
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="cloudtik-run", description=__doc__,
+                                formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--num-proc", "--num_proc", "-np", type=int, default=0, help="Total number of processes.")
+    p.add_argument("--nnodes", type=int, default=0, help="Number of nodes.")
+    p.add_argument("--nproc-per-node", "--nproc_per_node", type=int, default=0,
+                   help="Processes per node (default: number of visible GPUs).")
+    p.add_argument("--hosts", default="", help="Comma separated hosts, optionally host:slots.")
+    p.add_argument("--hostfile", default="", help="File with one 'host [slots=N]' per line.")
+    p.add_argument("--master-addr", "--master_addr", default="",
+                   help="Rendezvous address (default: the first host, or 127.0.0.1 on one node).")
+    p.add_argument("--master-port", "--master_port", type=int, default=29500)
+    p.add_argument("--launcher", default="", choices=["", "local", "distributed", "rsh", "mpi", "horovod",
+                                                      "horovod-local"])
+    p.add_argument("--rsh", default=None, help="Remote shell for the rsh/distributed launcher.")
+    p.add_argument("--node-rank", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--first-rank", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("--local-world", type=int, default=0, help=argparse.SUPPRESS)
+    p.add_argument("-m", "--module", action="store_true", help="Run the program as 'python -m'.")
+    p.add_argument("--no-python", "--no_python", action="store_true", help="Execute the program directly.")
+    p.add_argument("--log-dir", "--log_dir", default="", help="Write each rank's output to a file here.")
+    p.add_argument("--log-file-prefix", "--log_file_prefix", default="run")
+    p.add_argument("--no-bind-cpus", dest="bind_cpus", action="store_false",
+                   help="Do not pin ranks to their GPU's NUMA-node cores.")
+    p.add_argument("--verbose", action="store_true")
+    p.add_argument("program")
+    p.add_argument("program_args", nargs=argparse.REMAINDER)
+    return p
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    d = Distributor(args.num_proc, args.nnodes, args.nproc_per_node, args.hosts or None, args.hostfile or None)
+    launcher = args.launcher or ("distributed" if d.distributed_with_hosts and d.nnodes > 1 else "local")
+    args.launcher = launcher
+    rc = create_launcher(launcher, args, d).run()
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

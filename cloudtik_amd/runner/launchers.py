@@ -1,0 +1,228 @@
+"""Process launchers behind ``cloudtik-run`` (reference runtime/ai/runner/launcher.py,
+cpu/local_launcher.py, cpu/distributed_launcher.py, rsh/rsh_launcher.py,
+mpi/mpi_launcher.py, horovod/horovod_launcher.py).
+
+* ``local``       -- N ranks on this node, one per GPU: ``RANK / LOCAL_RANK / WORLD_SIZE /
+  LOCAL_WORLD_SIZE / NODE_RANK / MASTER_ADDR / MASTER_PORT`` (the ``torch.distributed``
+  env:// contract), each rank pinned to the cores of its GPU's NUMA node and given
+  ``OMP_NUM_THREADS`` = its core count.  If any rank fails the others are terminated
+  (exactly the process groups this launcher started) and its exit code is returned.
+* ``distributed`` -- multi-node: runs the local launcher on every host (directly on this
+  host, over ssh elsewhere) with its node rank; rank 0's host is the rendezvous master.
+* ``rsh``         -- same as distributed with a configurable remote shell (``--rsh``).
+* ``mpi``         -- ``mpirun -np N -H host:slots,...`` with the rank environment exported.
+* ``horovod``     -- distributed, plus ``HOROVOD_*`` variables for Horovod-style scripts
+  (served by cloudtik_amd.parallel.horovod on RCCL).
+"""
+from __future__ import annotations
+
+import os
+import shlex
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+from typing import Dict, List, Optional
+
+from cloudtik_amd.runner.affinity import rank_cpu_sets
+from cloudtik_amd.runner.distributor import Distributor
+
+
+def _is_local(host: str) -> bool:
+    if host in ("localhost", "127.0.0.1", socket.gethostname()):
+        return True
+    from cloudtik_amd.core.executor import local_ips
+    return host in local_ips()
+
+
+class Launcher:
+    def __init__(self, args, distributor: Distributor):
+        self.args = args
+        self.d = distributor
+
+    def program(self) -> List[str]:
+        a = self.args
+        prog = [a.program] + list(a.program_args)
+        if a.no_python:
+            return prog
+        py = [sys.executable, "-u"]
+        if a.module:
+            return py + ["-m"] + prog
+        return py + prog
+
+    def base_env(self) -> Dict[str, str]:
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env["MASTER_ADDR"] = self.args.master_addr or "127.0.0.1"
+        env["MASTER_PORT"] = str(self.args.master_port)
+        env["WORLD_SIZE"] = str(self.d.num_proc)
+        return env
+
+    def run(self) -> int:
+        raise NotImplementedError
+
+
+class LocalLauncher(Launcher):
+    """Spawns this node's ranks."""
+
+    def __init__(self, args, distributor, node_rank: int = 0, first_rank: int = 0,
+                 local_world: Optional[int] = None):
+        super().__init__(args, distributor)
+        self.node_rank = node_rank
+        self.first_rank = first_rank
+        self.local_world = local_world or min(distributor.nproc_per_node, distributor.num_proc)
+        self.procs: List[subprocess.Popen] = []
+        self._stopping = False
+
+    def rank_env(self, local_rank: int, cpus: Optional[List[int]]) -> Dict[str, str]:
+        env = self.base_env()
+        env.update(RANK=str(self.first_rank + local_rank), LOCAL_RANK=str(local_rank),
+                   LOCAL_WORLD_SIZE=str(self.local_world), NODE_RANK=str(self.node_rank),
+                   GROUP_RANK=str(self.node_rank))
+        if cpus and "OMP_NUM_THREADS" not in os.environ:
+            env["OMP_NUM_THREADS"] = str(max(1, len(cpus)))
+        if self.args.launcher == "horovod":
+            env.update(HOROVOD_RANK=env["RANK"], HOROVOD_SIZE=env["WORLD_SIZE"],
+                       HOROVOD_LOCAL_RANK=str(local_rank), HOROVOD_LOCAL_SIZE=str(self.local_world))
+        return env
+
+    def _terminate_all(self, sig=signal.SIGTERM):
+        self._stopping = True
+        for p in self.procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
+    def run(self) -> int:
+        cpu_sets = rank_cpu_sets(self.local_world) if self.args.bind_cpus else {}
+        prog = self.program()
+        log_dir = self.args.log_dir
+        if log_dir:
+            os.makedirs(log_dir, exist_ok=True)
+        for lr in range(self.local_world):
+            cpus = cpu_sets.get(lr)
+            env = self.rank_env(lr, cpus)
+            out = None
+            if log_dir:
+                rank = self.first_rank + lr
+                out = open(os.path.join(log_dir, f"{self.args.log_file_prefix}_{rank}.log"), "ab")
+
+            def pre(c=cpus):
+                if c:
+                    try:
+                        os.sched_setaffinity(0, c)
+                    except OSError:
+                        pass
+            if self.args.verbose:
+                print(f"[cloudtik-run] rank {env['RANK']} (local {lr}) cpus={cpus}: {' '.join(prog)}",
+                      file=sys.stderr)
+            self.procs.append(subprocess.Popen(prog, env=env, stdout=out, stderr=subprocess.STDOUT if out else None,
+                                               preexec_fn=pre, start_new_session=True))
+        prev = {s: signal.getsignal(s) for s in (signal.SIGINT, signal.SIGTERM)}
+        if threading.current_thread() is threading.main_thread():
+            for s in prev:
+                signal.signal(s, lambda *_: self._terminate_all())
+        rc = 0
+        try:
+            alive = set(range(len(self.procs)))
+            while alive:
+                for i in list(alive):
+                    r = self.procs[i].poll()
+                    if r is None:
+                        continue
+                    alive.discard(i)
+                    if r != 0 and rc == 0:
+                        rc = r
+                        if not self._stopping:
+                            print(f"[cloudtik-run] rank {self.first_rank + i} exited with {r}: stopping the job",
+                                  file=sys.stderr)
+                            self._terminate_all()
+                time.sleep(0.05)
+        finally:
+            if threading.current_thread() is threading.main_thread():
+                for s, h in prev.items():
+                    signal.signal(s, h)
+            self._terminate_all(signal.SIGKILL)
+        return rc if rc >= 0 else 128 - rc
+
+
+class DistributedLauncher(Launcher):
+    """Runs the local launcher on every host of the job."""
+
+    rsh_default = "ssh -o StrictHostKeyChecking=no -o UserKnownHostsFile=/dev/null"
+
+    def remote_command(self, host: str, node_rank: int, local_world: int, first_rank: int) -> str:
+        a = self.args
+        parts = ["cloudtik-run", "--launcher", "local" if a.launcher != "horovod" else "horovod-local",
+                 "--node-rank", str(node_rank), "--first-rank", str(first_rank),
+                 "--local-world", str(local_world), "--num-proc", str(self.d.num_proc),
+                 "--nproc-per-node", str(self.d.nproc_per_node),
+                 "--master-addr", a.master_addr, "--master-port", str(a.master_port)]
+        if a.module:
+            parts.append("-m")
+        if a.no_python:
+            parts.append("--no-python")
+        if a.log_dir:
+            parts += ["--log-dir", a.log_dir, "--log-file-prefix", a.log_file_prefix]
+        if not a.bind_cpus:
+            parts.append("--no-bind-cpus")
+        parts += [a.program] + list(a.program_args)
+        keep = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "CLOUDTIK_",
+                                                                       "TORCH_", "PYTHONPATH", "MIOPEN_"))}
+        exports = " ".join(f"{k}={shlex.quote(v)}" for k, v in keep.items())
+        return f"cd {shlex.quote(os.getcwd())} && env {exports} " + " ".join(shlex.quote(p) for p in parts)
+
+    def run(self) -> int:
+        placements = self.d.host_ranks()
+        if not self.args.master_addr:
+            first = placements[0][0] if placements else "127.0.0.1"
+            self.args.master_addr = "127.0.0.1" if _is_local(first) and len(placements) == 1 else first
+        rsh = shlex.split(getattr(self.args, "rsh", None) or self.rsh_default)
+        threads, codes = [], {}
+
+        def run_host(host, node_rank, n, first):
+            if _is_local(host):
+                codes[host] = LocalLauncher(self.args, self.d, node_rank, first, n).run()
+            else:
+                cmd = rsh + [host, self.remote_command(host, node_rank, n, first)]
+                codes[host] = subprocess.call(cmd)
+
+        for host, node_rank, n, first in placements:
+            t = threading.Thread(target=run_host, args=(host, node_rank, n, first), daemon=True)
+            t.start()
+            threads.append(t)
+        for t in threads:
+            t.join()
+        bad = [c for c in codes.values() if c != 0]
+        return bad[0] if bad else 0
+
+
+class MPILauncher(Launcher):
+    def run(self) -> int:
+        mpirun = shutil.which("mpirun")
+        if mpirun is None:
+            raise RuntimeError("mpirun not found: use --launcher distributed (RCCL does not need MPI)")
+        hosts = ",".join(f"{h}:{n}" for h, _, n, _ in self.d.host_ranks())
+        cmd = [mpirun, "-np", str(self.d.num_proc), "-H", hosts, "--bind-to", "none"]
+        env = self.base_env()
+        for k in ("MASTER_ADDR", "MASTER_PORT", "WORLD_SIZE", "HSA_ENABLE_IPC_MODE_LEGACY"):
+            cmd += ["-x", k]
+        cmd += self.program()
+        return subprocess.call(cmd, env=env)
+
+
+def create_launcher(name: str, args, distributor: Distributor) -> Launcher:
+    if name in ("local", "horovod-local"):
+        if name == "horovod-local":
+            args.launcher = "horovod"
+        return LocalLauncher(args, distributor, args.node_rank, args.first_rank, args.local_world or None)
+    if name in ("distributed", "rsh", "horovod"):
+        return DistributedLauncher(args, distributor)
+    if name == "mpi":
+        return MPILauncher(args, distributor)
+    raise ValueError(f"unknown launcher {name!r}")

@@ -127,12 +127,12 @@ class AIRuntime(RuntimeBase):
 
     # ---------------------------------------------------------------- node-side steps
     def install_steps(self, head):
+        # MI355X nodes are provisioned from a ROCm image: verify the stack, never fetch it
         return [
-            "python -c 'import torch; assert torch.version.hip' 2>/dev/null || "
+            "python3 -c 'import torch; assert torch.version.hip' 2>/dev/null || "
             "echo '[ai] PyTorch-ROCm not found: install torch for ROCm before using the AI runtime' >&2",
-            "python -c 'import mlflow' 2>/dev/null || pip install -q mlflow || true",
-            "python -c 'import cloudtik_amd.ops as o; o.require_native()' 2>/dev/null || "
-            "python -m cloudtik_amd.ops.build || true",
+            "python3 -c 'import mlflow' 2>/dev/null || "
+            "echo '[ai] mlflow not installed: the tracking server will not be started' >&2",
         ]
 
     def configure_steps(self, head):
@@ -142,12 +142,15 @@ class AIRuntime(RuntimeBase):
         if not head:
             return []
         return [
+            "python3 -c 'import mlflow' 2>/dev/null || exit 0; "
             "STORE=${AI_DATABASE_ENGINE:+${AI_DATABASE_ENGINE}://cloudtik@${AI_DATABASE_HOST}/mlflow}; "
             "STORE=${STORE:-sqlite:///$RUNTIME_PATH/mlflow/mlflow.db}; "
             "nohup mlflow server --host 0.0.0.0 --port ${MLFLOW_PORT:-5001} --backend-store-uri $STORE "
             "--default-artifact-root ${HDFS_NAMENODE_URI:-$RUNTIME_PATH/mlflow/artifacts} "
-            "> $RUNTIME_PATH/mlflow/logs/mlflow.log 2>&1 &",
+            "> $RUNTIME_PATH/mlflow/logs/mlflow.log 2>&1 & echo $! > $RUNTIME_PATH/mlflow/mlflow.pid",
         ]
 
     def stop_steps(self, head):
-        return ["pkill -f 'mlflow.server' || true"] if head else []
+        # stop exactly the server this node started (pid file), never by name pattern
+        return ["P=$RUNTIME_PATH/mlflow/mlflow.pid; [ -f $P ] && kill $(cat $P) 2>/dev/null; rm -f $P; true"] \
+            if head else []

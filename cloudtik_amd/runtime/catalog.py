@@ -64,6 +64,19 @@ def _S(name, port, kind=H, **kw):
 
 APACHE = "https://archive.apache.org/dist"
 
+
+def _bg(name: str, cmd: str) -> str:
+    """Start a foreground daemon in the background and record its pid (stopped by _kill)."""
+    return (f"mkdir -p $RUNTIME_PATH/pids $RUNTIME_PATH/{name}/logs; "
+            f"nohup {cmd} > $RUNTIME_PATH/{name}/logs/{name}.out 2>&1 & echo $! > $RUNTIME_PATH/pids/{name}.pid")
+
+
+def _kill(name: str, sudo: bool = False) -> str:
+    """Stop exactly the process recorded by _bg (never by name pattern)."""
+    k = "sudo kill" if sudo else "kill"
+    return f"P=$RUNTIME_PATH/pids/{name}.pid; [ -f $P ] && {k} $(cat $P) 2>/dev/null; rm -f $P; true"
+
+
 SPECS: List[RuntimeSpec] = [
     RuntimeSpec("spark", "Apache Spark on YARN with history server and auto executor sizing",
                 "3.3.1", "SPARK_HOME", APACHE + "/spark/spark-{version}/spark-{version}-bin-hadoop3.tgz",
@@ -100,8 +113,8 @@ SPECS: List[RuntimeSpec] = [
                 APACHE + "/hive/hive-standalone-metastore-{version}/hive-standalone-metastore-{version}-bin.tar.gz",
                 [_S("metastore", 9083, features=(sd.SERVICE_DISCOVERY_FEATURE_DATABASE,))],
                 ["HiveMetaStore"], [], {"metastore": "$METASTORE_HOME/logs"}, ["mysql", "postgres"],
-                start={"head": "nohup $METASTORE_HOME/bin/start-metastore > $METASTORE_HOME/logs/metastore.log 2>&1 &"},
-                stop={"head": "pkill -f HiveMetaStore || true"}),
+                start={"head": _bg("metastore", "$METASTORE_HOME/bin/start-metastore")},
+                stop={"head": _kill("metastore")}),
     RuntimeSpec("presto", "Presto interactive SQL", "0.276", "PRESTO_HOME",
                 "https://repo1.maven.org/maven2/com/facebook/presto/presto-server/{version}/presto-server-{version}.tar.gz",
                 [_S("presto", 8081, protocol=HTTP, features=(sd.SERVICE_DISCOVERY_FEATURE_ANALYTICS,))],
@@ -167,8 +180,9 @@ SPECS: List[RuntimeSpec] = [
                 "https://artifacts.elastic.co/downloads/elasticsearch/elasticsearch-{version}-linux-x86_64.tar.gz",
                 [_S("elasticsearch", 9200, A, protocol=HTTP)], ["Elasticsearch"], ["Elasticsearch"],
                 dependencies=["mount"],
-                start={"head": "$ELASTICSEARCH_HOME/bin/elasticsearch -d", "worker": "$ELASTICSEARCH_HOME/bin/elasticsearch -d"},
-                stop={"head": "pkill -f org.elasticsearch || true", "worker": "pkill -f org.elasticsearch || true"}),
+                start={"head": "mkdir -p $RUNTIME_PATH/pids; $ELASTICSEARCH_HOME/bin/elasticsearch -d -p $RUNTIME_PATH/pids/elasticsearch.pid",
+                       "worker": "mkdir -p $RUNTIME_PATH/pids; $ELASTICSEARCH_HOME/bin/elasticsearch -d -p $RUNTIME_PATH/pids/elasticsearch.pid"},
+                stop={"head": _kill("elasticsearch"), "worker": _kill("elasticsearch")}),
     RuntimeSpec("consul", "Consul service registry / KV (quorum)", "1.15.2",
                 download="https://releases.hashicorp.com/consul/{version}/consul_{version}_linux_amd64.zip",
                 services=[_S("consul", 8500, A, protocol=HTTP, features=(sd.SERVICE_DISCOVERY_FEATURE_KEY_VALUE,))],
@@ -180,8 +194,8 @@ SPECS: List[RuntimeSpec] = [
                 download="https://github.com/etcd-io/etcd/releases/download/v{version}/etcd-v{version}-linux-amd64.tar.gz",
                 services=[_S("etcd", 2379, W, features=(sd.SERVICE_DISCOVERY_FEATURE_KEY_VALUE,)), _S("etcd-peer", 2380, W, scope=LOCAL)],
                 worker_processes=["etcd"], quorum=True,
-                start={"worker": "nohup etcd --config-file $RUNTIME_PATH/etcd/etcd.yaml > $RUNTIME_PATH/etcd/etcd.log 2>&1 &"},
-                stop={"worker": "pkill -x etcd || true"}),
+                start={"worker": _bg("etcd", "etcd --config-file $RUNTIME_PATH/etcd/etcd.yaml")},
+                stop={"worker": _kill("etcd")}),
     RuntimeSpec("dnsmasq", "dnsmasq DNS forwarder (consul-backed)", services=[_S("dnsmasq", 53, A, features=(sd.SERVICE_DISCOVERY_FEATURE_DNS,))],
                 head_processes=["dnsmasq"], worker_processes=["dnsmasq"], dependencies=["consul"], apt=["dnsmasq"],
                 start={"head": "sudo service dnsmasq start", "worker": "sudo service dnsmasq start"},
@@ -194,9 +208,9 @@ SPECS: List[RuntimeSpec] = [
                 download="https://github.com/coredns/coredns/releases/download/v{version}/coredns_{version}_linux_amd64.tgz",
                 services=[_S("coredns", 53, A, features=(sd.SERVICE_DISCOVERY_FEATURE_DNS,))],
                 head_processes=["coredns"], worker_processes=["coredns"], dependencies=["consul"],
-                start={"head": "nohup coredns -conf $RUNTIME_PATH/coredns/Corefile > /dev/null 2>&1 &",
-                       "worker": "nohup coredns -conf $RUNTIME_PATH/coredns/Corefile > /dev/null 2>&1 &"},
-                stop={"head": "pkill -x coredns || true", "worker": "pkill -x coredns || true"}),
+                start={"head": _bg("coredns", "coredns -conf $RUNTIME_PATH/coredns/Corefile"),
+                       "worker": _bg("coredns", "coredns -conf $RUNTIME_PATH/coredns/Corefile")},
+                stop={"head": _kill("coredns"), "worker": _kill("coredns")}),
     RuntimeSpec("haproxy", "HAProxy L4/L7 load balancer (service-discovery backends)",
                 services=[_S("haproxy", 80, A, protocol=HTTP, features=(sd.SERVICE_DISCOVERY_FEATURE_LOAD_BALANCER,))],
                 head_processes=["haproxy"], worker_processes=["haproxy"], apt=["haproxy"],
@@ -219,24 +233,26 @@ SPECS: List[RuntimeSpec] = [
     RuntimeSpec("prometheus", "Prometheus with cluster / workspace service-discovery scrape", "2.45.0",
                 "PROMETHEUS_HOME", "https://github.com/prometheus/prometheus/releases/download/v{version}/prometheus-{version}.linux-amd64.tar.gz",
                 [_S("prometheus", 9090, protocol=HTTP, features=(sd.SERVICE_DISCOVERY_FEATURE_METRICS,))], ["prometheus"],
-                start={"head": "nohup $PROMETHEUS_HOME/prometheus --config.file=$PROMETHEUS_HOME/prometheus.yml > $PROMETHEUS_HOME/prometheus.log 2>&1 &"},
-                stop={"head": "pkill -x prometheus || true"}),
+                start={"head": _bg("prometheus", "$PROMETHEUS_HOME/prometheus --config.file=$PROMETHEUS_HOME/prometheus.yml")},
+                stop={"head": _kill("prometheus")}),
     RuntimeSpec("grafana", "Grafana dashboards (prometheus data source)", "10.0.3", "GRAFANA_HOME",
                 "https://dl.grafana.com/oss/release/grafana-{version}.linux-amd64.tar.gz",
                 [_S("grafana", 3000, protocol=HTTP)], ["grafana"],
-                start={"head": "nohup $GRAFANA_HOME/bin/grafana server --homepath $GRAFANA_HOME > /dev/null 2>&1 &"},
-                stop={"head": "pkill -f 'grafana server' || true"}),
+                start={"head": _bg("grafana", "$GRAFANA_HOME/bin/grafana server --homepath $GRAFANA_HOME")},
+                stop={"head": _kill("grafana")}),
     RuntimeSpec("nodex", "Node exporter (+ AMD GPU metrics textfile collector)", "1.6.1", "NODEX_HOME",
                 "https://github.com/prometheus/node_exporter/releases/download/v{version}/node_exporter-{version}.linux-amd64.tar.gz",
                 [_S("nodex", 9100, A, protocol=HTTP, features=(sd.SERVICE_DISCOVERY_FEATURE_METRICS,), metrics=True)],
                 ["node_exporter"], ["node_exporter"],
-                start={"head": "nohup $NODEX_HOME/node_exporter > /dev/null 2>&1 &", "worker": "nohup $NODEX_HOME/node_exporter > /dev/null 2>&1 &"},
-                stop={"head": "pkill -x node_exporter || true", "worker": "pkill -x node_exporter || true"}),
+                start={"head": _bg("node_exporter", "$NODEX_HOME/node_exporter"), "worker": _bg("node_exporter", "$NODEX_HOME/node_exporter")},
+                stop={"head": _kill("node_exporter"), "worker": _kill("node_exporter")}),
     RuntimeSpec("sshserver", "In-cluster passwordless SSH server (port 22022) used by MPI / rsh launchers",
                 services=[_S("sshserver", 22022, A, scope=LOCAL)], head_processes=["sshd"], worker_processes=["sshd"],
-                start={"head": "sudo /usr/sbin/sshd -f $RUNTIME_PATH/sshserver/sshd_config",
-                       "worker": "sudo /usr/sbin/sshd -f $RUNTIME_PATH/sshserver/sshd_config"},
-                stop={"head": "sudo pkill -f 'sshd -f' || true", "worker": "sudo pkill -f 'sshd -f' || true"}),
+                start={"head": "mkdir -p $RUNTIME_PATH/pids; sudo /usr/sbin/sshd -f $RUNTIME_PATH/sshserver/sshd_config "
+                               "-o PidFile=$RUNTIME_PATH/pids/sshserver.pid",
+                       "worker": "mkdir -p $RUNTIME_PATH/pids; sudo /usr/sbin/sshd -f $RUNTIME_PATH/sshserver/sshd_config "
+                               "-o PidFile=$RUNTIME_PATH/pids/sshserver.pid"},
+                stop={"head": _kill("sshserver", sudo=True), "worker": _kill("sshserver", sudo=True)}),
     RuntimeSpec("xinetd", "xinetd health-check endpoints for load balancers", head_processes=["xinetd"], worker_processes=["xinetd"],
                 apt=["xinetd"],
                 start={"head": "sudo service xinetd start", "worker": "sudo service xinetd start"},
@@ -245,8 +261,8 @@ SPECS: List[RuntimeSpec] = [
                 download="https://dl.min.io/server/minio/release/linux-amd64/minio",
                 services=[_S("minio", 9000, W, protocol=HTTP, features=(sd.SERVICE_DISCOVERY_FEATURE_STORAGE,))],
                 worker_processes=["minio"], quorum=True,
-                start={"worker": "nohup minio server $MINIO_VOLUMES > $RUNTIME_PATH/minio/minio.log 2>&1 &"},
-                stop={"worker": "pkill -x minio || true"}),
+                start={"worker": _bg("minio", "minio server $MINIO_VOLUMES")},
+                stop={"worker": _kill("minio")}),
 ]
 
 SPEC_BY_NAME = {s.name: s for s in SPECS}

@@ -90,6 +90,12 @@ class RuntimeBase(Runtime):
         env = dict(os.environ)
         env.setdefault(RUNTIME_PATH_ENV, runtime_path())
         env["IS_HEAD_NODE"] = "true" if head else "false"
+        # node variables are exported verbatim (never shell-expanded); resolve the runtime
+        # home references like MLFLOW_HOME=$RUNTIME_PATH/mlflow here, as plain strings
+        rp = env[RUNTIME_PATH_ENV]
+        for k, v in list(env.items()):
+            if "$RUNTIME_PATH" in v:
+                env[k] = v.replace("${RUNTIME_PATH}", rp).replace("$RUNTIME_PATH", rp)
         return env
 
     def node_install(self, head: bool):
