@@ -1,0 +1,270 @@
+// Bindings for RoPE, EmbeddingBag / interaction, detection ops and multi-tensor copy.
+// Host-side shape / dtype / alignment validation happens here, before any launch.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int ct_rope(const void*, void*, long, long, int, const void*, void*, long, long, int, const float*, const float*,
+            const int64_t*, int, long, int, int, int, hipStream_t);
+int ct_embbag_fwd(const float*, const int64_t*, const int64_t*, const int64_t*, const float*, void*, int, int, int,
+                  int, int, hipStream_t);
+int ct_embbag_bwd(const void*, int, float*, float*, const int64_t*, const int64_t*, const int64_t*, const float*,
+                  float*, int, int, int, int, float, hipStream_t);
+int ct_interact_fwd(const void*, const void*, void*, int, int, int, int, hipStream_t);
+int ct_interact_bwd(const void*, const void*, const void*, void*, void*, int, int, int, int, hipStream_t);
+int ct_nms(const float*, int, float, float, uint64_t*, int64_t*, int64_t*, hipStream_t);
+int ct_roi_align_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
+int ct_roi_align_bwd(const void*, const float*, float*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
+int ct_roi_pool_fwd(const void*, const float*, void*, int*, int, int, int, int, int, int, int, float, hipStream_t);
+int ct_roi_pool_bwd(const void*, const float*, const int*, float*, int, int, int, int, int, int, int, hipStream_t);
+int ct_focal_fwd(const void*, const int64_t*, float*, int, long, int, float, float, hipStream_t);
+int ct_focal_bwd(const void*, const int64_t*, const float*, void*, int, long, int, float, float, hipStream_t);
+int ct_mt_copy(const uint64_t*, const int64_t*, const int64_t*, int, long, void*, int, int, float, int, hipStream_t);
+}
+
+namespace {
+
+#define XCHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define XCHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define XCHECK_IN(x) do { XCHECK_CUDA(x); XCHECK_CONTIG(x); } while (0)
+#define XCHECK_DT(x, d) TORCH_CHECK((x).scalar_type() == (d), #x " has the wrong dtype")
+
+hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+int fb(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "expected fp32 or bf16");
+  return t.scalar_type() == at::kFloat ? 0 : 1;
+}
+
+// ---------------------------------------------------------------- RoPE
+// q: [T, Hq, D] view (token/head strides arbitrary, unit stride in D); k likewise (optional)
+void rope(at::Tensor q, c10::optional<at::Tensor> k, at::Tensor cos, at::Tensor sin,
+          c10::optional<at::Tensor> positions, int64_t seq_len, bool neox, bool backward) {
+  XCHECK_CUDA(q);
+  XCHECK_DT(q, at::kBFloat16);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1, "rope: q must be [T, H, D] with unit stride in D");
+  const long T = q.size(0);
+  const int D = (int)q.size(2);
+  TORCH_CHECK(D % 8 == 0, "rope: head dim must be a multiple of 8");
+  XCHECK_IN(cos); XCHECK_IN(sin); XCHECK_DT(cos, at::kFloat); XCHECK_DT(sin, at::kFloat);
+  TORCH_CHECK(cos.dim() == 2 && cos.size(1) == D / 2 && sin.sizes() == cos.sizes(), "rope: cos/sin must be [P, D/2]");
+  const int align = neox ? 4 : 8;
+  TORCH_CHECK(q.stride(0) % align == 0 && q.stride(1) % align == 0, "rope: q strides must keep vector alignment");
+  const void* kp = nullptr;
+  long kt = 0, kh = 0;
+  int hk = 0;
+  if (k.has_value() && k->defined()) {
+    XCHECK_CUDA(*k);
+    XCHECK_DT(*k, at::kBFloat16);
+    TORCH_CHECK(k->dim() == 3 && k->size(0) == T && k->size(2) == D && k->stride(2) == 1, "rope: k must be [T, Hk, D]");
+    TORCH_CHECK(k->stride(0) % align == 0 && k->stride(1) % align == 0, "rope: k strides must keep vector alignment");
+    kp = k->data_ptr(); kt = k->stride(0); kh = k->stride(1); hk = (int)k->size(1);
+  }
+  const int64_t* pp = nullptr;
+  if (positions.has_value() && positions->defined()) {
+    XCHECK_IN(*positions);
+    XCHECK_DT(*positions, at::kLong);
+    TORCH_CHECK(positions->numel() == T, "rope: one position per token");
+    pp = positions->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(seq_len > 0 && seq_len <= cos.size(0), "rope: seq_len must be in (0, P]");
+  }
+  const int rc = ct_rope(q.data_ptr(), q.data_ptr(), q.stride(0), q.stride(1), (int)q.size(1), kp, (void*)kp, kt, kh, hk,
+                         cos.data_ptr<float>(), sin.data_ptr<float>(), pp, (int)seq_len, T, D, neox ? 1 : 0,
+                         backward ? 1 : 0, stream());
+  TORCH_CHECK(rc == 0, "rope launch failed");
+}
+
+// ---------------------------------------------------------------- EmbeddingBag
+at::Tensor embbag_fwd(at::Tensor W, at::Tensor row_base, at::Tensor idx, at::Tensor offs,
+                      c10::optional<at::Tensor> psw, int64_t B, bool mean, bool bf16_out) {
+  XCHECK_IN(W); XCHECK_DT(W, at::kFloat); XCHECK_IN(row_base); XCHECK_IN(idx); XCHECK_IN(offs);
+  XCHECK_DT(idx, at::kLong); XCHECK_DT(offs, at::kLong); XCHECK_DT(row_base, at::kLong);
+  const int T = (int)row_base.numel(), E = (int)W.size(1);
+  TORCH_CHECK(offs.numel() == (long)T * B + 1, "embbag: offsets must have T*B+1 entries");
+  const float* pw = nullptr;
+  if (psw.has_value() && psw->defined()) {
+    XCHECK_IN(*psw); XCHECK_DT(*psw, at::kFloat);
+    TORCH_CHECK(psw->numel() == idx.numel());
+    pw = psw->data_ptr<float>();
+  }
+  auto out = at::empty({B, T, E}, W.options().dtype(bf16_out ? at::kBFloat16 : at::kFloat));
+  ct_embbag_fwd(W.data_ptr<float>(), row_base.data_ptr<int64_t>(), idx.data_ptr<int64_t>(), offs.data_ptr<int64_t>(),
+                pw, out.data_ptr(), bf16_out ? 1 : 0, T, (int)B, E, mean ? 1 : 0, stream());
+  return out;
+}
+
+// lr != 0: SGD-update W in place (sparse rows);  otherwise accumulate into dW
+void embbag_bwd(at::Tensor gout, at::Tensor W, c10::optional<at::Tensor> dW, at::Tensor row_base, at::Tensor idx,
+                at::Tensor offs, c10::optional<at::Tensor> psw, c10::optional<at::Tensor> dpsw, bool mean, double lr) {
+  XCHECK_IN(gout); XCHECK_IN(W); XCHECK_DT(W, at::kFloat);
+  const int T = (int)row_base.numel(), E = (int)W.size(1);
+  TORCH_CHECK(gout.dim() == 3 && gout.size(1) == T && gout.size(2) == E, "embbag_bwd: gout must be [B, T, E]");
+  const int B = (int)gout.size(0);
+  TORCH_CHECK(offs.numel() == (long)T * B + 1);
+  float* dwp = nullptr;
+  if (dW.has_value() && dW->defined()) {
+    XCHECK_IN(*dW); XCHECK_DT(*dW, at::kFloat);
+    TORCH_CHECK(dW->sizes() == W.sizes());
+    dwp = dW->data_ptr<float>();
+  } else {
+    TORCH_CHECK(lr != 0.0, "embbag_bwd: need dW or a learning rate");
+  }
+  const float* pw = (psw.has_value() && psw->defined()) ? psw->data_ptr<float>() : nullptr;
+  float* dpw = (dpsw.has_value() && dpsw->defined()) ? dpsw->data_ptr<float>() : nullptr;
+  ct_embbag_bwd(gout.data_ptr(), fb(gout), W.data_ptr<float>(), dwp, row_base.data_ptr<int64_t>(),
+                idx.data_ptr<int64_t>(), offs.data_ptr<int64_t>(), pw, dpw, T, B, E, mean ? 1 : 0, (float)lr, stream());
+}
+
+at::Tensor interact_fwd(at::Tensor x, at::Tensor emb) {
+  XCHECK_IN(x); XCHECK_IN(emb);
+  TORCH_CHECK(x.dim() == 2 && emb.dim() == 3 && emb.size(0) == x.size(0) && emb.size(2) == x.size(1),
+              "interact: x [B, E], emb [B, T, E]");
+  TORCH_CHECK(x.scalar_type() == emb.scalar_type());
+  const int B = (int)x.size(0), E = (int)x.size(1), T = (int)emb.size(1), F = T + 1;
+  auto out = at::empty({B, E + F * (F - 1) / 2}, x.options());
+  const int rc = ct_interact_fwd(x.data_ptr(), emb.data_ptr(), out.data_ptr(), fb(x), B, T, E, stream());
+  TORCH_CHECK(rc == 0, "interact_fwd: too many features for LDS");
+  return out;
+}
+
+std::vector<at::Tensor> interact_bwd(at::Tensor gout, at::Tensor x, at::Tensor emb) {
+  XCHECK_IN(gout); XCHECK_IN(x); XCHECK_IN(emb);
+  const int B = (int)x.size(0), E = (int)x.size(1), T = (int)emb.size(1), F = T + 1;
+  TORCH_CHECK(gout.size(0) == B && gout.size(1) == E + F * (F - 1) / 2 && gout.scalar_type() == x.scalar_type());
+  auto dx = at::empty_like(x);
+  auto demb = at::empty_like(emb);
+  const int rc = ct_interact_bwd(gout.data_ptr(), x.data_ptr(), emb.data_ptr(), dx.data_ptr(), demb.data_ptr(), fb(x),
+                                 B, T, E, stream());
+  TORCH_CHECK(rc == 0, "interact_bwd: too many features for LDS");
+  return {dx, demb};
+}
+
+// ---------------------------------------------------------------- detection
+// boxes must be sorted by descending score; returns kept indices (into the sorted boxes)
+at::Tensor nms_sorted(at::Tensor boxes, double thr, double offset) {
+  XCHECK_IN(boxes); XCHECK_DT(boxes, at::kFloat);
+  TORCH_CHECK(boxes.dim() == 2 && boxes.size(1) == 4, "nms: boxes must be [N, 4]");
+  const int n = (int)boxes.size(0);
+  auto lo = boxes.options().dtype(at::kLong);
+  if (n == 0) return at::empty({0}, lo);
+  TORCH_CHECK(n <= 524288, "nms: at most 524288 boxes");
+  const int cb = (n + 63) / 64;
+  auto mask = at::empty({(long)n * cb}, lo);
+  auto keep = at::empty({n}, lo);
+  auto nkeep = at::empty({1}, lo);
+  const int rc = ct_nms(boxes.data_ptr<float>(), n, (float)thr, (float)offset, (uint64_t*)mask.data_ptr<int64_t>(),
+                        keep.data_ptr<int64_t>(), nkeep.data_ptr<int64_t>(), stream());
+  TORCH_CHECK(rc == 0, "nms launch failed");
+  return keep.narrow(0, 0, nkeep.item<int64_t>());
+}
+
+void check_rois(const at::Tensor& feat, const at::Tensor& rois) {
+  XCHECK_IN(feat); XCHECK_IN(rois); XCHECK_DT(rois, at::kFloat);
+  TORCH_CHECK(feat.dim() == 4, "features must be NCHW");
+  TORCH_CHECK(rois.dim() == 2 && rois.size(1) == 5, "rois must be [K, 5] (batch, x1, y1, x2, y2)");
+}
+
+at::Tensor roi_align_fwd(at::Tensor feat, at::Tensor rois, double scale, int64_t PH, int64_t PW, int64_t sr, bool aligned) {
+  check_rois(feat, rois);
+  const int K = (int)rois.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
+  auto out = at::empty({K, C, PH, PW}, feat.options());
+  if (K) ct_roi_align_fwd(feat.data_ptr(), rois.data_ptr<float>(), out.data_ptr(), fb(feat), K, C, H, W, (int)PH, (int)PW,
+                          (float)scale, (int)sr, aligned ? 1 : 0, stream());
+  return out;
+}
+
+at::Tensor roi_align_bwd(at::Tensor gout, at::Tensor rois, std::vector<int64_t> fshape, double scale, int64_t sr, bool aligned) {
+  XCHECK_IN(gout); XCHECK_IN(rois);
+  TORCH_CHECK(fshape.size() == 4);
+  const int K = (int)rois.size(0), C = (int)fshape[1], H = (int)fshape[2], W = (int)fshape[3];
+  TORCH_CHECK(gout.dim() == 4 && gout.size(0) == K && gout.size(1) == C);
+  auto g = at::zeros(fshape, gout.options().dtype(at::kFloat));
+  if (K) ct_roi_align_bwd(gout.data_ptr(), rois.data_ptr<float>(), g.data_ptr<float>(), fb(gout), K, C, H, W,
+                          (int)gout.size(2), (int)gout.size(3), (float)scale, (int)sr, aligned ? 1 : 0, stream());
+  return gout.scalar_type() == at::kFloat ? g : g.to(gout.scalar_type());
+}
+
+std::vector<at::Tensor> roi_pool_fwd(at::Tensor feat, at::Tensor rois, double scale, int64_t PH, int64_t PW) {
+  check_rois(feat, rois);
+  const int K = (int)rois.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
+  auto out = at::empty({K, C, PH, PW}, feat.options());
+  auto arg = at::empty({K, C, PH, PW}, feat.options().dtype(at::kInt));
+  if (K) ct_roi_pool_fwd(feat.data_ptr(), rois.data_ptr<float>(), out.data_ptr(), arg.data_ptr<int>(), fb(feat), K, C, H,
+                         W, (int)PH, (int)PW, (float)scale, stream());
+  return {out, arg};
+}
+
+at::Tensor roi_pool_bwd(at::Tensor gout, at::Tensor rois, at::Tensor argmax, std::vector<int64_t> fshape) {
+  XCHECK_IN(gout); XCHECK_IN(rois); XCHECK_IN(argmax);
+  TORCH_CHECK(argmax.sizes() == gout.sizes());
+  const int K = (int)rois.size(0), C = (int)fshape[1], H = (int)fshape[2], W = (int)fshape[3];
+  auto g = at::zeros(fshape, gout.options().dtype(at::kFloat));
+  if (K) ct_roi_pool_bwd(gout.data_ptr(), rois.data_ptr<float>(), argmax.data_ptr<int>(), g.data_ptr<float>(), fb(gout),
+                         K, C, H, W, (int)gout.size(2), (int)gout.size(3), stream());
+  return gout.scalar_type() == at::kFloat ? g : g.to(gout.scalar_type());
+}
+
+at::Tensor focal_fwd(at::Tensor logits, at::Tensor targets, double gamma, double alpha) {
+  XCHECK_IN(logits); XCHECK_IN(targets); XCHECK_DT(targets, at::kLong);
+  TORCH_CHECK(logits.dim() == 2 && targets.numel() == logits.size(0));
+  auto loss = at::empty(logits.sizes(), logits.options().dtype(at::kFloat));
+  ct_focal_fwd(logits.data_ptr(), targets.data_ptr<int64_t>(), loss.data_ptr<float>(), fb(logits), logits.size(0),
+               (int)logits.size(1), (float)gamma, (float)alpha, stream());
+  return loss;
+}
+
+at::Tensor focal_bwd(at::Tensor logits, at::Tensor targets, at::Tensor gloss, double gamma, double alpha) {
+  XCHECK_IN(logits); XCHECK_IN(targets); XCHECK_IN(gloss); XCHECK_DT(gloss, at::kFloat);
+  TORCH_CHECK(gloss.sizes() == logits.sizes());
+  auto g = at::empty_like(logits);
+  ct_focal_bwd(logits.data_ptr(), targets.data_ptr<int64_t>(), gloss.data_ptr<float>(), g.data_ptr(), fb(logits),
+               logits.size(0), (int)logits.size(1), (float)gamma, (float)alpha, stream());
+  return g;
+}
+
+// ---------------------------------------------------------------- multi-tensor copy
+// pack (unpack=false): flat[offs[t]:...] = scale * tensors[t];  unpack: tensors[t] = scale * flat[...]
+void mt_copy(std::vector<at::Tensor> tensors, at::Tensor flat, double scale, bool unpack) {
+  XCHECK_IN(flat);
+  if (tensors.empty()) return;
+  const auto dt = tensors[0].scalar_type();
+  std::vector<int64_t> ptrs, sizes, offs;
+  long off = 0, mx = 0;
+  for (auto& t : tensors) {
+    XCHECK_IN(t);
+    TORCH_CHECK(t.scalar_type() == dt, "mt_copy: all tensors must share a dtype");
+    ptrs.push_back((int64_t)(uintptr_t)t.data_ptr());
+    sizes.push_back(t.numel());
+    offs.push_back(off);
+    off += t.numel();
+    mx = std::max<long>(mx, t.numel());
+  }
+  TORCH_CHECK(flat.numel() >= off, "mt_copy: flat buffer too small");
+  auto meta = at::tensor(ptrs, at::kLong);
+  meta = at::cat({meta, at::tensor(sizes, at::kLong), at::tensor(offs, at::kLong)}).to(flat.device(), /*non_blocking=*/true);
+  const int n = (int)tensors.size();
+  const int rc = ct_mt_copy((const uint64_t*)meta.data_ptr<int64_t>(), meta.data_ptr<int64_t>() + n,
+                            meta.data_ptr<int64_t>() + 2 * n, n, mx, flat.data_ptr(), fb(tensors[0]), fb(flat),
+                            (float)scale, unpack ? 1 : 0, stream());
+  TORCH_CHECK(rc == 0, "mt_copy: too many tensors");
+}
+
+}  // namespace
+
+void register_ext(pybind11::module& m) {
+  m.def("rope", &rope);
+  m.def("embbag_fwd", &embbag_fwd);
+  m.def("embbag_bwd", &embbag_bwd);
+  m.def("interact_fwd", &interact_fwd);
+  m.def("interact_bwd", &interact_bwd);
+  m.def("nms_sorted", &nms_sorted);
+  m.def("roi_align_fwd", &roi_align_fwd);
+  m.def("roi_align_bwd", &roi_align_bwd);
+  m.def("roi_pool_fwd", &roi_pool_fwd);
+  m.def("roi_pool_bwd", &roi_pool_bwd);
+  m.def("focal_fwd", &focal_fwd);
+  m.def("focal_bwd", &focal_bwd);
+  m.def("mt_copy", &mt_copy);
+}

@@ -256,6 +256,38 @@ extern "C" int ct_splitk_reduce(const float* P, int S, long n, void* g, int accu
   return 0;
 }
 
+// ---------------------------------------------------------------- multi-tensor pack / unpack
+// Gradient-bucket flatten for collectives (reference SSD distributed.py:13-48 and Horovod
+// tensor fusion, SURVEY.md §2.15 "Gradient bucket pack/scale/unpack"): tensor t (ptrs[t],
+// sizes[t] elements) <-> flat[offs[t] ...], with a scale and an optional fp32<->bf16 cast
+// (compression), for all tensors in ONE launch (blockIdx.y = tensor).
+template <typename TS, typename TD>
+__global__ void __launch_bounds__(256) mt_copy_kernel(const uint64_t* __restrict__ ptrs, const int64_t* __restrict__ sizes,
+                                                      const int64_t* __restrict__ offs, void* flat, float scale, int unpack) {
+  const int t = blockIdx.y;
+  const long n = sizes[t];
+  TS* tp = reinterpret_cast<TS*>(ptrs[t]);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    if (!unpack) reinterpret_cast<TD*>(flat)[offs[t] + i] = from_f<TD>(to_f<TS>(tp[i]) * scale);
+    else tp[i] = from_f<TS>(to_f<TD>(reinterpret_cast<const TD*>(flat)[offs[t] + i]) * scale);
+  }
+}
+
+extern "C" int ct_mt_copy(const uint64_t* ptrs, const int64_t* sizes, const int64_t* offs, int ntensors, long max_numel,
+                          void* flat, int tensor_dt, int flat_dt, float scale, int unpack, hipStream_t stream) {
+  if (ntensors <= 0) return 0;
+  if (ntensors > 65535) return -1;
+  long gx = (max_numel + 255) / 256;
+  if (gx > 256) gx = 256;
+  if (gx < 1) gx = 1;
+  const dim3 grid((unsigned)gx, (unsigned)ntensors);
+  if (tensor_dt == 0 && flat_dt == 0) mt_copy_kernel<float, float><<<grid, 256, 0, stream>>>(ptrs, sizes, offs, flat, scale, unpack);
+  else if (tensor_dt == 0 && flat_dt == 1) mt_copy_kernel<float, bf16_t><<<grid, 256, 0, stream>>>(ptrs, sizes, offs, flat, scale, unpack);
+  else if (tensor_dt == 1 && flat_dt == 0) mt_copy_kernel<bf16_t, float><<<grid, 256, 0, stream>>>(ptrs, sizes, offs, flat, scale, unpack);
+  else mt_copy_kernel<bf16_t, bf16_t><<<grid, 256, 0, stream>>>(ptrs, sizes, offs, flat, scale, unpack);
+  return 0;
+}
+
 // dtype codes: 0 = fp32, 1 = bf16
 extern "C" int ct_cast(const void* x, int xdt, void* y, int ydt, long n, float scale, int accumulate,
                        hipStream_t stream) {

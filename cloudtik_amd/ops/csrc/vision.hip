@@ -1,0 +1,335 @@
+// Detection ops for gfx950: NMS, ROIAlign fwd/bwd, ROIPool fwd/bwd, SigmoidFocalLoss
+// fwd/bwd -- the MI355X-native replacement of the Mask R-CNN csrc entry points
+// (reference maskrcnn_benchmark/csrc/vision.cpp:11-24, cpu/nms_cpu.cpp, cpu/ROIAlign_cpu.cpp;
+// SURVEY.md §2.13 N2-N4).  DeformConv / DeformPSROIPool are not implemented yet.
+//
+// NMS is the bitmask formulation: kernel 1 computes, for every box i and 64-box column
+// block, a 64-bit word of "box j > i overlaps i above the threshold" (one wave per
+// (row block, column block) tile, the column boxes staged in LDS); kernel 2 is ONE wave
+// that walks the boxes in score order 64 at a time: the diagonal words resolve a chunk
+// with scalar bit logic, then the kept boxes' rows are OR-ed into the removed bitmap
+// (lanes parallel over column words).  No host round trip.
+#include "common.h"
+
+namespace ct {
+
+// ------------------------------------------------------------------ NMS
+__device__ __forceinline__ float iou(const float* a, const float* b, float offset) {
+  const float l = fmaxf(a[0], b[0]), t = fmaxf(a[1], b[1]);
+  const float r = fminf(a[2], b[2]), btm = fminf(a[3], b[3]);
+  const float w = fmaxf(r - l + offset, 0.f), h = fmaxf(btm - t + offset, 0.f);
+  const float inter = w * h;
+  const float sa = (a[2] - a[0] + offset) * (a[3] - a[1] + offset);
+  const float sb = (b[2] - b[0] + offset) * (b[3] - b[1] + offset);
+  return inter / fmaxf(sa + sb - inter, 1e-12f);
+}
+
+__global__ void __launch_bounds__(64) nms_mask_kernel(const float* __restrict__ boxes, int n, float thr,
+                                                      float offset, uint64_t* __restrict__ mask, int cb) {
+  const int rb = blockIdx.y, colb = blockIdx.x;
+  if (colb < rb) return;                       // only higher-scored boxes suppress
+  __shared__ float cbox[64 * 4];
+  const int t = threadIdx.x;
+  const int cj = colb * 64 + t;
+  if (cj < n) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cbox[t * 4 + k] = boxes[cj * 4 + k];
+  }
+  __syncthreads();
+  const int i = rb * 64 + t;
+  if (i >= n) return;
+  float me[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) me[k] = boxes[i * 4 + k];
+  uint64_t bits = 0;
+  const int cols = min(64, n - colb * 64);
+  const int start = (colb == rb) ? t + 1 : 0;
+  for (int j = start; j < cols; ++j)
+    if (iou(me, cbox + j * 4, offset) > thr) bits |= (1ull << j);
+  mask[(long)i * cb + colb] = bits;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ void __launch_bounds__(64) nms_reduce_kernel(const uint64_t* __restrict__ mask, int n, int cb,
+                                                        int64_t* __restrict__ keep, int64_t* __restrict__ nkeep) {
+  extern __shared__ uint64_t removed[];
+  const int lane = threadIdx.x;
+  for (int d = lane; d < cb; d += 64) removed[d] = 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  long count = 0;
+  for (int c = 0; c < cb; ++c) {
+    const int box = c * 64 + lane;
+    const uint64_t diag = box < n ? mask[(long)box * cb + c] : 0ull;
+    uint64_t word = removed[c];
+    const int cols = min(64, n - c * 64);
+    uint64_t kept = 0;
+    for (int k = 0; k < cols; ++k) {           // uniform scalar walk of the chunk
+      if (!((word >> k) & 1ull)) {
+        kept |= 1ull << k;
+        word |= shfl64(diag, k);
+      }
+    }
+    // write the kept indices of this chunk in order
+    const bool mine = (kept >> lane) & 1ull;
+    const uint64_t below = lane ? (kept & ((1ull << lane) - 1ull)) : 0ull;
+    if (mine) keep[count + __popcll(below)] = box;
+    count += __popcll(kept);
+    // OR the kept rows into the later column words
+    for (int d = c + 1 + lane; d < cb; d += 64) {
+      uint64_t acc = removed[d];
+      uint64_t kk = kept;
+      while (kk) {
+        const int k = __ffsll((unsigned long long)kk) - 1;
+        kk &= kk - 1;
+        acc |= mask[(long)(c * 64 + k) * cb + d];
+      }
+      removed[d] = acc;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0) *nkeep = count;
+}
+
+// ------------------------------------------------------------------ ROIAlign
+template <typename T>
+__device__ __forceinline__ float bilinear(const T* f, int H, int W, float y, float x) {
+  if (y < -1.f || y > H || x < -1.f || x > W) return 0.f;
+  y = fmaxf(y, 0.f);
+  x = fmaxf(x, 0.f);
+  int y0 = (int)y, x0 = (int)x, y1, x1;
+  if (y0 >= H - 1) { y1 = y0 = H - 1; y = (float)y0; } else y1 = y0 + 1;
+  if (x0 >= W - 1) { x1 = x0 = W - 1; x = (float)x0; } else x1 = x0 + 1;
+  const float ly = y - y0, lx = x - x0, hy = 1.f - ly, hx = 1.f - lx;
+  return hy * hx * to_f<T>(f[y0 * W + x0]) + hy * lx * to_f<T>(f[y0 * W + x1]) +
+         ly * hx * to_f<T>(f[y1 * W + x0]) + ly * lx * to_f<T>(f[y1 * W + x1]);
+}
+
+struct RoiGeom { float x0, y0, bw, bh; int gh, gw; };
+
+__device__ __forceinline__ RoiGeom roi_geom(const float* r, float scale, int PH, int PW, int sr, bool aligned) {
+  const float off = aligned ? 0.5f : 0.f;
+  const float x0 = r[1] * scale - off, y0 = r[2] * scale - off;
+  const float x1 = r[3] * scale - off, y1 = r[4] * scale - off;
+  float rw = x1 - x0, rh = y1 - y0;
+  if (!aligned) { rw = fmaxf(rw, 1.f); rh = fmaxf(rh, 1.f); }
+  RoiGeom g;
+  g.x0 = x0; g.y0 = y0; g.bw = rw / PW; g.bh = rh / PH;
+  g.gh = sr > 0 ? sr : (int)ceilf(rh / PH);
+  g.gw = sr > 0 ? sr : (int)ceilf(rw / PW);
+  return g;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) roi_align_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ rois,
+                                                             T* __restrict__ out, int K, int C, int H, int W, int PH,
+                                                             int PW, float scale, int sr, int aligned) {
+  const long total = (long)K * C * PH * PW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int pw = i % PW, ph = (i / PW) % PH, c = (i / ((long)PW * PH)) % C;
+    const int k = i / ((long)PW * PH * C);
+    const float* r = rois + k * 5;
+    const int b = (int)r[0];
+    const RoiGeom g = roi_geom(r, scale, PH, PW, sr, aligned);
+    const T* f = feat + ((long)b * C + c) * H * W;
+    float acc = 0.f;
+    for (int iy = 0; iy < g.gh; ++iy) {
+      const float y = g.y0 + ph * g.bh + (iy + 0.5f) * g.bh / g.gh;
+      for (int ix = 0; ix < g.gw; ++ix) {
+        const float x = g.x0 + pw * g.bw + (ix + 0.5f) * g.bw / g.gw;
+        acc += bilinear(f, H, W, y, x);
+      }
+    }
+    out[i] = from_f<T>(acc / fmaxf((float)(g.gh * g.gw), 1.f));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) roi_align_bwd_kernel(const T* __restrict__ gout, const float* __restrict__ rois,
+                                                             float* __restrict__ gfeat, int K, int C, int H, int W, int PH,
+                                                             int PW, float scale, int sr, int aligned) {
+  const long total = (long)K * C * PH * PW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int pw = i % PW, ph = (i / PW) % PH, c = (i / ((long)PW * PH)) % C;
+    const int k = i / ((long)PW * PH * C);
+    const float* r = rois + k * 5;
+    const int b = (int)r[0];
+    const RoiGeom g = roi_geom(r, scale, PH, PW, sr, aligned);
+    float* f = gfeat + ((long)b * C + c) * H * W;
+    const float go = to_f<T>(gout[i]) / fmaxf((float)(g.gh * g.gw), 1.f);
+    for (int iy = 0; iy < g.gh; ++iy) {
+      float y = g.y0 + ph * g.bh + (iy + 0.5f) * g.bh / g.gh;
+      for (int ix = 0; ix < g.gw; ++ix) {
+        float x = g.x0 + pw * g.bw + (ix + 0.5f) * g.bw / g.gw;
+        if (y < -1.f || y > H || x < -1.f || x > W) continue;
+        y = fmaxf(y, 0.f);
+        x = fmaxf(x, 0.f);
+        int y0 = (int)y, x0 = (int)x, y1, x1;
+        float yy = y, xx = x;
+        if (y0 >= H - 1) { y1 = y0 = H - 1; yy = (float)y0; } else y1 = y0 + 1;
+        if (x0 >= W - 1) { x1 = x0 = W - 1; xx = (float)x0; } else x1 = x0 + 1;
+        const float ly = yy - y0, lx = xx - x0, hy = 1.f - ly, hx = 1.f - lx;
+        atomicAdd(f + y0 * W + x0, go * hy * hx);
+        atomicAdd(f + y0 * W + x1, go * hy * lx);
+        atomicAdd(f + y1 * W + x0, go * ly * hx);
+        atomicAdd(f + y1 * W + x1, go * ly * lx);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ ROIPool
+template <typename T>
+__global__ void __launch_bounds__(256) roi_pool_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ rois,
+                                                            T* __restrict__ out, int* __restrict__ argmax, int K, int C,
+                                                            int H, int W, int PH, int PW, float scale) {
+  const long total = (long)K * C * PH * PW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int pw = i % PW, ph = (i / PW) % PH, c = (i / ((long)PW * PH)) % C;
+    const int k = i / ((long)PW * PH * C);
+    const float* r = rois + k * 5;
+    const int b = (int)r[0];
+    const int x0 = (int)roundf(r[1] * scale), y0 = (int)roundf(r[2] * scale);
+    const int x1 = (int)roundf(r[3] * scale), y1 = (int)roundf(r[4] * scale);
+    const int rw = max(x1 - x0 + 1, 1), rh = max(y1 - y0 + 1, 1);
+    const float bw = (float)rw / PW, bh = (float)rh / PH;
+    int hs = min(max((int)floorf(ph * bh) + y0, 0), H), he = min(max((int)ceilf((ph + 1) * bh) + y0, 0), H);
+    int ws = min(max((int)floorf(pw * bw) + x0, 0), W), we = min(max((int)ceilf((pw + 1) * bw) + x0, 0), W);
+    const T* f = feat + ((long)b * C + c) * H * W;
+    float best = (he <= hs || we <= ws) ? 0.f : -INFINITY;
+    int arg = -1;
+    for (int y = hs; y < he; ++y)
+      for (int x = ws; x < we; ++x) {
+        const float v = to_f<T>(f[y * W + x]);
+        if (v > best) { best = v; arg = y * W + x; }
+      }
+    out[i] = from_f<T>(best);
+    argmax[i] = arg;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) roi_pool_bwd_kernel(const T* __restrict__ gout, const float* __restrict__ rois,
+                                                            const int* __restrict__ argmax, float* __restrict__ gfeat,
+                                                            int K, int C, int H, int W, int PH, int PW) {
+  const long total = (long)K * C * PH * PW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int a = argmax[i];
+    if (a < 0) continue;
+    const int c = (i / ((long)PW * PH)) % C;
+    const int k = i / ((long)PW * PH * C);
+    const int b = (int)rois[k * 5];
+    atomicAdd(gfeat + ((long)b * C + c) * H * W + a, to_f<T>(gout[i]));
+  }
+}
+
+// ------------------------------------------------------------------ SigmoidFocalLoss
+template <typename T>
+__global__ void __launch_bounds__(256) focal_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                         float* __restrict__ loss, long N, int C, float gamma, float alpha) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < N * C; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / C;
+    const int c = (int)(i % C);
+    const long t = tgt[n];
+    const float c1 = (t == c + 1), c2 = (t >= 0) & (t != c + 1);
+    const float x = to_f<T>(logits[i]);
+    const float p = 1.f / (1.f + __expf(-x));
+    const float term1 = powf(1.f - p, gamma) * __logf(fmaxf(p, 1.17549435e-38f));
+    // log(1-p) computed stably: -x*(x>=0) - log(1+exp(-|x|))
+    const float log1mp = -x * (x >= 0.f) - __logf(1.f + __expf(x - 2.f * x * (x >= 0.f)));
+    const float term2 = powf(p, gamma) * log1mp;
+    loss[i] = -c1 * alpha * term1 - c2 * (1.f - alpha) * term2;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) focal_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                         const float* __restrict__ gloss, T* __restrict__ glogits,
+                                                         long N, int C, float gamma, float alpha) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < N * C; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / C;
+    const int c = (int)(i % C);
+    const long t = tgt[n];
+    const float c1 = (t == c + 1), c2 = (t >= 0) & (t != c + 1);
+    const float x = to_f<T>(logits[i]);
+    const float p = 1.f / (1.f + __expf(-x));
+    const float logp = __logf(fmaxf(p, 1.17549435e-38f));
+    const float log1mp = -x * (x >= 0.f) - __logf(1.f + __expf(x - 2.f * x * (x >= 0.f)));
+    const float d1 = powf(1.f - p, gamma) * (1.f - p - gamma * p * logp);
+    const float d2 = powf(p, gamma) * (gamma * (1.f - p) * log1mp - p);
+    glogits[i] = from_f<T>(gloss[i] * (-c1 * alpha * d1 - c2 * (1.f - alpha) * d2));
+  }
+}
+
+inline int grid1d(long n) {
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+extern "C" int ct_nms(const float* boxes, int n, float thr, float offset, uint64_t* mask_ws, int64_t* keep,
+                      int64_t* nkeep, hipStream_t stream) {
+  if (n <= 0) return -1;
+  const int cb = (n + 63) / 64;
+  if (cb * 8 > 64 * 1024) return -2;               // removed bitmap must fit in LDS (n <= 524288)
+  nms_mask_kernel<<<dim3(cb, cb), 64, 0, stream>>>(boxes, n, thr, offset, mask_ws, cb);
+  nms_reduce_kernel<<<1, 64, cb * sizeof(uint64_t), stream>>>(mask_ws, n, cb, keep, nkeep);
+  return 0;
+}
+
+extern "C" int ct_roi_align_fwd(const void* feat, const float* rois, void* out, int dt, int K, int C, int H, int W,
+                                int PH, int PW, float scale, int sr, int aligned, hipStream_t stream) {
+  const int g = grid1d((long)K * C * PH * PW);
+  if (dt == 0) roi_align_fwd_kernel<float><<<g, 256, 0, stream>>>((const float*)feat, rois, (float*)out, K, C, H, W, PH, PW, scale, sr, aligned);
+  else roi_align_fwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)feat, rois, (bf16_t*)out, K, C, H, W, PH, PW, scale, sr, aligned);
+  return 0;
+}
+
+extern "C" int ct_roi_align_bwd(const void* gout, const float* rois, float* gfeat, int dt, int K, int C, int H, int W,
+                                int PH, int PW, float scale, int sr, int aligned, hipStream_t stream) {
+  const int g = grid1d((long)K * C * PH * PW);
+  if (dt == 0) roi_align_bwd_kernel<float><<<g, 256, 0, stream>>>((const float*)gout, rois, gfeat, K, C, H, W, PH, PW, scale, sr, aligned);
+  else roi_align_bwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)gout, rois, gfeat, K, C, H, W, PH, PW, scale, sr, aligned);
+  return 0;
+}
+
+extern "C" int ct_roi_pool_fwd(const void* feat, const float* rois, void* out, int* argmax, int dt, int K, int C, int H,
+                               int W, int PH, int PW, float scale, hipStream_t stream) {
+  const int g = grid1d((long)K * C * PH * PW);
+  if (dt == 0) roi_pool_fwd_kernel<float><<<g, 256, 0, stream>>>((const float*)feat, rois, (float*)out, argmax, K, C, H, W, PH, PW, scale);
+  else roi_pool_fwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)feat, rois, (bf16_t*)out, argmax, K, C, H, W, PH, PW, scale);
+  return 0;
+}
+
+extern "C" int ct_roi_pool_bwd(const void* gout, const float* rois, const int* argmax, float* gfeat, int dt, int K, int C,
+                               int H, int W, int PH, int PW, hipStream_t stream) {
+  const int g = grid1d((long)K * C * PH * PW);
+  if (dt == 0) roi_pool_bwd_kernel<float><<<g, 256, 0, stream>>>((const float*)gout, rois, argmax, gfeat, K, C, H, W, PH, PW);
+  else roi_pool_bwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)gout, rois, argmax, gfeat, K, C, H, W, PH, PW);
+  return 0;
+}
+
+extern "C" int ct_focal_fwd(const void* logits, const int64_t* tgt, float* loss, int dt, long N, int C, float gamma,
+                            float alpha, hipStream_t stream) {
+  const int g = grid1d(N * C);
+  if (dt == 0) focal_fwd_kernel<float><<<g, 256, 0, stream>>>((const float*)logits, tgt, loss, N, C, gamma, alpha);
+  else focal_fwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)logits, tgt, loss, N, C, gamma, alpha);
+  return 0;
+}
+
+extern "C" int ct_focal_bwd(const void* logits, const int64_t* tgt, const float* gloss, void* glogits, int dt, long N,
+                            int C, float gamma, float alpha, hipStream_t stream) {
+  const int g = grid1d(N * C);
+  if (dt == 0) focal_bwd_kernel<float><<<g, 256, 0, stream>>>((const float*)logits, tgt, gloss, (float*)glogits, N, C, gamma, alpha);
+  else focal_bwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)logits, tgt, gloss, (bf16_t*)glogits, N, C, gamma, alpha);
+  return 0;
+}

@@ -1,0 +1,222 @@
+"""Detection ops with HIP kernels (csrc/vision.hip) and torch references: nms, batched_nms,
+roi_align, roi_pool, sigmoid_focal_loss -- the Mask R-CNN csrc entry points (reference
+maskrcnn_benchmark/csrc/vision.cpp:11-24)."""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+
+def _native():
+    from cloudtik_amd import ops
+    return ops.require_native()
+
+
+def _use_native(*ts) -> bool:
+    from cloudtik_amd import ops
+    return ops._use_native(*ts)
+
+
+# ---------------------------------------------------------------------- NMS
+def _box_iou(a, b, offset=0.0):
+    lt = torch.maximum(a[:, None, :2], b[None, :, :2])
+    rb = torch.minimum(a[:, None, 2:], b[None, :, 2:])
+    wh = (rb - lt + offset).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    area = lambda x: (x[:, 2] - x[:, 0] + offset) * (x[:, 3] - x[:, 1] + offset)
+    return inter / (area(a)[:, None] + area(b)[None, :] - inter).clamp(min=1e-12)
+
+
+def nms_reference(boxes, scores, iou_threshold, offset=0.0):
+    order = scores.argsort(descending=True)
+    b = boxes[order].float()
+    iou = _box_iou(b, b, offset)
+    n = b.shape[0]
+    removed = torch.zeros(n, dtype=torch.bool)
+    keep = []
+    iou_cpu = iou.cpu()
+    for i in range(n):
+        if removed[i]:
+            continue
+        keep.append(i)
+        removed |= iou_cpu[i] > iou_threshold
+    return order[torch.tensor(keep, dtype=torch.long, device=boxes.device)] if keep else order[:0]
+
+
+def nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float, offset: float = 0.0) -> torch.Tensor:
+    """Indices of kept boxes, by decreasing score (torchvision.ops.nms semantics; ``offset=1``
+    gives the legacy +1 box-area convention of maskrcnn_benchmark)."""
+    if boxes.is_cuda and _use_native(boxes):
+        order = scores.argsort(descending=True)
+        keep = _native().nms_sorted(boxes[order].float().contiguous(), float(iou_threshold), float(offset))
+        return order[keep]
+    return nms_reference(boxes, scores, iou_threshold, offset)
+
+
+def batched_nms(boxes, scores, idxs, iou_threshold, offset=0.0):
+    """NMS per category: boxes of different ``idxs`` never suppress each other."""
+    if boxes.numel() == 0:
+        return torch.empty(0, dtype=torch.long, device=boxes.device)
+    shift = idxs.to(boxes.dtype)[:, None] * (boxes.max() + 1 + offset)
+    return nms(boxes + shift, scores, iou_threshold, offset)
+
+
+# ---------------------------------------------------------------------- ROIAlign
+def _bilinear_ref(f, y, x):
+    C, H, W = f.shape
+    valid = (y >= -1) & (y <= H) & (x >= -1) & (x <= W)
+    y = y.clamp(min=0)
+    x = x.clamp(min=0)
+    y0 = y.floor().long()
+    x0 = x.floor().long()
+    ycap = y0 >= H - 1
+    xcap = x0 >= W - 1
+    y0 = torch.where(ycap, torch.full_like(y0, H - 1), y0)
+    x0 = torch.where(xcap, torch.full_like(x0, W - 1), x0)
+    y = torch.where(ycap, y0.float(), y)
+    x = torch.where(xcap, x0.float(), x)
+    y1 = torch.where(ycap, y0, y0 + 1)
+    x1 = torch.where(xcap, x0, x0 + 1)
+    ly, lx = y - y0, x - x0
+    hy, hx = 1 - ly, 1 - lx
+    v = (hy * hx) * f[:, y0, x0] + (hy * lx) * f[:, y0, x1] + (ly * hx) * f[:, y1, x0] + (ly * lx) * f[:, y1, x1]
+    return v * valid
+
+
+def roi_align_reference(feat, rois, output_size, spatial_scale=1.0, sampling_ratio=-1, aligned=False):
+    PH, PW = output_size
+    K = rois.shape[0]
+    C = feat.shape[1]
+    out = torch.zeros(K, C, PH, PW, dtype=torch.float32, device=feat.device)
+    off = 0.5 if aligned else 0.0
+    for k in range(K):
+        b = int(rois[k, 0])
+        x0, y0, x1, y1 = [float(v) * spatial_scale - off for v in rois[k, 1:]]
+        rw, rh = x1 - x0, y1 - y0
+        if not aligned:
+            rw, rh = max(rw, 1.0), max(rh, 1.0)
+        bw, bh = rw / PW, rh / PH
+        gh = sampling_ratio if sampling_ratio > 0 else int(torch.tensor(rh / PH).ceil())
+        gw = sampling_ratio if sampling_ratio > 0 else int(torch.tensor(rw / PW).ceil())
+        f = feat[b].float()
+        for ph in range(PH):
+            for pw in range(PW):
+                ys = torch.tensor([y0 + ph * bh + (iy + 0.5) * bh / gh for iy in range(gh)], device=feat.device)
+                xs = torch.tensor([x0 + pw * bw + (ix + 0.5) * bw / gw for ix in range(gw)], device=feat.device)
+                yy, xx = torch.meshgrid(ys, xs, indexing="ij")
+                v = _bilinear_ref(f, yy.reshape(-1), xx.reshape(-1))
+                out[k, :, ph, pw] = v.sum(-1) / max(gh * gw, 1)
+    return out
+
+
+class _RoiAlignFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois, output_size, scale, sr, aligned):
+        ctx.save_for_backward(rois)
+        ctx.meta = (list(feat.shape), scale, sr, aligned)
+        return _native().roi_align_fwd(feat.contiguous(), rois.float().contiguous(), scale, output_size[0],
+                                       output_size[1], sr, aligned)
+
+    @staticmethod
+    def backward(ctx, g):
+        (rois,) = ctx.saved_tensors
+        shape, scale, sr, aligned = ctx.meta
+        return (_native().roi_align_bwd(g.contiguous(), rois.float().contiguous(), shape, scale, sr, aligned),
+                None, None, None, None, None)
+
+
+def roi_align(feat, rois, output_size, spatial_scale: float = 1.0, sampling_ratio: int = -1, aligned: bool = False):
+    """feat [N, C, H, W]; rois [K, 5] = (batch_idx, x1, y1, x2, y2) -> [K, C, PH, PW]."""
+    if isinstance(output_size, int):
+        output_size = (output_size, output_size)
+    if feat.is_cuda and _use_native(feat):
+        return _RoiAlignFn.apply(feat, rois, tuple(output_size), float(spatial_scale), int(sampling_ratio), bool(aligned))
+    return roi_align_reference(feat, rois, output_size, spatial_scale, sampling_ratio, aligned).to(feat.dtype)
+
+
+# ---------------------------------------------------------------------- ROIPool
+def roi_pool_reference(feat, rois, output_size, spatial_scale=1.0):
+    PH, PW = output_size
+    K, C, H, W = rois.shape[0], feat.shape[1], feat.shape[2], feat.shape[3]
+    out = torch.zeros(K, C, PH, PW, dtype=torch.float32, device=feat.device)
+    for k in range(K):
+        b = int(rois[k, 0])
+        x0, y0, x1, y1 = [int(round(float(v) * spatial_scale)) for v in rois[k, 1:]]
+        rw, rh = max(x1 - x0 + 1, 1), max(y1 - y0 + 1, 1)
+        bw, bh = rw / PW, rh / PH
+        import math
+        for ph in range(PH):
+            hs = min(max(int(math.floor(ph * bh)) + y0, 0), H)
+            he = min(max(int(math.ceil((ph + 1) * bh)) + y0, 0), H)
+            for pw in range(PW):
+                ws = min(max(int(math.floor(pw * bw)) + x0, 0), W)
+                we = min(max(int(math.ceil((pw + 1) * bw)) + x0, 0), W)
+                if he > hs and we > ws:
+                    out[k, :, ph, pw] = feat[b, :, hs:he, ws:we].float().amax(dim=(-1, -2))
+    return out
+
+
+class _RoiPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois, output_size, scale):
+        out, arg = _native().roi_pool_fwd(feat.contiguous(), rois.float().contiguous(), scale, output_size[0],
+                                          output_size[1])
+        ctx.save_for_backward(rois, arg)
+        ctx.shape = list(feat.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        rois, arg = ctx.saved_tensors
+        return _native().roi_pool_bwd(g.contiguous(), rois.float().contiguous(), arg, ctx.shape), None, None, None
+
+
+def roi_pool(feat, rois, output_size, spatial_scale: float = 1.0):
+    if isinstance(output_size, int):
+        output_size = (output_size, output_size)
+    if feat.is_cuda and _use_native(feat):
+        return _RoiPoolFn.apply(feat, rois, tuple(output_size), float(spatial_scale))
+    return roi_pool_reference(feat, rois, output_size, spatial_scale).to(feat.dtype)
+
+
+# ---------------------------------------------------------------------- SigmoidFocalLoss
+def sigmoid_focal_loss_reference(logits, targets, gamma, alpha):
+    N, C = logits.shape
+    x = logits.float()
+    cls = torch.arange(1, C + 1, device=logits.device)[None, :]
+    t = targets[:, None]
+    c1 = (t == cls).float()
+    c2 = ((t >= 0) & (t != cls)).float()
+    p = torch.sigmoid(x)
+    term1 = (1 - p) ** gamma * torch.log(p.clamp(min=torch.finfo(torch.float32).tiny))
+    term2 = p ** gamma * torch.nn.functional.logsigmoid(-x)
+    return -c1 * alpha * term1 - c2 * (1 - alpha) * term2
+
+
+class _FocalFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, gamma, alpha):
+        logits, targets = logits.contiguous(), targets.contiguous()
+        ctx.save_for_backward(logits, targets)
+        ctx.gamma, ctx.alpha = gamma, alpha
+        return _native().focal_fwd(logits, targets, gamma, alpha)
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, targets = ctx.saved_tensors
+        return _native().focal_bwd(logits, targets, g.float().contiguous(), ctx.gamma, ctx.alpha), None, None, None
+
+
+def sigmoid_focal_loss(logits, targets, gamma: float = 2.0, alpha: float = 0.25, reduction: str = "sum"):
+    """maskrcnn_benchmark semantics: targets in 1..C are foreground classes, 0 background,
+    negative entries ignored.  Returns per-element losses reduced by ``reduction``."""
+    if logits.is_cuda and _use_native(logits):
+        loss = _FocalFn.apply(logits, targets.to(torch.int64), float(gamma), float(alpha))
+    else:
+        loss = sigmoid_focal_loss_reference(logits, targets, gamma, alpha)
+    if reduction == "sum":
+        return loss.sum()
+    if reduction == "mean":
+        return loss.mean()
+    return loss

@@ -206,3 +206,28 @@ def test_gradbucketer_two_ranks_gloo():
     assert nb > 1
     torch.testing.assert_close(g0, g1)          # all-reduced grads agree
     torch.testing.assert_close(w0, w1)          # params identical after the step
+
+
+def test_new_op_references_cpu():
+    """CPU paths of the DLRM / detection / RoPE ops (the GPU kernels are pinned to these)."""
+    from cloudtik_amd import ops
+    from cloudtik_amd.ops.rope import rope_reference
+    cos, sin = ops.rotary_cache(16, 8)
+    x = torch.randn(2, 5, 3, 8, dtype=torch.bfloat16)
+    q, k = ops.apply_rotary(x, x, cos, sin)
+    back = rope_reference(q.reshape(-1, 3, 8).float(), cos, sin, torch.arange(10) % 5, inverse=True)
+    assert torch.allclose(back, x.reshape(-1, 3, 8).float(), atol=0.05)
+    ebc = ops.EmbeddingBagCollection([10, 20], 4)
+    idx, offs = ops.pack_bags([torch.tensor([1, 2, 3]), torch.tensor([5])], [torch.tensor([0, 1]), torch.tensor([0, 0])], 2)
+    out = ebc(idx, offs, 2)
+    ref = torch.nn.functional.embedding_bag(torch.tensor([1, 2, 3]), ebc.weight[:10], torch.tensor([0, 1]), mode="sum")
+    assert torch.allclose(out[:, 0], ref)
+    assert torch.allclose(out[0, 1], torch.zeros(4)) and torch.allclose(out[1, 1], ebc.weight[15])
+    z = ops.dot_interaction(torch.randn(3, 4), torch.randn(3, 2, 4))
+    assert z.shape == (3, 4 + 3)
+    boxes = torch.tensor([[0, 0, 10, 10], [1, 1, 11, 11], [50, 50, 60, 60.]])
+    assert ops.nms(boxes, torch.tensor([0.5, 0.9, 0.1]), 0.5).tolist() == [1, 2]
+    ra = ops.roi_align(torch.arange(16.).view(1, 1, 4, 4), torch.tensor([[0, 0, 0, 3, 3.]]), 1, aligned=True)
+    assert abs(ra.item() - 7.5) < 1e-4   # mean of a linear ramp over the box
+    fl = ops.sigmoid_focal_loss(torch.zeros(2, 3), torch.tensor([1, 0]))
+    assert fl.item() > 0
