@@ -227,7 +227,7 @@ def test_new_op_references_cpu():
     assert z.shape == (3, 4 + 3)
     boxes = torch.tensor([[0, 0, 10, 10], [1, 1, 11, 11], [50, 50, 60, 60.]])
     assert ops.nms(boxes, torch.tensor([0.5, 0.9, 0.1]), 0.5).tolist() == [1, 2]
-    ra = ops.roi_align(torch.arange(16.).view(1, 1, 4, 4), torch.tensor([[0, 0, 0, 3, 3.]]), 1, aligned=True)
+    ra = ops.roi_align(torch.arange(16.).view(1, 1, 4, 4), torch.tensor([[0, 0, 0, 3, 3.]]), 1, aligned=False)
     assert abs(ra.item() - 7.5) < 1e-4   # mean of a linear ramp over the box
     fl = ops.sigmoid_focal_loss(torch.zeros(2, 3), torch.tensor([1, 0]))
     assert fl.item() > 0
