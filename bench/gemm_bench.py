@@ -5,6 +5,10 @@ N*K/(256*256) = 16..192 output tiles, too few to fill 256 CUs)."""
 import argparse
 import json
 
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 

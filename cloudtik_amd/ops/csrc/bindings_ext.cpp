@@ -21,6 +21,12 @@ int ct_roi_pool_bwd(const void*, const float*, const int*, float*, int, int, int
 int ct_focal_fwd(const void*, const int64_t*, float*, int, long, int, float, float, hipStream_t);
 int ct_focal_bwd(const void*, const int64_t*, const float*, void*, int, long, int, float, float, hipStream_t);
 int ct_mt_copy(const uint64_t*, const int64_t*, const int64_t*, int, long, void*, int, int, float, int, hipStream_t);
+void* ct_loader_create(int, const void* const*, const long*, long, int, int, uint64_t, int, int, int, int, int, int);
+long ct_loader_num_batches(void*);
+void ct_loader_set_epoch(void*, long);
+long ct_loader_next_device(void*, void* const*, hipStream_t, hipStream_t);
+long ct_loader_next_host(void*, void* const*);
+void ct_loader_destroy(void*);
 }
 
 namespace {
@@ -251,9 +257,51 @@ void mt_copy(std::vector<at::Tensor> tensors, at::Tensor flat, double scale, boo
   TORCH_CHECK(rc == 0, "mt_copy: too many tensors");
 }
 
+// ---------------------------------------------------------------- native loader
+// cols: CPU contiguous tensors whose dim 0 is the row; the Python wrapper keeps them alive
+int64_t loader_create(std::vector<at::Tensor> cols, int64_t batch, bool shuffle, int64_t seed, bool drop_last,
+                      int64_t workers, int64_t slots, int64_t rank, int64_t world, bool pinned) {
+  TORCH_CHECK(!cols.empty(), "loader: no columns");
+  const long n = cols[0].size(0);
+  std::vector<const void*> ptrs;
+  std::vector<long> rb;
+  for (auto& c : cols) {
+    TORCH_CHECK(!c.is_cuda() && c.is_contiguous(), "loader: columns must be contiguous host tensors");
+    TORCH_CHECK(c.size(0) == n, "loader: all columns need the same row count");
+    ptrs.push_back(c.data_ptr());
+    rb.push_back((long)(c.numel() / std::max<long>(n, 1)) * (long)c.element_size());
+  }
+  void* h = ct_loader_create((int)cols.size(), ptrs.data(), rb.data(), n, (int)batch, shuffle, (uint64_t)seed, drop_last,
+                             (int)workers, (int)slots, (int)rank, (int)world, pinned ? 1 : 0);
+  TORCH_CHECK(h != nullptr, "loader: creation failed (bad arguments or pinned allocation failed)");
+  return (int64_t)(uintptr_t)h;
+}
+
+int64_t loader_num_batches(int64_t h) { return ct_loader_num_batches((void*)(uintptr_t)h); }
+void loader_set_epoch(int64_t h, int64_t epoch) { ct_loader_set_epoch((void*)(uintptr_t)h, epoch); }
+void loader_destroy(int64_t h) { ct_loader_destroy((void*)(uintptr_t)h); }
+
+int64_t loader_next_device(int64_t h, std::vector<at::Tensor> outs, int64_t copy_stream) {
+  std::vector<void*> ptrs;
+  for (auto& t : outs) { XCHECK_IN(t); ptrs.push_back(t.data_ptr()); }
+  return ct_loader_next_device((void*)(uintptr_t)h, ptrs.data(), (hipStream_t)(uintptr_t)copy_stream, stream());
+}
+
+int64_t loader_next_host(int64_t h, std::vector<at::Tensor> outs) {
+  std::vector<void*> ptrs;
+  for (auto& t : outs) { TORCH_CHECK(!t.is_cuda() && t.is_contiguous()); ptrs.push_back(t.data_ptr()); }
+  return ct_loader_next_host((void*)(uintptr_t)h, ptrs.data());
+}
+
 }  // namespace
 
 void register_ext(pybind11::module& m) {
+  m.def("loader_create", &loader_create);
+  m.def("loader_num_batches", &loader_num_batches);
+  m.def("loader_set_epoch", &loader_set_epoch);
+  m.def("loader_destroy", &loader_destroy);
+  m.def("loader_next_device", &loader_next_device, pybind11::call_guard<pybind11::gil_scoped_release>());
+  m.def("loader_next_host", &loader_next_host, pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("rope", &rope);
   m.def("embbag_fwd", &embbag_fwd);
   m.def("embbag_bwd", &embbag_bwd);
