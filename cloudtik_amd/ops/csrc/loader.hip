@@ -72,7 +72,9 @@ struct Loader {
       std::shuffle(perm.begin(), perm.end(), g);
     }
     const long gb = global_batches();
-    nbatches = gb / world + (rank < gb % world ? 1 : 0);
+    // drop_last: every rank runs the same number of steps (collectives stay matched);
+    // otherwise the first gb % world ranks see one extra batch (evaluation covers all data)
+    nbatches = drop_last ? gb / world : gb / world + (rank < gb % world ? 1 : 0);
     next_to_fill = next_to_take = 0;
     ready.clear();
   }

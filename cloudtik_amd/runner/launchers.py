@@ -82,8 +82,10 @@ class LocalLauncher(Launcher):
         env.update(RANK=str(self.first_rank + local_rank), LOCAL_RANK=str(local_rank),
                    LOCAL_WORLD_SIZE=str(self.local_world), NODE_RANK=str(self.node_rank),
                    GROUP_RANK=str(self.node_rank))
-        if cpus and "OMP_NUM_THREADS" not in os.environ:
-            env["OMP_NUM_THREADS"] = str(max(1, len(cpus)))
+        if "OMP_NUM_THREADS" not in os.environ:
+            # the rank's pinned cores, or a fair share of the node without GPU affinity
+            share = len(cpus) if cpus else (os.cpu_count() or 1) // max(1, self.local_world)
+            env["OMP_NUM_THREADS"] = str(max(1, share))
         if self.args.launcher == "horovod":
             env.update(HOROVOD_RANK=env["RANK"], HOROVOD_SIZE=env["WORLD_SIZE"],
                        HOROVOD_LOCAL_RANK=str(local_rank), HOROVOD_LOCAL_SIZE=str(self.local_world))

@@ -182,6 +182,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def state_dict(self):
         sd = super().state_dict()
         sd["flat"] = {k: v for k, v in self._flat_state().items()}
+        if self.space.master is not None:      # fp32 master shard (the bf16 model alone loses bits)
+            sd["flat"]["master"] = self.space.master
         sd["step_count"] = self.step_count
         return sd
 
@@ -190,7 +192,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self.step_count = sd.pop("step_count", 0)
         super().load_state_dict(sd)
         for k, v in flat.items():
-            getattr(self, k).copy_(v)
+            dst = self.space.master if k == "master" else getattr(self, k)
+            dst.copy_(v)
 
     def _flat_state(self):
         return {}

@@ -78,6 +78,11 @@ def test_virtual_cluster_lifecycle(cluster, tmp_path):
     job = tmp_path / "job.py"
     job.write_text("import sys\nprint('JOB-ARGS', sys.argv[1:])\n")
     assert "JOB-ARGS ['x', 'y']" in _run(env, "submit", cfg, str(job), "x", "y")
+    # north-star config #1: AI runtime MNIST MLP on CPU through `cloudtik submit` -> cloudtik-run
+    out = _run(env, "submit", cfg, os.path.join(ROOT, "examples", "ai", "mnist_mlp.py"), "--epochs", "2",
+               "--train-size", "3000")
+    res = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert res["final"]["eval_accuracy"] > 0.8
 
     assert "healthy" in _run(env, "health-check", cfg)
     ps = _run(env, "process-status", cfg)

@@ -19,7 +19,7 @@ def test_loader_shards_cover_dataset(world, drop_last):
             assert (b["x"][:, 0].numpy() == b["y"].numpy() * 3).all()
             seen += b["y"].tolist()
         L.close()
-    expect = (n // B) * B if drop_last else n
+    expect = (n // B // world) * world * B if drop_last else n
     assert len(seen) == expect and len(set(seen)) == expect
 
 
