@@ -98,6 +98,20 @@ def _write_remote_config(config, provider) -> str:
 
 def get_or_create_head_node(config: Dict[str, Any], no_restart: bool = False, restart_only: bool = False,
                             call_context: Optional[CallContext] = None) -> str:
+    from cloudtik_amd.core.event_system import CreateClusterEvent as Ev, global_event_system as events
+    ev = {"cluster_name": config["cluster_name"]}
+    events.execute_callback(Ev.up_started, ev)
+    try:
+        head = _get_or_create_head_node(config, no_restart, restart_only, call_context, events, ev)
+    except Exception as e:
+        events.execute_callback(Ev.cluster_booting_failed, dict(ev, error=str(e)))
+        raise
+    events.execute_callback(Ev.cluster_booting_completed, dict(ev, node_id=head))
+    return head
+
+
+def _get_or_create_head_node(config, no_restart, restart_only, call_context, events, ev) -> str:
+    from cloudtik_amd.core.event_system import CreateClusterEvent as Ev
     provider = _provider(config)
     head_type = config["head_node_type"]
     head = get_head_node(provider, config["cluster_name"])
@@ -108,6 +122,7 @@ def get_or_create_head_node(config: Dict[str, Any], no_restart: bool = False, re
         provider.terminate_node(head)
         head = None
     if head is None:
+        events.execute_callback(Ev.acquiring_new_head_node, ev)
         tags = node_tags(config, head_type, T.NODE_KIND_HEAD, T.CLOUDTIK_TAG_HEAD_NODE_SEQ_ID, provider)
         nt = config["available_node_types"][head_type]
         provider.create_node_with_resources(nt.get("node_config", {}), tags, 1, nt.get("resources", {}))
@@ -119,6 +134,7 @@ def get_or_create_head_node(config: Dict[str, Any], no_restart: bool = False, re
         if head is None:
             raise ClusterError("head node did not come up")
     head_ip = provider.internal_ip(head)
+    events.execute_callback(Ev.head_node_acquired, dict(ev, node_id=head, head_ip=head_ip))
     remote_cfg = _write_remote_config(config, provider)
     try:
         updater = create_updater(config, provider, head, is_head=True, head_ip=head_ip,
@@ -126,6 +142,10 @@ def get_or_create_head_node(config: Dict[str, Any], no_restart: bool = False, re
                                  file_mounts={BOOTSTRAP_CONFIG_REMOTE: remote_cfg}, call_context=call_context)
         if no_restart:
             updater.start_commands = []
+        stage_events = {"sync_files": Ev.ssh_control_acquired, "initialization": Ev.run_initialization_cmd,
+                        "setup": Ev.run_setup_cmd, "start": Ev.start_cloudtik_runtime}
+        updater.stage_callback = lambda st: st in stage_events and events.execute_callback(
+            stage_events[st], dict(ev, node_id=head))
         updater.run()
     finally:
         os.unlink(remote_cfg)
@@ -389,19 +409,22 @@ def submit_and_exec(config_file, script: str, script_args: Optional[List[str]] =
     runner = runner or RUNNERS.get(ext, "")
     args = " ".join(shlex.quote(a) for a in (script_args or []))
     cmd = f"cd {target_dir} && {runner} {remote} {args}".replace("  ", " ")
-    out = exec_cluster(config, cmd, node_ip=node_ip, with_output=with_output)
-    if job_waiter:
-        wait_for_job(config, job_waiter)
-    return out
-
-
-def wait_for_job(config, job_waiter_name: str, timeout: float = 3600):
-    for t in get_runtime_types(config):
-        rt = rf.get_runtime(t, config["runtime"].get(t, {}) or {})
-        w = rt.get_job_waiter(config)
-        if w is not None:
-            return w.wait_for_completion(job_waiter_name, timeout)
-    return None
+    if not job_waiter:
+        return exec_cluster(config, cmd, node_ip=node_ip, with_output=with_output)
+    # detached job in a named session, then wait for it with the requested waiter
+    from cloudtik_amd.core.job_waiter import create_job_waiter
+    session = f"cloudtik-job-{int(time.time() * 1000)}"
+    kind = job_waiter.split("+")[0]
+    if kind == "tmux":
+        launch = f"tmux new -d -s {session} {shlex.quote(cmd)}"
+    elif kind == "screen":
+        launch = f"screen -dmS {session} bash -c {shlex.quote(cmd)}"
+    else:
+        launch = (f"mkdir -p {target_dir} && nohup bash -c {shlex.quote(cmd)} > {target_dir}/{session}.log 2>&1 "
+                  f"& echo $! > {target_dir}/{session}.pid")
+    exec_cluster(config, launch, node_ip=node_ip)
+    create_job_waiter(config, job_waiter).wait_for_completion(n, cmd, session_name=session)
+    return session
 
 
 # ---------------------------------------------------------------------- scaling

@@ -103,8 +103,12 @@ class NodeUpdater:
     def _set_status(self, status: str):
         self.provider.set_node_tags(self.node_id, {T.CLOUDTIK_TAG_NODE_STATUS: status})
 
+    stage_callback = None       # optional fn(stage_name), e.g. cluster-creation events
+
     def _stage(self, name):
         self.stage_times[name] = time.time()
+        if self.stage_callback is not None:
+            self.stage_callback(name)
 
     # ------------------------------------------------------------------ stages
     def wait_ready(self, deadline: float):
