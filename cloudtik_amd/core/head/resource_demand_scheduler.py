@@ -121,15 +121,15 @@ class ResourceDemandScheduler:
                 bins += [self._resources(t) for _ in range(n)]
             return bins
 
-        # 2) explicit minimum cluster size: bundles against the TOTAL capacity of all nodes
-        demands = [dict(d) for d in resource_demands]
+        # 2) explicit minimum cluster size: bundles against the TOTAL capacity of all nodes;
+        # 3) pending demands against the FREE capacity -- two separate views of the same
+        #    nodes (a request is a floor on cluster size, a demand is unplaced load)
+        remaining = []
         if min_cluster_bundles:
             total_bins = [self._resources(t) for t, n in existing.items() for _ in range(n)]
             total_bins += capacity_bins(include_unused=False)
-            demands += bin_pack([dict(d) for d in min_cluster_bundles], total_bins)
-
-        # 3) demands onto free capacity, then greedy node additions
-        remaining = bin_pack(demands, capacity_bins())
+            remaining += bin_pack([dict(d) for d in min_cluster_bundles], total_bins)
+        remaining += bin_pack([dict(d) for d in resource_demands], capacity_bins())
         infeasible = []
         while remaining:
             best, best_score = None, None

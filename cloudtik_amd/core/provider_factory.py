@@ -35,6 +35,7 @@ _NODE_PROVIDERS = {
     "aliyun": _lazy("cloudtik_amd.providers.cloud.node_provider", "AliyunNodeProvider"),
     "huaweicloud": _lazy("cloudtik_amd.providers.cloud.node_provider", "HuaweiCloudNodeProvider"),
     "kubernetes": _lazy("cloudtik_amd.providers.kubernetes.node_provider", "KubernetesNodeProvider"),
+    "mock": _lazy("cloudtik_amd.providers.mock.node_provider", "MockProvider"),
     "external": None,
 }
 
@@ -63,6 +64,7 @@ _DATABASE_PROVIDERS = {k: _lazy("cloudtik_amd.providers.cloud.storage_provider",
 _PROVIDER_HOMES = {
     "local": "local", "onpremise": "onpremise", "virtual": "virtual", "aws": "aws", "gcp": "gcp",
     "azure": "azure", "aliyun": "aliyun", "huaweicloud": "huaweicloud", "kubernetes": "kubernetes",
+    "mock": "local",
 }
 
 

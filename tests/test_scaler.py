@@ -1,0 +1,178 @@
+"""Head scaler / resource demand scheduler with the mock provider (reference test strategy:
+tests/unit scaler tests over MockProvider + MockProcessRunner)."""
+import copy
+import json
+import socket
+import time
+
+import pytest
+
+from cloudtik_amd.core import tags as T
+from cloudtik_amd.core.head.resource_demand_scheduler import ResourceDemandScheduler, bin_pack
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+BASE = {
+    "provider": {"type": "mock"},
+    "available_node_types": {
+        "head.default": {"node_config": {"instance_type": "m.head"}, "resources": {"CPU": 8}},
+        "cpu.small": {"node_config": {"instance_type": "m.cpu"}, "resources": {"CPU": 4},
+                      "min_workers": 0, "max_workers": 10},
+        "gpu.mi355x": {"node_config": {"instance_type": "m.gpu"},
+                       "resources": {"CPU": 128, "GPU": 8, "accelerator_type:MI355X": 8},
+                       "min_workers": 0, "max_workers": 4},
+    },
+    "head_node_type": "head.default",
+    "max_workers": 12,
+    "runtime": {"types": ["ai"], "ai": {"with_gpu": True}},
+    "options": {"idle_timeout_minutes": 5},
+}
+
+
+@pytest.fixture
+def state(tmp_path):
+    from cloudtik_amd.core.state.state_client import StateClient, StateServer
+    srv = StateServer(port=_port(), data_dir=str(tmp_path)).start()
+    yield StateClient.create(srv.address)
+    srv.stop()
+
+
+def _setup(name, state, mutate=None):
+    from cloudtik_amd.core.cluster_config import bootstrap_config
+    from cloudtik_amd.core.head.scaler import ClusterScaler
+    from cloudtik_amd.core.provider_factory import get_node_provider
+    from cloudtik_amd.providers.mock.node_provider import MockProvider
+    MockProvider.reset(name)
+    cfg = copy.deepcopy(BASE)
+    cfg["cluster_name"] = name
+    if mutate:
+        mutate(cfg)
+    cfg = bootstrap_config(cfg, no_config_cache=True)
+    provider = get_node_provider(cfg["provider"], name, use_cache=False)
+    return cfg, provider, ClusterScaler(cfg, provider, state, head_ip="10.0.0.1", synchronous=True)
+
+
+def _workers(provider, name, status=None):
+    out = provider.non_terminated_nodes({T.CLOUDTIK_TAG_CLUSTER_NAME: name, T.CLOUDTIK_TAG_NODE_KIND: "worker"})
+    if status:
+        out = [n for n in out if provider.node_tags(n).get(T.CLOUDTIK_TAG_NODE_STATUS) == status]
+    return out
+
+
+def test_scheduler_bin_packing_and_gpu_conservation():
+    types = copy.deepcopy(BASE["available_node_types"])
+    s = ResourceDemandScheduler(types, 12, "head.default")
+    launch, infeasible = s.get_nodes_to_launch({}, {}, [{"CPU": 2}] * 5, {})
+    assert launch == {"cpu.small": 3}               # CPU demands never pick the 8-GPU node
+    launch, _ = s.get_nodes_to_launch({}, {}, [{"GPU": 8}] * 2 + [{"CPU": 1}], {})
+    assert launch == {"gpu.mi355x": 2}              # the CPU bundle fits on a GPU node's spare CPUs
+    launch, infeasible = s.get_nodes_to_launch({}, {}, [{"GPU": 16}], {})
+    assert launch == {} and infeasible == [{"GPU": 16}]
+    # free capacity of running nodes is used first
+    launch, _ = s.get_nodes_to_launch({"cpu.small": 1}, {}, [{"CPU": 4}], {"n1": {"CPU": 4}})
+    assert launch == {}
+    # per-type max
+    launch, _ = s.get_nodes_to_launch({"gpu.mi355x": 4}, {}, [{"GPU": 8}], {})
+    assert launch == {}
+    assert bin_pack([{"CPU": 3}, {"CPU": 2}], [{"CPU": 4}, {"CPU": 1}]) == [{"CPU": 2}]
+
+
+def test_min_workers_launched_and_set_up(state):
+    name = "sc-min"
+    cfg, provider, scaler = _setup(name, state, lambda c: c["available_node_types"]["cpu.small"].update(min_workers=2))
+    scaler.update()
+    ws = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    assert len(ws) == 2
+    cmds = provider.runner.commands_for(ws[0])
+    assert any("runtime install ai" in c for c in cmds)
+    assert any("node start --node-ip" in c and "--address=" in c for c in cmds)
+    st = json.loads(state.kv_get(b"scaling_status", namespace="scaling"))
+    assert st["workers"] == 2
+    scaler.update()                                   # steady state: nothing new
+    assert len(_workers(provider, name)) == 2
+
+
+def test_max_workers_and_outdated_config(state):
+    name = "sc-max"
+    cfg, provider, scaler = _setup(name, state, lambda c: c["available_node_types"]["cpu.small"].update(
+        min_workers=1, max_workers=2))
+    scaler.update()
+    from cloudtik_amd.core.cluster_utils import node_tags
+    provider.create_node({"instance_type": "m.cpu"}, node_tags(cfg, "cpu.small", "worker", 7), 2)
+    scaler.update()
+    assert len(_workers(provider, name)) == 2
+    # change the node config: every worker is replaced
+    old = set(_workers(provider, name))
+    new_cfg = copy.deepcopy(cfg)
+    new_cfg["available_node_types"]["cpu.small"]["node_config"]["instance_type"] = "m.cpu2"
+    scaler.reset_config(new_cfg)
+    scaler.update()
+    now = set(_workers(provider, name))
+    assert now and not (now & old)
+
+
+def test_failed_setup_is_replaced(state):
+    name = "sc-fail"
+    cfg, provider, scaler = _setup(name, state, lambda c: c["available_node_types"]["cpu.small"].update(min_workers=1))
+    provider.runner.fail_cmds.append("runtime install ai")
+    scaler.update()
+    (n,) = _workers(provider, name)
+    assert provider.node_tags(n)[T.CLOUDTIK_TAG_NODE_STATUS] == T.STATUS_UPDATE_FAILED
+    provider.runner.fail_cmds.clear()
+    scaler.update()                                   # terminate the failed node + launch a new one
+    ws = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    assert len(ws) == 1 and ws[0] != n
+
+
+def test_gpu_request_and_launch_failure_backoff(state):
+    name = "sc-gpu"
+    cfg, provider, scaler = _setup(name, state)
+    state.kv_put(b"cluster_requests", json.dumps({"bundles": [{"GPU": 8}] * 2}), namespace="scaling")
+    provider.fail_launches_of("m.gpu")
+    scaler.update()
+    st = scaler.summary()
+    assert "gpu.mi355x" in st["failed_launches"] and not _workers(provider, name)
+    provider.world["fail_launch"].clear()
+    scaler.tracker.failures.clear()
+    scaler.update()
+    ws = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    assert len(ws) == 2 and all(provider.node_tags(w)[T.CLOUDTIK_TAG_USER_NODE_TYPE] == "gpu.mi355x" for w in ws)
+
+
+def test_lost_heartbeat_triggers_recovery(state, monkeypatch):
+    from cloudtik_amd.core import constants as C
+    from cloudtik_amd.core.state.state_client import NODE_TABLE
+    name = "sc-hb"
+    cfg, provider, scaler = _setup(name, state, lambda c: c["available_node_types"]["cpu.small"].update(min_workers=1))
+    scaler.update()
+    (n,) = _workers(provider, name)
+    monkeypatch.setattr(C, "CLOUDTIK_HEARTBEAT_TIMEOUT_S", 1)
+    provider.set_node_tags(n, {"cloudtik-up-time": str(time.time() - 100)})
+    state.table_put(NODE_TABLE, n, {"node_id": n, "node_ip": provider.internal_ip(n),
+                                    "last_heartbeat_time": time.time() - 100})
+    before = len(provider.runner.commands_for(n))
+    scaler.update()
+    after = provider.runner.commands_for(n)
+    assert len(after) > before and any("node start" in c for c in after[before:])
+    assert any("lost heartbeat" in e for e in scaler.events)
+
+
+def test_idle_workers_scale_down_to_min(state):
+    name = "sc-idle"
+    cfg, provider, scaler = _setup(name, state, lambda c: (c["available_node_types"]["cpu.small"].update(
+        min_workers=1), c["options"].update(idle_timeout_minutes=0.001)))
+    state.kv_put(b"cluster_requests", json.dumps({"bundles": [{"CPU": 4}] * 3}), namespace="scaling")
+    scaler.update()
+    assert len(_workers(provider, name)) == 3
+    state.kv_put(b"cluster_requests", json.dumps({"bundles": []}), namespace="scaling")
+    scaler.update()                                   # records activity
+    time.sleep(0.2)
+    scaler.update()
+    assert len(_workers(provider, name)) == 1
