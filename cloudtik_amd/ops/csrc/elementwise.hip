@@ -21,20 +21,36 @@ __device__ __forceinline__ float act_g(float x, int act) {
 }
 
 // y[m, n] = act(z[m, n] + bias[n]); rows x N, N % 8 == 0.
+// 2-D mapping: blockIdx.x / threadIdx.x&63 pick a column vector (its bias lives in
+// registers), the 4 waves of the block and blockIdx.y stride over rows, 4 rows per step
+// so four independent 16-byte loads are in flight per lane (no 64-bit modulo per element).
+constexpr int kBaRows = 4;
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ z,
                                                            const bf16_t* __restrict__ bias,
-                                                           bf16_t* __restrict__ y, long total_vec,
+                                                           bf16_t* __restrict__ y, long M,
                                                            int nvec_row, int act) {
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
-       v += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(v % nvec_row);
-    const u16x8 zv = reinterpret_cast<const u16x8*>(z)[v];
-    u16x8 bv = u16x8(0);
-    if (bias) bv = reinterpret_cast<const u16x8*>(bias)[c];
-    u16x8 o;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (c >= nvec_row) return;
+  u16x8 bv = u16x8(0);
+  if (bias) bv = reinterpret_cast<const u16x8*>(bias)[c];
+  float b[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(act_f(bf2f(zv[j]) + bf2f(bv[j]), act));
-    reinterpret_cast<u16x8*>(y)[v] = o;
+  for (int j = 0; j < 8; ++j) b[j] = bf2f(bv[j]);
+  const long rstride = (long)gridDim.y * 4 * kBaRows;
+  const u16x8* zr = reinterpret_cast<const u16x8*>(z);
+  u16x8* yr = reinterpret_cast<u16x8*>(y);
+  for (long r0 = ((long)blockIdx.y * 4 + (threadIdx.x >> 6)) * kBaRows; r0 < M; r0 += rstride) {
+    u16x8 zv[kBaRows];
+#pragma unroll
+    for (int k = 0; k < kBaRows; ++k) zv[k] = (r0 + k < M) ? zr[(r0 + k) * nvec_row + c] : u16x8(0);
+#pragma unroll
+    for (int k = 0; k < kBaRows; ++k) {
+      if (r0 + k >= M) break;
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(act_f(bf2f(zv[k][j]) + b[j], act));
+      yr[(r0 + k) * nvec_row + c] = o;
+    }
   }
 }
 
@@ -163,9 +179,15 @@ using namespace ct;
 extern "C" int ct_bias_act_fwd(const void* z, const void* bias, void* y, long M, int N, int act,
                                hipStream_t stream) {
   if (N % 8) return -1;
-  const long tv = M * (N / 8);
-  bias_act_fwd_kernel<<<grid_for(tv), 256, 0, stream>>>((const bf16_t*)z, (const bf16_t*)bias,
-                                                         (bf16_t*)y, tv, N / 8, act);
+  const int nvec = N / 8;
+  const int gx = (nvec + 63) / 64;
+  // enough row blocks for ~8 waves per SIMD over 256 CUs, each wave 4 rows per step
+  long gy = (M + 4 * kBaRows - 1) / (4 * kBaRows);
+  const long want = (8L * 1024 + gx - 1) / gx;
+  if (gy > want) gy = want;
+  if (gy < 1) gy = 1;
+  bias_act_fwd_kernel<<<dim3(gx, (unsigned)gy), 256, 0, stream>>>((const bf16_t*)z, (const bf16_t*)bias,
+                                                                 (bf16_t*)y, M, nvec, act);
   return 0;
 }
 

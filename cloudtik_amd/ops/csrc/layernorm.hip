@@ -110,49 +110,69 @@ struct LnBwdArgs {
   int M, N; uint32_t thresh; float scale; uint64_t seed, offset;
 };
 
-template <int MAXV, bool RMS>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
+template <int MAXV, bool RMS, bool EXTRA>
+__global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
   const int N = a.N, nvec = N >> 3;
   const bool drop = a.thresh != 0;
   const bool want_dbias = a.dbias_part != nullptr;
-  float dg[MAXV][8], db[MAXV][8], dbi[MAXV][8], g[MAXV][8];
+  float dg[MAXV][8], db[MAXV][8], dbi[MAXV][8];
+  u16x8 gb[MAXV];                    // gamma kept packed (bf16): 4 VGPRs per 8 columns
   const u16x8* g8 = reinterpret_cast<const u16x8*>(a.gamma);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int c = lane + i * 64;
-    const u16x8 gv = c < nvec ? g8[c] : u16x8(0);
+    gb[i] = c < nvec ? g8[c] : u16x8(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; g[i][j] = bf2f(gv[j]); }
+    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; }
   }
-  for (int row = blockIdx.x * wpb + wid; row < a.M; row += gridDim.x * wpb) {
-    const u16x8* sr = reinterpret_cast<const u16x8*>(a.s + (size_t)row * N);
-    const u16x8* dyr = reinterpret_cast<const u16x8*>(a.dy + (size_t)row * N);
-    const float mean = RMS ? 0.f : a.mean[row];
-    const float rstd = a.rstd[row];
-    float xh[MAXV][8], dyg[MAXV][8];
+  // Software pipeline: the s / dy / dextra rows (and mean, rstd) of the NEXT row are in
+  // flight while this row's reductions and stores run -- the kernel is latency bound with
+  // one row per wave otherwise (measured 3.9 TB/s effective on MI355X before this change).
+  const int stride = gridDim.x * wpb;
+  int row = blockIdx.x * wpb + wid;
+  u16x8 nsv[MAXV], ndv[MAXV], nev[MAXV];
+  float nmean = 0.f, nrstd = 0.f;
+  auto prefetch = [&](int r) {
+    if (r >= a.M) return;
+    const u16x8* sr = reinterpret_cast<const u16x8*>(a.s + (size_t)r * N);
+    const u16x8* dyr = reinterpret_cast<const u16x8*>(a.dy + (size_t)r * N);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int c = lane + i * 64;
+      nsv[i] = c < nvec ? sr[c] : u16x8(0);
+      ndv[i] = c < nvec ? dyr[c] : u16x8(0);
+      if (EXTRA) nev[i] = c < nvec ? reinterpret_cast<const u16x8*>(a.dextra + (size_t)r * N)[c] : u16x8(0);
+    }
+    nmean = RMS ? 0.f : a.mean[r];
+    nrstd = a.rstd[r];
+  };
+  prefetch(row);
+  for (; row < a.M; row += stride) {
+    u16x8 csv[MAXV], cdv[MAXV], cev[MAXV];
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) { csv[i] = nsv[i]; cdv[i] = ndv[i]; if (EXTRA) cev[i] = nev[i]; }
+    const float mean = nmean, rstd = nrstd;
+    prefetch(row + stride);
+    // pass 1: row sums; xhat and dy*gamma are recomputed in pass 2 from the raw bf16
+    // registers instead of being kept live (keeps the kernel at 3 waves / SIMD)
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int c = lane + i * 64;
       if (c < nvec) {
-        const u16x8 sv = sr[c], dv = dyr[c];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float xhat = (bf2f(sv[j]) - mean) * rstd;
-          const float d = bf2f(dv[j]);
-          xh[i][j] = xhat;
-          dyg[i][j] = d * g[i][j];
+          const float xhat = (bf2f(csv[i][j]) - mean) * rstd;
+          const float d = bf2f(cdv[i][j]);
+          const float dgv = d * bf2f(gb[i][j]);
           dg[i][j] += d * xhat;
           db[i][j] += d;
-          s1 += dyg[i][j];
-          s2 += dyg[i][j] * xhat;
+          s1 += dgv;
+          s2 += dgv * xhat;
         }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { xh[i][j] = 0.f; dyg[i][j] = 0.f; }
       }
     }
     s1 = wave_sum(s1) / N;
@@ -161,14 +181,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
     for (int i = 0; i < MAXV; ++i) {
       const int c = lane + i * 64;
       if (c < nvec) {
-        u16x8 ev = u16x8(0);
-        if (a.dextra) ev = reinterpret_cast<const u16x8*>(a.dextra + (size_t)row * N)[c];
+        const u16x8 ev = EXTRA ? cev[i] : u16x8(0);
         uint32_t keep = 0xFFu;
         if (drop) keep = dropout_bits8(a.seed, a.offset, (uint64_t)row * nvec + c, a.thresh);
         u16x8 o, od;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float t = RMS ? rstd * (dyg[i][j] - xh[i][j] * s2) : rstd * (dyg[i][j] - s1 - xh[i][j] * s2);
+          const float xhat = (bf2f(csv[i][j]) - mean) * rstd;
+          const float dgv = bf2f(cdv[i][j]) * bf2f(gb[i][j]);
+          float t = RMS ? rstd * (dgv - xhat * s2) : rstd * (dgv - s1 - xhat * s2);
           t += bf2f(ev[j]);
           o[j] = f2bf(t);
           float tx = drop ? (((keep >> j) & 1u) ? t * a.scale : 0.f) : t;
@@ -275,8 +296,9 @@ extern "C" int ct_layernorm_fwd(const void* x, const void* bias, const void* res
 }
 
 extern "C" int ct_layernorm_bwd_grid(int M) {
+  // 768 blocks x 4 waves = 3 waves per SIMD on 256 CUs (the kernel's VGPR budget allows 3)
   const int grid = ceil_div(M, 4);
-  return grid > 512 ? 512 : grid;
+  return grid > 768 ? 768 : grid;
 }
 
 // Workspace: part = float[3 * grid * N] (grid = ct_layernorm_bwd_grid(M)).
@@ -297,8 +319,12 @@ extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, co
   a.scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed; a.offset = offset;
   const int mv = (N / 8 + 63) / 64;
-#define CT_LNB(MV) case MV: if (rms) ln_bwd_kernel<MV, true><<<grid, 256, 0, stream>>>(a); \
-                            else ln_bwd_kernel<MV, false><<<grid, 256, 0, stream>>>(a); break;
+#define CT_LNB(MV) case MV:                                                                  \
+    if (rms) { if (a.dextra) ln_bwd_kernel<MV, true, true><<<grid, 256, 0, stream>>>(a);          \
+               else ln_bwd_kernel<MV, true, false><<<grid, 256, 0, stream>>>(a); }                  \
+    else { if (a.dextra) ln_bwd_kernel<MV, false, true><<<grid, 256, 0, stream>>>(a);             \
+           else ln_bwd_kernel<MV, false, false><<<grid, 256, 0, stream>>>(a); }                     \
+    break;
   switch (mv) {
     CT_LNB(1) CT_LNB(2) CT_LNB(3) CT_LNB(4)
     default: return -1;
