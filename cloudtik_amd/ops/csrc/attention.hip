@@ -240,30 +240,10 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   }
 }
 
-// delta[bh, q] = sum_d O[q,d] * dO[q,d]   (one thread per (b, q, h) row of 64)
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, long o_sb,
-                                                         long o_ss, long o_sh, const bf16_t* __restrict__ dO,
-                                                         long d_sb, long d_ss, long d_sh,
-                                                         float* __restrict__ delta, int B, int H, int Sq) {
-  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (t >= (long)B * H * Sq) return;
-  const int q = t % Sq;
-  const int bh = t / Sq;
-  const int b = bh / H, h = bh % H;
-  const u16x8* op = reinterpret_cast<const u16x8*>(o + b * o_sb + h * o_sh + (long)q * o_ss);
-  const u16x8* dp = reinterpret_cast<const u16x8*>(dO + b * d_sb + h * d_sh + (long)q * d_ss);
-  float acc = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const u16x8 x = op[c], y = dp[c];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += bf2f(x[j]) * bf2f(y[j]);
-  }
-  delta[t] = acc;
-}
 
 struct AttnBwdArgs {
-  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dO;
+  const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dO; const bf16_t* o;
+  long o_sb, o_ss, o_sh;
   bf16_t* dq; bf16_t* dk; bf16_t* dv; float* dq_acc;
   long q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, do_sb, do_ss, do_sh;
   long dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
@@ -322,6 +302,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
 
   const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* dobase = a.dO + b * a.do_sb + h * a.do_sh;
+  const bf16_t* obase = a.o + b * a.o_sb + h * a.o_sh;
   const int trow = (lane >> 2) & 3;
   const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
   const int nq = (a.Sq + 31) / 32;
@@ -332,25 +313,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   // tile's MFMAs, written to LDS after the mid barrier): 2 barriers per q-tile, and the
   // global-load latency of tile t+1 hides under the compute of tile t.
   const int prow = tid >> 3, pch = tid & 7;
-  u16x8 pQ, pdO;
-  float pL = INFINITY, pD = 0.f;
+  // delta = rowsum(dO * O) is computed here (no separate kernel): each thread prefetches
+  // the O chunk matching its dO chunk; the 8 threads of a row reduce at staging time
+  u16x8 pQ, pdO, pO;
+  float pL = INFINITY;
 #define BWD_PREFETCH(qb_)                                                                   \
   {                                                                                         \
     const int q_ = (qb_) + prow;                                                            \
     const bool ok_ = q_ < a.Sq;                                                             \
     pQ = ok_ ? *reinterpret_cast<const u16x8*>(qbase + (long)q_ * a.q_ss + pch * 8) : u16x8(0); \
     pdO = ok_ ? *reinterpret_cast<const u16x8*>(dobase + (long)q_ * a.do_ss + pch * 8) : u16x8(0); \
+    pO = ok_ ? *reinterpret_cast<const u16x8*>(obase + (long)q_ * a.o_ss + pch * 8) : u16x8(0); \
     if (tid < 32) {                                                                         \
       const bool ok2_ = (qb_) + tid < a.Sq;                                                 \
       pL = ok2_ ? a.lse[(long)bh * a.Sq + (qb_) + tid] : INFINITY;                          \
-      pD = ok2_ ? a.delta[(long)bh * a.Sq + (qb_) + tid] : 0.f;                             \
     }                                                                                       \
   }
 #define BWD_STAGE()                                                                         \
   {                                                                                         \
     *reinterpret_cast<u16x8*>(Qs + swz(prow, pch)) = pQ;                                    \
     *reinterpret_cast<u16x8*>(dOs + swz(prow, pch)) = pdO;                                  \
-    if (tid < 32) { lse_s[tid] = pL; delta_s[tid] = pD; }                                   \
+    if (tid < 32) lse_s[tid] = pL;                                                          \
+    float dd_ = 0.f;                                                                        \
+    _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) dd_ += bf2f(pdO[j_]) * bf2f(pO[j_]);  \
+    dd_ += __shfl_xor(dd_, 1, 64);                                                          \
+    dd_ += __shfl_xor(dd_, 2, 64);                                                          \
+    dd_ += __shfl_xor(dd_, 4, 64);                                                          \
+    if (pch == 0) delta_s[prow] = dd_;                                                      \
   }
   BWD_PREFETCH(0);
   BWD_STAGE();
@@ -566,10 +555,9 @@ extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const l
   if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return -1;
   if (p_drop > 0.f && (Sk % 2)) return -2;
   const long rows = (long)B * H * Sq;
-  attn_delta_kernel<<<(int)((rows + 255) / 256), 256, 0, stream>>>(
-      (const bf16_t*)o, os[0], os[1], os[2], (const bf16_t*)dO, dos[0], dos[1], dos[2], delta, B, H, Sq);
   AttnBwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.dO = (const bf16_t*)dO;
+  a.o = (const bf16_t*)o; a.o_sb = os[0]; a.o_ss = os[1]; a.o_sh = os[2];
   a.dq = (bf16_t*)dq; a.dk = (bf16_t*)dk; a.dv = (bf16_t*)dv; a.dq_acc = dq_acc;
   a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
   a.k_sb = ks[0]; a.k_ss = ks[1]; a.k_sh = ks[2];
