@@ -111,6 +111,11 @@ class ClusterScaler:
         self.num_failures = 0
         self.events: List[str] = []
         self.last_update_time = None
+        from cloudtik_amd.core.head.quorum_manager import QuorumManager
+        from cloudtik_amd.core.head.scaling_policies import create_scaling_policy
+        self.quorum = QuorumManager(config, provider)
+        self.policy = create_scaling_policy(config, self.head_ip, metrics_source=self.node_metrics)
+        self.policy_requests: List[Dict[str, float]] = []
 
     # ------------------------------------------------------------------ inputs
     def _head_ip(self) -> Optional[str]:
@@ -131,8 +136,10 @@ class ClusterScaler:
         return list(self._kv_json(KEY_RESOURCE_DEMANDS) or [])
 
     def cluster_requests(self) -> List[Dict[str, float]]:
+        """`cloudtik scale` requests, raised to what the scaling policy asks for."""
         r = self._kv_json(KEY_CLUSTER_REQUESTS) or {}
-        return list(r.get("bundles", []))
+        user = list(r.get("bundles", []))
+        return user if len(user) >= len(self.policy_requests) else list(self.policy_requests)
 
     def heartbeats(self) -> Dict[str, Dict]:
         if self.state is None:
@@ -153,6 +160,9 @@ class ClusterScaler:
         self.scheduler.reset_config(config["available_node_types"], config.get("max_workers", 0),
                                     config["head_node_type"], opts.get("upscaling_speed", 1.0))
         self.idle_timeout_s = 60.0 * float(opts.get("idle_timeout_minutes", 5))
+        self.quorum.reset(config)
+        if self.policy is not None:
+            self.policy.reset(config)
 
     def update(self):
         try:
@@ -171,6 +181,9 @@ class ClusterScaler:
                 self.reset_config(new)
         now = time.time()
         self.last_update_time = now
+        if self.policy is not None:
+            st = self.policy.get_scaling_state()
+            self.policy_requests = list(((st.autoscaling_instructions or {}) if st else {}).get("resource_requests", []))
         workers = self.workers()
         tags = {n: self.provider.node_tags(n) for n in workers}
         types = self.config["available_node_types"]
@@ -223,8 +236,11 @@ class ClusterScaler:
             self._launch(nt, cnt)
         self.infeasible = infeasible
 
-        # 5) updates + recovery
+        # 5) updates + recovery (quorum runtimes: set up only a complete initial membership)
         workers = self.workers()
+        may_update = set(self.quorum.updatable(
+            [n for n in workers if self.provider.node_tags(n).get(T.CLOUDTIK_TAG_NODE_STATUS) == T.STATUS_UNINITIALIZED
+             or self.provider.node_tags(n).get(T.CLOUDTIK_TAG_QUORUM_ID)]))
         for n in workers:
             t = self.provider.node_tags(n)
             status = t.get(T.CLOUDTIK_TAG_NODE_STATUS)
@@ -233,11 +249,13 @@ class ClusterScaler:
                 self.updaters.pop(n)
                 if u.exitcode != 0:
                     self.failed_updates[n] += 1
+                self.quorum.on_update_done(n, u.exitcode == 0)
                 continue
             if u is not None:
                 continue
             if status == T.STATUS_UNINITIALIZED:
-                self._spawn_updater(n, recovery=False)
+                if n in may_update:
+                    self._spawn_updater(n, recovery=False)
             elif status == T.STATUS_UP_TO_DATE and self.state is not None:
                 beat = hb.get(n) or hb.get(self.provider.internal_ip(n) or "")
                 last = (beat or {}).get("last_heartbeat_time")
@@ -303,6 +321,7 @@ class ClusterScaler:
             self.updaters.pop(node_id)
             if u.exitcode != 0:
                 self.failed_updates[node_id] += 1
+            self.quorum.on_update_done(node_id, u.exitcode == 0)
         else:
             u.start()
 

@@ -1,0 +1,207 @@
+"""Built-in scaling policies (reference core/_private/cluster/scaling_policies.py:43-724,
+resource_scaling_policy.py; runtime-provided policies via ``Runtime.get_scaling_policy``).
+
+A policy turns node metrics into resource *requests* the scaler packs against the cluster
+(plus per-node resource states):
+
+* ``scaling-with-resources``: reports node resource usage, requests nothing;
+* ``scaling-with-load``: when the cluster's CPU load (load-avg / cores), memory use or --
+  MI355X addition -- average GPU busy %% stays above its threshold, request
+  ``scaling_step`` more worker nodes' worth of resources;
+* ``scaling-with-time``: a daily / weekly / monthly table of worker counts
+  (``"09:00": 4``, ``"Mon 18:00": "+2"``, ``"20:00": "*0.5"``) relative to min_workers or the
+  previous entry.
+
+Configured under ``runtime.scaling`` (``scaling_policy: scaling-with-load`` ...).
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Any, Dict, List, Optional
+
+from cloudtik_amd.core.provider_api import ScalingPolicy, ScalingState
+
+SCALING_WITH_RESOURCES = "scaling-with-resources"
+SCALING_WITH_LOAD = "scaling-with-load"
+SCALING_WITH_TIME = "scaling-with-time"
+
+WEEKDAYS = ["mon", "tue", "wed", "thu", "fri", "sat", "sun"]
+
+
+def _worker_type(config) -> Optional[str]:
+    types = [t for t in config.get("available_node_types", {}) if t != config.get("head_node_type")]
+    return types[0] if types else None
+
+
+def _node_bundle(config, node_type) -> Dict[str, float]:
+    res = config["available_node_types"].get(node_type, {}).get("resources") or {}
+    return {k: float(v) for k, v in res.items() if isinstance(v, (int, float)) and k in ("CPU", "GPU", "memory")}
+
+
+class ScalingWithResources(ScalingPolicy):
+    def __init__(self, config: Dict[str, Any], head_ip: str, metrics_source=None):
+        super().__init__(config, head_ip)
+        self.metrics_source = metrics_source        # callable -> {node_id: metrics row}
+        self.reset(config)
+
+    def name(self) -> str:
+        return SCALING_WITH_RESOURCES
+
+    def reset(self, config):
+        self.config = config
+        self.scaling_config = (config.get("runtime", {}).get("scaling") or {})
+
+    def _metrics(self) -> Dict[str, Dict[str, Any]]:
+        return self.metrics_source() if self.metrics_source else {}
+
+    def node_resource_states(self, metrics) -> Dict[str, Dict[str, Any]]:
+        out = {}
+        for nid, m in metrics.items():
+            total = dict(m.get("resources") or {})
+            cpus = float(m.get("cpu_count") or total.get("CPU", 0) or 0)
+            used_cpu = min(cpus, float((m.get("load_avg") or [0])[0]))
+            used_gpu = round(len(m.get("gpus") or []) * float(m.get("gpu_busy_percent_avg") or 0) / 100.0, 2)
+            out[nid] = {"total": total, "used": {"CPU": used_cpu, "GPU": used_gpu,
+                                                   "memory": float(m.get("memory_used") or 0)}}
+        return out
+
+    def requests(self, metrics) -> List[Dict[str, float]]:
+        return []
+
+    def get_scaling_state(self) -> Optional[ScalingState]:
+        metrics = self._metrics()
+        return ScalingState(autoscaling_instructions={"resource_requests": self.requests(metrics),
+                                                      "time": time.time()},
+                            node_resource_states=self.node_resource_states(metrics))
+
+
+class ScalingWithLoad(ScalingWithResources):
+    def name(self) -> str:
+        return SCALING_WITH_LOAD
+
+    def reset(self, config):
+        super().reset(config)
+        c = self.scaling_config
+        self.scaling_step = int(c.get("scaling_step", 1))
+        self.scaling_resource = c.get("scaling_resource", "CPU")
+        self.cpu_threshold = float(c.get("cpu_load_threshold", 0.85))
+        self.memory_threshold = float(c.get("memory_load_threshold", 0.85))
+        self.gpu_threshold = float(c.get("gpu_busy_threshold", 0.85))
+
+    def _utilisation(self, metrics):
+        cpus = sum(float(m.get("cpu_count") or 0) for m in metrics.values())
+        load = sum(float((m.get("load_avg") or [0])[0]) for m in metrics.values())
+        mem_t = sum(float(m.get("memory_total") or 0) for m in metrics.values())
+        mem_u = sum(float(m.get("memory_used") or 0) for m in metrics.values())
+        gpus = [g for m in metrics.values() for g in (m.get("gpus") or [])]
+        gpu_busy = (sum(float(g.get("busy_percent") or 0) for g in gpus) / (100.0 * len(gpus))) if gpus else 0.0
+        return {"cpu": load / cpus if cpus else 0.0, "memory": mem_u / mem_t if mem_t else 0.0, "gpu": gpu_busy,
+                "nodes": len(metrics)}
+
+    def requests(self, metrics) -> List[Dict[str, float]]:
+        if not metrics:
+            return []
+        u = self._utilisation(metrics)
+        res = self.scaling_resource.upper()
+        hot = (res == "CPU" and u["cpu"] > self.cpu_threshold) or \
+              (res == "MEMORY" and u["memory"] > self.memory_threshold) or \
+              (res == "GPU" and u["gpu"] > self.gpu_threshold)
+        if not hot:
+            return []
+        wt = _worker_type(self.config)
+        if wt is None:
+            return []
+        bundle = _node_bundle(self.config, wt)
+        # keep what runs now and add `scaling_step` nodes' worth
+        return [dict(bundle) for _ in range(max(0, u["nodes"] - 1) + self.scaling_step)]
+
+
+class ScalingWithTime(ScalingWithResources):
+    def name(self) -> str:
+        return SCALING_WITH_TIME
+
+    def reset(self, config):
+        super().reset(config)
+        c = self.scaling_config
+        self.periodic = c.get("scaling_periodic", "daily")
+        self.math_base = c.get("scaling_math_base", "on-min-workers")
+        self.table = self._expand(c.get("scaling_time_table", {}) or {})
+
+    def _seconds(self, spec: str) -> int:
+        parts = spec.strip().split()
+        day = 0
+        if self.periodic == "weekly" and len(parts) == 2:
+            day = WEEKDAYS.index(parts[0][:3].lower())
+        elif self.periodic == "monthly" and len(parts) == 2:
+            day = int(parts[0]) - 1
+        hh, mm = (parts[-1].split(":") + ["0"])[:2]
+        return day * 86400 + int(hh) * 3600 + int(mm) * 60
+
+    def _period(self) -> int:
+        return {"daily": 86400, "weekly": 7 * 86400, "monthly": 31 * 86400}[self.periodic]
+
+    def _min_workers(self) -> int:
+        wt = _worker_type(self.config)
+        return int(self.config["available_node_types"].get(wt, {}).get("min_workers", 0)) if wt else 0
+
+    def _expand(self, table: Dict[str, Any]) -> List:
+        entries = sorted((self._seconds(k), v) for k, v in table.items())
+        out, prev = [], self._min_workers()
+        for sec, spec in entries:
+            base = self._min_workers() if self.math_base == "on-min-workers" else prev
+            s = str(spec).strip()
+            if s.startswith(("+", "-")):
+                n = base + int(float(s))
+            elif s.startswith("*"):
+                n = int(math.ceil(base * float(s[1:])))
+            else:
+                n = int(float(s))
+            n = max(0, n)
+            out.append((sec, n))
+            prev = n
+        return out
+
+    def nodes_at(self, t: Optional[float] = None) -> Optional[int]:
+        if not self.table:
+            return None
+        lt = time.localtime(t if t is not None else time.time())
+        if self.periodic == "weekly":
+            now = lt.tm_wday * 86400
+        elif self.periodic == "monthly":
+            now = (lt.tm_mday - 1) * 86400
+        else:
+            now = 0
+        now += lt.tm_hour * 3600 + lt.tm_min * 60 + lt.tm_sec
+        current = self.table[-1][1]                 # wraps from the previous period
+        for sec, n in self.table:
+            if sec <= now:
+                current = n
+        return current
+
+    def requests(self, metrics) -> List[Dict[str, float]]:
+        n = self.nodes_at()
+        wt = _worker_type(self.config)
+        if n is None or wt is None:
+            return []
+        return [_node_bundle(self.config, wt) for _ in range(n)]
+
+
+POLICIES = {SCALING_WITH_RESOURCES: ScalingWithResources, SCALING_WITH_LOAD: ScalingWithLoad,
+            SCALING_WITH_TIME: ScalingWithTime}
+
+
+def create_scaling_policy(config: Dict[str, Any], head_ip: str, metrics_source=None) -> Optional[ScalingPolicy]:
+    """Runtime-provided policy first (e.g. YARN pending containers), then the built-ins."""
+    from cloudtik_amd.core import runtime_factory as rf
+    from cloudtik_amd.core.cluster_config import get_runtime_types
+    for t in get_runtime_types(config):
+        p = rf.get_runtime(t, config.get("runtime", {}).get(t, {}) or {}).get_scaling_policy(config, head_ip)
+        if p is not None:
+            return p
+    name = (config.get("runtime", {}).get("scaling") or {}).get("scaling_policy")
+    if not name:
+        return None
+    if name not in POLICIES:
+        raise ValueError(f"unknown scaling policy {name!r} (choices: {sorted(POLICIES)})")
+    return POLICIES[name](config, head_ip, metrics_source)

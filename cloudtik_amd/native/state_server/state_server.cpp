@@ -553,6 +553,24 @@ void cmd(Client& c, std::vector<std::string>& a) {
     w_int(c, cur);
     return;
   }
+  // ---- lock primitives (atomic: the server is single-threaded)
+  // DELIFEQ key token          -> 1 if key held token and was deleted (lock release)
+  // PEXPIREIFEQ key token ms   -> 1 if key holds token and its TTL was reset (lease renewal)
+  if (op == "DELIFEQ" || op == "PEXPIREIFEQ") {
+    if (!arity(op == "DELIFEQ" ? 3 : 4, op == "DELIFEQ" ? 3 : 4)) return;
+    Value* v = lookup(a[1]);
+    if (!v || v->type != VT::STR || v->str != a[2]) { w_int(c, 0); return; }
+    if (op == "DELIFEQ") {
+      g_db.erase(a[1]);
+    } else {
+      long long ms;
+      if (!parse_ll(a[3], ms)) { w_err(c, "value is not an integer"); return; }
+      v->expire_ms = now_ms() + ms;
+    }
+    ++g_dirty;
+    w_int(c, 1);
+    return;
+  }
   // ---- pub/sub
   if (op == "PUBLISH") {
     if (!arity(3, 3)) return;

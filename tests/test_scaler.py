@@ -176,3 +176,64 @@ def test_idle_workers_scale_down_to_min(state):
     time.sleep(0.2)
     scaler.update()
     assert len(_workers(provider, name)) == 1
+
+
+def test_scaling_with_load_requests_more_nodes():
+    from cloudtik_amd.core.head.scaling_policies import ScalingWithLoad, create_scaling_policy
+    cfg = copy.deepcopy(BASE)
+    cfg["runtime"]["scaling"] = {"scaling_policy": "scaling-with-load", "scaling_step": 2}
+    metrics = {"n1": {"cpu_count": 4, "load_avg": [3.9], "memory_total": 10, "memory_used": 1, "gpus": []},
+               "n2": {"cpu_count": 4, "load_avg": [3.8], "memory_total": 10, "memory_used": 1, "gpus": []}}
+    p = create_scaling_policy(cfg, "10.0.0.1", metrics_source=lambda: metrics)
+    assert isinstance(p, ScalingWithLoad)
+    st = p.get_scaling_state()
+    assert len(st.autoscaling_instructions["resource_requests"]) == 1 + 2
+    assert st.node_resource_states["n1"]["used"]["CPU"] == 3.9
+    metrics["n1"]["load_avg"] = [0.1]
+    metrics["n2"]["load_avg"] = [0.1]
+    assert p.get_scaling_state().autoscaling_instructions["resource_requests"] == []
+    # GPU-busy driven scaling
+    cfg["runtime"]["scaling"] = {"scaling_policy": "scaling-with-load", "scaling_resource": "GPU"}
+    p = create_scaling_policy(cfg, "10.0.0.1",
+                              metrics_source=lambda: {"g": {"cpu_count": 128, "load_avg": [1],
+                                                            "gpus": [{"busy_percent": 97}] * 8}})
+    assert len(p.get_scaling_state().autoscaling_instructions["resource_requests"]) == 1
+
+
+def test_scaling_with_time_table():
+    from cloudtik_amd.core.head.scaling_policies import ScalingWithTime
+    cfg = copy.deepcopy(BASE)
+    cfg["available_node_types"]["cpu.small"]["min_workers"] = 2
+    cfg["runtime"]["scaling"] = {"scaling_policy": "scaling-with-time", "scaling_math_base": "on-previous-time",
+                                 "scaling_time_table": {"08:00": "+3", "12:00": "*2", "20:00": 1}}
+    p = ScalingWithTime(cfg, "h")
+    t = time.mktime(time.strptime("2026-01-05 13:00", "%Y-%m-%d %H:%M"))
+    assert p.nodes_at(t) == 10                       # 2 + 3 = 5 at 08:00, *2 at 12:00
+    t = time.mktime(time.strptime("2026-01-05 07:00", "%Y-%m-%d %H:%M"))
+    assert p.nodes_at(t) == 1                        # wraps from the previous day's 20:00 entry
+
+
+def test_quorum_runtime_sets_up_complete_membership(state):
+    name = "sc-quorum"
+
+    def mutate(c):
+        c["runtime"]["types"] = ["zookeeper"]
+        c["runtime"]["zookeeper"] = {"minimal_nodes": 3}
+        c["available_node_types"]["cpu.small"].update(min_workers=3)
+        c["options"]["upscaling_speed"] = 0.1        # launches trickle in: max(5,...) still caps at 3 here
+    cfg, provider, scaler = _setup(name, state, mutate)
+    # launch only 2 first by shrinking min_workers, nothing may be set up
+    scaler.config["available_node_types"]["cpu.small"]["min_workers"] = 2
+    scaler.scheduler.node_types["cpu.small"]["min_workers"] = 2
+    scaler.update()
+    ws = _workers(provider, name)
+    assert len(ws) == 2 and all(provider.node_tags(w)[T.CLOUDTIK_TAG_NODE_STATUS] == T.STATUS_UNINITIALIZED
+                                for w in ws)
+    scaler.config["available_node_types"]["cpu.small"]["min_workers"] = 3
+    scaler.scheduler.node_types["cpu.small"]["min_workers"] = 3
+    scaler.update()
+    ws = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    assert len(ws) == 3
+    qids = {provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_ID] for w in ws}
+    assert len(qids) == 1
+    assert all(provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_JOIN] == T.QUORUM_JOIN_STATUS_SUCCESS for w in ws)

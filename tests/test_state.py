@@ -174,3 +174,28 @@ def test_protocol_error_closes_connection(server):
     s.close()
     # server still healthy
     assert StateClient.create(server.address, "secret").ping()
+
+
+def test_distributed_lock_and_leader_election(server):
+    from cloudtik_amd.core.state.lock import DistributedLock, LeaderElection
+    c1 = StateClient.create(server.address, "secret")
+    c2 = StateClient.create(server.address, "secret")
+    a = DistributedLock(c1, "job", ttl_ms=300)
+    b = DistributedLock(c2, "job", ttl_ms=300)
+    assert a.acquire(blocking=False) and not b.acquire(blocking=False)
+    assert not b.release()                 # cannot release someone else's lease
+    assert a.renew() and a.owner() == a.token
+    time.sleep(0.45)                        # lease expires without renewal
+    assert b.acquire(blocking=False) and not a.renew()
+    assert b.release() and a.acquire(timeout=1)
+    a.release()
+    events = []
+    e1 = LeaderElection(c1, "ctl", "node-1", ttl_ms=300, on_elected=lambda: events.append("1+"),
+                        on_demoted=lambda: events.append("1-"))
+    e2 = LeaderElection(c2, "ctl", "node-2", ttl_ms=300, on_elected=lambda: events.append("2+"))
+    e1.step()
+    e2.step()
+    assert e1.is_leader() and not e2.is_leader() and e2.leader() == "node-1"
+    e1.resign()                              # hand over
+    e2.step()
+    assert e2.is_leader() and events == ["1+", "1-", "2+"]
