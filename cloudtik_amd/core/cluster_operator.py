@@ -165,11 +165,19 @@ def _publish_services(config):
     except Exception:  # noqa: BLE001 -- providers without a workspace provider
         return
     head_ip = get_head_node_ip(config)
+    worker_ips = None
     gv = {}
     for t in get_runtime_types(config):
         rt = rf.get_runtime(t, config["runtime"].get(t, {}) or {})
         for name, svc in (rt.get_runtime_services(config) or {}).items():
-            gv[sd.service_global_key(config["cluster_name"], name)] = sd.encode_service_address(svc, head_ip)
+            if svc.get("scope") == sd.SERVICE_SCOPE_LOCAL:
+                continue                      # cluster-internal: not visible to the workspace
+            hosts = None
+            if svc.get("node_kind") in (sd.SERVICE_DISCOVERY_NODE_KIND_WORKER, sd.SERVICE_DISCOVERY_NODE_KIND_NODE):
+                if worker_ips is None:
+                    worker_ips = get_worker_node_ips(config)
+                hosts = ([head_ip] if svc["node_kind"] == sd.SERVICE_DISCOVERY_NODE_KIND_NODE else []) + worker_ips
+            gv[sd.service_global_key(config["cluster_name"], name)] = sd.encode_service_address(svc, head_ip, hosts)
     if gv:
         wp.publish_global_variables(config, gv)
 

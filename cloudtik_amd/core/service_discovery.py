@@ -75,7 +75,7 @@ def match_service(service: Dict[str, Any], selector: Optional[Dict[str, Any]]) -
     if not selector:
         return True
     for key, field in (("services", "name"), ("service_types", "service_type"),
-                       ("runtimes", "runtime"), ("clusters", "cluster")):
+                       ("runtimes", "service_type"), ("clusters", "cluster")):
         want = selector.get(key)
         if want and service.get(field) not in want:
             return False
@@ -93,8 +93,9 @@ def service_global_key(cluster_name: str, service_name: str) -> str:
     return f"service.{cluster_name}.{service_name}"
 
 
-def encode_service_address(service: Dict[str, Any], host: str) -> str:
-    return json.dumps({**service, "host": host}, sort_keys=True)
+def encode_service_address(service: Dict[str, Any], host: str, hosts: Optional[List[str]] = None) -> str:
+    """``host`` is where head-kind services listen; worker/all-kind services list every node."""
+    return json.dumps({**service, "host": host, "hosts": list(hosts) if hosts else [host]}, sort_keys=True)
 
 
 def decode_service_address(value: str) -> Dict[str, Any]:

@@ -106,6 +106,9 @@ class LocalLauncher(Launcher):
         log_dir = self.args.log_dir
         if log_dir:
             os.makedirs(log_dir, exist_ok=True)
+        # if this launcher is killed outright, the reaper still ends the ranks (and frees GPUs)
+        from cloudtik_amd.core.node.reaper import Reaper
+        reaper = Reaper()
         for lr in range(self.local_world):
             cpus = cpu_sets.get(lr)
             env = self.rank_env(lr, cpus)
@@ -125,6 +128,7 @@ class LocalLauncher(Launcher):
                       file=sys.stderr)
             self.procs.append(subprocess.Popen(prog, env=env, stdout=out, stderr=subprocess.STDOUT if out else None,
                                                preexec_fn=pre, start_new_session=True))
+            reaper.watch(self.procs[-1].pid)          # the rank leads its own process group
         prev = {s: signal.getsignal(s) for s in (signal.SIGINT, signal.SIGTERM)}
         if threading.current_thread() is threading.main_thread():
             for s in prev:
@@ -150,6 +154,7 @@ class LocalLauncher(Launcher):
                 for s, h in prev.items():
                     signal.signal(s, h)
             self._terminate_all(signal.SIGKILL)
+            reaper.release()
         return rc if rc >= 0 else 128 - rc
 
 

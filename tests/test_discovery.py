@@ -1,0 +1,109 @@
+"""Process reaper, node naming and runtime service discovery (CPU)."""
+import os
+import signal
+import subprocess
+import sys
+import time
+
+from cloudtik_amd.core import naming
+from cloudtik_amd.core import service_discovery as sd
+from cloudtik_amd.runtime.common import discovery as disc
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    # a zombie still answers kill(0): look at its state
+    with open(f"/proc/{pid}/stat") as f:
+        return f.read().split(")")[1].split()[0] != "Z"
+
+
+def test_reaper_kills_children_when_launcher_dies(tmp_path):
+    pidfile = tmp_path / "child.pid"
+    launcher = tmp_path / "launcher.py"
+    launcher.write_text(
+        "import subprocess, sys, time\n"
+        "from cloudtik_amd.core.node.reaper import Reaper\n"
+        "r = Reaper()\n"
+        "c = subprocess.Popen([sys.executable, '-c', 'import time; time.sleep(60)'], start_new_session=True)\n"
+        "r.watch(c.pid)\n"
+        f"open({str(pidfile)!r}, 'w').write(str(c.pid))\n"
+        "time.sleep(60)\n")
+    env = dict(os.environ, PYTHONPATH=os.getcwd())
+    lp = subprocess.Popen([sys.executable, str(launcher)], env=env)
+    try:
+        for _ in range(200):
+            if pidfile.exists() and pidfile.read_text():
+                break
+            time.sleep(0.05)
+        child = int(pidfile.read_text())
+        assert _alive(child)
+        lp.send_signal(signal.SIGKILL)          # launcher dies without cleanup
+        lp.wait()
+        for _ in range(100):
+            if not _alive(child):
+                break
+            time.sleep(0.05)
+        assert not _alive(child)
+    finally:
+        if lp.poll() is None:
+            lp.kill()
+
+
+def test_reaper_release_leaves_children_alone():
+    from cloudtik_amd.core.node.reaper import Reaper
+    c = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"], start_new_session=True)
+    try:
+        r = Reaper()
+        r.watch(c.pid)
+        r.release()
+        time.sleep(0.2)
+        assert c.poll() is None
+    finally:
+        c.kill()
+        c.wait()
+
+
+def test_naming():
+    cfg = {"cluster_name": "train", "workspace_name": "ws", "runtime": {"types": ["ai"]}}
+    assert naming.get_cluster_node_name("train", 3) == "train-3"
+    assert naming.get_cluster_node_sqdn("train-3", "train") == "train-3.train.node"
+    assert naming.get_cluster_head_host(cfg, "10.0.0.1") == "10.0.0.1"      # no DNS runtime
+    cfg["runtime"]["types"].append("consul")
+    assert naming.get_cluster_head_host(cfg, "10.0.0.1") == "train-1.train.ws.cloudtik"
+    env = naming.with_node_host_environment_variables(cfg, 2, "10.0.0.2", {})
+    assert env["CLOUDTIK_NODE_HOST"] == "train-2.train.ws.cloudtik"
+    assert naming.get_address_type_of_hostname("::1") == "ipv6"
+    assert naming.get_address_type_of_hostname("h.x") == "hostname"
+
+
+def _publish(cluster, runtime, svc_name, port, kind, host, hosts=None, features=()):
+    svc = sd.define_runtime_service(runtime, svc_name, port, node_kind=kind, features=list(features))
+    return {sd.service_global_key(cluster, f"{cluster}-{svc_name}"): sd.encode_service_address(svc, host, hosts)}
+
+
+def test_discovery_from_workspace_and_on_head():
+    gv = {}
+    gv.update(_publish("storage", "hdfs", "hdfs-rpc", 8020, "head", "10.1.0.1"))
+    gv.update(_publish("zk", "zookeeper", "zookeeper", 2181, "worker", "10.2.0.1", ["10.2.0.2", "10.2.0.3"]))
+    gv.update(_publish("db", "mysql", "mysql", 3306, "head", "10.3.0.1"))
+    gv.update(_publish("meta", "metastore", "metastore", 9083, "head", "10.4.0.1"))
+    cfg = {"cluster_name": "analytics", "runtime": {"types": ["spark"]}}
+    assert disc.discover_hdfs_from_workspace(cfg, global_variables=gv) == "hdfs://10.1.0.1:8020"
+    assert disc.discover_zookeeper_from_workspace(cfg, global_variables=gv) == "10.2.0.2:2181,10.2.0.3:2181"
+    assert disc.discover_metastore_from_workspace(cfg, global_variables=gv) == "thrift://10.4.0.1:9083"
+    assert disc.discover_database_from_workspace(cfg, global_variables=gv) == \
+        {"engine": "mysql", "address": "10.3.0.1", "port": 3306}
+    assert disc.discover_minio_from_workspace(cfg, global_variables=gv) is None
+    # selector restricts the candidate clusters
+    cfg["runtime"]["spark"] = {"hdfs_service_selector": {"clusters": ["other"]}}
+    assert disc.discover_hdfs_from_workspace(cfg, consumer="spark", global_variables=gv) is None
+    # a cluster never discovers itself through the workspace; it uses *_on_head
+    own = {"cluster_name": "storage", "runtime": {"types": ["hdfs", "zookeeper"]}}
+    assert disc.discover_hdfs_from_workspace(own, global_variables=gv) is None
+    assert disc.discover_hdfs_on_head(own, "10.1.0.1") == "hdfs://10.1.0.1:8020"
+    assert disc.discover_zookeeper_on_head(own, "10.1.0.1", ["10.1.0.5"]) == "10.1.0.5:2181"
+    assert disc.discover_service("hdfs", own, head_ip="10.1.0.1") == "hdfs://10.1.0.1:8020"
+    assert disc.discover_service("metastore", own, head_ip="10.1.0.1", global_variables=gv) == "thrift://10.4.0.1:9083"
