@@ -397,26 +397,32 @@ def submit_and_exec(config_file, script: str, script_args: Optional[List[str]] =
     target_dir = "~/user/jobs"
     name = os.path.basename(script)
     ex = _executor(config, provider, n)
-    if os.path.exists(script):
-        ex.run(f"mkdir -p {target_dir}")
-        ex.run_rsync_up(script, f"{target_dir}/{name}")
-        remote = f"{target_dir}/{name}"
-    elif script.startswith(("http://", "https://")):
-        ex.run(f"mkdir -p {target_dir} && wget -q -O {target_dir}/{name} {shlex.quote(script)}")
-        remote = f"{target_dir}/{name}"
-    else:
-        remote = script
-    ext = os.path.splitext(name)[1]
-    runner = None
-    for t in get_runtime_types(config):
-        rt = rf.get_runtime(t, config["runtime"].get(t, {}) or {})
-        r = rt.get_runnable_command(remote, runtime_options)
-        if r:
-            runner = " ".join(r[:-1])
-            break
-    runner = runner or RUNNERS.get(ext, "")
+    from cloudtik_amd.core.script_registry import get_registered_script
+    module = None if os.path.exists(script) else get_registered_script(script)
     args = " ".join(shlex.quote(a) for a in (script_args or []))
-    cmd = f"cd {target_dir} && {runner} {remote} {args}".replace("  ", " ")
+    if module:
+        # registered alias (e.g. ai.launch): run the module with the node's interpreter
+        cmd = f"mkdir -p {target_dir} && cd {target_dir} && ${{CLOUDTIK_PYTHON:-python3}} -m {module} {args}".rstrip()
+    else:
+        if os.path.exists(script):
+            ex.run(f"mkdir -p {target_dir}")
+            ex.run_rsync_up(script, f"{target_dir}/{name}")
+            remote = f"{target_dir}/{name}"
+        elif script.startswith(("http://", "https://")):
+            ex.run(f"mkdir -p {target_dir} && wget -q -O {target_dir}/{name} {shlex.quote(script)}")
+            remote = f"{target_dir}/{name}"
+        else:
+            remote = script
+        ext = os.path.splitext(name)[1]
+        runner = None
+        for t in get_runtime_types(config):
+            rt = rf.get_runtime(t, config["runtime"].get(t, {}) or {})
+            r = rt.get_runnable_command(remote, runtime_options)
+            if r:
+                runner = " ".join(r[:-1])
+                break
+        runner = runner or RUNNERS.get(ext, "")
+        cmd = f"cd {target_dir} && {runner} {remote} {args}".replace("  ", " ")
     if not job_waiter:
         return exec_cluster(config, cmd, node_ip=node_ip, with_output=with_output)
     # detached job in a named session, then wait for it with the requested waiter

@@ -1,0 +1,5 @@
+from .datasets import (ArrayImageDataset, HashTokenizer, ImageFolderDataset, TextClassificationDataset,  # noqa: F401
+                       synthetic_image_dataset)
+from .image_classification import ImageClassificationModel  # noqa: F401
+from .model_factory import get_model, get_supported_models, load_model  # noqa: F401
+from .text_classification import TextClassificationModel  # noqa: F401
