@@ -27,6 +27,7 @@ void ct_loader_set_epoch(void*, long);
 long ct_loader_next_device(void*, void* const*, hipStream_t, hipStream_t);
 long ct_loader_next_host(void*, void* const*);
 void ct_loader_destroy(void*);
+int ct_image_u8_to_bf16(const uint8_t*, void*, const uint8_t*, int, int, int, const float*, const float*, hipStream_t);
 }
 
 namespace {
@@ -295,7 +296,33 @@ int64_t loader_next_host(int64_t h, std::vector<at::Tensor> outs) {
 
 }  // namespace
 
+// images: uint8 [N, H, W, 3] contiguous -> bf16 [N, 3, H, W] channels_last; flip: optional uint8 [N]
+at::Tensor image_u8_to_bf16(at::Tensor images, c10::optional<at::Tensor> flip, std::vector<double> mean,
+                            std::vector<double> stdv) {
+  XCHECK_IN(images);
+  XCHECK_DT(images, at::kByte);
+  TORCH_CHECK(images.dim() == 4 && images.size(3) == 3, "image_u8_to_bf16: images must be [N, H, W, 3]");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "image_u8_to_bf16: 3 means and stds");
+  const int N = (int)images.size(0), H = (int)images.size(1), W = (int)images.size(2);
+  TORCH_CHECK(W % 4 == 0, "image_u8_to_bf16: width must be a multiple of 4");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(images.data_ptr()) & 3) == 0, "image_u8_to_bf16: 4-byte aligned input");
+  const uint8_t* fp = nullptr;
+  if (flip.has_value()) {
+    XCHECK_IN(*flip);
+    XCHECK_DT(*flip, at::kByte);
+    TORCH_CHECK(flip->numel() == N, "image_u8_to_bf16: one flip flag per image");
+    fp = flip->data_ptr<uint8_t>();
+  }
+  auto out = at::empty({N, H, W, 3}, images.options().dtype(at::kBFloat16));
+  float m[3], s[3];
+  for (int i = 0; i < 3; ++i) { m[i] = (float)mean[i]; s[i] = (float)stdv[i]; }
+  int rc = ct_image_u8_to_bf16(images.data_ptr<uint8_t>(), out.data_ptr(), fp, N, H, W, m, s, stream());
+  TORCH_CHECK(rc == 0, "ct_image_u8_to_bf16 failed: ", rc);
+  return out.permute({0, 3, 1, 2});
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("image_u8_to_bf16", &image_u8_to_bf16);
   m.def("loader_create", &loader_create);
   m.def("loader_num_batches", &loader_num_batches);
   m.def("loader_set_epoch", &loader_set_epoch);

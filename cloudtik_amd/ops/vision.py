@@ -220,3 +220,25 @@ def sigmoid_focal_loss(logits, targets, gamma: float = 2.0, alpha: float = 0.25,
     if reduction == "mean":
         return loss.mean()
     return loss
+
+
+# ---------------------------------------------------------------------- image ingest
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def images_to_tensor_reference(images: torch.Tensor, flip=None, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+    x = images.float() / 255.0
+    if flip is not None:
+        x = torch.where(flip.bool()[:, None, None, None], x.flip(2), x)
+    x = (x - torch.tensor(mean, device=x.device)) / torch.tensor(std, device=x.device)
+    return x.permute(0, 3, 1, 2)
+
+
+def images_to_tensor(images: torch.Tensor, flip: torch.Tensor = None, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+    """uint8 [N, H, W, 3] -> normalised [N, 3, H, W] (bf16 channels_last on the GPU, one HIP
+    pass with optional per-image horizontal flip; fp32 on the CPU)."""
+    if images.is_cuda and _use_native(images):
+        f = None if flip is None else flip.to(torch.uint8).contiguous()
+        return _native().image_u8_to_bf16(images.contiguous(), f, list(map(float, mean)), list(map(float, std)))
+    return images_to_tensor_reference(images, flip, mean, std)

@@ -35,3 +35,31 @@ def test_parquet_to_gpu(cuda, tmp_path):
     P = ParquetDataLoader(str(tmp_path), 128, shapes={"image": (3, 8, 8)}, device=cuda, shuffle=False)
     got = torch.cat([b["image"].cpu() for b in P])
     assert torch.equal(got, torch.from_numpy(imgs))
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_image_ingest_kernel(cuda, flip):
+    from cloudtik_amd import ops
+    from cloudtik_amd.ops.vision import images_to_tensor_reference
+    g = torch.Generator().manual_seed(1)
+    imgs = torch.randint(0, 256, (5, 24, 36, 3), generator=g, dtype=torch.uint8)
+    f = torch.tensor([1, 0, 1, 1, 0], dtype=torch.uint8) if flip else None
+    got = ops.images_to_tensor(imgs.cuda(), None if f is None else f.cuda())
+    assert got.dtype == torch.bfloat16 and got.shape == (5, 3, 24, 36)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    want = images_to_tensor_reference(imgs, f)
+    torch.testing.assert_close(got.float().cpu(), want, rtol=1e-2, atol=2e-2)
+
+
+def test_parquet_image_pipeline_gpu(cuda, tmp_path):
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONPATH=os.getcwd())
+    r = subprocess.run([sys.executable, "examples/ai/spark_parquet_resnet50.py", "--model", "small",
+                        "--image-size", "64", "--batch-size", "64", "--data-path", str(tmp_path / "pq"),
+                        "--epochs", "2", "--warmup", "2"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["value"] > 0 and res["final_loss"] == res["final_loss"]
