@@ -94,3 +94,5 @@ from .embedding import EmbeddingBagCollection, dot_interaction, embedding_bag, p
 from .vision import batched_nms, images_to_tensor, nms, roi_align, roi_pool, sigmoid_focal_loss  # noqa: E402,F401
 from . import multi_tensor  # noqa: E402,F401
 from .graph import CSR, SpMM, gbdt_histogram, gbdt_predict, spmm  # noqa: E402,F401
+from .deform import (DeformConv, DeformRoIPooling, DeformRoIPoolingPack, ModulatedDeformConv,  # noqa: E402,F401
+                     ModulatedDeformConvPack, deform_conv2d, deform_roi_pooling)
