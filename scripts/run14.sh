@@ -1,7 +1,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_data_gpu.py -x -q -m gpu > gpurun_out/pytest_data_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_data_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -m pytest tests/test_deform_gpu.py tests/test_data_gpu.py -x -q -m gpu > gpurun_out/pytest_new_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_new_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python examples/ai/spark_parquet_resnet50.py --data-path /tmp/ct_pq --epochs 3 > gpurun_out/pipeline_rn50.log 2>&1 || exit $?
 tail -1 gpurun_out/pipeline_rn50.log
 timeout -k 10 600 python bench/gbdt_bench.py > gpurun_out/gbdt_bench.log 2>&1 || exit $?

@@ -26,7 +26,7 @@ def test_deform_conv_fwd_bwd(modulated, cfg):
     args = (cfg["stride"], cfg["padding"], cfg["dilation"], cfg["groups"], cfg["dg"])
     leaves = [t.clone().requires_grad_() for t in (x, off, w, bias)] + \
         ([mask.clone().requires_grad_()] if modulated else [])
-    ref_leaves = [t.clone().requires_grad_() for t in leaves]
+    ref_leaves = [t.detach().clone().requires_grad_() for t in leaves]
     y = deform_conv2d(leaves[0], leaves[1], leaves[2], leaves[3], leaves[4] if modulated else None, *args)
     yr = deform_conv2d_reference(ref_leaves[0], ref_leaves[1], ref_leaves[2], ref_leaves[3],
                                  ref_leaves[4] if modulated else None, *args)
