@@ -495,6 +495,79 @@ class Booster:
             hist_prev = hist * split.view(-1, 1, 1, 1)
         return (feat, thr, dleft, leaf, gain_a, cover), final
 
+
+    def _grow_tree_gpu(self, bins, n_rows, g, h, sampled, feat_mask, margin, k_out):
+        """Single process: the whole tree (about 4 launches per level) is captured once into a
+        HIP graph and replayed every round, so growth is not bound by host launch latency.
+        With several ranks the per-level all-reduces run eagerly instead."""
+        import os
+        if _dist_on() or os.environ.get("CLOUDTIK_AMD_GBDT_GRAPH", "1") == "0":
+            return self._grow_tree_native(bins, n_rows, g, h, sampled, feat_mask, margin, k_out)
+        key = (k_out, bins.data_ptr(), n_rows, margin.data_ptr())
+        graphs = self.__dict__.setdefault("_graphs", {})
+        st = graphs.get(key)
+        if st is None:
+            bufs = (torch.empty_like(g), torch.empty_like(h), torch.empty_like(sampled), torch.empty_like(feat_mask))
+            for b, v in zip(bufs, (g, h, sampled, feat_mask)):
+                b.copy_(v)
+            side = torch.cuda.Stream(device=bins.device)
+            side.wait_stream(torch.cuda.current_stream(bins.device))
+            with torch.cuda.stream(side):                    # warm-up: workspace + allocator
+                self._grow_tree_native(bins, n_rows, *bufs, margin.clone(), k_out)
+            torch.cuda.current_stream(bins.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._grow_tree_native(bins, n_rows, *bufs, margin, k_out)
+            st = graphs[key] = (graph, bufs, out)
+        graph, bufs, out = st
+        for b, v in zip(bufs, (g, h, sampled, feat_mask)):
+            b.copy_(v)
+        graph.replay()
+        return tuple(t.clone() for t in out)
+
+    def _grow_tree_native(self, bins, n_rows, g, h, sampled, feat_mask, margin, k_out):
+        """GPU tree growth: per level one histogram kernel (smaller children only), one
+        split-search kernel (subtraction trick + scan + argmax per node/feature), one
+        finalize kernel (tree arrays + next slot map) and one row-partition kernel that also
+        adds leaf values to the margin.  No host synchronisation inside the tree."""
+        from cloudtik_amd import ops as _ops
+        C = _ops.require_native()
+        p = self.params
+        dev = bins.device
+        M, D = self.M, p.max_depth
+        F, B = bins.shape[0], self.mapper.max_bin
+        feat = torch.full((M,), -1, dtype=torch.int32, device=dev)
+        thr = torch.zeros(M, dtype=torch.int32, device=dev)
+        dleft = torch.zeros(M, dtype=torch.uint8, device=dev)
+        leaf = torch.zeros(M, dtype=torch.float32, device=dev)
+        gain = torch.zeros(M, dtype=torch.float32, device=dev)
+        cover = torch.zeros(M, dtype=torch.float32, device=dev)
+        sf = sampled.float()
+        gh = torch.stack([g * sf, h * sf], dim=1).float().contiguous()
+        node = torch.zeros(n_rows, dtype=torch.int32, device=dev)
+        ws = getattr(self, "_ws", None)
+        if ws is None or ws[0].numel() < (1 << D) * F:
+            L = (1 << D) * F
+            ws = (torch.empty(L, device=dev), torch.empty(L, dtype=torch.int32, device=dev),
+                  torch.empty(L, dtype=torch.int32, device=dev), torch.empty(L, device=dev),
+                  torch.empty(2 << D, device=dev), torch.empty(0, dtype=torch.int32, device=dev))
+            self._ws = ws
+        fmask = feat_mask.to(torch.uint8).contiguous()
+        hist_prev, smap = None, None
+        for level in range(D + 1):
+            n_level = 1 << level
+            last = level == D
+            part = ops.gbdt_histogram(bins, n_rows, node, gh, max(1, n_level // 2), B, slot_map=smap)
+            _allreduce_(part)
+            hist_cur = torch.empty(n_level, F, B, 2, device=dev)
+            slot_next = torch.empty(2 * n_level, dtype=torch.int32, device=dev) if not last else ws[5]
+            C.gbdt_level(part, hist_prev, smap, hist_cur, fmask, level, last, p.reg_lambda, p.reg_alpha,
+                         p.min_child_weight, p.gamma, p.eta, p.max_delta_step, feat, thr, dleft, leaf, gain, cover,
+                         slot_next, ws[0], ws[1], ws[2], ws[3], ws[4])
+            C.gbdt_partition(bins, n_rows, node, feat, thr, dleft, leaf, level, margin, k_out)
+            hist_prev, smap = hist_cur, slot_next
+        return feat, thr, dleft, leaf, gain, cover
+
     # ------------------------------------------------------------ training
     def _margin_init(self, n: int) -> torch.Tensor:
         K = self.objective.n_outputs
@@ -534,7 +607,9 @@ class Booster:
             eval_sets.append((name, eb, en, em, dm.y.to(dev),
                               dm.w.to(dev) if dm.w is not None else torch.ones(en, device=dev)))
         metrics = p.eval_metric or [self._default_metric()]
-        gen = torch.Generator(device="cpu").manual_seed(p.seed + (dist.get_rank() if _dist_on() else 0))
+        # row sampling on the device (no per-round host->device copy); the feature mask is
+        # drawn on the host from a seed shared by every rank so all ranks agree on it
+        gen = torch.Generator(device=dev).manual_seed(p.seed + (dist.get_rank() if _dist_on() else 0))
         fgen = torch.Generator(device="cpu").manual_seed(p.seed)        # same feature mask on every rank
         K = self.objective.n_outputs
         F = bins.shape[0]
@@ -542,7 +617,7 @@ class Booster:
         best_score, best_it, history = None, None, {}
         for it in range(num_boost_round):
             if p.subsample < 1:
-                sampled = (torch.rand(n, generator=gen) < p.subsample).to(dev)
+                sampled = torch.rand(n, device=dev, generator=gen) < p.subsample
             else:
                 sampled = torch.ones(n, dtype=torch.bool, device=dev)
             if p.colsample_bytree < 1:
@@ -553,9 +628,12 @@ class Booster:
             else:
                 feat_mask = torch.ones(F, dtype=torch.bool, device=dev)
             for k_out, (g, h) in enumerate(self.objective.grad_hess(margin, y, w)):
-                arrays, final = self._grow_tree(bins, n, g, h, sampled, feat_mask)
+                if bins.is_cuda:
+                    arrays = self._grow_tree_gpu(bins, n, g, h, sampled, feat_mask, margin, k_out)
+                else:
+                    arrays, final = self._grow_tree(bins, n, g, h, sampled, feat_mask)
+                    margin[:, k_out] += arrays[3][final]
                 new_trees.append(arrays)
-                margin[:, k_out] += arrays[3][final]
                 for (_, eb, en, em, _, _) in eval_sets:
                     em[:, k_out] += self._predict_one(eb, en, arrays)
             scores = {}
@@ -581,6 +659,7 @@ class Booster:
                     break
             history = scores
         self._append_trees(new_trees)
+        self.__dict__.pop("_graphs", None)
         self.best_iteration = best_it if best_it is not None else (self.num_trees // K) - 1
         self.best_score = best_score
         self.last_scores = history

@@ -48,12 +48,16 @@ def gbdt_histogram_reference(bins: torch.Tensor, n_rows: int, node: torch.Tensor
 
 
 def gbdt_histogram(bins: torch.Tensor, n_rows: int, node: torch.Tensor, gh: torch.Tensor, n_slots: int,
-                   n_bins: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   n_bins: int, out: Optional[torch.Tensor] = None,
+                   slot_map: Optional[torch.Tensor] = None) -> torch.Tensor:
     """hist[s, f, b] = sum over rows r with node[r] == s and bins[f, r] == b of gh[r].
 
     bins: uint8 [F, ldb] feature-major (ldb % 4 == 0); node: int32 [N] (-1 = inactive);
     gh: fp32 [N, 2].  Returns fp32 [n_slots, F, n_bins, 2]."""
     if not _use_native(bins):
+        if slot_map is not None:
+            node = torch.where((node >= 0) & (node < slot_map.numel()), slot_map[node.clamp(0, slot_map.numel() - 1).long()],
+                               torch.full_like(node, -1))
         return gbdt_histogram_reference(bins, n_rows, node, gh, n_slots, n_bins)
     F = bins.shape[0]
     hist = out if out is not None else torch.empty(n_slots, F, n_bins, 2, dtype=torch.float32, device=bins.device)
@@ -61,7 +65,7 @@ def gbdt_histogram(bins: torch.Tensor, n_rows: int, node: torch.Tensor, gh: torc
     per_pass = max(1, min(MAX_SLOTS_PER_PASS, (64 * 1024) // (n_bins * 8)))
     C = _native()
     for lo in range(0, n_slots, per_pass):
-        C.gbdt_hist(bins, int(n_rows), node, gh, hist, lo, min(per_pass, n_slots - lo))
+        C.gbdt_hist(bins, int(n_rows), node, gh, hist, lo, min(per_pass, n_slots - lo), slot_map)
     return hist
 
 

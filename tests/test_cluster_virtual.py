@@ -93,3 +93,25 @@ def test_virtual_cluster_lifecycle(cluster, tmp_path):
 
     _run(env, "stop", cfg, "-y")
     assert "RUNNING" not in _run(env, "info", cfg, "--json")
+
+
+def test_on_demand_workflow_example(tmp_path):
+    """examples/workflows/on_demand_ai_job.py: start -> wait -> submit (pid job waiter) -> stop."""
+    name = f"w{os.getpid() % 10000}"
+    cfg = tmp_path / "cluster.yaml"
+    cfg.write_text(CONFIG.format(name=name).replace("min_workers: 2", "min_workers: 1"))
+    marker = tmp_path / "done.txt"
+    job = tmp_path / "job.py"
+    job.write_text(f"open({str(marker)!r}, 'w').write('ok')\n")
+    env = dict(os.environ, CLOUDTIK_LOCAL_STATE_DIR=str(tmp_path / "state"), CLOUDTIK_UPDATE_INTERVAL_S="1",
+               CLOUDTIK_METRIC_PORT="0", CLOUDTIK_CONFIG_CACHE=str(tmp_path / "cache"),
+               CLOUDTIK_PYTHON=sys.executable, PYTHONPATH=ROOT)
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "workflows", "on_demand_ai_job.py"),
+                            str(cfg), str(job), "--min-workers", "1"], env=env, capture_output=True, text=True,
+                           timeout=400)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+        assert "job finished" in r.stdout and "cluster stopped" in r.stdout
+        assert marker.read_text() == "ok"
+    finally:
+        _run(env, "stop", str(cfg), "-y", "--hard", check=False)

@@ -129,3 +129,22 @@ def test_transfer_learning_gpu_bf16():
     assert m.dtype == torch.bfloat16
     hist = m.train(synthetic_image_dataset(128, 4, image_size=64), epochs=1, batch_size=32, log_every=0)
     assert np.isfinite(hist[-1]["loss"])
+
+
+def test_gbdt_native_level_kernels_match_cpu_growth():
+    """The fused GPU level kernels grow the same trees as the tensor-op CPU path."""
+    from cloudtik_amd.modeling.gbdt import DMatrix, train
+    rng = np.random.default_rng(3)
+    N, F = 20000, 10
+    X = rng.normal(size=(N, F)).astype(np.float32)
+    X[rng.random((N, F)) < 0.05] = np.nan
+    z = np.nan_to_num(X)
+    y = (z[:, 0] + 0.5 * z[:, 1] ** 2 - z[:, 2] + rng.normal(size=N) * 0.3).astype(np.float32)
+    for params in ({"objective": "reg:squarederror", "max_depth": 5, "eta": 0.3, "max_bin": 64},
+                   {"objective": "reg:squarederror", "max_depth": 4, "eta": 0.3, "max_bin": 256, "lambda": 2.0,
+                    "alpha": 0.5, "gamma": 0.1, "min_child_weight": 5, "colsample_bytree": 0.7}):
+        bg = train(params, DMatrix(X, y), 8, device=dev)
+        bc = train(params, DMatrix(X, y), 8, device="cpu")
+        assert torch.equal(bg.trees.feat[0].cpu(), bc.trees.feat[0]) and torch.equal(bg.trees.thr[0].cpu()[bc.trees.feat[0] >= 0], bc.trees.thr[0][bc.trees.feat[0] >= 0])
+        pg, pc = bg.predict(X), bc.predict(X)
+        assert np.corrcoef(pg, pc)[0, 1] > 0.999 and np.abs(pg - pc).mean() < 1e-2 * y.std()
