@@ -46,6 +46,8 @@ def parse():
                     help="masked-LM slots per sequence (reference phase-1: max_predictions_per_seq=76)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-dropout", action="store_true")
+    ap.add_argument("--conv-benchmark", action="store_true",
+                    help="ResNet: let MIOpen search convolution solvers (torch.backends.cudnn.benchmark)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--tunableop", default="use", choices=["off", "use", "tune"],
                     help="hipBLASLt solution selection via PyTorch TunableOp (results shipped in-tree)")
@@ -126,6 +128,8 @@ def bench_resnet(args, rank, world, device):
     from cloudtik_amd.train.optim import FusedSGD, FlatParamSpace
 
     torch.manual_seed(1234)
+    if args.conv_benchmark:
+        torch.backends.cudnn.benchmark = True
     model = resnet50(device=device)
     model.train()
     named = [(n, p) for n, p in model.named_parameters()]
@@ -161,8 +165,12 @@ def main():
     fn = bench_bert if args.model.startswith("bert") else bench_resnet
     step, info = fn(args, rank, world, device)
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
+    torch.cuda.synchronize()
+    if rank == 0:
+        print(f"[bench] warm-up {args.warmup} step(s): {time.perf_counter() - tw:.1f}s", file=sys.stderr)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

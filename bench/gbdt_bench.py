@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=100)
     ap.add_argument("--depth", type=int, default=8)
     a = ap.parse_args()
-    from cloudtik_amd.modeling.gbdt import DMatrix, train
+    from cloudtik_amd.modeling.gbdt import BinMapper, Booster, DMatrix, train
     from sklearn.metrics import roc_auc_score
     rng = np.random.default_rng(0)
     X = rng.normal(size=(a.rows, a.features)).astype(np.float32)
@@ -30,10 +30,17 @@ def main():
     n_tr = int(a.rows * 0.9)
     dtr, dte = DMatrix(X[:n_tr], y[:n_tr]), DMatrix(X[n_tr:], y[n_tr:])
     params = {"objective": "binary:logistic", "max_depth": a.depth, "eta": 0.1, "max_bin": 256}
-    train(params, dtr, 3)                         # warm-up: binning, kernels, allocator
+    train(params, dtr, 3)                         # warm-up: kernels, allocator
     torch.cuda.synchronize()
+    # quantisation (quantile sketch + binning to uint8 on the GPU) timed on its own
     t0 = time.time()
-    b = train(params, dtr, a.rounds)
+    b = Booster(params)
+    b.mapper = BinMapper(256).fit(dtr.X.to(b.device))
+    dtr.binned(b.mapper, b.device)
+    torch.cuda.synchronize()
+    t_prep = time.time() - t0
+    t0 = time.time()
+    b.train(dtr, a.rounds)
     torch.cuda.synchronize()
     t_train = time.time() - t0
     b.predict(dte)
@@ -42,7 +49,7 @@ def main():
     p = b.predict(dte)
     t_pred = time.time() - t0
     print(json.dumps({"rows": n_tr, "features": a.features, "depth": a.depth, "rounds": a.rounds,
-                      "train_seconds": round(t_train, 3), "ms_per_round": round(1000 * t_train / a.rounds, 3),
+                      "quantize_seconds": round(t_prep, 3), "train_seconds": round(t_train, 3), "ms_per_round": round(1000 * t_train / a.rounds, 3),
                       "predict_rows_per_sec": round(len(p) / t_pred), "test_auc": round(roc_auc_score(y[n_tr:], p), 4)}),
           flush=True)
 

@@ -75,19 +75,28 @@ class BinMapper:
             parts = [torch.empty_like(pad) for _ in sizes]
             dist.all_gather(parts, pad)
             Xs = torch.cat(parts)
-        Xs = Xs.float().cpu()
+        # quantiles on the sample's device (the GPU when training there): one sort of the
+        # [S, F] sample, then per feature either its distinct values (few of them) or the
+        # values at the quantile ranks
+        Xs = Xs.float()
         nb = self.max_bin - 2          # cuts; gives up to max_bin - 1 value bins
-        cuts = torch.full((Xs.shape[1], nb), float("inf"))
-        qs = torch.linspace(0, 1, nb + 2)[1:-1]
+        srt, _ = torch.sort(Xs, dim=0)                      # NaN sorts last
+        valid = (~torch.isnan(srt)).sum(0).cpu()
+        cuts = torch.full((Xs.shape[1], nb), float("inf"), device=Xs.device)
+        qs = torch.linspace(0, 1, nb + 2, device=Xs.device)[1:-1]
         for f in range(Xs.shape[1]):
-            col = Xs[:, f]
-            col = col[~torch.isnan(col)]
-            if col.numel() == 0:
+            n = int(valid[f])
+            if n == 0:
                 continue
-            u = torch.unique(col)
-            c = u[:-1] if u.numel() <= nb + 1 else torch.unique(torch.quantile(col[:16_000_000].double(), qs.double()).float())
-            c = c[c < u[-1]] if c.numel() else c
+            col = srt[:n, f]
+            u = torch.unique_consecutive(col)
+            if u.numel() <= nb + 1:
+                c = u[:-1]
+            else:
+                c = torch.unique_consecutive(col[(qs * (n - 1)).round().long()])
+                c = c[c < u[-1]]
             cuts[f, :c.numel()] = c[:nb]
+        cuts = cuts.cpu()
         self.cuts = cuts
         return self
 
