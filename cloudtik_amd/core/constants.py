@@ -123,3 +123,6 @@ CLOUDTIK_GPU_RESOURCE = "GPU"
 CLOUDTIK_ACCELERATOR_TYPE_PREFIX = "accelerator_type:"
 CLOUDTIK_ROCM_VISIBLE_ENVS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
 CLOUDTIK_GPU_HEALTH_TEMP_C = env_integer("CLOUDTIK_GPU_HEALTH_TEMP_C", 100)
+# a worker whose GPUs stay unhealthy (RAS uncorrectable errors, over-temperature) this long
+# is terminated and replaced by the scaler
+CLOUDTIK_GPU_UNHEALTHY_TIMEOUT_S = env_integer("CLOUDTIK_GPU_UNHEALTHY_TIMEOUT_S", 60)

@@ -107,6 +107,7 @@ class ClusterScaler:
         self.launch_lock = threading.Lock()
         self.updaters: Dict[str, Any] = {}
         self.failed_updates: Counter = Counter()
+        self.gpu_unhealthy_since: Dict[str, float] = {}
         self.last_active: Dict[str, float] = {}
         self.num_failures = 0
         self.events: List[str] = []
@@ -238,6 +239,7 @@ class ClusterScaler:
 
         # 5) updates + recovery (quorum runtimes: set up only a complete initial membership)
         workers = self.workers()
+        to_replace = []
         may_update = set(self.quorum.updatable(
             [n for n in workers if self.provider.node_tags(n).get(T.CLOUDTIK_TAG_NODE_STATUS) == T.STATUS_UNINITIALIZED
              or self.provider.node_tags(n).get(T.CLOUDTIK_TAG_QUORUM_ID)]))
@@ -263,7 +265,25 @@ class ClusterScaler:
                 if last is not None and now - last > C.CLOUDTIK_HEARTBEAT_TIMEOUT_S and now - started > C.CLOUDTIK_HEARTBEAT_TIMEOUT_S:
                     self._log(f"node {n} lost heartbeat for {now - last:.0f}s: recovering")
                     self._spawn_updater(n, recovery=True)
+                    continue
+                self._check_gpu_health(n, now, to_replace)
+        if to_replace:
+            # a GPU that keeps reporting uncorrectable errors / overheating is not fixed by
+            # restarting services: terminate the node; the next pass launches a replacement
+            self.provider.terminate_nodes(list(to_replace))
         self.publish_status()
+
+    def _check_gpu_health(self, n: str, now: float, to_replace: List[str]):
+        m = self.node_metrics().get(n) or self.node_metrics().get(self.provider.internal_ip(n) or "") or {}
+        if m.get("gpu_healthy", True):
+            self.gpu_unhealthy_since.pop(n, None)
+            return
+        since = self.gpu_unhealthy_since.setdefault(n, now)
+        if now - since >= C.CLOUDTIK_GPU_UNHEALTHY_TIMEOUT_S:
+            self._log(f"node {n} GPUs unhealthy for {now - since:.0f}s "
+                      f"({'; '.join(m.get('gpu_health_issues') or [])}): replacing")
+            self.gpu_unhealthy_since.pop(n, None)
+            to_replace.append(n)
 
     def _free_resources(self, unused: Dict[str, Dict]) -> Dict[str, Dict]:
         # without per-task accounting the free capacity of a node is its static resources

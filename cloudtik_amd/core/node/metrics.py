@@ -4,6 +4,13 @@ through GPUtil).  AMD GPUs are sampled from the amdgpu sysfs files of each card
 (``gpu_busy_percent``, ``mem_info_vram_used/total``, hwmon temperature / power), which
 cost microseconds and need no SMI library; ``amdsmi`` is used when importable for fields
 sysfs lacks.
+
+GPU health (SURVEY.md §5.3 "GPU health to NodeMonitor"): the amdgpu RAS counters under
+``device/ras/*_err_count`` ("ue: N" uncorrectable / "ce: M" correctable per IP block:
+umc = HBM, xgmi_wafl = xGMI links, gfx, sdma, mmhub, ...) and the edge/junction temperature
+against ``CLOUDTIK_GPU_HEALTH_TEMP_C`` give each GPU ``healthy`` + ``health_issues``; the
+node row carries ``gpu_healthy`` and the head's scaler recovers a node whose GPUs stay
+unhealthy (core/head/scaler.py).
 """
 from __future__ import annotations
 
@@ -46,6 +53,40 @@ def amd_gpu_cards(root: str = DRM_ROOT) -> List[str]:
     return out
 
 
+def ras_counts(dev: str) -> Dict[str, Dict[str, int]]:
+    """{block: {"ue": n, "ce": m}} from ``<dev>/ras/<block>_err_count``."""
+    out: Dict[str, Dict[str, int]] = {}
+    for f in sorted(glob.glob(os.path.join(dev, "ras", "*_err_count"))):
+        block = os.path.basename(f)[:-len("_err_count")]
+        txt = _read(f) or ""
+        cnt: Dict[str, int] = {}
+        for line in txt.splitlines():
+            k, _, v = line.partition(":")
+            try:
+                cnt[k.strip()] = int(v.strip())
+            except ValueError:
+                continue
+        if cnt:
+            out[block] = cnt
+    return out
+
+
+def gpu_health(g: Dict[str, Any], temp_limit_c: Optional[float] = None) -> List[str]:
+    """Reasons this GPU is unhealthy (empty list = healthy)."""
+    from cloudtik_amd.core import constants as C
+    limit = C.CLOUDTIK_GPU_HEALTH_TEMP_C if temp_limit_c is None else temp_limit_c
+    issues = []
+    for block, cnt in (g.get("ras") or {}).items():
+        if cnt.get("ue", 0) > 0:
+            issues.append(f"{block}: {cnt['ue']} uncorrectable error(s)")
+    t = g.get("temperature_c")
+    if t is not None and t >= limit:
+        issues.append(f"temperature {t:.0f}C >= {limit}C")
+    if g.get("vram_total") in (None, 0):
+        issues.append("VRAM not reported (device lost?)")
+    return issues
+
+
 def gpu_metrics(root: str = DRM_ROOT) -> List[Dict[str, Any]]:
     gpus = []
     for i, card in enumerate(amd_gpu_cards(root)):
@@ -64,6 +105,14 @@ def gpu_metrics(root: str = DRM_ROOT) -> List[Dict[str, Any]]:
             pw = _read_int(os.path.join(hw[0], "power1_average")) or _read_int(os.path.join(hw[0], "power1_input"))
             g["temperature_c"] = t / 1000.0 if t is not None else None
             g["power_w"] = pw / 1e6 if pw is not None else None
+            # the hottest sensor (junction / HBM) when the driver exposes several
+            temps = [_read_int(p) for p in glob.glob(os.path.join(hw[0], "temp*_input"))]
+            temps = [v for v in temps if v is not None]
+            if temps:
+                g["temperature_max_c"] = max(temps) / 1000.0
+        g["ras"] = ras_counts(dev)
+        g["health_issues"] = gpu_health(dict(g, temperature_c=g.get("temperature_max_c", g.get("temperature_c"))))
+        g["healthy"] = not g["health_issues"]
         gpus.append(g)
     return gpus
 
@@ -103,4 +152,6 @@ class NodeMetricsCollector:
             "network_tx_bytes_per_s": tx_rate,
             "gpus": gpus,
             "gpu_busy_percent_avg": (sum(g["busy_percent"] or 0 for g in gpus) / len(gpus)) if gpus else None,
+            "gpu_healthy": all(g["healthy"] for g in gpus),
+            "gpu_health_issues": [f"gpu{g['index']}: {i}" for g in gpus for i in g["health_issues"]],
         }

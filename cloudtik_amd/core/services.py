@@ -7,6 +7,20 @@ Every daemon is a child process in its own session with its output in
 so ``cloudtik node stop`` terminates exactly the processes this node started (never by
 name pattern).  The session directory is ``$CLOUDTIK_SESSION_DIR`` or
 ``~/.cloudtik/session``.
+
+Debug / profiling wrappers (reference services.py:246-339), keyed by the process name in
+upper case (``STATE_SERVER``, ``CONTROLLER``, ``NODE_MONITOR``, ...):
+
+* ``CLOUDTIK_<PROC>_VALGRIND=1``            valgrind memcheck (leak check, error exit code)
+* ``CLOUDTIK_<PROC>_VALGRIND_PROFILER=1``   valgrind callgrind
+* ``CLOUDTIK_<PROC>_PERFTOOLS_PROFILER=1``  gperftools CPU profiler (``LD_PRELOAD=$PERFTOOLS_PATH``,
+  ``CPUPROFILE=<logs>/<name>.prof``)
+* ``CLOUDTIK_<PROC>_GDB=1``                 run under gdb inside a detached tmux session
+* ``CLOUDTIK_<PROC>_TMUX=1``                run inside a detached tmux session
+* ``CLOUDTIK_JEMALLOC_PATH`` (+ ``CLOUDTIK_JEMALLOC_CONF``, ``CLOUDTIK_JEMALLOC_PROFILE=<proc>``)
+  preload jemalloc (with heap profiling for the named process)
+
+``fate_share=True`` makes the child die with its parent (``PR_SET_PDEATHSIG``).
 """
 from __future__ import annotations
 
@@ -64,7 +78,61 @@ def pid_alive(pid: int) -> bool:
         return True
 
 
-def start_process(name: str, argv: List[str], env: Optional[Dict[str, str]] = None) -> int:
+def _flag(name: str, what: str, environ=None) -> bool:
+    environ = os.environ if environ is None else environ
+    return environ.get(f"CLOUDTIK_{name.upper().replace('-', '_')}_{what}", "0") not in ("", "0", "false")
+
+
+def wrap_command(name: str, argv: List[str], env: Dict[str, str]) -> List[str]:
+    """Apply the debug/profiling wrapper requested for process ``name`` (see module doc).
+    Mutates ``env`` (preloads, profiler output) and returns the argv to execute."""
+    import shutil
+
+    def need(tool):
+        path = shutil.which(tool)
+        if path is None:
+            raise RuntimeError(f"{name}: a {tool} wrapper was requested but {tool} is not installed")
+        return path
+
+    jemalloc = env.get("CLOUDTIK_JEMALLOC_PATH")
+    if jemalloc:
+        env["LD_PRELOAD"] = (jemalloc + " " + env.get("LD_PRELOAD", "")).strip()
+        conf = env.get("CLOUDTIK_JEMALLOC_CONF", "")
+        if env.get("CLOUDTIK_JEMALLOC_PROFILE") == name:
+            conf = ",".join(x for x in (conf, f"prof:true,prof_prefix:{os.path.join(logs_dir(), name)}") if x)
+        if conf:
+            env["MALLOC_CONF"] = conf
+    if _flag(name, "VALGRIND", env):
+        argv = [need("valgrind"), "--leak-check=full", "--show-leak-kinds=definite", "--error-exitcode=1",
+                f"--log-file={os.path.join(logs_dir(), name)}.valgrind.%p"] + argv
+    elif _flag(name, "VALGRIND_PROFILER", env):
+        argv = [need("valgrind"), "--tool=callgrind",
+                f"--callgrind-out-file={os.path.join(logs_dir(), name)}.callgrind.%p"] + argv
+    elif _flag(name, "PERFTOOLS_PROFILER", env):
+        lib = env.get("PERFTOOLS_PATH")
+        if not lib:
+            raise RuntimeError(f"{name}: PERFTOOLS_PROFILER needs PERFTOOLS_PATH (libprofiler.so)")
+        env["LD_PRELOAD"] = (lib + " " + env.get("LD_PRELOAD", "")).strip()
+        env["CPUPROFILE"] = os.path.join(logs_dir(), f"{name}.prof")
+    if _flag(name, "GDB", env):
+        argv = [need("gdb"), "-ex", "run", "--args"] + argv
+    if _flag(name, "GDB", env) or _flag(name, "TMUX", env):
+        import shlex
+        argv = [need("tmux"), "new-session", "-d", "-s", f"cloudtik_{name}",
+                " ".join(shlex.quote(a) for a in argv)]
+    return argv
+
+
+def _pdeathsig():
+    try:
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
+def start_process(name: str, argv: List[str], env: Optional[Dict[str, str]] = None,
+                  fate_share: bool = False) -> int:
     existing = read_pid(name)
     if existing and pid_alive(existing):
         return existing
@@ -73,8 +141,10 @@ def start_process(name: str, argv: List[str], env: Optional[Dict[str, str]] = No
     e = _child_env()
     if env:
         e.update(env)
+    argv = wrap_command(name, list(argv), e)
     p = subprocess.Popen(argv, stdout=out, stderr=err, stdin=subprocess.DEVNULL, env=e,
-                         start_new_session=True, cwd=session_dir())
+                         start_new_session=True, cwd=session_dir(),
+                         preexec_fn=_pdeathsig if fate_share else None)
     with open(_pid_file(name), "w") as f:
         json.dump({"pid": p.pid, "argv": argv, "started": time.time()}, f)
     return p.pid

@@ -303,8 +303,11 @@ class StateServer:
 
     def __init__(self, port: int = 6789, bind: str = "127.0.0.1", password: Optional[str] = None,
                  data_dir: Optional[str] = None, save_interval: int = 0,
-                 log_file: Optional[str] = None):
+                 log_file: Optional[str] = None, sanitize: Optional[bool] = None):
         self.port, self.bind, self.password = int(port), bind, password
+        # ASan/UBSan build of the server: sanitize=True or
+        # CLOUDTIK_STATE_SERVER_SANITIZE=1
+        self.sanitize = os.environ.get("CLOUDTIK_STATE_SERVER_SANITIZE", "0") == "1" if sanitize is None else sanitize
         self.data_dir = data_dir or os.getcwd()
         self.save_interval = save_interval
         self.log_file = log_file
@@ -318,7 +321,7 @@ class StateServer:
     def start(self, wait: float = 10.0) -> "StateServer":
         from cloudtik_amd.native.build import state_server_path
         os.makedirs(self.data_dir, exist_ok=True)
-        cmd = [state_server_path(), "--port", str(self.port), "--bind", self.bind,
+        cmd = [state_server_path(sanitize=self.sanitize), "--port", str(self.port), "--bind", self.bind,
                "--dir", self.data_dir, "--save-interval", str(self.save_interval)]
         if self.password:
             cmd += ["--requirepass", self.password]

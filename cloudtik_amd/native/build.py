@@ -27,7 +27,8 @@ def build(force: bool = False, verbose: bool = True, sanitize: bool = False):
         if force or not os.path.exists(out) or os.path.getmtime(out) < newest:
             flags = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter"]
             if sanitize:
-                flags = ["-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
+                flags = ["-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                         "-fno-sanitize-recover=undefined"]
             cmd = ["g++", *flags, *srcs, "-o", out + ".tmp"]
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
             if r.returncode != 0:
@@ -39,10 +40,10 @@ def build(force: bool = False, verbose: bool = True, sanitize: bool = False):
     return outs
 
 
-def state_server_path() -> str:
-    p = os.path.join(BIN, "cloudtik-state-server")
+def state_server_path(sanitize: bool = False) -> str:
+    p = os.path.join(BIN, "cloudtik-state-server" + ("-asan" if sanitize else ""))
     if not os.path.exists(p):
-        build(verbose=False)
+        build(verbose=False, sanitize=sanitize)
     return p
 
 

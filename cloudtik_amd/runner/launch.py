@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import argparse
+import os
 import sys
 
 from cloudtik_amd.runner.distributor import Distributor
@@ -41,6 +42,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--log-file-prefix", "--log_file_prefix", default="run")
     p.add_argument("--no-bind-cpus", dest="bind_cpus", action="store_false",
                    help="Do not pin ranks to their GPU's NUMA-node cores.")
+    p.add_argument("--max-restarts", "--max_restarts", type=int, default=0,
+                   help="Restart the whole job up to N times after a rank fails; ranks see "
+                        "CLOUDTIK_RESTART_COUNT / CLOUDTIK_RESUME=1 and resume from their checkpoint.")
+    p.add_argument("--resume", action="store_true",
+                   help="Ask the program to resume from its latest checkpoint (CLOUDTIK_RESUME=1).")
+    p.add_argument("--profile", default="",
+                   help="Run every rank under 'rocprofv3 --kernel-trace --stats'; output in DIR/rank<R>.")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("program")
     p.add_argument("program_args", nargs=argparse.REMAINDER)
@@ -52,7 +60,22 @@ def main(argv=None) -> int:
     d = Distributor(args.num_proc, args.nnodes, args.nproc_per_node, args.hosts or None, args.hostfile or None)
     launcher = args.launcher or ("distributed" if d.distributed_with_hosts and d.nnodes > 1 else "local")
     args.launcher = launcher
-    rc = create_launcher(launcher, args, d).run()
+    if args.resume:
+        os.environ["CLOUDTIK_RESUME"] = "1"
+    base_port = args.master_port
+    rc = 0
+    for attempt in range(max(0, args.max_restarts) + 1):
+        os.environ["CLOUDTIK_RESTART_COUNT"] = str(attempt)
+        if attempt:
+            os.environ["CLOUDTIK_RESUME"] = "1"
+            # a fresh rendezvous port: the previous attempt's store may still be in TIME_WAIT
+            args.master_port = base_port + attempt
+            print(f"[cloudtik-run] restarting the job (attempt {attempt + 1} of {args.max_restarts + 1}) "
+                  f"after exit code {rc}", file=sys.stderr)
+        rc = create_launcher(launcher, args, d).run()
+        if rc == 0 or args.node_rank or args.first_rank:
+            # remote node launchers do not restart on their own: the driver restarts the job
+            break
     return rc
 
 

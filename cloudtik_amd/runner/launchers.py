@@ -112,6 +112,12 @@ class LocalLauncher(Launcher):
         for lr in range(self.local_world):
             cpus = cpu_sets.get(lr)
             env = self.rank_env(lr, cpus)
+            argv = prog
+            if getattr(self.args, "profile", ""):
+                # rocprofv3 per rank; the program follows '--' directly (no shell/env hop)
+                from cloudtik_amd.utils.profiling import rocprof_command
+                argv = rocprof_command(prog, os.path.join(os.path.abspath(self.args.profile),
+                                                          f"rank{self.first_rank + lr}"))
             out = None
             if log_dir:
                 rank = self.first_rank + lr
@@ -126,7 +132,7 @@ class LocalLauncher(Launcher):
             if self.args.verbose:
                 print(f"[cloudtik-run] rank {env['RANK']} (local {lr}) cpus={cpus}: {' '.join(prog)}",
                       file=sys.stderr)
-            self.procs.append(subprocess.Popen(prog, env=env, stdout=out, stderr=subprocess.STDOUT if out else None,
+            self.procs.append(subprocess.Popen(argv, env=env, stdout=out, stderr=subprocess.STDOUT if out else None,
                                                preexec_fn=pre, start_new_session=True))
             reaper.watch(self.procs[-1].pid)          # the rank leads its own process group
         prev = {s: signal.getsignal(s) for s in (signal.SIGINT, signal.SIGTERM)}
@@ -178,6 +184,8 @@ class DistributedLauncher(Launcher):
             parts += ["--log-dir", a.log_dir, "--log-file-prefix", a.log_file_prefix]
         if not a.bind_cpus:
             parts.append("--no-bind-cpus")
+        if getattr(a, "profile", ""):
+            parts += ["--profile", a.profile]
         parts += [a.program] + list(a.program_args)
         keep = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "CLOUDTIK_",
                                                                        "TORCH_", "PYTHONPATH", "MIOPEN_"))}

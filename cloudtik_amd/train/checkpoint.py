@@ -8,7 +8,12 @@ BERT's (commented-out) resume path, SURVEY.md §5 "checkpoint/resume").
   so a crash never leaves a half-written "latest" checkpoint;
 * ``load_latest`` restores model, optimizer, scheduler and RNG (torch CPU/GPU + the
   dropout Philox stream of cloudtik_amd.ops) and returns the metadata;
-* only tensors / numbers / strings are stored, loaded with ``weights_only=True``.
+* only tensors / numbers / strings are stored, loaded with ``weights_only=True``;
+* ``save_async``: the device state is copied into reused pinned host buffers on a side HIP
+  stream (the compute stream waits on that copy only, not on the host), and a writer thread
+  serialises the files.  Completion is agreed through per-rank marker files instead of a
+  collective, so no collective ever runs off the main thread; rank 0 commits (meta.json +
+  rename) once every rank's marker is present.
 """
 from __future__ import annotations
 
@@ -16,6 +21,8 @@ import json
 import os
 import re
 import shutil
+import threading
+import time
 from typing import Any, Dict, Optional
 
 import torch
@@ -81,6 +88,98 @@ class Checkpointer:
         _barrier()
         return final
 
+    # ------------------------------------------------------------------ async save
+    def _pinned_copy(self, obj, stream, key=""):
+        if isinstance(obj, torch.Tensor):
+            t = obj.detach()
+            if t.device.type != "cuda":
+                return t.clone()
+            buf = self._pinned.get(key)
+            if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
+                buf = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                self._pinned[key] = buf
+            with torch.cuda.stream(stream):
+                buf.copy_(t, non_blocking=True)
+            return buf
+        if isinstance(obj, dict):
+            return {k: self._pinned_copy(v, stream, f"{key}/{k}") for k, v in obj.items()}
+        if isinstance(obj, (list, tuple)):
+            return type(obj)(self._pinned_copy(v, stream, f"{key}/{i}") for i, v in enumerate(obj))
+        return obj
+
+    def save_async(self, step: int, model: torch.nn.Module, optimizer=None, scheduler=None, epoch: int = 0,
+                   extra: Optional[Dict[str, Any]] = None, timeout: float = 1800.0) -> "PendingSave":
+        prev = getattr(self, "_inflight", None)
+        if prev is not None:
+            prev.wait()                         # pinned buffers are reused: one save in flight
+        if not hasattr(self, "_pinned"):
+            self._pinned = {}
+        rank, world = _rank_world()
+        final = os.path.join(self.dir, f"step-{step}")
+        tmp = final + ".tmp"
+        if rank == 0:
+            shutil.rmtree(tmp, ignore_errors=True)
+            os.makedirs(tmp, exist_ok=True)
+        _barrier()
+        event = None
+        cuda = torch.cuda.is_available() and torch.cuda.is_initialized()
+        stream = None
+        if cuda:
+            stream = torch.cuda.Stream()
+            stream.wait_stream(torch.cuda.current_stream())
+        snap = {"model": model.state_dict() if rank == 0 else None,
+                "optim": optimizer.state_dict() if optimizer is not None else None}
+        if stream is not None:
+            snap = self._pinned_copy(snap, stream, "s")
+            event = torch.cuda.Event()
+            event.record(stream)
+            # later optimizer steps must not overwrite the tensors while they are copied
+            torch.cuda.current_stream().wait_event(event)
+        else:
+            snap = self._pinned_copy(snap, None, "s")
+        sched = scheduler.state_dict() if (rank == 0 and scheduler is not None
+                                           and hasattr(scheduler, "state_dict")) else None
+        rng = _rng_state()
+        meta = {"step": step, "epoch": epoch, "world_size": world, "extra": extra or {}}
+        pending = PendingSave(final)
+
+        def write():
+            try:
+                if event is not None:
+                    event.synchronize()
+                if rank == 0:
+                    torch.save(snap["model"], os.path.join(tmp, "model.pt"))
+                    if sched is not None:
+                        torch.save(sched, os.path.join(tmp, "scheduler.pt"))
+                if snap["optim"] is not None:
+                    torch.save(snap["optim"], os.path.join(tmp, f"optim-rank{rank}.pt"))
+                torch.save(rng, os.path.join(tmp, f"rng-rank{rank}.pt"))
+                open(os.path.join(tmp, f"done-rank{rank}"), "w").close()
+                if rank == 0:
+                    deadline = time.time() + timeout
+                    while not all(os.path.exists(os.path.join(tmp, f"done-rank{r}")) for r in range(world)):
+                        if time.time() > deadline:
+                            raise TimeoutError(f"ranks did not finish checkpoint {final}")
+                        time.sleep(0.05)
+                    for r in range(world):
+                        os.remove(os.path.join(tmp, f"done-rank{r}"))
+                    with open(os.path.join(tmp, "meta.json"), "w") as f:
+                        json.dump(meta, f)
+                    if os.path.exists(final):
+                        shutil.rmtree(final)
+                    os.replace(tmp, final)
+                    for old in self.steps()[:-self.keep] if self.keep else []:
+                        shutil.rmtree(os.path.join(self.dir, f"step-{old}"), ignore_errors=True)
+            except BaseException as e:  # noqa: BLE001 - surfaced by wait()
+                pending.error = e
+            finally:
+                pending.done.set()
+
+        pending.thread = threading.Thread(target=write, name=f"ckpt-{step}", daemon=True)
+        pending.thread.start()
+        self._inflight = pending
+        return pending
+
     # ------------------------------------------------------------------ load
     def load(self, step: int, model: torch.nn.Module, optimizer=None, scheduler=None,
              map_location="cpu", strict: bool = True) -> Dict[str, Any]:
@@ -110,6 +209,23 @@ class Checkpointer:
         if s is None:
             return None
         return self.load(s, model, optimizer, scheduler, **kw)
+
+
+class PendingSave:
+    """Handle of an in-flight ``save_async``; ``wait()`` re-raises a writer error.  On
+    rank != 0 it completes when this rank's files are written (rank 0 commits)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.done = threading.Event()
+        self.error: Optional[BaseException] = None
+        self.thread: Optional[threading.Thread] = None
+
+    def wait(self, timeout: Optional[float] = None) -> str:
+        self.done.wait(timeout)
+        if self.error is not None:
+            raise self.error
+        return self.path
 
 
 def _to_cpu(obj):

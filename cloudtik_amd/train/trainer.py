@@ -24,6 +24,8 @@ from typing import Any, Callable, Dict, Iterable, List, Optional
 import torch
 import torch.distributed as dist
 
+from cloudtik_amd.utils.fault import maybe_fail
+
 logger = logging.getLogger(__name__)
 
 
@@ -103,7 +105,9 @@ class Trainer:
                  lr_scheduler: Optional[Callable] = None, grad_accum: int = 1, clip_norm: Optional[float] = None,
                  checkpoint_dir: Optional[str] = None, checkpoint_every: int = 0, resume: bool = True,
                  log_every: int = 50, bucket_mb: float = 64.0, no_decay: Optional[Callable[[str], bool]] = None,
-                 callbacks: Optional[List[Callable]] = None, optimizer_kwargs: Optional[Dict] = None):
+                 callbacks: Optional[List[Callable]] = None, optimizer_kwargs: Optional[Dict] = None,
+                 step_timing: Optional[bool] = None, async_checkpoint: bool = False,
+                 metrics_port: Optional[int] = None):
         from cloudtik_amd.parallel import GradBucketer, broadcast_flat_params
         from cloudtik_amd.train.optim import build_optimizer
         self.rank, self.world, self.device = setup_distributed()
@@ -135,7 +139,16 @@ class Trainer:
             from cloudtik_amd.train.checkpoint import Checkpointer
             self.checkpointer = Checkpointer(checkpoint_dir)
         self.checkpoint_every = checkpoint_every
+        self.async_checkpoint = async_checkpoint
+        self._pending_save = None
+        from cloudtik_amd.utils.profiling import StepTimer
+        if step_timing is None:
+            step_timing = os.environ.get("CLOUDTIK_STEP_TIMING", "0") == "1"
+        self.timer = StepTimer(self.device, enabled=step_timing)
+        self.metrics = TrainMetrics.maybe_start(metrics_port, self.rank)
         self.global_step, self.start_epoch = 0, 0
+        self._skip_batches = 0
+        self._epoch_batches = 0
         self.history: List[Dict[str, float]] = []
         if self.checkpointer is not None and resume:
             meta = self.checkpointer.load_latest(self.model, self.optimizer, self.scheduler,
@@ -144,6 +157,8 @@ class Trainer:
                 # parameters are views of the flat buffer, so load_state_dict already wrote
                 # it; the fp32 master shard comes back with the optimizer state
                 self.global_step, self.start_epoch = meta["step"], meta["epoch"]
+                # a mid-epoch checkpoint: skip the micro-batches that epoch already consumed
+                self._skip_batches = int(meta.get("extra", {}).get("batches_in_epoch", 0))
                 if self.rank == 0:
                     logger.info("resumed from step %d (epoch %d)", self.global_step, self.start_epoch)
 
@@ -181,35 +196,51 @@ class Trainer:
             self._set_epoch(self.train_loader, epoch)
             sums: Dict[str, torch.Tensor] = {}
             count, t0, micro = 0, time.time(), 0
+            skip, self._skip_batches = self._skip_batches, 0
+            self._epoch_batches = 0
             for batch in self.train_loader:
+                self._epoch_batches += 1
+                if skip:
+                    skip -= 1
+                    continue
                 batch = _to_device(batch, self.device)
                 last_micro = (micro + 1) % self.grad_accum == 0
                 ctx = self.bucketer.no_sync() if (self.bucketer is not None and not last_micro) else _null()
                 with ctx:
-                    loss, metrics = self.step_fn(self.model, batch)
-                    loss.backward()
+                    with self.timer.phase("forward"):
+                        loss, metrics = self.step_fn(self.model, batch)
+                    with self.timer.phase("backward"):
+                        loss.backward()
                 micro += 1
                 for k, v in metrics.items():
                     sums[k] = sums.get(k, 0) + v.detach().float()
                 count += 1
                 if not last_micro:
                     continue
-                if self.bucketer is not None:
-                    self.bucketer.finish()
-                elif self.world > 1:
-                    for p in self.model.parameters():
-                        if p.grad is not None:
-                            dist.all_reduce(p.grad)
-                            p.grad.div_(self.world)
-                if self.clip_norm:
-                    self._clip()
-                self.optimizer.step()
-                if self.scheduler is not None:
-                    self.scheduler.step()
-                self.optimizer.zero_grad()
+                with self.timer.phase("comm"):
+                    if self.bucketer is not None:
+                        self.bucketer.finish()
+                    elif self.world > 1:
+                        for p in self.model.parameters():
+                            if p.grad is not None:
+                                dist.all_reduce(p.grad)
+                                p.grad.div_(self.world)
+                with self.timer.phase("optimizer"):
+                    if self.clip_norm:
+                        self._clip()
+                    self.optimizer.step()
+                    if self.scheduler is not None:
+                        self.scheduler.step()
+                    self.optimizer.zero_grad()
+                self.timer.step_done()
                 self.global_step += 1
+                maybe_fail(self.global_step, self.rank)
                 if self.log_every and self.global_step % self.log_every == 0:
                     m = self._reduce_metrics(sums, count)
+                    if self.timer.enabled:
+                        m.update({f"{k}_ms": v for k, v in self.timer.summary().items()})
+                    if self.metrics is not None:
+                        self.metrics.update(self.global_step, m)
                     if self.rank == 0:
                         logger.info("epoch %d step %d %s", epoch, self.global_step,
                                     " ".join(f"{k}={v:.4f}" for k, v in m.items()))
@@ -217,7 +248,7 @@ class Trainer:
                     cb(self, epoch, self.global_step)
                 if self.checkpointer is not None and self.checkpoint_every and \
                         self.global_step % self.checkpoint_every == 0:
-                    self.checkpointer.save(self.global_step, self.model, self.optimizer, self.scheduler, epoch)
+                    self._save(epoch, {"batches_in_epoch": self._epoch_batches})
                 if self.max_steps and self.global_step >= self.max_steps:
                     done = True
                     break
@@ -229,10 +260,22 @@ class Trainer:
             if self.rank == 0:
                 logger.info("epoch %d done: %s", epoch, m)
             if self.checkpointer is not None:
-                self.checkpointer.save(self.global_step, self.model, self.optimizer, self.scheduler, epoch + 1)
+                self._save(epoch + 1)
             if done:
                 break
+        if self._pending_save is not None:
+            self._pending_save.wait()
+            self._pending_save = None
         return self.history
+
+    def _save(self, epoch: int, extra: Optional[Dict] = None):
+        if not self.async_checkpoint:
+            self.checkpointer.save(self.global_step, self.model, self.optimizer, self.scheduler, epoch, extra)
+            return
+        if self._pending_save is not None:      # one checkpoint in flight at a time
+            self._pending_save.wait()
+        self._pending_save = self.checkpointer.save_async(self.global_step, self.model, self.optimizer,
+                                                          self.scheduler, epoch, extra)
 
     @torch.no_grad()
     def evaluate(self, loader: Optional[Iterable] = None) -> Dict[str, float]:
@@ -250,8 +293,51 @@ class Trainer:
         return self._reduce_metrics(sums, count)
 
     def close(self):
+        if self._pending_save is not None:
+            self._pending_save.wait()
+            self._pending_save = None
         if self.bucketer is not None:
             self.bucketer.remove()
+
+
+class TrainMetrics:
+    """Per-rank training metrics on a Prometheus endpoint (port ``base + rank``) for the
+    cluster's prometheus runtime to scrape (samples/s, step time, loss)."""
+
+    def __init__(self, port: int, rank: int):
+        from prometheus_client import CollectorRegistry, Gauge, start_http_server
+        self.registry = CollectorRegistry()
+        self.gauges = {}
+        self._Gauge = Gauge
+        self.rank = str(rank)
+        start_http_server(port, registry=self.registry)
+        self.port = port
+
+    @classmethod
+    def maybe_start(cls, port: Optional[int], rank: int):
+        if port is None:
+            v = os.environ.get("CLOUDTIK_TRAIN_METRICS_PORT")
+            port = int(v) if v else None
+        if not port:
+            return None
+        try:
+            return cls(port + rank, rank)
+        except Exception as e:  # noqa: BLE001 - metrics never stop training
+            logger.warning("training metrics endpoint disabled: %s", e)
+            return None
+
+    def update(self, step: int, values: Dict[str, float]):
+        values = dict(values, global_step=step)
+        for k, v in values.items():
+            name = "cloudtik_train_" + "".join(c if c.isalnum() else "_" for c in k)
+            g = self.gauges.get(name)
+            if g is None:
+                g = self.gauges[name] = self._Gauge(name, f"training metric {k}", ["rank"],
+                                                    registry=self.registry)
+            try:
+                g.labels(rank=self.rank).set(float(v))
+            except (TypeError, ValueError):
+                pass
 
 
 class _null:

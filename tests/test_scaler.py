@@ -237,3 +237,44 @@ def test_quorum_runtime_sets_up_complete_membership(state):
     qids = {provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_ID] for w in ws}
     assert len(qids) == 1
     assert all(provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_JOIN] == T.QUORUM_JOIN_STATUS_SUCCESS for w in ws)
+
+
+def test_unhealthy_gpu_node_is_replaced(state, monkeypatch):
+    """A worker whose GPUs keep reporting uncorrectable RAS errors is terminated and a
+    replacement is launched (SURVEY.md §5.3 GPU health)."""
+    from cloudtik_amd.core import constants as C
+    from cloudtik_amd.core.state.state_client import NODE_METRICS_TABLE, NODE_TABLE
+    name = "sc-gpuhealth"
+    cfg, provider, scaler = _setup(name, state, lambda c: c["available_node_types"]["gpu.mi355x"].update(min_workers=1))
+    scaler.update()
+    (n,) = _workers(provider, name)
+    monkeypatch.setattr(C, "CLOUDTIK_GPU_UNHEALTHY_TIMEOUT_S", 0)
+    state.table_put(NODE_TABLE, n, {"node_id": n, "node_ip": provider.internal_ip(n),
+                                    "last_heartbeat_time": time.time()})
+    state.table_put(NODE_METRICS_TABLE, n, {"node_id": n, "gpu_healthy": False,
+                                            "gpu_health_issues": ["gpu3: umc: 2 uncorrectable error(s)"]})
+    scaler.update()
+    assert any("GPUs unhealthy" in e and "umc" in e for e in scaler.events)
+    scaler.update()
+    now = _workers(provider, name)
+    assert n not in now and len(now) == 1
+
+
+def test_gpu_ras_health_from_sysfs(tmp_path):
+    from cloudtik_amd.core.node.metrics import gpu_metrics
+    card = tmp_path / "card0" / "device"
+    (card / "ras").mkdir(parents=True)
+    (card / "hwmon" / "hwmon0").mkdir(parents=True)
+    (card / "vendor").write_text("0x1002\n")
+    (card / "mem_info_vram_total").write_text(str(288 << 30))
+    (card / "mem_info_vram_used").write_text("0")
+    (card / "gpu_busy_percent").write_text("5")
+    (card / "hwmon" / "hwmon0" / "temp1_input").write_text("45000")
+    (card / "hwmon" / "hwmon0" / "temp2_input").write_text("61000")
+    (card / "ras" / "umc_err_count").write_text("ue: 0\nce: 3\n")
+    (card / "ras" / "xgmi_wafl_err_count").write_text("ue: 0\nce: 0\n")
+    (g,) = gpu_metrics(str(tmp_path))
+    assert g["healthy"] and g["ras"]["umc"] == {"ue": 0, "ce": 3} and g["temperature_max_c"] == 61.0
+    (card / "ras" / "xgmi_wafl_err_count").write_text("ue: 1\nce: 0\n")
+    (g,) = gpu_metrics(str(tmp_path))
+    assert not g["healthy"] and "xgmi_wafl" in g["health_issues"][0]

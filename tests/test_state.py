@@ -199,3 +199,41 @@ def test_distributed_lock_and_leader_election(server):
     e1.resign()                              # hand over
     e2.step()
     assert e2.is_leader() and events == ["1+", "1-", "2+"]
+
+
+def test_state_server_under_asan_ubsan(tmp_path):
+    """The state server built with -fsanitize=address,undefined serves a
+    concurrent KV / table / list / pub-sub / snapshot workload and exits without a report."""
+    import os
+    log = tmp_path / "asan.log"
+    os.environ.setdefault("ASAN_OPTIONS", "detect_leaks=1:abort_on_error=0")
+    srv = StateServer(port=_free_port(), data_dir=str(tmp_path), password="pw", log_file=str(log),
+                      sanitize=True).start(wait=60)
+    try:
+        errs = []
+
+        def worker(i):
+            try:
+                c = StateClient.create(srv.address, "pw")
+                for j in range(30):
+                    c.conn.incr("n")
+                    c.table_put("t", f"{i}-{j}", {"v": "x" * (j * 97)})
+                    c.conn.rpush("l", str(j))
+                c.table_get_all("t")
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+        sub = StateClient.create(srv.address, "pw")
+        ps = sub.conn
+        ps.execute("SUBSCRIBE", "ch")
+        ts = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        pub = StateClient.create(srv.address, "pw")
+        pub.conn.execute("PUBLISH", "ch", "hello")
+        pub.save()
+        assert not errs
+        assert int(pub.conn.get("n")) == 240
+    finally:
+        srv.stop()
+    text = log.read_text(errors="replace") if log.exists() else ""
+    assert "AddressSanitizer" not in text and "runtime error" not in text, text[-3000:]
