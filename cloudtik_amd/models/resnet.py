@@ -33,31 +33,58 @@ class BatchNormAct(nn.Module):
         self.register_buffer("running_mean", torch.zeros(C, device=device))
         self.register_buffer("running_var", torch.ones(C, device=device))
         self.relu, self.eps, self.momentum = relu, eps, momentum
+        self.frozen = False        # detection fine-tuning: running statistics only (FrozenBatchNorm)
 
     def forward(self, x, residual=None):
         return ops.batch_norm_act(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                  residual=residual, relu=self.relu, training=self.training,
+                                  residual=residual, relu=self.relu, training=self.training and not self.frozen,
                                   momentum=self.momentum, eps=self.eps)
 
 
-def _conv(cin, cout, k, stride=1, device=None, dtype=None):
-    c = nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False, device=device, dtype=torch.float32)
+def _conv(cin, cout, k, stride=1, device=None, dtype=None, groups=1, dilation=1):
+    c = nn.Conv2d(cin, cout, k, stride=stride, padding=dilation * (k // 2), bias=False, device=device,
+                  dtype=torch.float32, groups=groups, dilation=dilation)
     nn.init.kaiming_normal_(c.weight, mode="fan_out", nonlinearity="relu")
     return c.to(dtype) if dtype is not None else c
 
 
+class BasicBlock(nn.Module):
+    """Two 3x3 convolutions (ResNet-18/34; the SSD-ResNet34 backbone)."""
+    expansion = 1
+
+    def __init__(self, cin, width, stride=1, downsample=False, device=None, dtype=None, groups=1,
+                 base_width=64, dilation=1):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        self.conv1 = _conv(cin, width, 3, stride, dilation=dilation, **kw)
+        self.bn1 = BatchNormAct(width, **kw)
+        self.conv2 = _conv(width, width, 3, dilation=dilation, **kw)
+        self.bn2 = BatchNormAct(width, relu=True, zero_init=True, **kw)   # fused add + ReLU
+        self.down = None
+        if downsample:
+            self.down = _conv(cin, width, 1, stride, **kw)
+            self.down_bn = BatchNormAct(width, relu=False, **kw)
+
+    def forward(self, x):
+        idt = self.down_bn(self.down(x)) if self.down is not None else x
+        return self.bn2(self.conv2(self.bn1(self.conv1(x))), residual=idt)
+
+
 class Bottleneck(nn.Module):
+    """1x1 -> 3x3 (grouped for ResNeXt: ``groups`` x ``base_width``) -> 1x1, v1.5 stride."""
     expansion = 4
 
-    def __init__(self, cin, width, stride=1, downsample=False, device=None, dtype=None):
+    def __init__(self, cin, width, stride=1, downsample=False, device=None, dtype=None, groups=1,
+                 base_width=64, dilation=1):
         super().__init__()
         kw = dict(device=device, dtype=dtype)
         cout = width * self.expansion
-        self.conv1 = _conv(cin, width, 1, **kw)
-        self.bn1 = BatchNormAct(width, **kw)
-        self.conv2 = _conv(width, width, 3, stride, **kw)   # v1.5: stride on the 3x3
-        self.bn2 = BatchNormAct(width, **kw)
-        self.conv3 = _conv(width, cout, 1, **kw)
+        inner = int(width * (base_width / 64.0)) * groups
+        self.conv1 = _conv(cin, inner, 1, **kw)
+        self.bn1 = BatchNormAct(inner, **kw)
+        self.conv2 = _conv(inner, inner, 3, stride, groups=groups, dilation=dilation, **kw)  # v1.5
+        self.bn2 = BatchNormAct(inner, **kw)
+        self.conv3 = _conv(inner, cout, 1, **kw)
         self.bn3 = BatchNormAct(cout, relu=True, zero_init=True, **kw)  # fused add + ReLU
         self.down = None
         if downsample:
@@ -72,20 +99,28 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, device=None, dtype=torch.bfloat16):
+    """ResNet / ResNeXt family (torchvision-equivalent topology; ``features()`` returns the
+    C2..C5 maps for detection backbones)."""
+
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, device=None, dtype=torch.bfloat16,
+                 block=None, groups=1, width_per_group=64):
         super().__init__()
+        block = block or Bottleneck
         kw = dict(device=device, dtype=dtype)
         self.conv1 = _conv(3, 64, 7, 2, **kw)
         self.bn1 = BatchNormAct(64, **kw)
         cin = 64
         stages = []
+        self.stage_channels = []
         for i, (n, w) in enumerate(zip(layers, (64, 128, 256, 512))):
             blocks = []
             for j in range(n):
                 stride = 2 if (j == 0 and i > 0) else 1
-                blocks.append(Bottleneck(cin, w, stride, downsample=(j == 0), **kw))
-                cin = w * 4
+                down = j == 0 and (stride != 1 or cin != w * block.expansion)
+                blocks.append(block(cin, w, stride, downsample=down, groups=groups, base_width=width_per_group, **kw))
+                cin = w * block.expansion
             stages.append(nn.Sequential(*blocks))
+            self.stage_channels.append(cin)
         self.layer1, self.layer2, self.layer3, self.layer4 = stages
         fc = nn.Linear(cin, num_classes, device=device)
         bound = 1.0 / math.sqrt(cin)
@@ -95,16 +130,42 @@ class ResNet(nn.Module):
         if device is not None and torch.device(device).type == "cuda":
             self.to(memory_format=torch.channels_last)
 
+    def stem(self, x):
+        return F.max_pool2d(self.bn1(self.conv1(x)), 3, 2, 1)
+
+    def features(self, x):
+        """[C2, C3, C4, C5] (strides 4, 8, 16, 32)."""
+        c2 = self.layer1(self.stem(x))
+        c3 = self.layer2(c2)
+        c4 = self.layer3(c3)
+        return [c2, c3, c4, self.layer4(c4)]
+
     def forward(self, x):
-        x = self.bn1(self.conv1(x))
-        x = F.max_pool2d(x, 3, 2, 1)
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(self.stem(x)))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 
 
 def resnet50(num_classes=1000, device=None, dtype=torch.bfloat16):
     return ResNet((3, 4, 6, 3), num_classes, device=device, dtype=dtype)
+
+
+def resnet34(num_classes=1000, device=None, dtype=torch.bfloat16):
+    return ResNet((3, 4, 6, 3), num_classes, device=device, dtype=dtype, block=BasicBlock)
+
+
+def resnet101(num_classes=1000, device=None, dtype=torch.bfloat16):
+    return ResNet((3, 4, 23, 3), num_classes, device=device, dtype=dtype)
+
+
+def resnext50_32x4d(num_classes=1000, device=None, dtype=torch.bfloat16):
+    return ResNet((3, 4, 6, 3), num_classes, device=device, dtype=dtype, groups=32, width_per_group=4)
+
+
+def resnext101_32x16d(num_classes=1000, device=None, dtype=torch.bfloat16):
+    """ResNeXt101-32x16d (the reference's quickstart inference model,
+    applications/ai/quickstart/bin/resnext-32x16d*)."""
+    return ResNet((3, 4, 23, 3), num_classes, device=device, dtype=dtype, groups=32, width_per_group=16)
 
 
 def resnet18_like_small(num_classes=10, device=None, dtype=torch.float32):

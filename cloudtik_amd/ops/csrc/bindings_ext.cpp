@@ -16,6 +16,8 @@ int ct_interact_bwd(const void*, const void*, const void*, void*, void*, int, in
 int ct_nms(const float*, int, float, float, uint64_t*, int64_t*, int64_t*, hipStream_t);
 int ct_roi_align_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
 int ct_roi_align_bwd(const void*, const float*, float*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
+int ct_roi_align_nhwc_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
+int ct_roi_align_nhwc_bwd(const void*, const float*, float*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
 int ct_roi_pool_fwd(const void*, const float*, void*, int*, int, int, int, int, int, int, int, float, hipStream_t);
 int ct_roi_pool_bwd(const void*, const float*, const int*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ct_focal_fwd(const void*, const int64_t*, float*, int, long, int, float, float, hipStream_t);
@@ -193,6 +195,36 @@ at::Tensor roi_align_bwd(at::Tensor gout, at::Tensor rois, std::vector<int64_t> 
   return gout.scalar_type() == at::kFloat ? g : g.to(gout.scalar_type());
 }
 
+// channels_last features [N, C, H, W] (NHWC in memory) -> channels_last [K, C, PH, PW]
+at::Tensor roi_align_nhwc_fwd(at::Tensor feat, at::Tensor rois, double scale, int64_t PH, int64_t PW, int64_t sr,
+                              bool aligned) {
+  XCHECK_IN(rois); XCHECK_DT(rois, at::kFloat);
+  TORCH_CHECK(feat.is_cuda() && feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "roi_align_nhwc: features must be channels_last");
+  TORCH_CHECK(rois.is_contiguous() && rois.dim() == 2 && rois.size(1) == 5, "rois must be [K, 5]");
+  const int K = (int)rois.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
+  TORCH_CHECK(C % 8 == 0, "roi_align_nhwc: channels must be a multiple of 8");
+  auto out = at::empty({K, C, PH, PW}, feat.options(), at::MemoryFormat::ChannelsLast);
+  if (K) TORCH_CHECK(ct_roi_align_nhwc_fwd(feat.data_ptr(), rois.data_ptr<float>(), out.data_ptr(), fb(feat), K, C, H, W,
+                                           (int)PH, (int)PW, (float)scale, (int)sr, aligned ? 1 : 0, stream()) == 0);
+  return out;
+}
+
+at::Tensor roi_align_nhwc_bwd(at::Tensor gout, at::Tensor rois, std::vector<int64_t> fshape, double scale, int64_t sr,
+                              bool aligned) {
+  XCHECK_IN(rois);
+  TORCH_CHECK(fshape.size() == 4);
+  gout = gout.contiguous(at::MemoryFormat::ChannelsLast);
+  const int K = (int)rois.size(0), C = (int)fshape[1], H = (int)fshape[2], W = (int)fshape[3];
+  TORCH_CHECK(gout.dim() == 4 && gout.size(0) == K && gout.size(1) == C && C % 8 == 0);
+  // (at::zeros drops TensorOptions' memory format: allocate channels_last, then clear)
+  auto g = at::empty(fshape, gout.options().dtype(at::kFloat), at::MemoryFormat::ChannelsLast).zero_();
+  if (K) TORCH_CHECK(ct_roi_align_nhwc_bwd(gout.data_ptr(), rois.data_ptr<float>(), g.data_ptr<float>(), fb(gout), K, C,
+                                           H, W, (int)gout.size(2), (int)gout.size(3), (float)scale, (int)sr,
+                                           aligned ? 1 : 0, stream()) == 0);
+  return gout.scalar_type() == at::kFloat ? g : g.to(gout.scalar_type());
+}
+
 std::vector<at::Tensor> roi_pool_fwd(at::Tensor feat, at::Tensor rois, double scale, int64_t PH, int64_t PW) {
   check_rois(feat, rois);
   const int K = (int)rois.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
@@ -337,6 +369,8 @@ void register_ext(pybind11::module& m) {
   m.def("nms_sorted", &nms_sorted);
   m.def("roi_align_fwd", &roi_align_fwd);
   m.def("roi_align_bwd", &roi_align_bwd);
+  m.def("roi_align_nhwc_fwd", &roi_align_nhwc_fwd);
+  m.def("roi_align_nhwc_bwd", &roi_align_nhwc_bwd);
   m.def("roi_pool_fwd", &roi_pool_fwd);
   m.def("roi_pool_bwd", &roi_pool_bwd);
   m.def("focal_fwd", &focal_fwd);

@@ -203,6 +203,30 @@ class _BNActFn(torch.autograd.Function):
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None
 
 
+class _BNAffineFn(torch.autograd.Function):
+    """Frozen BatchNorm (running statistics) + residual + ReLU with autograd: the forward is
+    the fused ``bn_apply`` HIP kernel; the backward is ``dy * relu_mask * scale`` (the affine
+    parameters are frozen, so no parameter gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, a, b, residual, relu):
+        res = residual.contiguous(memory_format=torch.channels_last) if (residual is not None and x.dim() == 4) \
+            else residual
+        y = _C().bn_apply(x, res, a, b, bool(relu))
+        ctx.save_for_backward(y if relu else torch.empty(0), a)
+        ctx.cfg = (relu, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, a = ctx.saved_tensors
+        relu, has_res = ctx.cfg
+        g = dy * (y > 0) if relu else dy
+        shape = (1, -1, 1, 1) if dy.dim() == 4 else (1, -1)
+        dx = g * a.view(shape).to(g.dtype)
+        return dx, None, None, (g if has_res else None), None
+
+
 def _bn_native_ok(x):
     if x.dtype != torch.bfloat16 or x.dim() not in (2, 4):
         return False
@@ -225,6 +249,12 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, residual=None, re
         b = bias.float() - running_mean * a
         res = residual.contiguous(memory_format=torch.channels_last) if (residual is not None and x.dim() == 4) else residual
         return _C().bn_apply(x, res, a.contiguous(), b.contiguous(), bool(relu))
+    if _native(x) and _bn_native_ok(x) and not training and not (weight.requires_grad or bias.requires_grad):
+        # frozen BN inside a trained network (detection backbones)
+        with torch.no_grad():
+            a = (weight.float() * torch.rsqrt(running_var + eps)).contiguous()
+            b = (bias.float() - running_mean * a).contiguous()
+        return _BNAffineFn.apply(x, a, b, residual, bool(relu))
     if x.dtype != running_mean.dtype:
         y = torch.nn.functional.batch_norm(x.float(), running_mean, running_var, weight.float(), bias.float(),
                                            training, momentum, eps).to(x.dtype)

@@ -126,12 +126,77 @@ class _RoiAlignFn(torch.autograd.Function):
                 None, None, None, None, None)
 
 
+class _RoiAlignNHWCFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois, output_size, scale, sr, aligned):
+        rois = rois.float().contiguous()
+        ctx.save_for_backward(rois)
+        ctx.meta = (list(feat.shape), scale, sr, aligned)
+        return _native().roi_align_nhwc_fwd(feat, rois, scale, output_size[0], output_size[1], sr, aligned)
+
+    @staticmethod
+    def backward(ctx, g):
+        (rois,) = ctx.saved_tensors
+        shape, scale, sr, aligned = ctx.meta
+        return (_native().roi_align_nhwc_bwd(g, rois, shape, scale, sr, aligned), None, None, None, None, None)
+
+
+def roi_align_vectorized(feat, rois, output_size, spatial_scale=1.0, sampling_ratio=2, aligned=False):
+    """Vectorised (autograd-differentiable) ROIAlign for a fixed ``sampling_ratio`` > 0: the
+    CPU path of detection models (same sampling rule as ``roi_align_reference``)."""
+    PH, PW = output_size
+    K = rois.shape[0]
+    N, C, H, W = feat.shape
+    if K == 0:
+        return feat.new_zeros(0, C, PH, PW)
+    g = int(sampling_ratio)
+    off = 0.5 if aligned else 0.0
+    r = rois.float()
+    b = r[:, 0].long()
+    x0, y0 = r[:, 1] * spatial_scale - off, r[:, 2] * spatial_scale - off
+    rw, rh = r[:, 3] * spatial_scale - off - x0, r[:, 4] * spatial_scale - off - y0
+    if not aligned:
+        rw, rh = rw.clamp(min=1.0), rh.clamp(min=1.0)
+    frac_y = (torch.arange(PH * g, device=feat.device, dtype=torch.float32) + 0.5) / (PH * g)
+    frac_x = (torch.arange(PW * g, device=feat.device, dtype=torch.float32) + 0.5) / (PW * g)
+    ys = y0[:, None] + frac_y[None] * rh[:, None]            # [K, PH*g]
+    xs = x0[:, None] + frac_x[None] * rw[:, None]            # [K, PW*g]
+    yy = ys[:, :, None].expand(K, PH * g, PW * g)
+    xx = xs[:, None, :].expand(K, PH * g, PW * g)
+    valid = (yy >= -1) & (yy <= H) & (xx >= -1) & (xx <= W)
+    yy, xx = yy.clamp(min=0), xx.clamp(min=0)
+    y0i, x0i = yy.floor().long(), xx.floor().long()
+    ycap, xcap = y0i >= H - 1, x0i >= W - 1
+    y0i, x0i = torch.where(ycap, H - 1, y0i), torch.where(xcap, W - 1, x0i)
+    yy, xx = torch.where(ycap, y0i.float(), yy), torch.where(xcap, x0i.float(), xx)
+    y1i, x1i = torch.where(ycap, y0i, y0i + 1), torch.where(xcap, x0i, x0i + 1)
+    ly, lx = yy - y0i, xx - x0i
+    hy, hx = 1 - ly, 1 - lx
+    f = feat.permute(0, 2, 3, 1).reshape(N * H * W, C).float()
+    base = (b * H * W)[:, None, None]
+
+    def tap(yi, xi):
+        return f[(base + yi * W + xi).reshape(-1)].reshape(K, PH * g, PW * g, C)
+    v = ((hy * hx)[..., None] * tap(y0i, x0i) + (hy * lx)[..., None] * tap(y0i, x1i)
+         + (ly * hx)[..., None] * tap(y1i, x0i) + (ly * lx)[..., None] * tap(y1i, x1i))
+    v = v * valid[..., None]
+    v = v.reshape(K, PH, g, PW, g, C).mean(dim=(2, 4))
+    return v.permute(0, 3, 1, 2).to(feat.dtype)
+
+
 def roi_align(feat, rois, output_size, spatial_scale: float = 1.0, sampling_ratio: int = -1, aligned: bool = False):
     """feat [N, C, H, W]; rois [K, 5] = (batch_idx, x1, y1, x2, y2) -> [K, C, PH, PW]."""
     if isinstance(output_size, int):
         output_size = (output_size, output_size)
     if feat.is_cuda and _use_native(feat):
+        if feat.dim() == 4 and feat.shape[1] % 8 == 0 and feat.shape[1] > 1 and \
+                feat.is_contiguous(memory_format=torch.channels_last):
+            # NHWC maps (FPN pyramids): vectorised channel-contiguous kernel, channels_last output
+            return _RoiAlignNHWCFn.apply(feat, rois, tuple(output_size), float(spatial_scale), int(sampling_ratio),
+                                         bool(aligned))
         return _RoiAlignFn.apply(feat, rois, tuple(output_size), float(spatial_scale), int(sampling_ratio), bool(aligned))
+    if sampling_ratio > 0:
+        return roi_align_vectorized(feat, rois, output_size, spatial_scale, sampling_ratio, aligned)
     return roi_align_reference(feat, rois, output_size, spatial_scale, sampling_ratio, aligned).to(feat.dtype)
 
 

@@ -29,6 +29,21 @@ SEG = 8192
 ALIGN = 64
 
 
+def _memory_order(t: torch.Tensor) -> torch.Tensor:
+    """``t`` permuted so that its logical order is its memory order (dense tensors)."""
+    if t.is_contiguous():
+        return t
+    perm = sorted(range(t.dim()), key=lambda d: (-t.stride(d), d))
+    return t.permute(perm)
+
+
+def _flat_view(flat: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """A view of the 1-D slice ``flat`` with ``like``'s shape and strides (same layout)."""
+    if like.is_contiguous():
+        return flat.view(like.shape)
+    return flat.as_strided(like.shape, like.stride())
+
+
 class FlatParamSpace:
     def __init__(self, params: Sequence[torch.nn.Parameter], names: Optional[Sequence[str]] = None,
                  grad_dtype: Optional[torch.dtype] = None, shard: Tuple[int, int] = (0, 1),
@@ -65,9 +80,13 @@ class FlatParamSpace:
         self.grad = torch.zeros(self.total, dtype=self.grad_dtype, device=dev)
         with torch.no_grad():
             for p, o, n in zip(params, self.offsets, self.numels):
-                self.model[o:o + n].copy_(p.data.reshape(-1))
-                p.data = self.model[o:o + n].view_as(p)
-                p.grad = self.grad[o:o + n].view_as(p)
+                # keep each parameter's memory layout: a channels_last conv weight stays
+                # channels_last as a view of the flat buffer (MIOpen's NHWC solvers need
+                # input, weight and gradients in the same layout; an NCHW weight next to
+                # NHWC activations sends the backward pass to the naive fallback kernels)
+                self.model[o:o + n].copy_(_memory_order(p.data).reshape(-1))
+                p.data = _flat_view(self.model[o:o + n], p)
+                p.grad = _flat_view(self.grad[o:o + n], p)
                 p._ct_flat_grad = True   # ops.linear may accumulate dW straight into it
         # fp32 master copy of THIS rank's shard only
         self.master = self.model[self.shard_lo:self.shard_hi].float().clone() \
