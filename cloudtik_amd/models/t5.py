@@ -1,0 +1,261 @@
+"""T5 encoder-decoder (t5-small / base / large topologies).
+
+Reference workload: the quickstart T5 inference (applications/ai/quickstart, HF
+``T5ForConditionalGeneration``).  Random-init weights, same architecture:
+pre-norm blocks with RMS LayerNorm (no mean, no bias), un-scaled attention with a learned
+bucketed relative-position bias shared by all layers of a stack, ReLU (v1.0) or gated-GELU
+(v1.1) feed-forward, tied input/output embeddings scaled by d_model^-0.5.
+
+MI355X mapping: RMS norms run in the HIP LayerNorm kernel (``rms=True``), the residual add
+fused into the next norm; attention uses PyTorch SDPA with the relative-position bias as an
+additive mask (the bias is per-head [H, Sq, Sk], which the d64 MFMA kernel's per-key bias
+does not express); the training loss is the fused linear + cross-entropy HIP kernel over
+the 32128-token vocabulary; generation keeps a per-layer KV cache.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from cloudtik_amd import ops
+
+
+@dataclass
+class T5Config:
+    vocab_size: int = 32128
+    d_model: int = 768
+    d_kv: int = 64
+    d_ff: int = 3072
+    num_layers: int = 12
+    num_decoder_layers: int = 12
+    num_heads: int = 12
+    relative_attention_num_buckets: int = 32
+    relative_attention_max_distance: int = 128
+    dropout_rate: float = 0.1
+    layer_norm_epsilon: float = 1e-6
+    gated_gelu: bool = False          # T5 v1.1 feed-forward
+    pad_token_id: int = 0
+    decoder_start_token_id: int = 0
+    eos_token_id: int = 1
+
+    @classmethod
+    def small(cls, **kw):
+        return cls(d_model=512, d_ff=2048, num_layers=6, num_decoder_layers=6, num_heads=8, **kw)
+
+    @classmethod
+    def base(cls, **kw):
+        return cls(**kw)
+
+    @classmethod
+    def large(cls, **kw):
+        return cls(d_model=1024, d_ff=4096, num_layers=24, num_decoder_layers=24, num_heads=16, **kw)
+
+    @classmethod
+    def tiny(cls, **kw):
+        base = dict(vocab_size=64, d_model=32, d_kv=8, d_ff=64, num_layers=2, num_decoder_layers=2, num_heads=4,
+                    relative_attention_num_buckets=8, relative_attention_max_distance=16, dropout_rate=0.0)
+        base.update(kw)
+        return cls(**base)
+
+
+def relative_position_bucket(rel: torch.Tensor, bidirectional: bool, num_buckets: int, max_distance: int):
+    """T5 bucketing of (key - query) offsets: exact buckets for small offsets, log-spaced
+    buckets up to ``max_distance``, one shared bucket beyond."""
+    ret = torch.zeros_like(rel)
+    if bidirectional:
+        num_buckets //= 2
+        ret = ret + (rel > 0).long() * num_buckets
+        n = rel.abs()
+    else:
+        n = (-rel).clamp(min=0)
+    max_exact = num_buckets // 2
+    small = n < max_exact
+    large = max_exact + (torch.log(n.float().clamp(min=1) / max_exact) / math.log(max_distance / max_exact)
+                         * (num_buckets - max_exact)).long()
+    large = large.clamp(max=num_buckets - 1)
+    return ret + torch.where(small, n, large)
+
+
+class T5Norm(nn.Module):
+    def __init__(self, d, eps, device=None, dtype=None):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d, device=device, dtype=dtype))
+        self.eps = eps
+
+    def forward(self, x, residual=None):
+        return ops.layer_norm(x, self.weight, None, eps=self.eps, residual=residual, rms=True)
+
+
+class T5Attention(nn.Module):
+    def __init__(self, cfg: T5Config, relative_bias: bool, causal: bool, device=None, dtype=None):
+        super().__init__()
+        inner = cfg.num_heads * cfg.d_kv
+        kw = dict(bias=False, device=device, dtype=dtype)
+        self.q, self.k, self.v = nn.Linear(cfg.d_model, inner, **kw), nn.Linear(cfg.d_model, inner, **kw), \
+            nn.Linear(cfg.d_model, inner, **kw)
+        self.o = nn.Linear(inner, cfg.d_model, **kw)
+        self.h, self.dk = cfg.num_heads, cfg.d_kv
+        self.causal = causal
+        self.cfg = cfg
+        self.rel = nn.Embedding(cfg.relative_attention_num_buckets, cfg.num_heads, device=device, dtype=dtype) \
+            if relative_bias else None
+
+    def position_bias(self, sq: int, sk: int, device, offset: int = 0) -> torch.Tensor:
+        """[1, H, sq, sk] additive bias (query positions start at ``offset``)."""
+        qpos = torch.arange(offset, offset + sq, device=device)[:, None]
+        kpos = torch.arange(sk, device=device)[None, :]
+        bucket = relative_position_bucket(kpos - qpos, not self.causal, self.cfg.relative_attention_num_buckets,
+                                          self.cfg.relative_attention_max_distance)
+        return self.rel(bucket).permute(2, 0, 1).unsqueeze(0)
+
+    def _split(self, x):
+        B, S, _ = x.shape
+        return x.view(B, S, self.h, self.dk).transpose(1, 2)
+
+    def forward(self, x, kv=None, bias=None, cache=None):
+        """``kv``: encoder states for cross-attention; ``cache``: (k, v) of earlier decoder steps."""
+        B, S, _ = x.shape
+        q = self._split(self.q(x))
+        src = x if kv is None else kv
+        if kv is not None and cache is not None:
+            k, v = cache                                   # cross-attention K/V computed once
+        else:
+            k, v = self._split(self.k(src)), self._split(self.v(src))
+            if cache is not None:
+                k, v = torch.cat([cache[0], k], 2), torch.cat([cache[1], v], 2)
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.to(q.dtype) if bias is not None else None,
+                                           dropout_p=self.cfg.dropout_rate if self.training else 0.0,
+                                           scale=1.0)                 # T5 folds the scale into init
+        return self.o(o.transpose(1, 2).reshape(B, S, -1)), (k, v)
+
+
+class T5FF(nn.Module):
+    def __init__(self, cfg: T5Config, device=None, dtype=None):
+        super().__init__()
+        kw = dict(bias=False, device=device, dtype=dtype)
+        self.gated = cfg.gated_gelu
+        self.wi = nn.Linear(cfg.d_model, cfg.d_ff, **kw)
+        if self.gated:
+            self.wi_1 = nn.Linear(cfg.d_model, cfg.d_ff, **kw)
+        self.wo = nn.Linear(cfg.d_ff, cfg.d_model, **kw)
+        self.p = cfg.dropout_rate
+
+    def forward(self, x):
+        h = F.gelu(self.wi(x), approximate="tanh") * self.wi_1(x) if self.gated else F.relu(self.wi(x))
+        if self.training and self.p:
+            h = F.dropout(h, self.p)
+        return self.wo(h)
+
+
+class T5Block(nn.Module):
+    def __init__(self, cfg: T5Config, decoder: bool, relative_bias: bool, device=None, dtype=None):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        self.ln_sa = T5Norm(cfg.d_model, cfg.layer_norm_epsilon, **kw)
+        self.sa = T5Attention(cfg, relative_bias, causal=decoder, **kw)
+        self.decoder = decoder
+        if decoder:
+            self.ln_ca = T5Norm(cfg.d_model, cfg.layer_norm_epsilon, **kw)
+            self.ca = T5Attention(cfg, False, causal=False, **kw)
+        self.ln_ff = T5Norm(cfg.d_model, cfg.layer_norm_epsilon, **kw)
+        self.ff = T5FF(cfg, **kw)
+        self.p = cfg.dropout_rate
+
+    def _drop(self, x):
+        return F.dropout(x, self.p) if (self.training and self.p) else x
+
+    def forward(self, x, bias, enc=None, enc_bias=None, cache=None):
+        new_cache = {}
+        h, new_cache["self"] = self.sa(self.ln_sa(x), bias=bias, cache=cache.get("self") if cache else None)
+        x = x + self._drop(h)
+        if self.decoder:
+            h, new_cache["cross"] = self.ca(self.ln_ca(x), kv=enc, bias=enc_bias,
+                                            cache=cache.get("cross") if cache else None)
+            x = x + self._drop(h)
+        x = x + self._drop(self.ff(self.ln_ff(x)))
+        return x, new_cache
+
+
+class T5Stack(nn.Module):
+    def __init__(self, cfg: T5Config, decoder: bool, embed: nn.Embedding, device=None, dtype=None):
+        super().__init__()
+        n = cfg.num_decoder_layers if decoder else cfg.num_layers
+        self.embed = embed
+        self.blocks = nn.ModuleList([T5Block(cfg, decoder, i == 0, device, dtype) for i in range(n)])
+        self.final = T5Norm(cfg.d_model, cfg.layer_norm_epsilon, device, dtype)
+        self.decoder = decoder
+        self.p = cfg.dropout_rate
+
+    def forward(self, ids, mask=None, enc=None, enc_mask=None, caches=None, offset: int = 0):
+        x = self.embed(ids)
+        if self.training and self.p:
+            x = F.dropout(x, self.p)
+        B, S = ids.shape
+        sk = S + offset
+        bias = self.blocks[0].sa.position_bias(S, sk, ids.device, offset)
+        if self.decoder and S > 1:
+            causal = torch.ones(S, sk, dtype=torch.bool, device=ids.device).tril(offset)
+            bias = bias.masked_fill(~causal, float("-inf"))
+        if mask is not None:
+            bias = bias + (1.0 - mask[:, None, None, :].to(bias.dtype)) * -1e9
+        enc_bias = None
+        if enc_mask is not None:
+            enc_bias = (1.0 - enc_mask[:, None, None, :].to(x.dtype)) * -1e9
+        new_caches = []
+        for i, blk in enumerate(self.blocks):
+            x, c = blk(x, bias, enc, enc_bias, caches[i] if caches else None)
+            new_caches.append(c)
+        x = self.final(x)
+        if self.training and self.p:
+            x = F.dropout(x, self.p)
+        return x, new_caches
+
+
+class T5ForConditionalGeneration(nn.Module):
+    def __init__(self, cfg: T5Config = None, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        cfg = cfg or T5Config()
+        self.cfg = cfg
+        self.shared = nn.Embedding(cfg.vocab_size, cfg.d_model, device=device, dtype=dtype)
+        nn.init.normal_(self.shared.weight, std=1.0)
+        self.encoder = T5Stack(cfg, False, self.shared, device, dtype)
+        self.decoder = T5Stack(cfg, True, self.shared, device, dtype)
+        self.dtype = dtype
+
+    def _shift_right(self, labels):
+        start = torch.full_like(labels[:, :1], self.cfg.decoder_start_token_id)
+        ids = torch.cat([start, labels[:, :-1]], 1)
+        return ids.masked_fill(ids == -100, self.cfg.pad_token_id)
+
+    def forward(self, input_ids, labels, attention_mask=None, decoder_input_ids=None):
+        """Training: mean token cross-entropy (tied, d_model^-0.5-scaled output head)."""
+        enc, _ = self.encoder(input_ids, attention_mask)
+        dec_ids = decoder_input_ids if decoder_input_ids is not None else self._shift_right(labels)
+        dec, _ = self.decoder(dec_ids, enc=enc, enc_mask=attention_mask)
+        x = (dec * (self.cfg.d_model ** -0.5)).reshape(-1, self.cfg.d_model)
+        return ops.cross_entropy_fused(x, self.shared.weight, None, labels.reshape(-1), ignore_index=-100)
+
+    def logits(self, dec):
+        return F.linear(dec * (self.cfg.d_model ** -0.5), self.shared.weight)
+
+    @torch.no_grad()
+    def generate(self, input_ids, attention_mask=None, max_new_tokens: int = 32) -> torch.Tensor:
+        """Greedy decoding with a KV cache (self-attention K/V grow; cross K/V computed once)."""
+        enc, _ = self.encoder(input_ids, attention_mask)
+        B = input_ids.shape[0]
+        cur = torch.full((B, 1), self.cfg.decoder_start_token_id, dtype=torch.long, device=input_ids.device)
+        out, caches = [], None
+        done = torch.zeros(B, dtype=torch.bool, device=input_ids.device)
+        for step in range(max_new_tokens):
+            dec, caches = self.decoder(cur, enc=enc, enc_mask=attention_mask, caches=caches, offset=step)
+            nxt = self.logits(dec[:, -1]).float().argmax(-1)
+            nxt = torch.where(done, torch.full_like(nxt, self.cfg.pad_token_id), nxt)
+            out.append(nxt)
+            done |= nxt == self.cfg.eos_token_id
+            cur = nxt[:, None]
+        return torch.stack(out, 1)

@@ -96,3 +96,4 @@ from . import multi_tensor  # noqa: E402,F401
 from .graph import CSR, SpMM, gbdt_histogram, gbdt_predict, spmm  # noqa: E402,F401
 from .deform import (DeformConv, DeformRoIPooling, DeformRoIPoolingPack, ModulatedDeformConv,  # noqa: E402,F401
                      ModulatedDeformConvPack, deform_conv2d, deform_roi_pooling)
+from .rnnt import rnnt_loss, rnnt_loss_reference  # noqa: E402,F401

@@ -22,6 +22,10 @@ int ct_roi_pool_fwd(const void*, const float*, void*, int*, int, int, int, int, 
 int ct_roi_pool_bwd(const void*, const float*, const int*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ct_focal_fwd(const void*, const int64_t*, float*, int, long, int, float, float, hipStream_t);
 int ct_focal_bwd(const void*, const int64_t*, const float*, void*, int, long, int, float, float, hipStream_t);
+int ct_rnnt_fwd(const void*, int, const int*, const int*, const int*, float*, float*, float*, float*, float*, int, int,
+                int, int, int, hipStream_t);
+int ct_rnnt_bwd(const void*, int, const int*, const int*, const int*, const float*, const float*, const float*,
+                const float*, const float*, const float*, void*, int, int, int, int, int, hipStream_t);
 int ct_mt_copy(const uint64_t*, const int64_t*, const int64_t*, int, long, void*, int, int, float, int, hipStream_t);
 void* ct_loader_create(int, const void* const*, const long*, long, int, int, uint64_t, int, int, int, int, int, int);
 long ct_loader_num_batches(void*);
@@ -263,6 +267,48 @@ at::Tensor focal_bwd(at::Tensor logits, at::Tensor targets, at::Tensor gloss, do
   return g;
 }
 
+// ---------------------------------------------------------------- RNN-T loss
+// logits [B, T, U+1, V] (bf16/fp32), labels [B, U] int32, lengths int32 -> (loglik [B], state)
+std::vector<at::Tensor> rnnt_fwd(at::Tensor logits, at::Tensor labels, at::Tensor tlen, at::Tensor ulen, int64_t blank) {
+  XCHECK_IN(logits); XCHECK_IN(labels); XCHECK_IN(tlen); XCHECK_IN(ulen);
+  XCHECK_DT(labels, at::kInt); XCHECK_DT(tlen, at::kInt); XCHECK_DT(ulen, at::kInt);
+  TORCH_CHECK(logits.dim() == 4, "rnnt: logits must be [B, T, U+1, V]");
+  const int B = (int)logits.size(0), Tm = (int)logits.size(1), U1 = (int)logits.size(2), V = (int)logits.size(3);
+  TORCH_CHECK(labels.dim() == 2 && labels.size(0) == B && labels.size(1) == U1 - 1, "rnnt: labels must be [B, U]");
+  TORCH_CHECK(tlen.numel() == B && ulen.numel() == B);
+  TORCH_CHECK(blank >= 0 && blank < V, "rnnt: blank out of range");
+  // lengths must fit the padded lattice (checked on the host: a bad length would index out of bounds)
+  auto tl = tlen.cpu(), ul = ulen.cpu();
+  for (int b = 0; b < B; ++b) {
+    const int t = tl.data_ptr<int>()[b], u = ul.data_ptr<int>()[b];
+    TORCH_CHECK(t >= 1 && t <= Tm && u >= 0 && u <= U1 - 1, "rnnt: length out of range for utterance ", b);
+  }
+  auto f = logits.options().dtype(at::kFloat);
+  const long rows = (long)B * Tm * U1;
+  auto lse = at::empty({rows}, f), lp = at::empty({rows, 2}, f);
+  auto alpha = at::empty({B, Tm, U1}, f), beta = at::empty({B, Tm, U1}, f), loglik = at::empty({B}, f);
+  const int rc = ct_rnnt_fwd(logits.data_ptr(), fb(logits), labels.data_ptr<int>(), tlen.data_ptr<int>(),
+                             ulen.data_ptr<int>(), lse.data_ptr<float>(), lp.data_ptr<float>(), alpha.data_ptr<float>(),
+                             beta.data_ptr<float>(), loglik.data_ptr<float>(), B, Tm, U1, V, (int)blank, stream());
+  TORCH_CHECK(rc == 0, "rnnt_fwd failed (", rc, ")");
+  return {loglik, lse, lp, alpha, beta};
+}
+
+at::Tensor rnnt_bwd(at::Tensor logits, at::Tensor labels, at::Tensor tlen, at::Tensor ulen, at::Tensor lse,
+                    at::Tensor lp, at::Tensor alpha, at::Tensor beta, at::Tensor loglik, at::Tensor gloss,
+                    int64_t blank) {
+  XCHECK_IN(logits); XCHECK_IN(gloss); XCHECK_DT(gloss, at::kFloat);
+  const int B = (int)logits.size(0), Tm = (int)logits.size(1), U1 = (int)logits.size(2), V = (int)logits.size(3);
+  TORCH_CHECK(gloss.numel() == B);
+  auto grad = at::empty_like(logits);
+  const int rc = ct_rnnt_bwd(logits.data_ptr(), fb(logits), labels.data_ptr<int>(), tlen.data_ptr<int>(),
+                             ulen.data_ptr<int>(), lse.data_ptr<float>(), lp.data_ptr<float>(), alpha.data_ptr<float>(),
+                             beta.data_ptr<float>(), loglik.data_ptr<float>(), gloss.data_ptr<float>(), grad.data_ptr(),
+                             B, Tm, U1, V, (int)blank, stream());
+  TORCH_CHECK(rc == 0, "rnnt_bwd failed (", rc, ")");
+  return grad;
+}
+
 // ---------------------------------------------------------------- multi-tensor copy
 // pack (unpack=false): flat[offs[t]:...] = scale * tensors[t];  unpack: tensors[t] = scale * flat[...]
 void mt_copy(std::vector<at::Tensor> tensors, at::Tensor flat, double scale, bool unpack) {
@@ -370,6 +416,8 @@ void register_ext(pybind11::module& m) {
   m.def("roi_align_fwd", &roi_align_fwd);
   m.def("roi_align_bwd", &roi_align_bwd);
   m.def("roi_align_nhwc_fwd", &roi_align_nhwc_fwd);
+  m.def("rnnt_fwd", &rnnt_fwd);
+  m.def("rnnt_bwd", &rnnt_bwd);
   m.def("roi_align_nhwc_bwd", &roi_align_nhwc_bwd);
   m.def("roi_pool_fwd", &roi_pool_fwd);
   m.def("roi_pool_bwd", &roi_pool_bwd);

@@ -33,6 +33,9 @@ MODELS = {
     "ssd_resnet34_300": (300, 32),
     "ssd_mobilenet": (300, 64),
     "yolov4": (608, 16),
+    "rnnt": (0, 32),            # MLPerf RNN-T, 400 feature frames, 60 labels
+    "t5_base": (0, 16),         # T5-base, 128 source tokens, 32 generated
+    "transnetv2": (0, 8),       # 100-frame 48x27 windows
 }
 
 
@@ -58,6 +61,21 @@ def build(name, dev, num_classes=81):
         return ssd300_mobilenet_v1(91, device=dev)
     if name == "yolov4":
         return yolov4(80, device=dev)
+    if name == "rnnt":
+        from cloudtik_amd.models.rnnt import rnnt_mlperf
+        m = rnnt_mlperf(device=dev)
+        with torch.no_grad():
+            # random init argmaxes to a non-blank label almost every joint step (blank is 1
+            # of 29 classes); a trained transducer mostly predicts blank.  Bias the blank
+            # logit so greedy decoding emits at a speech-like rate instead of 30 labels per frame.
+            m.joint_out.bias[m.cfg.blank] += 6.0
+        return m
+    if name == "t5_base":
+        from cloudtik_amd.models.t5 import T5Config, T5ForConditionalGeneration
+        return T5ForConditionalGeneration(T5Config.base(), device=dev)
+    if name == "transnetv2":
+        from cloudtik_amd.models.transnetv2 import TransNetV2
+        return TransNetV2(device=dev)
     raise ValueError(name)
 
 
@@ -71,7 +89,26 @@ def infer_fn(name, model, size):
         return f
     if name == "yolov4":
         return lambda x: model.postprocess(model(x), (size, size))
+    if name == "rnnt":
+        return lambda x: model.greedy_decode(*x)
+    if name == "t5_base":
+        return lambda x: model.generate(x, max_new_tokens=32)
+    if name == "transnetv2":
+        return model.predict_transitions
     raise ValueError(name)
+
+
+def make_input(name, batch, size, dev):
+    """Synthetic input of the model's shape (images unless the model says otherwise)."""
+    if name == "rnnt":
+        from cloudtik_amd.models.rnnt import synthetic_speech_batch
+        f, fl, _, _ = synthetic_speech_batch(batch, T=400, U=60, device=dev)
+        return f, fl
+    if name == "t5_base":
+        return torch.randint(2, 32128, (batch, 128), device=dev)
+    if name == "transnetv2":
+        return torch.randint(0, 256, (batch, 100, 27, 48, 3), dtype=torch.uint8, device=dev)
+    return torch.randn(batch, 3, size, size, device=dev)
 
 
 def run(name, args, dev):
@@ -80,7 +117,7 @@ def run(name, args, dev):
     batch = args.batch or batch
     torch.manual_seed(0)
     model = build(name, dev)
-    x = torch.randn(batch, 3, size, size, device=dev)
+    x = make_input(name, batch, size, dev)
     if name in ("resnet50", "resnext101_32x16d"):
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     if args.train:
@@ -88,7 +125,24 @@ def run(name, args, dev):
         from cloudtik_amd.train.optim import build_optimizer
         model.train()
         opt = build_optimizer("sgd", model, 0.01, 1e-4, momentum=0.9)
-        if name in ("resnet50", "resnext101_32x16d"):
+        if name == "rnnt":
+            from cloudtik_amd.models.rnnt import synthetic_speech_batch
+            sb = synthetic_speech_batch(batch, T=400, U=60, device=dev)
+
+            def step():
+                loss = model(*sb)
+                loss.backward()
+                opt.step()
+                opt.zero_grad()
+        elif name == "t5_base":
+            y = torch.randint(2, 32128, (batch, 32), device=dev)
+
+            def step():
+                loss = model(x, y)
+                loss.backward()
+                opt.step()
+                opt.zero_grad()
+        elif name in ("resnet50", "resnext101_32x16d"):
             y = torch.randint(0, 1000, (batch,), device=dev)
 
             def step():
@@ -120,8 +174,10 @@ def run(name, args, dev):
         step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    unit = {"rnnt": "utterances_per_sec", "t5_base": "sequences_per_sec",
+            "transnetv2": "windows_per_sec"}.get(name, "images_per_sec")
     out = {"model": name, "mode": "train" if args.train else "inference", "batch": batch, "size": size,
-           "images_per_sec": round(batch * args.steps / dt, 2), "ms_per_batch": round(dt / args.steps * 1000, 3),
+           unit: round(batch * args.steps / dt, 2), "ms_per_batch": round(dt / args.steps * 1000, 3),
            "dtype": "bf16", "data": "synthetic, random-init weights"}
     print(json.dumps(out), flush=True)
     del model
