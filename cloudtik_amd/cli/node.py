@@ -138,3 +138,21 @@ def dump(output):
     with tarfile.open(output, "w:gz") as t:
         t.add(services.logs_dir(), arcname="logs")
     click.echo(output)
+
+
+@node.command(name="service-daemon")
+@click.argument("command", type=click.Choice(["start", "stop"]))
+@click.argument("identifier")
+@click.option("--service-class", default=None, help="ServiceRunner / PullJob class (module.Class).")
+@click.option("--pull-script", default=None, help="Script run every --interval seconds.")
+@click.option("--interval", type=float, default=None)
+@click.argument("service_args", nargs=-1)
+def service_daemon(command, identifier, service_class, pull_script, interval, service_args):
+    """Start / stop a generic service daemon or periodic pull job on this node."""
+    from cloudtik_amd.core.service_daemon import start_service_daemon, stop_service_daemon
+    if command == "start":
+        pid = start_service_daemon(identifier, service_class, pull_script, interval, list(service_args))
+        click.echo(f"service daemon {identifier} started (pid {pid})")
+    else:
+        ok = stop_service_daemon(identifier)
+        click.echo(f"service daemon {identifier} {'stopped' if ok else 'was not running'}")

@@ -1,7 +1,7 @@
 """Build the native control-plane / runtime components in-tree (host C++, no GPU code):
 
 * ``bin/cloudtik-state-server``  -- RESP state server (state_server/state_server.cpp)
-* ``bin/cloudtik-loader-bench``  -- (see data/csrc) nothing else yet
+* ``bin/libcloudtik_criteo.so``   -- Criteo TSV parser / dictionary encoder (criteo/criteo.cpp)
 
 Called from ``cloudtik_amd.ops.build.build_all`` and ``__graft_entry__.build``.
 """
@@ -15,6 +15,8 @@ BIN = os.path.join(HERE, "bin")
 
 TARGETS = {
     "cloudtik-state-server": [os.path.join(HERE, "state_server", "state_server.cpp")],
+    # shared libraries (ctypes) end in .so
+    "libcloudtik_criteo.so": [os.path.join(HERE, "criteo", "criteo.cpp")],
 }
 
 
@@ -22,13 +24,17 @@ def build(force: bool = False, verbose: bool = True, sanitize: bool = False):
     os.makedirs(BIN, exist_ok=True)
     outs = []
     for name, srcs in TARGETS.items():
+        if sanitize and name.endswith(".so"):
+            continue            # sanitizer builds are for the executables (a .so would need ASan preloaded)
         out = os.path.join(BIN, name + ("-asan" if sanitize else ""))
         newest = max(os.path.getmtime(s) for s in srcs)
         if force or not os.path.exists(out) or os.path.getmtime(out) < newest:
-            flags = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter"]
+            flags = ["-O2", "-g", "-std=c++17", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread"]
             if sanitize:
                 flags = ["-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
-                         "-fno-sanitize-recover=undefined"]
+                         "-fno-sanitize-recover=undefined", "-pthread"]
+            if name.endswith(".so"):
+                flags += ["-shared", "-fPIC"]
             cmd = ["g++", *flags, *srcs, "-o", out + ".tmp"]
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
             if r.returncode != 0:
