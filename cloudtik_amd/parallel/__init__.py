@@ -67,3 +67,4 @@ def all_reduce_max(x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+from .sequence import ring_attention, ulysses_attention  # noqa: F401,E402
