@@ -19,6 +19,51 @@ import torch.nn.functional as F
 # split-K for weight-gradient GEMMs: 0 disables, otherwise the maximum split factor
 _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 
+# Weight-gradient GEMMs on a side HIP stream: they depend only on (dY, X) and write disjoint
+# slices of the flat gradient buffer, so they can run concurrently with the dgrad chain of the
+# backward pass (filling the CUs the dgrad GEMM's last wave leaves idle).  Consumers of the
+# gradients -- the bucketed all-reduce and the optimizer -- order themselves after this
+# stream via ``grad_stream_event()`` / ``sync_grad_stream()``.
+_WGRAD_STREAM = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM", "1") == "1"
+_streams = {}
+
+
+def grad_stream():
+    """The side stream used for weight-gradient GEMMs on the current device (or None)."""
+    if not _WGRAD_STREAM or not torch.cuda.is_available():
+        return None
+    dev = torch.cuda.current_device()
+    s = _streams.get(dev)
+    if s is None:
+        s = _streams[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def set_wgrad_stream(enabled: bool) -> None:
+    global _WGRAD_STREAM
+    _WGRAD_STREAM = bool(enabled)
+
+
+def sync_grad_stream() -> None:
+    """Make the current stream wait for every weight gradient issued so far."""
+    s = _streams.get(torch.cuda.current_device()) if torch.cuda.is_available() else None
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
+def wgrad_on_side_stream(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Issue ``g += dy2^T x2`` on the gradient side stream; False if disabled."""
+    s = grad_stream()
+    if s is None or not g.is_cuda:
+        return False
+    cur = torch.cuda.current_stream()
+    s.wait_stream(cur)                       # dY / X produced (and grad zeroed) on the main stream
+    with torch.cuda.stream(s):
+        wgrad_accumulate(g, dy2, x2)
+    dy2.record_stream(s)
+    x2.record_stream(s)
+    return True
+
 
 def splitk_factor(T: int, N: int, K: int) -> int:
     """Split factor for dW[N,K] = dY[T,N]^T X[T,K].  hipBLASLt's 256x256 macro-tiles give only
@@ -71,7 +116,8 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             g = Wp.grad
             if g is not None and getattr(Wp, "_ct_flat_grad", False) and g.dtype == dy.dtype:
-                wgrad_accumulate(g, dy2, x2)
+                if not wgrad_on_side_stream(g, dy2, x2):
+                    wgrad_accumulate(g, dy2, x2)
                 cb = getattr(Wp, "_ct_grad_ready", None)
                 if cb is not None:
                     cb(Wp)

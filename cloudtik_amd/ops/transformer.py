@@ -24,7 +24,7 @@ import math
 
 import torch
 
-from cloudtik_amd.ops.linear import wgrad_accumulate
+from cloudtik_amd.ops.linear import wgrad_accumulate, wgrad_on_side_stream
 
 
 def _C():
@@ -46,7 +46,8 @@ def _ready(*params):
 def _wgrad(p, dy2, x2):
     """dW = dy2^T x2, accumulated into the flat buffer when possible."""
     if _flat(p):
-        wgrad_accumulate(p.grad, dy2, x2)
+        if not wgrad_on_side_stream(p.grad, dy2, x2):
+            wgrad_accumulate(p.grad, dy2, x2)
         _ready(p)
         return None
     return dy2.t() @ x2

@@ -84,6 +84,19 @@ class GradBucketer:
                 self._next += 1
 
     def _launch(self, b):
+        from cloudtik_amd.ops.linear import grad_stream
+        side = grad_stream()
+        if side is not None:
+            # weight grads of this bucket were written on the side stream, bias / LayerNorm
+            # grads on the main one: issue the collective from the side stream after it has
+            # caught up with the main stream, so RCCL waits for both
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                self._launch_on_current(b)
+        else:
+            self._launch_on_current(b)
+
+    def _launch_on_current(self, b):
         lo, hi, _ = self.buckets[b]
         t = self.space.grad[lo:hi]
         if self.comm_dtype is not None and self.comm_dtype != t.dtype:
@@ -107,14 +120,18 @@ class GradBucketer:
     def finish(self):
         """Launch any bucket not yet launched (unused params / no overlap), then make the
         compute stream wait for every reduction.  Call before optimizer.step()."""
+        from cloudtik_amd.ops.linear import sync_grad_stream
         if self.world <= 1:
+            sync_grad_stream()
             return
         while self._next < len(self.buckets):
             self._launch(self._next)
             self._next += 1
+        sync_grad_stream()
         for w, dst, buf in self._works:
             w.wait()
             if dst is not None:
+                buf.record_stream(torch.cuda.current_stream()) if buf.is_cuda else None
                 dst.copy_(buf)
         self._works.clear()
         self._pending = [len(m) for _, _, m in self.buckets]

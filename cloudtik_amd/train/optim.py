@@ -29,6 +29,13 @@ SEG = 8192
 ALIGN = 64
 
 
+def _sync_grads():
+    """Order the optimizer after weight-gradient GEMMs issued on the gradient side stream."""
+    if torch.cuda.is_available():
+        from cloudtik_amd.ops.linear import sync_grad_stream
+        sync_grad_stream()
+
+
 def _memory_order(t: torch.Tensor) -> torch.Tensor:
     """``t`` permuted so that its logical order is its memory order (dense tensors)."""
     if t.is_contiguous():
@@ -241,6 +248,7 @@ class FusedLAMB(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        _sync_grads()
         loss = closure() if closure is not None else None
         self.step_count += 1
         sp = self.space
@@ -339,6 +347,7 @@ class FusedAdam(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        _sync_grads()
         loss = closure() if closure is not None else None
         self.step_count += 1
         sp = self.space
@@ -385,6 +394,7 @@ class FusedSGD(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        _sync_grads()
         loss = closure() if closure is not None else None
         self.step_count += 1
         sp = self.space
