@@ -196,7 +196,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float* __restrict__ p1, const float* __restrict__ p2, int nblk, int M, int C,
     const bf16_t* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ invstd, PT* __restrict__ dgamma, PT* __restrict__ dbeta,
-    float* __restrict__ ca, float* __restrict__ c1, float* __restrict__ c0) {
+    float* __restrict__ ca, float* __restrict__ c1, float* __restrict__ c0, int acc) {
   __shared__ float s1[16][64], s2[16][64];
   const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -207,8 +207,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   __syncthreads();
   if (pl != 0 || c >= C) return;
   for (int k = 1; k < 16; ++k) { sdy += s1[k][cl]; sdx += s2[k][cl]; }
-  if (dgamma) dgamma[c] = from_f<PT>(sdx);
-  if (dbeta) dbeta[c] = from_f<PT>(sdy);
+  // acc: accumulate into the (flat-buffer) parameter gradients instead of overwriting, so
+  // no separate AccumulateGrad kernel runs per BatchNorm parameter
+  if (dgamma) dgamma[c] = from_f<PT>(acc ? to_f<PT>(dgamma[c]) + sdx : sdx);
+  if (dbeta) dbeta[c] = from_f<PT>(acc ? to_f<PT>(dbeta[c]) + sdy : sdy);
   const float g = gamma ? bf2f(gamma[c]) : 1.f;
   const float is = invstd[c];
   const float a = g * is;
@@ -310,14 +312,15 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
   bn_bwd_reduce_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
                                                  (const bf16_t*)x, save_mean, save_invstd, L, relu,
                                                  part, part + (size_t)1024 * C);
-  if (param_fp32)
+  const int acc = (param_fp32 >> 1) & 1;   // bit 1: accumulate into dgamma / dbeta
+  if (param_fp32 & 1)
     bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
         part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
-        (float*)dgamma, (float*)dbeta, coef, coef + C, coef + 2 * C);
+        (float*)dgamma, (float*)dbeta, coef, coef + C, coef + 2 * C, acc);
   else
     bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
         part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
-        (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C);
+        (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
   bn_bwd_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
                                                        (const bf16_t*)x, coef, coef + C, coef + 2 * C,

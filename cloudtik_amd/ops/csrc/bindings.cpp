@@ -423,7 +423,8 @@ at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, a
 
 // returns (dx, dres, dgamma, dbeta)
 std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor gamma,
-                               at::Tensor save_mean, at::Tensor save_invstd, bool relu, bool need_dres) {
+                               at::Tensor save_mean, at::Tensor save_invstd, bool relu, bool need_dres,
+                               c10::optional<at::Tensor> dgamma_acc, c10::optional<at::Tensor> dbeta_acc) {
   check_nhwc(x, "x");
   at::Tensor dyc = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
   check_nhwc(dyc, "dy"); check_nhwc(y, "y");
@@ -431,14 +432,22 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Te
   const long M = nhwc_rows(x);
   auto dx = at::empty_like(x);
   at::Tensor dres = need_dres ? at::empty_like(x) : at::Tensor();
-  auto dgamma = at::empty_like(gamma), dbeta = at::empty_like(gamma);
+  // optional accumulate targets (flat gradient buffer views): both or neither
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined();
+  if (acc) {
+    TORCH_CHECK(dbeta_acc.has_value() && dbeta_acc->defined(), "bn_bwd: dgamma_acc needs dbeta_acc");
+    TORCH_CHECK(dgamma_acc->is_contiguous() && dbeta_acc->is_contiguous() && dgamma_acc->numel() == C &&
+                dbeta_acc->numel() == C && dgamma_acc->scalar_type() == gamma.scalar_type() &&
+                dbeta_acc->scalar_type() == gamma.scalar_type(), "bn_bwd: bad accumulate targets");
+  }
+  auto dgamma = acc ? *dgamma_acc : at::empty_like(gamma), dbeta = acc ? *dbeta_acc : at::empty_like(gamma);
   auto fo = x.options().dtype(at::kFloat);
   auto part = at::empty({2 * 1024 * (long)C}, fo);
   auto coef = at::empty({3 * (long)C}, fo);
   int rc = ct_bn_bwd(dyc.data_ptr(), y.data_ptr(), x.data_ptr(), gamma.data_ptr(),
                      save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr(),
                      need_dres ? dres.data_ptr() : nullptr, dgamma.data_ptr(), dbeta.data_ptr(),
-                     gamma.scalar_type() == at::kFloat ? 1 : 0, part.data_ptr<float>(),
+                     (gamma.scalar_type() == at::kFloat ? 1 : 0) | (acc ? 2 : 0), part.data_ptr<float>(),
                      coef.data_ptr<float>(), (int)M, C, relu ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "bn_bwd: unsupported C=", C);
   return {dx, dres, dgamma, dbeta};

@@ -208,3 +208,27 @@ def test_multi_tensor_pack_unpack(cuda, flat_dtype):
     unpack(flat, outs, scale=2.0)
     for a, b in zip(outs, ts):
         assert _rel(a, b) < (1e-7 if flat_dtype == torch.float32 else 5e-3)
+
+
+@pytest.mark.gpu
+def test_bn_grads_accumulate_into_flat_buffer(cuda):
+    """BatchNorm parameter gradients written straight into the flat gradient buffer equal the
+    autograd (AccumulateGrad) path, and the bucketer is notified for every parameter."""
+    import copy
+    from cloudtik_amd.models.resnet import ResNet
+    from cloudtik_amd.train.optim import FlatParamSpace
+    torch.manual_seed(0)
+    a = ResNet((1, 1, 1, 1), 10, device=cuda, dtype=torch.bfloat16)
+    b = copy.deepcopy(a)
+    space = FlatParamSpace(list(b.parameters()))
+    seen = []
+    for p in space.params:
+        p._ct_grad_ready = lambda p, seen=seen: seen.append(id(p))
+        p.register_post_accumulate_grad_hook(lambda p, seen=seen: seen.append(id(p)))
+    x = torch.randn(8, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for m in (a, b):
+        torch.nn.functional.cross_entropy(m(x).float(), torch.arange(8, device=cuda) % 10).backward()
+    torch.cuda.synchronize()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pb.grad.float(), pa.grad.float(), atol=2e-2, rtol=2e-2, msg=n)
+    assert set(id(p) for p in space.params) <= set(seen)
