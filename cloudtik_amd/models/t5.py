@@ -6,11 +6,13 @@ pre-norm blocks with RMS LayerNorm (no mean, no bias), un-scaled attention with 
 bucketed relative-position bias shared by all layers of a stack, ReLU (v1.0) or gated-GELU
 (v1.1) feed-forward, tied input/output embeddings scaled by d_model^-0.5.
 
-MI355X mapping: RMS norms run in the HIP LayerNorm kernel (``rms=True``), the residual add
-fused into the next norm; attention uses PyTorch SDPA with the relative-position bias as an
-additive mask (the bias is per-head [H, Sq, Sk], which the d64 MFMA kernel's per-key bias
-does not express); the training loss is the fused linear + cross-entropy HIP kernel over
-the 32128-token vocabulary; generation keeps a per-layer KV cache.
+MI355X mapping: RMS norms run in the HIP LayerNorm kernel (``rms=True``); the relative
+position bias is carried as one [H, Sq + Sk - 1] vector per stack (bias depends only on
+key - query) and added inside the MFMA flash-attention kernel (``ops.attention_relbias``),
+so inference never materialises an [H, Sq, Sk] bias; cross-attention uses the MFMA kernel
+with the per-key padding mask; training self-attention (which needs the bias gradient) uses
+SDPA with the gathered bias; the training loss is the fused linear + cross-entropy HIP
+kernel over the 32128-token vocabulary; generation keeps a per-layer KV cache.
 """
 from __future__ import annotations
 
@@ -105,33 +107,70 @@ class T5Attention(nn.Module):
         self.rel = nn.Embedding(cfg.relative_attention_num_buckets, cfg.num_heads, device=device, dtype=dtype) \
             if relative_bias else None
 
-    def position_bias(self, sq: int, sk: int, device, offset: int = 0) -> torch.Tensor:
-        """[1, H, sq, sk] additive bias (query positions start at ``offset``)."""
-        qpos = torch.arange(offset, offset + sq, device=device)[:, None]
-        kpos = torch.arange(sk, device=device)[None, :]
-        bucket = relative_position_bucket(kpos - qpos, not self.causal, self.cfg.relative_attention_num_buckets,
+    def relative_vector(self, sq: int, sk: int, device, offset: int = 0):
+        """Per-head bias for every (key - query) offset: ``relvec [H, sq + sk - 1]`` with
+        ``score(q, k) += relvec[h, k - q + rel_base]``, ``rel_base = sq - 1``; query
+        positions start at ``offset`` (decoding with a KV cache)."""
+        rel_base = sq - 1
+        rel = torch.arange(sq + sk - 1, device=device) - rel_base - offset
+        bucket = relative_position_bucket(rel, not self.causal, self.cfg.relative_attention_num_buckets,
                                           self.cfg.relative_attention_max_distance)
-        return self.rel(bucket).permute(2, 0, 1).unsqueeze(0)
+        return self.rel(bucket).t().float(), rel_base
+
+    @staticmethod
+    def full_bias(relvec, rel_base, sq, sk, causal_offset=None, key_bias=None):
+        """Materialised [B|1, H, sq, sk] additive bias (the SDPA path)."""
+        dev = relvec.device
+        idx = torch.arange(sk, device=dev)[None, :] - torch.arange(sq, device=dev)[:, None] + rel_base
+        bias = relvec[:, idx][None]
+        if causal_offset is not None:
+            allowed = torch.ones(sq, sk, dtype=torch.bool, device=dev).tril(causal_offset)
+            bias = bias.masked_fill(~allowed, float("-inf"))
+        if key_bias is not None:
+            bias = bias + key_bias[:, None, None, :]
+        return bias
 
     def _split(self, x):
         B, S, _ = x.shape
-        return x.view(B, S, self.h, self.dk).transpose(1, 2)
+        return x.view(B, S, self.h, self.dk)
 
-    def forward(self, x, kv=None, bias=None, cache=None):
-        """``kv``: encoder states for cross-attention; ``cache``: (k, v) of earlier decoder steps."""
+    def forward(self, x, kv=None, rel=None, key_bias=None, cache=None, offset: int = 0):
+        """``kv``: encoder states for cross-attention; ``rel``: (relvec, rel_base) of the stack;
+        ``key_bias`` [B, Sk] additive key mask; ``cache``: (k, v) of earlier decoder steps."""
+        from cloudtik_amd import ops
         B, S, _ = x.shape
-        q = self._split(self.q(x))
+        q = self._split(self.q(x))                                    # [B, S, H, D]
         src = x if kv is None else kv
         if kv is not None and cache is not None:
-            k, v = cache                                   # cross-attention K/V computed once
+            k, v = cache                                              # cross-attention K/V computed once
         else:
             k, v = self._split(self.k(src)), self._split(self.v(src))
             if cache is not None:
-                k, v = torch.cat([cache[0], k], 2), torch.cat([cache[1], v], 2)
-        o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias.to(q.dtype) if bias is not None else None,
-                                           dropout_p=self.cfg.dropout_rate if self.training else 0.0,
-                                           scale=1.0)                 # T5 folds the scale into init
-        return self.o(o.transpose(1, 2).reshape(B, S, -1)), (k, v)
+                k, v = torch.cat([cache[0], k], 1), torch.cat([cache[1], v], 1)
+        Sk = k.shape[1]
+        grad = torch.is_grad_enabled() and self.training
+        kernel_ok = q.is_cuda and q.dtype == torch.bfloat16 and self.dk == 64
+        # causal masking in the kernel is top-left aligned: exact for prefill (offset 0) and for
+        # single-token decode steps (every cached key is visible)
+        causal = self.causal and S > 1
+        if rel is not None and kernel_ok and not grad and (offset == 0 or not causal):
+            relvec, rel_base = rel
+            o = ops.attention_relbias(q, k, v, relvec, rel_base, key_bias, scale=1.0, causal=causal)
+        elif rel is None and kernel_ok and not (self.training and self.cfg.dropout_rate):
+            o = ops.attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), key_bias=key_bias,
+                              scale=1.0, causal=causal).transpose(1, 2)          # T5 folds the scale into init
+        else:
+            bias = None
+            if rel is not None:
+                bias = self.full_bias(rel[0], rel[1], S, Sk, offset if causal else None, key_bias)
+            elif key_bias is not None:
+                bias = key_bias[:, None, None, :]
+            o = F.scaled_dot_product_attention(
+                q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                attn_mask=bias.to(q.dtype) if bias is not None else None,
+                dropout_p=self.cfg.dropout_rate if self.training else 0.0,
+                is_causal=causal and bias is None, scale=1.0).transpose(1, 2)
+        return self.o(o.reshape(B, S, -1)), (k, v)
 
 
 class T5FF(nn.Module):
@@ -169,12 +208,13 @@ class T5Block(nn.Module):
     def _drop(self, x):
         return F.dropout(x, self.p) if (self.training and self.p) else x
 
-    def forward(self, x, bias, enc=None, enc_bias=None, cache=None):
+    def forward(self, x, rel, key_bias=None, enc=None, enc_bias=None, cache=None, offset: int = 0):
         new_cache = {}
-        h, new_cache["self"] = self.sa(self.ln_sa(x), bias=bias, cache=cache.get("self") if cache else None)
+        h, new_cache["self"] = self.sa(self.ln_sa(x), rel=rel, key_bias=key_bias,
+                                       cache=cache.get("self") if cache else None, offset=offset)
         x = x + self._drop(h)
         if self.decoder:
-            h, new_cache["cross"] = self.ca(self.ln_ca(x), kv=enc, bias=enc_bias,
+            h, new_cache["cross"] = self.ca(self.ln_ca(x), kv=enc, key_bias=enc_bias,
                                             cache=cache.get("cross") if cache else None)
             x = x + self._drop(h)
         x = x + self._drop(self.ff(self.ln_ff(x)))
@@ -197,18 +237,12 @@ class T5Stack(nn.Module):
             x = F.dropout(x, self.p)
         B, S = ids.shape
         sk = S + offset
-        bias = self.blocks[0].sa.position_bias(S, sk, ids.device, offset)
-        if self.decoder and S > 1:
-            causal = torch.ones(S, sk, dtype=torch.bool, device=ids.device).tril(offset)
-            bias = bias.masked_fill(~causal, float("-inf"))
-        if mask is not None:
-            bias = bias + (1.0 - mask[:, None, None, :].to(bias.dtype)) * -1e9
-        enc_bias = None
-        if enc_mask is not None:
-            enc_bias = (1.0 - enc_mask[:, None, None, :].to(x.dtype)) * -1e9
+        rel = self.blocks[0].sa.relative_vector(S, sk, ids.device, offset)
+        key_bias = (1.0 - mask.float()) * -1e9 if mask is not None else None
+        enc_bias = (1.0 - enc_mask.float()) * -1e9 if enc_mask is not None else None
         new_caches = []
         for i, blk in enumerate(self.blocks):
-            x, c = blk(x, bias, enc, enc_bias, caches[i] if caches else None)
+            x, c = blk(x, rel, key_bias, enc, enc_bias, caches[i] if caches else None, offset)
             new_caches.append(c)
         x = self.final(x)
         if self.training and self.p:

@@ -123,7 +123,7 @@ from .functional import (  # noqa: E402,F401
     layer_norm, bias_act, bias_gelu, dropout, embedding3, cross_entropy_fused, batch_norm_act,
     ACT_NONE, ACT_GELU, ACT_RELU,
 )
-from .attention import attention, attention_packed  # noqa: E402,F401
+from .attention import attention, attention_packed, attention_relbias  # noqa: E402,F401
 from .linear import linear  # noqa: E402,F401
 from .rope import apply_rotary, rotary_cache  # noqa: E402,F401
 from .embedding import EmbeddingBagCollection, dot_interaction, embedding_bag, pack_bags  # noqa: E402,F401

@@ -113,3 +113,27 @@ def attention(q, k, v, key_bias=None, p=0.0, scale=None, causal=False):
                           float(p), seed, offset, bool(causal))
         return o.transpose(1, 2)
     return ref.attention(q, k, v, key_bias, p, seed, offset, scale, causal)
+
+
+def attention_relbias(q, k, v, rel_bias, rel_base: int, key_bias=None, scale: float = 1.0, causal: bool = False):
+    """Inference attention with a relative-position bias (T5): q/k/v ``[B, S, H, D]``,
+    ``rel_bias [H, L]`` adds ``rel_bias[h, k - q + rel_base]`` to every score (natural-log
+    units), ``key_bias [B, Sk]`` masks keys.  HIP MFMA kernel on the GPU (bf16, D = 64);
+    fp32 PyTorch reference elsewhere.  Forward only."""
+    B, Sq, H, D = q.shape
+    Sk = k.shape[1]
+    if (q.is_cuda and q.dtype == torch.bfloat16 and D == 64 and rel_bias.shape[1] <= 4096
+            and _ops().native_available()):
+        o = torch.empty_like(q)
+        kb = key_bias.float().contiguous() if key_bias is not None else None
+        _ops().require_native().attn_fwd_relbias(q, k, v, o, kb, rel_bias.float().contiguous(), int(rel_base),
+                                                 float(scale), bool(causal))
+        return o
+    idx = (torch.arange(Sk, device=q.device)[None, :] - torch.arange(Sq, device=q.device)[:, None] + rel_base)
+    bias = rel_bias.float()[:, idx.clamp(0, rel_bias.shape[1] - 1)][None]            # [1, H, Sq, Sk]
+    if key_bias is not None:
+        bias = bias + key_bias.float()[:, None, None, :]
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) * scale + bias
+    if causal:
+        s = s.masked_fill(torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    return torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), v.float()).to(q.dtype)

@@ -76,18 +76,27 @@ struct AttnFwdArgs {
   int B, H, Sq, Sk;
   float scale_log2;                // softmax scale * log2(e)
   uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
+  // relative-position bias (T5): score(q, k) += relb[h][k - q + rel_base] (natural-log units)
+  const float* relb; long relb_sh; int relb_len; int rel_base;
 };
 
-template <bool DROP, bool CAUSAL>
+constexpr int kRelBiasMax = 4096;   // LDS floats for one head's relative-offset bias vector
+
+template <bool DROP, bool CAUSAL, bool REL = false>
 __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   // [buf][K,V][64 rows][128 B] then [buf][64] fp32 log2-domain key bias (-inf past Sk)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + 2 * 64 * 4];
   float* kbias_lds = reinterpret_cast<float*>(smem + 32768);
+  // one head's relative-position bias vector, log2-scaled (REL variant only; the first
+  // K/V tile's barrier below publishes it)
+  __shared__ float relb_lds[REL ? kRelBiasMax : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qi = blockIdx.x * 128 + w * 32 + r;
   const bool qvalid = qi < a.Sq;
   const float LOG2E = 1.4426950408889634f;
+  if (REL)
+    for (int i = tid; i < a.relb_len; i += 256) relb_lds[i] = a.relb[h * a.relb_sh + i] * LOG2E;
 
   const bf16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (long)qi * a.q_ss;
   bf16x8_t qf[4];
@@ -161,6 +170,11 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
         const int i = 4 * g + j;
         float x0 = fmaf(S0[i], a.scale_log2, b0[j]);
         float x1 = fmaf(S1[i], a.scale_log2, b1[j]);
+        if (REL) {
+          const int ri = kt * 64 + 8 * g + 4 * hh + j - qi + a.rel_base;
+          x0 += relb_lds[min(max(ri, 0), a.relb_len - 1)];
+          x1 += relb_lds[min(max(ri + 32, 0), a.relb_len - 1)];
+        }
         if (CAUSAL) {
           const int key0 = kt * 64 + 8 * g + 4 * hh + j;
           if (key0 > qi) x0 = -INFINITY;
@@ -534,12 +548,40 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
   a.scale_log2 = scale * 1.4426950408889634f;
   drop_params(p_drop, seed, offset, &a.thr16, &a.inv_keep, &a.hash_base);
   a.causal = causal;
+  a.relb = nullptr; a.relb_sh = 0; a.relb_len = 0; a.rel_base = 0;
   dim3 grid((Sq + 127) / 128, B * H);
   const bool drop = p_drop > 0.f;
   if (drop && causal) attn_fwd_d64_kernel<true, true><<<grid, 256, 0, stream>>>(a);
   else if (drop) attn_fwd_d64_kernel<true, false><<<grid, 256, 0, stream>>>(a);
   else if (causal) attn_fwd_d64_kernel<false, true><<<grid, 256, 0, stream>>>(a);
   else attn_fwd_d64_kernel<false, false><<<grid, 256, 0, stream>>>(a);
+  return 0;
+}
+
+// Forward with a per-head relative-position bias vector relb [H, relb_len] (row stride
+// relb_sh): score(q, k) += relb[h][k - q + rel_base].  Inference path (no dropout).
+extern "C" int ct_attn_fwd_relbias(const void* q, const long* qs, const void* k, const long* ks,
+                                   const void* v, const long* vs, void* o, const long* os,
+                                   const float* kbias, long kb_sb, const float* relb, long relb_sh,
+                                   int relb_len, int rel_base, float* lse, int B, int H, int Sq, int Sk,
+                                   float scale, int causal, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0 || relb_len <= 0) return -1;
+  if (relb_len > kRelBiasMax) return -4;
+  AttnFwdArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
+  a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
+  a.k_sb = ks[0]; a.k_ss = ks[1]; a.k_sh = ks[2];
+  a.v_sb = vs[0]; a.v_ss = vs[1]; a.v_sh = vs[2];
+  a.o_sb = os[0]; a.o_ss = os[1]; a.o_sh = os[2];
+  a.kbias = kbias; a.kb_sb = kb_sb; a.lse = lse;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.thr16 = 0; a.inv_keep = 1.f; a.hash_base = 0;
+  a.causal = causal;
+  a.relb = relb; a.relb_sh = relb_sh; a.relb_len = relb_len; a.rel_base = rel_base;
+  dim3 grid((Sq + 127) / 128, B * H);
+  if (causal) attn_fwd_d64_kernel<false, true, true><<<grid, 256, 0, stream>>>(a);
+  else attn_fwd_d64_kernel<false, false, true><<<grid, 256, 0, stream>>>(a);
   return 0;
 }
 

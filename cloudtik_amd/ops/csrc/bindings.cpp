@@ -44,6 +44,9 @@ int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, 
 int ct_attn_fwd(const void*, const long*, const void*, const long*, const void*, const long*, void*,
                 const long*, const float*, long, float*, int, int, int, int, float, float, uint64_t,
                 uint64_t, int, hipStream_t);
+int ct_attn_fwd_relbias(const void*, const long*, const void*, const long*, const void*, const long*, void*,
+                        const long*, const float*, long, const float*, long, int, int, float*, int, int, int, int,
+                        float, int, hipStream_t);
 int ct_attn_bwd(const void*, const long*, const void*, const long*, const void*, const long*,
                 const void*, const long*, const void*, const long*, void*, const long*, void*,
                 const long*, void*, const long*, const float*, long, const float*, float*, float*,
@@ -357,6 +360,34 @@ at::Tensor attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o,
   return lse;
 }
 
+// inference forward with a T5-style relative-position bias vector relb [H, L]
+at::Tensor attn_fwd_relbias(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o,
+                            c10::optional<at::Tensor> key_bias, at::Tensor relb, int64_t rel_base, double scale,
+                            bool causal) {
+  long qs[3], ks[3], vs[3], os[3];
+  bshd_strides(q, qs, "q"); bshd_strides(k, ks, "k"); bshd_strides(v, vs, "v"); bshd_strides(o, os, "o");
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(2) == H && v.size(2) == H && v.size(1) == Sk);
+  TORCH_CHECK(o.size(0) == B && o.size(1) == Sq && o.size(2) == H);
+  CHECK_F32(relb); CHECK_CUDA(relb);
+  TORCH_CHECK(relb.dim() == 2 && relb.size(0) == H && (relb.stride(1) == 1 || relb.size(1) == 1),
+              "relb must be [H, L] fp32");
+  const long L = relb.size(1);
+  TORCH_CHECK(rel_base >= Sq - 1 && rel_base + Sk <= L, "relb does not cover every (key - query) offset");
+  const float* kb = nullptr; long kb_sb = 0;
+  if (key_bias.has_value() && key_bias->defined()) {
+    CHECK_F32(*key_bias); CHECK_CUDA(*key_bias);
+    TORCH_CHECK(key_bias->dim() == 2 && key_bias->size(0) == B && key_bias->size(1) == Sk && key_bias->stride(1) == 1);
+    kb = key_bias->data_ptr<float>(); kb_sb = key_bias->stride(0);
+  }
+  auto lse = at::empty({(long)B * H, Sq}, q.options().dtype(at::kFloat));
+  int rc = ct_attn_fwd_relbias(q.data_ptr(), qs, k.data_ptr(), ks, v.data_ptr(), vs, o.data_ptr(), os, kb, kb_sb,
+                               relb.data_ptr<float>(), relb.stride(0), (int)L, (int)rel_base, lse.data_ptr<float>(),
+                               B, H, Sq, Sk, (float)scale, causal ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "attn_fwd_relbias failed rc=", rc);
+  return lse;
+}
+
 void attn_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor dO, at::Tensor dq,
               at::Tensor dk, at::Tensor dv, c10::optional<at::Tensor> key_bias, at::Tensor lse,
               double scale, double p, int64_t seed, int64_t offset, bool causal) {
@@ -482,6 +513,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
+  m.def("attn_fwd_relbias", &attn_fwd_relbias);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
 }
