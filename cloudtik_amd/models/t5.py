@@ -16,7 +16,9 @@ kernel over the 32128-token vocabulary; generation keeps a per-layer KV cache.
 """
 from __future__ import annotations
 
+import logging
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -26,6 +28,7 @@ import torch.nn.functional as F
 
 from cloudtik_amd import ops
 
+logger = logging.getLogger(__name__)
 
 @dataclass
 class T5Config:
@@ -278,8 +281,20 @@ class T5ForConditionalGeneration(nn.Module):
         return F.linear(dec * (self.cfg.d_model ** -0.5), self.shared.weight)
 
     @torch.no_grad()
-    def generate(self, input_ids, attention_mask=None, max_new_tokens: int = 32) -> torch.Tensor:
-        """Greedy decoding with a KV cache (self-attention K/V grow; cross K/V computed once)."""
+    def generate(self, input_ids, attention_mask=None, max_new_tokens: int = 32,
+                 use_graph: Optional[bool] = None) -> torch.Tensor:
+        """Greedy decoding with a KV cache (self-attention K/V grow; cross K/V computed once).
+
+        On the GPU the decode step is captured once into a HIP graph over a static KV cache
+        of ``max_new_tokens`` slots and replayed per token (``_generate_graph``): a decode step
+        is ~15 small kernels per layer, so launch overhead, not math, bounds eager decoding."""
+        if use_graph is None:
+            use_graph = input_ids.is_cuda and os.environ.get("CLOUDTIK_AMD_T5_GRAPH", "1") == "1"
+        if use_graph and input_ids.is_cuda:
+            try:
+                return self._generate_graph(input_ids, attention_mask, max_new_tokens)
+            except RuntimeError as e:          # capture unsupported by some op: eager fallback
+                logger.warning("T5 graph decoding unavailable (%s); decoding eagerly", e)
         enc, _ = self.encoder(input_ids, attention_mask)
         B = input_ids.shape[0]
         cur = torch.full((B, 1), self.cfg.decoder_start_token_id, dtype=torch.long, device=input_ids.device)
@@ -293,3 +308,92 @@ class T5ForConditionalGeneration(nn.Module):
             done |= nxt == self.cfg.eos_token_id
             cur = nxt[:, None]
         return torch.stack(out, 1)
+
+    def _generate_graph(self, input_ids, attention_mask, max_new: int) -> torch.Tensor:
+        """Graph-replayed greedy decoding.  The captured graph and its static buffers are cached
+        per (batch, source length, steps, masked): a later call only runs the encoder, copies the
+        cross-attention K/V and the source mask into the static buffers and replays."""
+        cfg = self.cfg
+        dev = input_ids.device
+        B, S, T = input_ids.shape[0], input_ids.shape[1], max_new
+        dec = self.decoder
+        enc, _ = self.encoder(input_ids, attention_mask)
+        key = (B, S, T, attention_mask is not None, str(dev))
+        cache = getattr(self, "_graphs", None)
+        if cache is None:
+            cache = self._graphs = {}
+        st = cache.get(key)
+        if st is None:
+            st = cache[key] = self._capture_decode(B, S, T, enc.dtype, dev, attention_mask is not None)
+        for i, b in enumerate(dec.blocks):
+            st["cross"][i][0].copy_(b.ca._split(b.ca.k(enc)))
+            st["cross"][i][1].copy_(b.ca._split(b.ca.v(enc)))
+        if attention_mask is not None:
+            st["enc_bias"].copy_((1.0 - attention_mask.float()) * -1e9)
+        st["reset"]()
+        for _ in range(T):
+            st["graph"].replay()
+        return st["out"].clone()
+
+    def _capture_decode(self, B, S, T, dtype, dev, masked: bool):
+        cfg = self.cfg
+        H, D = cfg.num_heads, cfg.d_kv
+        dec = self.decoder
+        kc = [torch.zeros(B, T, H, D, dtype=dtype, device=dev) for _ in dec.blocks]
+        vc = [torch.zeros(B, T, H, D, dtype=dtype, device=dev) for _ in dec.blocks]
+        cross = [(torch.zeros(B, S, H, D, dtype=dtype, device=dev), torch.zeros(B, S, H, D, dtype=dtype, device=dev))
+                 for _ in dec.blocks]
+        enc_bias = torch.zeros(B, S, device=dev) if masked else None
+        cur = torch.full((B, 1), cfg.decoder_start_token_id, dtype=torch.long, device=dev)
+        pos = torch.zeros(1, dtype=torch.long, device=dev)
+        out = torch.full((B, T), cfg.pad_token_id, dtype=torch.long, device=dev)
+        done = torch.zeros(B, dtype=torch.bool, device=dev)
+        slots = torch.arange(T, device=dev)
+        pad = torch.full((B,), cfg.pad_token_id, dtype=torch.long, device=dev)
+        sa0 = dec.blocks[0].sa
+
+        def step():
+            x = dec.embed(cur)
+            bucket = relative_position_bucket(slots - pos, False, cfg.relative_attention_num_buckets,
+                                              cfg.relative_attention_max_distance)
+            relvec = sa0.rel(bucket).t().float().contiguous()              # query at `pos`, keys 0..T-1
+            key_bias = torch.where(slots <= pos, 0.0, -1e9).float()[None].expand(B, T).contiguous()
+            for i, blk in enumerate(dec.blocks):
+                h = blk.ln_sa(x)
+                a = blk.sa
+                q, k, v = a._split(a.q(h)), a._split(a.k(h)), a._split(a.v(h))
+                kc[i].index_copy_(1, pos, k)
+                vc[i].index_copy_(1, pos, v)
+                o = ops.attention_relbias(q, kc[i], vc[i], relvec, 0, key_bias, scale=1.0, causal=False)
+                x = x + a.o(o.reshape(B, 1, -1))
+                h = blk.ln_ca(x)
+                c = blk.ca
+                q = c._split(c.q(h))
+                o = ops.attention(q.transpose(1, 2), cross[i][0].transpose(1, 2), cross[i][1].transpose(1, 2),
+                                  key_bias=enc_bias, scale=1.0).transpose(1, 2)
+                x = x + c.o(o.reshape(B, 1, -1))
+                x = x + blk.ff(blk.ln_ff(x))
+            x = dec.final(x)
+            nxt = self.logits(x[:, -1]).float().argmax(-1)
+            nxt = torch.where(done, pad, nxt)
+            out.index_copy_(1, pos, nxt[:, None])
+            done.logical_or_(nxt == cfg.eos_token_id)
+            cur.copy_(nxt[:, None])
+            pos.add_(1)
+
+        def reset():
+            cur.fill_(cfg.decoder_start_token_id)
+            pos.zero_()
+            out.fill_(cfg.pad_token_id)
+            done.zero_()
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):          # warm up (lazy inits, library handles) off the capture
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        reset()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        return {"graph": graph, "cross": cross, "enc_bias": enc_bias, "out": out, "reset": reset}

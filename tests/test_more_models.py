@@ -110,3 +110,15 @@ def test_t5_kernel_path_matches_sdpa_path(cuda):
     enc_s, _ = m.encoder(x, mask)
     torch.testing.assert_close(enc_k.float(), enc_s.detach().float(), atol=5e-2, rtol=5e-2)
     assert gen_k.shape == (2, 6)
+
+
+@pytest.mark.gpu
+def test_t5_graph_generation_matches_eager(cuda):
+    torch.manual_seed(0)
+    m = T5ForConditionalGeneration(T5Config.small(), device=cuda).eval()
+    x = torch.randint(2, 32128, (3, 24), device=cuda)
+    mask = torch.ones_like(x)
+    mask[2, 18:] = 0
+    eager = m.generate(x, mask, max_new_tokens=10, use_graph=False)
+    graph = m._generate_graph(x, mask, 10)
+    assert torch.equal(eager, graph)
