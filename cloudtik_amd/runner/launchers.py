@@ -31,6 +31,15 @@ from cloudtik_amd.runner.affinity import rank_cpu_sets
 from cloudtik_amd.runner.distributor import Distributor
 
 
+def cloudtik_rsh_agent(rsh: Optional[str]) -> Optional[str]:
+    """``--rsh cloudtik`` selects the ``cloudtik-rsh`` agent (remote commands through
+    ``cloudtik head exec --node-ip``; reference runtime/ai/scripts/cloudtik-rsh.sh)."""
+    if rsh in ("cloudtik", "cloudtik-rsh"):
+        return shutil.which("cloudtik-rsh") or os.path.join(
+            os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "bin", "cloudtik-rsh")
+    return None
+
+
 def _is_local(host: str) -> bool:
     if host in ("localhost", "127.0.0.1", socket.gethostname()):
         return True
@@ -197,7 +206,8 @@ class DistributedLauncher(Launcher):
         if not self.args.master_addr:
             first = placements[0][0] if placements else "127.0.0.1"
             self.args.master_addr = "127.0.0.1" if _is_local(first) and len(placements) == 1 else first
-        rsh = shlex.split(getattr(self.args, "rsh", None) or self.rsh_default)
+        agent = cloudtik_rsh_agent(getattr(self.args, "rsh", None))
+        rsh = [agent] if agent else shlex.split(getattr(self.args, "rsh", None) or self.rsh_default)
         threads, codes = [], {}
 
         def run_host(host, node_rank, n, first):
@@ -224,6 +234,10 @@ class MPILauncher(Launcher):
             raise RuntimeError("mpirun not found: use --launcher distributed (RCCL does not need MPI)")
         hosts = ",".join(f"{h}:{n}" for h, _, n, _ in self.d.host_ranks())
         cmd = [mpirun, "-np", str(self.d.num_proc), "-H", hosts, "--bind-to", "none"]
+        agent = cloudtik_rsh_agent(getattr(self.args, "rsh", None))
+        if agent:
+            # OpenMPI spawns its remote daemons through the agent (reference mpi_launcher.py:81)
+            cmd += ["-mca", "plm_rsh_agent", agent]
         env = self.base_env()
         for k in ("MASTER_ADDR", "MASTER_PORT", "WORLD_SIZE", "HSA_ENABLE_IPC_MODE_LEGACY"):
             cmd += ["-x", k]

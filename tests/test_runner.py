@@ -110,3 +110,21 @@ def test_run_function_api():
     from cloudtik_amd.runner import run
     out = run(lambda x: (int(os.environ["RANK"]), x * 2), args=(21,), num_proc=2, master_port=_port())
     assert out == [(0, 42), (1, 42)]
+
+
+def test_cloudtik_rsh_agent_routes_through_head_exec(tmp_path):
+    """--rsh cloudtik starts remote node launchers with `cloudtik head exec CMD --node-ip IP`
+    (reference runtime/ai/scripts/cloudtik-rsh.sh); a fake cloudtik runs them locally."""
+    job = tmp_path / "job.py"
+    job.write_text(JOB)
+    fake = tmp_path / "fake_cloudtik"
+    calls = tmp_path / "calls.txt"
+    fake.write_text('#!/bin/bash\n# args: head exec "<cmd>" --node-ip=<ip>\necho "$4" >> %s\n'
+                    'export PATH="%s:$PATH"\nexec bash -c "$3"\n' % (calls, os.path.join(ROOT, "bin")))
+    fake.chmod(0o755)
+    r = subprocess.run([RUN, "--hosts", "10.255.0.3:1,10.255.0.4:1", "--rsh", "cloudtik", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), str(job)], capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, PYTHONPATH=ROOT, CLOUDTIK_BIN=str(fake)))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert sorted(calls.read_text().split()) == ["--node-ip=10.255.0.3", "--node-ip=10.255.0.4"]
+    assert sorted(int(l[1]) for l in _results(tmp_path)) == [0, 1]
