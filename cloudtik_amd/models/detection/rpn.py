@@ -72,6 +72,44 @@ class RPN(nn.Module):
         keep = ops.batched_nms(b, s, lvl, self.nms_thresh)[:post]
         return b[keep]
 
+    def _select_batched(self, obj: List[torch.Tensor], reg: List[torch.Tensor], anchors: List[torch.Tensor],
+                        image_sizes: List[Tuple[int, int]]) -> List[torch.Tensor]:
+        """All images at once: obj[l] [N, HWA], reg[l] [N, HWA, 4] -> proposals per image.
+
+        Same result as ``_select`` per image, but boxes are decoded only where the top-k
+        selected them, and every (image, level) pair is one segment of a single segmented-NMS
+        launch (static segment offsets: no host sync until the final per-image counts).
+        Boxes failing the size filter are parked as empty boxes far outside the image, so
+        they suppress nothing, and are dropped afterwards."""
+        pre = self.pre_nms_top_n[0 if self.training else 1]
+        post = self.post_nms_top_n[0 if self.training else 1]
+        N = obj[0].shape[0]
+        sc, bx, ks = [], [], []
+        for o, r, a in zip(obj, reg, anchors):
+            k = min(pre, o.shape[1])
+            s, i = o.topk(k, dim=1)                                              # sorted, [N, k]
+            codes = r.gather(1, i[..., None].expand(-1, -1, 4)).reshape(-1, 4)
+            bx.append(self.coder.decode(codes, a[i.reshape(-1)]).reshape(N, k, 4))
+            sc.append(s)
+            ks.append(k)
+        s, b = torch.cat(sc, 1), torch.cat(bx, 1)                              # [N, K], [N, K, 4]
+        K = s.shape[1]
+        hw = torch.tensor([[w, h, w, h] for h, w in image_sizes], dtype=b.dtype, device=b.device)
+        b = torch.minimum(b.clamp(min=0), hw[:, None, :])
+        ws, hs = b[..., 2] - b[..., 0], b[..., 3] - b[..., 1]
+        valid = (ws >= self.min_size) & (hs >= self.min_size)
+        b = torch.where(valid[..., None], b, torch.full_like(b, -1e4))
+        off = [0]
+        for _ in range(N):
+            for k in ks:
+                off.append(off[-1] + k)
+        keep = ops.nms_segments(b.reshape(-1, 4), off, self.nms_thresh).reshape(N, K) & valid
+        s = torch.where(keep, s, torch.full_like(s, float("-inf")))
+        top, idx = s.topk(min(post, K), dim=1)
+        counts = torch.isfinite(top).sum(1).tolist()
+        sel = b.gather(1, idx[..., None].expand(-1, -1, 4))
+        return [sel[n, :c] for n, c in enumerate(counts)]
+
     def forward(self, feats: List[torch.Tensor], image_sizes: List[Tuple[int, int]],
                 targets: Optional[List[Dict[str, torch.Tensor]]] = None):
         logits, deltas = self.head(feats)
@@ -79,11 +117,9 @@ class RPN(nn.Module):
         N = feats[0].shape[0]
         obj = [B.permute_flatten(l, 1).squeeze(-1).float() for l in logits]          # [N, HWA] per level
         reg = [B.permute_flatten(d, 4).float() for d in deltas]                      # [N, HWA, 4]
-        proposals = []
         with torch.no_grad():
-            for n in range(N):
-                dec = [self.coder.decode(r[n].detach(), a) for r, a in zip(reg, anchors)]
-                proposals.append(self._select([o[n].detach() for o in obj], dec, image_sizes[n]))
+            proposals = self._select_batched([o.detach() for o in obj], [r.detach() for r in reg], anchors,
+                                             image_sizes)
         losses = {}
         if self.training and targets is not None:
             losses = self.loss(torch.cat(obj, 1), torch.cat(reg, 1), torch.cat(anchors), targets)

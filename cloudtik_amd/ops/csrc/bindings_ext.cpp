@@ -14,6 +14,8 @@ int ct_embbag_bwd(const void*, int, float*, float*, const int64_t*, const int64_
 int ct_interact_fwd(const void*, const void*, void*, int, int, int, int, hipStream_t);
 int ct_interact_bwd(const void*, const void*, const void*, void*, void*, int, int, int, int, hipStream_t);
 int ct_nms(const float*, int, float, float, uint64_t*, int64_t*, int64_t*, hipStream_t);
+int ct_nms_segmented(const float*, const int64_t*, const int64_t*, int, int, float, float, uint64_t*, uint8_t*,
+                     hipStream_t);
 int ct_roi_align_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
 int ct_roi_align_bwd(const void*, const float*, float*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
 int ct_roi_align_nhwc_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
@@ -171,6 +173,42 @@ at::Tensor nms_sorted(at::Tensor boxes, double thr, double offset) {
                         keep.data_ptr<int64_t>(), nkeep.data_ptr<int64_t>(), stream());
   TORCH_CHECK(rc == 0, "nms launch failed");
   return keep.narrow(0, 0, nkeep.item<int64_t>());
+}
+
+// many NMS problems in one launch: boxes sorted by (segment, score desc), segment s owning
+// rows [seg_offsets[s], seg_offsets[s+1]) (host int64).  Returns uint8 keep flags per row.
+at::Tensor nms_segmented(at::Tensor boxes, at::Tensor seg_offsets, double thr, double offset) {
+  XCHECK_IN(boxes); XCHECK_DT(boxes, at::kFloat);
+  TORCH_CHECK(boxes.dim() == 2 && boxes.size(1) == 4, "nms: boxes must be [N, 4]");
+  TORCH_CHECK(!seg_offsets.is_cuda() && seg_offsets.scalar_type() == at::kLong && seg_offsets.dim() == 1 &&
+                  seg_offsets.is_contiguous(), "nms_segmented: seg_offsets must be a contiguous host int64 vector");
+  const long nseg = seg_offsets.numel() - 1;
+  const long N = boxes.size(0);
+  auto keep = at::zeros({N}, boxes.options().dtype(at::kByte));
+  if (nseg <= 0 || N == 0) return keep;
+  const int64_t* so = seg_offsets.data_ptr<int64_t>();
+  TORCH_CHECK(so[0] == 0 && so[nseg] == N, "nms_segmented: offsets must span the boxes");
+  TORCH_CHECK(nseg <= 65535, "nms_segmented: at most 65535 segments");
+  auto moff = at::empty({nseg}, seg_offsets.options());
+  int64_t* mo = moff.data_ptr<int64_t>();
+  long total = 0, max_n = 0;
+  for (long s = 0; s < nseg; ++s) {
+    const long n = so[s + 1] - so[s];
+    TORCH_CHECK(n >= 0, "nms_segmented: offsets must be non-decreasing");
+    mo[s] = total;
+    total += n * ((n + 63) / 64);
+    max_n = std::max(max_n, n);
+  }
+  TORCH_CHECK(max_n <= 524288, "nms: at most 524288 boxes per segment");
+  if (max_n == 0) return keep;
+  auto seg_d = seg_offsets.to(boxes.device());
+  auto moff_d = moff.to(boxes.device());
+  auto mask = at::empty({std::max(total, 1L)}, boxes.options().dtype(at::kLong));
+  const int rc = ct_nms_segmented(boxes.data_ptr<float>(), seg_d.data_ptr<int64_t>(), moff_d.data_ptr<int64_t>(),
+                                  (int)nseg, (int)max_n, (float)thr, (float)offset,
+                                  (uint64_t*)mask.data_ptr<int64_t>(), keep.data_ptr<uint8_t>(), stream());
+  TORCH_CHECK(rc == 0, "nms_segmented launch failed (", rc, ")");
+  return keep;
 }
 
 void check_rois(const at::Tensor& feat, const at::Tensor& rois) {
@@ -413,6 +451,7 @@ void register_ext(pybind11::module& m) {
   m.def("interact_fwd", &interact_fwd);
   m.def("interact_bwd", &interact_bwd);
   m.def("nms_sorted", &nms_sorted);
+  m.def("nms_segmented", &nms_segmented);
   m.def("roi_align_fwd", &roi_align_fwd);
   m.def("roi_align_bwd", &roi_align_bwd);
   m.def("roi_align_nhwc_fwd", &roi_align_nhwc_fwd);

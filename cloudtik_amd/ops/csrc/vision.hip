@@ -116,6 +116,96 @@ __global__ void __launch_bounds__(NMS_REDUCE_THREADS) nms_reduce_kernel(const ui
   if (tid == 0) *nkeep = count;
 }
 
+// ------------------------------------------------------------------ segmented NMS
+// Many independent NMS problems in one launch (RPN: per image x pyramid level; box head: per
+// image x class).  Boxes are sorted by (segment, score desc); segment s owns boxes
+// [seg[s], seg[s+1]) and its bitmask lives at mask + moff[s].  Mask tiles outside a segment
+// exit at once; the reduction runs one 8-wave workgroup per segment, so the serial
+// 64-box chunk walk is as long as the LARGEST segment rather than the sum of all of them.
+__global__ void __launch_bounds__(64) nms_mask_seg_kernel(const float* __restrict__ boxes,
+                                                          const int64_t* __restrict__ seg,
+                                                          const int64_t* __restrict__ moff, float thr, float offset,
+                                                          uint64_t* __restrict__ mask) {
+  const int s = blockIdx.z;
+  const long base = seg[s];
+  const int n = (int)(seg[s + 1] - base);
+  const int cb = (n + 63) / 64;
+  const int rb = blockIdx.y, colb = blockIdx.x;
+  if (rb >= cb || colb >= cb || colb < rb) return;
+  __shared__ float cbox[64 * 4];
+  const int t = threadIdx.x;
+  const int cj = colb * 64 + t;
+  if (cj < n) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cbox[t * 4 + k] = boxes[(base + cj) * 4 + k];
+  }
+  __syncthreads();
+  const int i = rb * 64 + t;
+  if (i >= n) return;
+  float me[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) me[k] = boxes[(base + i) * 4 + k];
+  uint64_t bits = 0;
+  const int cols = min(64, n - colb * 64);
+  const int start = (colb == rb) ? t + 1 : 0;
+  for (int j = start; j < cols; ++j)
+    if (iou(me, cbox + j * 4, offset) > thr) bits |= (1ull << j);
+  mask[moff[s] + (long)i * cb + colb] = bits;
+}
+
+__global__ void __launch_bounds__(NMS_REDUCE_THREADS) nms_reduce_seg_kernel(const uint64_t* __restrict__ mask_all,
+                                                                            const int64_t* __restrict__ seg,
+                                                                            const int64_t* __restrict__ moff,
+                                                                            uint8_t* __restrict__ keep) {
+  extern __shared__ uint64_t removed[];
+  __shared__ uint64_t kept_s;
+  const int s = blockIdx.x;
+  const long base = seg[s];
+  const int n = (int)(seg[s + 1] - base);
+  const int cb = (n + 63) / 64;
+  const uint64_t* mask = mask_all + moff[s];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int d = tid; d < cb; d += NMS_REDUCE_THREADS) removed[d] = 0;
+  __syncthreads();
+  for (int c = 0; c < cb; ++c) {
+    if (wave == 0) {
+      const int box = c * 64 + lane;
+      const uint64_t diag = box < n ? mask[(long)box * cb + c] : 0ull;
+      uint64_t word = removed[c];
+      const int cols = min(64, n - c * 64);
+      uint64_t kept = 0;
+      for (int k = 0; k < cols; ++k) {
+        if (!((word >> k) & 1ull)) {
+          kept |= 1ull << k;
+          word |= shfl64(diag, k);
+        }
+      }
+      if (box < n) keep[base + box] = (kept >> lane) & 1ull ? 1 : 0;
+      if (lane == 0) kept_s = kept;
+    }
+    __syncthreads();
+    const uint64_t kept = kept_s;
+    if (c + 1 < cb && kept) {
+      int rows[64 / NMS_REDUCE_WAVES + 1];
+      int nr = 0, r = 0;
+      for (uint64_t kk = kept; kk; kk &= kk - 1, ++r)
+        if ((r % NMS_REDUCE_WAVES) == wave) rows[nr++] = c * 64 + (__ffsll((unsigned long long)kk) - 1);
+      for (int d = c + 1 + lane; d < cb; d += 64) {
+        uint64_t acc = 0;
+        int i = 0;
+        for (; i + 4 <= nr; i += 4) {
+          const uint64_t a0 = mask[(long)rows[i] * cb + d], a1 = mask[(long)rows[i + 1] * cb + d];
+          const uint64_t a2 = mask[(long)rows[i + 2] * cb + d], a3 = mask[(long)rows[i + 3] * cb + d];
+          acc |= (a0 | a1) | (a2 | a3);
+        }
+        for (; i < nr; ++i) acc |= mask[(long)rows[i] * cb + d];
+        if (acc) atomicOr((unsigned long long*)&removed[d], (unsigned long long)acc);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ ROIAlign
 template <typename T>
 __device__ __forceinline__ float bilinear(const T* f, int H, int W, float y, float x) {
@@ -295,6 +385,31 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_fwd_kernel(const T* __rest
   }
 }
 
+// Backward: atomics, not arithmetic, bound this kernel.  With the detection models' sampling
+// ratio 2 the bilinear weights of a bin are separable -- W(row, col) = Wy(row) * Wx(col) with
+// Wy / Wx each summed over the bin's 2 sample rows / columns -- and neighbouring samples share
+// pixels, so a bin touches ~3 x 3 distinct pixels through its 16 taps.  The per-axis tap
+// lists (4 entries, sorted) are merged in registers (static indexing, no scratch) and one
+// fp32 atomic is issued per distinct pixel and channel.  Other sampling ratios take the
+// direct per-tap path.
+__device__ __forceinline__ void axis_taps(float v, int n, float p0, float step, int idx[4], float w[4]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float y = p0 + (s + 0.5f) * step;
+    if (y < -1.f || y > n) { idx[2 * s] = idx[2 * s + 1] = (s ? idx[1] : 0); w[2 * s] = w[2 * s + 1] = 0.f; continue; }
+    y = fmaxf(y, 0.f);
+    int y0 = (int)y, y1;
+    if (y0 >= n - 1) { y1 = y0 = n - 1; y = (float)y0; } else y1 = y0 + 1;
+    const float l = y - y0;
+    idx[2 * s] = y0; idx[2 * s + 1] = y1;
+    w[2 * s] = (1.f - l) * v; w[2 * s + 1] = l * v;
+  }
+  // merge equal neighbours (the list is non-decreasing): fold into the first occurrence
+#pragma unroll
+  for (int j = 3; j >= 1; --j)
+    if (idx[j] == idx[j - 1]) { w[j - 1] += w[j]; w[j] = 0.f; }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __restrict__ gout,
                                                                   const float* __restrict__ rois,
@@ -314,6 +429,25 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __rest
     Vec8<T>::load(gout + bin * C + cg * 8, go);
     const float inv = 1.f / fmaxf((float)(g.gh * g.gw), 1.f);
     float* f = gfeat + (long)b * H * W * C + cg * 8;
+    if (g.gh == 2 && g.gw == 2) {
+      int ry[4], cx[4];
+      float wy[4], wx[4];
+      axis_taps(inv, H, g.y0 + ph * g.bh, g.bh / 2, ry, wy);
+      axis_taps(1.f, W, g.x0 + pw * g.bw, g.bw / 2, cx, wx);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        if (wy[a] == 0.f) continue;
+#pragma unroll
+        for (int c2 = 0; c2 < 4; ++c2) {
+          const float wq = wy[a] * wx[c2];
+          if (wq == 0.f) continue;
+          float* dst = f + ((long)ry[a] * W + cx[c2]) * C;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) unsafeAtomicAdd(dst + c, go[c] * wq);
+        }
+      }
+      continue;
+    }
     for (int iy = 0; iy < g.gh; ++iy) {
       const float y = g.y0 + ph * g.bh + (iy + 0.5f) * g.bh / g.gh;
       for (int ix = 0; ix < g.gw; ++ix) {
@@ -433,6 +567,17 @@ extern "C" int ct_nms(const float* boxes, int n, float thr, float offset, uint64
   nms_mask_kernel<<<dim3(cb, cb), 64, 0, stream>>>(boxes, n, thr, offset, mask_ws, cb);
   nms_reduce_kernel<<<1, NMS_REDUCE_THREADS, cb * sizeof(uint64_t), stream>>>(mask_ws, n, cb, keep, nkeep);
   return 0;
+}
+
+// seg [nseg+1] / moff [nseg] on the device; max_n = largest segment (host-known)
+extern "C" int ct_nms_segmented(const float* boxes, const int64_t* seg, const int64_t* moff, int nseg, int max_n,
+                                float thr, float offset, uint64_t* mask_ws, uint8_t* keep, hipStream_t stream) {
+  if (nseg <= 0 || max_n <= 0) return -1;
+  const int cb = (max_n + 63) / 64;
+  if (cb * 8 > 64 * 1024 || nseg > 65535) return -2;
+  nms_mask_seg_kernel<<<dim3(cb, cb, nseg), 64, 0, stream>>>(boxes, seg, moff, thr, offset, mask_ws);
+  nms_reduce_seg_kernel<<<nseg, NMS_REDUCE_THREADS, cb * sizeof(uint64_t), stream>>>(mask_ws, seg, moff, keep);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 extern "C" int ct_roi_align_fwd(const void* feat, const float* rois, void* out, int dt, int K, int C, int H, int W,

@@ -54,10 +54,41 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float, offset:
     return nms_reference(boxes, scores, iou_threshold, offset)
 
 
+def nms_segments(boxes: torch.Tensor, offsets, iou_threshold: float, offset: float = 0.0) -> torch.Tensor:
+    """Keep mask (bool [N]) for many independent NMS problems at once: segment ``s`` is rows
+    ``offsets[s]:offsets[s+1]`` of ``boxes``, each segment already sorted by decreasing score.
+    On the GPU this is ONE mask launch + one reduction launch with a workgroup per segment
+    (csrc/vision.hip ``nms_*_seg_kernel``), so the serial chunk walk is as long as the largest
+    segment instead of the sum of all of them (the box-shift trick)."""
+    off = torch.as_tensor(offsets, dtype=torch.long).cpu().contiguous()
+    if boxes.is_cuda and _use_native(boxes):
+        return _native().nms_segmented(boxes.float().contiguous(), off, float(iou_threshold), float(offset)).bool()
+    keep = torch.zeros(boxes.shape[0], dtype=torch.bool, device=boxes.device)
+    for s in range(off.numel() - 1):
+        lo, hi = int(off[s]), int(off[s + 1])
+        if hi > lo:
+            b = boxes[lo:hi]
+            # sorted already: the reference's argsort of a decreasing ramp is the identity
+            k = nms_reference(b, torch.arange(hi - lo, 0, -1, device=b.device, dtype=torch.float32),
+                              iou_threshold, offset)
+            keep[lo + k] = True
+    return keep
+
+
 def batched_nms(boxes, scores, idxs, iou_threshold, offset=0.0):
-    """NMS per category: boxes of different ``idxs`` never suppress each other."""
+    """NMS per category: boxes of different ``idxs`` never suppress each other.  Returns kept
+    indices by decreasing score.  On the GPU every category is its own segment of one
+    segmented-NMS launch (one host sync for the segment sizes)."""
     if boxes.numel() == 0:
         return torch.empty(0, dtype=torch.long, device=boxes.device)
+    if boxes.is_cuda and _use_native(boxes):
+        order = scores.argsort(descending=True, stable=True)
+        order = order[idxs[order].argsort(stable=True)]             # (category, score desc)
+        _, counts = torch.unique_consecutive(idxs[order], return_counts=True)
+        off = torch.zeros(counts.numel() + 1, dtype=torch.long)
+        off[1:] = counts.cpu().cumsum(0)
+        kept = order[nms_segments(boxes[order], off, iou_threshold, offset)]
+        return kept[scores[kept].argsort(descending=True, stable=True)]
     shift = idxs.to(boxes.dtype)[:, None] * (boxes.max() + 1 + offset)
     return nms(boxes + shift, scores, iou_threshold, offset)
 

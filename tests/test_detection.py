@@ -283,7 +283,8 @@ def test_nms_large_matches_reference(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_roi_align_nhwc_matches_reference(cuda, dtype):
+@pytest.mark.parametrize("sr", [2, 3])
+def test_roi_align_nhwc_matches_reference(cuda, dtype, sr):
     from cloudtik_amd import ops
     from cloudtik_amd.ops.vision import roi_align_vectorized
     g = torch.Generator().manual_seed(11)
@@ -292,10 +293,10 @@ def test_roi_align_nhwc_matches_reference(cuda, dtype):
     wh = torch.rand(40, 2, generator=g) * 30 + 0.5
     rois = torch.cat([torch.randint(0, 2, (40, 1), generator=g).float(), xy, xy + wh], 1)
     fg = f.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
-    out = ops.roi_align(fg, rois.to(cuda), 7, 0.5, 2, True)
+    out = ops.roi_align(fg, rois.to(cuda), 7, 0.5, sr, True)
     assert out.is_contiguous(memory_format=torch.channels_last)
     fr = f.clone().requires_grad_()
-    ref = roi_align_vectorized(fr, rois, (7, 7), 0.5, 2, True)
+    ref = roi_align_vectorized(fr, rois, (7, 7), 0.5, sr, True)
     tol = dict(atol=2e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(out.float().cpu(), ref.to(dtype).float(), **tol)
     go = torch.randn(ref.shape, generator=g)
@@ -303,3 +304,76 @@ def test_roi_align_nhwc_matches_reference(cuda, dtype):
     ref.backward(go)
     torch.testing.assert_close(fg.grad.float().cpu(), fr.grad, **(dict(atol=5e-2, rtol=5e-2)
                                                                    if dtype == torch.bfloat16 else tol))
+
+
+def _clustered_boxes(n, seed, spread=600):
+    g = torch.Generator().manual_seed(seed)
+    ctr = torch.rand(max(n // 16, 1), 2, generator=g) * spread
+    pts = ctr[torch.randint(0, ctr.shape[0], (n,), generator=g)] + torch.randn(n, 2, generator=g) * 6
+    wh = torch.rand(n, 2, generator=g) * 40 + 10
+    return torch.cat([pts, pts + wh], 1), torch.rand(n, generator=g)
+
+
+def test_rpn_batched_selection_matches_per_image_cpu():
+    """The all-images segmented-NMS proposal path keeps exactly what the per-image
+    (level-shifted batched_nms) path keeps."""
+    from cloudtik_amd.models.detection.rpn import RPN
+    torch.manual_seed(0)
+    ag = B.AnchorGenerator(((32,), (64,)), (0.5, 1.0, 2.0), (8, 16))
+    rpn = RPN(16, ag, pre_nms_top_n=(300, 200), post_nms_top_n=(150, 100), min_size=2.0).eval()
+    feats = [torch.randn(2, 16, 20, 24), torch.randn(2, 16, 10, 12)]
+    sizes = [(150, 180), (160, 190)]
+    with torch.no_grad():
+        logits, deltas = rpn.head(feats)
+        anchors = ag(feats)
+        obj = [B.permute_flatten(l, 1).squeeze(-1).float() for l in logits]
+        reg = [B.permute_flatten(d, 4).float() * 2 for d in deltas]
+        got = rpn._select_batched(obj, reg, anchors, sizes)
+        for n in range(2):
+            dec = [rpn.coder.decode(r[n], a) for r, a in zip(reg, anchors)]
+            ref = rpn._select([o[n] for o in obj], dec, sizes[n])
+            assert got[n].shape == ref.shape
+            torch.testing.assert_close(got[n], ref)
+
+
+def test_nms_segments_cpu_matches_per_segment():
+    from cloudtik_amd import ops
+    from cloudtik_amd.ops.vision import nms_reference
+    boxes, scores = _clustered_boxes(400, 3, spread=200)
+    off = [0, 0, 130, 131, 400]
+    sb, ss = [], []
+    for lo, hi in zip(off[:-1], off[1:]):
+        o = scores[lo:hi].argsort(descending=True)
+        sb.append(boxes[lo:hi][o])
+        ss.append(scores[lo:hi][o])
+    b, s = torch.cat(sb), torch.cat(ss)
+    keep = ops.nms_segments(b, off, 0.5)
+    for lo, hi in zip(off[:-1], off[1:]):
+        ref = torch.zeros(hi - lo, dtype=torch.bool)
+        if hi > lo:
+            ref[nms_reference(b[lo:hi], s[lo:hi], 0.5)] = True
+        assert torch.equal(keep[lo:hi], ref)
+
+
+@pytest.mark.gpu
+def test_segmented_nms_gpu_matches_reference(cuda):
+    """Segmented kernel: empty, single-box and multi-chunk segments in one launch, and
+    batched_nms (category segments) vs the box-shift CPU path."""
+    from cloudtik_amd import ops
+    from cloudtik_amd.ops.vision import nms_reference
+    boxes, scores = _clustered_boxes(3000, 7, spread=300)
+    off = [0, 0, 1, 700, 700, 2999, 3000]
+    b = torch.cat([boxes[lo:hi][scores[lo:hi].argsort(descending=True)] for lo, hi in zip(off[:-1], off[1:])])
+    keep = ops.nms_segments(b.to(cuda), off, 0.6).cpu()
+    ramp = torch.arange(3000, 0, -1).float()
+    for lo, hi in zip(off[:-1], off[1:]):
+        ref = torch.zeros(hi - lo, dtype=torch.bool)
+        if hi > lo:
+            ref[nms_reference(b[lo:hi], ramp[lo:hi], 0.6)] = True
+        # ties at exactly the threshold may flip a box or two between fp paths
+        assert (keep[lo:hi] != ref).sum() <= 2
+    idx = torch.randint(0, 17, (3000,), generator=torch.Generator().manual_seed(1))
+    got = ops.batched_nms(boxes.to(cuda), scores.to(cuda), idx.to(cuda), 0.5).cpu()
+    ref = ops.batched_nms(boxes, scores, idx, 0.5)
+    assert (scores[got][1:] <= scores[got][:-1]).all()
+    assert len(set(got.tolist()) ^ set(ref.tolist())) <= 4
