@@ -299,7 +299,8 @@ __global__ void __launch_bounds__(256) roi_align_bwd_kernel(const T* __restrict_
 // the 32 threads of a 256-channel bin read one contiguous 512-byte row segment (no NCHW
 // transpose of the pyramid, and the [K, PH, PW, C] output is the channels_last layout the
 // box / mask head convolutions consume).  Backward scatters with per-channel fp32 atomics
-// into an NHWC gradient; neighbouring lanes hit neighbouring addresses.
+// into an NHWC gradient; neighbouring lanes hit neighbouring addresses (the backward gives
+// each lane channels cg, cg + C/8, ... for that).
 template <typename T> struct Vec8;
 template <> struct Vec8<bf16_t> {
   __device__ static void load(const bf16_t* p, float v[8]) {
@@ -425,10 +426,15 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __rest
     const float* r = rois + k * 5;
     const int b = (int)r[0];
     const RoiGeom g = roi_geom(r, scale, PH, PW, sr, aligned);
+    // lane-strided channels (cg, cg + CG, ...): consecutive lanes of a wave add into
+    // consecutive floats, so every atomic instruction covers whole 128 B lines instead of
+    // scattering 4 B per lane over 32 B strides
     float go[8];
-    Vec8<T>::load(gout + bin * C + cg * 8, go);
+    const T* gp = gout + bin * C + cg;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) go[c] = to_f<T>(gp[c * CG]);
     const float inv = 1.f / fmaxf((float)(g.gh * g.gw), 1.f);
-    float* f = gfeat + (long)b * H * W * C + cg * 8;
+    float* f = gfeat + (long)b * H * W * C + cg;
     if (g.gh == 2 && g.gw == 2) {
       int ry[4], cx[4];
       float wy[4], wx[4];
@@ -443,7 +449,7 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __rest
           if (wq == 0.f) continue;
           float* dst = f + ((long)ry[a] * W + cx[c2]) * C;
 #pragma unroll
-          for (int c = 0; c < 8; ++c) unsafeAtomicAdd(dst + c, go[c] * wq);
+          for (int c = 0; c < 8; ++c) unsafeAtomicAdd(dst + c * CG, go[c] * wq);
         }
       }
       continue;
@@ -459,7 +465,7 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __rest
           float* dst = f + (long)t.o[q] * C;
           const float wq = t.w[q] * inv;
 #pragma unroll
-          for (int c = 0; c < 8; ++c) unsafeAtomicAdd(dst + c, go[c] * wq);
+          for (int c = 0; c < 8; ++c) unsafeAtomicAdd(dst + c * CG, go[c] * wq);
         }
       }
     }

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Steady-state per-step kernel summary from a rocprofv3 ``*_kernel_trace.csv``.
+
+Warmup (MIOpen find, TunableOp tuning, first-call JIT) swamps ``--stats`` totals.  This tool
+cuts the trace at a kernel that runs exactly once per training step (the fused optimizer by
+default), keeps the last ``--steps`` complete steps, and prints per-step kernel time by name,
+the GPU-busy time and the wall span of a step (busy / span = how launch- or host-bound the
+step is).
+
+    python scripts/steady_profile.py gpurun_out/prof/x_kernel_trace.csv --delim sgd_kernel --steps 5
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--delim", default="sgd_kernel", help="substring of the once-per-step kernel name")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    rows = []
+    with open(a.csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    marks = [i for i, r in enumerate(rows) if a.delim in r[2]]
+    # the optimizer may be split over several launches per step: keep the first of each run
+    starts = [m for j, m in enumerate(marks) if j == 0 or m != marks[j - 1] + 1]
+    if len(starts) < a.steps + 1:
+        raise SystemExit(f"only {len(starts)} '{a.delim}' launches; need {a.steps + 1}")
+    lo, hi = starts[-a.steps - 1] + 1, starts[-1] + 1
+    win = rows[lo:hi]
+    tot = defaultdict(float)
+    cnt = defaultdict(int)
+    for s, e, n in win:
+        tot[n] += (e - s) / 1e3
+        cnt[n] += 1
+    busy = sum(tot.values()) / a.steps
+    span = (rows[starts[-1]][1] - rows[starts[-a.steps - 1]][1]) / 1e3 / a.steps
+    print(f"## {a.title or a.csv}\n")
+    print(f"Steady state over the last {a.steps} steps (cut at `{a.delim}`): GPU-busy {busy / 1e3:.2f} ms "
+          f"per step, step span {span / 1e3:.2f} ms ({100 * busy / span:.0f}% busy), "
+          f"{len(win) / a.steps:.0f} kernels per step.\n")
+    print("| kernel | ms/step | calls/step | % busy |\n|---|---:|---:|---:|")
+    for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
+        short = n if len(n) <= 100 else n[:97] + "..."
+        print(f"| `{short}` | {t / a.steps / 1e3:.3f} | {cnt[n] / a.steps:.0f} | {100 * t / a.steps / busy:.1f} |")
+
+
+if __name__ == "__main__":
+    main()
