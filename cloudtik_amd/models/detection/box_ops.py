@@ -101,14 +101,14 @@ class Matcher:
     def __call__(self, iou: torch.Tensor) -> torch.Tensor:
         if iou.numel() == 0:
             return torch.full((iou.shape[1],), self.BELOW_LOW, dtype=torch.long, device=iou.device)
+        # elementwise selects only: boolean-mask assignment would go through nonzero() and
+        # stall the host on the GPU once per call
         vals, idx = iou.max(0)
-        out = idx.clone()
-        out[vals < self.low] = self.BELOW_LOW
-        out[(vals >= self.low) & (vals < self.high)] = self.BETWEEN
+        out = torch.where(vals < self.low, torch.full_like(idx, self.BELOW_LOW),
+                          torch.where(vals < self.high, torch.full_like(idx, self.BETWEEN), idx))
         if self.allow_low_quality:
             best = iou.max(1, keepdim=True).values
-            gt_i, col = torch.nonzero((iou == best) & (best > 0), as_tuple=True)
-            out[col] = idx[col]
+            out = torch.where(((iou == best) & (best > 0)).any(0), idx, out)
         return out
 
 
@@ -127,6 +127,35 @@ def sample_pos_neg(labels: torch.Tensor, batch_size: int, positive_fraction: flo
     nm = torch.zeros_like(labels, dtype=torch.bool)
     pm[pp] = True
     nm[nn_] = True
+    return pm, nm
+
+
+def sample_pos_neg_batched(labels: torch.Tensor, batch_size: int, positive_fraction: float,
+                           generator: torch.Generator = None):
+    """``sample_pos_neg`` for a batch of images at once, with no host synchronisation:
+    labels [N, A] -> boolean masks (pos, neg) [N, A].
+
+    Each candidate draws a uniform key; the positives with the ``batch_size *
+    positive_fraction`` smallest keys are taken (a uniform random subset), then the negatives
+    with the smallest keys fill the rest of the row's ``batch_size``.  Counts stay on the
+    device (top-k + comparisons), so the caller never waits for the GPU."""
+    N, A = labels.shape
+    dev = labels.device
+    P = int(batch_size * positive_fraction)
+    r = torch.rand(labels.shape, device=dev, generator=generator)
+    never = torch.full_like(r, 2.0)
+    pm = torch.zeros_like(labels, dtype=torch.bool)
+    nm = torch.zeros_like(labels, dtype=torch.bool)
+    n_pos = torch.zeros(N, 1, dtype=torch.long, device=dev)
+    if P > 0:
+        pk, pi = torch.where(labels >= 1, r, never).topk(min(P, A), dim=1, largest=False)
+        pos_ok = pk < 2
+        pm = pm.scatter(1, pi, pos_ok)
+        n_pos = pos_ok.sum(1, keepdim=True)
+    kn = min(batch_size, A)
+    nk, ni = torch.where(labels == 0, r, never).topk(kn, dim=1, largest=False)
+    neg_ok = (nk < 2) & (torch.arange(kn, device=dev)[None, :] < batch_size - n_pos)
+    nm = nm.scatter(1, ni, neg_ok)
     return pm, nm
 
 

@@ -4,7 +4,8 @@ native components N3-N4).
 
 * ``MultiScaleRoIAlign`` assigns each RoI to a pyramid level (``k = 4 + log2(sqrt(area)/224)``,
   clamped to the available levels) and pools it with the HIP ROIAlign kernel
-  (``ops.roi_align``, bwd by atomics into the feature map); one launch per level.
+  (``ops.roi_align_multilevel``, bwd by atomics into the feature maps); ONE launch for all
+  levels -- the kernel reads each RoI's level, so there is no per-level split and no host sync.
 * Mask targets are produced by the same ROIAlign kernel: the ground-truth masks are treated
   as a batch of one-channel images and every positive proposal is pooled from the mask of
   its matched object (``rois[:, 0]`` = gt index) to 28x28 -- no CPU polygon rasterisation.
@@ -64,21 +65,11 @@ class MultiScaleRoIAlign(nn.Module):
     def forward(self, feats: List[torch.Tensor], boxes: List[torch.Tensor]) -> torch.Tensor:
         rois = _to_rois(boxes)
         feats = feats[:len(self.strides)]
-        C = feats[0].shape[1]
-        out = feats[0].new_zeros(rois.shape[0], C, self.output_size, self.output_size)
-        if feats[0].is_contiguous(memory_format=torch.channels_last) and feats[0].is_cuda:
-            out = out.contiguous(memory_format=torch.channels_last)      # NHWC ROIAlign output layout
         if len(feats) == 1:
             return ops.roi_align(feats[0], rois, self.output_size, 1.0 / self.strides[0], self.sampling_ratio,
                                  self.aligned)
-        lvl = self.level_of(rois)
-        for l, f in enumerate(feats):
-            idx = torch.nonzero(lvl == l).squeeze(1)
-            if idx.numel() == 0:
-                continue
-            out = out.index_copy(0, idx, ops.roi_align(f, rois[idx], self.output_size, 1.0 / self.strides[l],
-                                                       self.sampling_ratio, self.aligned).to(out.dtype))
-        return out
+        return ops.roi_align_multilevel(feats, rois, self.level_of(rois), self.output_size,
+                                        [1.0 / s for s in self.strides], self.sampling_ratio, self.aligned)
 
 
 class TwoMLPHead(nn.Module):
@@ -170,23 +161,42 @@ class RoIHeads(nn.Module):
 
     # ------------------------------------------------------------------ training
     def _sample(self, proposals, targets):
-        out_p, out_lab, out_tgt, out_gt = [], [], [], []
+        """Fixed-size, sync-free RoI sampling: every image yields exactly
+        ``batch_size_per_image`` rows (fewer only if it has fewer candidates), ordered
+        positives first, then negatives, then padding rows (label -1, ignored by the losses).
+        Sampling is the batched top-k draw of ``B.sample_pos_neg_batched``, so no step waits
+        for a nonzero() on the host, and the box / mask heads always see the same shapes."""
+        S = self.batch_size_per_image
+        cands, labs, mids = [], [], []
         for p, t in zip(proposals, targets):
             gt = t["boxes"].to(p)
             p = torch.cat([p, gt])                     # ground truth joins the proposals
-            m = self.matcher(B.box_iou(gt, p)) if gt.numel() else torch.full((p.shape[0],), -1, device=p.device,
-                                                                            dtype=torch.long)
-            lab = t["labels"].to(p.device)[m.clamp(min=0)].long() if gt.numel() else torch.zeros_like(m)
-            lab[m == B.Matcher.BELOW_LOW] = 0
-            lab[m == B.Matcher.BETWEEN] = -1
-            pos, neg = B.sample_pos_neg(lab, self.batch_size_per_image, self.positive_fraction)
-            keep = torch.nonzero(pos | neg).squeeze(1)
-            p, lab, mi = p[keep], lab[keep], m[keep].clamp(min=0)
-            out_p.append(p)
-            out_lab.append(lab)
-            out_tgt.append(self.coder.encode(gt[mi], p) if gt.numel() else torch.zeros_like(p))
-            out_gt.append(mi)
-        return out_p, out_lab, out_tgt, out_gt
+            if gt.numel():
+                m = self.matcher(B.box_iou(gt, p))
+                lab = t["labels"].to(p.device)[m.clamp(min=0)].long()
+                lab = torch.where(m == B.Matcher.BELOW_LOW, 0, torch.where(m == B.Matcher.BETWEEN, -1, lab))
+            else:
+                m = torch.full((p.shape[0],), -1, device=p.device, dtype=torch.long)
+                lab = torch.zeros_like(m)
+            cands.append(p)
+            labs.append(lab)
+            mids.append(m.clamp(min=0))
+        L = max(c.shape[0] for c in cands)
+        pad = lambda xs, v: torch.stack([F.pad(x, (0, 0) * (x.dim() - 1) + (0, L - x.shape[0]), value=v)  # noqa: E731
+                                         for x in xs])
+        cand, lab, mid = pad(cands, 0.0), pad(labs, -1), pad(mids, 0)
+        pm, nm = B.sample_pos_neg_batched(lab, S, self.positive_fraction)
+        key = torch.where(pm, 0, torch.where(nm, 1, 2))
+        order = key.sort(dim=1, stable=True).indices[:, :min(S, L)]
+        valid = key.gather(1, order) < 2
+        sel_p = cand.gather(1, order[..., None].expand(-1, -1, 4))
+        sel_lab = torch.where(valid, lab.gather(1, order), -1)
+        sel_m = mid.gather(1, order)
+        tgts = []
+        for n, t in enumerate(targets):
+            gt = t["boxes"].to(sel_p)
+            tgts.append(self.coder.encode(gt[sel_m[n]], sel_p[n]) if gt.numel() else torch.zeros_like(sel_p[n]))
+        return list(sel_p.unbind(0)), sel_lab, torch.stack(tgts), sel_m
 
     def forward(self, feats: List[torch.Tensor], proposals: List[torch.Tensor], image_sizes: List[Tuple[int, int]],
                 targets: Optional[List[Dict[str, torch.Tensor]]] = None):
@@ -198,12 +208,13 @@ class RoIHeads(nn.Module):
         cls, reg = self.box_predictor(x)
         cls, reg = cls.float(), reg.float()
         if self.training and targets is not None:
-            lab = torch.cat(labels)
-            tgt = torch.cat(reg_t)
-            loss_cls = F.cross_entropy(cls, lab)
-            pos = torch.nonzero(lab > 0).squeeze(1)
-            r = reg.view(reg.shape[0], -1, 4)[pos, lab[pos]]
-            loss_box = B.smooth_l1(r, tgt[pos], beta=1.0 / 9) / max(lab.numel(), 1)
+            lab = labels.reshape(-1)
+            tgt = reg_t.reshape(-1, 4)
+            n_valid = (lab >= 0).sum().clamp(min=1)
+            loss_cls = F.cross_entropy(cls, lab, ignore_index=-1, reduction="sum") / n_valid
+            pos = (lab > 0).float()
+            r = reg.view(reg.shape[0], -1, 4).gather(1, lab.clamp(min=0)[:, None, None].expand(-1, 1, 4))[:, 0]
+            loss_box = (B.smooth_l1(r, tgt, beta=1.0 / 9, reduction="none").sum(-1) * pos).sum() / n_valid
             losses = {"loss_classifier": loss_cls, "loss_box_reg": loss_box}
             if self.with_mask:
                 losses["loss_mask"] = self._mask_loss(feats, props, labels, gt_idx, targets)
@@ -211,25 +222,26 @@ class RoIHeads(nn.Module):
         return self._postprocess(feats, cls, reg, props, image_sizes), {}
 
     def _mask_loss(self, feats, props, labels, gt_idx, targets):
-        pos_boxes, pos_labels, tgts = [], [], []
-        for p, lab, gi, t in zip(props, labels, gt_idx, targets):
-            pos = torch.nonzero(lab > 0).squeeze(1)
-            pos_boxes.append(p[pos])
-            pos_labels.append(lab[pos])
-            if pos.numel() == 0:
+        """Positives sit in the first ``P`` rows of every image (``_sample``'s order), so the
+        mask head always runs on exactly N x P RoIs; non-positive rows carry zero weight."""
+        P = min(int(self.batch_size_per_image * self.positive_fraction), labels.shape[1])
+        M = self.mask_head_size
+        boxes = [p[:P] for p in props]
+        lab = labels[:, :P]
+        w = (lab > 0).float()
+        tgts = []
+        for p, gi, t in zip(boxes, gt_idx[:, :P], targets):
+            masks = t["masks"]
+            if masks.shape[0] == 0:
+                tgts.append(torch.zeros(P, M, M, device=p.device))
                 continue
-            masks = t["masks"].to(device=p.device, dtype=torch.float32)[:, None]      # [G, 1, H, W]
-            rois = torch.cat([gi[pos].float()[:, None], p[pos].float()], 1)
-            M = self.mask_head_size
-            tgts.append(ops.roi_align(masks, rois, M, 1.0, 2, True)[:, 0] >= 0.5)
-        n = sum(b.shape[0] for b in pos_boxes)
-        if n == 0:
-            return sum(p.sum() * 0 for p in self.mask_head.parameters())
-        lab = torch.cat(pos_labels)
-        bound = self._mask_rows(int(self.batch_size_per_image * self.positive_fraction) * len(props))
-        x = _pad_rows(self.mask_pool(feats, pos_boxes), bound)
-        logits = self.mask_head(x, _pad_rows(lab, bound))[:n].float()
-        return F.binary_cross_entropy_with_logits(logits, torch.cat(tgts).float())
+            masks = masks.to(device=p.device, dtype=torch.float32)[:, None]            # [G, 1, H, W]
+            rois = torch.cat([gi.float()[:, None], p.float()], 1)
+            tgts.append((ops.roi_align(masks, rois, M, 1.0, 2, True)[:, 0] >= 0.5).float())
+        x = self.mask_pool(feats, boxes)
+        logits = self.mask_head(x, lab.clamp(min=0).reshape(-1)).float()
+        bce = F.binary_cross_entropy_with_logits(logits, torch.cat(tgts), reduction="none").mean((1, 2))
+        return (bce * w.reshape(-1)).sum() / w.sum().clamp(min=1)
 
     def _mask_rows(self, bound: int) -> int:
         return bound if self.pad_mask_rois else 0

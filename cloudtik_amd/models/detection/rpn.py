@@ -126,23 +126,23 @@ class RPN(nn.Module):
         return proposals, losses
 
     def loss(self, obj, reg, anchors, targets):
+        """Sync-free: matching by selects, batched top-k sampling, and losses as masked sums
+        over all anchors (no boolean indexing, whose nonzero() would stall the host)."""
         labels, tgts = [], []
-        for n, t in enumerate(targets):
+        for t in targets:
             gt = t["boxes"].to(anchors)
-            m = self.matcher(B.box_iou(gt, anchors))
-            lab = (m >= 0).float()
-            lab[m == B.Matcher.BETWEEN] = -1
+            if gt.numel():
+                m = self.matcher(B.box_iou(gt, anchors))
+                lab = torch.where(m >= 0, 1.0, torch.where(m == B.Matcher.BETWEEN, -1.0, 0.0))
+                tgts.append(self.coder.encode(gt[m.clamp(min=0)], anchors))
+            else:
+                lab = torch.zeros(anchors.shape[0], device=anchors.device)
+                tgts.append(torch.zeros_like(anchors))
             labels.append(lab)
-            tgts.append(self.coder.encode(gt[m.clamp(min=0)], anchors) if gt.numel() else torch.zeros_like(anchors))
-        pos, neg = [], []
-        for lab in labels:
-            p, q = B.sample_pos_neg(lab, self.batch_size_per_image, self.positive_fraction)
-            pos.append(p)
-            neg.append(q)
-        pos, neg = torch.stack(pos), torch.stack(neg)
         labels, tgts = torch.stack(labels), torch.stack(tgts)
-        sampled = pos | neg
-        n_s = max(int(sampled.sum()), 1)
-        box = B.smooth_l1(reg[pos], tgts[pos], beta=1.0 / 9) / n_s
-        cls = F.binary_cross_entropy_with_logits(obj[sampled], labels[sampled])
+        pos, neg = B.sample_pos_neg_batched(labels, self.batch_size_per_image, self.positive_fraction)
+        sampled = (pos | neg).float()
+        n_s = sampled.sum().clamp(min=1)
+        box = (B.smooth_l1(reg, tgts, beta=1.0 / 9, reduction="none").sum(-1) * pos).sum() / n_s
+        cls = (F.binary_cross_entropy_with_logits(obj, labels.clamp(min=0), reduction="none") * sampled).sum() / n_s
         return {"loss_objectness": cls, "loss_rpn_box_reg": box}

@@ -127,7 +127,7 @@ from .attention import attention, attention_packed, attention_relbias  # noqa: E
 from .linear import linear  # noqa: E402,F401
 from .rope import apply_rotary, rotary_cache  # noqa: E402,F401
 from .embedding import EmbeddingBagCollection, dot_interaction, embedding_bag, pack_bags  # noqa: E402,F401
-from .vision import batched_nms, images_to_tensor, nms, nms_segments, roi_align, roi_pool, sigmoid_focal_loss  # noqa: E402,F401
+from .vision import batched_nms, images_to_tensor, nms, nms_segments, roi_align, roi_align_multilevel, roi_pool, sigmoid_focal_loss  # noqa: E402,F401
 from . import multi_tensor  # noqa: E402,F401
 from .graph import CSR, SpMM, gbdt_histogram, gbdt_predict, spmm  # noqa: E402,F401
 from .deform import (DeformConv, DeformRoIPooling, DeformRoIPoolingPack, ModulatedDeformConv,  # noqa: E402,F401

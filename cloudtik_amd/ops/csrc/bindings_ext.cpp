@@ -18,8 +18,10 @@ int ct_nms_segmented(const float*, const int64_t*, const int64_t*, int, int, flo
                      hipStream_t);
 int ct_roi_align_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
 int ct_roi_align_bwd(const void*, const float*, float*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
-int ct_roi_align_nhwc_fwd(const void*, const float*, void*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
-int ct_roi_align_nhwc_bwd(const void*, const float*, float*, int, int, int, int, int, int, int, float, int, int, hipStream_t);
+int ct_roi_align_nhwc_fwd(const void* const*, const int*, const float*, int, const int*, const float*, void*, int, int,
+                          int, int, int, int, int, hipStream_t);
+int ct_roi_align_nhwc_bwd(const void*, float* const*, const int*, const float*, int, const int*, const float*, int, int,
+                          int, int, int, int, int, hipStream_t);
 int ct_roi_pool_fwd(const void*, const float*, void*, int*, int, int, int, int, int, int, int, float, hipStream_t);
 int ct_roi_pool_bwd(const void*, const float*, const int*, float*, int, int, int, int, int, int, int, hipStream_t);
 int ct_focal_fwd(const void*, const int64_t*, float*, int, long, int, float, float, hipStream_t);
@@ -237,34 +239,87 @@ at::Tensor roi_align_bwd(at::Tensor gout, at::Tensor rois, std::vector<int64_t> 
   return gout.scalar_type() == at::kFloat ? g : g.to(gout.scalar_type());
 }
 
-// channels_last features [N, C, H, W] (NHWC in memory) -> channels_last [K, C, PH, PW]
-at::Tensor roi_align_nhwc_fwd(at::Tensor feat, at::Tensor rois, double scale, int64_t PH, int64_t PW, int64_t sr,
-                              bool aligned) {
+// channels_last feature maps [N, C, H_l, W_l] (NHWC in memory; one per pyramid level) ->
+// channels_last [K, C, PH, PW].  ``lvl`` [K] int32 picks each RoI's level (undefined when
+// there is one level).  All levels in one launch.
+void check_levels(const std::vector<at::Tensor>& feats, const at::Tensor& rois, const c10::optional<at::Tensor>& lvl,
+                  const std::vector<double>& scales) {
+  TORCH_CHECK(!feats.empty() && feats.size() <= 5 && scales.size() == feats.size(), "roi_align_nhwc: 1-5 levels");
   XCHECK_IN(rois); XCHECK_DT(rois, at::kFloat);
-  TORCH_CHECK(feat.is_cuda() && feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "roi_align_nhwc: features must be channels_last");
-  TORCH_CHECK(rois.is_contiguous() && rois.dim() == 2 && rois.size(1) == 5, "rois must be [K, 5]");
-  const int K = (int)rois.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
+  TORCH_CHECK(rois.dim() == 2 && rois.size(1) == 5, "rois must be [K, 5]");
+  TORCH_CHECK(feats.size() == 1 || (lvl.has_value() && lvl->defined()), "roi_align_nhwc: levels need lvl");
+  if (lvl.has_value() && lvl->defined()) {
+    XCHECK_IN(*lvl); XCHECK_DT(*lvl, at::kInt);
+    TORCH_CHECK(lvl->numel() == rois.size(0), "roi_align_nhwc: one level per RoI");
+  }
+}
+
+at::Tensor roi_align_nhwc_fwd(std::vector<at::Tensor> feats, at::Tensor rois, c10::optional<at::Tensor> lvl,
+                              std::vector<double> scales, int64_t PH, int64_t PW, int64_t sr, bool aligned) {
+  check_levels(feats, rois, lvl, scales);
+  const auto& f0 = feats[0];
+  const int K = (int)rois.size(0), C = (int)f0.size(1);
   TORCH_CHECK(C % 8 == 0, "roi_align_nhwc: channels must be a multiple of 8");
-  auto out = at::empty({K, C, PH, PW}, feat.options(), at::MemoryFormat::ChannelsLast);
-  if (K) TORCH_CHECK(ct_roi_align_nhwc_fwd(feat.data_ptr(), rois.data_ptr<float>(), out.data_ptr(), fb(feat), K, C, H, W,
-                                           (int)PH, (int)PW, (float)scale, (int)sr, aligned ? 1 : 0, stream()) == 0);
+  std::vector<const void*> ptrs;
+  std::vector<int> hw;
+  std::vector<float> sc;
+  for (size_t l = 0; l < feats.size(); ++l) {
+    const auto& f = feats[l];
+    TORCH_CHECK(f.is_cuda() && f.dim() == 4 && f.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "roi_align_nhwc: features must be channels_last");
+    TORCH_CHECK(f.size(0) == f0.size(0) && f.size(1) == C && f.scalar_type() == f0.scalar_type(),
+                "roi_align_nhwc: levels must share batch, channels and dtype");
+    ptrs.push_back(f.data_ptr());
+    hw.push_back((int)f.size(2)); hw.push_back((int)f.size(3));
+    sc.push_back((float)scales[l]);
+  }
+  auto out = at::empty({K, C, PH, PW}, f0.options(), at::MemoryFormat::ChannelsLast);
+  const int* lp = (lvl.has_value() && lvl->defined()) ? lvl->data_ptr<int>() : nullptr;
+  if (K) TORCH_CHECK(ct_roi_align_nhwc_fwd(ptrs.data(), hw.data(), sc.data(), (int)feats.size(), lp,
+                                           rois.data_ptr<float>(), out.data_ptr(), fb(f0), K, C, (int)PH, (int)PW,
+                                           (int)sr, aligned ? 1 : 0, stream()) == 0);
   return out;
 }
 
-at::Tensor roi_align_nhwc_bwd(at::Tensor gout, at::Tensor rois, std::vector<int64_t> fshape, double scale, int64_t sr,
-                              bool aligned) {
-  XCHECK_IN(rois);
-  TORCH_CHECK(fshape.size() == 4);
+// shapes: 4 ints per level.  The fp32 gradients of all levels share one zeroed buffer (one
+// fill, one cast); each level is returned as a channels_last view of it in gout's dtype.
+std::vector<at::Tensor> roi_align_nhwc_bwd(at::Tensor gout, at::Tensor rois, c10::optional<at::Tensor> lvl,
+                                           std::vector<int64_t> shapes, std::vector<double> scales, int64_t sr,
+                                           bool aligned) {
+  const size_t nlev = scales.size();
+  TORCH_CHECK(shapes.size() == 4 * nlev && nlev >= 1 && nlev <= 5, "roi_align_nhwc_bwd: 4 dims per level");
+  XCHECK_IN(rois); XCHECK_DT(rois, at::kFloat);
+  TORCH_CHECK(nlev == 1 || (lvl.has_value() && lvl->defined()), "roi_align_nhwc_bwd: levels need lvl");
   gout = gout.contiguous(at::MemoryFormat::ChannelsLast);
-  const int K = (int)rois.size(0), C = (int)fshape[1], H = (int)fshape[2], W = (int)fshape[3];
+  const int K = (int)rois.size(0), C = (int)shapes[1];
   TORCH_CHECK(gout.dim() == 4 && gout.size(0) == K && gout.size(1) == C && C % 8 == 0);
-  // (at::zeros drops TensorOptions' memory format: allocate channels_last, then clear)
-  auto g = at::empty(fshape, gout.options().dtype(at::kFloat), at::MemoryFormat::ChannelsLast).zero_();
-  if (K) TORCH_CHECK(ct_roi_align_nhwc_bwd(gout.data_ptr(), rois.data_ptr<float>(), g.data_ptr<float>(), fb(gout), K, C,
-                                           H, W, (int)gout.size(2), (int)gout.size(3), (float)scale, (int)sr,
-                                           aligned ? 1 : 0, stream()) == 0);
-  return gout.scalar_type() == at::kFloat ? g : g.to(gout.scalar_type());
+  std::vector<int64_t> offs;
+  int64_t total = 0;
+  for (size_t l = 0; l < nlev; ++l) {
+    TORCH_CHECK(shapes[4 * l + 1] == C && shapes[4 * l] == shapes[0], "roi_align_nhwc_bwd: level shapes");
+    offs.push_back(total);
+    total += shapes[4 * l] * shapes[4 * l + 1] * shapes[4 * l + 2] * shapes[4 * l + 3];
+  }
+  auto buf = at::zeros({total}, gout.options().dtype(at::kFloat));
+  std::vector<float*> ptrs;
+  std::vector<int> hw;
+  std::vector<float> sc;
+  for (size_t l = 0; l < nlev; ++l) {
+    ptrs.push_back(buf.data_ptr<float>() + offs[l]);
+    hw.push_back((int)shapes[4 * l + 2]); hw.push_back((int)shapes[4 * l + 3]);
+    sc.push_back((float)scales[l]);
+  }
+  const int* lp = (lvl.has_value() && lvl->defined()) ? lvl->data_ptr<int>() : nullptr;
+  if (K) TORCH_CHECK(ct_roi_align_nhwc_bwd(gout.data_ptr(), ptrs.data(), hw.data(), sc.data(), (int)nlev, lp,
+                                           rois.data_ptr<float>(), fb(gout), K, C, (int)gout.size(2),
+                                           (int)gout.size(3), (int)sr, aligned ? 1 : 0, stream()) == 0);
+  if (gout.scalar_type() != at::kFloat) buf = buf.to(gout.scalar_type());
+  std::vector<at::Tensor> grads;
+  for (size_t l = 0; l < nlev; ++l) {
+    const int64_t N = shapes[4 * l], H = shapes[4 * l + 2], W = shapes[4 * l + 3];
+    grads.push_back(buf.as_strided({N, C, H, W}, {H * W * C, 1, W * C, C}, offs[l]));
+  }
+  return grads;
 }
 
 std::vector<at::Tensor> roi_pool_fwd(at::Tensor feat, at::Tensor rois, double scale, int64_t PH, int64_t PW) {

@@ -348,11 +348,28 @@ __device__ __forceinline__ Tap4 bilinear_taps(int H, int W, float y, float x) {
   return t;
 }
 
+// Pyramid levels of one multi-level ROIAlign launch (FPN P2-P5): every RoI carries its level
+// (``lvl``, int32; null = level 0), so all levels are pooled by ONE launch with no host-side
+// split (the per-level nonzero() + index_copy of a level loop costs a host sync per level).
+constexpr int kMaxLevels = 5;
+template <typename P> struct Levels {
+  P f[kMaxLevels];
+  int H[kMaxLevels], W[kMaxLevels];
+  float scale[kMaxLevels];
+};
+// select level l with static indices (v_cndmask), so the descriptor stays in kernel arguments
+template <typename P>
+__device__ __forceinline__ void pick_level(const Levels<P>& L, int l, P& f, int& H, int& W, float& scale) {
+  f = L.f[0]; H = L.H[0]; W = L.W[0]; scale = L.scale[0];
+#pragma unroll
+  for (int j = 1; j < kMaxLevels; ++j)
+    if (l == j) { f = L.f[j]; H = L.H[j]; W = L.W[j]; scale = L.scale[j]; }
+}
+
 template <typename T>
-__global__ void __launch_bounds__(256) roi_align_nhwc_fwd_kernel(const T* __restrict__ feat,
+__global__ void __launch_bounds__(256) roi_align_nhwc_fwd_kernel(const Levels<const T*> L, const int* __restrict__ lvl,
                                                                   const float* __restrict__ rois, T* __restrict__ out,
-                                                                  int K, int C, int H, int W, int PH, int PW,
-                                                                  float scale, int sr, int aligned) {
+                                                                  int K, int C, int PH, int PW, int sr, int aligned) {
   const int CG = C / 8;
   const long total = (long)K * PH * PW * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -361,6 +378,10 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_fwd_kernel(const T* __rest
     const int pw = bin % PW, ph = (bin / PW) % PH, k = bin / ((long)PW * PH);
     const float* r = rois + k * 5;
     const int b = (int)r[0];
+    const T* feat;
+    int H, W;
+    float scale;
+    pick_level(L, lvl ? lvl[k] : 0, feat, H, W, scale);
     const RoiGeom g = roi_geom(r, scale, PH, PW, sr, aligned);
     const T* f = feat + (long)b * H * W * C + cg * 8;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -412,11 +433,10 @@ __device__ __forceinline__ void axis_taps(float v, int n, float p0, float step, 
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __restrict__ gout,
-                                                                  const float* __restrict__ rois,
-                                                                  float* __restrict__ gfeat, int K, int C, int H,
-                                                                  int W, int PH, int PW, float scale, int sr,
-                                                                  int aligned) {
+__global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __restrict__ gout, const Levels<float*> L,
+                                                                  const int* __restrict__ lvl,
+                                                                  const float* __restrict__ rois, int K, int C, int PH,
+                                                                  int PW, int sr, int aligned) {
   const int CG = C / 8;
   const long total = (long)K * PH * PW * CG;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -425,6 +445,10 @@ __global__ void __launch_bounds__(256) roi_align_nhwc_bwd_kernel(const T* __rest
     const int pw = bin % PW, ph = (bin / PW) % PH, k = bin / ((long)PW * PH);
     const float* r = rois + k * 5;
     const int b = (int)r[0];
+    float* gfeat;
+    int H, W;
+    float scale;
+    pick_level(L, lvl ? lvl[k] : 0, gfeat, H, W, scale);
     const RoiGeom g = roi_geom(r, scale, PH, PW, sr, aligned);
     // lane-strided channels (cg, cg + CG, ...): consecutive lanes of a wave add into
     // consecutive floats, so every atomic instruction covers whole 128 B lines instead of
@@ -602,21 +626,34 @@ extern "C" int ct_roi_align_bwd(const void* gout, const float* rois, float* gfea
   return 0;
 }
 
-extern "C" int ct_roi_align_nhwc_fwd(const void* feat, const float* rois, void* out, int dt, int K, int C, int H,
-                                     int W, int PH, int PW, float scale, int sr, int aligned, hipStream_t stream) {
-  if (C % 8) return 1;
+// nlev levels: feats[l] / gfeats[l] NHWC maps of hw[2l] x hw[2l+1]; lvl [K] int32 on the
+// device (null when nlev == 1)
+extern "C" int ct_roi_align_nhwc_fwd(const void* const* feats, const int* hw, const float* scales, int nlev,
+                                     const int* lvl, const float* rois, void* out, int dt, int K, int C, int PH, int PW,
+                                     int sr, int aligned, hipStream_t stream) {
+  if (C % 8 || nlev < 1 || nlev > kMaxLevels || (nlev > 1 && !lvl)) return 1;
   const int g = grid1d((long)K * PH * PW * (C / 8));
-  if (dt == 0) roi_align_nhwc_fwd_kernel<float><<<g, 256, 0, stream>>>((const float*)feat, rois, (float*)out, K, C, H, W, PH, PW, scale, sr, aligned);
-  else roi_align_nhwc_fwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)feat, rois, (bf16_t*)out, K, C, H, W, PH, PW, scale, sr, aligned);
+  if (dt == 0) {
+    Levels<const float*> L{};
+    for (int l = 0; l < nlev; ++l) { L.f[l] = (const float*)feats[l]; L.H[l] = hw[2 * l]; L.W[l] = hw[2 * l + 1]; L.scale[l] = scales[l]; }
+    roi_align_nhwc_fwd_kernel<float><<<g, 256, 0, stream>>>(L, nlev > 1 ? lvl : nullptr, rois, (float*)out, K, C, PH, PW, sr, aligned);
+  } else {
+    Levels<const bf16_t*> L{};
+    for (int l = 0; l < nlev; ++l) { L.f[l] = (const bf16_t*)feats[l]; L.H[l] = hw[2 * l]; L.W[l] = hw[2 * l + 1]; L.scale[l] = scales[l]; }
+    roi_align_nhwc_fwd_kernel<bf16_t><<<g, 256, 0, stream>>>(L, nlev > 1 ? lvl : nullptr, rois, (bf16_t*)out, K, C, PH, PW, sr, aligned);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-extern "C" int ct_roi_align_nhwc_bwd(const void* gout, const float* rois, float* gfeat, int dt, int K, int C, int H,
-                                     int W, int PH, int PW, float scale, int sr, int aligned, hipStream_t stream) {
-  if (C % 8) return 1;
+extern "C" int ct_roi_align_nhwc_bwd(const void* gout, float* const* gfeats, const int* hw, const float* scales,
+                                     int nlev, const int* lvl, const float* rois, int dt, int K, int C, int PH, int PW,
+                                     int sr, int aligned, hipStream_t stream) {
+  if (C % 8 || nlev < 1 || nlev > kMaxLevels || (nlev > 1 && !lvl)) return 1;
   const int g = grid1d((long)K * PH * PW * (C / 8));
-  if (dt == 0) roi_align_nhwc_bwd_kernel<float><<<g, 256, 0, stream>>>((const float*)gout, rois, gfeat, K, C, H, W, PH, PW, scale, sr, aligned);
-  else roi_align_nhwc_bwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)gout, rois, gfeat, K, C, H, W, PH, PW, scale, sr, aligned);
+  Levels<float*> L{};
+  for (int l = 0; l < nlev; ++l) { L.f[l] = gfeats[l]; L.H[l] = hw[2 * l]; L.W[l] = hw[2 * l + 1]; L.scale[l] = scales[l]; }
+  if (dt == 0) roi_align_nhwc_bwd_kernel<float><<<g, 256, 0, stream>>>((const float*)gout, L, nlev > 1 ? lvl : nullptr, rois, K, C, PH, PW, sr, aligned);
+  else roi_align_nhwc_bwd_kernel<bf16_t><<<g, 256, 0, stream>>>((const bf16_t*)gout, L, nlev > 1 ? lvl : nullptr, rois, K, C, PH, PW, sr, aligned);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

@@ -158,18 +158,56 @@ class _RoiAlignFn(torch.autograd.Function):
 
 
 class _RoiAlignNHWCFn(torch.autograd.Function):
+    """One launch over 1-5 NHWC pyramid levels; ``lvl`` (int32 [K] or None) is each RoI's
+    level.  Backward returns every level's gradient from one shared zeroed fp32 buffer."""
+
     @staticmethod
-    def forward(ctx, feat, rois, output_size, scale, sr, aligned):
+    def forward(ctx, rois, lvl, output_size, scales, sr, aligned, *feats):
         rois = rois.float().contiguous()
-        ctx.save_for_backward(rois)
-        ctx.meta = (list(feat.shape), scale, sr, aligned)
-        return _native().roi_align_nhwc_fwd(feat, rois, scale, output_size[0], output_size[1], sr, aligned)
+        ctx.save_for_backward(rois, lvl)
+        shapes = [d for f in feats for d in f.shape]
+        ctx.meta = (shapes, list(scales), sr, aligned)
+        return _native().roi_align_nhwc_fwd(list(feats), rois, lvl, list(scales), output_size[0], output_size[1],
+                                            sr, aligned)
 
     @staticmethod
     def backward(ctx, g):
-        (rois,) = ctx.saved_tensors
-        shape, scale, sr, aligned = ctx.meta
-        return (_native().roi_align_nhwc_bwd(g, rois, shape, scale, sr, aligned), None, None, None, None, None)
+        rois, lvl = ctx.saved_tensors
+        shapes, scales, sr, aligned = ctx.meta
+        grads = _native().roi_align_nhwc_bwd(g, rois, lvl, shapes, scales, sr, aligned)
+        return (None, None, None, None, None, None, *grads)
+
+
+def _nhwc_ok(f: torch.Tensor) -> bool:
+    return f.dim() == 4 and f.shape[1] % 8 == 0 and f.shape[1] > 1 and \
+        f.is_contiguous(memory_format=torch.channels_last)
+
+
+def roi_align_multilevel(feats, rois, levels, output_size, scales, sampling_ratio: int = 2, aligned: bool = False):
+    """Pool every RoI from its own pyramid level: ``levels[k]`` indexes ``feats`` / ``scales``.
+
+    On the GPU (channels_last maps) this is one kernel for all levels and all RoIs -- no
+    per-level split, so no host sync; elsewhere a per-level loop over ``roi_align``."""
+    if isinstance(output_size, int):
+        output_size = (output_size, output_size)
+    if feats[0].is_cuda and _use_native(feats[0]) and all(_nhwc_ok(f) for f in feats) and len(feats) <= 5:
+        lvl = levels.to(torch.int32).contiguous() if len(feats) > 1 else None
+        return _RoiAlignNHWCFn.apply(rois, lvl, tuple(output_size), tuple(float(s) for s in scales),
+                                     int(sampling_ratio), bool(aligned), *feats)
+    out = None
+    for l, (f, s) in enumerate(zip(feats, scales)):
+        idx = torch.nonzero(levels == l).squeeze(1)
+        if idx.numel() == 0:
+            continue
+        o = roi_align(f, rois[idx], output_size, s, sampling_ratio, aligned)
+        if out is None:
+            out = o.new_zeros((rois.shape[0],) + tuple(o.shape[1:]))
+            if o.is_contiguous(memory_format=torch.channels_last) and o.is_cuda:
+                out = out.contiguous(memory_format=torch.channels_last)
+        out = out.index_copy(0, idx, o.to(out.dtype))
+    if out is None:
+        out = feats[0].new_zeros(rois.shape[0], feats[0].shape[1], *output_size)
+    return out
 
 
 def roi_align_vectorized(feat, rois, output_size, spatial_scale=1.0, sampling_ratio=2, aligned=False):
@@ -220,11 +258,10 @@ def roi_align(feat, rois, output_size, spatial_scale: float = 1.0, sampling_rati
     if isinstance(output_size, int):
         output_size = (output_size, output_size)
     if feat.is_cuda and _use_native(feat):
-        if feat.dim() == 4 and feat.shape[1] % 8 == 0 and feat.shape[1] > 1 and \
-                feat.is_contiguous(memory_format=torch.channels_last):
+        if _nhwc_ok(feat):
             # NHWC maps (FPN pyramids): vectorised channel-contiguous kernel, channels_last output
-            return _RoiAlignNHWCFn.apply(feat, rois, tuple(output_size), float(spatial_scale), int(sampling_ratio),
-                                         bool(aligned))
+            return _RoiAlignNHWCFn.apply(rois, None, tuple(output_size), (float(spatial_scale),),
+                                         int(sampling_ratio), bool(aligned), feat)
         return _RoiAlignFn.apply(feat, rois, tuple(output_size), float(spatial_scale), int(sampling_ratio), bool(aligned))
     if sampling_ratio > 0:
         return roi_align_vectorized(feat, rois, output_size, spatial_scale, sampling_ratio, aligned)

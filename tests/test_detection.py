@@ -306,6 +306,56 @@ def test_roi_align_nhwc_matches_reference(cuda, dtype, sr):
                                                                    if dtype == torch.bfloat16 else tol))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_roi_align_multilevel_matches_per_level(cuda, dtype):
+    """One launch over 4 NHWC levels (each RoI reads its own level) vs the CPU per-level loop,
+    forward and the per-level feature gradients."""
+    from cloudtik_amd import ops
+    g = torch.Generator().manual_seed(13)
+    shapes = [(2, 32, 40, 48), (2, 32, 20, 24), (2, 32, 10, 12), (2, 32, 5, 6)]
+    feats = [torch.randn(s, generator=g) for s in shapes]
+    K = 60
+    xy = torch.rand(K, 2, generator=g) * 150
+    wh = torch.rand(K, 2, generator=g) * 120 + 2
+    rois = torch.cat([torch.randint(0, 2, (K, 1), generator=g).float(), xy, xy + wh], 1)
+    lvl = torch.randint(0, 4, (K,), generator=g)
+    scales = [1 / 4, 1 / 8, 1 / 16, 1 / 32]
+    fg = [f.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_() for f in feats]
+    out = ops.roi_align_multilevel(fg, rois.to(cuda), lvl.to(cuda), 7, scales, 2, False)
+    fr = [f.clone().requires_grad_() for f in feats]
+    ref = ops.roi_align_multilevel(fr, rois, lvl, 7, scales, 2, False)
+    tol = dict(atol=2e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(out.float().cpu(), ref.to(dtype).float(), **tol)
+    go = torch.randn(ref.shape, generator=g)
+    out.backward(go.to(cuda, dtype))
+    ref.backward(go)
+    for a, b in zip(fg, fr):
+        assert a.grad.shape == b.grad.shape
+        torch.testing.assert_close(a.grad.float().cpu(), b.grad, **(dict(atol=5e-2, rtol=5e-2)
+                                                                   if dtype == torch.bfloat16 else tol))
+
+
+def test_sample_pos_neg_batched_counts_and_uniformity():
+    g = torch.Generator().manual_seed(2)
+    lab = torch.full((3, 1000), -1)
+    lab[0, :50] = 1                     # few positives: all taken, negatives fill the rest
+    lab[0, 50:900] = 0
+    lab[1, :400] = 2                    # many positives: capped at 64
+    lab[1, 400:] = 0
+    lab[2, :10] = 0                     # almost nothing to draw from
+    pm, nm = B.sample_pos_neg_batched(lab, 256, 0.25, generator=g)
+    assert pm[0].sum() == 50 and nm[0].sum() == 206
+    assert pm[1].sum() == 64 and nm[1].sum() == 192
+    assert pm[2].sum() == 0 and nm[2].sum() == 10
+    assert not (pm & nm).any() and (lab[pm] >= 1).all() and (lab[nm] == 0).all()
+    hits = torch.zeros(400)
+    for _ in range(200):
+        p, _ = B.sample_pos_neg_batched(lab[1:2], 256, 0.25, generator=g)
+        hits += p[0, :400].float()
+    assert hits.min() > 0 and hits.max() < 4 * hits.mean()   # every positive gets drawn
+
+
 def _clustered_boxes(n, seed, spread=600):
     g = torch.Generator().manual_seed(seed)
     ctr = torch.rand(max(n // 16, 1), 2, generator=g) * spread
