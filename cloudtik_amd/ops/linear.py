@@ -25,6 +25,8 @@ _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 # gradients -- the bucketed all-reduce and the optimizer -- order themselves after this
 # stream via ``grad_stream_event()`` / ``sync_grad_stream()``.
 _WGRAD_STREAM = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM", "1") == "1"
+# weight-gradient GEMMs through the HIP gemm_tn kernel instead of hipBLASLt
+_HIP_WGRAD = os.environ.get("CLOUDTIK_AMD_WGRAD_KERNEL", "blas") == "hip"
 _streams = {}
 
 
@@ -86,6 +88,16 @@ def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> No
     T, N = dy2.shape
     K = x2.shape[1]
     S = splitk_factor(T, N, K) if (g.is_cuda and g.dtype == torch.bfloat16 and g.is_contiguous()) else 1
+    if _HIP_WGRAD and S > 1 and N % 256 == 0 and K % 256 == 0 and T % (64 * S) == 0:
+        # hand-written MFMA kernel (csrc/gemm.hip): fp32 slabs straight from the [T, N] / [T, K]
+        # operands through transposing LDS reads; parity with hipBLASLt on the BERT shapes
+        # (bench/gemm_tn_probe.py), so opt-in
+        from cloudtik_amd import ops
+        C = ops.require_native()
+        P = torch.empty(S, N, K, device=g.device, dtype=torch.float32)
+        if C.gemm_tn(dy2.contiguous(), x2.contiguous(), P, S, 0):
+            C.splitk_reduce(P, g, True)
+            return
     if S == 1:
         g.addmm_(dy2.t(), x2)
         return
