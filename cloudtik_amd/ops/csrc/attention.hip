@@ -122,8 +122,8 @@ __global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                 \
     const int key_ = (kt_) * 64 + srow + 32 * i_;                                    \
     const bool ok_ = key_ < a.Sk;                                                    \
-    stK[i_] = ok_ ? *reinterpret_cast<const u16x8*>(kp + (long)key_ * a.k_ss + sch * 8) : u16x8(0); \
-    stV[i_] = ok_ ? *reinterpret_cast<const u16x8*>(vp + (long)key_ * a.v_ss + sch * 8) : u16x8(0); \
+    stK[i_] = ok_ ? *reinterpret_cast<const u16x8*>(kp + (key_ * (int)a.k_ss + sch * 8)) : u16x8(0); \
+    stV[i_] = ok_ ? *reinterpret_cast<const u16x8*>(vp + (key_ * (int)a.v_ss + sch * 8)) : u16x8(0); \
   }                                                                                  \
   if (tid < 64) {                                                                    \
     const int kk_ = (kt_) * 64 + tid;                                                \
@@ -317,6 +317,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   const bf16_t* qbase = a.q + b * a.q_sb + h * a.q_sh;
   const bf16_t* dobase = a.dO + b * a.do_sb + h * a.do_sh;
   const bf16_t* obase = a.o + b * a.o_sb + h * a.o_sh;
+  bf16_t* dqbase = a.dq + b * a.dq_sb + h * a.dq_sh;
   const int trow = (lane >> 2) & 3;
   const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
   const int nq = (a.Sq + 31) / 32;
@@ -335,9 +336,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   {                                                                                         \
     const int q_ = (qb_) + prow;                                                            \
     const bool ok_ = q_ < a.Sq;                                                             \
-    pQ = ok_ ? *reinterpret_cast<const u16x8*>(qbase + (long)q_ * a.q_ss + pch * 8) : u16x8(0); \
-    pdO = ok_ ? *reinterpret_cast<const u16x8*>(dobase + (long)q_ * a.do_ss + pch * 8) : u16x8(0); \
-    pO = ok_ ? *reinterpret_cast<const u16x8*>(obase + (long)q_ * a.o_ss + pch * 8) : u16x8(0); \
+    pQ = ok_ ? *reinterpret_cast<const u16x8*>(qbase + (q_ * (int)a.q_ss + pch * 8)) : u16x8(0); \
+    pdO = ok_ ? *reinterpret_cast<const u16x8*>(dobase + (q_ * (int)a.do_ss + pch * 8)) : u16x8(0); \
+    pO = ok_ ? *reinterpret_cast<const u16x8*>(obase + (q_ * (int)a.o_ss + pch * 8)) : u16x8(0); \
     if (tid < 32) {                                                                         \
       const bool ok2_ = (qb_) + tid < a.Sq;                                                 \
       pL = ok2_ ? a.lse[(long)bh * a.Sq + (qb_) + tid] : INFINITY;                          \
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
         const int d = dt_q * 32 + r;
         const float val = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
         if (q < a.Sq) {
-          if (single_block) a.dq[b * a.dq_sb + h * a.dq_sh + (long)q * a.dq_ss + d] = f2bf(val);
+          if (single_block) dqbase[q * (int)a.dq_ss + d] = f2bf(val);
           else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
         }
       }
@@ -530,6 +531,9 @@ static void drop_params(float p, uint64_t seed, uint64_t offset, uint32_t* thr16
 }
 
 // strides: [batch, seq, head] in elements for each tensor; head_dim must be 64 (contiguous)
+// the kernels index rows inside one (batch, head) slice with 32-bit offsets
+static inline bool fits32(long rows, long row_stride) { return rows * row_stride + 64 < (1L << 31); }
+
 extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const long* ks,
                            const void* v, const long* vs, void* o, const long* os,
                            const float* kbias, long kb_sb, float* lse, int B, int H, int Sq,
@@ -537,6 +541,7 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
                            int causal, hipStream_t stream) {
   if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return -1;
   if (p_drop > 0.f && (Sk % 2)) return -2;
+  if (!fits32(Sq, qs[1]) || !fits32(Sk, ks[1]) || !fits32(Sk, vs[1]) || !fits32(Sq, os[1])) return -5;
   AttnFwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
   a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
@@ -567,6 +572,7 @@ extern "C" int ct_attn_fwd_relbias(const void* q, const long* qs, const void* k,
                                    float scale, int causal, hipStream_t stream) {
   if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0 || relb_len <= 0) return -1;
   if (relb_len > kRelBiasMax) return -4;
+  if (!fits32(Sq, qs[1]) || !fits32(Sk, ks[1]) || !fits32(Sk, vs[1]) || !fits32(Sq, os[1])) return -5;
   AttnFwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
   a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
@@ -596,6 +602,8 @@ extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const l
                            uint64_t offset, int causal, hipStream_t stream) {
   if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return -1;
   if (p_drop > 0.f && (Sk % 2)) return -2;
+  if (!fits32(Sq, qs[1]) || !fits32(Sk, ks[1]) || !fits32(Sk, vs[1]) || !fits32(Sq, os[1]) ||
+      !fits32(Sq, dos[1]) || !fits32(Sq, dqs[1])) return -5;
   const long rows = (long)B * H * Sq;
   AttnBwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.dO = (const bf16_t*)dO;
