@@ -5,8 +5,8 @@ node").
 The provider interface, config schema, defaults and instance templates are kept so cluster
 YAML stays portable.  ``AWSNodeProvider`` is implemented against boto3 (EC2 instances as
 nodes, tags as node tags, ``cloudtik-cluster-name`` filters); it needs boto3 and
-credentials at run time.  GCP / Azure / Aliyun / Huawei Cloud raise a clear error naming the
-SDK they need -- their resource-provisioning code is not part of this build.
+credentials at run time.  Aliyun / Huawei Cloud raise a clear error naming the
+SDK they need.  GCP and Azure are implemented over their REST APIs in rest_providers.py.
 """
 from __future__ import annotations
 
@@ -108,12 +108,8 @@ class _SDKProvider(NodeProvider):
         raise NotImplementedError
 
 
-class GCPNodeProvider(_SDKProvider):
-    sdk, name = "googleapiclient", "gcp"
-
-
-class AzureNodeProvider(_SDKProvider):
-    sdk, name = "azure.mgmt.compute", "azure"
+# GCP and Azure speak the clouds' REST APIs directly (no SDK needed): rest_providers.py
+from cloudtik_amd.providers.cloud.rest_providers import AzureNodeProvider, GCPNodeProvider  # noqa: E402,F401
 
 
 class AliyunNodeProvider(_SDKProvider):
