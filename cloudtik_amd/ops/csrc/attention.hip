@@ -466,14 +466,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     }
     __syncthreads();   // (B2) red visible; staged tile t+1 visible for the next iteration
     if (kh == 0) {
+      const int d = dt_q * 32 + r;
+      if (single_block && qb + 32 <= a.Sq) {
+        // whole tile in range (every q-tile when Sq % 32 == 0): no per-element exec-mask
+        // branches around the 16 stores
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const int d = dt_q * 32 + r;
-        const float val = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
-        if (q < a.Sq) {
-          if (single_block) dqbase[q * (int)a.dq_ss + d] = f2bf(val);
-          else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
+        for (int i = 0; i < 16; ++i) {
+          const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          dqbase[q * (int)a.dq_ss + d] = f2bf((acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const float val = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
+          if (q < a.Sq) {
+            if (single_block) dqbase[q * (int)a.dq_ss + d] = f2bf(val);
+            else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
+          }
         }
       }
     }
