@@ -268,7 +268,7 @@ struct AttnBwdArgs {
   uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
 };
 
-template <bool DROP>
+template <bool DROP, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   // LDS: Q tile 4K | dO tile 4K | K block 16K | dS 8K | dQ pair-reduce 8K | lse, delta
   // LDS: Q tile 4K | dO tile 4K | K block 16K | V block 16K | dS^T 8K | dQ pair-reduce 8K | lse, delta
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
       for (int j = 0; j < 4; ++j) {
         const int i = 4 * g + j;
         float x = fmaf(S[i], a.scale_log2, kb2);
-        if (a.causal && key_l > qb + 8 * g + 4 * hh + j) x = -INFINITY;
+        if (CAUSAL && key_l > qb + 8 * g + 4 * hh + j) x = -INFINITY;
         const float p = __builtin_amdgcn_exp2f(x - L4[j]);
         float pd = p, dpv = dP[i];
         if (DROP) {
@@ -635,8 +635,15 @@ extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const l
   if (nkb > 1 && !dq_acc) return -3;
   if (nkb > 1) hipMemsetAsync(dq_acc, 0, sizeof(float) * rows * 64, stream);
   dim3 grid(nkb, B * H);
-  if (p_drop > 0.f) attn_bwd_d64_kernel<true><<<grid, 256, 0, stream>>>(a);
-  else attn_bwd_d64_kernel<false><<<grid, 256, 0, stream>>>(a);
+  // causal masking is a template parameter (as in the forward): no per-element test of a
+  // runtime flag in the non-causal (BERT) kernel
+  if (p_drop > 0.f) {
+    if (causal) attn_bwd_d64_kernel<true, true><<<grid, 256, 0, stream>>>(a);
+    else attn_bwd_d64_kernel<true, false><<<grid, 256, 0, stream>>>(a);
+  } else {
+    if (causal) attn_bwd_d64_kernel<false, true><<<grid, 256, 0, stream>>>(a);
+    else attn_bwd_d64_kernel<false, false><<<grid, 256, 0, stream>>>(a);
+  }
   if (nkb > 1)
     attn_dq_convert_kernel<<<(int)((rows * 64 + 255) / 256), 256, 0, stream>>>(
         dq_acc, (bf16_t*)dq, dqs[0], dqs[1], dqs[2], B, H, Sq);
