@@ -260,7 +260,11 @@ class Trainer:
             if self.rank == 0:
                 logger.info("epoch %d done: %s", epoch, m)
             if self.checkpointer is not None:
-                self._save(epoch + 1)
+                if done:
+                    # stopped by max_steps, possibly mid-epoch: resume inside this epoch
+                    self._save(epoch, {"batches_in_epoch": self._epoch_batches})
+                else:
+                    self._save(epoch + 1)
             if done:
                 break
         if self._pending_save is not None:
