@@ -185,6 +185,11 @@ class RoIHeads(nn.Module):
         pad = lambda xs, v: torch.stack([F.pad(x, (0, 0) * (x.dim() - 1) + (0, L - x.shape[0]), value=v)  # noqa: E731
                                          for x in xs])
         cand, lab, mid = pad(cands, 0.0), pad(labs, -1), pad(mids, 0)
+        # padding candidates become 1x1 boxes (never sampled: label -1), so pooling and box
+        # encoding stay finite
+        n_real = torch.tensor([c.shape[0] for c in cands], device=cand.device)
+        is_pad = torch.arange(L, device=cand.device)[None, :] >= n_real[:, None]
+        cand = torch.where(is_pad[..., None], cand.new_tensor([0.0, 0.0, 1.0, 1.0]), cand)
         pm, nm = B.sample_pos_neg_batched(lab, S, self.positive_fraction)
         key = torch.where(pm, 0, torch.where(nm, 1, 2))
         order = key.sort(dim=1, stable=True).indices[:, :min(S, L)]
@@ -214,7 +219,10 @@ class RoIHeads(nn.Module):
             loss_cls = F.cross_entropy(cls, lab, ignore_index=-1, reduction="sum") / n_valid
             pos = (lab > 0).float()
             r = reg.view(reg.shape[0], -1, 4).gather(1, lab.clamp(min=0)[:, None, None].expand(-1, 1, 4))[:, 0]
-            loss_box = (B.smooth_l1(r, tgt, beta=1.0 / 9, reduction="none").sum(-1) * pos).sum() / n_valid
+            # non-positive rows (negatives, padding, zero-width proposals whose encoded targets
+            # are inf) regress onto themselves: zero loss AND zero, finite gradient
+            tgt = torch.where(pos[:, None] > 0, tgt, r.detach())
+            loss_box = B.smooth_l1(r, tgt, beta=1.0 / 9, reduction="none").sum() / n_valid
             losses = {"loss_classifier": loss_cls, "loss_box_reg": loss_box}
             if self.with_mask:
                 losses["loss_mask"] = self._mask_loss(feats, props, labels, gt_idx, targets)

@@ -143,6 +143,8 @@ class RPN(nn.Module):
         pos, neg = B.sample_pos_neg_batched(labels, self.batch_size_per_image, self.positive_fraction)
         sampled = (pos | neg).float()
         n_s = sampled.sum().clamp(min=1)
-        box = (B.smooth_l1(reg, tgts, beta=1.0 / 9, reduction="none").sum(-1) * pos).sum() / n_s
+        # non-positive anchors regress onto themselves: zero loss and zero, finite gradient
+        tgts = torch.where(pos[..., None], tgts, reg.detach())
+        box = B.smooth_l1(reg, tgts, beta=1.0 / 9, reduction="none").sum() / n_s
         cls = (F.binary_cross_entropy_with_logits(obj, labels.clamp(min=0), reduction="none") * sampled).sum() / n_s
         return {"loss_objectness": cls, "loss_rpn_box_reg": box}

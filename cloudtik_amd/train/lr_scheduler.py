@@ -91,3 +91,28 @@ class StepDecayScheduler(_Sched):
     def step(self):
         self.last_epoch += 1
         self._set(self.get_lr())
+
+
+class WarmupMultiStepScheduler(_Sched):
+    """Mask R-CNN / SSD schedule (maskrcnn_benchmark solver/lr_scheduler.py WarmupMultiStepLR):
+    linear warm-up from ``warmup_factor`` x lr over ``warmup_steps``, then x``gamma`` at
+    each milestone step."""
+
+    def __init__(self, optimizer, milestones, gamma=0.1, warmup_factor=1.0 / 3, warmup_steps=500):
+        super().__init__(optimizer)
+        self.milestones, self.gamma = sorted(int(m) for m in milestones), gamma
+        self.warmup_factor, self.warmup_steps = warmup_factor, warmup_steps
+        self._set(self.get_lr())
+
+    def get_lr(self):
+        e = self.last_epoch
+        f = 1.0
+        if e < self.warmup_steps:
+            a = e / max(1, self.warmup_steps)
+            f = self.warmup_factor * (1 - a) + a
+        decay = self.gamma ** sum(1 for m in self.milestones if e >= m)
+        return [b * f * decay for b in self.base_lrs]
+
+    def step(self):
+        self.last_epoch += 1
+        self._set(self.get_lr())
