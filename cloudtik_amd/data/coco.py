@@ -162,7 +162,8 @@ class CocoLoader:
 
     def __init__(self, ds: CocoDetection, batch_size: int, min_size: int = 800, max_size: int = 1333,
                  rank: int = 0, world: int = 1, seed: int = 0, workers: int = 8, prefetch: int = 2,
-                 flip_prob: float = 0.5, device=None, size_divisibility: int = 32, drop_last: bool = True):
+                 flip_prob: float = 0.5, device=None, size_divisibility: int = 32, drop_last: bool = True,
+                 fixed_canvas: bool = False):
         self.ds, self.batch_size = ds, batch_size
         self.min_size, self.max_size = min_size, max_size
         self.rank, self.world, self.seed = rank, world, seed
@@ -170,6 +171,10 @@ class CocoLoader:
         self.flip_prob = flip_prob if ds.train else 0.0
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.div, self.drop_last, self.epoch = size_divisibility, drop_last, 0
+        # fixed_canvas: batches are grouped by orientation (reference AspectRatioGroupedBatchSampler)
+        # and padded to one canvas per orientation, so the conv / GEMM shapes take two values
+        # for the whole run -- MIOpen solver lookups and kernel selection happen once, not per batch
+        self.fixed_canvas = fixed_canvas
         self._pool = None
 
     def __len__(self):
@@ -185,8 +190,19 @@ class CocoLoader:
         per = n // self.world if self.drop_last else -(-n // self.world)
         idx = idx[self.rank * per:(self.rank + 1) * per]
         rng = random.Random(self.seed * 7919 + self.epoch)
-        for b in range(len(self)):
-            sel = idx[b * self.batch_size:(b + 1) * self.batch_size]
+        if self.fixed_canvas:
+            land = [i for i in idx if self.ds.images[int(i)][0]["width"] >= self.ds.images[int(i)][0]["height"]]
+            port = [i for i in idx if self.ds.images[int(i)][0]["width"] < self.ds.images[int(i)][0]["height"]]
+            groups = [g[b:b + self.batch_size] for g in (land, port) for b in range(0, len(g), self.batch_size)]
+            if self.ds.train:
+                rng.shuffle(groups)
+            if self.drop_last:
+                # full batches only, and every rank yields len(self) of them (collectives stay matched)
+                groups = [g for g in groups if len(g) == self.batch_size]
+                groups = (groups * len(self))[:len(self)] if groups else []
+        else:
+            groups = [idx[b * self.batch_size:(b + 1) * self.batch_size] for b in range(len(self))]
+        for sel in groups:
             if len(sel) == 0:
                 break
             tasks = []
@@ -199,6 +215,9 @@ class CocoLoader:
     def _collate(self, samples, ids):
         H = max(s[4][0] for s in samples)
         W = max(s[4][1] for s in samples)
+        if self.fixed_canvas:
+            lo, hi = -(-self.min_size // self.div) * self.div, -(-self.max_size // self.div) * self.div
+            H, W = (lo, hi) if W >= H and H <= lo else (hi, lo) if H > W and W <= lo else (hi, hi)
         H, W = -(-H // self.div) * self.div, -(-W // self.div) * self.div
         imgs = torch.zeros(len(samples), 3, H, W)
         targets, sizes, scales = [], [], []

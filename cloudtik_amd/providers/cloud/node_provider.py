@@ -5,8 +5,8 @@ node").
 The provider interface, config schema, defaults and instance templates are kept so cluster
 YAML stays portable.  ``AWSNodeProvider`` is implemented against boto3 (EC2 instances as
 nodes, tags as node tags, ``cloudtik-cluster-name`` filters); it needs boto3 and
-credentials at run time.  Aliyun / Huawei Cloud raise a clear error naming the
-SDK they need.  GCP and Azure are implemented over their REST APIs in rest_providers.py.
+credentials at run time.  GCP and Azure are implemented over their REST APIs in
+rest_providers.py, Aliyun and Huawei Cloud over their signed HTTP APIs in signed_providers.py.
 """
 from __future__ import annotations
 
@@ -94,27 +94,9 @@ class AWSNodeProvider(NodeProvider):
             self.client.terminate_instances(InstanceIds=list(node_ids))
 
 
-class _SDKProvider(NodeProvider):
-    sdk = ""
-    name = ""
-
-    def __init__(self, provider_config, cluster_name):
-        super().__init__(provider_config, cluster_name)
-        _require(self.sdk, self.name)
-        raise NotImplementedError(f"{self.name}: VM provisioning is not implemented in this build; use the local, "
-                                  "onpremise or virtual providers for MI355X hosts")
-
-    def non_terminated_nodes(self, tag_filters):  # pragma: no cover
-        raise NotImplementedError
-
-
 # GCP and Azure speak the clouds' REST APIs directly (no SDK needed): rest_providers.py
 from cloudtik_amd.providers.cloud.rest_providers import AzureNodeProvider, GCPNodeProvider  # noqa: E402,F401
 
 
-class AliyunNodeProvider(_SDKProvider):
-    sdk, name = "aliyunsdkcore", "aliyun"
-
-
-class HuaweiCloudNodeProvider(_SDKProvider):
-    sdk, name = "huaweicloudsdkecs", "huaweicloud"
+# Aliyun and Huawei Cloud speak the clouds' signed HTTP APIs (no SDK needed): signed_providers.py
+from cloudtik_amd.providers.cloud.signed_providers import AliyunNodeProvider, HuaweiCloudNodeProvider  # noqa: E402,F401,E501

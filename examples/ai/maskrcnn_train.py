@@ -46,6 +46,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, nargs="*", default=[60000, 80000])
     ap.add_argument("--warmup-iters", type=int, default=500)
     ap.add_argument("--workers", type=int, default=8)
+    ap.add_argument("--no-fixed-canvas", action="store_true",
+                    help="pad each batch to its own size instead of one canvas per orientation")
     ap.add_argument("--ckpt-dir", default="")
     ap.add_argument("--ckpt-every", type=int, default=2500)
     ap.add_argument("--log-every", type=int, default=20)
@@ -117,6 +119,8 @@ def main(argv=None):
     from cloudtik_amd.train.trainer import Trainer, setup_distributed
 
     rank, world, device = setup_distributed()
+    import logging
+    logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING, format="%(asctime)s %(message)s")
     torch.manual_seed(args.seed)
     with_masks = args.model == "maskrcnn"
     root = args.coco_root
@@ -128,9 +132,9 @@ def main(argv=None):
     dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
     model = build(train_ds.num_classes, device=device, dtype=dtype)
     train = CocoLoader(train_ds, args.batch, args.min_size, args.max_size, rank=rank, world=world, seed=args.seed,
-                       workers=args.workers, device=device)
+                       workers=args.workers, device=device, fixed_canvas=not args.no_fixed_canvas)
     val = CocoLoader(val_ds, args.batch, args.min_size, args.max_size, rank=rank, world=world, workers=args.workers,
-                     device=device, drop_last=False)
+                     device=device, drop_last=False, fixed_canvas=not args.no_fixed_canvas)
     result = {}
     if not args.eval_only:
         lr = args.lr * args.batch * world / 16

@@ -176,3 +176,176 @@ def test_gcp_launch_failure_is_structured():
     with pytest.raises(NodeLaunchException) as e:
         p.create_node({}, {T.CLOUDTIK_TAG_NODE_KIND: "worker"}, 1)
     assert e.value.category == "GCPInsertFailed" and "QUOTA" in e.value.description
+
+
+# ------------------------------------------------------------- Aliyun / Huawei Cloud (signed)
+from cloudtik_amd.providers.cloud.signed_providers import (AliyunNodeProvider, HuaweiCloudNodeProvider,  # noqa: E402
+                                                           aliyun_sign, huawei_sign)
+
+
+def test_aliyun_signature_known_answer():
+    """The worked example of Aliyun's RPC signature v1.0 documentation (DescribeRegions)."""
+    p = dict(Timestamp="2016-02-23T12:46:24Z", Format="XML", AccessKeyId="testid", Action="DescribeRegions",
+             SignatureMethod="HMAC-SHA1", SignatureNonce="3ee8c1b8-83d3-44af-a94f-4e0ad82fd6cf",
+             Version="2014-05-26", SignatureVersion="1.0")
+    assert aliyun_sign(p, "testsecret") == "OLeaidS1JvxuMvnyHOwuJ+uX5qY="
+
+
+def test_huawei_signature_shape_and_sensitivity():
+    hdr = {"Host": "ecs.cn-north-4.myhuaweicloud.com", "X-Sdk-Date": "20240101T000000Z",
+           "Content-Type": "application/json"}
+    url = "https://ecs.cn-north-4.myhuaweicloud.com/v1/p/cloudservers/detail"
+    a = huawei_sign("GET", url, {"offset": 1, "limit": 100}, hdr, b"", "AK", "SK")
+    m = re.fullmatch(r"SDK-HMAC-SHA256 Access=AK, SignedHeaders=content-type;host;x-sdk-date, Signature=([0-9a-f]{64})", a)
+    assert m
+    # query order does not matter (canonical sort); any change of path / query / body / key does
+    assert huawei_sign("GET", url, {"limit": 100, "offset": 1}, hdr, b"", "AK", "SK") == a
+    for args in [("GET", url + "x", {"offset": 1, "limit": 100}, hdr, b"", "AK", "SK"),
+                 ("GET", url, {"offset": 2, "limit": 100}, hdr, b"", "AK", "SK"),
+                 ("POST", url, {"offset": 1, "limit": 100}, hdr, b"{}", "AK", "SK"),
+                 ("GET", url, {"offset": 1, "limit": 100}, hdr, b"", "AK", "SK2")]:
+        assert huawei_sign(*args) != a
+
+
+class FakeAliyunECS:
+    def __init__(self):
+        self.inst, self.calls, self.n = {}, [], 0
+
+    @staticmethod
+    def _indexed(params, prefix):
+        out, i = [], 1
+        while f"{prefix}.{i}" in params:
+            out.append(params[f"{prefix}.{i}"])
+            i += 1
+        return out
+
+    def __call__(self, action, params):
+        self.calls.append((action, params))
+        assert params["RegionId"] == "cn-hangzhou"
+        tags = {}
+        i = 1
+        while f"Tag.{i}.Key" in params:
+            tags[params[f"Tag.{i}.Key"]] = params[f"Tag.{i}.Value"]
+            i += 1
+        if action == "RunInstances":
+            ids = []
+            for _ in range(int(params["Amount"])):
+                self.n += 1
+                iid = f"i-{self.n:04d}"
+                self.inst[iid] = {"InstanceId": iid, "Status": "Pending", "InstanceType": params["InstanceType"],
+                                  "Tags": {"Tag": [{"TagKey": k, "TagValue": v} for k, v in tags.items()]},
+                                  "VpcAttributes": {"PrivateIpAddress": {"IpAddress": [f"172.16.0.{self.n}"]}},
+                                  "PublicIpAddress": {"IpAddress": []}, "EipAddress": {"IpAddress": ""}}
+                ids.append(iid)
+            return {"InstanceIdSets": {"InstanceIdSet": ids}}
+        if action == "DescribeInstances":
+            sel = list(self.inst.values())
+            if "InstanceIds" in params:
+                want = set(__import__("json").loads(params["InstanceIds"]))
+                sel = [x for x in sel if x["InstanceId"] in want]
+            sel = [x for x in sel if all({t["TagKey"]: t["TagValue"] for t in x["Tags"]["Tag"]}.get(k) == v
+                                         for k, v in tags.items())]
+            ps, pn = int(params["PageSize"]), int(params["PageNumber"])
+            return {"Instances": {"Instance": sel[(pn - 1) * ps:pn * ps]}, "TotalCount": len(sel)}
+        if action == "TagResources":
+            assert params["ResourceType"] == "instance"
+            inst = self.inst[params["ResourceId.1"]]
+            cur = {t["TagKey"]: t["TagValue"] for t in inst["Tags"]["Tag"]}
+            cur.update(tags)
+            inst["Tags"]["Tag"] = [{"TagKey": k, "TagValue": v} for k, v in cur.items()]
+            return {}
+        if action == "DeleteInstances":
+            assert params["Force"] == "true"
+            for iid in self._indexed(params, "InstanceId"):
+                del self.inst[iid]
+            return {}
+        raise AssertionError(action)
+
+
+def test_aliyun_provider_contract():
+    api = FakeAliyunECS()
+    p = AliyunNodeProvider({"region": "cn-hangzhou", "_transport": api}, "c1")
+    other = AliyunNodeProvider({"region": "cn-hangzhou", "_transport": api}, "c2")
+    made = p.create_node({"InstanceType": "ecs.gn8-mi355x", "ImageId": "img"}, {T.CLOUDTIK_TAG_NODE_KIND: "worker"}, 2)
+    other.create_node({"InstanceType": "ecs.g7"}, {T.CLOUDTIK_TAG_NODE_KIND: "head"}, 1)
+    assert len(made) == 2 and sorted(p.non_terminated_nodes({})) == sorted(made)
+    assert p.non_terminated_nodes({T.CLOUDTIK_TAG_NODE_KIND: "head"}) == []
+    a = sorted(made)[0]
+    assert not p.is_running(a) and not p.is_terminated(a)
+    api.inst[a]["Status"] = "Running"
+    p.non_terminated_nodes({})
+    assert p.is_running(a) and p.internal_ip(a).startswith("172.16.") and p.external_ip(a) is None
+    p.set_node_tags(a, {T.CLOUDTIK_TAG_NODE_STATUS: "up-to-date"})
+    assert p.node_tags(a)[T.CLOUDTIK_TAG_NODE_STATUS] == "up-to-date"
+    assert p.non_terminated_nodes({T.CLOUDTIK_TAG_NODE_STATUS: "up-to-date"}) == [a]
+    p.terminate_nodes(list(made))
+    assert p.non_terminated_nodes({}) == [] and len(other.non_terminated_nodes({})) == 1
+    assert p.is_terminated(a)
+
+
+class FakeHuaweiECS:
+    def __init__(self):
+        self.srv, self.calls, self.n = {}, [], 0
+
+    def __call__(self, method, url, params, body):
+        self.calls.append((method, url, params, body))
+        m = re.match(r"https://ecs\.cn-north-4\.myhuaweicloud\.com/(v1|v1\.1)/proj/cloudservers(.*)$", url)
+        assert m, url
+        ver, rest = m.groups()
+        if ver == "v1.1" and method == "POST" and rest == "":
+            s = body["server"]
+            assert s["flavorRef"] and s["imageRef"] and s["nics"][0]["subnet_id"] == "sn"
+            ids = []
+            for _ in range(s["count"]):
+                self.n += 1
+                sid = f"srv-{self.n}"
+                self.srv[sid] = {"id": sid, "status": "BUILD", "tags": [f"{t['key']}={t['value']}"
+                                                                         for t in s["server_tags"]],
+                                 "addresses": {"vpc": [{"addr": f"192.168.0.{self.n}", "OS-EXT-IPS:type": "fixed"}]}}
+                ids.append(sid)
+            return {"job_id": "j1", "serverIds": ids}
+        if method == "GET" and rest == "/detail":
+            lim, off = params["limit"], params["offset"]
+            vals = list(self.srv.values())
+            return {"servers": vals[(off - 1) * lim:off * lim], "count": len(vals)}
+        if method == "POST" and rest == "/delete":
+            for s in body["servers"]:
+                self.srv.pop(s["id"])
+            return {"job_id": "j2"}
+        sid = rest.split("/")[1]
+        if sid not in self.srv:
+            raise CloudAPIError(404, "not found")
+        if method == "GET":
+            return {"server": self.srv[sid]}
+        if rest.endswith("/tags/action"):
+            assert body["action"] == "create"
+            cur = dict(t.partition("=")[::2] for t in self.srv[sid]["tags"])
+            cur.update({t["key"]: t["value"] for t in body["tags"]})
+            self.srv[sid]["tags"] = [f"{k}={v}" for k, v in cur.items()]
+            return {}
+        raise AssertionError(url)
+
+
+def test_huaweicloud_provider_contract():
+    api = FakeHuaweiECS()
+    cfg = {"region": "cn-north-4", "project_id": "proj", "_transport": api}
+    p = HuaweiCloudNodeProvider(cfg, "c1")
+    made = p.create_node({"flavor": "mi355x.8xlarge", "image_id": "img", "vpc_id": "vpc", "subnet_id": "sn"},
+                         {T.CLOUDTIK_TAG_NODE_KIND: "worker"}, 3)
+    HuaweiCloudNodeProvider(cfg, "c2").create_node({"flavor": "f", "image_id": "i", "subnet_id": "sn"}, {}, 1)
+    assert sorted(p.non_terminated_nodes({})) == sorted(made)
+    a = sorted(made)[0]
+    assert not p.is_running(a) and not p.is_terminated(a)
+    api.srv[a]["status"] = "ACTIVE"
+    p.non_terminated_nodes({})
+    assert p.is_running(a) and p.internal_ip(a).startswith("192.168.0.") and p.external_ip(a) is None
+    p.set_node_tags(a, {T.CLOUDTIK_TAG_NODE_STATUS: "up-to-date"})
+    assert p.non_terminated_nodes({T.CLOUDTIK_TAG_NODE_STATUS: "up-to-date"}) == [a]
+    p.terminate_nodes(list(made))
+    assert p.non_terminated_nodes({}) == [] and p.is_terminated(a)
+
+
+def test_factory_resolves_signed_providers():
+    from cloudtik_amd.core.provider_factory import _NODE_PROVIDERS
+    assert _NODE_PROVIDERS["aliyun"]() is AliyunNodeProvider
+    assert _NODE_PROVIDERS["huaweicloud"]() is HuaweiCloudNodeProvider

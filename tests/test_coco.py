@@ -127,3 +127,31 @@ def test_warmup_multistep_schedule():
         lrs.append(O.param_groups[0]["lr"])
     assert lrs[0] == pytest.approx(0.02 / 3) and lrs[2] == pytest.approx(0.02)
     assert lrs[4] == pytest.approx(0.002) and lrs[6] == pytest.approx(0.0002)
+
+
+def test_fixed_canvas_groups_by_orientation(tmp_path):
+    """fixed_canvas: one padded canvas per orientation, batches never mix orientations, every
+    eval image is still visited once, and train ranks yield equal batch counts."""
+    import json
+    from PIL import Image
+    from cloudtik_amd.data.coco import CocoDetection, CocoLoader
+    images, anns = [], []
+    for i, (w, h) in enumerate([(200, 120), (120, 200), (210, 100), (100, 190), (220, 130), (180, 110), (90, 170)]):
+        Image.new("RGB", (w, h), (i * 20, 40, 90)).save(tmp_path / f"{i}.jpg")
+        images.append({"id": i + 1, "file_name": f"{i}.jpg", "width": w, "height": h})
+        anns.append({"id": i + 1, "image_id": i + 1, "category_id": 1, "iscrowd": 0, "bbox": [5, 5, 40, 30],
+                     "area": 1200.0, "segmentation": [[5, 5, 45, 5, 45, 35, 5, 35]]})
+    ann = tmp_path / "ann.json"
+    ann.write_text(json.dumps({"images": images, "annotations": anns, "categories": [{"id": 1, "name": "a"}]}))
+    ds = CocoDetection(str(tmp_path), str(ann), train=False, with_masks=False)
+    ld = CocoLoader(ds, 2, min_size=96, max_size=160, workers=0, fixed_canvas=True, drop_last=False)
+    seen, shapes = [], set()
+    for imgs, _, sizes, ids, _ in ld:
+        shapes.add(tuple(imgs.shape[2:]))
+        assert len({h >= w for h, w in sizes}) == 1 or len(sizes) == 1
+        seen += list(ids)
+    assert sorted(seen) == list(range(1, 8)) and shapes <= {(96, 160), (160, 96)}
+    tr = CocoDetection(str(tmp_path), str(ann), train=True, with_masks=False)
+    counts = [sum(1 for _ in CocoLoader(tr, 2, 96, 160, rank=r, world=2, workers=0, fixed_canvas=True))
+              for r in range(2)]
+    assert counts[0] == counts[1] == len(CocoLoader(tr, 2, 96, 160, rank=0, world=2, workers=0))
