@@ -1,0 +1,89 @@
+// Bindings for the one-shot P2P all-reduce (p2p.hip): IPC export / import of staging and
+// signal buffers and the launch.  Pointers cross the Python boundary as integers; every
+// launch re-checks ranks, sizes, dtype and alignment before anything reaches the GPU.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+extern "C" {
+size_t ct_p2p_signal_bytes();
+int ct_p2p_alloc_signal(void**);
+int ct_p2p_alloc(void**, size_t);
+int ct_p2p_free(void*);
+int ct_ipc_get(void*, char*);
+int ct_ipc_handle_size();
+int ct_ipc_open(const char*, void**);
+int ct_ipc_close(void*);
+int ct_p2p_allreduce(const void* const*, uint32_t* const*, void*, long, int, int, int, uint32_t, uint32_t, int,
+                     hipStream_t);
+}
+
+namespace {
+
+int64_t p2p_alloc(int64_t bytes, bool signal) {
+  void* p = nullptr;
+  int rc = signal ? ct_p2p_alloc_signal(&p) : ct_p2p_alloc(&p, (size_t)bytes);
+  TORCH_CHECK(rc == 0 && p, "p2p_alloc failed: ", rc);
+  return reinterpret_cast<int64_t>(p);
+}
+
+void p2p_free(int64_t ptr) { TORCH_CHECK(ct_p2p_free(reinterpret_cast<void*>(ptr)) == 0, "p2p_free failed"); }
+
+pybind11::bytes ipc_get(int64_t ptr) {
+  std::string h(ct_ipc_handle_size(), '\0');
+  TORCH_CHECK(ct_ipc_get(reinterpret_cast<void*>(ptr), &h[0]) == 0, "hipIpcGetMemHandle failed");
+  return pybind11::bytes(h);
+}
+
+int64_t ipc_open(const std::string& h) {
+  TORCH_CHECK((int)h.size() == ct_ipc_handle_size(), "ipc_open: bad handle size");
+  void* p = nullptr;
+  TORCH_CHECK(ct_ipc_open(h.data(), &p) == 0 && p, "hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void ipc_close(int64_t ptr) { TORCH_CHECK(ct_ipc_close(reinterpret_cast<void*>(ptr)) == 0, "ipc_close failed"); }
+
+// staging [rank] must hold at least out.numel() elements of out's dtype (checked by the caller
+// against the registered capacity `cap_bytes`)
+void p2p_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, at::Tensor out,
+                   int64_t cap_bytes, int64_t rank, int64_t world, int64_t epoch, int64_t max_spin, int64_t blocks) {
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "p2p_allreduce: out must be a contiguous GPU tensor");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "p2p_allreduce: fp32 / bf16");
+  TORCH_CHECK((int64_t)data.size() == world && (int64_t)sig.size() == world, "p2p_allreduce: one buffer per rank");
+  TORCH_CHECK(out.numel() * (int64_t)out.element_size() <= cap_bytes, "p2p_allreduce: bucket exceeds staging");
+  std::vector<const void*> d(world);
+  std::vector<uint32_t*> s(world);
+  for (int64_t r = 0; r < world; ++r) {
+    d[r] = reinterpret_cast<const void*>(data[r]);
+    s[r] = reinterpret_cast<uint32_t*>(sig[r]);
+  }
+  int rc = ct_p2p_allreduce(d.data(), s.data(), out.data_ptr(), (long)out.numel(),
+                            out.scalar_type() == at::kFloat ? 0 : 1, (int)rank, (int)world, (uint32_t)epoch,
+                            (uint32_t)max_spin, (int)blocks, at::hip::getCurrentHIPStream().stream());
+  TORCH_CHECK(rc == 0, "ct_p2p_allreduce failed: ", rc);
+}
+
+// the error word the kernel sets when a barrier times out (synchronous read)
+int64_t p2p_error(int64_t sig) {
+  uint32_t v = 0;
+  const size_t off = ct_p2p_signal_bytes() / sizeof(uint32_t) - 64;
+  TORCH_CHECK(hipMemcpy(&v, reinterpret_cast<uint32_t*>(sig) + off, 4, hipMemcpyDeviceToHost) == hipSuccess,
+              "p2p_error: read failed");
+  return v;
+}
+
+}  // namespace
+
+void register_p2p(pybind11::module& m) {
+  m.def("p2p_alloc", &p2p_alloc);
+  m.def("p2p_free", &p2p_free);
+  m.def("ipc_get", &ipc_get);
+  m.def("ipc_open", &ipc_open);
+  m.def("ipc_close", &ipc_close);
+  m.def("p2p_allreduce", &p2p_allreduce);
+  m.def("p2p_error", &p2p_error);
+}

@@ -41,6 +41,11 @@ class GradBucketer:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
         self.comm_dtype = comm_dtype
+        # small buckets over the one-shot P2P kernel instead of RCCL (opt-in, parallel/p2p.py)
+        self.p2p = None
+        if self.world > 1 and space.grad.is_cuda:
+            from cloudtik_amd.parallel.p2p import from_env
+            self.p2p = from_env(group)
         esize = space.grad.element_size()
         cap = max(1, int(bucket_mb * 1024 * 1024 / esize))
         # buckets: param-aligned, contiguous ranges of the flat buffer
@@ -99,6 +104,12 @@ class GradBucketer:
     def _launch_on_current(self, b):
         lo, hi, _ = self.buckets[b]
         t = self.space.grad[lo:hi]
+        if self.p2p is not None:
+            buf = t if self.comm_dtype in (None, t.dtype) else t.to(self.comm_dtype)
+            if self.p2p.supports(buf):
+                self.p2p.all_reduce(buf)   # stream-ordered: no work handle to wait on
+                self._works.append((None, t if buf is not t else None, buf))
+                return
         if self.comm_dtype is not None and self.comm_dtype != t.dtype:
             buf = t.to(self.comm_dtype)
             w = dist.all_reduce(buf, group=self.group, async_op=True)
@@ -129,7 +140,8 @@ class GradBucketer:
             self._next += 1
         sync_grad_stream()
         for w, dst, buf in self._works:
-            w.wait()
+            if w is not None:
+                w.wait()
             if dst is not None:
                 buf.record_stream(torch.cuda.current_stream()) if buf.is_cuda else None
                 dst.copy_(buf)
