@@ -47,12 +47,13 @@ int64_t ipc_open(const std::string& h) {
 
 void ipc_close(int64_t ptr) { TORCH_CHECK(ct_ipc_close(reinterpret_cast<void*>(ptr)) == 0, "ipc_close failed"); }
 
-// staging [rank] must hold at least out.numel() elements of out's dtype (checked by the caller
-// against the registered capacity `cap_bytes`)
+// In place on `out`: copies it into this rank's staging buffer data[rank] (capacity
+// `cap_bytes`), then one kernel sums every rank's staging buffer into `out`.
 void p2p_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>& sig, at::Tensor out,
                    int64_t cap_bytes, int64_t rank, int64_t world, int64_t epoch, int64_t max_spin, int64_t blocks) {
   TORCH_CHECK(out.is_cuda() && out.is_contiguous(), "p2p_allreduce: out must be a contiguous GPU tensor");
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "p2p_allreduce: fp32 / bf16");
+  TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "p2p_allreduce: bad rank / world");
   TORCH_CHECK((int64_t)data.size() == world && (int64_t)sig.size() == world, "p2p_allreduce: one buffer per rank");
   TORCH_CHECK(out.numel() * (int64_t)out.element_size() <= cap_bytes, "p2p_allreduce: bucket exceeds staging");
   std::vector<const void*> d(world);
@@ -61,9 +62,13 @@ void p2p_allreduce(const std::vector<int64_t>& data, const std::vector<int64_t>&
     d[r] = reinterpret_cast<const void*>(data[r]);
     s[r] = reinterpret_cast<uint32_t*>(sig[r]);
   }
+  hipStream_t st = at::hip::getCurrentHIPStream().stream();
+  // stage this rank's input (stream ordered before the kernel's release fence)
+  TORCH_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(data[rank]), out.data_ptr(), out.numel() * out.element_size(),
+                             hipMemcpyDeviceToDevice, st) == hipSuccess, "p2p_allreduce: staging copy failed");
   int rc = ct_p2p_allreduce(d.data(), s.data(), out.data_ptr(), (long)out.numel(),
                             out.scalar_type() == at::kFloat ? 0 : 1, (int)rank, (int)world, (uint32_t)epoch,
-                            (uint32_t)max_spin, (int)blocks, at::hip::getCurrentHIPStream().stream());
+                            (uint32_t)max_spin, (int)blocks, st);
   TORCH_CHECK(rc == 0, "ct_p2p_allreduce failed: ", rc);
 }
 

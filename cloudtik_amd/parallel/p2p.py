@@ -9,7 +9,7 @@ peers' buffers at once: ``P2PAllReducer`` keeps one IPC-exported staging buffer 
 uncached signal buffer per rank, maps every peer's pair once (``hipIpcOpenMemHandle``,
 handles exchanged over the process group), and each ``all_reduce`` is
 
-    copy input -> own staging buffer;  one kernel (ops/csrc/p2p.hip): barrier-in on the
+    copy input -> own staging buffer (hipMemcpyAsync);  one kernel (ops/csrc/p2p.hip): barrier-in on the
     signal buffers, sum all ranks' staging buffers in fixed rank order (fp32 accumulate,
     bit-identical on every rank), write the output, barrier-out.
 
@@ -65,16 +65,11 @@ class P2PAllReducer:
         return (t.is_cuda and t.is_contiguous() and t.dtype in (torch.float32, torch.bfloat16)
                 and t.numel() * t.element_size() <= self.max_bytes and t.data_ptr() % 16 == 0)
 
-    def _staging_view(self, t: torch.Tensor) -> torch.Tensor:
-        """Non-owning tensor over the local staging buffer (freed in close())."""
-        return _from_ptr(self._staging, t.numel(), t.dtype, self.device)
-
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over the group (same contract as ``dist.all_reduce``)."""
         if not self.supports(t):
             dist.all_reduce(t, group=self.group)
             return t
-        self._staging_view(t).copy_(t.view(-1))
         self._epoch = (self._epoch + 1) & 0xFFFFFFFF or 1
         self._C.p2p_allreduce(self._data, self._sig, t, self.max_bytes, self.rank, self.world, self._epoch,
                               self.max_spin, self.blocks)
@@ -96,18 +91,6 @@ class P2PAllReducer:
         self._C.p2p_free(self._signal)
         self._staging = self._signal = None
         self._opened = []
-
-
-class _Cai:
-    def __init__(self, ptr: int, numel: int, typestr: str):
-        self.__cuda_array_interface__ = {"shape": (numel,), "typestr": typestr, "data": (ptr, False), "version": 2}
-
-
-def _from_ptr(ptr: int, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
-    """Non-owning tensor over raw device memory (``__cuda_array_interface__``; bf16 as int16)."""
-    if dtype is torch.bfloat16:
-        return torch.as_tensor(_Cai(ptr, numel, "<i2"), device=device).view(torch.bfloat16)
-    return torch.as_tensor(_Cai(ptr, numel, "<f4"), device=device)
 
 
 def from_env(group=None) -> Optional[P2PAllReducer]:

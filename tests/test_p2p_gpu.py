@@ -44,14 +44,22 @@ def _worker(rank, world, port, q):
                 torch.cuda.synchronize()
                 stage(f"{dtype} n={n} ok")
                 ref = full.float().sum(0)
-                out[(str(dtype), n)] = (t.float().cpu(), ref)
+                out[(str(dtype), n)] = (t.float().cpu().numpy(), ref.numpy())
         # many back-to-back calls reuse the staging buffers (barrier-out ordering)
         x = torch.full((4096,), float(rank + 1), device="cuda")
         for _ in range(50):
             ar.all_reduce(x)
         torch.cuda.synchronize()
+        import time
+        y = torch.ones(2048, device="cuda")
+        t0 = time.perf_counter()
+        for _ in range(200):
+            ar.all_reduce(y)
+            y.fill_(1.0)
+        torch.cuda.synchronize()
+        stage(f"latency 8 KiB fp32: {(time.perf_counter() - t0) / 200 * 1e6:.1f} us/call (two ranks sharing one GPU)")
         ar.check()
-        out["chain"] = (x[:4].cpu(), None)
+        out["chain"] = (x[:4].cpu().numpy(), None)
         ar.close()
         dist.destroy_process_group()
         q.put((rank, out, None))
@@ -82,12 +90,13 @@ def test_p2p_oneshot_allreduce_two_ranks_one_gpu():
         p.join(timeout=60)
         assert p.exitcode == 0
     for key, (got, ref) in res[0].items():
-        assert torch.equal(got, res[1][key][0]), key  # identical on every rank
+        got = torch.from_numpy(got)
+        assert torch.equal(got, torch.from_numpy(res[1][key][0])), key  # identical on every rank
         if ref is not None:
             tol = 1e-5 if "float32" in key[0] else 2e-2
-            torch.testing.assert_close(got, ref.to(got.dtype).float(), rtol=tol, atol=tol)
+            torch.testing.assert_close(got, torch.from_numpy(ref), rtol=tol, atol=tol)
     # 50 sums of [1, 2] -> first call 3, then doubling every call
-    assert torch.equal(res[0]["chain"][0], torch.full((4,), 3.0 * 2 ** 49))
+    assert torch.equal(torch.from_numpy(res[0]["chain"][0]), torch.full((4,), 3.0 * 2 ** 49))
 
 
 def test_p2p_from_env_disabled_without_gpu(monkeypatch):
