@@ -1,71 +1,129 @@
 #!/usr/bin/env python3
-"""Headline benchmark: BERT-large phase-1 pretraining throughput (tokens/s, whole job).
+"""Headline benchmark: BERT-large pretraining tokens/s + ResNet-50 training images/s, whole job.
 
 Metric / config from BASELINE.json ("samples/sec ResNet-50 + tokens/sec BERT-large, whole
-node, 1/2/4/8 MI355X").  Default run = BERT-large (24 x 1024, 16 heads, vocab 30522),
-seq 128, 76 masked-LM slots per sequence (max_predictions_per_seq of the reference's
-run_ddp_bert_pretrain_phase1.sh:72), per-GPU batch 256, LAMB (lr 3.5e-4, wd 0.01, betas 0.9/0.999 --
-the reference's run_ddp_bert_pretrain_phase1.sh:63 hyper-parameters), bf16 compute with
-fp32 master weights, dropout 0.1, random-init weights, synthetic token data.
-Data-parallel over RCCL with one process per GPU (weak scaling: fixed per-GPU batch).
-``--model resnet50`` measures the ResNet-50 half of the metric (images/s).
+node, 1/2/4/8 MI355X").  One invocation measures BOTH halves, one after the other in the
+same rank processes:
 
-Protocol: W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier +
-torch.cuda.synchronize() on both sides; the max time over ranks is reported.  Every timed
-step is a full forward + backward + gradient all-reduce + optimizer step + LR update.
+* BERT-large (24 x 1024, 16 heads, vocab 30522), seq 128, 76 masked-LM slots per sequence
+  (max_predictions_per_seq, reference run_ddp_bert_pretrain_phase1.sh:72), per-GPU batch 256,
+  LAMB (lr 3.5e-4, wd 0.01, betas 0.9/0.999: run_ddp_bert_pretrain_phase1.sh:63) with fp32
+  master weights, bf16 compute, dropout 0.1 -> ``value`` (tokens/s over all ranks);
+* ResNet-50 v1.5, 224x224, per-GPU batch 256, SGD momentum 0.9, wd 1e-4, bf16 NHWC
+  (reference protocol: examples/runtime/ai/basics/pytorch/
+  imagenet-resnet50-synthetic-pytorch-distributed.py:156-210) -> ``resnet50_images_per_sec``.
 
-    python bench.py --gpus N --steps K --warmup W
-    torchrun --nproc-per-node N bench.py --gpus N ...
+Random-init weights and synthetic data (one resident batch per rank, re-used every step).
+Data parallel over RCCL, one process per GPU, weak scaling (fixed per-GPU batch).
+
+Protocol per model: W untimed warm-up steps, then EXACTLY K timed steps bracketed by a
+barrier + torch.cuda.synchronize() on both sides; the max time over ranks is reported.  Each
+timed step is forward + backward + bucketed gradient all-reduce + optimizer step (+ LR
+schedule for BERT).
+
+Launch:
+    python bench.py --gpus N --steps K --warmup W          # spawns N rank processes itself
+    torchrun --nproc-per-node N bench.py --gpus N ...       # or ranks from the environment
+Options: ``--model bert-large|resnet50`` (one half only), ``--impl eager`` (stock PyTorch
+baseline: HF BertForPreTraining + SDPA + DDP + per-tensor LAMB / nn.Conv2d+BatchNorm2d
+ResNet-50 + DDP + torch SGD), ``--compare-eager`` (also run the eager baseline and report
+the ratio), ``--device cpu --model tiny`` (gloo plumbing check).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # no published reference number exists (BASELINE.json "published": {}); vs_baseline = null
 BASELINE = {"bert-large": None, "resnet50": None}
+TUNE_FILE = os.path.join(REPO, "cloudtik_amd", "ops", "tunableop", "gfx950_tunableop.csv")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="bert-large", choices=["bert-large", "bert-base", "resnet50"])
-    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default per model)")
+    ap.add_argument("--model", default="all", choices=["all", "bert-large", "bert-base", "resnet50", "tiny"])
+    ap.add_argument("--impl", default="native", choices=["native", "eager"])
+    ap.add_argument("--compare-eager", action="store_true",
+                    help="also run the stock-PyTorch baseline of the same config and report the ratio")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--batch", type=int, default=0, help="BERT per-GPU batch (default 256)")
+    ap.add_argument("--rn-batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--max-pred", type=int, default=76,
                     help="masked-LM slots per sequence (reference phase-1: max_predictions_per_seq=76)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="gradient buffer / all-reduce dtype of the native path")
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--conv-benchmark", action="store_true",
                     help="ResNet: let MIOpen search convolution solvers (torch.backends.cudnn.benchmark)")
-    ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--tunableop", default="use", choices=["off", "use", "tune"],
                     help="hipBLASLt solution selection via PyTorch TunableOp (results shipped in-tree)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-TUNE_FILE = os.path.join(REPO, "cloudtik_amd", "ops", "tunableop", "gfx950_tunableop.csv")
+# ------------------------------------------------------------------ rank launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
+def spawn_ranks(n: int) -> int:
+    """Start n rank processes of this script (one per GPU) and wait for them.
+
+    Runs before anything touches the GPU in this (parent) process.  If any rank fails, the
+    others are terminated (no rank is left blocked in a collective until the RCCL timeout).
+    Returns the first non-zero exit code, else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CLOUDTIK_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 30
+                for q in live:
+                    try:
+                        q.wait(max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+        time.sleep(0.2)
+    return rc if rc >= 0 else 128 - rc
+
+
+# ------------------------------------------------------------------ TunableOp
 def setup_tunableop(mode, rank):
     """Library GEMMs: let TunableOp pick the fastest hipBLASLt solution per shape.  The tuned
     table (gfx950) is committed in-tree; `--tunableop tune` regenerates it."""
-    if mode == "off":
+    import torch
+    if mode == "off" or not torch.cuda.is_available():
         return
     import torch.cuda.tunable as tn
     if mode == "use" and not os.path.exists(TUNE_FILE):
         return
-    os.makedirs(os.path.dirname(TUNE_FILE), exist_ok=True)
     tn.enable(True)
     tn.set_filename(TUNE_FILE if rank == 0 or mode == "use" else TUNE_FILE + f".rank{rank}")
     tn.tuning_enable(mode == "tune")
@@ -74,12 +132,9 @@ def setup_tunableop(mode, rank):
         tn.set_max_tuning_iterations(30)
 
 
-def finish_tunableop(mode, rank):
-    # TunableOp writes the results file itself when the process exits
-    return None
-
-
-def bench_bert(args, rank, world, device):
+# ------------------------------------------------------------------ native builders
+def build_bert(args, rank, world, device, kind):
+    import torch
     from cloudtik_amd.models.bert import BertConfig, BertForPreTraining, synthetic_pretraining_batch
     from cloudtik_amd.parallel import GradBucketer, broadcast_flat_params
     from cloudtik_amd.train.optim import FusedLAMB, FlatParamSpace
@@ -88,13 +143,15 @@ def bench_bert(args, rank, world, device):
 
     ops.manual_seed(1234 + rank)
     torch.manual_seed(1234)
-    cfg = BertConfig.large() if args.model == "bert-large" else BertConfig.base()
+    cfg = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "tiny": BertConfig.tiny}[kind]()
     if args.no_dropout:
         cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = 0.0
-    model = BertForPreTraining(cfg, device=device, dtype=torch.bfloat16)
+    dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    model = BertForPreTraining(cfg, device=device, dtype=dtype)
     model.train()
-    named = [(n, p) for n, p in model.named_parameters()]
-    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    named = list(model.named_parameters())
+    gd = torch.float32 if args.grad_dtype == "fp32" else None
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named], grad_dtype=gd)
     opt = FusedLAMB(space, lr=3.5e-4, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01,
                     no_decay=BertForPreTraining.no_decay)
     sched = LinearWarmupPolyDecayScheduler(opt, start_warmup_steps=0, warmup_steps=0,
@@ -102,9 +159,11 @@ def bench_bert(args, rank, world, device):
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=args.bucket_mb)
     opt.grad_scale = ddp.grad_scale
-    B = args.batch or 256
+    B = args.batch or (256 if kind != "tiny" else 4)
+    S = args.seq if kind != "tiny" else 32
+    P = args.max_pred if kind != "tiny" else 5
     gen = torch.Generator().manual_seed(42 + rank)
-    batch = synthetic_pretraining_batch(cfg, B, args.seq, args.max_pred, device=device, generator=gen)
+    batch = synthetic_pretraining_batch(cfg, B, S, P, device=device, generator=gen)
 
     def step():
         loss = model(**batch)
@@ -115,94 +174,261 @@ def bench_bert(args, rank, world, device):
         opt.zero_grad()
         return loss
 
-    info = dict(model="bert-large" if args.model == "bert-large" else "bert-base", per_gpu_batch=B,
-                seq_len=args.seq, unit="tokens/s", items_per_step=B * args.seq,
-                metric="bert_large_pretrain_tokens_per_sec" if args.model == "bert-large"
-                else "bert_base_pretrain_tokens_per_sec")
-    return step, info
+    def close():
+        ddp.remove()
+
+    info = dict(model=kind if kind != "tiny" else "bert-tiny", per_gpu_batch=B, seq_len=S, max_pred=P,
+                unit="tokens/s", items_per_step=B * S,
+                metric="bert_large_pretrain_tokens_per_sec" if kind in ("bert-large", "tiny")
+                else "bert_base_pretrain_tokens_per_sec",
+                optimizer="fused LAMB (HIP)", impl="native")
+    return step, close, info
 
 
-def bench_resnet(args, rank, world, device):
-    from cloudtik_amd.models.resnet import resnet50, ResNetTrainStep
+def build_resnet(args, rank, world, device, kind):
+    import torch
+    from cloudtik_amd.models.resnet import resnet50, resnet18_like_small, ResNetTrainStep
     from cloudtik_amd.parallel import GradBucketer, broadcast_flat_params
     from cloudtik_amd.train.optim import FusedSGD, FlatParamSpace
 
     torch.manual_seed(1234)
     if args.conv_benchmark:
         torch.backends.cudnn.benchmark = True
-    model = resnet50(device=device)
+    tiny = kind == "tiny"
+    model = resnet18_like_small(device=device) if tiny else resnet50(device=device)
     model.train()
-    named = [(n, p) for n, p in model.named_parameters()]
-    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    named = list(model.named_parameters())
+    gd = torch.float32 if args.grad_dtype == "fp32" else None
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named], grad_dtype=gd)
     opt = FusedSGD(space, lr=0.1, momentum=0.9, weight_decay=1e-4,
                    no_decay=lambda n: n.endswith("bias") or ".bn" in n or n.startswith("bn"))
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=args.bucket_mb)
     opt.grad_scale = ddp.grad_scale
-    B = args.batch or 256
+    B = args.rn_batch or (256 if not tiny else 4)
+    R = 224 if not tiny else 32
     g = torch.Generator().manual_seed(7 + rank)
-    x = torch.randn(B, 3, 224, 224, generator=g).to(device=device, dtype=torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (B,), generator=g).to(device)
+    x = torch.randn(B, 3, R, R, generator=g).to(device=device, dtype=next(model.parameters()).dtype)
+    if device.type == "cuda":
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10 if tiny else 1000, (B,), generator=g).to(device)
     ts = ResNetTrainStep(model, opt, ddp)
 
+    info = dict(model="resnet50" if not tiny else "resnet-tiny", per_gpu_batch=B, seq_len=None,
+                unit="images/s", items_per_step=B, metric="resnet50_train_images_per_sec",
+                optimizer="fused SGD (HIP)", impl="native", image_size=R)
+    return (lambda: ts(x, y)), ddp.remove, info
+
+
+# ------------------------------------------------------------------ eager (stock PyTorch) builders
+def _ddp(model, device, world):
+    import torch
+    if world <= 1:
+        return model
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    return DDP(model, device_ids=[device.index] if device.type == "cuda" else None)
+
+
+def build_bert_eager(args, rank, world, device, kind):
+    import torch
+    from cloudtik_amd.benchmarks.eager import (ReferenceLAMB, build_hf_bert, dense_mlm_labels, hf_bert_config,
+                                               lamb_param_groups)
+    from cloudtik_amd.models.bert import BertConfig, synthetic_pretraining_batch
+    tiny = kind == "tiny"
+    extra = dict(vocab_size=512, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                 intermediate_size=512, max_position_embeddings=128) if tiny else {}
+    if args.no_dropout:
+        extra.update(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    hcfg = hf_bert_config(large=kind != "bert-base", **extra)
+    model = build_hf_bert(hcfg, device)
+    model.train()
+    opt = ReferenceLAMB(lamb_param_groups(model, 0.01), lr=3.5e-4, betas=(0.9, 0.999), eps=1e-6)
+    dm = _ddp(model, device, world)
+    B = args.batch or (256 if not tiny else 4)
+    S = args.seq if not tiny else 32
+    P = args.max_pred if not tiny else 5
+    ours = BertConfig(vocab_size=hcfg.vocab_size)
+    gen = torch.Generator().manual_seed(42 + rank)
+    b = synthetic_pretraining_batch(ours, B, S, P, device=device, generator=gen)
+    labels = dense_mlm_labels(b, S)
+    amp = device.type == "cuda"
+
     def step():
-        return ts(x, y)
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
+            out = dm(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"],
+                     attention_mask=b["attention_mask"], labels=labels, next_sentence_label=b["next_sentence_labels"])
+        out.loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return out.loss
 
-    info = dict(model="resnet50", per_gpu_batch=B, seq_len=None, unit="images/s", items_per_step=B,
-                metric="resnet50_train_images_per_sec")
-    return step, info
+    info = dict(model=kind if not tiny else "bert-tiny", per_gpu_batch=B, seq_len=S, max_pred=P, unit="tokens/s",
+                items_per_step=B * S, metric="bert_large_pretrain_tokens_per_sec",
+                optimizer="per-tensor LAMB (stock PyTorch)", impl="eager")
+    return step, (lambda: None), info
 
 
-def main():
-    args = parse()
-    from cloudtik_amd.parallel import init_distributed, barrier, all_reduce_max
-    rank, world, local, device = init_distributed()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.backends.cuda.matmul.allow_tf32 = False
-    setup_tunableop(args.tunableop, rank)
-    fn = bench_bert if args.model.startswith("bert") else bench_resnet
-    step, info = fn(args, rank, world, device)
+def build_resnet_eager(args, rank, world, device, kind):
+    import torch
+    import torch.nn.functional as F
+    from cloudtik_amd.benchmarks.eager import StockResNet50
+    tiny = kind == "tiny"
+    torch.manual_seed(1234)
+    if args.conv_benchmark:
+        torch.backends.cudnn.benchmark = True
+    model = StockResNet50(num_classes=10 if tiny else 1000).to(device)
+    if device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, foreach=True)
+    dm = _ddp(model, device, world)
+    B = args.rn_batch or (256 if not tiny else 4)
+    R = 224 if not tiny else 32
+    g = torch.Generator().manual_seed(7 + rank)
+    x = torch.randn(B, 3, R, R, generator=g).to(device)
+    if device.type == "cuda":
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10 if tiny else 1000, (B,), generator=g).to(device)
+    amp = device.type == "cuda"
+
+    def step():
+        with torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp):
+            loss = F.cross_entropy(dm(x).float(), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    info = dict(model="resnet50" if not tiny else "resnet-tiny", per_gpu_batch=B, seq_len=None, unit="images/s",
+                items_per_step=B, metric="resnet50_train_images_per_sec", optimizer="torch.optim.SGD (foreach)",
+                impl="eager", image_size=R)
+    return step, (lambda: None), info
+
+
+# ------------------------------------------------------------------ timing
+def timed(step, args, rank, world, device):
+    """W warm-up steps, then K timed steps between barrier+sync brackets.  Returns
+    (max elapsed over ranks, per-rank elapsed list, last loss)."""
+    import torch
+    import torch.distributed as dist
+    from cloudtik_amd.parallel import barrier
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
 
     tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if rank == 0:
         print(f"[bench] warm-up {args.warmup} step(s): {time.perf_counter() - tw:.1f}s", file=sys.stderr)
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
+    loss = None
     for _ in range(args.steps):
         loss = step()
     barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    elapsed = all_reduce_max(t1 - t0)
-    ms = elapsed / args.steps * 1000.0
-    total_items = info["items_per_step"] * world * args.steps
-    value = total_items / elapsed
-    lossv = float(loss.detach().float().item())
+    sync()
+    el = time.perf_counter() - t0
+    per_rank = [el]
+    if dist.is_initialized():
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        per_rank = [float(o.item()) for o in out]
+    return max(per_rank), per_rank, float(loss.detach().float().item())
+
+
+def run_one(build, args, rank, world, device, kind):
+    import gc
+    import torch
+    step, close, info = build(args, rank, world, device, kind)
+    elapsed, per_rank, loss = timed(step, args, rank, world, device)
+    close()
+    del step
+    gc.collect()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    info.update(elapsed=elapsed, ms=elapsed / args.steps * 1e3,
+                per_rank_ms=[round(e / args.steps * 1e3, 3) for e in per_rank],
+                value=info["items_per_step"] * world * args.steps / elapsed, loss=loss)
+    return info
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
+    import torch
+    import torch.distributed as dist
+    from cloudtik_amd.parallel import init_distributed
+    backend = "gloo" if args.device == "cpu" else None
+    rank, world, local, device = init_distributed(backend=backend)
+    if args.device == "cpu":
+        device = torch.device("cpu")
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    if args.impl == "native" or args.compare_eager:
+        setup_tunableop(args.tunableop, rank)
+
+    if args.model == "all":
+        kinds = [("bert", "bert-large"), ("resnet", "resnet50")]
+    elif args.model == "tiny":
+        kinds = [("bert", "tiny"), ("resnet", "tiny")]
+    elif args.model == "resnet50":
+        kinds = [("resnet", "resnet50")]
+    else:
+        kinds = [("bert", args.model)]
+    builders = {("bert", "native"): build_bert, ("resnet", "native"): build_resnet,
+                ("bert", "eager"): build_bert_eager, ("resnet", "eager"): build_resnet_eager}
+    results = []
+    for fam, kind in kinds:
+        r = run_one(builders[(fam, args.impl)], args, rank, world, device, kind)
+        if args.compare_eager and args.impl == "native":
+            e = run_one(builders[(fam, "eager")], args, rank, world, device, kind)
+            r["eager_value"], r["eager_ms"] = e["value"], e["ms"]
+        results.append(r)
+
     if rank == 0:
-        base = BASELINE.get(info["model"])
-        cfg = {"model": info["model"], "global_batch": info["per_gpu_batch"] * world,
-               "per_gpu_batch": info["per_gpu_batch"], "parallelism": f"dp{world}",
-               "optimizer": "fused LAMB (HIP)" if info["model"].startswith("bert") else "fused SGD (HIP)",
-               "loss_last_step": round(lossv, 4)}
-        if info["seq_len"]:
-            cfg["seq_len"] = info["seq_len"]
-            cfg["max_pred"] = args.max_pred
-            cfg["sentences_per_sec"] = round(value / info["seq_len"], 2)
-        out = {"metric": info["metric"], "value": round(value, 2), "unit": info["unit"],
+        head = results[0]
+        base = BASELINE.get(head["model"])
+        cfg = {"model": head["model"], "global_batch": head["per_gpu_batch"] * world,
+               "per_gpu_batch": head["per_gpu_batch"], "parallelism": f"dp{world}",
+               "optimizer": head["optimizer"], "impl": head["impl"], "loss_last_step": round(head["loss"], 4),
+               "grad_dtype": args.grad_dtype if head["impl"] == "native" else "fp32 (autocast)"}
+        if head["seq_len"]:
+            cfg.update(seq_len=head["seq_len"], max_pred=head["max_pred"],
+                       sentences_per_sec=round(head["value"] / head["seq_len"], 2))
+        out = {"metric": head["metric"], "value": round(head["value"], 2), "unit": head["unit"],
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": (round(value / base, 4) if base else None), "dtype": "bf16",
-               "data": "synthetic (random tokens/images, random-init weights)", "config": cfg}
+               "ms_per_step": round(head["ms"], 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": (round(head["value"] / base, 4) if base else None),
+               "dtype": "bf16" if device.type == "cuda" else "fp32",
+               "data": "synthetic (one resident random batch per rank, re-used every step; random-init weights)",
+               "config": cfg,
+               "world_size_seen_by_rccl": dist.get_world_size() if dist.is_initialized() else 1,
+               "backend": dist.get_backend() if dist.is_initialized() else None,
+               "per_rank_ms_per_step": head["per_rank_ms"]}
+        if "eager_value" in head:
+            out["eager_value"] = round(head["eager_value"], 2)
+            out["speedup_vs_eager"] = round(head["value"] / head["eager_value"], 3)
+        for r in results[1:]:
+            key = "resnet50" if r["model"].startswith("resnet") else r["model"].replace("-", "_")
+            out[f"{key}_images_per_sec" if r["unit"] == "images/s" else f"{key}_value"] = round(r["value"], 2)
+            out[f"{key}_ms_per_step"] = round(r["ms"], 3)
+            out[f"{key}_per_gpu_batch"] = r["per_gpu_batch"]
+            out[f"{key}_per_rank_ms_per_step"] = r["per_rank_ms"]
+            out[f"{key}_loss_last_step"] = round(r["loss"], 4)
+            if "eager_value" in r:
+                out[f"{key}_eager_value"] = round(r["eager_value"], 2)
+                out[f"{key}_speedup_vs_eager"] = round(r["value"] / r["eager_value"], 3)
         print(json.dumps(out), flush=True)
-    finish_tunableop(args.tunableop, rank)
-    if torch.distributed.is_initialized():
-        torch.distributed.destroy_process_group()
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -17,9 +17,11 @@
 //      staging buffer for the next call while a peer still reads it.
 //
 // Latency is one kernel: no ring steps, each byte crosses xGMI once per peer on the
-// direct link.  The spin loops are bounded (`max_spin` polls with s_sleep); a timed-out
-// wait sets the error word of the rank's own signal buffer and the kernel exits, so a
-// missing peer surfaces as an error on the host, never as a hung GPU.
+// direct link.  The spin loops are bounded in WALL-CLOCK time (the constant-rate device
+// clock, `timeout_ticks`; the host sizes it like an RCCL timeout, minutes by default): a
+// timed-out wait sets an error word in pinned, host-mapped memory and the kernel exits, so
+// a missing peer surfaces on the host (the bucketer reads the word every step without a
+// device sync and raises) and never as a hung GPU.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
@@ -42,7 +44,8 @@ struct P2PArgs {
   long n;                       // elements
   int rank, world;
   uint32_t epoch;
-  uint32_t max_spin;
+  uint64_t timeout_ticks;       // wall_clock64() ticks
+  uint32_t* err;                // host-mapped error word (fine-grained pinned memory)
 };
 
 __device__ inline bool barrier(const P2PArgs& a, int bank, uint32_t value) {
@@ -59,11 +62,11 @@ __device__ inline bool barrier(const P2PArgs& a, int bank, uint32_t value) {
   __syncthreads();
   if (threadIdx.x < a.world) {
     const uint32_t* mine = a.sig[a.rank] + (bank * kMaxBlocks + b) * kMaxRanks + threadIdx.x;
-    uint32_t spins = 0;
+    const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
-      if (++spins > a.max_spin) {
+      if (wall_clock64() - t0 > a.timeout_ticks) {
         ok = 0;
-        __hip_atomic_store(a.sig[a.rank] + kSigSlots, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.err, 1u + (uint32_t)bank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -151,6 +154,23 @@ int ct_p2p_alloc_signal(void** ptr) {
 
 int ct_p2p_alloc(void** ptr, size_t bytes) { return hipMalloc(ptr, bytes) == hipSuccess ? 0 : 1; }
 
+// pinned, host-mapped, coherent word pair: the kernel stores, the host reads without a sync
+int ct_p2p_alloc_flag(void** host, void** dev) {
+  if (hipHostMalloc(host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return 1;
+  ::memset(*host, 0, 64);
+  return hipHostGetDevicePointer(dev, *host, 0) == hipSuccess ? 0 : 2;
+}
+
+int ct_p2p_free_flag(void* host) { return hipHostFree(host) == hipSuccess ? 0 : 1; }
+
+// device wall-clock ticks per second (for the barrier timeout)
+long ct_p2p_clock_hz() {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return 0;
+  return (long)khz * 1000L;
+}
+
 int ct_p2p_free(void* ptr) { return hipFree(ptr) == hipSuccess ? 0 : 1; }
 
 int ct_ipc_get(void* ptr, char* out /* HIP_IPC_HANDLE_SIZE bytes */) {
@@ -172,9 +192,10 @@ int ct_ipc_close(void* ptr) { return hipIpcCloseMemHandle(ptr) == hipSuccess ? 0
 
 // dtype: 0 = fp32, 1 = bf16.  Staging buffers must be 16-byte aligned and hold n elements.
 int ct_p2p_allreduce(const void* const* data, uint32_t* const* sig, void* out, long n, int dtype, int rank, int world,
-                     uint32_t epoch, uint32_t max_spin, int blocks, hipStream_t stream) {
+                     uint32_t epoch, uint64_t timeout_ticks, uint32_t* err, int blocks, hipStream_t stream) {
   if (world < 1 || world > ct::kMaxRanks || rank < 0 || rank >= world || n < 0) return 1;
   if (blocks < 1 || blocks > ct::kMaxBlocks) return 2;
+  if (!err) return 6;
   ct::P2PArgs a{};
   for (int r = 0; r < world; ++r) {
     if (!data[r] || !sig[r] || (reinterpret_cast<uintptr_t>(data[r]) & 15)) return 3;
@@ -187,7 +208,8 @@ int ct_p2p_allreduce(const void* const* data, uint32_t* const* sig, void* out, l
   a.rank = rank;
   a.world = world;
   a.epoch = epoch;
-  a.max_spin = max_spin;
+  a.timeout_ticks = timeout_ticks;
+  a.err = err;
   if (dtype == 0)
     hipLaunchKernelGGL(ct::oneshot_allreduce_kernel<float>, dim3(blocks), dim3(ct::kThreads), 0, stream, a);
   else if (dtype == 1)

@@ -46,6 +46,7 @@ class GradBucketer:
         if self.world > 1 and space.grad.is_cuda:
             from cloudtik_amd.parallel.p2p import from_env
             self.p2p = from_env(group)
+            self._comm_stream = torch.cuda.Stream() if self.p2p is not None else None
         esize = space.grad.element_size()
         cap = max(1, int(bucket_mb * 1024 * 1024 / esize))
         # buckets: param-aligned, contiguous ranges of the flat buffer
@@ -91,6 +92,17 @@ class GradBucketer:
     def _launch(self, b):
         from cloudtik_amd.ops.linear import grad_stream
         side = grad_stream()
+        if self.p2p is not None and self._p2p_fits(b):
+            # the one-shot kernel spins until the slowest rank reaches this bucket: give it
+            # its own stream so weight-gradient GEMMs queued on the side stream (and the
+            # main-stream dgrad chain) never wait behind that spin
+            comm = self._comm_stream
+            comm.wait_stream(torch.cuda.current_stream())
+            if side is not None:
+                comm.wait_stream(side)
+            with torch.cuda.stream(comm):
+                self._launch_on_current(b)
+            return
         if side is not None:
             # weight grads of this bucket were written on the side stream, bias / LayerNorm
             # grads on the main one: issue the collective from the side stream after it has
@@ -104,18 +116,23 @@ class GradBucketer:
     def _launch_on_current(self, b):
         lo, hi, _ = self.buckets[b]
         t = self.space.grad[lo:hi]
-        if self.p2p is not None:
+        if self.p2p is not None and self._p2p_fits(b):
             buf = t if self.comm_dtype in (None, t.dtype) else t.to(self.comm_dtype)
-            if self.p2p.supports(buf):
-                self.p2p.all_reduce(buf)   # stream-ordered: no work handle to wait on
-                self._works.append((None, t if buf is not t else None, buf))
-                return
+            self.p2p.all_reduce(buf)   # stream-ordered on the comm stream: no work handle
+            self._works.append((None, t if buf is not t else None, buf))
+            return
         if self.comm_dtype is not None and self.comm_dtype != t.dtype:
             buf = t.to(self.comm_dtype)
             w = dist.all_reduce(buf, group=self.group, async_op=True)
             self._works.append((w, t, buf))
         else:
             self._works.append((dist.all_reduce(t, group=self.group, async_op=True), None, None))
+
+    def _p2p_fits(self, b) -> bool:
+        lo, hi, _ = self.buckets[b]
+        dt = self.comm_dtype or self.space.grad.dtype
+        return (hi - lo) * torch.empty((), dtype=dt).element_size() <= self.p2p.max_bytes \
+            and dt in (torch.float32, torch.bfloat16)
 
     # ------------------------------------------------------------------ API
     @contextlib.contextmanager
@@ -139,6 +156,11 @@ class GradBucketer:
             self._launch(self._next)
             self._next += 1
         sync_grad_stream()
+        if self.p2p is not None:
+            torch.cuda.current_stream().wait_stream(self._comm_stream)
+            # a barrier that timed out in an earlier (finished) kernel means some rank's
+            # gradients were never reduced: fatal, never a silent divergence of the ranks
+            self.p2p.check()
         for w, dst, buf in self._works:
             if w is not None:
                 w.wait()

@@ -14,13 +14,21 @@ handles exchanged over the process group), and each ``all_reduce`` is
     bit-identical on every rank), write the output, barrier-out.
 
 Buckets larger than ``max_bytes`` (and non-fp32/bf16 or misaligned tensors) go to RCCL
-through ``torch.distributed.all_reduce``.  Barrier waits are bounded in the kernel; a rank
-that never arrives raises ``RuntimeError`` on ``check()`` instead of hanging the GPU.
-Opt-in for the Trainer through ``CLOUDTIK_P2P_ALLREDUCE_BYTES`` (see parallel/ddp.py).
+through ``torch.distributed.all_reduce``.  Barrier waits are bounded in WALL-CLOCK time
+(``timeout_s``, default ``CLOUDTIK_P2P_TIMEOUT_S`` or 300 s -- an RCCL-like timeout, so a
+slow peer doing a first-step solver search or a checkpoint is waited for); a timed-out wait
+sets a host-mapped error word that ``check()`` reads without a device sync.  The gradient
+bucketer calls ``check()`` every step and raises, so a missing peer is fatal for the job
+(restart from the last checkpoint) instead of silently diverging ranks.
+Opt-in for the Trainer through ``CLOUDTIK_P2P_ALLREDUCE_BYTES`` (see parallel/ddp.py); only
+enabled when every rank of the group runs on ONE host (xGMI domain), decided collectively.
+Verified so far with two ranks sharing one MI355X (tests/test_p2p_gpu.py); the cross-GPU
+xGMI path has not been measured yet.
 """
 from __future__ import annotations
 
 import os
+import socket
 from typing import List, Optional
 
 import torch
@@ -28,7 +36,7 @@ import torch.distributed as dist
 
 
 class P2PAllReducer:
-    def __init__(self, group=None, max_bytes: int = 4 << 20, blocks: int = 32, max_spin: int = 1 << 24,
+    def __init__(self, group=None, max_bytes: int = 4 << 20, blocks: int = 32, timeout_s: Optional[float] = None,
                  device: Optional[torch.device] = None):
         from cloudtik_amd import ops
         ops.require_native()
@@ -38,11 +46,13 @@ class P2PAllReducer:
         if self.world > 8:
             raise ValueError("the one-shot P2P all-reduce spans at most 8 ranks (one xGMI-connected node)")
         self.max_bytes = int(max_bytes)
-        self.blocks, self.max_spin = int(blocks), int(max_spin)
+        self.blocks = int(blocks)
+        self.timeout_s = float(timeout_s if timeout_s is not None else os.environ.get("CLOUDTIK_P2P_TIMEOUT_S", 300))
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         with torch.cuda.device(self.device):
             self._staging = self._C.p2p_alloc(self.max_bytes, False)
             self._signal = self._C.p2p_alloc(0, True)
+            self._err_host, self._err_dev = self._C.p2p_alloc_flag()
             mine = (self._C.ipc_get(self._staging), self._C.ipc_get(self._signal))
             handles: List = [None] * self.world
             dist.all_gather_object(handles, mine, group=group)
@@ -72,13 +82,21 @@ class P2PAllReducer:
             return t
         self._epoch = (self._epoch + 1) & 0xFFFFFFFF or 1
         self._C.p2p_allreduce(self._data, self._sig, t, self.max_bytes, self.rank, self.world, self._epoch,
-                              self.max_spin, self.blocks)
+                              self.timeout_s, self._err_dev, self.blocks)
         return t
 
+    def error(self) -> int:
+        """Non-zero once a barrier of an already-finished kernel timed out (1 = barrier-in: the
+        output is this rank's unreduced input; 2 = barrier-out).  No device sync."""
+        return int(self._C.p2p_error(self._err_host)) if self._staging is not None else 0
+
     def check(self):
-        """Synchronous: raise if any barrier of this rank timed out since construction."""
-        if self._C.p2p_error(self._signal):
-            raise RuntimeError(f"rank {self.rank}: P2P all-reduce barrier timed out (a peer did not arrive)")
+        """Raise if any barrier of this rank timed out (among kernels finished so far)."""
+        e = self.error()
+        if e:
+            raise RuntimeError(f"rank {self.rank}: P2P all-reduce {'barrier-in' if e == 1 else 'barrier-out'} "
+                               f"timed out after {self.timeout_s:.0f}s (a peer did not arrive); the reduced "
+                               f"gradients are invalid -- restart from the last checkpoint")
 
     def close(self):
         if self._staging is None:
@@ -89,13 +107,35 @@ class P2PAllReducer:
             self._C.ipc_close(p)
         self._C.p2p_free(self._staging)
         self._C.p2p_free(self._signal)
+        self._C.p2p_free_flag(self._err_host)
         self._staging = self._signal = None
         self._opened = []
 
 
 def from_env(group=None) -> Optional[P2PAllReducer]:
-    """``CLOUDTIK_P2P_ALLREDUCE_BYTES=<n>`` (> 0) enables the one-shot path for buckets up to n bytes."""
+    """``CLOUDTIK_P2P_ALLREDUCE_BYTES=<n>`` (> 0) enables the one-shot path for buckets up to n bytes.
+
+    The decision is COLLECTIVE: every rank contributes (hostname, n, GPU available) and the
+    path is enabled only if all ranks agree and share one host, so either every rank builds a
+    reducer (whose constructor is itself collective) or none does -- a 2-node job never gets
+    foreign IPC handles and never leaves ranks waiting in a barrier the others skipped."""
+    if not dist.is_initialized():
+        return None
     n = int(os.environ.get("CLOUDTIK_P2P_ALLREDUCE_BYTES", "0") or 0)
-    if n <= 0 or not torch.cuda.is_available() or not dist.is_initialized() or dist.get_world_size(group) > 8:
+    world = dist.get_world_size(group)
+    mine = (socket.gethostname(), n, bool(torch.cuda.is_available()))
+    votes: List = [None] * world
+    dist.all_gather_object(votes, mine, group=group)
+    if not decide(votes):
         return None
     return P2PAllReducer(group, max_bytes=n)
+
+
+def decide(votes) -> bool:
+    """Enable the one-shot path iff all ranks asked for the same n > 0, have a GPU, sit on
+    one host, and there are at most 8 of them (one xGMI-connected node)."""
+    if not votes or len(votes) > 8:
+        return False
+    hosts = {v[0] for v in votes}
+    sizes = {v[1] for v in votes}
+    return len(hosts) == 1 and len(sizes) == 1 and next(iter(sizes)) > 0 and all(v[2] for v in votes)

@@ -27,6 +27,7 @@ import torch
 
 SEG = 8192
 ALIGN = 64
+_DYN_SLOTS = 8
 
 
 def _sync_grads():
@@ -185,7 +186,15 @@ class _FlatOptimizer(torch.optim.Optimizer):
             [0.0 if (no_decay is not None and no_decay(n)) else gwd.get(id(p), defaults.get("weight_decay", 0.0))
              for n, p in zip(space.names, space.params)], dtype=torch.float32, device=space.device)
         self.dyn = torch.zeros(4, dtype=torch.float32, device=space.device)
-        self._dyn_host = torch.zeros(4, dtype=torch.float32, pin_memory=space.device.type == "cuda")
+        # per-step scalars (lr, grad scale, bias corrections) reach the device through a RING of
+        # pinned host slots: an async H2D copy reads host memory when it EXECUTES, so a single
+        # reused slot would let a CPU that runs ahead overwrite step k's values with step k+1's
+        # before the copy ran.  A slot is rewritten only after the event recorded behind its
+        # previous copy has completed (blocks only if the CPU is _DYN_SLOTS steps ahead).
+        pinned = space.device.type == "cuda"
+        self._dyn_ring = [torch.zeros(4, dtype=torch.float32, pin_memory=pinned) for _ in range(_DYN_SLOTS)]
+        self._dyn_events = [None] * _DYN_SLOTS
+        self._dyn_slot = 0
         self.grad_scale = 1.0
         self.step_count = 0
 
@@ -202,8 +211,18 @@ class _FlatOptimizer(torch.optim.Optimizer):
         t = self.step_count
         bc1 = 1.0 / (1.0 - b1 ** t) if b1 is not None else 1.0
         bc2 = 1.0 / (1.0 - b2 ** t) if b2 is not None else 1.0
-        self._dyn_host.copy_(torch.tensor([self._lr(), self.grad_scale, bc1, bc2]))
-        self.dyn.copy_(self._dyn_host, non_blocking=True)
+        i = self._dyn_slot = (self._dyn_slot + 1) % _DYN_SLOTS
+        host, ev = self._dyn_ring[i], self._dyn_events[i]
+        if ev is not None:
+            ev.synchronize()
+        host.copy_(torch.tensor([self._lr(), self.grad_scale, bc1, bc2], dtype=torch.float32))
+        if self.dyn.is_cuda:
+            self.dyn.copy_(host, non_blocking=True)
+            if ev is None:
+                ev = self._dyn_events[i] = torch.cuda.Event()
+            ev.record()
+        else:
+            self.dyn.copy_(host)
 
     def state_dict(self):
         sd = super().state_dict()

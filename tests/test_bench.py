@@ -1,0 +1,37 @@
+"""bench.py contract: `--gpus N` without a launcher spawns N ranks itself, both halves of the
+metric (BERT tokens/s + ResNet-50 images/s) land in ONE JSON line, and the world size seen
+by the process group is N."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu", "--model", "tiny",
+                          "--steps", "2", "--warmup", "1", *extra], capture_output=True, text=True, env=env,
+                         timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_two_ranks_and_reports_both_metrics():
+    r = _run("--gpus", "2")
+    assert r["n_gpus"] == 2 and r["world_size_seen_by_rccl"] == 2
+    assert r["metric"] == "bert_large_pretrain_tokens_per_sec" and r["value"] > 0
+    assert r["resnet50_images_per_sec"] > 0
+    assert len(r["per_rank_ms_per_step"]) == 2
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 8
+    assert r["steps"] == 2 and r["warmup"] == 1
+
+
+def test_bench_single_process_eager_impl():
+    r = _run("--gpus", "1", "--impl", "eager")
+    assert r["n_gpus"] == 1 and r["config"]["impl"] == "eager"
+    assert r["value"] > 0 and r["resnet50_images_per_sec"] > 0

@@ -290,3 +290,41 @@ def test_bert_layer_blocks_match_composed(cuda, p):
     assert _rel(y, y2) < 1e-2
     assert _rel(gx_blocks, x.grad) < 2e-2
     assert _rel(g_blocks, sp.grad.float()) < 2e-2
+
+
+@pytest.mark.parametrize("name", ["adamw", "lamb"])
+def test_optimizer_step_scalars_under_cpu_run_ahead(cuda, name):
+    """The CPU queues several optimizer steps behind a long GPU kernel without synchronising:
+    each step must still see ITS OWN lr / bias-correction factors (the per-step scalars are
+    staged through pinned host memory that an async copy reads only when it executes)."""
+    from cloudtik_amd.train.optim import FlatParamSpace, FusedAdam, FusedLAMB
+    torch.manual_seed(0)
+    w0 = torch.randn(4096, device=cuda)
+    p = torch.nn.Parameter(w0.clone())
+    sp = FlatParamSpace([p], names=["w"])
+    kw = dict(lr=1e-2, weight_decay=0.01, space=sp)
+    opt = FusedAdam(sp, **kw) if name == "adamw" else FusedLAMB(sp, bias_correction=True, **kw)
+    lrs = [1e-2, 3e-2, 5e-3, 2e-2]
+    grads = [torch.randn(4096, device=cuda) for _ in lrs]
+    torch.cuda.synchronize()
+    for lr, g in zip(lrs, grads):
+        torch.cuda._sleep(20_000_000)            # keep the GPU busy so the CPU runs ahead
+        for grp in opt.param_groups:
+            grp["lr"] = lr
+        sp.grad[:4096].copy_(g)
+        opt.step()
+    torch.cuda.synchronize()
+    # fp32 reference of the same update rule, step by step
+    w = w0.double().cpu()
+    m = torch.zeros_like(w)
+    v = torch.zeros_like(w)
+    b1, b2, eps = 0.9, 0.999, opt.eps
+    for t, (lr, g) in enumerate(zip(lrs, grads), 1):
+        g = g.double().cpu()
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        u = (m / (1 - b1 ** t)) / ((v / (1 - b2 ** t)).sqrt() + eps) + 0.01 * w
+        if name == "lamb":
+            u = u * (w.norm() / u.norm())
+        w = w - lr * u
+    assert _rel(p.detach().double().cpu(), w) < 1e-5

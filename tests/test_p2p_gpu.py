@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
         torch.cuda.set_device(0)
         from cloudtik_amd.parallel.p2p import P2PAllReducer
         stage("init")
-        ar = P2PAllReducer(max_bytes=1 << 20, blocks=8, max_spin=1 << 22)
+        ar = P2PAllReducer(max_bytes=1 << 20, blocks=8, timeout_s=60)
         stage("mapped peers")
         out = {}
         for dtype in (torch.float32, torch.bfloat16):
