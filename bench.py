@@ -64,7 +64,7 @@ def parse(argv=None):
                     help="masked-LM slots per sequence (reference phase-1: max_predictions_per_seq=76)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
-                    help="gradient buffer / all-reduce dtype of the native path")
+                    help="native path: fp32 = bf16 per-backward grads reduced / accumulated in fp32")
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--conv-benchmark", action="store_true",
                     help="ResNet: let MIOpen search convolution solvers (torch.backends.cudnn.benchmark)")
@@ -150,14 +150,14 @@ def build_bert(args, rank, world, device, kind):
     model = BertForPreTraining(cfg, device=device, dtype=dtype)
     model.train()
     named = list(model.named_parameters())
-    gd = torch.float32 if args.grad_dtype == "fp32" else None
-    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named], grad_dtype=gd)
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
     opt = FusedLAMB(space, lr=3.5e-4, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01,
                     no_decay=BertForPreTraining.no_decay)
     sched = LinearWarmupPolyDecayScheduler(opt, start_warmup_steps=0, warmup_steps=0,
                                            total_steps=13700, end_learning_rate=0.0, degree=1.0)
     broadcast_flat_params(space)
-    ddp = GradBucketer(space, bucket_mb=args.bucket_mb)
+    ddp = GradBucketer(space, bucket_mb=args.bucket_mb,
+                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None)
     opt.grad_scale = ddp.grad_scale
     B = args.batch or (256 if kind != "tiny" else 4)
     S = args.seq if kind != "tiny" else 32
@@ -198,12 +198,12 @@ def build_resnet(args, rank, world, device, kind):
     model = resnet18_like_small(device=device) if tiny else resnet50(device=device)
     model.train()
     named = list(model.named_parameters())
-    gd = torch.float32 if args.grad_dtype == "fp32" else None
-    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named], grad_dtype=gd)
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
     opt = FusedSGD(space, lr=0.1, momentum=0.9, weight_decay=1e-4,
                    no_decay=lambda n: n.endswith("bias") or ".bn" in n or n.startswith("bn"))
     broadcast_flat_params(space)
-    ddp = GradBucketer(space, bucket_mb=args.bucket_mb)
+    ddp = GradBucketer(space, bucket_mb=args.bucket_mb,
+                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None)
     opt.grad_scale = ddp.grad_scale
     B = args.rn_batch or (256 if not tiny else 4)
     R = 224 if not tiny else 32

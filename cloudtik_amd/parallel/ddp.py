@@ -21,8 +21,10 @@ Design (MI355X):
   so buckets must be large enough for RCCL's multi-channel rings to reach link rate while
   still leaving >=10 buckets of overlap for BERT-large (670 MB of bf16 grads); the
   reference's single 8 GiB bucket (no overlap at all) is available with bucket_mb=8192.
-* ``mode='reduce_scatter'`` pairs with a ZeRO-1 sharded optimizer (each rank steps 1/world
-  of the flat space, then parameters are all-gathered): same wire bytes as all-reduce.
+* ``reduce_dtype=torch.float32``: the bf16 per-backward gradients are added into an fp32
+  buffer (``space.main_grad``) bucket by bucket and the all-reduce sums fp32; micro-batches
+  under ``no_sync()`` are accumulated into the same fp32 buffer when the context exits, and
+  the optimizer reads the fp32 result (no bf16 rounding of partial sums anywhere).
 """
 from __future__ import annotations
 
@@ -35,10 +37,15 @@ import torch.distributed as dist
 
 class GradBucketer:
     def __init__(self, space, group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 comm_dtype: Optional[torch.dtype] = None):
+                 comm_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None):
         self.space = space
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.fp32 = reduce_dtype == torch.float32 and space.grad.dtype != torch.float32
+        if self.fp32:
+            if space.main_grad is None:
+                space.main_grad = torch.zeros(space.total, dtype=torch.float32, device=space.grad.device)
+            comm_dtype = None
         self.overlap = overlap and self.world > 1
         self.comm_dtype = comm_dtype
         # small buckets over the one-shot P2P kernel instead of RCCL (opt-in, parallel/p2p.py)
@@ -116,6 +123,15 @@ class GradBucketer:
     def _launch_on_current(self, b):
         lo, hi, _ = self.buckets[b]
         t = self.space.grad[lo:hi]
+        if self.fp32:
+            m = self.space.main_grad[lo:hi]
+            m.add_(t)                      # fp32 sum of earlier micro-batches + this backward
+            if self.p2p is not None and self._p2p_fits(b):
+                self.p2p.all_reduce(m)
+                self._works.append((None, None, None))
+            else:
+                self._works.append((dist.all_reduce(m, group=self.group, async_op=True), None, None))
+            return
         if self.p2p is not None and self._p2p_fits(b):
             buf = t if self.comm_dtype in (None, t.dtype) else t.to(self.comm_dtype)
             self.p2p.all_reduce(buf)   # stream-ordered on the comm stream: no work handle
@@ -130,7 +146,7 @@ class GradBucketer:
 
     def _p2p_fits(self, b) -> bool:
         lo, hi, _ = self.buckets[b]
-        dt = self.comm_dtype or self.space.grad.dtype
+        dt = torch.float32 if self.fp32 else (self.comm_dtype or self.space.grad.dtype)
         return (hi - lo) * torch.empty((), dtype=dt).element_size() <= self.p2p.max_bytes \
             and dt in (torch.float32, torch.bfloat16)
 
@@ -144,13 +160,26 @@ class GradBucketer:
             yield
         finally:
             self._enabled = prev
+        if self.fp32:
+            self.accumulate_local()
+
+    def accumulate_local(self):
+        """fp32 mode: move this backward's gradients into the fp32 buffer (no communication)."""
+        from cloudtik_amd.ops.linear import sync_grad_stream
+        if self.space.grad.is_cuda:
+            sync_grad_stream()
+        self.space.main_grad.add_(self.space.grad)
+        self.space.grad.zero_()
 
     def finish(self):
         """Launch any bucket not yet launched (unused params / no overlap), then make the
         compute stream wait for every reduction.  Call before optimizer.step()."""
         from cloudtik_amd.ops.linear import sync_grad_stream
         if self.world <= 1:
-            sync_grad_stream()
+            if self.space.grad.is_cuda:
+                sync_grad_stream()
+            if self.fp32:
+                self.space.main_grad.add_(self.space.grad)
             return
         while self._next < len(self.buckets):
             self._launch(self._next)

@@ -96,6 +96,9 @@ class FlatParamSpace:
                 p.data = _flat_view(self.model[o:o + n], p)
                 p.grad = _flat_view(self.grad[o:o + n], p)
                 p._ct_flat_grad = True   # ops.linear may accumulate dW straight into it
+        # fp32 gradient the optimizer reads instead of ``grad`` when a bucketer reduces /
+        # accumulates in fp32 (parallel.GradBucketer(reduce_dtype=torch.float32))
+        self.main_grad: Optional[torch.Tensor] = None
         # fp32 master copy of THIS rank's shard only
         self.master = self.model[self.shard_lo:self.shard_hi].float().clone() \
             if self.dtype != torch.float32 else None
@@ -136,11 +139,19 @@ class FlatParamSpace:
         return self.model[self.shard_lo:self.shard_hi]
 
     @property
+    def reduced_grad(self) -> torch.Tensor:
+        """The gradient the optimizer consumes: the fp32 reduction buffer if one is attached,
+        else the (model-dtype) gradient buffer itself."""
+        return self.main_grad if self.main_grad is not None else self.grad
+
+    @property
     def shard_grad(self) -> torch.Tensor:
-        return self.grad[self.shard_lo:self.shard_hi]
+        return self.reduced_grad[self.shard_lo:self.shard_hi]
 
     def zero_grad(self):
         self.grad.zero_()
+        if self.main_grad is not None:
+            self.main_grad.zero_()
 
     def tensor_wd(self, wd_fn: Callable[[str, torch.nn.Parameter], float]) -> torch.Tensor:
         return torch.tensor([float(wd_fn(n, p)) for n, p in zip(self.names, self.params)],

@@ -174,7 +174,7 @@ class Trainer:
         return {k: t[i].item() / n for i, k in enumerate(keys)}
 
     def _clip(self):
-        g = self.space.grad if self.space is not None else None
+        g = self.space.reduced_grad if self.space is not None else None
         if g is None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip_norm)
             return

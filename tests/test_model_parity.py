@@ -1,0 +1,149 @@
+"""Model / optimizer parity against the reference's own building blocks.
+
+* ``models.bert.BertForPreTraining`` vs Hugging Face ``transformers.BertForPreTraining`` --
+  the model the reference instantiates for BERT-large pretraining
+  (run_pretrain_mlperf.py:449-471) -- with weights mapped one to one: loss and every
+  parameter gradient at fp32, dropout 0, padded attention mask.
+* ``train.optim.FusedLAMB`` (CPU path; the GPU kernels are pinned to it in
+  tests/test_ops_gpu.py) vs the reference LAMB update rule
+  (bert_large/training/lamb.py:61-139, transcribed in benchmarks.eager.ReferenceLAMB).
+"""
+import pytest
+import torch
+
+transformers = pytest.importorskip("transformers")
+
+
+def _hf_and_ours(V=512, H=64, L=2, NH=4, I=128):
+    from cloudtik_amd.benchmarks.eager import hf_bert_config
+    from cloudtik_amd.models.bert import BertConfig, BertForPreTraining
+    hcfg = hf_bert_config(vocab_size=V, hidden_size=H, num_hidden_layers=L, num_attention_heads=NH,
+                          intermediate_size=I, max_position_embeddings=64, hidden_dropout_prob=0.0,
+                          attention_probs_dropout_prob=0.0)
+    torch.manual_seed(0)
+    hf = transformers.BertForPreTraining(hcfg).float().eval()
+    cfg = BertConfig(vocab_size=V, hidden_size=H, num_hidden_layers=L, num_attention_heads=NH,
+                     intermediate_size=I, max_position_embeddings=64, hidden_dropout_prob=0.0,
+                     attention_probs_dropout_prob=0.0)
+    ours = BertForPreTraining(cfg, dtype=torch.float32).eval()
+    sd = hf.state_dict()
+    m = {}                                        # our name -> HF tensor(s)
+    m["bert.word_embeddings"] = sd["bert.embeddings.word_embeddings.weight"]
+    m["bert.position_embeddings"] = sd["bert.embeddings.position_embeddings.weight"]
+    m["bert.token_type_embeddings"] = sd["bert.embeddings.token_type_embeddings.weight"]
+    m["bert.emb_ln_weight"] = sd["bert.embeddings.LayerNorm.weight"]
+    m["bert.emb_ln_bias"] = sd["bert.embeddings.LayerNorm.bias"]
+    for i in range(L):
+        p = f"bert.encoder.layer.{i}."
+        q = f"bert.layers.{i}."
+        for kind in ("weight", "bias"):
+            m[q + f"qkv_{kind}"] = torch.cat([sd[p + f"attention.self.{n}.{kind}"] for n in ("query", "key", "value")])
+            m[q + f"out_{kind}"] = sd[p + f"attention.output.dense.{kind}"]
+            m[q + f"ln1_{kind}"] = sd[p + f"attention.output.LayerNorm.{kind}"]
+            m[q + f"ffn1_{kind}"] = sd[p + f"intermediate.dense.{kind}"]
+            m[q + f"ffn2_{kind}"] = sd[p + f"output.dense.{kind}"]
+            m[q + f"ln2_{kind}"] = sd[p + f"output.LayerNorm.{kind}"]
+    m["bert.pooler_weight"] = sd["bert.pooler.dense.weight"]
+    m["bert.pooler_bias"] = sd["bert.pooler.dense.bias"]
+    m["mlm_dense_weight"] = sd["cls.predictions.transform.dense.weight"]
+    m["mlm_dense_bias"] = sd["cls.predictions.transform.dense.bias"]
+    m["mlm_ln_weight"] = sd["cls.predictions.transform.LayerNorm.weight"]
+    m["mlm_ln_bias"] = sd["cls.predictions.transform.LayerNorm.bias"]
+    m["mlm_decoder_bias"] = sd["cls.predictions.bias"]
+    m["nsp_weight"] = sd["cls.seq_relationship.weight"]
+    m["nsp_bias"] = sd["cls.seq_relationship.bias"]
+    mine = dict(ours.named_parameters())
+    assert set(m) == set(mine), set(mine) ^ set(m)
+    with torch.no_grad():
+        for n, t in m.items():
+            mine[n].zero_()
+            mine[n][: t.shape[0]].copy_(t)        # vocab rows beyond V are padding
+    return hf, ours, cfg
+
+
+def test_bert_pretraining_matches_hf_loss_and_grads():
+    from cloudtik_amd.benchmarks.eager import dense_mlm_labels
+    from cloudtik_amd.models.bert import synthetic_pretraining_batch
+    hf, ours, cfg = _hf_and_ours()
+    B, S, P = 3, 32, 6
+    b = synthetic_pretraining_batch(cfg, B, S, P, generator=torch.Generator().manual_seed(3))
+    b["attention_mask"][1, 24:] = 0               # padded keys
+    labels = dense_mlm_labels(b, S)
+    out = hf(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], attention_mask=b["attention_mask"],
+             labels=labels, next_sentence_label=b["next_sentence_labels"])
+    loss_ours = ours(**b)
+    torch.testing.assert_close(loss_ours, out.loss, rtol=1e-5, atol=1e-5)
+    out.loss.backward()
+    loss_ours.backward()
+    hg = {n: p.grad for n, p in hf.named_parameters() if p.grad is not None}
+    og = {n: p.grad for n, p in ours.named_parameters()}
+    q = "bert.layers.0."
+    p = "bert.encoder.layer.0."
+    pairs = [
+        (og["bert.word_embeddings"][: cfg.vocab_size], hg["bert.embeddings.word_embeddings.weight"]),
+        (og["bert.position_embeddings"], hg["bert.embeddings.position_embeddings.weight"]),
+        (og[q + "qkv_weight"], torch.cat([hg[p + f"attention.self.{n}.weight"] for n in ("query", "key", "value")])),
+        (og[q + "qkv_bias"], torch.cat([hg[p + f"attention.self.{n}.bias"] for n in ("query", "key", "value")])),
+        (og[q + "ffn1_weight"], hg[p + "intermediate.dense.weight"]),
+        (og[q + "ln2_weight"], hg[p + "output.LayerNorm.weight"]),
+        (og["mlm_decoder_bias"][: cfg.vocab_size], hg["cls.predictions.bias"]),
+        (og["mlm_dense_weight"], hg["cls.predictions.transform.dense.weight"]),
+        (og["bert.pooler_weight"], hg["bert.pooler.dense.weight"]),
+        (og["nsp_weight"], hg["cls.seq_relationship.weight"]),
+    ]
+    for a, r in pairs:
+        torch.testing.assert_close(a, r, rtol=1e-4, atol=1e-6)
+
+
+def test_fused_lamb_matches_reference_rule():
+    from cloudtik_amd.benchmarks.eager import ReferenceLAMB
+    from cloudtik_amd.train.optim import FlatParamSpace, FusedLAMB
+
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(24, 40), torch.nn.LayerNorm(40), torch.nn.Linear(40, 6))
+
+    nd = lambda n: n.endswith("bias") or n.startswith("1.")  # noqa: E731  (LayerNorm = module 1)
+    a, b = make(), make()
+    named = list(a.named_parameters())
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    fused = FusedLAMB(space, lr=5e-3, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01, no_decay=nd, space=space)
+    groups = [{"params": [p for n, p in b.named_parameters() if not nd(n)], "weight_decay": 0.01},
+              {"params": [p for n, p in b.named_parameters() if nd(n)], "weight_decay": 0.0}]
+    ref = ReferenceLAMB(groups, lr=5e-3, betas=(0.9, 0.999), eps=1e-6)
+    for it in range(5):
+        x = torch.randn(16, 24, generator=torch.Generator().manual_seed(it))
+        for m, opt in ((a, fused), (b, ref)):
+            m(x).pow(2).mean().backward()
+            opt.step()
+            opt.zero_grad()
+    for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.gpu
+def test_bert_native_kernels_match_hf_fp32():
+    """The bf16 HIP path (hand-scheduled blocks, MFMA attention, fused LN / xent kernels) vs
+    the fp32 Hugging Face model with identical weights."""
+    from cloudtik_amd.benchmarks.eager import dense_mlm_labels
+    from cloudtik_amd.models.bert import synthetic_pretraining_batch
+    hf, ours, cfg = _hf_and_ours(V=1024, H=256, L=2, NH=4, I=1024)
+    ours = ours.to("cuda", torch.bfloat16).train()
+    B, S, P = 8, 128, 20
+    b = synthetic_pretraining_batch(cfg, B, S, P, generator=torch.Generator().manual_seed(3))
+    b["attention_mask"][1, 100:] = 0
+    labels = dense_mlm_labels(b, S)
+    out = hf(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], attention_mask=b["attention_mask"],
+             labels=labels, next_sentence_label=b["next_sentence_labels"])
+    out.loss.backward()
+    loss = ours(**{k: v.cuda() for k, v in b.items()})
+    loss.backward()
+    assert abs(loss.item() - out.loss.item()) < 2e-2 * out.loss.item()
+    hg = dict(hf.named_parameters())
+    og = dict(ours.named_parameters())
+    for mine, theirs in (("bert.layers.0.ffn1_weight", "bert.encoder.layer.0.intermediate.dense.weight"),
+                         ("bert.layers.1.out_weight", "bert.encoder.layer.1.attention.output.dense.weight"),
+                         ("mlm_dense_weight", "cls.predictions.transform.dense.weight")):
+        a, r = og[mine].grad.float().cpu().reshape(-1), hg[theirs].grad.reshape(-1)
+        cos = torch.nn.functional.cosine_similarity(a, r, dim=0).item()
+        assert cos > 0.99, (mine, cos)

@@ -103,3 +103,59 @@ def test_p2p_from_env_disabled_without_gpu(monkeypatch):
     from cloudtik_amd.parallel import p2p
     monkeypatch.delenv("CLOUDTIK_P2P_ALLREDUCE_BYTES", raising=False)
     assert p2p.from_env() is None
+
+
+def _late_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from cloudtik_amd.parallel.p2p import P2PAllReducer
+        ar = P2PAllReducer(max_bytes=1 << 16, blocks=4, timeout_s=0.5)
+        t = torch.ones(1024, device="cuda")
+        ar.all_reduce(t)                 # both ranks: fine
+        torch.cuda.synchronize()
+        ok_first = ar.error() == 0
+        raised = False
+        if rank == 0:                    # rank 1 skips this call: rank 0's barrier-in times out
+            ar.all_reduce(t)
+            torch.cuda.synchronize()
+            try:
+                ar.check()
+            except RuntimeError:
+                raised = True
+        dist.barrier()
+        ar.close()
+        dist.destroy_process_group()
+        q.put((rank, (ok_first, raised), None))
+    except Exception as e:
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.gpu
+def test_p2p_missing_peer_is_reported_not_hung():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_late_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, out, err = q.get(timeout=240)
+        assert err is None, f"rank {rank}: {err}"
+        res[rank] = out
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == (True, True)        # the timed-out barrier surfaced as an error on rank 0
+    assert res[1] == (True, False)
+
+
+def test_p2p_enable_decision_is_collective():
+    from cloudtik_amd.parallel.p2p import decide
+    assert decide([("h", 1 << 20, True)] * 8)
+    assert not decide([("h", 1 << 20, True)] * 9)                      # beyond one node
+    assert not decide([("h", 1 << 20, True), ("g", 1 << 20, True)])    # two hosts
+    assert not decide([("h", 1 << 20, True), ("h", 0, True)])          # ranks disagree
+    assert not decide([("h", 1 << 20, True), ("h", 1 << 20, False)])   # a rank without GPU
