@@ -65,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="native path: fp32 = bf16 per-backward grads reduced / accumulated in fp32")
+    ap.add_argument("--zero", action="store_true",
+                    help="ZeRO-1: reduce-scatter gradients, shard optimizer state, all-gather weights")
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--conv-benchmark", action="store_true",
                     help="ResNet: let MIOpen search convolution solvers (torch.backends.cudnn.benchmark)")
@@ -150,14 +152,16 @@ def build_bert(args, rank, world, device, kind):
     model = BertForPreTraining(cfg, device=device, dtype=dtype)
     model.train()
     named = list(model.named_parameters())
-    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named],
+                           shard=(rank, world) if args.zero and world > 1 else (0, 1))
     opt = FusedLAMB(space, lr=3.5e-4, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01,
                     no_decay=BertForPreTraining.no_decay)
     sched = LinearWarmupPolyDecayScheduler(opt, start_warmup_steps=0, warmup_steps=0,
                                            total_steps=13700, end_learning_rate=0.0, degree=1.0)
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=args.bucket_mb,
-                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None)
+                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
+                       mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale
     B = args.batch or (256 if kind != "tiny" else 4)
     S = args.seq if kind != "tiny" else 32
@@ -198,12 +202,14 @@ def build_resnet(args, rank, world, device, kind):
     model = resnet18_like_small(device=device) if tiny else resnet50(device=device)
     model.train()
     named = list(model.named_parameters())
-    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named],
+                           shard=(rank, world) if args.zero and world > 1 else (0, 1))
     opt = FusedSGD(space, lr=0.1, momentum=0.9, weight_decay=1e-4,
                    no_decay=lambda n: n.endswith("bias") or ".bn" in n or n.startswith("bn"))
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=args.bucket_mb,
-                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None)
+                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
+                       mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale
     B = args.rn_batch or (256 if not tiny else 4)
     R = 224 if not tiny else 32
@@ -399,7 +405,8 @@ def main():
         cfg = {"model": head["model"], "global_batch": head["per_gpu_batch"] * world,
                "per_gpu_batch": head["per_gpu_batch"], "parallelism": f"dp{world}",
                "optimizer": head["optimizer"], "impl": head["impl"], "loss_last_step": round(head["loss"], 4),
-               "grad_dtype": args.grad_dtype if head["impl"] == "native" else "fp32 (autocast)"}
+               "grad_dtype": args.grad_dtype if head["impl"] == "native" else "fp32 (autocast)",
+               "zero1": bool(args.zero and world > 1)}
         if head["seq_len"]:
             cfg.update(seq_len=head["seq_len"], max_pred=head["max_pred"],
                        sentences_per_sec=round(head["value"] / head["seq_len"], 2))

@@ -12,20 +12,40 @@ import torch.distributed as dist
 from .ddp import GradBucketer, broadcast_flat_params  # noqa: F401
 
 
+# launcher families: (rank, size, local rank, local size) variables.  Rank and size are
+# taken from ONE family (reference runner/util/env.py:22-45 does the same pairing); the
+# torch/cloudtik-run family comes first because it is the innermost launcher when several
+# are nested (torchrun under an mpirun allocation), then Horovod, OpenMPI, MPICH/PMI.
+_FAMILIES = (("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"),
+             ("HOROVOD_RANK", "HOROVOD_SIZE", "HOROVOD_LOCAL_RANK", "HOROVOD_LOCAL_SIZE"),
+             ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK",
+              "OMPI_COMM_WORLD_LOCAL_SIZE"),
+             ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID", "MPI_LOCALNRANKS"))
+
+
 def env_rank_info():
-    """(rank, world, local_rank) from the launcher environment (torch/PMI/OMPI/Horovod
-    conventions, mirroring runtime/ai/runner/util/env.py:22-71 of the reference)."""
-    def first(*names, default=None):
-        for n in names:
-            v = os.environ.get(n)
-            if v not in (None, ""):
-                return int(v)
-        return default
-    rank = first("RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "HOROVOD_RANK", default=0)
-    world = first("WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "HOROVOD_SIZE", default=1)
-    local = first("LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK",
-                  "HOROVOD_LOCAL_RANK", default=0)
-    return rank, world, local
+    """(rank, world, local_rank) from the launcher environment -- the ONE implementation used
+    by bench.py, the Trainer and the Horovod-compatible API."""
+    env = os.environ
+    for rk, sz, lr, _ in _FAMILIES:
+        r, w = env.get(rk), env.get(sz)
+        if r not in (None, "") and w not in (None, ""):
+            local = env.get(lr)
+            if local in (None, ""):
+                local = next((env[f[2]] for f in _FAMILIES if env.get(f[2]) not in (None, "")), 0)
+            return int(r), int(w), int(local)
+        if (r not in (None, "")) != (w not in (None, "")):
+            raise RuntimeError(f"only one of {rk} / {sz} is set: cannot determine rank and world size")
+    return 0, 1, 0
+
+
+def env_local_world() -> int:
+    env = os.environ
+    for f in _FAMILIES:
+        v = env.get(f[3])
+        if v not in (None, ""):
+            return int(v)
+    return 1
 
 
 def init_distributed(backend: str = None, timeout_s: int = 1800):

@@ -21,6 +21,11 @@ Design (MI355X):
   so buckets must be large enough for RCCL's multi-channel rings to reach link rate while
   still leaving >=10 buckets of overlap for BERT-large (670 MB of bf16 grads); the
   reference's single 8 GiB bucket (no overlap at all) is available with bucket_mb=8192.
+* ``mode="reduce_scatter"`` (ZeRO-1, with ``FlatParamSpace(shard=(rank, world))``): buckets
+  are cut at multiples of world x 64 elements (a parameter may straddle two), each bucket is
+  reduce-scattered so that rank r receives the summed chunk r, the optimizer steps only
+  those chunks (state and fp32 master weights for 1/world of the model), and the updated
+  weights are all-gathered bucket by bucket after the step.
 * ``reduce_dtype=torch.float32``: the bf16 per-backward gradients are added into an fp32
   buffer (``space.main_grad``) bucket by bucket and the all-reduce sums fp32; micro-batches
   under ``no_sync()`` are accumulated into the same fp32 buffer when the context exits, and
@@ -37,10 +42,18 @@ import torch.distributed as dist
 
 class GradBucketer:
     def __init__(self, space, group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 comm_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None):
+                 comm_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None,
+                 mode: str = "all_reduce"):
         self.space = space
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if mode not in ("all_reduce", "reduce_scatter"):
+            raise ValueError(f"unknown mode {mode!r}")
+        self.zero = mode == "reduce_scatter" and self.world > 1
+        if space.world > 1 and not self.zero:
+            raise ValueError("a sharded FlatParamSpace needs GradBucketer(mode='reduce_scatter')")
+        if self.zero and (space.world != self.world or space.rank != dist.get_rank(group)):
+            raise ValueError("FlatParamSpace(shard=(rank, world)) must match the process group")
         self.fp32 = reduce_dtype == torch.float32 and space.grad.dtype != torch.float32
         if self.fp32:
             if space.main_grad is None:
@@ -50,29 +63,32 @@ class GradBucketer:
         self.comm_dtype = comm_dtype
         # small buckets over the one-shot P2P kernel instead of RCCL (opt-in, parallel/p2p.py)
         self.p2p = None
-        if self.world > 1 and space.grad.is_cuda:
+        if self.world > 1 and space.grad.is_cuda and not self.zero:
             from cloudtik_amd.parallel.p2p import from_env
             self.p2p = from_env(group)
             self._comm_stream = torch.cuda.Stream() if self.p2p is not None else None
         esize = space.grad.element_size()
         cap = max(1, int(bucket_mb * 1024 * 1024 / esize))
-        # buckets: param-aligned, contiguous ranges of the flat buffer
         self.buckets: List[tuple] = []
         self.param_bucket = {}
-        lo = 0
-        members: List[int] = []
-        for i, (o, n) in enumerate(zip(space.offsets, space.numels)):
-            members.append(i)
-            end = o + n
-            if end - lo >= cap:
-                hi = space.offsets[i + 1] if i + 1 < len(space.offsets) else space.total
-                self.buckets.append((lo, hi, list(members)))
-                lo, members = hi, []
-        if members or lo < space.total:
-            self.buckets.append((lo, space.total, list(members)))
+        if self.zero:
+            self._build_uniform_buckets(cap)
+        else:
+            # buckets: param-aligned, contiguous ranges of the flat buffer
+            lo = 0
+            members: List[int] = []
+            for i, (o, n) in enumerate(zip(space.offsets, space.numels)):
+                members.append(i)
+                end = o + n
+                if end - lo >= cap:
+                    hi = space.offsets[i + 1] if i + 1 < len(space.offsets) else space.total
+                    self.buckets.append((lo, hi, list(members)))
+                    lo, members = hi, []
+            if members or lo < space.total:
+                self.buckets.append((lo, space.total, list(members)))
         for b, (_, _, mem) in enumerate(self.buckets):
             for i in mem:
-                self.param_bucket[id(space.params[i])] = b
+                self.param_bucket.setdefault(id(space.params[i]), []).append(b)
         self._pending = [len(m) for _, _, m in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._next = 0
@@ -84,17 +100,47 @@ class GradBucketer:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
                 p._ct_grad_ready = self._on_grad   # fused-wgrad GEMMs (ops.linear) report here
 
+    # ------------------------------------------------------------------ ZeRO-1 layout
+    def _build_uniform_buckets(self, cap):
+        """Buckets at multiples of world x ALIGN elements; rank r owns chunk r of each."""
+        from cloudtik_amd.train.optim import ALIGN
+        sp, W, r = self.space, self.world, self.space.rank
+        unit = ALIGN * W
+        cap = max(unit, (cap // unit) * unit)
+        pieces, self._chunks = [], []
+        lo, loc = 0, 0
+        while lo < sp.total:
+            hi = min(lo + cap, sp.total)           # sp.total is a multiple of unit
+            mem = [i for i, (o, n) in enumerate(zip(sp.offsets, sp.numels)) if o < hi and o + n > lo]
+            self.buckets.append((lo, hi, mem))
+            c = (hi - lo) // W
+            pieces.append((lo + r * c, lo + (r + 1) * c, loc))
+            self._chunks.append((loc, c))
+            loc += c
+            lo = hi
+        gdt = torch.float32 if self.fp32 else sp.grad.dtype
+        sp.set_shard_pieces(pieces, gdt, norm_allreduce=lambda t: dist.all_reduce(t, group=self.group),
+                            gather_fn=self._gather_into, after_step=self._gather_params)
+
+    def _gather_into(self, local, full):
+        for (lo, hi, _), (loc, c) in zip(self.buckets, self._chunks):
+            dist.all_gather_into_tensor(full[lo:hi], local[loc:loc + c].contiguous(), group=self.group)
+
+    def _gather_params(self):
+        """After the optimizer step: every rank's updated chunk -> the full model buffer."""
+        self._gather_into(self.space.local_model, self.space.model)
+
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
         if not self._enabled:
             return
-        b = self.param_bucket[id(p)]
-        self._pending[b] -= 1
-        if self._pending[b] == 0:
-            self._ready[b] = True
-            while self._next < len(self.buckets) and self._ready[self._next]:
-                self._launch(self._next)
-                self._next += 1
+        for b in self.param_bucket[id(p)]:
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._ready[b] = True
+        while self._next < len(self.buckets) and self._ready[self._next]:
+            self._launch(self._next)
+            self._next += 1
 
     def _launch(self, b):
         from cloudtik_amd.ops.linear import grad_stream
@@ -123,6 +169,15 @@ class GradBucketer:
     def _launch_on_current(self, b):
         lo, hi, _ = self.buckets[b]
         t = self.space.grad[lo:hi]
+        if self.zero:
+            src = t
+            if self.fp32:
+                src = self.space.main_grad[lo:hi]
+                src.add_(t)
+            loc, c = self._chunks[b]
+            out = self.space.local_grad[loc:loc + c]
+            self._works.append((dist.reduce_scatter_tensor(out, src, group=self.group, async_op=True), None, None))
+            return
         if self.fp32:
             m = self.space.main_grad[lo:hi]
             m.add_(t)                      # fp32 sum of earlier micro-batches + this backward

@@ -9,9 +9,12 @@ role -- bf16 model weights, fp32 master weights, gradients -- and points each
 * the gradient buffer IS the data-parallel communication buffer: buckets are plain
   slices, so RCCL all-reduces / reduce-scatters need no pack/unpack copies
   (cloudtik_amd.parallel.ddp);
-* with ``shard=(rank, world)`` each rank owns 1/world of the flat space (ZeRO-1): the
-  optimizer state is sharded, gradients are reduce-scattered and parameters all-gathered
-  -- the same bytes on the wire as an all-reduce, 1/world of the optimizer HBM traffic.
+* with ``shard=(rank, world)`` and ``GradBucketer(mode="reduce_scatter")`` each rank owns
+  1/world of the flat space (ZeRO-1): chunk ``rank`` of every gradient bucket, packed into
+  shard-local buffers.  Optimizer state and fp32 master weights exist only for the shard,
+  gradients are reduce-scattered bucket by bucket during backward, the updated weights are
+  all-gathered after the step -- the same bytes on the wire as an all-reduce, 1/world of the
+  optimizer HBM traffic and state memory.  Checkpoints hold the state in the global layout.
 
 Reference optimizers reproduced: LAMB (bert_large/training/lamb.py:61-139 -- bf16 params
 with fp32 master copy, no bias correction, trust ratio only where weight_decay != 0),
@@ -99,26 +102,72 @@ class FlatParamSpace:
         # fp32 gradient the optimizer reads instead of ``grad`` when a bucketer reduces /
         # accumulates in fp32 (parallel.GradBucketer(reduce_dtype=torch.float32))
         self.main_grad: Optional[torch.Tensor] = None
+        # the shard as (global lo, global hi, shard-local offset) pieces: one contiguous slice
+        # by default; set_shard_pieces() switches to ZeRO-1's bucket-interleaved layout
+        self.pieces: List[Tuple[int, int, int]] = [(self.shard_lo, self.shard_hi, 0)]
+        self.local_grad: Optional[torch.Tensor] = None    # reduce-scatter output (ZeRO-1)
+        self.local_model: Optional[torch.Tensor] = None   # this rank's updated weights (ZeRO-1)
+        self.norm_allreduce: Optional[Callable[[torch.Tensor], None]] = None
+        self.gather_fn: Optional[Callable[[torch.Tensor, torch.Tensor], None]] = None
+        self._after_step: Optional[Callable[[], None]] = None
         # fp32 master copy of THIS rank's shard only
         self.master = self.model[self.shard_lo:self.shard_hi].float().clone() \
             if self.dtype != torch.float32 else None
         self._build_segments()
 
+    def set_shard_pieces(self, pieces: Sequence[Tuple[int, int, int]], grad_dtype: torch.dtype,
+                         norm_allreduce: Callable[[torch.Tensor], None],
+                         gather_fn: Callable[[torch.Tensor, torch.Tensor], None],
+                         after_step: Callable[[], None]):
+        """ZeRO-1 layout: this rank owns ``pieces`` (global ranges, packed back to back in
+        shard-local buffers).  ``gather_fn(local, full)`` rebuilds a global-layout tensor from
+        every rank's shard-local one; ``after_step`` all-gathers the updated weights."""
+        assert sum(h - l for l, h, _ in pieces) == self.shard_size, "pieces must cover one shard"
+        self.pieces = list(pieces)
+        self.local_model = self.local_of(self.model)
+        self.local_grad = torch.zeros(self.shard_size, dtype=grad_dtype, device=self.device)
+        self.master = self.local_model.float().clone() if self.dtype != torch.float32 else None
+        self.norm_allreduce, self.gather_fn, self._after_step = norm_allreduce, gather_fn, after_step
+        self._build_segments()
+
+    @property
+    def sharded(self) -> bool:
+        return self.local_model is not None
+
+    def local_of(self, full: torch.Tensor) -> torch.Tensor:
+        """This rank's pieces of a global-layout flat tensor, packed."""
+        if len(self.pieces) == 1:
+            lo, hi, _ = self.pieces[0]
+            return full[lo:hi].clone()
+        return torch.cat([full[lo:hi] for lo, hi, _ in self.pieces])
+
+    def full_of(self, local: torch.Tensor) -> torch.Tensor:
+        """Global-layout tensor assembled from every rank's shard-local ``local``."""
+        if self.gather_fn is None:
+            return local
+        full = torch.zeros(self.total, dtype=local.dtype, device=local.device)
+        self.gather_fn(local, full)
+        return full
+
+    def after_step(self):
+        if self._after_step is not None:
+            self._after_step()
+
     # ------------------------------------------------------------------ segments
     def _build_segments(self):
         seg_tensor, seg_start, seg_len, first = [], [], [], []
-        lo, hi = self.shard_lo, self.shard_hi
         for t, (o, n) in enumerate(zip(self.offsets, self.numels)):
             first.append(len(seg_tensor))
             padded = ((n + ALIGN - 1) // ALIGN) * ALIGN
-            a, b = max(o, lo), min(o + padded, hi)
-            s = a
-            while s < b:
-                e = min(s + SEG, b)
-                seg_tensor.append(t)
-                seg_start.append(s - lo)      # relative to the shard
-                seg_len.append(e - s)
-                s = e
+            for lo, hi, loc in self.pieces:      # a tensor may span several pieces
+                a, b = max(o, lo), min(o + padded, hi)
+                s = a
+                while s < b:
+                    e = min(s + SEG, b)
+                    seg_tensor.append(t)
+                    seg_start.append(loc + s - lo)      # shard-local
+                    seg_len.append(e - s)
+                    s = e
         first.append(len(seg_tensor))
         dev = self.device
         self.nseg = len(seg_tensor)
@@ -132,10 +181,12 @@ class FlatParamSpace:
     @property
     def shard_params(self) -> torch.Tensor:
         """fp32 weights owned by this rank (master copy, or the model buffer if fp32)."""
-        return self.master if self.master is not None else self.model[self.shard_lo:self.shard_hi]
+        return self.master if self.master is not None else self.shard_model
 
     @property
     def shard_model(self) -> torch.Tensor:
+        if self.local_model is not None:
+            return self.local_model
         return self.model[self.shard_lo:self.shard_hi]
 
     @property
@@ -146,18 +197,24 @@ class FlatParamSpace:
 
     @property
     def shard_grad(self) -> torch.Tensor:
+        if self.local_grad is not None:
+            return self.local_grad
         return self.reduced_grad[self.shard_lo:self.shard_hi]
 
     def zero_grad(self):
         self.grad.zero_()
         if self.main_grad is not None:
             self.main_grad.zero_()
+        if self.local_grad is not None:
+            self.local_grad.zero_()
 
     def tensor_wd(self, wd_fn: Callable[[str, torch.nn.Parameter], float]) -> torch.Tensor:
         return torch.tensor([float(wd_fn(n, p)) for n, p in zip(self.names, self.params)],
                             dtype=torch.float32, device=self.device)
 
     def sync_master_from_model(self):
+        if self.local_model is not None:
+            self.local_model.copy_(self.local_of(self.model))
         if self.master is not None:
             self.master.copy_(self.shard_model.float())
 
@@ -236,19 +293,30 @@ class _FlatOptimizer(torch.optim.Optimizer):
             self.dyn.copy_(host)
 
     def state_dict(self):
+        """Flat optimizer state in the GLOBAL layout (ZeRO-1 shards are gathered), so a
+        checkpoint restores onto any sharding / world size."""
         sd = super().state_dict()
-        sd["flat"] = {k: v for k, v in self._flat_state().items()}
-        if self.space.master is not None:      # fp32 master shard (the bf16 model alone loses bits)
-            sd["flat"]["master"] = self.space.master
+        sp = self.space
+        flat = dict(self._flat_state())
+        if sp.master is not None:      # fp32 master shard (the bf16 model alone loses bits)
+            flat["master"] = sp.master
+        sd["flat"] = {k: (sp.full_of(v) if sp.sharded else v) for k, v in flat.items()}
+        sd["flat_layout"] = "global" if sp.sharded else ("shard" if sp.world > 1 else "global")
         sd["step_count"] = self.step_count
         return sd
 
     def load_state_dict(self, sd):
+        sd = dict(sd)
         flat = sd.pop("flat", {})
+        layout = sd.pop("flat_layout", "shard")
         self.step_count = sd.pop("step_count", 0)
         super().load_state_dict(sd)
+        sp = self.space
         for k, v in flat.items():
-            dst = self.space.master if k == "master" else getattr(self, k)
+            dst = sp.master if k == "master" else getattr(self, k)
+            v = v.to(dst.device)
+            if layout == "global" and v.numel() == sp.total and dst.numel() != sp.total:
+                v = sp.local_of(v)
             dst.copy_(v)
 
     def _flat_state(self):
@@ -271,7 +339,9 @@ class FusedLAMB(_FlatOptimizer):
         self.seg_part = torch.zeros(max(1, 2 * sp.nseg), dtype=torch.float32, device=sp.device)
         self.tensor_part = torch.zeros(2 * len(sp.params), dtype=torch.float32, device=sp.device)
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=sp.device)
-        self.norm_allreduce: Optional[Callable[[torch.Tensor], None]] = None  # set by ZeRO wrapper
+        # per-tensor norm all-reduce over the data-parallel group; ZeRO-1 (space.sharded) sets
+        # one on the space, an explicit one here takes precedence
+        self.norm_allreduce: Optional[Callable[[torch.Tensor], None]] = None
 
     def _flat_state(self):
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
@@ -285,26 +355,30 @@ class FusedLAMB(_FlatOptimizer):
         b1, b2 = self.betas
         self._push_dyn(b1 if self.bias_correction else None, b2 if self.bias_correction else None)
         g = sp.shard_grad
+        if self.seg_part.numel() < 2 * sp.nseg:      # segments rebuilt by a ZeRO-1 layout
+            self.seg_part = torch.zeros(2 * sp.nseg, dtype=torch.float32, device=sp.device)
         if _is_native(g):
             from cloudtik_amd import ops
             C = ops.require_native()
+            nar = self.norm_allreduce or sp.norm_allreduce
             if self.max_grad_norm:
                 self._sumsq.zero_()
                 C.sumsq_into(g, self._sumsq)
-                if self.norm_allreduce is not None:
-                    self.norm_allreduce(self._sumsq)
+                if nar is not None:
+                    nar(self._sumsq)
                 C.clip_coef(self._sumsq, self.dyn, float(self.grad_scale), float(self.max_grad_norm))
             wm = sp.shard_model if sp.master is not None else None
             C.lamb_step(g, self.exp_avg, self.exp_avg_sq, sp.shard_params, wm, sp.seg_tensor,
                         sp.seg_start, sp.seg_len, sp.tensor_first_seg, self._wd, self.dyn, b1, b2,
                         self.eps, self.bias_correction, self.trust_all, self.seg_part, self.tensor_part, 1)
-            if self.norm_allreduce is not None:
-                self.norm_allreduce(self.tensor_part)
+            if nar is not None:
+                nar(self.tensor_part)
             C.lamb_step(g, self.exp_avg, self.exp_avg_sq, sp.shard_params, wm, sp.seg_tensor,
                         sp.seg_start, sp.seg_len, sp.tensor_first_seg, self._wd, self.dyn, b1, b2,
                         self.eps, self.bias_correction, self.trust_all, self.seg_part, self.tensor_part, 2)
         else:
             self._step_torch(g)
+        sp.after_step()
         return loss
 
     def _step_torch(self, g):
@@ -315,11 +389,12 @@ class FusedLAMB(_FlatOptimizer):
         bc1 = 1.0 / (1.0 - b1 ** t) if self.bias_correction else 1.0
         bc2 = 1.0 / (1.0 - b2 ** t) if self.bias_correction else 1.0
         gf = g.float() * gs
+        nar = self.norm_allreduce or sp.norm_allreduce
         if self.max_grad_norm:
             nrm = gf.pow(2).sum()
-            if self.norm_allreduce is not None:
+            if nar is not None:
                 buf = nrm.reshape(1).clone()
-                self.norm_allreduce(buf)
+                nar(buf)
                 nrm = buf[0]
             coef = torch.clamp(self.max_grad_norm / (nrm.sqrt() + 1e-6), max=1.0)
             gf = gf * coef
@@ -334,8 +409,8 @@ class FusedLAMB(_FlatOptimizer):
         tp = torch.zeros(2 * T, dtype=torch.float32, device=w.device)
         tp[0::2].index_add_(0, tid[valid], (w * w)[valid])
         tp[1::2].index_add_(0, tid[valid], (u * u)[valid])
-        if self.norm_allreduce is not None:
-            self.norm_allreduce(tp)
+        if nar is not None:
+            nar(tp)
         wn, un = tp[0::2].sqrt(), tp[1::2].sqrt()
         ratio = torch.where((wn > 0) & (un > 0), wn / un.clamp_min(1e-30), torch.ones_like(wn))
         if not self.trust_all:
@@ -406,6 +481,7 @@ class FusedAdam(_FlatOptimizer):
             w.sub_(lr * upd)
             if sp.master is not None:
                 sp.shard_model.copy_(w)
+        sp.after_step()
         return loss
 
 
@@ -451,6 +527,7 @@ class FusedSGD(_FlatOptimizer):
             w.sub_(self._lr() * gf)
             if sp.master is not None:
                 sp.shard_model.copy_(w)
+        sp.after_step()
         return loss
 
 

@@ -30,36 +30,18 @@ logger = logging.getLogger(__name__)
 
 
 def rank_env() -> Dict[str, int]:
-    """RANK / WORLD_SIZE / LOCAL_RANK from torch, Horovod, OpenMPI or PMI variables
-    (reference runner/util/env.py:22-71 and trainer.py:231-232)."""
-    def first(*names, default=None):
-        for n in names:
-            v = os.environ.get(n)
-            if v not in (None, ""):
-                return int(v)
-        return default
-    return {"rank": first("RANK", "HOROVOD_RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", default=0),
-            "world": first("WORLD_SIZE", "HOROVOD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", default=1),
-            "local_rank": first("LOCAL_RANK", "HOROVOD_LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID",
-                                default=0)}
+    """RANK / WORLD_SIZE / LOCAL_RANK from torch, Horovod, OpenMPI or PMI variables (one
+    implementation: parallel.env_rank_info; reference runner/util/env.py:22-71)."""
+    from cloudtik_amd.parallel import env_rank_info
+    rank, world, local = env_rank_info()
+    return {"rank": rank, "world": world, "local_rank": local}
 
 
 def setup_distributed(backend: Optional[str] = None):
     """Initialise the process group if the job has several ranks; returns (rank, world, device)."""
-    env = rank_env()
-    use_gpu = torch.cuda.is_available()
-    device = torch.device("cuda", env["local_rank"] % max(1, torch.cuda.device_count())) if use_gpu \
-        else torch.device("cpu")
-    if use_gpu:
-        torch.cuda.set_device(device)
-    if env["world"] > 1 and not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29500")
-        os.environ["RANK"], os.environ["WORLD_SIZE"] = str(env["rank"]), str(env["world"])
-        backend = backend or ("nccl" if use_gpu else "gloo")
-        kw = {"device_id": device} if backend == "nccl" else {}
-        dist.init_process_group(backend, rank=env["rank"], world_size=env["world"], **kw)
-    return env["rank"], env["world"], device
+    from cloudtik_amd.parallel import init_distributed
+    rank, world, _, device = init_distributed(backend=backend)
+    return rank, world, device
 
 
 def partition_dataset(dataset, rank: int, world: int, seed: int = 0, shuffle: bool = True):
@@ -107,13 +89,16 @@ class Trainer:
                  log_every: int = 50, bucket_mb: float = 64.0, no_decay: Optional[Callable[[str], bool]] = None,
                  callbacks: Optional[List[Callable]] = None, optimizer_kwargs: Optional[Dict] = None,
                  step_timing: Optional[bool] = None, async_checkpoint: bool = False,
-                 metrics_port: Optional[int] = None):
+                 metrics_port: Optional[int] = None, zero: bool = False,
+                 reduce_dtype: Optional[torch.dtype] = None):
         from cloudtik_amd.parallel import GradBucketer, broadcast_flat_params
         from cloudtik_amd.train.optim import build_optimizer
         self.rank, self.world, self.device = setup_distributed()
         self.model = model.to(self.device)
+        zero = zero and self.world > 1
         if isinstance(optimizer, str):
             self.optimizer = build_optimizer(optimizer, self.model, lr, weight_decay, no_decay,
+                                             shard=(self.rank, self.world) if zero else (0, 1),
                                              **(optimizer_kwargs or {}))
         else:
             self.optimizer = optimizer
@@ -121,7 +106,8 @@ class Trainer:
         self.bucketer = None
         if self.space is not None:
             broadcast_flat_params(self.space)
-            self.bucketer = GradBucketer(self.space, bucket_mb=bucket_mb)
+            self.bucketer = GradBucketer(self.space, bucket_mb=bucket_mb, reduce_dtype=reduce_dtype,
+                                         mode="reduce_scatter" if self.space.world > 1 else "all_reduce")
             self.optimizer.grad_scale = self.bucketer.grad_scale / grad_accum
         elif self.world > 1:
             for p in self.model.parameters():
@@ -174,12 +160,15 @@ class Trainer:
         return {k: t[i].item() / n for i, k in enumerate(keys)}
 
     def _clip(self):
-        g = self.space.reduced_grad if self.space is not None else None
+        g = self.space.shard_grad if self.space is not None else None
         if g is None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip_norm)
             return
         scale = self.optimizer.grad_scale
-        norm = g.float().norm() * scale
+        sq = g.float().pow(2).sum()
+        if self.space.sharded:                      # ZeRO-1: each rank holds 1/world of the grads
+            dist.all_reduce(sq)
+        norm = sq.sqrt() * scale
         coef = (self.clip_norm / (norm + 1e-6)).clamp(max=1.0)
         g.mul_(coef.to(g.dtype))
 

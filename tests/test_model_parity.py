@@ -14,16 +14,16 @@ import torch
 transformers = pytest.importorskip("transformers")
 
 
-def _hf_and_ours(V=512, H=64, L=2, NH=4, I=128):
+def _hf_and_ours(V=512, H=64, L=2, NH=4, I=128, maxpos=64):
     from cloudtik_amd.benchmarks.eager import hf_bert_config
     from cloudtik_amd.models.bert import BertConfig, BertForPreTraining
     hcfg = hf_bert_config(vocab_size=V, hidden_size=H, num_hidden_layers=L, num_attention_heads=NH,
-                          intermediate_size=I, max_position_embeddings=64, hidden_dropout_prob=0.0,
+                          intermediate_size=I, max_position_embeddings=maxpos, hidden_dropout_prob=0.0,
                           attention_probs_dropout_prob=0.0)
     torch.manual_seed(0)
     hf = transformers.BertForPreTraining(hcfg).float().eval()
     cfg = BertConfig(vocab_size=V, hidden_size=H, num_hidden_layers=L, num_attention_heads=NH,
-                     intermediate_size=I, max_position_embeddings=64, hidden_dropout_prob=0.0,
+                     intermediate_size=I, max_position_embeddings=maxpos, hidden_dropout_prob=0.0,
                      attention_probs_dropout_prob=0.0)
     ours = BertForPreTraining(cfg, dtype=torch.float32).eval()
     sd = hf.state_dict()
@@ -127,7 +127,7 @@ def test_bert_native_kernels_match_hf_fp32():
     the fp32 Hugging Face model with identical weights."""
     from cloudtik_amd.benchmarks.eager import dense_mlm_labels
     from cloudtik_amd.models.bert import synthetic_pretraining_batch
-    hf, ours, cfg = _hf_and_ours(V=1024, H=256, L=2, NH=4, I=1024)
+    hf, ours, cfg = _hf_and_ours(V=1024, H=256, L=2, NH=4, I=1024, maxpos=128)
     ours = ours.to("cuda", torch.bfloat16).train()
     B, S, P = 8, 128, 20
     b = synthetic_pretraining_batch(cfg, B, S, P, generator=torch.Generator().manual_seed(3))
