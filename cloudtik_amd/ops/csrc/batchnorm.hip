@@ -1,5 +1,11 @@
 // Training BatchNorm for NHWC (channels_last) bf16 activations, fused with the residual
-// add and ReLU that follow it in every ResNet bottleneck.
+// add and ReLU that follow it in every ResNet bottleneck.  The backward never re-reads the
+// BN output for the ReLU mask when there is no residual: the mask is the sign of the
+// forward pre-activation, recomputed from x with the saved affine coefficients (one fewer
+// activation-sized read in each backward pass).  A one-pass fp64-atomic variant of the
+// statistics reduction (last block finalises) was measured 4-6x SLOWER on MI355X: ~1000
+// blocks x C same-address device-scope atomics serialise, so block partials + a small
+// finalize launch stay.
 //
 // Reference hot path: torchvision resnet50 trained channels_last + bf16 under DDP
 // (applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296) and
@@ -24,7 +30,7 @@ __device__ __forceinline__ void bn_thread(const BnLayout& L, int& cv, int& rl) {
   rl = threadIdx.x / L.CV;
 }
 
-// per-block (mean, M2) over rows [b*R, (b+1)*R)
+// per-block (mean, M2) over rows [b*R, (b+1)*R), 4 rows in flight per thread
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, BnLayout L,
                                                        float* __restrict__ pmean,
                                                        float* __restrict__ pm2) {
@@ -38,7 +44,17 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
   if (rl < L.RPI) {
-    for (int r = r0 + rl; r < r1; r += L.RPI) {
+    int r = r0 + rl;
+    for (; r + 3 * L.RPI < r1; r += 4 * L.RPI) {
+      u16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const u16x8*>(x + (size_t)(r + u * L.RPI) * L.C)[cv];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float f = bf2f(v[u][j]); s[j] += f; q[j] += f * f; }
+    }
+    for (; r < r1; r += L.RPI) {
       const u16x8 v = reinterpret_cast<const u16x8*>(x + (size_t)r * L.C)[cv];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { const float f = bf2f(v[j]); s[j] += f; q[j] += f * f; }
@@ -65,41 +81,39 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
 }
 
 // Chan-merge of block partials; writes save_mean/save_invstd, affine (a, b) and updates
-// running statistics.  Block = 64 channels x 16 partial-lanes; each lane Chan-merges a
-// strided subset of the block partials, then the 16 lane results merge through LDS.
+// running statistics.  One wave per channel (16 channels per 1024-thread block): each lane
+// loads its <= nblk/64 partials up front (independent loads in flight, not a dependent
+// chain), merges them, then the 64 lane results merge through a 6-step shuffle tree.
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float qb) {
+  const float nn = n + nb;
+  if (nn <= 0.f) return;
+  const float d = mb - mean;
+  mean += d * nb / nn;
+  m2 += qb + d * d * n * nb / nn;
+  n = nn;
+}
+
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     const float* __restrict__ pmean, const float* __restrict__ pm2, int nblk, BnLayout L,
     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta, float eps, float momentum,
     float* __restrict__ run_mean, float* __restrict__ run_var, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ coef_a, float* __restrict__ coef_b) {
-  __shared__ float sn[16][64], sm[16][64], sq[16][64];
-  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 16 + (threadIdx.x >> 6);
+  if (c >= L.C) return;                              // whole wave exits together
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < L.C) {
-    for (int b = pl; b < nblk; b += 16) {
-      const int r0 = b * L.rows_per_blk;
-      const float nb = (float)max(0, min(L.M, r0 + L.rows_per_blk) - r0);
-      if (nb <= 0.f) continue;
-      const float mb = pmean[(size_t)b * L.C + c], qb = pm2[(size_t)b * L.C + c];
-      const float nn = n + nb;
-      const float d = mb - mean;
-      mean += d * nb / nn;
-      m2 += qb + d * d * n * nb / nn;
-      n = nn;
-    }
+#pragma unroll 8
+  for (int b = lane; b < nblk; b += 64) {
+    const int r0 = b * L.rows_per_blk;
+    const float nb = (float)max(0, min(L.M, r0 + L.rows_per_blk) - r0);
+    chan_merge(n, mean, m2, nb, pmean[(size_t)b * L.C + c], pm2[(size_t)b * L.C + c]);
   }
-  sn[pl][cl] = n; sm[pl][cl] = mean; sq[pl][cl] = m2;
-  __syncthreads();
-  if (pl != 0 || c >= L.C) return;
-  for (int k = 1; k < 16; ++k) {
-    const float nb = sn[k][cl];
-    if (nb <= 0.f) continue;
-    const float nn = n + nb, d = sm[k][cl] - mean;
-    mean += d * nb / nn;
-    m2 += sq[k][cl] + d * d * n * nb / nn;
-    n = nn;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float nb = __shfl_xor(n, off), mb = __shfl_xor(mean, off), qb = __shfl_xor(m2, off);
+    chan_merge(n, mean, m2, nb, mb, qb);
   }
+  if (lane != 0) return;
   const float var = n > 0.f ? m2 / n : 0.f;
   const float invstd = rsqrtf(var + eps);
   const float g = gamma ? bf2f(gamma[c]) : 1.f, bt = beta ? bf2f(beta[c]) : 0.f;
@@ -113,6 +127,9 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
   }
 }
+
+// pre-activation of the fused forward, evaluated identically in forward and backward
+__device__ __forceinline__ float bn_pre(float x, float a, float b, float r) { return __builtin_fmaf(x, a, b) + r; }
 
 // y = act(x * a[c] + b[c] (+ res))
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x,
@@ -133,7 +150,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float aj = j < 4 ? a0[j] : a1[j - 4], bj = j < 4 ? b0[j] : b1[j - 4];
-      float t = bf2f(xv[j]) * aj + bj + bf2f(rv[j]);
+      float t = bn_pre(bf2f(xv[j]), aj, bj, bf2f(rv[j]));
       if (relu) t = fmaxf(t, 0.f);
       o[j] = f2bf(t);
     }
@@ -141,11 +158,36 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// per-block sums of dy' and dy'*xhat
+// ReLU mask source for the backward: mode 0 = no ReLU, 1 = read y (fused residual add),
+// 2 = recompute the pre-activation from x and the forward affine (a, b): no y read at all
+struct BnMask {
+  int mode;
+  const bf16_t* y;
+  const float* fa;
+  const float* fb;
+};
+
+__device__ __forceinline__ void bn_mask8(const BnMask& mk, size_t o, int cv, const u16x8& xv, bool (&on)[8]) {
+  if (mk.mode == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) on[j] = true;
+  } else if (mk.mode == 1) {
+    const u16x8 yv = reinterpret_cast<const u16x8*>(mk.y)[o];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) on[j] = bf2f(yv[j]) > 0.f;
+  } else {
+    const f32x4* a4 = reinterpret_cast<const f32x4*>(mk.fa) + 2 * cv;
+    const f32x4* b4 = reinterpret_cast<const f32x4*>(mk.fb) + 2 * cv;
+    const f32x4 aa[2] = {a4[0], a4[1]}, bb[2] = {b4[0], b4[1]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) on[j] = bf2f(f2bf(bn_pre(bf2f(xv[j]), aa[j >> 2][j & 3], bb[j >> 2][j & 3], 0.f))) > 0.f;
+  }
+}
+
+// per-block sums of dy' and dy'*xhat (dy' = masked dy), 4 rows in flight per thread
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ invstd, BnLayout L, int relu,
-    float* __restrict__ p1, float* __restrict__ p2) {
+    const bf16_t* __restrict__ dy, BnMask mk, const bf16_t* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ invstd, BnLayout L, float* __restrict__ p1, float* __restrict__ p2) {
   __shared__ float l1[256 * 8];
   __shared__ float l2[256 * 8];
   int cv, rl;
@@ -159,15 +201,37 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     mu[j] = mean[cv * 8 + j]; is[j] = invstd[cv * 8 + j];
   }
   if (rl < L.RPI) {
-    for (int r = r0 + rl; r < r1; r += L.RPI) {
+    int r = r0 + rl;
+    for (; r + 3 * L.RPI < r1; r += 4 * L.RPI) {
+      u16x8 g[4], xv[4];
+      size_t o[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        o[u] = (size_t)(r + u * L.RPI) * L.CV + cv;
+        g[u] = reinterpret_cast<const u16x8*>(dy)[o[u]];
+        xv[u] = reinterpret_cast<const u16x8*>(x)[o[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        bool on[8];
+        bn_mask8(mk, o[u], cv, xv[u], on);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = on[j] ? bf2f(g[u][j]) : 0.f;
+          s1[j] += d;
+          s2[j] += d * (bf2f(xv[u][j]) - mu[j]) * is[j];
+        }
+      }
+    }
+    for (; r < r1; r += L.RPI) {
       const size_t o = (size_t)r * L.CV + cv;
       const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
       const u16x8 xv = reinterpret_cast<const u16x8*>(x)[o];
-      u16x8 yv = u16x8(1);
-      if (relu) yv = reinterpret_cast<const u16x8*>(y)[o];
+      bool on[8];
+      bn_mask8(mk, o, cv, xv, on);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float d = (relu && !(bf2f(yv[j]) > 0.f)) ? 0.f : bf2f(g[j]);
+        const float d = on[j] ? bf2f(g[j]) : 0.f;
         s1[j] += d;
         s2[j] += d * (bf2f(xv[j]) - mu[j]) * is[j];
       }
@@ -190,23 +254,22 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   }
 }
 
-// dgamma, dbeta and dx = a*dy' + c1*x + c0 coefficients (64 channels x 16 lanes per block)
+// dgamma, dbeta and dx = a*dy' + c1*x + c0 coefficients (one wave per channel, as above)
 template <typename PT>
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float* __restrict__ p1, const float* __restrict__ p2, int nblk, int M, int C,
     const bf16_t* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ invstd, PT* __restrict__ dgamma, PT* __restrict__ dbeta,
     float* __restrict__ ca, float* __restrict__ c1, float* __restrict__ c0, int acc) {
-  __shared__ float s1[16][64], s2[16][64];
-  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 16 + (threadIdx.x >> 6);
+  if (c >= C) return;
   float sdy = 0.f, sdx = 0.f;
-  if (c < C)
-    for (int b = pl; b < nblk; b += 16) { sdy += p1[(size_t)b * C + c]; sdx += p2[(size_t)b * C + c]; }
-  s1[pl][cl] = sdy; s2[pl][cl] = sdx;
-  __syncthreads();
-  if (pl != 0 || c >= C) return;
-  for (int k = 1; k < 16; ++k) { sdy += s1[k][cl]; sdx += s2[k][cl]; }
+#pragma unroll 8
+  for (int b = lane; b < nblk; b += 64) { sdy += p1[(size_t)b * C + c]; sdx += p2[(size_t)b * C + c]; }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) { sdy += __shfl_xor(sdy, off); sdx += __shfl_xor(sdx, off); }
+  if (lane != 0) return;
   // acc: accumulate into the (flat-buffer) parameter gradients instead of overwriting, so
   // no separate AccumulateGrad kernel runs per BatchNorm parameter
   if (dgamma) dgamma[c] = from_f<PT>(acc ? to_f<PT>(dgamma[c]) + sdx : sdx);
@@ -221,16 +284,16 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const bf16_t* __restrict__ dy, BnMask mk, const bf16_t* __restrict__ x,
     const float* __restrict__ ca, const float* __restrict__ c1, const float* __restrict__ c0,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long total_vec, int CV, int relu) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long total_vec, int CV) {
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
        v += (long)gridDim.x * blockDim.x) {
     const int cv = (int)(v % CV);
     const u16x8 g = reinterpret_cast<const u16x8*>(dy)[v];
     const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
-    u16x8 yv = u16x8(1);
-    if (relu) yv = reinterpret_cast<const u16x8*>(y)[v];
+    bool on[8];
+    bn_mask8(mk, (size_t)v, cv, xv, on);
     const f32x4* a4 = reinterpret_cast<const f32x4*>(ca) + 2 * cv;
     const f32x4* k4 = reinterpret_cast<const f32x4*>(c1) + 2 * cv;
     const f32x4* z4 = reinterpret_cast<const f32x4*>(c0) + 2 * cv;
@@ -238,7 +301,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     u16x8 o, od;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d = (relu && !(bf2f(yv[j]) > 0.f)) ? 0.f : bf2f(g[j]);
+      const float d = on[j] ? bf2f(g[j]) : 0.f;
       o[j] = f2bf(aa[j >> 2][j & 3] * d + kk[j >> 2][j & 3] * bf2f(xv[j]) + zz[j >> 2][j & 3]);
       od[j] = f2bf(d);
     }
@@ -270,9 +333,9 @@ inline int ew_grid(long work) {
 
 using namespace ct;
 
-extern "C" int ct_bn_max_blocks() { return 1024; }
+extern "C" int ct_bn_max_blocks() { return 2048; }
 
-// workspace: part = float[2 * 1024 * C]; stat = float[4 * C] (save_mean, save_invstd, a, b)
+// workspace: part = float[2 * 2048 * C]; stat = float[4 * C] (save_mean, save_invstd, a, b)
 extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma, const void* beta,
                                float* run_mean, float* run_var, void* y, float* part, float* stat,
                                int M, int C, float eps, float momentum, int relu,
@@ -280,8 +343,8 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
   if (C % 8 || C / 8 > 256 || M <= 0) return -1;
   BnLayout L = bn_layout(M, C, 512);
   const int nblk = bn_nblk(L);
-  bn_stats_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)1024 * C);
-  bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)1024 * C, nblk, L,
+  bn_stats_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
+  bn_finalize_kernel<<<ceil_div(C, 16), 1024, 0, stream>>>(part, part + (size_t)2048 * C, nblk, L,
                                                            (const bf16_t*)gamma, (const bf16_t*)beta,
                                                            eps, momentum, run_mean, run_var, stat,
                                                            stat + C, stat + 2 * C, stat + 3 * C);
@@ -301,29 +364,30 @@ extern "C" int ct_bn_apply(const void* x, const void* res, const float* a, const
   return 0;
 }
 
-// workspace: part = float[2 * 1024 * C]; coef = float[3 * C]
-extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const void* gamma,
-                         const float* save_mean, const float* save_invstd, void* dx, void* dres,
-                         void* dgamma, void* dbeta, int param_fp32, float* part, float* coef, int M,
-                         int C, int relu, hipStream_t stream) {
-  if (C % 8 || C / 8 > 256 || M <= 0) return -1;
+// stat = the forward's float[4C] (mean, invstd, a, b).  relu_mode: 0 none, 1 read y,
+// 2 recompute from x (no residual in the forward).  part = float[2 * 2048 * C],
+// coef = float[3 * C] scratch.
+extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const void* gamma, const float* stat,
+                         void* dx, void* dres, void* dgamma, void* dbeta, int param_flags, float* part,
+                         float* coef, int M, int C, int relu_mode, hipStream_t stream) {
+  if (C % 8 || C / 8 > 256 || M <= 0 || relu_mode < 0 || relu_mode > 2) return -1;
+  if (relu_mode == 1 && !y) return -2;
   BnLayout L = bn_layout(M, C, 512);
   const int nblk = bn_nblk(L);
-  bn_bwd_reduce_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
-                                                 (const bf16_t*)x, save_mean, save_invstd, L, relu,
-                                                 part, part + (size_t)1024 * C);
-  const int acc = (param_fp32 >> 1) & 1;   // bit 1: accumulate into dgamma / dbeta
-  if (param_fp32 & 1)
-    bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
-        part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
+  const BnMask mk{relu_mode, (const bf16_t*)y, stat + 2 * C, stat + 3 * C};
+  bn_bwd_reduce_kernel<<<nblk, 256, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
+                                                 part, part + (size_t)2048 * C);
+  const int acc = (param_flags >> 1) & 1;   // bit 1: accumulate into dgamma / dbeta
+  if (param_flags & 1)
+    bn_bwd_finalize_kernel<float><<<ceil_div(C, 16), 1024, 0, stream>>>(
+        part, part + (size_t)2048 * C, nblk, M, C, (const bf16_t*)gamma, stat, stat + C,
         (float*)dgamma, (float*)dbeta, coef, coef + C, coef + 2 * C, acc);
   else
-    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
-        part, part + (size_t)1024 * C, nblk, M, C, (const bf16_t*)gamma, save_mean, save_invstd,
+    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 16), 1024, 0, stream>>>(
+        part, part + (size_t)2048 * C, nblk, M, C, (const bf16_t*)gamma, stat, stat + C,
         (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
-  bn_bwd_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)dy, (const bf16_t*)y,
-                                                       (const bf16_t*)x, coef, coef + C, coef + 2 * C,
-                                                       (bf16_t*)dx, (bf16_t*)dres, tv, C / 8, relu);
+  bn_bwd_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, coef, coef + C,
+                                                       coef + 2 * C, (bf16_t*)dx, (bf16_t*)dres, tv, C / 8);
   return 0;
 }

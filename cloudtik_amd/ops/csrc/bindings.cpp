@@ -3,6 +3,8 @@
 // kernel can fault the GPU), fetches the current HIP stream and calls the extern "C"
 // launcher.  No allocation happens inside the launchers; workspaces come from the caller.
 #include <torch/extension.h>
+#include <map>
+#include <mutex>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
@@ -39,8 +41,8 @@ int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, co
 int ct_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, float*,
                     float*, int, int, float, float, int, hipStream_t);
 int ct_bn_apply(const void*, const void*, const float*, const float*, void*, int, int, int, hipStream_t);
-int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, const float*, void*,
-              void*, void*, void*, int, float*, float*, int, int, int, hipStream_t);
+int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, void*, void*, void*, void*, int,
+              float*, float*, int, int, int, hipStream_t);
 int ct_attn_fwd(const void*, const long*, const void*, const long*, const void*, const long*, void*,
                 const long*, const float*, long, float*, int, int, int, int, float, float, uint64_t,
                 uint64_t, int, hipStream_t);
@@ -419,26 +421,26 @@ static void check_nhwc(const at::Tensor& x, const char* name) {
 }
 static int64_t nhwc_rows(const at::Tensor& x) { return x.numel() / x.size(1); }
 
-// returns (y, save_mean, save_invstd)
+// returns (y, stat) with stat = float[4C]: save_mean, save_invstd, a, b (y = x * a + b ...)
 std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma,
                                      at::Tensor beta, at::Tensor run_mean, at::Tensor run_var,
                                      double eps, double momentum, bool relu) {
   check_nhwc(x, "x");
   const int C = x.size(1);
   const long M = nhwc_rows(x);
+  TORCH_CHECK(C <= 2048, "bn_fwd_train: C <= 2048");
   if (res.has_value() && res->defined()) { check_nhwc(*res, "residual"); TORCH_CHECK(res->sizes() == x.sizes()); }
   TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
   CHECK_F32(run_mean); CHECK_F32(run_var);
   auto y = at::empty_like(x);
-  auto fo = x.options().dtype(at::kFloat);
-  auto part = at::empty({2 * 1024 * (long)C}, fo);
-  auto stat = at::empty({4 * (long)C}, fo);
+  auto stat = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
+  auto part = at::empty({2 * 2048 * (long)C}, x.options().dtype(at::kFloat));
   int rc = ct_bn_fwd_train(x.data_ptr(), optr(res), gamma.data_ptr(), beta.data_ptr(),
                            run_mean.data_ptr<float>(), run_var.data_ptr<float>(), y.data_ptr(),
                            part.data_ptr<float>(), stat.data_ptr<float>(), (int)M, C, (float)eps,
                            (float)momentum, relu ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "bn_fwd_train: unsupported C=", C);
-  return {y, stat.narrow(0, 0, C), stat.narrow(0, C, C)};
+  return {y, stat};
 }
 
 at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, at::Tensor b, bool relu) {
@@ -452,15 +454,25 @@ at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, a
   return y;
 }
 
-// returns (dx, dres, dgamma, dbeta)
-std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor gamma,
-                               at::Tensor save_mean, at::Tensor save_invstd, bool relu, bool need_dres,
+// returns (dx, dres, dgamma, dbeta).  relu_mode: 0 no ReLU, 1 mask from y (forward had a
+// residual), 2 mask recomputed from x and the forward's (a, b) -- y may be undefined then.
+std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor gamma,
+                               at::Tensor stat, int64_t relu_mode, bool need_dres,
                                c10::optional<at::Tensor> dgamma_acc, c10::optional<at::Tensor> dbeta_acc) {
   check_nhwc(x, "x");
   at::Tensor dyc = dy.dim() == 4 ? dy.contiguous(at::MemoryFormat::ChannelsLast) : dy.contiguous();
-  check_nhwc(dyc, "dy"); check_nhwc(y, "y");
+  check_nhwc(dyc, "dy");
   const int C = x.size(1);
   const long M = nhwc_rows(x);
+  TORCH_CHECK(C <= 2048 && stat.numel() == 4 * (long)C, "bn_bwd: stat must be float[4C], C <= 2048");
+  CHECK_F32(stat);
+  TORCH_CHECK(relu_mode >= 0 && relu_mode <= 2, "bn_bwd: relu_mode 0/1/2");
+  if (relu_mode == 1) {
+    TORCH_CHECK(y.has_value() && y->defined(), "bn_bwd: relu_mode 1 needs y");
+    check_nhwc(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes(), "bn_bwd: y shape");
+  }
+  TORCH_CHECK(dyc.sizes() == x.sizes(), "bn_bwd: dy shape");
   auto dx = at::empty_like(x);
   at::Tensor dres = need_dres ? at::empty_like(x) : at::Tensor();
   // optional accumulate targets (flat gradient buffer views): both or neither
@@ -472,14 +484,13 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Te
                 dbeta_acc->scalar_type() == gamma.scalar_type(), "bn_bwd: bad accumulate targets");
   }
   auto dgamma = acc ? *dgamma_acc : at::empty_like(gamma), dbeta = acc ? *dbeta_acc : at::empty_like(gamma);
-  auto fo = x.options().dtype(at::kFloat);
-  auto part = at::empty({2 * 1024 * (long)C}, fo);
-  auto coef = at::empty({3 * (long)C}, fo);
-  int rc = ct_bn_bwd(dyc.data_ptr(), y.data_ptr(), x.data_ptr(), gamma.data_ptr(),
-                     save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr(),
-                     need_dres ? dres.data_ptr() : nullptr, dgamma.data_ptr(), dbeta.data_ptr(),
+  auto coef = at::empty({3 * (long)C}, x.options().dtype(at::kFloat));
+  auto part = at::empty({2 * 2048 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_bwd(dyc.data_ptr(), relu_mode == 1 ? y->data_ptr() : nullptr, x.data_ptr(), gamma.data_ptr(),
+                     stat.data_ptr<float>(), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
+                     dgamma.data_ptr(), dbeta.data_ptr(),
                      (gamma.scalar_type() == at::kFloat ? 1 : 0) | (acc ? 2 : 0), part.data_ptr<float>(),
-                     coef.data_ptr<float>(), (int)M, C, relu ? 1 : 0, cur_stream());
+                     coef.data_ptr<float>(), (int)M, C, (int)relu_mode, cur_stream());
   TORCH_CHECK(rc == 0, "bn_bwd: unsupported C=", C);
   return {dx, dres, dgamma, dbeta};
 }

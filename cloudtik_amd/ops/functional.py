@@ -190,28 +190,32 @@ def cross_entropy_fused(x, W, b, labels, V=None, ignore_index=-100, label_smooth
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, run_mean, run_var, relu, momentum, eps):
-        y, mean, invstd = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu)
-        ctx.save_for_backward(x, y, gamma, mean, invstd)
+        y, stat = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu)
+        has_res = residual is not None
+        # ReLU mask for the backward: without a residual it is recomputed from x and the
+        # forward's affine coefficients (stat), so y is neither saved nor re-read
+        mode = 0 if not relu else (1 if has_res else 2)
+        ctx.save_for_backward(x, y if mode == 1 else None, gamma, stat)
         ctx.params = (gamma, beta)
-        ctx.cfg = (relu, residual is not None)
+        ctx.cfg = (mode, has_res)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, gamma, mean, invstd = ctx.saved_tensors
-        relu, has_res = ctx.cfg
+        x, y, gamma, stat = ctx.saved_tensors
+        mode, has_res = ctx.cfg
         wp, bp = ctx.params
         flat = all(p is not None and p.grad is not None and getattr(p, "_ct_flat_grad", False)
                    and p.grad.is_contiguous() and p.grad.dtype == gamma.dtype for p in (wp, bp))
         if flat:
             # accumulate straight into the flat gradient buffer (no AccumulateGrad kernels)
-            dx, dres, _, _ = _C().bn_bwd(dy, y, x, gamma, mean, invstd, relu, has_res, wp.grad, bp.grad)
+            dx, dres, _, _ = _C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, wp.grad, bp.grad)
             for p in (wp, bp):
                 cb = getattr(p, "_ct_grad_ready", None)
                 if cb is not None:
                     cb(p)
             return dx, None, None, (dres if has_res else None), None, None, None, None, None
-        dx, dres, dg, db = _C().bn_bwd(dy, y, x, gamma, mean, invstd, relu, has_res, None, None)
+        dx, dres, dg, db = _C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, None, None)
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None
 
 

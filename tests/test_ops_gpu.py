@@ -328,3 +328,30 @@ def test_optimizer_step_scalars_under_cpu_run_ahead(cuda, name):
             u = u * (w.norm() / u.norm())
         w = w - lr * u
     assert _rel(p.detach().double().cpu(), w) < 1e-5
+
+
+@pytest.mark.parametrize("C", [64, 1024])
+def test_batchnorm_repeat_and_relu_modes(cuda, C):
+    """Back-to-back calls of different sizes are independent (same input -> same output), and
+    the no-residual backward (ReLU mask recomputed from x and the forward's affine
+    coefficients) matches the backward that reads the mask from y, bit for bit."""
+    torch.manual_seed(1)
+    C_ = ops.require_native()
+    xa, xb = [(torch.randn(n, C, 7, 7, device=cuda) * 1.5 + 0.3).bfloat16().contiguous(
+        memory_format=torch.channels_last) for n in (4, 16)]
+    xs = [xa, xb, xa]
+    g = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
+    b = (0.1 * torch.randn(C, device=cuda)).bfloat16()
+    outs = []
+    for x in xs:
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        y, stat = C_.bn_fwd_train(x, None, g, b, rm, rv, 1e-5, 0.1, True)
+        dy = torch.randn_like(y, generator=None)
+        d2 = C_.bn_bwd(dy, None, x, g, stat, 2, False, None, None)
+        d1 = C_.bn_bwd(dy, y, x, g, stat, 1, False, None, None)
+        assert torch.equal(d1[0], d2[0]) and torch.equal(d1[2], d2[2]) and torch.equal(d1[3], d2[3])
+        outs.append((y, stat, rm.clone()))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1])
+    ref_mean = xs[1].float().mean(dim=(0, 2, 3))
+    assert _rel(outs[1][1][:C], ref_mean) < 1e-4
