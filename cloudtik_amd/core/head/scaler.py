@@ -152,7 +152,24 @@ class ClusterScaler:
         if self.state is None:
             return {}
         from cloudtik_amd.core.state.state_client import NODE_METRICS_TABLE
-        return self.state.table_get_all(NODE_METRICS_TABLE)
+        rows = self.state.table_get_all(NODE_METRICS_TABLE)
+        # tag each row with its node type (scaling-by-node-type routes metrics by it)
+        types = {}
+        try:
+            for n in self.workers():
+                t = self.provider.node_tags(n).get(T.CLOUDTIK_TAG_USER_NODE_TYPE)
+                types[n] = t
+                ip = self.provider.internal_ip(n)
+                if ip:
+                    types[ip] = t
+        except Exception:  # noqa: BLE001 - metrics stay usable without types
+            return rows
+        for nid, row in rows.items():
+            if isinstance(row, dict) and "node_type" not in row:
+                t = types.get(nid) or types.get(row.get("node_ip") or row.get("ip"))
+                if t:
+                    row["node_type"] = t
+        return rows
 
     # ------------------------------------------------------------------ round
     def reset_config(self, config: Dict[str, Any]):

@@ -10,7 +10,11 @@ A policy turns node metrics into resource *requests* the scaler packs against th
   ``scaling_step`` more worker nodes' worth of resources;
 * ``scaling-with-time``: a daily / weekly / monthly table of worker counts
   (``"09:00": 4``, ``"Mon 18:00": "+2"``, ``"20:00": "*0.5"``) relative to min_workers or the
-  previous entry.
+  previous entry;
+* ``scaling-by-node-type`` (reference scaling_policies.py:595): ``scaling_policy_by_node_type``
+  maps worker node types to their own load / time policy and scaling parameters (e.g. CPU
+  ETL nodes scale with load, MI355X GPU nodes on a time table); each sees only the metrics of
+  its own nodes and requests bundles of its own type, and the requests are concatenated.
 
 Configured under ``runtime.scaling`` (``scaling_policy: scaling-with-load`` ...).
 """
@@ -25,6 +29,7 @@ from cloudtik_amd.core.provider_api import ScalingPolicy, ScalingState
 SCALING_WITH_RESOURCES = "scaling-with-resources"
 SCALING_WITH_LOAD = "scaling-with-load"
 SCALING_WITH_TIME = "scaling-with-time"
+SCALING_BY_NODE_TYPE = "scaling-by-node-type"
 
 WEEKDAYS = ["mon", "tue", "wed", "thu", "fri", "sat", "sun"]
 
@@ -40,9 +45,12 @@ def _node_bundle(config, node_type) -> Dict[str, float]:
 
 
 class ScalingWithResources(ScalingPolicy):
-    def __init__(self, config: Dict[str, Any], head_ip: str, metrics_source=None):
+    def __init__(self, config: Dict[str, Any], head_ip: str, metrics_source=None, node_type: Optional[str] = None,
+                 scaling_config: Optional[Dict[str, Any]] = None):
         super().__init__(config, head_ip)
         self.metrics_source = metrics_source        # callable -> {node_id: metrics row}
+        self.node_type = node_type                  # scale only this worker type (by-node-type)
+        self._scaling_override = scaling_config
         self.reset(config)
 
     def name(self) -> str:
@@ -50,7 +58,11 @@ class ScalingWithResources(ScalingPolicy):
 
     def reset(self, config):
         self.config = config
-        self.scaling_config = (config.get("runtime", {}).get("scaling") or {})
+        self.scaling_config = self._scaling_override if self._scaling_override is not None \
+            else (config.get("runtime", {}).get("scaling") or {})
+
+    def _wtype(self) -> Optional[str]:
+        return self.node_type or _worker_type(self.config)
 
     def _metrics(self) -> Dict[str, Dict[str, Any]]:
         return self.metrics_source() if self.metrics_source else {}
@@ -109,7 +121,7 @@ class ScalingWithLoad(ScalingWithResources):
               (res == "GPU" and u["gpu"] > self.gpu_threshold)
         if not hot:
             return []
-        wt = _worker_type(self.config)
+        wt = self._wtype()
         if wt is None:
             return []
         bundle = _node_bundle(self.config, wt)
@@ -142,7 +154,7 @@ class ScalingWithTime(ScalingWithResources):
         return {"daily": 86400, "weekly": 7 * 86400, "monthly": 31 * 86400}[self.periodic]
 
     def _min_workers(self) -> int:
-        wt = _worker_type(self.config)
+        wt = self._wtype()
         return int(self.config["available_node_types"].get(wt, {}).get("min_workers", 0)) if wt else 0
 
     def _expand(self, table: Dict[str, Any]) -> List:
@@ -181,14 +193,59 @@ class ScalingWithTime(ScalingWithResources):
 
     def requests(self, metrics) -> List[Dict[str, float]]:
         n = self.nodes_at()
-        wt = _worker_type(self.config)
+        wt = self._wtype()
         if n is None or wt is None:
             return []
         return [_node_bundle(self.config, wt) for _ in range(n)]
 
 
+class ScalingByNodeType(ScalingWithResources):
+    """One sub-policy per worker node type; metrics rows are routed by their ``node_type``
+    and rows of other types are still reported as node resource states."""
+
+    def __init__(self, config, head_ip, metrics_source=None, policies: Optional[Dict[str, ScalingPolicy]] = None):
+        self.policies = dict(policies or {})
+        super().__init__(config, head_ip, metrics_source)
+
+    def name(self) -> str:
+        return SCALING_BY_NODE_TYPE
+
+    def reset(self, config):
+        super().reset(config)
+        for p in getattr(self, "policies", {}).values():
+            p.reset(config)
+
+    def get_scaling_state(self) -> Optional[ScalingState]:
+        metrics = self._metrics()
+        by_type: Dict[str, Dict[str, Any]] = {t: {} for t in self.policies}
+        other = {}
+        for nid, row in metrics.items():
+            t = row.get("node_type")
+            (by_type[t] if t in by_type else other)[nid] = row
+        requests: List[Dict[str, float]] = []
+        states = self.node_resource_states(other)
+        for t, p in self.policies.items():
+            requests += p.requests(by_type[t])
+            states.update(p.node_resource_states(by_type[t]))
+        return ScalingState(autoscaling_instructions={"resource_requests": requests, "time": time.time()},
+                            node_resource_states=states)
+
+
 POLICIES = {SCALING_WITH_RESOURCES: ScalingWithResources, SCALING_WITH_LOAD: ScalingWithLoad,
             SCALING_WITH_TIME: ScalingWithTime}
+
+
+def _by_node_type(config, head_ip, metrics_source, table) -> Optional[ScalingPolicy]:
+    types = config.get("available_node_types") or {}
+    policies = {}
+    for t, sc in (table or {}).items():
+        if t == config.get("head_node_type") or t not in types or not sc:
+            continue
+        name = sc.get("scaling_policy")
+        if name not in (SCALING_WITH_LOAD, SCALING_WITH_TIME):
+            raise ValueError(f"node type {t}: scaling_policy must be {SCALING_WITH_LOAD} or {SCALING_WITH_TIME}")
+        policies[t] = POLICIES[name](config, head_ip, metrics_source, node_type=t, scaling_config=sc)
+    return ScalingByNodeType(config, head_ip, metrics_source, policies) if policies else None
 
 
 def create_scaling_policy(config: Dict[str, Any], head_ip: str, metrics_source=None) -> Optional[ScalingPolicy]:
@@ -199,7 +256,10 @@ def create_scaling_policy(config: Dict[str, Any], head_ip: str, metrics_source=N
         p = rf.get_runtime(t, config.get("runtime", {}).get(t, {}) or {}).get_scaling_policy(config, head_ip)
         if p is not None:
             return p
-    name = (config.get("runtime", {}).get("scaling") or {}).get("scaling_policy")
+    scaling = config.get("runtime", {}).get("scaling") or {}
+    if scaling.get("scaling_policy_by_node_type"):
+        return _by_node_type(config, head_ip, metrics_source, scaling["scaling_policy_by_node_type"])
+    name = scaling.get("scaling_policy")
     if not name:
         return None
     if name not in POLICIES:

@@ -11,6 +11,12 @@ BUILT_IN_RUNTIME_NONE = "none"
 
 _CUSTOM = {
     "ai": ("cloudtik_amd.runtime.ai.runtime", "AIRuntime"),
+    # self-configuring Hadoop family: conf files rendered per node, executor sizing, YARN
+    # scaling policy / job waiter (cloudtik_amd/runtime/hadoop)
+    "hadoop": ("cloudtik_amd.runtime.hadoop.runtimes", "HadoopRuntime"),
+    "hdfs": ("cloudtik_amd.runtime.hadoop.runtimes", "HdfsRuntime"),
+    "yarn": ("cloudtik_amd.runtime.hadoop.runtimes", "YarnRuntime"),
+    "spark": ("cloudtik_amd.runtime.hadoop.runtimes", "SparkRuntime"),
 }
 
 

@@ -278,3 +278,28 @@ def test_gpu_ras_health_from_sysfs(tmp_path):
     (card / "ras" / "xgmi_wafl_err_count").write_text("ue: 1\nce: 0\n")
     (g,) = gpu_metrics(str(tmp_path))
     assert not g["healthy"] and "xgmi_wafl" in g["health_issues"][0]
+
+
+def test_scaling_by_node_type_routes_metrics_and_bundles():
+    """scaling-by-node-type (reference scaling_policies.py:595): CPU workers scale with load,
+    GPU workers follow a time table; each requests bundles of its own type."""
+    from cloudtik_amd.core.head.scaling_policies import ScalingByNodeType, create_scaling_policy
+    cfg = {"head_node_type": "head",
+           "available_node_types": {
+               "head": {"resources": {"CPU": 8}},
+               "cpu": {"min_workers": 1, "resources": {"CPU": 64, "memory": 256}},
+               "gpu": {"min_workers": 0, "resources": {"CPU": 128, "GPU": 8}}},
+           "runtime": {"scaling": {"scaling_policy_by_node_type": {
+               "cpu": {"scaling_policy": "scaling-with-load", "scaling_resource": "CPU", "cpu_load_threshold": 0.5},
+               "gpu": {"scaling_policy": "scaling-with-time", "scaling_time_table": {"00:00": 2}},
+               "head": {"scaling_policy": "scaling-with-load"}}}}}
+    metrics = {"n1": {"node_type": "cpu", "cpu_count": 64, "load_avg": [60.0], "resources": {"CPU": 64}},
+               "n2": {"node_type": "gpu", "cpu_count": 128, "load_avg": [1.0], "resources": {"CPU": 128, "GPU": 8}},
+               "n3": {"cpu_count": 8, "load_avg": [0.1]}}
+    p = create_scaling_policy(cfg, "10.0.0.1", metrics_source=lambda: metrics)
+    assert isinstance(p, ScalingByNodeType) and set(p.policies) == {"cpu", "gpu"}
+    st = p.get_scaling_state()
+    reqs = st.autoscaling_instructions["resource_requests"]
+    assert sum(1 for r in reqs if r.get("GPU") == 8) == 2               # time table: 2 GPU nodes
+    assert sum(1 for r in reqs if r.get("CPU") == 64 and "GPU" not in r) == 1   # load 0.94 > 0.5: +1 step
+    assert set(st.node_resource_states) == {"n1", "n2", "n3"}
