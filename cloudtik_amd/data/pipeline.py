@@ -6,10 +6,11 @@ read it back through Petastorm).
 * ``write_image_shards``  -- the ETL side: image rows (uint8 HWC + label) written as Parquet
   part files, by Spark when pyspark is installed (one task per part) and by a process pool
   of pyarrow writers otherwise; paths may be local or ``hdfs://`` / object-store URLs.
-* ``ParquetImageLoader``  -- the training side: each rank reads its own part files,
-  the native loader stages uint8 batches in pinned host memory and copies them with
-  hipMemcpyAsync on a side stream, and one HIP pass (``ops.images_to_tensor``) turns them
-  into normalised, optionally flipped bf16 channels-last tensors on the GPU.
+* ``ParquetImageLoader``  -- the training side: each rank streams its own part files row
+  group by row group with bounded host memory (data/streaming.py), stages uint8 batches in
+  pinned host slots and copies them on a side stream, and one HIP pass
+  (``ops.images_to_tensor``) turns them into normalised, optionally flipped bf16
+  channels-last tensors on the GPU.
 """
 from __future__ import annotations
 
@@ -67,30 +68,57 @@ def rank_parts(root: str, rank: int, world: int) -> List[str]:
 
 
 class ParquetImageLoader:
+    """Batches of (normalised bf16 NHWC images, labels) from a rank's Parquet part files.
+
+    ``streaming=True`` (default): row groups are decoded on the fly with bounded host memory
+    (data/streaming.py), staged through pinned slots and copied on a side stream.
+    ``streaming=False``: the rank's parts are loaded once into host memory and served by the
+    native prefetching loader (small datasets, repeated epochs without re-reading)."""
+
     def __init__(self, paths: Sequence[str], batch_size: int, image_size: int = 224, shuffle: bool = True,
                  seed: int = 0, flip_prob: float = 0.5, num_workers: int = 4, prefetch: int = 4,
-                 mean=None, std=None, device=None):
-        from cloudtik_amd.data.loader import NativeLoader
-        from cloudtik_amd.data.parquet import read_parquet_columns
+                 mean=None, std=None, device=None, streaming: bool = True, window: int = 4, read_ahead: int = 2):
         from cloudtik_amd.ops.vision import IMAGENET_MEAN, IMAGENET_STD
-        cols = read_parquet_columns(list(paths), ["image", "label"], shapes={"image": (image_size, image_size, 3)})
-        self.num_rows = len(cols["label"])
-        # equal-size batches on every rank keep the collectives in lockstep
-        self.loader = NativeLoader(cols, batch_size, shuffle=shuffle, seed=seed, drop_last=True,
-                                   num_workers=num_workers, prefetch=prefetch, device=device)
+        self.streaming = streaming
+        shapes = {"image": (image_size, image_size, 3)}
+        if streaming:
+            from cloudtik_amd.data.streaming import ParquetRowGroupStream, PinnedStager, agree_min_batches
+            self.stream = ParquetRowGroupStream(paths, batch_size, ["image", "label"], shapes, shuffle=shuffle,
+                                                seed=seed, window=window, read_ahead=read_ahead,
+                                                num_workers=num_workers, drop_last=True)
+            self.stream.max_batches = agree_min_batches(len(self.stream))
+            self.num_rows = self.stream.num_rows
+            dev = torch.device(device) if device is not None else (
+                torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+            self.stager = PinnedStager(dev, prefetch)
+        else:
+            from cloudtik_amd.data.loader import NativeLoader
+            from cloudtik_amd.data.parquet import read_parquet_columns
+            cols = read_parquet_columns(list(paths), ["image", "label"], shapes=shapes)
+            self.num_rows = len(cols["label"])
+            # equal-size batches on every rank keep the collectives in lockstep
+            self.loader = NativeLoader(cols, batch_size, shuffle=shuffle, seed=seed, drop_last=True,
+                                       num_workers=num_workers, prefetch=prefetch, device=device)
         self.flip_prob = flip_prob
         self.mean, self.std = mean or IMAGENET_MEAN, std or IMAGENET_STD
         self.gen = torch.Generator(device="cpu").manual_seed(seed + 17)
 
     def __len__(self) -> int:
-        return len(self.loader)
+        return len(self.stream) if self.streaming else len(self.loader)
 
     def set_epoch(self, epoch: int):
-        self.loader.set_epoch(epoch)
+        (self.stream if self.streaming else self.loader).set_epoch(epoch)
+
+    def _batches(self):
+        if not self.streaming:
+            yield from self.loader
+            return
+        for b in self.stream:
+            yield self.stager(b)
 
     def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
         from cloudtik_amd import ops
-        for b in self.loader:
+        for b in self._batches():
             imgs = b["image"]
             flip = None
             if self.flip_prob > 0:
@@ -99,4 +127,5 @@ class ParquetImageLoader:
             yield ops.images_to_tensor(imgs, flip, self.mean, self.std), b["label"]
 
     def close(self):
-        self.loader.close()
+        if not self.streaming:
+            self.loader.close()

@@ -9,8 +9,9 @@ ResNet-50 trains from it with the pinned-memory hipMemcpyAsync loader, one rank 
 Stage 1 (rank 0, skipped when the part files exist): Spark (if pyspark is installed) or a
 pyarrow process pool writes ``--parts`` Parquet files of uint8 224x224x3 images + labels
 (synthetic content; no dataset can be downloaded here).  Stage 2: every rank reads its own
-part files (ParquetImageLoader: native pinned loader -> side-stream async H2D of uint8 ->
-fused normalise/flip kernel -> bf16 channels-last), and trains ResNet-50 with fused SGD
+part files (ParquetImageLoader: row groups streamed with bounded host memory -> pinned
+slots -> side-stream async H2D of uint8 -> fused normalise/flip kernel -> bf16
+channels-last; ``--resident`` loads the parts into RAM for the native loader instead), and trains ResNet-50 with fused SGD
 and bucketed RCCL all-reduce.  Prints one JSON line with images/s of the whole job and the
 pipeline efficiency (throughput relative to the same steps on one GPU-resident batch).
 """
@@ -37,6 +38,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "small"])
     ap.add_argument("--etl-engine", default="auto", choices=["auto", "spark", "pyarrow"])
+    ap.add_argument("--resident", action="store_true",
+                    help="load the rank's parts into host RAM first (default: stream row groups)")
+    ap.add_argument("--window", type=int, default=4, help="streaming shuffle window (row groups)")
+    ap.add_argument("--workers", type=int, default=4, help="row-group decode threads")
     args = ap.parse_args()
 
     from cloudtik_amd.data.pipeline import ParquetImageLoader, rank_parts, write_image_shards
@@ -59,7 +64,8 @@ def main():
         dist.barrier()
 
     loader = ParquetImageLoader(rank_parts(args.data_path, rank, world), args.batch_size, args.image_size,
-                                seed=rank, device=device)
+                                seed=rank, device=device, streaming=not args.resident, window=args.window,
+                                num_workers=args.workers)
     if args.model == "resnet50":
         model = resnet50(device=device, dtype=torch.bfloat16 if gpu else torch.float32)
     else:
@@ -113,7 +119,8 @@ def main():
                           "value": round(ips, 1) if ips else None, "resident_batch_images_per_sec": round(resident_ips, 1),
                           "pipeline_efficiency": round(ips / resident_ips, 4) if ips else None, "n_gpus": world,
                           "batch_per_gpu": args.batch_size, "etl_seconds": round(etl_s, 2), "rows": rows,
-                          "parts": parts, "final_loss": float(loss.detach()), "data": "synthetic parquet"}), flush=True)
+                          "parts": parts, "final_loss": float(loss.detach()), "data": "synthetic parquet",
+                          "loader": "resident" if args.resident else "streaming"}), flush=True)
     loader.close()
     if dist.is_initialized():
         dist.destroy_process_group()

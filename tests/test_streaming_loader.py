@@ -1,0 +1,100 @@
+"""Streaming Parquet -> batch loader (data/streaming.py): every row exactly once per epoch,
+epoch-dependent shuffling, equal batch counts, and host memory bounded by the row-group
+window -- not by the dataset size (the loader that first read every part file into RAM
+cannot work at ImageNet scale)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _write(root, parts=6, rows=100, rg=32):
+    from cloudtik_amd.data.parquet import write_parquet
+    ids = 0
+    for p in range(parts):
+        x = np.arange(ids, ids + rows, dtype=np.int64)
+        write_parquet(os.path.join(root, f"part-{p:05d}.parquet"),
+                      {"id": x, "feat": np.repeat(x[:, None], 4, 1).astype(np.float32)}, row_group_size=rg)
+        ids += rows
+    return ids
+
+
+def test_stream_covers_every_row_once_and_reshuffles(tmp_path):
+    from cloudtik_amd.data.streaming import ParquetRowGroupStream
+    n = _write(str(tmp_path))
+    s = ParquetRowGroupStream([str(tmp_path)], 16, ["id", "feat"], shuffle=True, seed=3, window=3, read_ahead=2,
+                              drop_last=False)
+    seen = [np.concatenate([b["id"] for b in s])]
+    assert sorted(seen[0].tolist()) == list(range(n))
+    for b in s:
+        assert (b["feat"][:, 0] == b["id"]).all()            # columns stay row-aligned
+    s.set_epoch(1)
+    e1 = np.concatenate([b["id"] for b in s])
+    assert sorted(e1.tolist()) == list(range(n)) and not np.array_equal(e1, seen[0])
+    s2 = ParquetRowGroupStream([str(tmp_path)], 16, ["id"], shuffle=True, seed=3, window=3, drop_last=True)
+    assert len(s2) == n // 16 and len(list(s2)) == n // 16 and all(len(b["id"]) == 16 for b in s2)
+
+
+def test_image_loader_streams_on_cpu(tmp_path):
+    from cloudtik_amd.data.pipeline import ParquetImageLoader, rank_parts, write_image_shards
+    write_image_shards(str(tmp_path), 160, 4, image_size=8, num_classes=5, workers=1)
+    ld = ParquetImageLoader(rank_parts(str(tmp_path), 0, 2), 16, image_size=8, device="cpu", window=2)
+    xs = list(ld)
+    assert len(xs) == len(ld) == 5
+    x, y = xs[0]
+    assert x.shape == (16, 3, 8, 8) and y.shape == (16,)
+
+
+_RSS_PROBE = r"""
+import json, sys, threading, time, os, psutil
+sys.path.insert(0, sys.argv[1])
+from cloudtik_amd.data.streaming import ParquetRowGroupStream
+proc = psutil.Process()
+peak = [0]
+stop = [False]
+def sample():
+    while not stop[0]:
+        peak[0] = max(peak[0], proc.memory_info().rss)
+        time.sleep(0.002)
+s = ParquetRowGroupStream([sys.argv[2]], 64, ["image", "label"], shapes={"image": (64, 64, 3)},
+                          window=2, read_ahead=2, num_workers=2)
+base = proc.memory_info().rss
+th = threading.Thread(target=sample); th.start()
+rows = 0
+for b in s:
+    rows += len(b["label"])
+stop[0] = True; th.join()
+print(json.dumps({"rows": rows, "delta_mb": (peak[0] - base) / 2**20}))
+"""
+
+
+def _rss_delta(root):
+    out = subprocess.run([sys.executable, "-c", _RSS_PROBE, REPO, str(root)], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_stream_host_memory_does_not_grow_with_dataset(tmp_path):
+    """Peak RSS growth while streaming a 4x larger dataset stays the same: the working set
+    is the row-group window (plus allocator retention), not the data.  (Measured: ~230 MB
+    of allocator/pool retention for both 48 MB and 192 MB of images; a reader that loads
+    everything first grows by the full dataset.)"""
+    from cloudtik_amd.data.parquet import write_parquet
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 255, (512, 64 * 64 * 3), dtype=np.uint8)     # 6 MiB per part
+    small, big = tmp_path / "small", tmp_path / "big"
+    for root, parts in ((small, 8), (big, 32)):
+        root.mkdir()
+        for p in range(parts):
+            write_parquet(str(root / f"part-{p:05d}.parquet"), {"image": img, "label": np.arange(512, dtype=np.int64)},
+                          row_group_size=128)
+    a, b = _rss_delta(small), _rss_delta(big)
+    assert a["rows"] == 8 * 512 and b["rows"] == 32 * 512
+    # 4x the data (+144 MiB): the peak may not grow by more than a fraction of that
+    assert b["delta_mb"] < a["delta_mb"] + 48, (a, b)
