@@ -82,7 +82,7 @@ class ParquetImageLoader:
         self.streaming = streaming
         shapes = {"image": (image_size, image_size, 3)}
         if streaming:
-            from cloudtik_amd.data.streaming import ParquetRowGroupStream, PinnedStager, agree_min_batches
+            from cloudtik_amd.data.streaming import ParquetRowGroupStream, PinnedBatchLoader, agree_min_batches
             self.stream = ParquetRowGroupStream(paths, batch_size, ["image", "label"], shapes, shuffle=shuffle,
                                                 seed=seed, window=window, read_ahead=read_ahead,
                                                 num_workers=num_workers, drop_last=True)
@@ -90,7 +90,7 @@ class ParquetImageLoader:
             self.num_rows = self.stream.num_rows
             dev = torch.device(device) if device is not None else (
                 torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
-            self.stager = PinnedStager(dev, prefetch)
+            self.pinned = PinnedBatchLoader(self.stream, dev, prefetch)
         else:
             from cloudtik_amd.data.loader import NativeLoader
             from cloudtik_amd.data.parquet import read_parquet_columns
@@ -113,8 +113,7 @@ class ParquetImageLoader:
         if not self.streaming:
             yield from self.loader
             return
-        for b in self.stream:
-            yield self.stager(b)
+        yield from self.pinned
 
     def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
         from cloudtik_amd import ops

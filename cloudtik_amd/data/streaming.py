@@ -9,9 +9,10 @@ nothing is loaded up front.  Per epoch:
   in flight (pyarrow releases the GIL while decoding);
 * decoded row groups enter a shuffle pool of ``window`` row groups; full batches are drawn
   from a random permutation of the pool and the remainder carries over;
-* each batch is copied into one of ``prefetch`` pinned host slots and sent to the GPU with a
-  non-blocking copy on a side stream; a slot is rewritten only after the event recorded
-  behind its previous copy has completed.
+* a background producer gathers each batch's rows straight from the decoded row groups
+  into one of ``prefetch`` pinned host slots (one copy per byte, no pool concatenation);
+  the consumer sends the slot to the GPU with a non-blocking copy on a side stream, and a
+  slot is rewritten only after the event recorded behind its previous copy has completed.
 
 Host memory is therefore bounded by ``(window + read_ahead) x row-group bytes + prefetch x
 batch bytes`` whatever the dataset size.  Every rank yields the same number of batches per
@@ -83,8 +84,7 @@ class ParquetRowGroupStream:
             f.close()
         out = {}
         for name in self.columns:
-            # own copies: numpy views would pin the Arrow buffers until the pool drains
-            a = np.array(_column_to_numpy(t.column(name)), copy=True)
+            a = _column_to_numpy(t.column(name))
             if name in self.shapes:
                 a = a.reshape((a.shape[0],) + tuple(self.shapes[name]))
             out[name] = a
@@ -92,93 +92,175 @@ class ParquetRowGroupStream:
         return out
 
     def __iter__(self) -> Iterator[Dict[str, np.ndarray]]:
+        return self.iter_into(None)
+
+    def iter_into(self, alloc=None) -> Iterator[Dict[str, np.ndarray]]:
+        """Yield batches; ``alloc(B, like)`` may supply the output arrays (e.g. pinned host
+        slots) -- rows are gathered straight from the decoded row groups into them, grouped
+        by row group (order inside a batch carries no meaning), one copy per byte."""
         rng = np.random.default_rng(self.seed + 7919 * self.epoch)
         order = list(range(len(self.units)))
         if self.shuffle:
             rng.shuffle(order)
         limit = len(self)
         emitted = 0
-        pool: List[Dict[str, np.ndarray]] = []
-        pool_rows = 0
         B = self.batch_size
+        pool: Dict[int, Dict[str, np.ndarray]] = {}
+        carry_rg = np.empty(0, np.int64)
+        carry_row = np.empty(0, np.int64)
+        new_rg: List[np.ndarray] = []
+        new_row: List[np.ndarray] = []
+        uid = 0
+
+        def gather(rg_ids, rows, n_out):
+            srt = np.argsort(rg_ids, kind="stable")
+            rg_ids, rows = rg_ids[srt], rows[srt]
+            cuts = np.flatnonzero(np.diff(rg_ids)) + 1
+            starts = np.concatenate([[0], cuts])
+            ends = np.concatenate([cuts, [n_out]])
+            like = pool[int(rg_ids[0])]
+            out = alloc(n_out, like) if alloc is not None else \
+                {c: np.empty((n_out,) + like[c].shape[1:], like[c].dtype) for c in self.columns}
+            for s0, e0 in zip(starts, ends):
+                src = pool[int(rg_ids[s0])]
+                for c in self.columns:
+                    np.take(src[c], rows[s0:e0], axis=0, out=out[c][s0:e0])
+            return out
+
         with ThreadPoolExecutor(self.num_workers) as ex:
             pending = collections.deque()
             it = iter(order)
 
             def refill():
                 while len(pending) < self.read_ahead:
-                    i = next(it, None)
-                    if i is None:
+                    k = next(it, None)
+                    if k is None:
                         return
-                    pending.append(ex.submit(self._read, self.units[i]))
+                    pending.append(ex.submit(self._read, self.units[k]))
             refill()
             while True:
                 exhausted = not pending
                 if not exhausted:
-                    rg = pending.popleft().result()
+                    arrays = pending.popleft().result()
                     refill()
-                    pool.append(rg)
-                    pool_rows += len(rg[self.columns[0]])
-                    if len(pool) < self.window:
+                    n = len(arrays[self.columns[0]])
+                    pool[uid] = arrays
+                    new_rg.append(np.full(n, uid, np.int64))
+                    new_row.append(np.arange(n, dtype=np.int64))
+                    uid += 1
+                    if len(new_rg) < self.window:
                         continue                      # keep filling the shuffle window
-                elif not pool_rows:
+                rg_ids = np.concatenate([carry_rg] + new_rg)
+                rows = np.concatenate([carry_row] + new_row)
+                new_rg, new_row = [], []
+                if not len(rg_ids):
                     return
-                merged = {n: np.concatenate([r[n] for r in pool]) if len(pool) > 1 else pool[0][n]
-                          for n in self.columns}
-                perm = rng.permutation(pool_rows) if self.shuffle else np.arange(pool_rows)
-                nb = pool_rows // B
+                if self.shuffle:
+                    perm = rng.permutation(len(rg_ids))
+                    rg_ids, rows = rg_ids[perm], rows[perm]
+                nb = len(rg_ids) // B
                 for b in range(nb):
                     if emitted >= limit:
                         return
-                    idx = perm[b * B:(b + 1) * B]
-                    yield {n: merged[n][idx] for n in self.columns}
+                    yield gather(rg_ids[b * B:(b + 1) * B], rows[b * B:(b + 1) * B], B)
                     emitted += 1
-                rest = perm[nb * B:]
-                pool = [{n: merged[n][rest] for n in self.columns}] if len(rest) else []
-                pool_rows = len(rest)
-                del merged
+                carry_rg, carry_row = rg_ids[nb * B:], rows[nb * B:]
+                live = set(np.unique(carry_rg).tolist())
+                for k in [k for k in pool if k not in live]:
+                    del pool[k]                        # row group fully consumed
                 if exhausted:
-                    if pool_rows and not self.drop_last and emitted < limit:
-                        yield pool[0]
+                    if len(carry_rg) and not self.drop_last and emitted < limit:
+                        yield gather(carry_rg, carry_row, len(carry_rg))
                     return
 
 
-class PinnedStager:
-    """numpy batch -> pinned host slot -> device, asynchronously on a side stream."""
+class PinnedBatchLoader:
+    """Background producer: gathers each batch straight into one of ``prefetch`` pinned
+    host slots; the consumer issues the H2D copy on a side stream, records an event, and
+    the producer reuses the slot only once that event has completed."""
 
-    def __init__(self, device, prefetch: int = 4):
+    def __init__(self, stream: ParquetRowGroupStream, device, prefetch: int = 4):
+        self.stream = stream
         self.device = torch.device(device)
         self.on_gpu = self.device.type == "cuda"
         self.prefetch = max(2, prefetch)
         self.slots: List[Optional[Dict[str, torch.Tensor]]] = [None] * self.prefetch
-        self.events: List[Optional[torch.cuda.Event]] = [None] * self.prefetch
-        self.i = 0
-        self.stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
+        self.events: List[Optional[object]] = [None] * self.prefetch
+        self.copy_stream = torch.cuda.Stream(device=self.device) if self.on_gpu else None
 
-    def __call__(self, batch: Dict[str, np.ndarray]) -> Dict[str, torch.Tensor]:
-        if not self.on_gpu:
-            return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in batch.items()}
-        i = self.i = (self.i + 1) % self.prefetch
-        ev = self.events[i]
-        if ev is not None:
-            ev.synchronize()                   # the copy that last read this slot has finished
+    def __len__(self):
+        return len(self.stream)
+
+    def _slot(self, i, B, like):
         slot = self.slots[i]
-        if slot is None or any(slot[k].shape != v.shape or slot[k].dtype != torch.from_numpy(v[:0]).dtype
-                               for k, v in batch.items()):
-            slot = self.slots[i] = {k: torch.empty(v.shape, dtype=torch.from_numpy(v[:0]).dtype, pin_memory=True)
-                                    for k, v in batch.items()}
-        for k, v in batch.items():
-            slot[k].numpy()[...] = v
-        cur = torch.cuda.current_stream(self.device)
-        with torch.cuda.stream(self.stream):
-            out = {k: t.to(self.device, non_blocking=True) for k, t in slot.items()}
-            if ev is None:
-                ev = self.events[i] = torch.cuda.Event()
-            ev.record(self.stream)
-        cur.wait_stream(self.stream)
-        for t in out.values():
-            t.record_stream(cur)
-        return out
+        if slot is None or slot[self.stream.columns[0]].shape[0] != B:
+            slot = self.slots[i] = {c: torch.empty((B,) + like[c].shape[1:],
+                                                   dtype=torch.from_numpy(like[c][:0]).dtype,
+                                                   pin_memory=self.on_gpu)
+                                    for c in self.stream.columns}
+        return {c: t.numpy() for c, t in slot.items()}
+
+    def __iter__(self) -> Iterator[Dict[str, torch.Tensor]]:
+        import queue
+        import threading
+        ready: "queue.Queue" = queue.Queue()
+        free: "queue.Queue" = queue.Queue()
+        for i in range(self.prefetch):
+            free.put(i)
+        stop = threading.Event()
+        current = [None]
+
+        def alloc(B, like):
+            i = free.get()
+            while i is None:
+                i = free.get()
+            ev = self.events[i]
+            if ev is not None:
+                ev.synchronize()               # the H2D copy that last read this slot is done
+            current[0] = i
+            return self._slot(i, B, like)
+
+        def produce():
+            try:
+                for batch in self.stream.iter_into(alloc):
+                    if stop.is_set():
+                        return
+                    ready.put((current[0], batch))
+                ready.put(None)
+            except BaseException as e:  # noqa: BLE001 - surfaced in the consumer
+                ready.put(e)
+
+        th = threading.Thread(target=produce, daemon=True, name="parquet-batch-producer")
+        th.start()
+        try:
+            while True:
+                item = ready.get()
+                if item is None:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                i, batch = item
+                if not self.on_gpu:
+                    out = {c: torch.from_numpy(a.copy()) for c, a in batch.items()}
+                    free.put(i)
+                    yield out
+                    continue
+                cur = torch.cuda.current_stream(self.device)
+                with torch.cuda.stream(self.copy_stream):
+                    out = {c: self.slots[i][c].to(self.device, non_blocking=True) for c in batch}
+                    if self.events[i] is None:
+                        self.events[i] = torch.cuda.Event()
+                    self.events[i].record(self.copy_stream)
+                free.put(i)
+                cur.wait_stream(self.copy_stream)
+                for t in out.values():
+                    t.record_stream(cur)
+                yield out
+        finally:
+            stop.set()
+            for _ in range(self.prefetch):
+                free.put(None)                 # wake a producer blocked on a slot
+            th.join(timeout=30)
 
 
 def agree_min_batches(n: int) -> int:

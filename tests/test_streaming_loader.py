@@ -48,6 +48,10 @@ def test_image_loader_streams_on_cpu(tmp_path):
     assert len(xs) == len(ld) == 5
     x, y = xs[0]
     assert x.shape == (16, 3, 8, 8) and y.shape == (16,)
+    for i, _ in enumerate(ld):          # an early break stops the producer thread cleanly
+        if i == 1:
+            break
+    assert len(list(ld)) == 5
 
 
 _RSS_PROBE = r"""
