@@ -34,6 +34,11 @@ def _column_to_numpy(col) -> np.ndarray:
     import pyarrow as pa
     col = col.combine_chunks() if isinstance(col, pa.ChunkedArray) else col
     t = col.type
+    if pa.types.is_fixed_size_binary(t):
+        # raw row bytes (images): one memcpy-free view of the values buffer
+        w = t.byte_width
+        buf = col.buffers()[1]
+        return np.frombuffer(buf, dtype=np.uint8, count=(col.offset + len(col)) * w).reshape(-1, w)[col.offset:]
     if pa.types.is_fixed_size_list(t) or pa.types.is_list(t) or pa.types.is_large_list(t):
         values = col.flatten().to_numpy(zero_copy_only=False)
         n = len(col)
@@ -80,17 +85,28 @@ def write_parquet(path: str, columns: Dict[str, np.ndarray], row_group_size: int
     """Write numpy columns ([rows] or [rows, ...] -> fixed-size list) to one Parquet file."""
     import pyarrow as pa
     import pyarrow.parquet as pq
-    arrays, names = [], []
+    arrays, names, dict_cols = [], [], []
     for name, a in columns.items():
         a = np.ascontiguousarray(a)
         if a.ndim == 1:
             arrays.append(pa.array(a))
+            dict_cols.append(name)
+        elif a.dtype == np.uint8:
+            # uint8 tensors (images) as fixed-size binary rows: Parquet stores them as plain
+            # byte arrays, so reading is a copy, not a per-element level decode (~50x faster
+            # than a list<uint8> column for 224x224x3 images)
+            flat = a.reshape(a.shape[0], -1)
+            w = flat.shape[1]
+            arrays.append(pa.FixedSizeBinaryArray.from_buffers(pa.binary(w), len(flat),
+                                                               [None, pa.py_buffer(flat.reshape(-1))]))
         else:
             flat = a.reshape(a.shape[0], -1)
             arrays.append(pa.FixedSizeListArray.from_arrays(pa.array(flat.reshape(-1)), flat.shape[1]))
+            dict_cols.append(name)
         names.append(name)
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-    pq.write_table(pa.Table.from_arrays(arrays, names=names), path, row_group_size=row_group_size)
+    pq.write_table(pa.Table.from_arrays(arrays, names=names), path, row_group_size=row_group_size,
+                   use_dictionary=dict_cols)
 
 
 class ParquetDataLoader:
