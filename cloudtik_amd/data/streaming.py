@@ -195,7 +195,7 @@ class PinnedBatchLoader:
         slot = self.slots[i]
         if slot is None or slot[self.stream.columns[0]].shape[0] != B:
             slot = self.slots[i] = {c: torch.empty((B,) + like[c].shape[1:],
-                                                   dtype=torch.from_numpy(like[c][:0]).dtype,
+                                                   dtype=torch.from_numpy(np.empty(0, like[c].dtype)).dtype,
                                                    pin_memory=self.on_gpu)
                                     for c in self.stream.columns}
         return {c: t.numpy() for c, t in slot.items()}
