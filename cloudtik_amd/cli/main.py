@@ -172,6 +172,24 @@ def submit(cluster_config_file, script, script_args, node_ip, job_waiter, cluste
         _fail(str(e))
 
 
+@cli.command(context_settings={"ignore_unknown_options": True})
+@click.argument("cluster_config_file")
+@click.argument("script")
+@click.argument("script_args", nargs=-1, type=click.UNPROCESSED)
+@click.option("--node-ip", default=None)
+@click.option("--job-waiter", default=None, help="Run detached in tmux and wait with this waiter (e.g. yarn).")
+@_cluster_name
+def run(cluster_config_file, script, script_args, node_ip, job_waiter, cluster_name):
+    """Run a built-in script: a registered alias (e.g. ai.launch) or <runtime>/<script>.
+
+    Use exec / submit for your own commands and scripts."""
+    from cloudtik_amd.core import cluster_operator as op
+    try:
+        op.run_script(cluster_config_file, script, list(script_args), node_ip, job_waiter, cluster_name)
+    except Exception as e:  # noqa: BLE001
+        _fail(str(e))
+
+
 @cli.command()
 @click.argument("cluster_config_file")
 @click.option("--cpus", type=int, default=None)
@@ -426,6 +444,25 @@ def _register_groups():
     from cloudtik_amd.cli.head import head
     for g in (node, runtime, workspace, storage, database, head):
         cli.add_command(g)
+    _register_runtime_groups()
+
+
+def _register_runtime_groups():
+    """Runtime packages contribute command groups: ``cloudtik_amd.runtime.<name>.cli`` exposing
+    a click group called ``<name>`` becomes ``cloudtik <name> ...`` (reference scripts.py:66)."""
+    import importlib
+    import pkgutil
+    import cloudtik_amd.runtime as rt_pkg
+    for info in pkgutil.iter_modules(rt_pkg.__path__):
+        if not info.ispkg:
+            continue
+        try:
+            mod = importlib.import_module(f"{rt_pkg.__name__}.{info.name}.cli")
+        except ImportError:
+            continue
+        grp = getattr(mod, info.name, None)
+        if isinstance(grp, click.Group) and info.name not in cli.commands:
+            cli.add_command(grp)
 
 
 _register_groups()

@@ -196,6 +196,8 @@ def post_prepare(config: Dict[str, Any]) -> Dict[str, Any]:
 
 def validate_config(config: Dict[str, Any]) -> None:
     jschema.validate(config, load_schema("cluster"))
+    if config.get("runtime"):
+        jschema.validate(config["runtime"], load_schema("runtime"), path=["runtime"])
     nts = get_available_node_types(config)
     head = config.get("head_node_type")
     if head not in nts:

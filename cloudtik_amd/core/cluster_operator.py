@@ -602,3 +602,83 @@ def monitor_cluster(config_file, lines: int = 100, follow: bool = False, timeout
             out.flush()
     finally:
         ps.close()
+
+
+# ---------------------------------------------------------------------- built-in scripts / runtime services
+def get_cluster_metrics(config) -> Dict[str, Any]:
+    """Per-node resource metrics rows (alias of cluster_resource_metrics for the head CLI)."""
+    return cluster_resource_metrics(config)
+
+
+def _builtin_script_command(script: str, args: List[str]) -> str:
+    """A registered alias -> ``python -m module``; ``<runtime>/<file>.sh|.py`` -> the script
+    shipped in that runtime package on the node; anything else is not built in."""
+    from cloudtik_amd.core.script_registry import get_registered_script
+    qargs = " ".join(shlex.quote(a) for a in args)
+    module = get_registered_script(script)
+    if module:
+        return f"${{CLOUDTIK_PYTHON:-python3}} -m {module} {qargs}".rstrip()
+    parts = script.split("/")
+    if len(parts) == 2 and parts[1].endswith((".sh", ".py")):
+        rt, name = parts
+        here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "runtime", rt)
+        for sub in ("scripts", ""):
+            if os.path.exists(os.path.join(here, sub, name)):
+                root = ("$(${CLOUDTIK_PYTHON:-python3} -c 'import cloudtik_amd, os; "
+                        "print(os.path.dirname(cloudtik_amd.__file__))')")
+                path = f"{root}/runtime/{rt}/{sub + '/' if sub else ''}{name}"
+                runner = "bash" if name.endswith(".sh") else "${CLOUDTIK_PYTHON:-python3}"
+                return f"{runner} \"{path}\" {qargs}".rstrip()
+    raise ValueError(f"{script!r} is not a built-in script (a registered alias or <runtime>/<script>); "
+                     f"use `cloudtik exec` or `cloudtik submit` for your own commands")
+
+
+def run_script(config_file, script: str, script_args: Optional[List[str]] = None, node_ip: Optional[str] = None,
+               job_waiter: Optional[str] = None, override_cluster_name: Optional[str] = None,
+               with_output: bool = False):
+    """``cloudtik run``: run a built-in script on the head (or a node) of the cluster
+    (reference scripts.py:678 run / _run_script)."""
+    config = _config(config_file, override_cluster_name)
+    cmd = _builtin_script_command(script, list(script_args or []))
+    if not job_waiter:
+        return exec_cluster(config, cmd, node_ip=node_ip, with_output=with_output)
+    from cloudtik_amd.core.job_waiter import create_job_waiter
+    session = f"cloudtik-run-{int(time.time() * 1000)}"
+    exec_cluster(config, f"tmux new -d -s {session} {shlex.quote(cmd)}", node_ip=node_ip)
+    waiter = create_job_waiter(config, job_waiter)
+    provider = _provider(config)
+    return waiter.wait_for_completion(_node_by_ip(config, provider, node_ip), cmd, session)
+
+
+def runtime_services(config_file, command: str, runtimes: Optional[List[str]] = None,
+                     node_ip: Optional[str] = None, workers_only: bool = False,
+                     override_cluster_name: Optional[str] = None):
+    """Start / stop the services of (some of) the cluster's runtimes on its nodes, head first
+    on start and last on stop (reference head_scripts.py:925-1036 `cloudtik head runtime`)."""
+    if command not in ("start", "stop"):
+        raise ValueError("command must be start or stop")
+    config = _config(config_file, override_cluster_name)
+    types = get_runtime_types(config)
+    sel = [t for t in types if not runtimes or t in runtimes]
+    unknown = set(runtimes or []) - set(types)
+    if unknown:
+        raise ValueError(f"runtimes {sorted(unknown)} are not configured on this cluster")
+    provider = _provider(config)
+    head = get_head_node(provider, config["cluster_name"])
+    if node_ip:
+        nodes = [_node_by_ip(config, provider, node_ip)]
+    else:
+        workers = get_worker_nodes(provider, config["cluster_name"])
+        nodes = list(workers) if workers_only or head is None else \
+            ([head] + list(workers) if command == "start" else list(workers) + [head])
+    order = sel if command == "start" else list(reversed(sel))
+    done = []
+    for n in nodes:
+        is_head = provider.node_tags(n).get(T.CLOUDTIK_TAG_NODE_KIND) == T.NODE_KIND_HEAD
+        flag = " --head" if is_head else ""
+        cmd = " && ".join(f"cloudtik runtime services {t} {command}{flag}" for t in order)
+        if not cmd:
+            continue
+        exec_cluster(config, cmd, node_ip=provider.internal_ip(n))
+        done.append(provider.internal_ip(n))
+    return done

@@ -4,7 +4,8 @@ Resolution order (reference ``utils.py:465-597``):
 
 1. a config with ``from: <template>`` is merged ON TOP of that template, recursively
    (user template dirs from ``$CLOUDTIK_USER_TEMPLATES`` first, then the built-in
-   ``cloudtik_amd/templates``);
+   ``cloudtik_amd/templates``, then the generated provider size / GPU-family templates of
+   ``instance_templates.py``);
 2. the root of the chain is merged on top of the provider's system defaults
    (``providers/<type>/defaults.yaml``, which itself chains ``from: defaults`` to the global
    ``providers/defaults.yaml``).
@@ -65,7 +66,16 @@ def merge_config_hierarchy(provider: Dict[str, Any], config: Dict[str, Any], sys
                            object_name: Optional[str] = None) -> Dict[str, Any]:
     base = config.get("from")
     if base:
-        tmpl = load_yaml(template_path(base, system))
+        path = template_path(base, system)
+        if os.path.exists(path) or system:
+            tmpl = load_yaml(path)
+        else:
+            # provider size / GPU-family templates are generated (core/config/instance_templates.py)
+            from .instance_templates import synthesize
+            tmpl = synthesize(base)
+            if tmpl is None:
+                raise FileNotFoundError(f"no template {base!r} ({path} does not exist and it is not a "
+                                        f"known <provider>/<size> or <provider>/gpu/<family>/<size> template)")
         tp = tmpl.get("provider", {}).get("type")
         if tp and tp != provider.get("type"):
             raise RuntimeError(f"Template provider type ({tp}) doesn't match ({provider.get('type')})!")

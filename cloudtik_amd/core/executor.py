@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import hashlib
 import json
+import re
 import logging
 import os
 import shlex
@@ -59,13 +60,27 @@ class ProcessRunnerError(Exception):
         self.special_case = special_case
 
 
-def with_environment_variables(cmd: str, env: Optional[Dict[str, Any]]) -> str:
+# environment variables whose values never appear in printed / logged commands or errors
+# (reference command_executor.py:23-70 is_key_with_privacy)
+_PRIVACY_KEY = re.compile(r"(PASSWORD|PASSWD|SECRET|TOKEN|CREDENTIAL|PRIVATE|ACCESS_KEY|API_KEY|AUTH|_KEY$)",
+                          re.IGNORECASE)
+PRIVACY_MASK = "<hidden>"
+
+
+def is_key_with_privacy(key: str) -> bool:
+    return bool(_PRIVACY_KEY.search(key or ""))
+
+
+def with_environment_variables(cmd: str, env: Optional[Dict[str, Any]], for_print: bool = False) -> str:
+    """``export K=V; ... cmd``; with ``for_print`` the values of privacy keys are masked."""
     if not env:
         return cmd
     parts = []
     for k, v in env.items():
         if not isinstance(v, str):
             v = json.dumps(v, separators=(",", ":"))
+        if for_print and is_key_with_privacy(k):
+            v = PRIVACY_MASK
         parts.append(f"export {k}={shlex.quote(v)};")
     if "CLOUDTIK_BIN_DIR" in env:
         # same-host nodes run this checkout's `cloudtik` / `cloudtik-run` wrappers
@@ -73,8 +88,16 @@ def with_environment_variables(cmd: str, env: Optional[Dict[str, Any]]) -> str:
     return " ".join(parts) + " " + cmd
 
 
+def printable_command(cmd: str, env: Optional[Dict[str, Any]], cmd_to_print: Optional[str] = None) -> str:
+    return with_environment_variables(cmd_to_print or cmd, env, for_print=True)
+
+
 def run_cmd_with_runner(process_runner, final_cmd, with_output=False, silent=False, timeout=None,
-                        shell=False):
+                        shell=False, printable=None):
+    """Run ``final_cmd``; errors and debug logs carry ``printable`` (secrets masked), never
+    the real command line."""
+    shown = printable if printable is not None else final_cmd
+    logger.debug("running: %s", shown)
     try:
         if with_output:
             return process_runner.check_output(final_cmd, shell=shell, timeout=timeout) \
@@ -87,7 +110,7 @@ def run_cmd_with_runner(process_runner, final_cmd, with_output=False, silent=Fal
             kw["timeout"] = timeout
         return process_runner.check_call(final_cmd, shell=shell, **kw)
     except subprocess.CalledProcessError as e:
-        raise ProcessRunnerError("Command failed", "cmd_failed", code=e.returncode, command=final_cmd)
+        raise ProcessRunnerError("Command failed", "cmd_failed", code=e.returncode, command=shown) from None
 
 
 class CommandExecutor:
@@ -155,9 +178,11 @@ class LocalCommandExecutor(CommandExecutor):
             shutdown_after_run=False, cmd_to_print=None, silent=False):
         if not cmd:
             return None
+        shown = printable_command(cmd, environment_variables, cmd_to_print)
         cmd = with_environment_variables(cmd, environment_variables)
         final = ["bash", "-c", cmd]
-        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent)
+        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent,
+                                   printable=["bash", "-c", shown])
 
     def run_rsync_up(self, source, target, options=None):
         target = os.path.expanduser(target)
@@ -258,12 +283,17 @@ class SSHCommandExecutor(CommandExecutor):
             pf = port_forward if isinstance(port_forward, list) else [port_forward]
             for local, remote in pf:
                 final += ["-L", f"{local}:localhost:{remote}"]
+        shown = list(final)
         if cmd:
+            printable = printable_command(cmd, environment_variables, cmd_to_print)
             cmd = with_environment_variables(cmd, environment_variables)
             if shutdown_after_run:
                 cmd += "; sudo shutdown -h now"
+                printable += "; sudo shutdown -h now"
             final += ["bash", "--login", "-c", "-i", shlex.quote("set -i || true; " + cmd)]
-        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent)
+            shown += ["bash", "--login", "-c", "-i", shlex.quote("set -i || true; " + printable)]
+        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent,
+                                   printable=shown)
 
     def _rsync(self, src, dst, options):
         self._set_ssh_ip_if_required()
@@ -317,11 +347,13 @@ class DockerCommandExecutor(CommandExecutor):
             return self.host.run(cmd, timeout, exit_on_fail, port_forward, with_output,
                                  environment_variables, "auto", ssh_options_override_ssh_key,
                                  shutdown_after_run, cmd_to_print, silent)
+        shown = printable_command(cmd, environment_variables, cmd_to_print)
         cmd = with_environment_variables(cmd, environment_variables)
-        inner = f"{self.docker_cmd} exec {'-it' if self.call_context.allow_interactive else ''} " \
-                f"{self.container_name} /bin/bash -c {shlex.quote(cmd)}"
+        flags = '-it' if self.call_context.allow_interactive else ''
+        inner = f"{self.docker_cmd} exec {flags} {self.container_name} /bin/bash -c {shlex.quote(cmd)}"
+        inner_shown = f"{self.docker_cmd} exec {flags} {self.container_name} /bin/bash -c {shlex.quote(shown)}"
         return self.host.run(inner, timeout, exit_on_fail, port_forward, with_output, None, "host",
-                             ssh_options_override_ssh_key, shutdown_after_run, cmd_to_print, silent)
+                             ssh_options_override_ssh_key, shutdown_after_run, inner_shown, silent)
 
     def run_rsync_up(self, source, target, options=None):
         staging = f"/tmp/cloudtik_docker_staging{target}"
@@ -405,9 +437,11 @@ class KubernetesCommandExecutor(CommandExecutor):
             shutdown_after_run=False, cmd_to_print=None, silent=False):
         if not cmd:
             return None
+        shown = printable_command(cmd, environment_variables, cmd_to_print)
         cmd = with_environment_variables(cmd, environment_variables)
-        final = self.kubectl + ["exec", "-i", "-n", self.namespace, self.node_id, "--", "bash", "-c", cmd]
-        return run_cmd_with_runner(self.process_runner, final, with_output=with_output, silent=silent)
+        base = self.kubectl + ["exec", "-i", "-n", self.namespace, self.node_id, "--", "bash", "-c"]
+        return run_cmd_with_runner(self.process_runner, base + [cmd], with_output=with_output, silent=silent,
+                                   printable=base + [shown])
 
     def run_rsync_up(self, source, target, options=None):
         run_cmd_with_runner(self.process_runner, self.kubectl + ["cp", source, f"{self.namespace}/{self.node_id}:{target}"])

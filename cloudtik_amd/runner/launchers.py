@@ -202,29 +202,83 @@ class DistributedLauncher(Launcher):
         return f"cd {shlex.quote(os.getcwd())} && env {exports} " + " ".join(shlex.quote(p) for p in parts)
 
     def run(self) -> int:
+        """Start the local launcher on every host; the first host that fails stops the job
+        everywhere (reference rsh/rsh_exec.py:196-263 terminate-all), so no rank is left
+        blocked in an RCCL collective until the communicator timeout.
+
+        Each remote launcher runs as the leader of its own process group (``setsid``) and
+        writes its pid to a per-job file; terminate-all signals that whole group over the
+        same remote shell, then ends the local ssh clients."""
+        import uuid
         placements = self.d.host_ranks()
         if not self.args.master_addr:
             first = placements[0][0] if placements else "127.0.0.1"
             self.args.master_addr = "127.0.0.1" if _is_local(first) and len(placements) == 1 else first
         agent = cloudtik_rsh_agent(getattr(self.args, "rsh", None))
         rsh = [agent] if agent else shlex.split(getattr(self.args, "rsh", None) or self.rsh_default)
-        threads, codes = [], {}
+        job = uuid.uuid4().hex[:12]
+        codes: Dict[str, int] = {}
+        remote: Dict[str, subprocess.Popen] = {}
+        locals_: Dict[str, LocalLauncher] = {}
+        lock = threading.Lock()
+        failed = threading.Event()
+
+        def pidfile(node_rank):
+            return f"/tmp/cloudtik-job-{job}-{node_rank}.pid"
 
         def run_host(host, node_rank, n, first):
             if _is_local(host):
-                codes[host] = LocalLauncher(self.args, self.d, node_rank, first, n).run()
+                ll = LocalLauncher(self.args, self.d, node_rank, first, n)
+                with lock:
+                    locals_[host] = ll
+                rc = ll.run()
             else:
-                cmd = rsh + [host, self.remote_command(host, node_rank, n, first)]
-                codes[host] = subprocess.call(cmd)
+                inner = self.remote_command(host, node_rank, n, first)
+                wrapped = (f"setsid sh -c {shlex.quote(f'echo $$ > {pidfile(node_rank)}; exec sh -c {shlex.quote(inner)}')}"
+                           f"; rc=$?; rm -f {pidfile(node_rank)}; exit $rc")
+                p = subprocess.Popen(rsh + [host, wrapped])
+                with lock:
+                    remote[host] = p
+                rc = p.wait()
+            with lock:
+                codes[host] = rc
+            if rc != 0:
+                failed.set()
 
+        threads = []
         for host, node_rank, n, first in placements:
             t = threading.Thread(target=run_host, args=(host, node_rank, n, first), daemon=True)
             t.start()
             threads.append(t)
+        ranks = {h: nr for h, nr, _, _ in placements}
+        while any(t.is_alive() for t in threads):
+            if failed.wait(0.2):
+                bad = {h: c for h, c in codes.items() if c != 0}
+                print(f"[cloudtik-run] host(s) {sorted(bad)} failed ({bad}): terminating the job on every host",
+                      file=sys.stderr)
+                self.terminate_all(rsh, remote, locals_, ranks, pidfile, lock)
+                break
         for t in threads:
-            t.join()
+            t.join(timeout=60)
         bad = [c for c in codes.values() if c != 0]
         return bad[0] if bad else 0
+
+    @staticmethod
+    def terminate_all(rsh, remote, locals_, ranks, pidfile, lock):
+        with lock:
+            rem, loc = dict(remote), dict(locals_)
+        for host, p in rem.items():
+            if p.poll() is None:
+                kill = f"[ -f {pidfile(ranks[host])} ] && kill -TERM -- -$(cat {pidfile(ranks[host])}) 2>/dev/null; true"
+                subprocess.call(rsh + [host, kill], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        for ll in loc.values():
+            ll._terminate_all()
+        deadline = time.time() + 30
+        for p in rem.values():
+            try:
+                p.wait(max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
 
 
 class MPILauncher(Launcher):

@@ -128,3 +128,26 @@ def test_cloudtik_rsh_agent_routes_through_head_exec(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert sorted(calls.read_text().split()) == ["--node-ip=10.255.0.3", "--node-ip=10.255.0.4"]
     assert sorted(int(l[1]) for l in _results(tmp_path)) == [0, 1]
+
+
+def test_distributed_launcher_terminates_all_hosts_on_failure(tmp_path):
+    """A rank failing on one host ends the job on every host (reference rsh_exec.py:196-263):
+    the healthy host's ranks (sleeping 120 s) are signalled through the remote shell and the
+    launcher returns the failing exit code long before they would have finished."""
+    import time
+    rsh = tmp_path / "fake_rsh"
+    rsh.write_text('#!/bin/bash\nshift\nexport PATH="%s:$PATH"\nexec bash -c "$1"\n' % os.path.join(ROOT, "bin"))
+    rsh.chmod(0o755)
+    marker = tmp_path / "alive"
+    prog = (f"if [ $NODE_RANK = 1 ]; then sleep 2; exit 5; fi; "
+            f"trap 'echo terminated > {marker}_$RANK; exit 143' TERM; sleep 120 & wait")
+    t0 = time.time()
+    r = subprocess.run([RUN, "--hosts", "10.255.0.5:2,10.255.0.6:1", "--rsh", str(rsh), "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), "--no-python", "bash", "-c", prog],
+                       capture_output=True, text=True, timeout=100, env=dict(os.environ, PYTHONPATH=ROOT))
+    took = time.time() - t0
+    assert r.returncode == 5, r.stdout + r.stderr
+    assert took < 60, took
+    assert "terminating the job on every host" in r.stderr
+    time.sleep(1)
+    assert sorted(p.name for p in tmp_path.glob("alive_*")) == ["alive_0", "alive_1"]
