@@ -70,13 +70,24 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return r;
 }
 
+// GELU (exact, erf form) and its derivative without the libm erf: erf(|z|) = 1 - P(t) e^{-z^2}
+// with t = 1 / (1 + p |z|) (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 -- far below the
+// bf16 resolution of the tensors these feed).  For z = x / sqrt(2), e^{-z^2} = e^{-x^2/2} is
+// the same exponential the normal pdf in the derivative needs: one exp + one rcp + a few FMA
+// per element instead of the branchy libm erf plus a second exp.
+__device__ __forceinline__ float gelu_cdf_e(float x, float e) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(x), 1.f));
+  const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
+                                      -0.284496736f), 0.254829592f);
+  const float erf_abs = fmaf(-poly, e, 1.f);
+  return 0.5f + 0.5f * copysignf(erf_abs, x);
+}
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  return x * gelu_cdf_e(x, __expf(-0.5f * x * x));
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  const float e = __expf(-0.5f * x * x);
+  return fmaf(x * 0.3989422804014327f, e, gelu_cdf_e(x, e));
 }
 
 // Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5 "XCD swizzle

@@ -70,7 +70,29 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(
   if (cv < nvec_row) {
     u16x8 bv = u16x8(0);
     if (bias) bv = reinterpret_cast<const u16x8*>(bias)[cv];
-    for (int row = blockIdx.x * 4 + rl; row < M; row += gridDim.x * 4) {
+    const int rstep = gridDim.x * 4;
+    int row = blockIdx.x * 4 + rl;
+    // two rows per step: four independent 16-byte loads in flight per lane
+    for (; row + rstep < M; row += 2 * rstep) {
+      const long i0 = (long)row * nvec_row + cv, i1 = (long)(row + rstep) * nvec_row + cv;
+      const u16x8 g0 = reinterpret_cast<const u16x8*>(dy)[i0], g1 = reinterpret_cast<const u16x8*>(dy)[i1];
+      const u16x8 z0 = act != ACT_NONE ? reinterpret_cast<const u16x8*>(z)[i0] : u16x8(0);
+      const u16x8 z1 = act != ACT_NONE ? reinterpret_cast<const u16x8*>(z)[i1] : u16x8(0);
+      u16x8 o0, o1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d0 = bf2f(g0[j]) * act_g(bf2f(z0[j]) + bf2f(bv[j]), act);
+        const float d1 = bf2f(g1[j]) * act_g(bf2f(z1[j]) + bf2f(bv[j]), act);
+        o0[j] = f2bf(d0);
+        o1[j] = f2bf(d1);
+        acc[j] += d0 + d1;
+      }
+      if (dz) {
+        reinterpret_cast<u16x8*>(dz)[i0] = o0;
+        reinterpret_cast<u16x8*>(dz)[i1] = o1;
+      }
+    }
+    for (; row < M; row += rstep) {
       const long idx = (long)row * nvec_row + cv;
       const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[idx];
       const u16x8 zv = act != ACT_NONE ? reinterpret_cast<const u16x8*>(z)[idx] : u16x8(0);

@@ -258,9 +258,52 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
   }
 }
 
+// Up to three column sums in ONE launch (blockIdx.y picks the (partials, output) pair):
+// the LayerNorm backward's dgamma / dbeta / dbias reductions are tiny (a few MB) and were
+// three back-to-back launch latencies.
+struct Colsum3 { const float* part[3]; void* out[3]; };
+
+template <typename OUT>
+__global__ __launch_bounds__(1024) void colsum3_kernel(Colsum3 c, int P, int N, int accumulate) {
+  __shared__ float red[16][64];
+  const float* __restrict__ part = c.part[blockIdx.y];
+  OUT* __restrict__ out = reinterpret_cast<OUT*>(c.out[blockIdx.y]);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  float t = 0.f;
+  if (col < N) {
+    int p = rl;
+    for (; p + 48 < P; p += 64) {
+      const float a = part[(size_t)p * N + col], b = part[(size_t)(p + 16) * N + col];
+      const float d = part[(size_t)(p + 32) * N + col], e = part[(size_t)(p + 48) * N + col];
+      t += (a + b) + (d + e);
+    }
+    for (; p < P; p += 16) t += part[(size_t)p * N + col];
+  }
+  red[rl][cl] = t;
+  __syncthreads();
+  if (rl == 0 && col < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][cl];
+    if (accumulate) s += to_f<OUT>(out[col]);
+    out[col] = from_f<OUT>(s);
+  }
+}
+
 }  // namespace ct
 
 using namespace ct;
+
+static int colsum_multi(const float* const* parts, void* const* outs, int n, int P, int N, int out_fp32,
+                        int accumulate, hipStream_t stream) {
+  Colsum3 c{};
+  for (int i = 0; i < n; ++i) { c.part[i] = parts[i]; c.out[i] = outs[i]; }
+  const dim3 grid(ceil_div(N, 64), n);
+  if (out_fp32) colsum3_kernel<float><<<grid, 1024, 0, stream>>>(c, P, N, accumulate);
+  else colsum3_kernel<bf16_t><<<grid, 1024, 0, stream>>>(c, P, N, accumulate);
+  return 0;
+}
 
 extern "C" int ct_colsum(const float* part, void* out, int P, int N, int out_fp32, int accumulate,
                          hipStream_t stream) {
@@ -330,8 +373,11 @@ extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, co
     default: return -1;
   }
 #undef CT_LNB
-  ct_colsum(a.dg_part, dgamma, grid, N, param_fp32, accumulate, stream);
-  if (a.db_part) ct_colsum(a.db_part, dbeta, grid, N, param_fp32, accumulate, stream);
-  if (a.dbias_part) ct_colsum(a.dbias_part, dbias, grid, N, param_fp32, accumulate, stream);
-  return 0;
+  const float* parts[3];
+  void* outs[3];
+  int n = 0;
+  parts[n] = a.dg_part; outs[n++] = dgamma;
+  if (a.db_part) { parts[n] = a.db_part; outs[n++] = dbeta; }
+  if (a.dbias_part) { parts[n] = a.dbias_part; outs[n++] = dbias; }
+  return colsum_multi(parts, outs, n, grid, N, param_fp32, accumulate, stream);
 }
