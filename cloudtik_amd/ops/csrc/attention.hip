@@ -82,8 +82,12 @@ struct AttnFwdArgs {
 
 constexpr int kRelBiasMax = 4096;   // LDS floats for one head's relative-offset bias vector
 
-template <bool DROP, bool CAUSAL, bool REL = false>
-__global__ __launch_bounds__(256) void attn_fwd_d64_kernel(AttnFwdArgs a) {
+// WPE: waves per SIMD the register budget must allow (256 threads = 1 wave per SIMD per
+// workgroup).  The compiler's default budget (236 VGPR + 32 AGPR) allowed ONE resident
+// workgroup per CU, so a workgroup's Q/K/V loads never overlapped another's MFMAs; at 2 the
+// kernel fits in ~170 VGPRs without spills.
+template <bool DROP, bool CAUSAL, bool REL = false, int WPE = 2>
+__global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   // [buf][K,V][64 rows][128 B] then [buf][64] fp32 log2-domain key bias (-inf past Sk)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + 2 * 64 * 4];
   float* kbias_lds = reinterpret_cast<float*>(smem + 32768);
@@ -566,10 +570,17 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
   a.relb = nullptr; a.relb_sh = 0; a.relb_len = 0; a.rel_base = 0;
   dim3 grid((Sq + 127) / 128, B * H);
   const bool drop = p_drop > 0.f;
-  if (drop && causal) attn_fwd_d64_kernel<true, true><<<grid, 256, 0, stream>>>(a);
-  else if (drop) attn_fwd_d64_kernel<true, false><<<grid, 256, 0, stream>>>(a);
-  else if (causal) attn_fwd_d64_kernel<false, true><<<grid, 256, 0, stream>>>(a);
-  else attn_fwd_d64_kernel<false, false><<<grid, 256, 0, stream>>>(a);
+  static const int wpe = [] {
+    const char* e = getenv("CLOUDTIK_AMD_ATTN_FWD_WPE");
+    return e && atoi(e) == 3 ? 3 : (e && atoi(e) == 1 ? 1 : 2);
+  }();
+#define CT_ATTN_FWD(W)                                                                          \
+  if (drop && causal) attn_fwd_d64_kernel<true, true, false, W><<<grid, 256, 0, stream>>>(a);    \
+  else if (drop) attn_fwd_d64_kernel<true, false, false, W><<<grid, 256, 0, stream>>>(a);        \
+  else if (causal) attn_fwd_d64_kernel<false, true, false, W><<<grid, 256, 0, stream>>>(a);      \
+  else attn_fwd_d64_kernel<false, false, false, W><<<grid, 256, 0, stream>>>(a);
+  if (wpe == 3) { CT_ATTN_FWD(3) } else if (wpe == 1) { CT_ATTN_FWD(1) } else { CT_ATTN_FWD(2) }
+#undef CT_ATTN_FWD
   return 0;
 }
 

@@ -104,8 +104,13 @@ def _expand(spec):
     return spec
 
 
+# keys every runtime section accepts: the quorum manager's minimal node count (quorum
+# runtimes wait for it before configuring, core/head/quorum_manager.py)
+COMMON = {"minimal_nodes": "i"}
+
+
 def _section(keys: Dict[str, Any], strict: bool = True) -> Dict[str, Any]:
-    out = {"type": "object", "properties": {k: _expand(v) for k, v in keys.items()}}
+    out = {"type": "object", "properties": {k: _expand(v) for k, v in dict(COMMON, **keys).items()}}
     if strict:
         out["patternProperties"] = {"^with_": {"type": ["boolean", "string"]}}
         out["additionalProperties"] = False
