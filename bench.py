@@ -129,6 +129,8 @@ def setup_tunableop(mode, rank):
     tn.enable(True)
     tn.set_filename(TUNE_FILE if rank == 0 or mode == "use" else TUNE_FILE + f".rank{rank}")
     tn.tuning_enable(mode == "tune")
+    # "use": read-only -- N ranks must not rewrite the shared in-tree table at exit
+    tn.write_file_on_exit(mode == "tune")
     if mode == "tune":
         tn.set_max_tuning_duration(60)
         tn.set_max_tuning_iterations(30)

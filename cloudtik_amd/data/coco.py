@@ -178,28 +178,42 @@ class CocoLoader:
         self._pool = None
 
     def __len__(self):
+        if self.fixed_canvas:
+            if self.drop_last:
+                # every rank yields the minimum number of full same-orientation batches over
+                # all ranks (each rank can compute every rank's split: same permutation seed)
+                return min(sum(1 for g in self._groups(r) if len(g) == self.batch_size) for r in range(self.world))
+            return len(self._groups(self.rank))
         per = len(self.ds) // self.world if self.drop_last else -(-len(self.ds) // self.world)
         return per // self.batch_size if self.drop_last else -(-per // self.batch_size)
 
     def set_epoch(self, epoch: int):
         self.epoch = epoch
 
-    def _batches(self):
+    def _rank_indices(self, rank):
         n = len(self.ds)
         idx = np.random.default_rng(self.seed + self.epoch).permutation(n) if self.ds.train else np.arange(n)
         per = n // self.world if self.drop_last else -(-n // self.world)
-        idx = idx[self.rank * per:(self.rank + 1) * per]
+        return idx[rank * per:(rank + 1) * per]
+
+    def _groups(self, rank):
+        """Same-orientation batches (landscape / portrait canvases) of ``rank``'s images."""
+        idx = self._rank_indices(rank)
+        land = [i for i in idx if self.ds.images[int(i)][0]["width"] >= self.ds.images[int(i)][0]["height"]]
+        port = [i for i in idx if self.ds.images[int(i)][0]["width"] < self.ds.images[int(i)][0]["height"]]
+        return [g[b:b + self.batch_size] for g in (land, port) for b in range(0, len(g), self.batch_size)]
+
+    def _batches(self):
+        idx = self._rank_indices(self.rank)
         rng = random.Random(self.seed * 7919 + self.epoch)
         if self.fixed_canvas:
-            land = [i for i in idx if self.ds.images[int(i)][0]["width"] >= self.ds.images[int(i)][0]["height"]]
-            port = [i for i in idx if self.ds.images[int(i)][0]["width"] < self.ds.images[int(i)][0]["height"]]
-            groups = [g[b:b + self.batch_size] for g in (land, port) for b in range(0, len(g), self.batch_size)]
+            groups = self._groups(self.rank)
             if self.ds.train:
                 rng.shuffle(groups)
             if self.drop_last:
-                # full batches only, and every rank yields len(self) of them (collectives stay matched)
-                groups = [g for g in groups if len(g) == self.batch_size]
-                groups = (groups * len(self))[:len(self)] if groups else []
+                # full batches only, no image twice; ranks with more full batches drop the
+                # surplus so every rank yields len(self) batches (collectives stay matched)
+                groups = [g for g in groups if len(g) == self.batch_size][:len(self)]
         else:
             groups = [idx[b * self.batch_size:(b + 1) * self.batch_size] for b in range(len(self))]
         for sel in groups:

@@ -152,6 +152,9 @@ def test_fixed_canvas_groups_by_orientation(tmp_path):
         seen += list(ids)
     assert sorted(seen) == list(range(1, 8)) and shapes <= {(96, 160), (160, 96)}
     tr = CocoDetection(str(tmp_path), str(ann), train=True, with_masks=False)
-    counts = [sum(1 for _ in CocoLoader(tr, 2, 96, 160, rank=r, world=2, workers=0, fixed_canvas=True))
-              for r in range(2)]
-    assert counts[0] == counts[1] == len(CocoLoader(tr, 2, 96, 160, rank=0, world=2, workers=0))
+    loaders = [CocoLoader(tr, 2, 96, 160, rank=r, world=2, workers=0, fixed_canvas=True) for r in range(2)]
+    ids = [[i for _, _, _, b, _ in ld for i in b] for ld in loaders]
+    assert len(ids[0]) // 2 == len(ids[1]) // 2 == len(loaders[0]) == len(loaders[1])
+    assert all(len(x) == len(set(x)) for x in ids)            # no image twice within an epoch
+    assert not set(ids[0]) & set(ids[1])                       # ranks see disjoint images
+    assert len(ld) == sum(1 for _ in ld)                       # eval __len__ matches what it yields

@@ -19,7 +19,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, per_device=False):
     import faulthandler
     import sys
     faulthandler.enable()
@@ -29,7 +29,7 @@ def _worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(rank if per_device else 0)
         from cloudtik_amd.parallel.p2p import P2PAllReducer
         stage("init")
         ar = P2PAllReducer(max_bytes=1 << 20, blocks=8, timeout_s=60)
@@ -67,13 +67,12 @@ def _worker(rank, world, port, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.gpu
-def test_p2p_oneshot_allreduce_two_ranks_one_gpu():
+def _run_pair(per_device):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, per_device)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -97,6 +96,20 @@ def test_p2p_oneshot_allreduce_two_ranks_one_gpu():
             torch.testing.assert_close(got, torch.from_numpy(ref), rtol=tol, atol=tol)
     # 50 sums of [1, 2] -> first call 3, then doubling every call
     assert torch.equal(torch.from_numpy(res[0]["chain"][0]), torch.full((4,), 3.0 * 2 ** 49))
+
+
+@pytest.mark.gpu
+def test_p2p_oneshot_allreduce_two_ranks_one_gpu():
+    """Both ranks on GPU 0: IPC export / import, signal barriers and the fixed-order sum."""
+    _run_pair(per_device=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (xGMI peers)")
+def test_p2p_oneshot_allreduce_across_xgmi_peers():
+    """One rank per GPU: peer mapping with hipIpcMemLazyEnablePeerAccess, coherence of the
+    staging buffers read over xGMI, system-scope fences across the GPUs' L2s."""
+    _run_pair(per_device=True)
 
 
 def test_p2p_from_env_disabled_without_gpu(monkeypatch):
