@@ -77,6 +77,17 @@ def _kill(name: str, sudo: bool = False) -> str:
     return f"P=$RUNTIME_PATH/pids/{name}.pid; [ -f $P ] && {k} $(cat $P) 2>/dev/null; rm -f $P; true"
 
 
+# per-runtime quorum semantics: Kafka brokers need their minimal set but no quorum of their
+# own (ZooKeeper holds it); a MinIO server pool is fixed at creation (erasure sets), so its
+# quorum cannot grow by joining nodes; ZooKeeper / etcd / Consul servers / MongoDB replica
+# sets reconfigure membership online
+QUORUM_CONSTRAINTS: Dict[str, Tuple[bool, bool, bool]] = {
+    "kafka": (True, False, True),
+    "minio": (True, True, False),
+    "zookeeper": (True, True, True), "etcd": (True, True, True), "consul": (True, True, True),
+    "mongodb": (True, True, True),
+}
+
 SPECS: List[RuntimeSpec] = [
     RuntimeSpec("spark", "Apache Spark on YARN with history server and auto executor sizing",
                 "3.3.1", "SPARK_HOME", APACHE + "/spark/spark-{version}/spark-{version}-bin-hadoop3.tgz",
@@ -309,9 +320,11 @@ class CatalogRuntime(RuntimeBase):
                 for s in self.spec.services if s.node_kind in (H, A)}
 
     def get_node_constraints(self, cluster_config, node_type=None):
+        """(require minimal nodes before setup, manage a quorum of them, quorum can grow at
+        runtime) -- reference Runtime.get_node_constraints."""
         if not self.spec.quorum:
             return None
-        return True, True, True   # minimal nodes, quorum, scale-up constraint
+        return QUORUM_CONSTRAINTS.get(self.name, (True, True, True))
 
     def get_logs(self):
         return dict(self.spec.logs)
