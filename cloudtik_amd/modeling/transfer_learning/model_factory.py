@@ -4,11 +4,13 @@ from __future__ import annotations
 
 from typing import Dict, List
 
+from .anomaly_detection import ImageAnomalyDetectionModel
 from .image_classification import BACKBONES, ImageClassificationModel
 from .text_classification import ENCODERS, TextClassificationModel
 
 USE_CASES = {"image_classification": (ImageClassificationModel, BACKBONES),
-             "text_classification": (TextClassificationModel, ENCODERS)}
+             "text_classification": (TextClassificationModel, ENCODERS),
+             "image_anomaly_detection": (ImageAnomalyDetectionModel, BACKBONES)}
 
 
 def get_supported_models(framework: str = "pytorch", use_case: str = None) -> Dict[str, List[str]]:
