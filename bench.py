@@ -127,10 +127,18 @@ def setup_tunableop(mode, rank):
     if mode == "use" and not os.path.exists(TUNE_FILE):
         return
     tn.enable(True)
-    tn.set_filename(TUNE_FILE if rank == 0 or mode == "use" else TUNE_FILE + f".rank{rank}")
+    if mode == "use":
+        # every rank reads its own private copy: N ranks never rewrite the shared in-tree
+        # table at exit (TunableOp writes its results file when the process ends)
+        import shutil
+        import tempfile
+        fd, path = tempfile.mkstemp(prefix=f"tunableop_rank{rank}_", suffix=".csv")
+        os.close(fd)
+        shutil.copyfile(TUNE_FILE, path)
+        tn.set_filename(path)
+    else:
+        tn.set_filename(TUNE_FILE if rank == 0 else TUNE_FILE + f".rank{rank}")
     tn.tuning_enable(mode == "tune")
-    # "use": read-only -- N ranks must not rewrite the shared in-tree table at exit
-    tn.write_file_on_exit(mode == "tune")
     if mode == "tune":
         tn.set_max_tuning_duration(60)
         tn.set_max_tuning_iterations(30)
