@@ -127,7 +127,9 @@ def setup_tunableop(mode, rank):
     if mode == "use" and not os.path.exists(TUNE_FILE):
         return
     tn.enable(True)
-    if mode == "use":
+    if mode == "use" and os.environ.get("CLOUDTIK_BENCH_TUNE_DIRECT") == "1":
+        tn.set_filename(TUNE_FILE)
+    elif mode == "use":
         # every rank reads its own private copy: N ranks never rewrite the shared in-tree
         # table at exit (TunableOp writes its results file when the process ends)
         import shutil
@@ -409,6 +411,10 @@ def main():
             r["eager_value"], r["eager_ms"] = e["value"], e["ms"]
         results.append(r)
 
+    if rank == 0 and device.type == "cuda" and args.tunableop != "off":
+        import torch.cuda.tunable as tn
+        print(f"[bench] TunableOp: {len(tn.get_results() or [])} tuned GEMM solutions in use "
+              f"({tn.get_filename()})", file=sys.stderr)
     if rank == 0:
         head = results[0]
         base = BASELINE.get(head["model"])
