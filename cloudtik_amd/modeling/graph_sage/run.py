@@ -2,9 +2,15 @@
 training -> node embeddings -> tabular data with embedding columns (reference
 graph_sage/modeling/run.py:504-700, build_graph.py, embeddings.py).
 
-Partitioning and DGL graph servers of the reference are replaced by a GPU-resident graph per
-rank (``cloudtik-run -np N`` gives data-parallel training over RCCL); ``--num-parts`` and
-the server/sampler options are accepted for compatibility and ignored.
+Two distributed modes (``cloudtik-run -np N``):
+
+* ``--num-parts 1`` (default): the whole graph is resident on every GPU (288 GB HBM3E holds
+  billion-edge graphs) and training is data-parallel over RCCL.
+* ``--num-parts N`` (= world size): rank 0 partitions the graph (``distributed.py``, LDG),
+  every rank loads its partition, samples across partitions with all-to-alls and holds a
+  shard of the node embeddings -- the reference's partitioned DistGraph training without
+  separate graph-server / sampler processes (``--num-servers``/``--num-samplers`` are
+  accepted and ignored).
 """
 from __future__ import annotations
 
@@ -95,6 +101,9 @@ def run(args):
     graph = build_graph(df, cfg)
     result = {"num_nodes": graph.num_nodes, "num_edges": graph.num_edges}
     model_file = args.model_file or os.path.join(args.output_dir, "graph_sage.pt")
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if args.num_parts > 1 and not args.single_node:
+        return _run_partitioned(args, df, cfg, graph, result, model_file, rank, world)
     tc = TrainConfig(num_epochs=args.num_epochs, num_hidden=args.num_hidden, num_layers=args.num_layers,
                      fan_out=[int(x) for x in str(args.fan_out).split(",")], batch_size=args.batch_size,
                      batch_size_eval=args.batch_size_eval, eval_every=args.eval_every, lr=args.lr,
@@ -108,6 +117,42 @@ def run(args):
         trainer.model.load_state_dict(torch.load(model_file, weights_only=True)["state_dict"])
     if not args.no_predict and rank == 0:
         emb = trainer.embeddings().float().cpu().numpy()
+        out = args.predict_output or os.path.join(args.output_dir, "node_embeddings.npy")
+        np.save(out, emb)
+        data_out = os.path.join(args.output_dir, args.data_with_embeddings_name)
+        apply_embeddings(df, graph, emb, cfg["node_columns"]).to_csv(data_out, index=False)
+        result["embeddings"] = out
+        result["data_with_embeddings"] = data_out
+    if rank == 0:
+        print(json.dumps(result, default=float), flush=True)
+    return result
+
+
+def _run_partitioned(args, df, cfg, graph, result, model_file, rank, world):
+    import torch
+    import torch.distributed as dist
+    from .distributed import DistGraph, DistLinkPredictionTrainer, DistTrainConfig, partition_graph
+
+    if args.num_parts != world:
+        raise SystemExit(f"--num-parts {args.num_parts} needs {args.num_parts} ranks (got {world})")
+    part_dir = os.path.join(args.temp_dir, f"{args.graph_name}_parts")
+    if rank == 0 and not (args.no_partition_graph and os.path.exists(os.path.join(part_dir, "partition.json"))):
+        result["partition"] = partition_graph(graph, args.num_parts, part_dir)
+    dist.barrier()
+    device = args.device or (f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu")
+    dg = DistGraph(part_dir, rank, world, device)
+    tc = DistTrainConfig(num_hidden=args.num_hidden, num_layers=args.num_layers,
+                         fan_out=tuple(int(x) for x in str(args.fan_out).split(",")), batch_size=args.batch_size,
+                         num_epochs=args.num_epochs, lr=args.lr)
+    trainer = DistLinkPredictionTrainer(dg, tc)
+    if not args.no_train:
+        result.update(trainer.train())
+        result["test_auc"] = trainer.evaluate(2)
+        if rank == 0:
+            trainer.save(model_file)
+    emb = trainer.gather_embeddings() if not args.no_predict else None
+    if emb is not None:
+        emb = emb.numpy()
         out = args.predict_output or os.path.join(args.output_dir, "node_embeddings.npy")
         np.save(out, emb)
         data_out = os.path.join(args.output_dir, args.data_with_embeddings_name)

@@ -114,7 +114,8 @@ def _free_port():
     return p
 
 
-def test_graph_sage_ddp_gloo(tmp_path):
+@pytest.mark.parametrize("num_parts", [1, 2])
+def test_graph_sage_ddp_gloo(tmp_path, num_parts):
     df = _table(3000)
     raw = tmp_path / "tx.csv"
     df.to_csv(raw, index=False)
@@ -126,9 +127,12 @@ def test_graph_sage_ddp_gloo(tmp_path):
                         "-m", "cloudtik_amd.modeling.graph_sage.run", "--raw-data-path", str(raw),
                         "--tabular2graph", str(tmp_path / "t2g.yaml"), "--output-dir", str(tmp_path / "out"),
                         "--num-epochs", "2", "--num-hidden", "16", "--fan-out", "5,5", "--batch-size", "256",
-                        "--log-every", "0", "--device", "cpu"],
+                        "--log-every", "0", "--device", "cpu", "--num-parts", str(num_parts),
+                        "--temp-dir", str(tmp_path)],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     import json
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert res["test_auc"] > 0.75
+    assert res["test_auc"] > 0.75, res
+    if num_parts > 1:        # partitioned graph + sharded embeddings, cut edges sampled remotely
+        assert res["partition"]["edge_cut"] > 0 and os.path.exists(res["embeddings"])
