@@ -118,6 +118,9 @@ def build_ops(force=False, jobs=None, verbose=True):
         link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
                 *[f"-L{p}" for p in lib], "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
                 "-ltorch_hip", "-ltorch_python",
+                # PyTorch's own hipBLASLt (bindings_lt.cpp shares its handle and workspace;
+                # /opt/rocm's copy would be a second, incompatible instance)
+                *[os.path.join(p, "libhipblaslt.so") for p in lib if os.path.exists(os.path.join(p, "libhipblaslt.so"))],
                 *[f"-Wl,-rpath,{p}" for p in lib if "torch" in p]]
         _run(link)
         os.replace(out + ".tmp", out)

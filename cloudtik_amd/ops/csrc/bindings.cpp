@@ -499,6 +499,7 @@ void register_ext(pybind11::module& m);   // bindings_ext.cpp
 void register_graph(pybind11::module& m); // bindings_graph.cpp
 void register_deform(pybind11::module& m); // bindings_deform.cpp
 void register_p2p(pybind11::module& m);    // bindings_p2p.cpp
+void register_lt(pybind11::module& m);     // bindings_lt.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "cloudtik_amd CDNA4 (gfx950) op library";
@@ -506,6 +507,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_graph(m);
   register_deform(m);
   register_p2p(m);
+  register_lt(m);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);

@@ -1,0 +1,191 @@
+// hipBLASLt matmul with fused epilogues (bias+GELU with the pre-activation kept, dGELU with the
+// bias gradient, bias gradients of the wgrad operands), for the BERT FFN / QKV hot paths where
+// the separate elementwise pass costs a full read+write of a [tokens, 4*hidden] activation.
+//
+// Row-major torch semantics: D[M,N] = alpha * op(A)[M,K] @ op(B)[K,N] + beta * C.  hipBLASLt
+// is column-major, so the call is issued as D^T = op(B)^T op(A)^T (operands swapped); the
+// "rows" of hipBLASLt's D are then our N (feature) dimension, which is what bias / bias-grad
+// vectors are indexed by.  Matmul descriptors and the heuristic's algorithm are cached per
+// (shape, strides, ops, epilogue) key; the handle and workspace are PyTorch's own.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/HIPContextLight.h>
+#include <hipblaslt/hipblaslt.h>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace {
+
+#define LT_CHECK(x)                                                                     \
+  do {                                                                                  \
+    hipblasStatus_t st_ = (x);                                                          \
+    TORCH_CHECK(st_ == HIPBLAS_STATUS_SUCCESS, "hipBLASLt: ", #x, " failed: ", (int)st_); \
+  } while (0)
+
+using Key = std::tuple<long, long, long, long, long, long, long, long, long, int, int, int, int, int>;
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  bool ok = false;
+};
+
+std::mutex g_mu;
+std::map<Key, Plan> g_plans;
+
+hipDataType dt(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return HIP_R_16BF;
+    case at::kHalf: return HIP_R_16F;
+    case at::kFloat: return HIP_R_32F;
+    default: TORCH_CHECK(false, "lt_matmul: unsupported dtype");
+  }
+  return HIP_R_32F;
+}
+
+bool rowmajor_ok(const at::Tensor& t) { return t.dim() == 2 && t.stride(1) == 1 && t.stride(0) >= t.size(1); }
+
+}  // namespace
+
+// epilogue: hipblasLtEpilogue_t value.  bias: bias (fwd) or bias-gradient output (BGRAD*,
+// DGELU_BGRAD).  aux: pre-activation output (GELU_AUX*) or input (DGELU*).  Returns False when
+// hipBLASLt has no algorithm for the combination (caller falls back to separate kernels).
+bool lt_matmul(at::Tensor A, at::Tensor B, at::Tensor D, bool trans_a, bool trans_b, double alpha, double beta,
+               c10::optional<at::Tensor> C, int64_t epilogue, c10::optional<at::Tensor> bias,
+               c10::optional<at::Tensor> aux) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "lt_matmul: GPU tensors");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "lt_matmul: 2-D row-major operands");
+  const long M = D.size(0), N = D.size(1);
+  const long K = trans_a ? A.size(0) : A.size(1);
+  TORCH_CHECK((trans_a ? A.size(1) : A.size(0)) == M, "lt_matmul: A rows");
+  TORCH_CHECK((trans_b ? B.size(1) : B.size(0)) == K && (trans_b ? B.size(0) : B.size(1)) == N, "lt_matmul: B shape");
+  const at::Tensor& Ct = (C.has_value() && C->defined()) ? *C : D;
+  TORCH_CHECK(rowmajor_ok(Ct) && Ct.size(0) == M && Ct.size(1) == N, "lt_matmul: C shape");
+  const bool has_bias = bias.has_value() && bias->defined();
+  const bool has_aux = aux.has_value() && aux->defined();
+  if (has_bias) TORCH_CHECK(bias->is_contiguous() && bias->numel() >= N, "lt_matmul: bias length");
+  if (has_aux) TORCH_CHECK(rowmajor_ok(*aux) && aux->size(0) == M && aux->size(1) == N, "lt_matmul: aux shape");
+  const int bias_dt = has_bias ? (int)dt(*bias) : -1;
+  const int aux_dt = has_aux ? (int)dt(*aux) : -1;
+  Key key{M, N, K, A.stride(0), B.stride(0), Ct.stride(0), D.stride(0), has_aux ? aux->stride(0) : 0,
+          (long)dt(A) * 64 + (long)dt(D), (int)trans_a, (int)trans_b, (int)epilogue, bias_dt, aux_dt};
+  const size_t ws_size = at::cuda::getCUDABlasLtWorkspaceSize();
+  void* ws = at::cuda::getCUDABlasLtWorkspace();
+  hipblasLtHandle_t handle = at::cuda::getCurrentCUDABlasLtHandle();
+
+  Plan* plan;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+      Plan p;
+      LT_CHECK(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+      // swapped operands: hipBLASLt A := our B, hipBLASLt B := our A
+      hipblasOperation_t opa = trans_b ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+      hipblasOperation_t opb = trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opa, sizeof(opa)));
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opb, sizeof(opb)));
+      hipblasLtEpilogue_t ep = (hipblasLtEpilogue_t)epilogue;
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)));
+      if (has_bias) {
+        hipDataType bt = dt(*bias);
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+      }
+      if (has_aux) {
+        int64_t ld = aux->stride(0);
+        hipDataType at_ = dt(*aux);
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld)));
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at_,
+                                                 sizeof(at_)));
+      }
+      // hipBLASLt A (= our B): stored col-major as [N, K] (no trans) or [K, N] (trans)
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt(B), trans_b ? K : N, trans_b ? N : K, B.stride(0)));
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.b, dt(A), trans_a ? M : K, trans_a ? K : M, A.stride(0)));
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.c, dt(Ct), N, M, Ct.stride(0)));
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.d, dt(D), N, M, D.stride(0)));
+      hipblasLtMatmulPreference_t pref;
+      LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+      uint64_t wsb = ws_size;
+      LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
+                                                     sizeof(wsb)));
+      // the epilogue pointers must be set for the heuristic to see a complete problem
+      if (has_bias) {
+        void* bp = bias->data_ptr();
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
+      }
+      if (has_aux) {
+        void* ap = aux->data_ptr();
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &ap,
+                                                 sizeof(ap)));
+      }
+      hipblasLtMatmulHeuristicResult_t res[8];
+      int n = 0;
+      hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(handle, p.desc, p.a, p.b, p.c, p.d, pref, 8, res, &n);
+      hipblasLtMatmulPreferenceDestroy(pref);
+      for (int i = 0; st == HIPBLAS_STATUS_SUCCESS && i < n; ++i) {
+        if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= ws_size) {
+          p.algo = res[i].algo;
+          p.ws = res[i].workspaceSize;
+          p.ok = true;
+          break;
+        }
+      }
+      it = g_plans.emplace(key, p).first;
+    }
+    plan = &it->second;
+  }
+  if (!plan->ok) return false;
+  if (has_bias) {
+    void* bp = bias->data_ptr();
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(plan->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
+  }
+  if (has_aux) {
+    void* ap = aux->data_ptr();
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(plan->desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &ap,
+                                             sizeof(ap)));
+  }
+  const float al = (float)alpha, be = (float)beta;
+  LT_CHECK(hipblasLtMatmul(handle, plan->desc, &al, B.data_ptr(), plan->a, A.data_ptr(), plan->b, &be,
+                           Ct.data_ptr(), plan->c, D.data_ptr(), plan->d, &plan->algo, ws, plan->ws,
+                           at::hip::getCurrentHIPStream().stream()));
+  return true;
+}
+
+extern "C" int ct_gemm_nt(const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
+                          void*, long, float*, hipStream_t);
+
+// D[M,N] = A[M,K] @ B[N,K]^T through the hand-written MFMA kernel (csrc/gemm_nt.hip) with
+// epilogue 0 plain (accumulate: D +=), 1 bias + GELU keeping aux = pre-activation, 2 dGELU
+// with aux = pre-activation and dbias += column sums.  False when the shape is unsupported.
+bool gemm_nt(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumulate, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> aux, c10::optional<at::Tensor> dbias) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "gemm_nt: GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+              D.scalar_type() == at::kBFloat16, "gemm_nt: bf16 operands");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "gemm_nt: 2-D row-major operands");
+  const long M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && D.size(0) == M && D.size(1) == N, "gemm_nt: shape mismatch");
+  const bool hb = bias.has_value() && bias->defined(), ha = aux.has_value() && aux->defined(),
+             hd = dbias.has_value() && dbias->defined();
+  if (hb) TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                      "gemm_nt: bias");
+  if (ha) TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && rowmajor_ok(*aux) && aux->size(0) == M &&
+                      aux->size(1) == N, "gemm_nt: aux");
+  if (hd) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->is_contiguous() && dbias->numel() == N,
+                      "gemm_nt: dbias");
+  TORCH_CHECK(epi != 1 || (hb && ha), "gemm_nt: epilogue 1 needs bias and aux");
+  TORCH_CHECK(epi != 2 || ha, "gemm_nt: epilogue 2 needs aux");
+  int rc = ct_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0), (int)M,
+                      (int)N, (int)K, (int)epi, accumulate ? 1 : 0, hb ? bias->data_ptr() : nullptr,
+                      ha ? aux->data_ptr() : nullptr, ha ? aux->stride(0) : 0,
+                      hd ? dbias->data_ptr<float>() : nullptr, at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
+void register_lt(pybind11::module& m) {
+  m.def("gemm_nt", &gemm_nt, "hand-written MFMA GEMM A @ B^T with fused epilogues");
+  m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
+}

@@ -1,0 +1,362 @@
+// Forward / data-gradient GEMM for gfx950 with fused epilogues:
+//     D[M, N] = A[M, K] . B[N, K]^T   (bf16 in, fp32 accumulate; both operands K-contiguous)
+// epilogues: plain (optionally D += ...), bias + erf-GELU keeping the pre-activation
+// (BERT FFN1 forward), and dGELU + bias-gradient column sums (BERT FFN dgrad).  The point is
+// the epilogue: without it the [tokens, 4*hidden] activation makes one extra HBM round trip
+// per GEMM through a separate elementwise kernel (bias_act_fwd / bias_act_bwd, ~100-200 us
+// per layer on BERT-large).  hipBLASLt on this image offers no GELU_AUX / DGELU epilogue
+// kernels for bf16 on gfx950 (bench/lt_epilogue_probe.py), and its GELU is the tanh form.
+//
+// Structure (256 x 256 x 64 tile, 512 threads = 8 waves as 2 (M) x 4 (N), 128 x 64 per wave):
+//   * both operands staged global -> LDS with global_load_lds (16 B per lane, lane-linear
+//     LDS side, the 16-B chunk XOR swizzle (row >> 1) & 7 applied on the source address) into
+//     two 64 KiB buffers of four 16 KiB half-tile images each (cut by reading phase, below);
+//   * every K-tile runs as 4 phases, one per 64 x 32 quadrant of the wave's output; each phase
+//     = [ds_read_b128 fragments + LDS-DMA issue] barrier [16 MFMA 16x16x32] barrier;
+//   * the two wave groups (M halves) run one barrier apart ("ping-pong"): while one group
+//     multiplies, the other reads its fragments and issues the next DMA, so the SIMD sees a
+//     steady MFMA stream without register-double-buffered fragments;
+//   * exactly one half-tile DMA (2 glds per wave) and one counted vmcnt(8) per phase, four
+//     halves in flight; fragment reads 12 / 4 / 8 / 0 per phase (schedule: nt_stage_slot);
+//   * the MFMA is issued as B-fragment x A-fragment, so each lane ends up with 4 consecutive
+//     output COLUMNS of one row: 8-byte stores, and the bias / aux vectors load 8 bytes too;
+//   * blockIdx -> tile goes through the bijective XCD remap; N-tiles vary fastest so the
+//     blocks resident on one XCD share A panels in its L2.
+// Reference: the BERT encoder FFN (HF BertIntermediate + BertOutput).
+#include "common.h"
+#include <cstdlib>
+
+namespace ct {
+
+typedef __attribute__((ext_vector_type(8))) short nt_s16x8;
+typedef __attribute__((address_space(3))) nt_s16x8 nt_lds_s16x8;
+typedef __attribute__((address_space(3))) void nt_lds_void;
+
+constexpr int NT_BM = 256, NT_BN = 256, NT_BK = 64, NT_THREADS = 512;
+constexpr int NT_ROWB = NT_BK * 2;        // 128 B per LDS image row
+constexpr int NT_HALF = 128 * NT_ROWB;    // 16 KiB: 128 rows of one operand
+constexpr int NT_BUF = 4 * NT_HALF;       // 64 KiB per K-tile buffer
+
+enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2 };
+
+struct NtArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  bf16_t* D;
+  const bf16_t* bias;   // EPI 1: [N]; EPI 2 (optional): added to aux before gelu'
+  bf16_t* aux;          // EPI 1: pre-activation out; EPI 2: pre-activation in
+  float* dbias;         // EPI 2: [N] fp32, accumulated with atomics (may be null)
+  long lda, ldb, ldd, ldaux;
+  int M, N, K;
+  int accumulate;       // EPI 0: D += result
+};
+
+__device__ __forceinline__ int nt_swz(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void nt_glds16(const void* g, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(nt_lds_void*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
+}
+
+// 16 x 32 MFMA operand fragment: rows [r0, r0 + 16), k [32 ks, 32 ks + 32); lane l holds row
+// r0 + (l & 15), k 32 ks + 8 (l >> 4) .. + 8.  Conflict-free for ds_read_b128's lane groups.
+__device__ __forceinline__ nt_s16x8 nt_frag(const char* img, int r0, int ks, int lane) {
+  const int row = r0 + (lane & 15);
+  const int kc = ks * 4 + (lane >> 4);
+  return *(const nt_lds_s16x8*)(img + row * NT_ROWB + ((kc ^ nt_swz(row)) << 4));
+}
+
+__device__ __forceinline__ void nt_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void nt_mma_begin() {
+  nt_bar();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_setprio(1);
+}
+
+__device__ __forceinline__ void nt_mma_end() {
+  __builtin_amdgcn_s_setprio(0);
+  nt_bar();
+}
+
+// Half-tile images (16 KiB each, 128 rows x 64 k) are cut by the phase that reads them, not by
+// position: A0 = the first 64 rows of each wave group (tile rows 0-63, 128-191), A1 = the other
+// 64 (64-127, 192-255), B0 = the first 32 columns of each wave column (0-31, 64-95, ...), B1 = the
+// other 32.  Phase q0 reads A0 + B0, q1 B1, q2 A1, q3 nothing, so every half has its own last
+// read and is restaged as soon as that allows: one half per phase, in the order A0 B0 B1 A1,
+// virtual index v = 4 * tile - 6 + slot (tile 0 and half of tile 1 in the prologue, then the
+// half v = p at phase p).  Every phase waits vmcnt(8): the half issued 4 phases earlier has
+// landed, and it is first read 5 phases after its issue (one phase after the wait, as the
+// barrier offset between the wave groups requires); a half is restaged >= 2 phases after its
+// last read (WAR for the group that runs ahead).
+__device__ __forceinline__ void nt_stage_slot(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B,
+                                              long ldb, long m0, long n0, long k0, int slot, char* dst, int wave,
+                                              int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;
+    const int r = piece * 8 + (lane >> 3);               // image row 0..127
+    const int c = (lane & 7) ^ nt_swz(r);
+    const bf16_t* src;
+    if (slot == 0 || slot == 3) {                        // A0 / A1
+      const long row = m0 + ((r >> 6) << 7) + (slot == 3 ? 64 : 0) + (r & 63);
+      src = A + row * lda;
+    } else {                                             // B0 / B1
+      const long col = n0 + ((r >> 5) << 6) + (slot == 2 ? 32 : 0) + (r & 31);
+      src = B + col * ldb;
+    }
+    nt_glds16(src + k0 + c * 8, dst + piece * 1024);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void nt_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+struct NtCtx {
+  const bf16_t* A;
+  const bf16_t* B;
+  long lda, ldb, m0, n0;
+  char* lds;
+  int wave, lane, ra, rb;
+};
+
+// one 16-MFMA quadrant: acc[I0 + i][J0 + j] += A-frags fa[QM] x B-frags fb[QN]
+template <int I0, int J0>
+__device__ __forceinline__ void nt_quad(f32x4 (&acc)[8][4], const nt_s16x8 (&fa)[4][2], const nt_s16x8 (&fb)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb[j][ks], (bf16x8_t)fa[i][ks],
+                                                                       acc[I0 + i][J0 + j], 0, 0, 0);
+}
+
+// half with virtual index v (see above) -> its buffer slot
+__device__ __forceinline__ void nt_stage_v(const NtCtx& c, int v) {
+  const int T = (v + 6) >> 2, slot = (v + 6) & 3;
+  nt_stage_slot(c.A, c.lda, c.B, c.ldb, c.m0, c.n0, (long)T * NT_BK, slot,
+                c.lds + (T & 1) * NT_BUF + slot * NT_HALF, c.wave, c.lane);
+}
+
+
+// DMA plan of one K-tile t (POS: 0 steady, 1 = K-tile nk-2, 2 = the last K-tile): phase q
+// issues half v = 4t + q (virtual index, slot order A0 B0 B1 A1) and waits vmcnt(8) in steady
+// state (the half of 4 phases ago has landed).  Measured alternatives that change nothing
+// (within 2 %): two halves in each of the read-light phases q1 / q3 only, and DMA issued
+// before instead of after the phase's fragment reads.
+template <int POS>
+struct NtPlan {
+  static constexpr bool issue(int q) { return POS == 0 || (POS == 1 && q < 2); }
+  static constexpr int wait(int q) {
+    return POS == 0 ? 8 : (POS == 1 ? (q < 2 ? 8 : (q == 2 ? 6 : 4)) : (q == 0 ? 2 : 0));
+  }
+};
+
+template <int POS, int DIAG>
+__device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][4], nt_s16x8 (&fa)[2][4][2],
+                                         nt_s16x8 (&fb)[2][2][2]) {
+  const char* buf = c.lds + (t & 1) * NT_BUF;
+  constexpr bool WAIT = DIAG == 0, BAR = DIAG != 2;
+  constexpr bool DMA = DIAG == 0 || DIAG == 3;
+  using P = NtPlan<POS>;
+#define NT_PHASE_TAIL(Q, I0, J0, FA, FB)                                             \
+  if constexpr (DMA && P::issue(Q)) nt_stage_v(c, 4 * t + Q);                        \
+  if constexpr (WAIT) nt_vm<P::wait(Q)>();                                           \
+  if constexpr (BAR) nt_mma_begin(); else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+  nt_quad<I0, J0>(acc, FA, FB);                                                      \
+  if constexpr (BAR) nt_mma_end(); else __builtin_amdgcn_sched_barrier(0);
+  // ---- q0: B0 + A0 fragments
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = nt_frag(buf + 1 * NT_HALF, c.rb + j * 16, ks, c.lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fa[0][i][ks] = nt_frag(buf + 0 * NT_HALF, c.ra + i * 16, ks, c.lane);
+  NT_PHASE_TAIL(0, 0, 0, fa[0], fb[0])
+  // ---- q1: B1 fragments
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = nt_frag(buf + 2 * NT_HALF, c.rb + j * 16, ks, c.lane);
+  NT_PHASE_TAIL(1, 0, 2, fa[0], fb[1])
+  // ---- q2: A1 fragments
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fa[1][i][ks] = nt_frag(buf + 3 * NT_HALF, c.ra + i * 16, ks, c.lane);
+  NT_PHASE_TAIL(2, 4, 2, fa[1], fb[1])
+  // ---- q3: no fragment reads
+  NT_PHASE_TAIL(3, 4, 0, fa[1], fb[0])
+#undef NT_PHASE_TAIL
+}
+
+// DIAG (timing diagnostics only, wrong results): 1 = no DMA / vmcnt in the K loop (MFMA + LDS
+// reads + barriers), 2 = additionally no barriers (MFMA + LDS reads), 3 = DMA issued but never
+// waited for in the K loop
+template <int EPI, bool BGRAD, int DIAG = 0>
+__global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * NT_BUF];    // 128 KiB, the only LDS object
+  const int tiles_n = a.N / NT_BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = L / tiles_n, tn = L % tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const long m0 = (long)tm * NT_BM, n0 = (long)tn * NT_BN;
+  const int nk = a.K / NT_BK;
+  const NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, lds, wave, lane, wr * 64, wc * 32};
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  nt_s16x8 fa[2][4][2];   // [qm][frag][ks]: A rows wr*128 + qm*64 + 16 frag
+  nt_s16x8 fb[2][2][2];   // [qn][frag][ks]: B rows wc*64 + qn*32 + 16 frag
+
+  // prologue: halves -6 .. -1 (all of K-tile 0, A0 + B0 of K-tile 1); wait for tile 0's A0, B0
+#pragma unroll
+  for (int v = -6; v < -2; ++v) nt_stage_v(c, v);
+  if (nk > 1) {
+    nt_stage_v(c, -2);
+    nt_stage_v(c, -1);
+    nt_vm<8>();
+  } else {
+    nt_vm<4>();
+  }
+  nt_bar();
+  if (wr == 1) nt_bar();                                 // group 1 runs one barrier behind
+
+  // steady state: every phase issues one half and keeps 4 in flight; the last two K-tiles
+  // drain (halves beyond 4 nk - 7 do not exist)
+  int t = 0;
+  for (; t < nk - 2; ++t) nt_ktile<0, DIAG>(c, t, acc, fa, fb);
+  if (nk >= 2) {
+    nt_ktile<1, DIAG>(c, t, acc, fa, fb);
+    ++t;
+  }
+  nt_ktile<2, DIAG>(c, t, acc, fa, fb);
+  if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
+
+  // ---- epilogue: acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
+  const long mrow = m0 + wr * 128 + (lane & 15);
+  const long ncol = n0 + wc * 64 + (lane >> 4) * 4;
+  float bv[4][4] = {};
+  if (EPI == NT_EPI_BIAS_GELU_AUX || (EPI == NT_EPI_DGELU_BGRAD && a.bias)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u16x4 b = *(const u16x4*)(a.bias + ncol + j * 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[j][r] = bf2f(b[r]);
+    }
+  }
+  float cs[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = mrow + i * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long n = ncol + j * 16;
+      bf16_t* dp = a.D + m * a.ldd + n;
+      u16x4 out;
+      if constexpr (EPI == NT_EPI_PLAIN) {
+        if (a.accumulate) {
+          const u16x4 old = *(const u16x4*)dp;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r] + bf2f(old[r]));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r]);
+        }
+      } else if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) {
+        u16x4 pre;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r] + bv[j][r];
+          pre[r] = f2bf(v);
+          out[r] = f2bf(gelu_erf(v));
+        }
+        *(u16x4*)(a.aux + m * a.ldaux + n) = pre;
+      } else {
+        const u16x4 z = *(const u16x4*)(a.aux + m * a.ldaux + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = acc[i][j][r] * gelu_erf_grad(bf2f(z[r]) + bv[j][r]);
+          out[r] = f2bf(g);
+          if constexpr (BGRAD) cs[j][r] += g;
+        }
+      }
+      *(u16x4*)dp = out;
+    }
+  }
+  if constexpr (EPI == NT_EPI_DGELU_BGRAD && BGRAD) {
+    // column sums: reduce the 16 rows held by lanes sharing (lane >> 4), then one atomic per
+    // column per wave (vector-memory float atomics)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cs[j][r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if ((lane & 15) == 0) atomicAdd(a.dbias + ncol + j * 16 + r, v);
+      }
+  }
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+// D[M,N] = A[M,K] . B[N,K]^T (row-major, K-contiguous operands) with epilogue `epi`:
+//   0: plain (accumulate: D += result); 1: aux = result + bias, D = gelu(aux);
+//   2: D = result * gelu'(aux [+ bias]), dbias += column sums (bias, dbias may be null).
+// Returns nonzero (and launches nothing) when the shape / alignment is not supported.
+extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void* D, long ldd, int M, int N, int K,
+                          int epi, int accumulate, const void* bias, void* aux, long ldaux, float* dbias,
+                          hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % NT_BM || N % NT_BN || K % NT_BK) return 1;
+  if (lda % 8 || ldb % 8 || ldd % 4 || lda < K || ldb < K || ldd < N) return 2;
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 7)) return 3;
+  if (epi == 1 && (!bias || !aux || ((uintptr_t)bias & 7))) return 4;
+  if ((epi == 1 || epi == 2) && (!aux || ((uintptr_t)aux & 7) || ldaux % 4 || ldaux < N)) return 4;
+  if (bias && ((uintptr_t)bias & 7)) return 4;
+  const long blocks = (long)(M / NT_BM) * (N / NT_BN);
+  if (blocks > (1L << 30)) return 5;
+  NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias,
+           lda, ldb, ldd, ldaux, M, N, K, accumulate};
+  static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
+  if (diag == 1) { gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
+  if (diag == 2) { gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
+  if (diag == 3) { gemm_nt_kernel<0, false, 3><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
+  switch (epi) {
+    case 0: gemm_nt_kernel<0, false><<<(int)blocks, NT_THREADS, 0, stream>>>(a); break;
+    case 1: gemm_nt_kernel<1, false><<<(int)blocks, NT_THREADS, 0, stream>>>(a); break;
+    case 2:
+      if (dbias) gemm_nt_kernel<2, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+      else gemm_nt_kernel<2, false><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+      break;
+    default: return 6;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}

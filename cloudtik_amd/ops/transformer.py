@@ -21,6 +21,7 @@ Block structure (BERT / HF BertLayer, reference run_pretrain_mlperf.py:449-471):
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -30,6 +31,26 @@ from cloudtik_amd.ops.linear import wgrad_accumulate, wgrad_on_side_stream
 def _C():
     from cloudtik_amd import ops
     return ops.require_native()
+
+
+# FFN dgrad through the hand-written MFMA GEMM with the dGELU + bias-gradient epilogue
+# (csrc/gemm_nt.hip): dz = (df @ W2) * gelu'(z + b1) and db1 in one kernel instead of a
+# hipBLASLt GEMM + a bias_act_bwd pass over the [tokens, 4H] activation
+_FUSED_FFN_DGRAD = os.environ.get("CLOUDTIK_AMD_FUSED_FFN_DGRAD", "0") == "1"
+
+
+def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f):
+    """dz = (df @ W2) * gelu'(z + b1f); db1f += column sums of dz.  None when unsupported."""
+    T, F = z.shape
+    if T % 256 or F % 256 or df.shape[1] % 64:
+        return None
+    W2t = W2.t().contiguous()                     # [F, H]: K-contiguous B operand
+    dz = torch.empty_like(z)
+    db = torch.zeros(F, device=z.device, dtype=torch.float32)
+    if not C.gemm_nt(df, W2t, dz, 2, False, b1f, z, db):
+        return None
+    db1f.add_(db)
+    return dz
 
 
 def _flat(p) -> bool:
@@ -150,9 +171,11 @@ class _FFNBlockFn(torch.autograd.Function):
             df = ds
         _ready(*[p for p, f in ((g2, fg2), (b2, fb2), (b2f, fb2f)) if f])
         dW2 = _wgrad(W2, df, h)
-        dh = torch.mm(df, W2)
         db1f, fb1f = _vec_grad_out(b1f)
-        dz = C.bias_act_bwd_into(dh, z, b1f, 1, db1f, True)
+        dz = _fused_ffn_dgrad(C, df.contiguous(), W2, z, b1f, db1f) if _FUSED_FFN_DGRAD else None
+        if dz is None:
+            dh = torch.mm(df, W2)
+            dz = C.bias_act_bwd_into(dh, z, b1f, 1, db1f, True)
         if fb1f:
             _ready(b1f)
         dW1 = _wgrad(W1, dz, x2)

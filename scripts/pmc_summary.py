@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--pmc", nargs="+", required=True)
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--title", default="")
+    ap.add_argument("--raw", action="store_true", help="also list every counter's mean per kernel")
     a = ap.parse_args()
     dur = collections.defaultdict(list)
     for r in csv.DictReader(open(a.trace)):
@@ -44,6 +45,11 @@ def main():
         lds = (f"{c['SQ_LDS_BANK_CONFLICT']:.3g} / {c['SQ_INSTS_LDS']:.3g}"
                if "SQ_LDS_BANK_CONFLICT" in c and "SQ_INSTS_LDS" in c else "-")
         print(f"| `{name}` | {len(ds)} | {us:.1f} | {rd:.1f} | {wr:.1f} | {tbs:.2f} | {tf:.0f} | {busy:.0f} | {lds} |")
+    if a.raw:
+        print("\n| kernel | counter | mean per dispatch |\n|---|---|---:|")
+        for name, _ in rows:
+            for k, v in sorted(ctr.get(name, {}).items()):
+                print(f"| `{name[:40]}` | {k} | {sum(v) / len(v):.4g} |")
     print("\nTFLOP/s = "
           "SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 / duration; durations from a separate --kernel-trace run "
           "(counter runs are serialised and not timed).")

@@ -1,0 +1,97 @@
+"""Hand-written MFMA GEMM D = A @ B^T (csrc/gemm_nt.hip) and its fused epilogues against
+fp32 PyTorch references: plain / accumulate, bias + erf-GELU with the pre-activation kept,
+dGELU with bias-gradient column sums; K-tile counts 1, 2, 3 and 16 exercise the prologue,
+the steady-state DMA schedule and the drain; unsupported shapes are refused."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    from cloudtik_amd import ops
+    return ops.require_native()
+
+
+def _gelu(x):
+    return 0.5 * x * (1 + torch.erf(x / math.sqrt(2)))
+
+
+def _gelu_grad(x):
+    return 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+
+
+def _rand(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return (torch.randn(*shape, device="cuda", generator=g) * scale).to(torch.bfloat16)
+
+
+def _close(out, ref, tol=2e-2):
+    err = (out.float() - ref).abs().max().item()
+    assert err <= tol * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 256, 128), (256, 768, 192), (2048, 1024, 1024)])
+def test_gemm_nt_plain_and_accumulate(M, N, K):
+    C = _C()
+    A, B = _rand(M, K, seed=1), _rand(N, K, scale=K ** -0.5, seed=2)
+    D = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nt(A, B, D, 0, False, None, None, None)
+    ref = A.float() @ B.float().t()
+    _close(D, ref)
+    base = _rand(M, N, seed=3)
+    D2 = base.clone()
+    assert C.gemm_nt(A, B, D2, 0, True, None, None, None)
+    _close(D2, ref + base.float())
+
+
+def test_gemm_nt_bias_gelu_aux():
+    C = _C()
+    M, N, K = 1024, 512, 256
+    A, B, bias = _rand(M, K, seed=4), _rand(N, K, scale=K ** -0.5, seed=5), _rand(N, scale=0.5, seed=6)
+    h = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    aux = torch.empty_like(h)
+    assert C.gemm_nt(A, B, h, 1, False, bias, aux, None)
+    z = A.float() @ B.float().t() + bias.float()
+    _close(aux, z)
+    _close(h, _gelu(z))
+
+
+def test_gemm_nt_dgelu_bgrad():
+    C = _C()
+    M, N, K = 1024, 512, 320
+    A, B = _rand(M, K, seed=7), _rand(N, K, scale=K ** -0.5, seed=8)
+    aux = _rand(M, N, seed=9)
+    dz = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    db = torch.full((N,), 0.25, device="cuda", dtype=torch.float32)      # accumulates into existing
+    assert C.gemm_nt(A, B, dz, 2, False, None, aux, db)
+    ref = (A.float() @ B.float().t()) * _gelu_grad(aux.float())
+    _close(dz, ref)
+    torch.testing.assert_close(db, ref.sum(0) + 0.25, rtol=2e-3, atol=2e-2)
+    dz2 = torch.empty_like(dz)
+    assert C.gemm_nt(A, B, dz2, 2, False, None, aux, None)               # no bias gradient
+    assert torch.equal(dz, dz2)
+    # pre-activation = aux + bias (aux saved without the bias, as the FFN block does)
+    bias = _rand(N, scale=0.5, seed=12)
+    db3 = torch.zeros(N, device="cuda", dtype=torch.float32)
+    assert C.gemm_nt(A, B, dz2, 2, False, bias, aux, db3)
+    ref3 = (A.float() @ B.float().t()) * _gelu_grad(aux.float() + bias.float())
+    _close(dz2, ref3)
+    torch.testing.assert_close(db3, ref3.sum(0), rtol=2e-3, atol=2e-2)
+
+
+def test_gemm_nt_strided_operands_and_refusals():
+    C = _C()
+    big = _rand(512, 384, seed=10)
+    A = big[:, :256]                      # lda = 384
+    B = _rand(256, 256, seed=11)
+    D = torch.empty(512, 256, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nt(A, B, D, 0, False, None, None, None)
+    _close(D, A.float() @ B.float().t())
+    bad = torch.empty(500, 256, device="cuda", dtype=torch.bfloat16)
+    assert not C.gemm_nt(_rand(500, 256), B, bad, 0, False, None, None, None)     # M % 256
+    assert not C.gemm_nt(_rand(256, 96), _rand(256, 96), torch.empty(256, 256, device="cuda",
+                                                                      dtype=torch.bfloat16), 0, False, None, None,
+                         None)                                                     # K % 64

@@ -255,10 +255,21 @@ def test_wgrad_splitk_accumulate(cuda, N, K):
     assert _rel(g2, ref) < 5e-3
 
 
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_bert_layer_blocks_match_composed(cuda, p):
-    """Hand-scheduled block backward == composed-op autograd (same dropout streams)."""
+@pytest.mark.parametrize("p,fused", [(0.0, False), (0.1, False), (0.1, True)])
+def test_bert_layer_blocks_match_composed(cuda, p, fused, monkeypatch):
+    """Hand-scheduled block backward == composed-op autograd (same dropout streams); `fused`
+    routes the FFN dgrad through the MFMA GEMM with the dGELU + bias-gradient epilogue."""
     from cloudtik_amd.models.bert import BertConfig, BertLayer
+    from cloudtik_amd.ops import transformer as T
+    monkeypatch.setattr(T, "_FUSED_FFN_DGRAD", fused)
+    if fused:
+        calls = []
+        orig_fused = T._fused_ffn_dgrad
+        def spy(*a):
+            r = orig_fused(*a)
+            calls.append(r is not None)
+            return r
+        monkeypatch.setattr(T, "_fused_ffn_dgrad", spy)
     from cloudtik_amd.train.optim import FlatParamSpace
     cfg = BertConfig.tiny(hidden_size=256, num_attention_heads=4, intermediate_size=1024,
                           hidden_dropout_prob=p, attention_probs_dropout_prob=p)
@@ -290,6 +301,8 @@ def test_bert_layer_blocks_match_composed(cuda, p):
     assert _rel(y, y2) < 1e-2
     assert _rel(gx_blocks, x.grad) < 2e-2
     assert _rel(g_blocks, sp.grad.float()) < 2e-2
+    if fused:
+        assert calls and all(calls), "fused FFN dgrad path not taken"
 
 
 @pytest.mark.parametrize("name", ["adamw", "lamb"])
