@@ -58,6 +58,26 @@ __device__ __forceinline__ void nt_glds16(const void* g, const char* lds_wave_ba
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
 }
 
+// same, addressed as a wave-uniform 64-bit base (SGPRs) + a per-lane 32-bit byte offset: no
+// per-lane 64-bit address arithmetic and no address VGPR pairs to keep live
+__device__ __forceinline__ void nt_glds16s(const void* sbase, unsigned voff, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(nt_lds_void*)lds_wave_base);
+  // (readfirstlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends
+  // into the high word)
+  const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)sbase) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)sbase >> 32)) << 32);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
+               : "memory", "m0");
+}
+
+// per-lane byte offset of a staging piece: row (lane >> 3) of the piece's 8, 16-B chunk
+// (lane & 7) ^ swizzle; the swizzle of image row piece*8 + (lane >> 3) depends on the piece
+// only through its parity
+__device__ __forceinline__ unsigned nt_lane_off(long ld, int parity, int lane) {
+  const int cc = (lane & 7) ^ ((parity * 4 + (lane >> 4)) & 7);
+  return (unsigned)(((lane >> 3) * ld + cc * 8) * 2);
+}
+
 // 16 x 32 MFMA operand fragment: rows [r0, r0 + 16), k [32 ks, 32 ks + 32); lane l holds row
 // r0 + (l & 15), k 32 ks + 8 (l >> 4) .. + 8.  Conflict-free for ds_read_b128's lane groups.
 __device__ __forceinline__ nt_s16x8 nt_frag(const char* img, int r0, int ks, int lane) {
@@ -101,18 +121,17 @@ __device__ __forceinline__ void nt_stage_slot(const bf16_t* __restrict__ A, long
                                               int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int piece = wave * 2 + i;
-    const int r = piece * 8 + (lane >> 3);               // image row 0..127
-    const int c = (lane & 7) ^ nt_swz(r);
-    const bf16_t* src;
+    const int piece = wave * 2 + i;                      // image rows piece*8 .. +8
+    const bf16_t* base;
+    unsigned off;
     if (slot == 0 || slot == 3) {                        // A0 / A1
-      const long row = m0 + ((r >> 6) << 7) + (slot == 3 ? 64 : 0) + (r & 63);
-      src = A + row * lda;
+      base = A + (m0 + ((piece >> 3) << 7) + (slot == 3 ? 64 : 0) + (piece & 7) * 8) * lda + k0;
+      off = nt_lane_off(lda, i, lane);
     } else {                                             // B0 / B1
-      const long col = n0 + ((r >> 5) << 6) + (slot == 2 ? 32 : 0) + (r & 31);
-      src = B + col * ldb;
+      base = B + (n0 + ((piece >> 2) << 6) + (slot == 2 ? 32 : 0) + (piece & 3) * 8) * ldb + k0;
+      off = nt_lane_off(ldb, i, lane);
     }
-    nt_glds16(src + k0 + c * 8, dst + piece * 1024);
+    nt_glds16s(base, off, dst + piece * 1024);
   }
 }
 
@@ -203,6 +222,80 @@ __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][
 #undef NT_PHASE_TAIL
 }
 
+// epilogue over one wave's accumulators: acc[i][j][r] holds D[mrow + 16i][ncol + 16j + r]
+template <int EPI, bool BGRAD, int NJ>
+__device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[8][NJ], long mrow, long ncol,
+                                            int lane) {
+  float bv[NJ][4] = {};
+  if (EPI == NT_EPI_BIAS_GELU_AUX || (EPI == NT_EPI_DGELU_BGRAD && a.bias)) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const u16x4 b = *(const u16x4*)(a.bias + ncol + j * 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[j][r] = bf2f(b[r]);
+    }
+  }
+  float cs[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const long m = mrow + i * 16;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const long n = ncol + j * 16;
+      bf16_t* dp = a.D + m * a.ldd + n;
+      u16x4 out;
+      if constexpr (EPI == NT_EPI_PLAIN) {
+        if (a.accumulate) {
+          const u16x4 old = *(const u16x4*)dp;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r] + bf2f(old[r]));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r]);
+        }
+      } else if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) {
+        u16x4 pre;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r] + bv[j][r];
+          pre[r] = f2bf(v);
+          out[r] = f2bf(gelu_erf(v));
+        }
+        *(u16x4*)(a.aux + m * a.ldaux + n) = pre;
+      } else {
+        const u16x4 z = *(const u16x4*)(a.aux + m * a.ldaux + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = acc[i][j][r] * gelu_erf_grad(bf2f(z[r]) + bv[j][r]);
+          out[r] = f2bf(g);
+          if constexpr (BGRAD) cs[j][r] += g;
+        }
+      }
+      *(u16x4*)dp = out;
+    }
+  }
+  if constexpr (EPI == NT_EPI_DGELU_BGRAD && BGRAD) {
+    // column sums: reduce the 16 rows held by lanes sharing (lane >> 4), then one atomic per
+    // column per wave (vector-memory float atomics)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cs[j][r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if ((lane & 15) == 0) atomicAdd(a.dbias + ncol + j * 16 + r, v);
+      }
+  }
+}
+
 // DIAG (timing diagnostics only, wrong results): 1 = no DMA / vmcnt in the K loop (MFMA + LDS
 // reads + barriers), 2 = additionally no barriers (MFMA + LDS reads), 3 = DMA issued but never
 // waited for in the K loop
@@ -251,77 +344,8 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   nt_ktile<2, DIAG>(c, t, acc, fa, fb);
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 
-  // ---- epilogue: acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
-  const long mrow = m0 + wr * 128 + (lane & 15);
-  const long ncol = n0 + wc * 64 + (lane >> 4) * 4;
-  float bv[4][4] = {};
-  if (EPI == NT_EPI_BIAS_GELU_AUX || (EPI == NT_EPI_DGELU_BGRAD && a.bias)) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u16x4 b = *(const u16x4*)(a.bias + ncol + j * 16);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[j][r] = bf2f(b[r]);
-    }
-  }
-  float cs[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
-
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const long m = mrow + i * 16;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long n = ncol + j * 16;
-      bf16_t* dp = a.D + m * a.ldd + n;
-      u16x4 out;
-      if constexpr (EPI == NT_EPI_PLAIN) {
-        if (a.accumulate) {
-          const u16x4 old = *(const u16x4*)dp;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r] + bf2f(old[r]));
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r]);
-        }
-      } else if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) {
-        u16x4 pre;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = acc[i][j][r] + bv[j][r];
-          pre[r] = f2bf(v);
-          out[r] = f2bf(gelu_erf(v));
-        }
-        *(u16x4*)(a.aux + m * a.ldaux + n) = pre;
-      } else {
-        const u16x4 z = *(const u16x4*)(a.aux + m * a.ldaux + n);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = acc[i][j][r] * gelu_erf_grad(bf2f(z[r]) + bv[j][r]);
-          out[r] = f2bf(g);
-          if constexpr (BGRAD) cs[j][r] += g;
-        }
-      }
-      *(u16x4*)dp = out;
-    }
-  }
-  if constexpr (EPI == NT_EPI_DGELU_BGRAD && BGRAD) {
-    // column sums: reduce the 16 rows held by lanes sharing (lane >> 4), then one atomic per
-    // column per wave (vector-memory float atomics)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = cs[j][r];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if ((lane & 15) == 0) atomicAdd(a.dbias + ncol + j * 16 + r, v);
-      }
-  }
+  // acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
+  nt_epilogue<EPI, BGRAD, 4>(a, acc, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + (lane >> 4) * 4, lane);
 }
 
 }  // namespace ct
@@ -346,6 +370,17 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias,
            lda, ldb, ldd, ldaux, M, N, K, accumulate};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
+  switch (epi) {
+      case 0: gemm_nt4_kernel<0, false><<<(int)blocks, N4_THREADS, 0, stream>>>(a); break;
+      case 1: gemm_nt4_kernel<1, false><<<(int)blocks, N4_THREADS, 0, stream>>>(a); break;
+      case 2:
+        if (dbias) gemm_nt4_kernel<2, true><<<(int)blocks, N4_THREADS, 0, stream>>>(a);
+        else gemm_nt4_kernel<2, false><<<(int)blocks, N4_THREADS, 0, stream>>>(a);
+        break;
+      default: return 6;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : 7;
+  }
   if (diag == 1) { gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
   if (diag == 2) { gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
   if (diag == 3) { gemm_nt_kernel<0, false, 3><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }

@@ -95,3 +95,18 @@ def test_gemm_nt_strided_operands_and_refusals():
     assert not C.gemm_nt(_rand(256, 96), _rand(256, 96), torch.empty(256, 256, device="cuda",
                                                                       dtype=torch.bfloat16), 0, False, None, None,
                          None)                                                     # K % 64
+
+
+def test_gemm_nt_operands_spanning_4gb_addresses():
+    """Operand rows whose addresses span > 2^32 bytes (the staging addresses are split into a
+    wave-uniform 64-bit base + a 32-bit lane offset: a sign-extension bug would fault here)."""
+    C = _C()
+    big = torch.empty(5 * 2 ** 30 // 2, device="cuda", dtype=torch.bfloat16)     # 5 GiB
+    M, N, K = 512, 256, 2 ** 22                                                   # rows 8 MiB apart:
+    A2 = big[: M * K].view(M, K)[:, :256]                                         # 4 GiB of addresses
+    B = _rand(N, 256, seed=13)
+    A2.copy_(_rand(M, 256, seed=14))
+    D = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nt(A2, B, D, 0, False, None, None, None)
+    _close(D, A2.float() @ B.float().t())
+    del A2, big
