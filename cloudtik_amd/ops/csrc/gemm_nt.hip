@@ -370,17 +370,6 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias,
            lda, ldb, ldd, ldaux, M, N, K, accumulate};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
-  switch (epi) {
-      case 0: gemm_nt4_kernel<0, false><<<(int)blocks, N4_THREADS, 0, stream>>>(a); break;
-      case 1: gemm_nt4_kernel<1, false><<<(int)blocks, N4_THREADS, 0, stream>>>(a); break;
-      case 2:
-        if (dbias) gemm_nt4_kernel<2, true><<<(int)blocks, N4_THREADS, 0, stream>>>(a);
-        else gemm_nt4_kernel<2, false><<<(int)blocks, N4_THREADS, 0, stream>>>(a);
-        break;
-      default: return 6;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : 7;
-  }
   if (diag == 1) { gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
   if (diag == 2) { gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
   if (diag == 3) { gemm_nt_kernel<0, false, 3><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
