@@ -7,6 +7,8 @@
     cloudtik-run --hostfile hosts --launcher mpi train.py
     cloudtik-run -m package.module args                    # python -m
     cloudtik-run --no-python ./binary args
+    cloudtik-run --launcher cpu --throughput-mode infer.py # CPU job: one process per socket
+    cloudtik-run --cpu --hosts h1,h2 --ncores-per-proc 8 prep.py   # CPU job on 2 nodes
 """
 from __future__ import annotations
 
@@ -30,8 +32,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--master-addr", "--master_addr", default="",
                    help="Rendezvous address (default: the first host, or 127.0.0.1 on one node).")
     p.add_argument("--master-port", "--master_port", type=int, default=29500)
-    p.add_argument("--launcher", default="", choices=["", "local", "distributed", "rsh", "mpi", "horovod",
+    p.add_argument("--launcher", default="", choices=["", "local", "cpu", "distributed", "rsh", "mpi", "horovod",
                                                       "horovod-local"])
+    p.add_argument("--cpu", action="store_true",
+                   help="CPU processes placed by the core-pool scheduler (with --hosts: on every node)")
     p.add_argument("--rsh", default=None, help="Remote shell for the rsh/distributed launcher.")
     p.add_argument("--node-rank", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--first-rank", type=int, default=0, help=argparse.SUPPRESS)
@@ -50,6 +54,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--profile", default="",
                    help="Run every rank under 'rocprofv3 --kernel-trace --stats'; output in DIR/rank<R>.")
     p.add_argument("--verbose", action="store_true")
+    from cloudtik_amd.runner.cpu import add_cpu_args
+    add_cpu_args(p)
     p.add_argument("program")
     p.add_argument("program_args", nargs=argparse.REMAINDER)
     return p
@@ -57,8 +63,11 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
+    if args.launcher == "cpu":
+        args.cpu = True
     d = Distributor(args.num_proc, args.nnodes, args.nproc_per_node, args.hosts or None, args.hostfile or None)
-    launcher = args.launcher or ("distributed" if d.distributed_with_hosts and d.nnodes > 1 else "local")
+    launcher = args.launcher or ("distributed" if d.distributed_with_hosts and d.nnodes > 1 else
+                                 ("cpu" if args.cpu else "local"))
     args.launcher = launcher
     if args.resume:
         os.environ["CLOUDTIK_RESUME"] = "1"

@@ -109,8 +109,14 @@ class LocalLauncher(Launcher):
                 except (ProcessLookupError, PermissionError):
                     pass
 
-    def run(self) -> int:
+    def rank_plan(self):
+        """[(argv prefix, extra env, cpus)] per local rank: GPU ranks pinned to their GPU's
+        NUMA-node cores."""
         cpu_sets = rank_cpu_sets(self.local_world) if self.args.bind_cpus else {}
+        return [([], {}, cpu_sets.get(lr)) for lr in range(self.local_world)]
+
+    def run(self) -> int:
+        plan = self.rank_plan()
         prog = self.program()
         log_dir = self.args.log_dir
         if log_dir:
@@ -119,9 +125,10 @@ class LocalLauncher(Launcher):
         from cloudtik_amd.core.node.reaper import Reaper
         reaper = Reaper()
         for lr in range(self.local_world):
-            cpus = cpu_sets.get(lr)
+            prefix, extra_env, cpus = plan[lr]
             env = self.rank_env(lr, cpus)
-            argv = prog
+            env.update(extra_env)
+            argv = prefix + prog
             if getattr(self.args, "profile", ""):
                 # rocprofv3 per rank; the program follows '--' directly (no shell/env hop)
                 from cloudtik_amd.utils.profiling import rocprof_command
@@ -132,14 +139,14 @@ class LocalLauncher(Launcher):
                 rank = self.first_rank + lr
                 out = open(os.path.join(log_dir, f"{self.args.log_file_prefix}_{rank}.log"), "ab")
 
-            def pre(c=cpus):
+            def pre(c=None if prefix else cpus):
                 if c:
                     try:
                         os.sched_setaffinity(0, c)
                     except OSError:
                         pass
             if self.args.verbose:
-                print(f"[cloudtik-run] rank {env['RANK']} (local {lr}) cpus={cpus}: {' '.join(prog)}",
+                print(f"[cloudtik-run] rank {env['RANK']} (local {lr}) cpus={cpus}: {' '.join(argv)}",
                       file=sys.stderr)
             self.procs.append(subprocess.Popen(argv, env=env, stdout=out, stderr=subprocess.STDOUT if out else None,
                                                preexec_fn=pre, start_new_session=True))
@@ -173,6 +180,29 @@ class LocalLauncher(Launcher):
         return rc if rc >= 0 else 128 - rc
 
 
+class CpuLauncher(LocalLauncher):
+    """CPU processes on this node placed by the core-pool scheduler (runner/cpu.py): per
+    process a core list, a numactl / taskset prefix, OMP_NUM_THREADS and the allocator /
+    OpenMP-runtime preloads (reference runtime/ai/runner/cpu/local_launcher.py:222-352)."""
+
+    def rank_plan(self):
+        from cloudtik_amd.runner.cpu import cpu_plan
+        a = self.args
+        if a.local_world:
+            # a remote node launcher: its share of the job is fixed by the driver
+            a.num_proc = a.local_world
+        plan = cpu_plan(a)
+        self.local_world = len(plan)
+        if self.node_rank == 0 and self.first_rank == 0 and self.d.nnodes <= 1:
+            self.d.num_proc = len(plan)
+        if a.verbose:
+            for i, (prefix, env, cpus) in enumerate(plan):
+                print(f"[cloudtik-run] cpu process {i}: {' '.join(prefix) or '(affinity mask)'} "
+                      f"OMP_NUM_THREADS={env.get('OMP_NUM_THREADS')} LD_PRELOAD={env.get('LD_PRELOAD', '')}",
+                      file=sys.stderr)
+        return [(prefix, env, cpus) for prefix, env, cpus in plan]
+
+
 class DistributedLauncher(Launcher):
     """Runs the local launcher on every host of the job."""
 
@@ -180,7 +210,8 @@ class DistributedLauncher(Launcher):
 
     def remote_command(self, host: str, node_rank: int, local_world: int, first_rank: int) -> str:
         a = self.args
-        parts = ["cloudtik-run", "--launcher", "local" if a.launcher != "horovod" else "horovod-local",
+        local = "horovod-local" if a.launcher == "horovod" else ("cpu" if getattr(a, "cpu", False) else "local")
+        parts = ["cloudtik-run", "--launcher", local,
                  "--node-rank", str(node_rank), "--first-rank", str(first_rank),
                  "--local-world", str(local_world), "--num-proc", str(self.d.num_proc),
                  "--nproc-per-node", str(self.d.nproc_per_node),
@@ -195,6 +226,9 @@ class DistributedLauncher(Launcher):
             parts.append("--no-bind-cpus")
         if getattr(a, "profile", ""):
             parts += ["--profile", a.profile]
+        if getattr(a, "cpu", False):
+            from cloudtik_amd.runner.cpu import cpu_flags_argv
+            parts += cpu_flags_argv(a)
         parts += [a.program] + list(a.program_args)
         keep = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "CLOUDTIK_",
                                                                        "TORCH_", "PYTHONPATH", "MIOPEN_"))}
@@ -300,6 +334,9 @@ class MPILauncher(Launcher):
 
 
 def create_launcher(name: str, args, distributor: Distributor) -> Launcher:
+    if name == "cpu" or (name == "local" and getattr(args, "cpu", False)):
+        args.cpu = True
+        return CpuLauncher(args, distributor, args.node_rank, args.first_rank, args.local_world or None)
     if name in ("local", "horovod-local"):
         if name == "horovod-local":
             args.launcher = "horovod"
