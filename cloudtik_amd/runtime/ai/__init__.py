@@ -10,3 +10,9 @@ _script_aliases_ = {
     "ai.modeling.gbdt": "cloudtik_amd.modeling.gbdt.run",
     "ai.modeling.transfer_learning": "cloudtik_amd.modeling.transfer_learning.run",
 }
+
+# in-process fixes for the cloud-storage / tracking libraries the AI runtime drives
+# (reference runtime/ai/conf/patches; see patches.py): applied when they get imported
+from cloudtik_amd.runtime.ai import patches as _patches  # noqa: E402
+
+_patches.install()
