@@ -17,6 +17,12 @@ _CUSTOM = {
     "hdfs": ("cloudtik_amd.runtime.hadoop.runtimes", "HdfsRuntime"),
     "yarn": ("cloudtik_amd.runtime.hadoop.runtimes", "YarnRuntime"),
     "spark": ("cloudtik_amd.runtime.hadoop.runtimes", "SparkRuntime"),
+    # service runtimes that render their own configuration (cloudtik_amd/runtime/configured.py)
+    **{n: ("cloudtik_amd.runtime.configured", c) for n, c in (
+        ("zookeeper", "ZooKeeperRuntime"), ("kafka", "KafkaRuntime"), ("redis", "RedisRuntime"),
+        ("mongodb", "MongoDBRuntime"), ("consul", "ConsulRuntime"), ("etcd", "EtcdRuntime"),
+        ("coredns", "CoreDNSRuntime"), ("mysql", "MySQLRuntime"), ("postgres", "PostgresRuntime"),
+        ("prometheus", "PrometheusRuntime"), ("grafana", "GrafanaRuntime"), ("haproxy", "HAProxyRuntime"))},
 }
 
 

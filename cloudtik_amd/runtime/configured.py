@@ -1,0 +1,363 @@
+"""Self-configuring service runtimes: the configuration files the catalogue's start commands
+expect, rendered per node at ``cloudtik runtime configure`` time (reference
+runtime/{zookeeper,kafka,redis,mongodb,consul,etcd,coredns,mysql,postgres,prometheus,grafana,
+haproxy}/scripts/configure.{sh,py} + conf templates -- server ensembles from the quorum
+members, broker / server ids from node sequence ids, replication wiring to the head).
+
+Membership comes from the provider while the node's setup environment is built
+(``with_environment_variables``: the workers of this cluster -- of the same quorum when the
+runtime forms one -- sorted by sequence id, as ``<NAME>_MEMBERS=seq@ip,...``), so every member
+of a quorum is configured with the same ensemble.  Settings come from the cluster's
+``runtime.<name>`` section (same keys as the reference schema, see schema/build.py).  Each
+runtime's ``files()`` maps absolute paths to file contents; ``node_configure`` writes them and
+then runs the catalogue's configure steps.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Any, Dict, List, Optional, Tuple
+
+from cloudtik_amd.core import tags as T
+from cloudtik_amd.runtime.catalog import SPEC_BY_NAME, CatalogRuntime
+
+DATA_DISK_GLOB = "/mnt/cloudtik/data_disk_*"
+
+
+def members_of(provider, node_id: Optional[str], quorum: bool) -> List[Tuple[int, str]]:
+    """(seq id, internal ip) of the cluster's workers (same quorum id as ``node_id`` when it
+    has one), in sequence order."""
+    qid = provider.node_tags(node_id).get(T.CLOUDTIK_TAG_QUORUM_ID) if (quorum and node_id) else None
+    out = []
+    for n in provider.non_terminated_nodes({T.CLOUDTIK_TAG_NODE_KIND: T.NODE_KIND_WORKER}):
+        t = provider.node_tags(n)
+        if qid and t.get(T.CLOUDTIK_TAG_QUORUM_ID) != qid:
+            continue
+        seq = t.get(T.CLOUDTIK_TAG_NODE_SEQ_ID) or "0"
+        out.append((int(seq) if str(seq).isdigit() else 0, provider.internal_ip(n)))
+    return sorted(out)
+
+
+def parse_members(s: str) -> List[Tuple[int, str]]:
+    out = []
+    for item in (s or "").split(","):
+        if "@" in item:
+            seq, ip = item.split("@", 1)
+            out.append((int(seq), ip))
+    return out
+
+
+def _props(d: Dict[str, Any]) -> str:
+    return "".join(f"{k}={v}\n" for k, v in d.items())
+
+
+class ConfiguredRuntime(CatalogRuntime):
+    """Catalogue runtime + rendered configuration files."""
+
+    members_env = ""           # e.g. ZOOKEEPER_MEMBERS; "" = no membership needed
+    quorum_members = True      # restrict membership to this node's quorum
+
+    def with_environment_variables(self, config, provider, node_id):
+        env = super().with_environment_variables(config, provider, node_id)
+        if self.members_env and provider is not None:
+            m = members_of(provider, node_id, self.quorum_members)
+            env[self.members_env] = ",".join(f"{s}@{ip}" for s, ip in m)
+        return env
+
+    # ---------------------------------------------------------------- node side
+    def ctx(self, head: bool, env: Dict[str, str]) -> Dict[str, Any]:
+        rp = env.get("RUNTIME_PATH", "")
+        home = env.get(self.spec.home_env) if self.spec.home_env else None
+        seq = env.get("CLOUDTIK_NODE_SEQ_ID") or "1"
+        return {"head": head, "rp": rp, "dir": os.path.join(rp, self.name), "home": home or os.path.join(rp, self.name),
+                "ip": env.get("CLOUDTIK_NODE_IP") or "127.0.0.1",
+                "head_ip": env.get("CLOUDTIK_HEAD_IP") or env.get("CLOUDTIK_NODE_IP") or "127.0.0.1",
+                "seq": int(seq) if str(seq).isdigit() else 1, "cluster": env.get("CLOUDTIK_CLUSTER", "cloudtik"),
+                "members": parse_members(env.get(self.members_env, "")) if self.members_env else [],
+                "cfg": self.runtime_config or {}}
+
+    def files(self, c: Dict[str, Any]) -> Dict[str, str]:
+        return {}
+
+    def render(self, head: bool) -> Dict[str, str]:
+        env = self.node_env(head)
+        out = self.files(self.ctx(head, env))
+        for path, text in out.items():
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "w") as f:
+                f.write(text)
+        return out
+
+    def node_configure(self, head: bool):
+        self.render(head)
+        return self._run_steps(self.configure_steps(head), head)
+
+
+def _extra(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    return dict(cfg.get("config", {}) or {})
+
+
+# ----------------------------------------------------------------------------- ZooKeeper
+class ZooKeeperRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["zookeeper"]
+    members_env = "ZOOKEEPER_MEMBERS"
+
+    def files(self, c):
+        if c["head"]:
+            return {}
+        data = os.path.join(c["dir"], "data")
+        conf = {"tickTime": 2000, "initLimit": 10, "syncLimit": 5, "dataDir": data, "clientPort": 2181,
+                "4lw.commands.whitelist": "srvr,ruok,mntr,stat", "admin.enableServer": "false"}
+        conf.update(_extra(c["cfg"]))
+        servers = "".join(f"server.{s}={ip}:2888:3888\n" for s, ip in c["members"])
+        return {os.path.join(c["home"], "conf", "zoo.cfg"): _props(conf) + servers,
+                os.path.join(data, "myid"): f"{c['seq']}\n"}
+
+
+# ----------------------------------------------------------------------------- Kafka
+class KafkaRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["kafka"]
+    members_env = "KAFKA_MEMBERS"
+    quorum_members = False
+
+    def with_environment_variables(self, config, provider, node_id):
+        env = super().with_environment_variables(config, provider, node_id)
+        rc = (config or {}).get("runtime", {}) or {}
+        zk = (rc.get("kafka", {}) or {}).get("zookeeper_connect")
+        if not zk and "zookeeper" in (rc.get("types") or []) and provider is not None:
+            # ZooKeeper of the same cluster: its members (all workers run it)
+            zk = ",".join(f"{ip}:2181" for _, ip in members_of(provider, node_id, False))
+        if zk:
+            env["KAFKA_ZOOKEEPER_CONNECT"] = zk
+        return env
+
+    def ctx(self, head, env):
+        c = super().ctx(head, env)
+        c["zk"] = env.get("KAFKA_ZOOKEEPER_CONNECT") or c["cfg"].get("zookeeper_connect") or f"{c['head_ip']}:2181"
+        return c
+
+    def files(self, c):
+        if c["head"]:
+            return {}
+        import glob
+        disks = sorted(glob.glob(DATA_DISK_GLOB))
+        logs = ",".join(os.path.join(d, "kafka-logs") for d in disks) or os.path.join(c["dir"], "kafka-logs")
+        rf = max(1, min(3, len(c["members"]) or 1))
+        conf = {"broker.id": c["seq"], "listeners": f"PLAINTEXT://{c['ip']}:9092",
+                "advertised.listeners": f"PLAINTEXT://{c['ip']}:9092", "log.dirs": logs,
+                "zookeeper.connect": c["zk"], "num.partitions": 8, "default.replication.factor": rf,
+                "offsets.topic.replication.factor": rf, "transaction.state.log.replication.factor": rf,
+                "transaction.state.log.min.isr": max(1, rf - 1), "log.retention.hours": 168,
+                "num.network.threads": 8, "num.io.threads": 16}
+        conf.update(_extra(c["cfg"]))
+        return {os.path.join(c["home"], "config", "server.properties"): _props(conf)}
+
+
+# ----------------------------------------------------------------------------- Redis
+class RedisRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["redis"]
+
+    def files(self, c):
+        cfg = c["cfg"]
+        mode = cfg.get("cluster_mode", "none")
+        port = int(cfg.get("port", 6379))
+        lines = ["bind 0.0.0.0", f"port {port}", f"dir {os.path.join(c['dir'], 'data')}", "appendonly yes",
+                 f"logfile {os.path.join(c['dir'], 'logs', 'redis.log')}", "protected-mode no"]
+        if cfg.get("password"):
+            lines += [f"requirepass {cfg['password']}", f"masterauth {cfg['password']}"]
+        if mode == "replication" and not c["head"]:
+            lines.append(f"replicaof {c['head_ip']} {port}")
+        elif mode == "sharding":
+            lines += ["cluster-enabled yes", f"cluster-config-file {os.path.join(c['dir'], 'data', 'nodes.conf')}",
+                      "cluster-node-timeout 5000"]
+        lines += [f"{k} {v}" for k, v in _extra(cfg).items()]
+        return {os.path.join(c["dir"], "redis.conf"): "\n".join(lines) + "\n"}
+
+    def configure_steps(self, head):
+        return [f"mkdir -p $RUNTIME_PATH/redis/data $RUNTIME_PATH/redis/logs"]
+
+
+# ----------------------------------------------------------------------------- MongoDB
+class MongoDBRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["mongodb"]
+
+    def files(self, c):
+        cfg = c["cfg"]
+        conf = {"storage": {"dbPath": os.path.join(c["dir"], "data")},
+                "net": {"port": int(cfg.get("port", 27017)), "bindIp": "0.0.0.0"},
+                "systemLog": {"destination": "file", "path": os.path.join(c["dir"], "logs", "mongod.log"),
+                              "logAppend": True},
+                "processManagement": {"fork": True}}
+        if cfg.get("cluster_mode", "none") == "replication":
+            conf["replication"] = {"replSetName": cfg.get("replication_set_name") or f"{c['cluster']}-rs"}
+        import yaml
+        return {os.path.join(c["dir"], "mongod.conf"): yaml.safe_dump(conf, sort_keys=False)}
+
+    def configure_steps(self, head):
+        return ["mkdir -p $RUNTIME_PATH/mongodb/data $RUNTIME_PATH/mongodb/logs"]
+
+
+# ----------------------------------------------------------------------------- Consul
+class ConsulRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["consul"]
+    members_env = "CONSUL_MEMBERS"
+
+    def files(self, c):
+        cfg = c["cfg"]
+        servers_on_workers = bool(cfg.get("server", False))
+        server = (not c["head"]) if servers_on_workers else c["head"]
+        join = [ip for _, ip in c["members"]] if servers_on_workers else [c["head_ip"]]
+        conf = {"datacenter": cfg.get("data_center") or c["cluster"], "data_dir": os.path.join(c["dir"], "data"),
+                "bind_addr": c["ip"], "client_addr": "0.0.0.0", "server": server,
+                "retry_join": [ip for ip in join if ip != c["ip"]] or join,
+                "ports": {"http": int(cfg.get("http_port", 8500)), "dns": int(cfg.get("dns_port", 8600))},
+                "ui_config": {"enabled": bool(server)}}
+        if server:
+            conf["bootstrap_expect"] = len(join) if servers_on_workers else 1
+        if not cfg.get("disable_cluster_node_name"):
+            conf["node_name"] = f"{c['cluster']}-{c['seq']}"
+        return {os.path.join(c["dir"], "consul.d", "consul.json"): json.dumps(conf, indent=2) + "\n"}
+
+
+# ----------------------------------------------------------------------------- etcd
+class EtcdRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["etcd"]
+    members_env = "ETCD_MEMBERS"
+
+    def files(self, c):
+        if c["head"]:
+            return {}
+        import yaml
+        peers = ",".join(f"etcd{s}=http://{ip}:2380" for s, ip in c["members"])
+        conf = {"name": f"etcd{c['seq']}", "data-dir": os.path.join(c["dir"], "data"),
+                "listen-peer-urls": f"http://{c['ip']}:2380",
+                "listen-client-urls": f"http://{c['ip']}:2379,http://127.0.0.1:2379",
+                "initial-advertise-peer-urls": f"http://{c['ip']}:2380",
+                "advertise-client-urls": f"http://{c['ip']}:2379", "initial-cluster": peers,
+                "initial-cluster-token": f"cloudtik-{c['cluster']}", "initial-cluster-state": "new"}
+        return {os.path.join(c["dir"], "etcd.yaml"): yaml.safe_dump(conf, sort_keys=False)}
+
+
+# ----------------------------------------------------------------------------- CoreDNS
+class CoreDNSRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["coredns"]
+
+    def files(self, c):
+        port = int(c["cfg"].get("port", 53))
+        text = (f"consul:{port} {{\n    forward . 127.0.0.1:8600\n    cache 30\n}}\n"
+                f".:{port} {{\n    forward . /etc/resolv.conf\n    cache 30\n    errors\n}}\n")
+        return {os.path.join(c["dir"], "Corefile"): text}
+
+
+# ----------------------------------------------------------------------------- MySQL / PostgreSQL
+class MySQLRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["mysql"]
+
+    def files(self, c):
+        cfg = c["cfg"]
+        lines = ["[mysqld]", f"server-id = {c['seq']}", "bind-address = 0.0.0.0",
+                 f"port = {int(cfg.get('port', 3306))}", "max_connections = 1000"]
+        if cfg.get("cluster_mode", "none") in ("replication", "group_replication"):
+            lines += ["log_bin = mysql-bin", "binlog_format = ROW", "gtid_mode = ON",
+                      "enforce_gtid_consistency = ON", "log_replica_updates = ON"]
+            if not c["head"]:
+                lines.append("read_only = ON")
+        return {os.path.join(c["dir"], "conf.d", "cloudtik.cnf"): "\n".join(lines) + "\n"}
+
+    def configure_steps(self, head):
+        # the packaged server reads /etc/mysql/mysql.conf.d
+        return ["mkdir -p $RUNTIME_PATH/mysql/logs",
+                "[ -d /etc/mysql/mysql.conf.d ] && sudo cp $RUNTIME_PATH/mysql/conf.d/cloudtik.cnf "
+                "/etc/mysql/mysql.conf.d/zz-cloudtik.cnf || true"]
+
+
+class PostgresRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["postgres"]
+
+    def files(self, c):
+        cfg = c["cfg"]
+        repl = cfg.get("cluster_mode", "none") == "replication"
+        conf = [f"listen_addresses = '*'", f"port = {int(cfg.get('port', 5432))}", "max_connections = 500"]
+        if repl:
+            conf += ["wal_level = replica", "max_wal_senders = 16", "max_replication_slots = 16",
+                     "hot_standby = on", f"archive_mode = {'on' if cfg.get('archive_mode') else 'off'}"]
+            if not c["head"]:
+                user = cfg.get("replication_user", "repl_user")
+                conf.append(f"primary_conninfo = 'host={c['head_ip']} port={int(cfg.get('port', 5432))} "
+                            f"user={user} application_name={c['cluster']}-{c['seq']}'")
+        hba = ["host all all 0.0.0.0/0 scram-sha-256"]
+        if repl:
+            hba.append("host replication all 0.0.0.0/0 scram-sha-256")
+        return {os.path.join(c["dir"], "conf.d", "cloudtik.conf"): "\n".join(conf) + "\n",
+                os.path.join(c["dir"], "conf.d", "pg_hba.cloudtik.conf"): "\n".join(hba) + "\n"}
+
+    def configure_steps(self, head):
+        # packaged server: include dir conf.d + hba rules appended once
+        return ["mkdir -p $RUNTIME_PATH/postgres/logs",
+                "for d in /etc/postgresql/*/main; do [ -d $d ] || continue; sudo mkdir -p $d/conf.d && "
+                "sudo cp $RUNTIME_PATH/postgres/conf.d/cloudtik.conf $d/conf.d/zz-cloudtik.conf && "
+                "(sudo grep -q cloudtik-hba $d/pg_hba.conf || (echo '# cloudtik-hba' | sudo tee -a $d/pg_hba.conf "
+                ">/dev/null && sudo tee -a $d/pg_hba.conf < $RUNTIME_PATH/postgres/conf.d/pg_hba.cloudtik.conf "
+                ">/dev/null)); done; true"]
+
+
+# ----------------------------------------------------------------------------- Prometheus / Grafana
+class PrometheusRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["prometheus"]
+    members_env = "PROMETHEUS_MEMBERS"
+    quorum_members = False
+
+    def files(self, c):
+        import yaml
+        cfg = c["cfg"]
+        nodes = [c["head_ip"]] + [ip for _, ip in c["members"]]
+        scrape = [{"job_name": "cloudtik-nodes", "static_configs": [{"targets": [f"{ip}:9100" for ip in nodes],
+                                                                     "labels": {"cluster": c["cluster"]}}]},
+                  {"job_name": "cloudtik-training", "static_configs": [{"targets": [f"{ip}:9500" for ip in nodes]}]}]
+        for fed in cfg.get("federation_targets") or []:
+            scrape.append({"job_name": f"federate-{fed}", "honor_labels": True, "metrics_path": "/federate",
+                           "params": {"match[]": ['{job=~".+"}']}, "static_configs": [{"targets": [fed]}]})
+        conf = {"global": {"scrape_interval": "15s", "evaluation_interval": "15s"}, "scrape_configs": scrape}
+        return {os.path.join(c["home"], "prometheus.yml"): yaml.safe_dump(conf, sort_keys=False)}
+
+
+class GrafanaRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["grafana"]
+
+    def files(self, c):
+        import yaml
+        cfg = c["cfg"]
+        sources = cfg.get("data_sources") or [{"name": "cloudtik-prometheus", "type": "prometheus",
+                                               "url": f"http://{c['head_ip']}:9090", "isDefault": True}]
+        conf = {"apiVersion": 1, "datasources": [dict({"access": "proxy"}, **s) for s in sources]}
+        # $GRAFANA_HOME/conf/provisioning is where a tarball install looks by default
+        return {os.path.join(c["home"], "conf", "provisioning", "datasources", "cloudtik.yaml"):
+                yaml.safe_dump(conf, sort_keys=False)}
+
+
+# ----------------------------------------------------------------------------- HAProxy
+class HAProxyRuntime(ConfiguredRuntime):
+    spec = SPEC_BY_NAME["haproxy"]
+
+    def files(self, c):
+        cfg = c["cfg"]
+        port = int(cfg.get("port", 80))
+        mode = "http" if cfg.get("protocol", "http") == "http" else "tcp"
+        servers = (cfg.get("backend") or {}).get("servers") or []
+        lines = ["global", "    maxconn 20000", "defaults", f"    mode {mode}", "    timeout connect 5s",
+                 "    timeout client 60s", "    timeout server 60s",
+                 "frontend cloudtik", f"    bind *:{port}", "    default_backend cloudtik-servers",
+                 "backend cloudtik-servers", "    balance roundrobin"]
+        for i, s in enumerate(servers):
+            lines.append(f"    server s{i} {s} check")
+        return {os.path.join(c["dir"], "haproxy.cfg"): "\n".join(lines) + "\n"}
+
+    def configure_steps(self, head):
+        return ["mkdir -p $RUNTIME_PATH/haproxy/logs",
+                "[ -d /etc/haproxy ] && sudo cp $RUNTIME_PATH/haproxy/haproxy.cfg /etc/haproxy/haproxy.cfg || true"]
+
+
+CONFIGURED = {"zookeeper": ZooKeeperRuntime, "kafka": KafkaRuntime, "redis": RedisRuntime,
+              "mongodb": MongoDBRuntime, "consul": ConsulRuntime, "etcd": EtcdRuntime, "coredns": CoreDNSRuntime,
+              "mysql": MySQLRuntime, "postgres": PostgresRuntime, "prometheus": PrometheusRuntime,
+              "grafana": GrafanaRuntime, "haproxy": HAProxyRuntime}
