@@ -89,26 +89,44 @@ class DatabaseProvider(StorageProvider):
 
 
 class LoadBalancerProvider:
-    """Cloud load balancers with multiple service groups (reference 157 LoC)."""
+    """Load balancers of a workspace (reference core/load_balancer_provider.py).
+
+    A load balancer config is ``{"name", "type": "network"|"application", "scheme":
+    "internet-facing"|"internal", "tags", "service_groups": [{"listeners": [{"protocol",
+    "port"}], "services": [{"name", "protocol", "port", "route_path", "service_path",
+    "default", "targets": [{"address", "port", "node_id", "seq_id"}]}]}]}``; ``list`` maps
+    name -> ``{"name", "type", "scheme", "tags", ...provider ids}``.  Implementations:
+    core/load_balancer.py (HAProxy on the node, for local / on-premise) and
+    providers/cloud/load_balancer.py (AWS ELBv2, GCP, Azure)."""
 
     def __init__(self, provider_config: Dict[str, Any], workspace_name: str):
         self.provider_config = provider_config
         self.workspace_name = workspace_name
 
-    def list(self) -> List[Dict[str, Any]]:
+    def support_multi_service_group(self) -> bool:
+        return True
+
+    def list(self) -> Dict[str, Dict[str, Any]]:
         raise NotImplementedError
 
-    def get(self, load_balancer_name: str) -> Dict[str, Any]:
-        raise NotImplementedError
+    def get(self, load_balancer_name: str) -> Optional[Dict[str, Any]]:
+        return self.list().get(load_balancer_name)
 
     def create(self, load_balancer_config: Dict[str, Any]):
         raise NotImplementedError
 
-    def update(self, load_balancer_config: Dict[str, Any]):
+    def update(self, load_balancer: Dict[str, Any], load_balancer_config: Dict[str, Any]):
         raise NotImplementedError
 
-    def delete(self, load_balancer_config: Dict[str, Any]):
+    def delete(self, load_balancer: Dict[str, Any]):
         raise NotImplementedError
+
+    def validate_config(self, provider_config: Dict[str, Any]):
+        return None
+
+    @staticmethod
+    def bootstrap_config(config: Dict[str, Any], provider_config: Dict[str, Any]) -> Dict[str, Any]:
+        return provider_config
 
 
 class ScalingState:

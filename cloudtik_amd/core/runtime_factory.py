@@ -22,7 +22,8 @@ _CUSTOM = {
         ("zookeeper", "ZooKeeperRuntime"), ("kafka", "KafkaRuntime"), ("redis", "RedisRuntime"),
         ("mongodb", "MongoDBRuntime"), ("consul", "ConsulRuntime"), ("etcd", "EtcdRuntime"),
         ("coredns", "CoreDNSRuntime"), ("mysql", "MySQLRuntime"), ("postgres", "PostgresRuntime"),
-        ("prometheus", "PrometheusRuntime"), ("grafana", "GrafanaRuntime"), ("haproxy", "HAProxyRuntime"))},
+        ("prometheus", "PrometheusRuntime"), ("grafana", "GrafanaRuntime"), ("haproxy", "HAProxyRuntime"),
+        ("loadbalancer", "LoadBalancerRuntime"))},
 }
 
 

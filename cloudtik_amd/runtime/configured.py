@@ -357,7 +357,59 @@ class HAProxyRuntime(ConfiguredRuntime):
                 "[ -d /etc/haproxy ] && sudo cp $RUNTIME_PATH/haproxy/haproxy.cfg /etc/haproxy/haproxy.cfg || true"]
 
 
+# ----------------------------------------------------------------------------- load balancer
+class LoadBalancerRuntime(ConfiguredRuntime):
+    """Head-only driver of the workspace's load balancers (reference runtime/loadbalancer).
+    ``backend.config_mode: static`` -> the load balancers for ``backend.services`` are
+    reconciled once at configure time; ``dynamic`` (default) -> the controller pull job
+    (core/load_balancer.py ``LoadBalancerController``) discovers the services matching
+    ``backend.selector`` (default: this cluster's services with the load-balancer feature)
+    and reconciles on every change, under Consul leader election when Consul runs."""
+
+    spec = SPEC_BY_NAME["loadbalancer"]
+
+    def _controller_config(self, c) -> Dict[str, Any]:
+        cfg = c["cfg"]
+        backend = cfg.get("backend") or {}
+        selector = backend.get("selector") or {"clusters": [c["cluster"]], "tags": ["cloudtik-f-load-balancer"]}
+        provider = dict(cfg.get("provider") or {})
+        provider.setdefault("type", os.environ.get("CLOUDTIK_PROVIDER_TYPE", "haproxy"))
+        consul = cfg.get("consul_address") or (f"{c['head_ip']}:8500" if cfg.get("use_consul", True) else None)
+        return {"provider_config": provider, "workspace_name": os.environ.get("CLOUDTIK_WORKSPACE", "default"),
+                "service_selector": selector, "interval": backend.get("interval", 15), "consul_address": consul,
+                "config_mode": backend.get("config_mode", "dynamic"), "services": backend.get("services") or {}}
+
+    def files(self, c):
+        if not c["head"]:
+            return {}
+        return {os.path.join(c["dir"], "controller.json"): json.dumps(self._controller_config(c), indent=1)}
+
+    def node_configure(self, head: bool):
+        out = self.render(head)
+        if head:
+            cc = json.loads(next(iter(out.values())))
+            if cc["config_mode"] == "static":
+                from cloudtik_amd.core.load_balancer import LoadBalancerManager, backend_services_from_config
+                LoadBalancerManager(cc["provider_config"], cc["workspace_name"]).update(
+                    backend_services_from_config({"services": cc["services"]}))
+        return self._run_steps(self.configure_steps(head), head)
+
+    def start_steps(self, head):
+        if not head:
+            return []
+        c = self.ctx(head, self.node_env(head))
+        cc = self._controller_config(c)
+        if cc["config_mode"] == "static":
+            return []
+        return [f"cloudtik node service-daemon start loadbalancer "
+                f"--service-class cloudtik_amd.core.load_balancer.LoadBalancerController "
+                f"config_file={os.path.join(c['dir'], 'controller.json')}"]
+
+    def stop_steps(self, head):
+        return ["cloudtik node service-daemon stop loadbalancer"] if head else []
+
+
 CONFIGURED = {"zookeeper": ZooKeeperRuntime, "kafka": KafkaRuntime, "redis": RedisRuntime,
               "mongodb": MongoDBRuntime, "consul": ConsulRuntime, "etcd": EtcdRuntime, "coredns": CoreDNSRuntime,
               "mysql": MySQLRuntime, "postgres": PostgresRuntime, "prometheus": PrometheusRuntime,
-              "grafana": GrafanaRuntime, "haproxy": HAProxyRuntime}
+              "grafana": GrafanaRuntime, "haproxy": HAProxyRuntime, "loadbalancer": LoadBalancerRuntime}
