@@ -709,4 +709,9 @@ def cloud_workspace(provider_config: Dict[str, Any], workspace_name: str, transp
         return AzureWorkspace(provider_config, workspace_name, call)
     if t == "aws":
         return AWSWorkspace(provider_config, workspace_name, transport or provider_config.get("_client_factory"))
+    if t == "kubernetes":
+        from cloudtik_amd.providers.kubernetes.workspace import Kubectl, KubernetesWorkspace
+        kubectl = provider_config.get("_kubectl") or Kubectl(provider_config.get("kubectl"))
+        return KubernetesWorkspace(provider_config, workspace_name, kubectl,
+                                   transport or provider_config.get("_cloud_transport"))
     return None

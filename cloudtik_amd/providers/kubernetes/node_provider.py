@@ -105,12 +105,30 @@ class KubernetesNodeProvider(NodeProvider):
             if gpus:
                 for c in pod["spec"]["containers"][:1]:
                     c.setdefault("resources", {}).setdefault("limits", {})["amd.com/gpu"] = int(gpus)
+            if tags.get(T.CLOUDTIK_TAG_NODE_KIND) == T.NODE_KIND_HEAD:
+                spec = pod.setdefault("spec", {})
+                spec.setdefault("serviceAccountName", self.provider_config.get(
+                    "head_service_account", "cloudtik-head-service-account"))
+                self._ensure_cluster_services()
+            else:
+                pod.setdefault("spec", {}).setdefault("serviceAccountName", self.provider_config.get(
+                    "worker_service_account", "cloudtik-worker-service-account"))
+            if self.provider_config.get("cloud_provider", {}).get("type") == "azure":
+                md["labels"]["azure.workload.identity/use"] = "true"
             try:
                 self._k("apply", "-f", "-", input_obj=pod)
             except RuntimeError as e:
                 raise NodeLaunchException("KubernetesApplyFailed", str(e))
             created[name] = pod
         return created
+
+    def _ensure_cluster_services(self):
+        """Head / external head / headless node services of this cluster (workspace.py
+        ``cluster_services``), applied once per head launch (apply is idempotent)."""
+        from cloudtik_amd.providers.kubernetes.workspace import cluster_services
+        for svc in cluster_services(self.namespace, self.cluster_name, self.provider_config.get("head_ports") or {},
+                                    bool(self.provider_config.get("use_external_head_service"))):
+            self._k("apply", "-f", "-", input_obj=svc)
 
     def set_node_tags(self, node_id, tags):
         self._k("label", "pod", node_id, "--overwrite", *[f"{k}={_label_value(v)}" for k, v in tags.items()])
