@@ -14,6 +14,11 @@ Each virtual node gets
   per-node ROCm container instead (``DockerCommandExecutor``; /dev/kfd + /dev/dri passed
   through, GPUs split between nodes with ``HIP_VISIBLE_DEVICES``).
 
+With ``provider.use_containers: true`` every node is instead a docker container on the
+workspace's bridge network with an exclusive GPU / NUMA-local CPU slice, memory limit and data
+disks (providers/virtual/containers.py), addressed by its bridge IP -- the reference's
+virtual container scheduler, laid out for MI355X.
+
 On an 8 x MI355X host this lets one box rehearse multi-node layouts, e.g. 4 nodes x 2 GPUs.
 """
 from __future__ import annotations
@@ -82,6 +87,14 @@ class VirtualNodeProvider(NodeProvider):
         os.makedirs(self.root, exist_ok=True)
         self.store = FileStateStore(os.path.join(self.root, "nodes.json"))
         self.prefix = _cluster_prefix(cluster_name)
+        self.containers = None
+        if provider_config.get("use_containers"):
+            from cloudtik_amd.providers.virtual.containers import DockerNodes
+            self.containers = DockerNodes(provider_config, cluster_name,
+                                          provider_config.get("workspace_name", cluster_name), self.root,
+                                          runner=provider_config.get("_docker_runner"),
+                                          gpus=provider_config.get("_host_gpus"),
+                                          numa_cpus=provider_config.get("_host_numa_cpus"))
 
     # ------------------------------------------------------------------ queries
     def _nodes(self):
@@ -135,7 +148,21 @@ class VirtualNodeProvider(NodeProvider):
                 nid = f"{self.cluster_name}-{seq}"
                 node = {"state": "running", "ip": f"{self.prefix}.{seq}", "tags": dict(tags),
                         "instance_type": node_config.get("instance_type", "virtual"),
-                        "gpu_ids": node_config.get("gpu_ids")}
+                        "gpu_ids": node_config.get("gpu_ids"), "seq": seq}
+                if self.containers is not None:
+                    res = node_config.get("resources") or {}
+                    alloc_tab = st.setdefault("alloc", {})
+                    alloc = self.containers.scheduler.allocate(
+                        alloc_tab, int(node_config.get("gpus", res.get("GPU", 0)) or 0),
+                        int(node_config.get("cpus", res.get("CPU", 1)) or 1))
+                    alloc_tab[nid] = alloc
+                    ctags = dict(tags, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name})
+                    try:
+                        node["ip"] = self.containers.start(nid, node_config, ctags, alloc, seq)
+                    except Exception as e:  # noqa: BLE001 - docker failed: release the slice
+                        alloc_tab.pop(nid, None)
+                        raise NodeLaunchException("ContainerStartFailed", str(e))
+                    node.update(container=nid, gpu_ids=None, alloc=alloc)
                 nodes[nid] = node
                 created[nid] = node
                 os.makedirs(self.node_home(nid), exist_ok=True)
@@ -151,6 +178,9 @@ class VirtualNodeProvider(NodeProvider):
             n = st.get("nodes", {}).get(node_id)
             if n:
                 n["state"] = "terminated"
+                if n.get("container") and self.containers is not None:
+                    self.containers.stop(n["container"], seq=n.get("seq", 0))
+                    st.get("alloc", {}).pop(node_id, None)
 
     # ------------------------------------------------------------------ execution
     def get_command_executor(self, call_context, log_prefix, node_id, auth_config, cluster_name,
@@ -161,6 +191,9 @@ class VirtualNodeProvider(NodeProvider):
             env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in n["gpu_ids"])
         host = VirtualCommandExecutor(call_context, log_prefix, auth_config, cluster_name,
                                       process_runner, node_id, self, self.node_home(node_id), env)
+        if n.get("container"):
+            from cloudtik_amd.providers.virtual.containers import ContainerExecutor
+            return ContainerExecutor(host, n["container"], (self.provider_config.get("docker_cmd") or ["docker"])[0])
         if docker_config and docker_config.get("enabled") and docker_config.get("image"):
             dc = dict(docker_config)
             dc.setdefault("container_name", f"cloudtik-{node_id}")
@@ -175,7 +208,12 @@ class VirtualNodeProvider(NodeProvider):
     def cleanup_cluster(self, cluster_config, deep=False):
         if deep:
             with self.store.transaction() as st:
+                if self.containers is not None:
+                    for nid, n in st.get("nodes", {}).items():
+                        if n.get("container") and n.get("state") == "running":
+                            self.containers.stop(n["container"], seq=n.get("seq", 0))
                 st["nodes"] = {}
+                st["alloc"] = {}
                 st["next_seq"] = 1
 
     # ------------------------------------------------------------------ config hooks
