@@ -20,6 +20,7 @@
 // Channels are the contiguous dimension: a thread owns 8 channels (one 16-byte vector) and
 // walks rows, so every load is a full coalesced 16-byte-per-lane access.
 #include "common.h"
+#include <stdlib.h>
 
 namespace ct {
 
@@ -178,30 +179,58 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
 // pre-activation of the fused forward, evaluated identically in forward and backward
 __device__ __forceinline__ float bn_pre(float x, float a, float b, float r) { return __builtin_fmaf(x, a, b) + r; }
 
+// 8 per-channel floats (two 16-byte loads) for channel vector cv
+__device__ __forceinline__ void bn_load8(const float* __restrict__ p, int cv, float (&o)[8]) {
+  const f32x4 lo = reinterpret_cast<const f32x4*>(p)[2 * cv], hi = reinterpret_cast<const f32x4*>(p)[2 * cv + 1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { o[j] = lo[j]; o[4 + j] = hi[j]; }
+}
+
+// The element-wise passes are grid-stride loops over 16-byte channel vectors.  When the
+// vector count per row (CV = C/8) divides the block size -- every ResNet width -- the grid
+// stride is a multiple of CV, so a thread always sees the same channel vector: its
+// per-channel coefficients are loaded ONCE, before the loop, and the loop body is the two
+// or three streaming loads and the store.  (The first version re-loaded 4-10 coefficient
+// vectors per 16 data bytes through the cache and took a 64-bit modulo per vector: 3.6-3.9
+// TB/s; unrolling the loop several vectors deep did not help, pmc_resnet50.md.)  Other
+// widths take the per-vector path.
+__device__ __forceinline__ bool bn_fixed_cv(int CV) { return (blockDim.x % CV) == 0; }
+
 // y = act(x * a[c] + b[c] (+ res))
+template <int BN_EW>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x,
                                                        const bf16_t* __restrict__ res,
                                                        const float* __restrict__ a,
                                                        const float* __restrict__ b,
                                                        bf16_t* __restrict__ y, long total_vec,
                                                        int CV, int relu) {
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
-       v += (long)gridDim.x * blockDim.x) {
-    const int cv = (int)(v % CV);
-    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
-    u16x8 rv = u16x8(0);
-    if (res) rv = reinterpret_cast<const u16x8*>(res)[v];
-    const f32x4 a0 = reinterpret_cast<const f32x4*>(a)[2 * cv], a1 = reinterpret_cast<const f32x4*>(a)[2 * cv + 1];
-    const f32x4 b0 = reinterpret_cast<const f32x4*>(b)[2 * cv], b1 = reinterpret_cast<const f32x4*>(b)[2 * cv + 1];
-    u16x8 o;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const bool fixed = bn_fixed_cv(CV);
+  float av[8], bv[8];
+  if (fixed) { bn_load8(a, threadIdx.x % CV, av); bn_load8(b, threadIdx.x % CV, bv); }
+  for (long v0 = t0; v0 < total_vec; v0 += BN_EW * stride) {
+    u16x8 xv[BN_EW], rv[BN_EW];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float aj = j < 4 ? a0[j] : a1[j - 4], bj = j < 4 ? b0[j] : b1[j - 4];
-      float t = bn_pre(bf2f(xv[j]), aj, bj, bf2f(rv[j]));
-      if (relu) t = fmaxf(t, 0.f);
-      o[j] = f2bf(t);
+    for (int u = 0; u < BN_EW; ++u) {
+      const long v = v0 + u * stride;
+      xv[u] = v < total_vec ? reinterpret_cast<const u16x8*>(x)[v] : u16x8(0);
+      rv[u] = (res && v < total_vec) ? reinterpret_cast<const u16x8*>(res)[v] : u16x8(0);
     }
-    reinterpret_cast<u16x8*>(y)[v] = o;
+#pragma unroll
+    for (int u = 0; u < BN_EW; ++u) {
+      const long v = v0 + u * stride;
+      if (v >= total_vec) break;
+      if (!fixed) { const int cv = (int)(v % CV); bn_load8(a, cv, av); bn_load8(b, cv, bv); }
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = bn_pre(bf2f(xv[u][j]), av[j], bv[j], bf2f(rv[u][j]));
+        if (relu) t = fmaxf(t, 0.f);
+        o[j] = f2bf(t);
+      }
+      reinterpret_cast<u16x8*>(y)[v] = o;
+    }
   }
 }
 
@@ -214,20 +243,18 @@ struct BnMask {
   const float* fb;
 };
 
-__device__ __forceinline__ void bn_mask8(const BnMask& mk, size_t o, int cv, const u16x8& xv, bool (&on)[8]) {
-  if (mk.mode == 0) {
+// forward affine of channel vector cv (mode 2 only)
+__device__ __forceinline__ void bn_mask_coef(const BnMask& mk, int cv, float (&fa)[8], float (&fb)[8]) {
+  if (mk.mode == 2) { bn_load8(mk.fa, cv, fa); bn_load8(mk.fb, cv, fb); }
+}
+
+__device__ __forceinline__ void bn_mask8(const BnMask& mk, const u16x8& yv, const u16x8& xv, const float (&fa)[8],
+                                         const float (&fb)[8], bool (&on)[8]) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) on[j] = true;
-  } else if (mk.mode == 1) {
-    const u16x8 yv = reinterpret_cast<const u16x8*>(mk.y)[o];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) on[j] = bf2f(yv[j]) > 0.f;
-  } else {
-    const f32x4* a4 = reinterpret_cast<const f32x4*>(mk.fa) + 2 * cv;
-    const f32x4* b4 = reinterpret_cast<const f32x4*>(mk.fb) + 2 * cv;
-    const f32x4 aa[2] = {a4[0], a4[1]}, bb[2] = {b4[0], b4[1]};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) on[j] = bf2f(f2bf(bn_pre(bf2f(xv[j]), aa[j >> 2][j & 3], bb[j >> 2][j & 3], 0.f))) > 0.f;
+  for (int j = 0; j < 8; ++j) {
+    if (mk.mode == 0) on[j] = true;
+    else if (mk.mode == 1) on[j] = bf2f(yv[j]) > 0.f;
+    else on[j] = bf2f(f2bf(bn_pre(bf2f(xv[j]), fa[j], fb[j], 0.f))) > 0.f;
   }
 }
 
@@ -241,27 +268,29 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
   bn_thread(L, cv, rl);
   const int r0 = blockIdx.x * L.rows_per_blk;
   const int r1 = min(L.M, r0 + L.rows_per_blk);
-  float s1[8], s2[8], mu[8], is[8];
+  float s1[8], s2[8], mu[8], is[8], fa[8], fb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     s1[j] = 0.f; s2[j] = 0.f;
     mu[j] = mean[cv * 8 + j]; is[j] = invstd[cv * 8 + j];
   }
+  bn_mask_coef(mk, cv, fa, fb);
   if (rl < L.RPI) {
     int r = r0 + rl;
     for (; r + 3 * L.RPI < r1; r += 4 * L.RPI) {
-      u16x8 g[4], xv[4];
+      u16x8 g[4], xv[4], yv[4];
       size_t o[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         o[u] = (size_t)(r + u * L.RPI) * L.CV + cv;
         g[u] = reinterpret_cast<const u16x8*>(dy)[o[u]];
         xv[u] = reinterpret_cast<const u16x8*>(x)[o[u]];
+        yv[u] = mk.mode == 1 ? reinterpret_cast<const u16x8*>(mk.y)[o[u]] : u16x8(0);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         bool on[8];
-        bn_mask8(mk, o[u], cv, xv[u], on);
+        bn_mask8(mk, yv[u], xv[u], fa, fb, on);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float d = on[j] ? bf2f(g[u][j]) : 0.f;
@@ -274,8 +303,9 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
       const size_t o = (size_t)r * L.CV + cv;
       const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
       const u16x8 xv = reinterpret_cast<const u16x8*>(x)[o];
+      const u16x8 yv = mk.mode == 1 ? reinterpret_cast<const u16x8*>(mk.y)[o] : u16x8(0);
       bool on[8];
-      bn_mask8(mk, o, cv, xv, on);
+      bn_mask8(mk, yv, xv, fa, fb, on);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = on[j] ? bf2f(g[j]) : 0.f;
@@ -330,30 +360,50 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   c0[c] = -a * sdy / M - k * is * mean[c];
 }
 
+template <int BN_EW>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dy, BnMask mk, const bf16_t* __restrict__ x,
     const float* __restrict__ ca, const float* __restrict__ c1, const float* __restrict__ c0,
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long total_vec, int CV) {
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec;
-       v += (long)gridDim.x * blockDim.x) {
-    const int cv = (int)(v % CV);
-    const u16x8 g = reinterpret_cast<const u16x8*>(dy)[v];
-    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
-    bool on[8];
-    bn_mask8(mk, (size_t)v, cv, xv, on);
-    const f32x4* a4 = reinterpret_cast<const f32x4*>(ca) + 2 * cv;
-    const f32x4* k4 = reinterpret_cast<const f32x4*>(c1) + 2 * cv;
-    const f32x4* z4 = reinterpret_cast<const f32x4*>(c0) + 2 * cv;
-    const f32x4 aa[2] = {a4[0], a4[1]}, kk[2] = {k4[0], k4[1]}, zz[2] = {z4[0], z4[1]};
-    u16x8 o, od;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const bool fixed = bn_fixed_cv(CV);
+  float aa[8], kk[8], zz[8], fa[8], fb[8];
+  if (fixed) {
+    const int cv = threadIdx.x % CV;
+    bn_load8(ca, cv, aa); bn_load8(c1, cv, kk); bn_load8(c0, cv, zz);
+    bn_mask_coef(mk, cv, fa, fb);
+  }
+  for (long v0 = blockIdx.x * (long)blockDim.x + threadIdx.x; v0 < total_vec; v0 += BN_EW * stride) {
+    u16x8 g[BN_EW], xv[BN_EW], yv[BN_EW];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d = on[j] ? bf2f(g[j]) : 0.f;
-      o[j] = f2bf(aa[j >> 2][j & 3] * d + kk[j >> 2][j & 3] * bf2f(xv[j]) + zz[j >> 2][j & 3]);
-      od[j] = f2bf(d);
+    for (int u = 0; u < BN_EW; ++u) {
+      const long v = v0 + u * stride;
+      const bool in = v < total_vec;
+      g[u] = in ? reinterpret_cast<const u16x8*>(dy)[v] : u16x8(0);
+      xv[u] = in ? reinterpret_cast<const u16x8*>(x)[v] : u16x8(0);
+      yv[u] = (in && mk.mode == 1) ? reinterpret_cast<const u16x8*>(mk.y)[v] : u16x8(0);
     }
-    reinterpret_cast<u16x8*>(dx)[v] = o;
-    if (dres) reinterpret_cast<u16x8*>(dres)[v] = od;
+#pragma unroll
+    for (int u = 0; u < BN_EW; ++u) {
+      const long v = v0 + u * stride;
+      if (v >= total_vec) break;
+      if (!fixed) {
+        const int cv = (int)(v % CV);
+        bn_load8(ca, cv, aa); bn_load8(c1, cv, kk); bn_load8(c0, cv, zz);
+        bn_mask_coef(mk, cv, fa, fb);
+      }
+      bool on[8];
+      bn_mask8(mk, yv[u], xv[u], fa, fb, on);
+      u16x8 o, od;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = on[j] ? bf2f(g[u][j]) : 0.f;
+        o[j] = f2bf(aa[j] * d + kk[j] * bf2f(xv[u][j]) + zz[j]);
+        od[j] = f2bf(d);
+      }
+      reinterpret_cast<u16x8*>(dx)[v] = o;
+      if (dres) reinterpret_cast<u16x8*>(dres)[v] = od;
+    }
   }
 }
 
@@ -371,8 +421,8 @@ inline BnLayout bn_layout(int M, int C, int target_blocks) {
 }
 inline int bn_nblk(const BnLayout& L) { return (L.M + L.rows_per_blk - 1) / L.rows_per_blk; }
 
-inline int ew_grid(long work) {
-  long g = (work + 255) / 256;
+inline int ew_grid(long work, int ew) {
+  long g = (work + 256L * ew - 1) / (256L * ew);   // >= ew vectors per thread
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
@@ -382,13 +432,41 @@ using namespace ct;
 
 extern "C" int ct_bn_max_blocks() { return 2048; }
 
+// vectors per thread per iteration of the apply kernels (CLOUDTIK_AMD_BN_EW: 1, 2 or 4)
+static int bn_ew() {
+  static int n = [] {
+    const char* e = getenv("CLOUDTIK_AMD_BN_EW");
+    int v = e ? atoi(e) : 1;
+    return v >= 4 ? 4 : (v >= 2 ? 2 : 1);
+  }();
+  return n;
+}
+
+#define BN_EW_DISPATCH(KERNEL, GRIDWORK, ...)                                              \
+  do {                                                                                       \
+    const int ew_ = bn_ew();                                                                 \
+    if (ew_ == 4) KERNEL<4><<<ew_grid(GRIDWORK, 4), 256, 0, stream>>>(__VA_ARGS__);          \
+    else if (ew_ == 2) KERNEL<2><<<ew_grid(GRIDWORK, 2), 256, 0, stream>>>(__VA_ARGS__);     \
+    else KERNEL<1><<<ew_grid(GRIDWORK, 1), 256, 0, stream>>>(__VA_ARGS__);                   \
+  } while (0)
+
+// partial-block count of the reductions (CLOUDTIK_AMD_BN_BLOCKS, <= 2048; default 512)
+static int bn_target_blocks() {
+  static int n = [] {
+    const char* e = getenv("CLOUDTIK_AMD_BN_BLOCKS");
+    int v = e ? atoi(e) : 512;
+    return v < 64 ? 64 : (v > 2048 ? 2048 : v);
+  }();
+  return n;
+}
+
 // workspace: part = float[2 * 2048 * C]; stat = float[4 * C] (save_mean, save_invstd, a, b)
 extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma, const void* beta,
                                float* run_mean, float* run_var, void* y, float* part, float* stat,
                                int M, int C, float eps, float momentum, int relu,
                                hipStream_t stream) {
   if (C % 8 || C / 8 > BN_RT || M <= 0) return -1;
-  BnLayout L = bn_layout(M, C, 512);
+  BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
   bn_stats_kernel<<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
   bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)2048 * C, nblk, L,
@@ -396,8 +474,8 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
                                                            eps, momentum, run_mean, run_var, stat,
                                                            stat + C, stat + 2 * C, stat + 3 * C);
   const long tv = (long)M * (C / 8);
-  bn_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)res, stat + 2 * C,
-                                                   stat + 3 * C, (bf16_t*)y, tv, C / 8, relu);
+  BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, stat + 2 * C, stat + 3 * C,
+                 (bf16_t*)y, tv, C / 8, relu);
   return 0;
 }
 
@@ -406,8 +484,7 @@ extern "C" int ct_bn_apply(const void* x, const void* res, const float* a, const
                            int M, int C, int relu, hipStream_t stream) {
   if (C % 8) return -1;
   const long tv = (long)M * (C / 8);
-  bn_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)x, (const bf16_t*)res, a, b,
-                                                   (bf16_t*)y, tv, C / 8, relu);
+  BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, a, b, (bf16_t*)y, tv, C / 8, relu);
   return 0;
 }
 
@@ -419,7 +496,7 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
                          float* coef, int M, int C, int relu_mode, hipStream_t stream) {
   if (C % 8 || C / 8 > BN_RT || M <= 0 || relu_mode < 0 || relu_mode > 2) return -1;
   if (relu_mode == 1 && !y) return -2;
-  BnLayout L = bn_layout(M, C, 512);
+  BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
   const BnMask mk{relu_mode, (const bf16_t*)y, stat + 2 * C, stat + 3 * C};
   bn_bwd_reduce_kernel<<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
@@ -434,7 +511,7 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
         part, part + (size_t)2048 * C, nblk, M, C, (const bf16_t*)gamma, stat, stat + C,
         (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
-  bn_bwd_apply_kernel<<<ew_grid(tv), 256, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, coef, coef + C,
-                                                       coef + 2 * C, (bf16_t*)dx, (bf16_t*)dres, tv, C / 8);
+  BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dy, mk, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
+                 (bf16_t*)dx, (bf16_t*)dres, tv, C / 8);
   return 0;
 }
