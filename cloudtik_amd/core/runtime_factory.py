@@ -24,6 +24,14 @@ _CUSTOM = {
         ("coredns", "CoreDNSRuntime"), ("mysql", "MySQLRuntime"), ("postgres", "PostgresRuntime"),
         ("prometheus", "PrometheusRuntime"), ("grafana", "GrafanaRuntime"), ("haproxy", "HAProxyRuntime"),
         ("loadbalancer", "LoadBalancerRuntime"))},
+    # part 2: query engines, frameworks, stores, gateways, DNS, poolers, node utilities
+    **{n: ("cloudtik_amd.runtime.configured_more", c) for n, c in (
+        ("metastore", "MetastoreRuntime"), ("presto", "PrestoRuntime"), ("trino", "TrinoRuntime"),
+        ("flink", "FlinkRuntime"), ("ray", "RayRuntime"), ("minio", "MinIORuntime"),
+        ("elasticsearch", "ElasticsearchRuntime"), ("nginx", "NginxRuntime"), ("kong", "KongRuntime"),
+        ("apisix", "APISIXRuntime"), ("dnsmasq", "DnsmasqRuntime"), ("bind", "BindRuntime"),
+        ("pgbouncer", "PgBouncerRuntime"), ("pgpool", "PgpoolRuntime"), ("mount", "MountRuntime"),
+        ("sshserver", "SSHServerRuntime"), ("xinetd", "XinetdRuntime"), ("nodex", "NodexRuntime"))},
 }
 
 
