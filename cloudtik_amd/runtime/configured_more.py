@@ -56,6 +56,11 @@ def _db_of(cfg: Dict[str, Any], env_head: str) -> Dict[str, Any]:
     """The metastore / gateway database: ``database`` section, else the cluster's MySQL /
     Postgres runtime on the head."""
     db = dict(cfg.get("database") or {})
+    # schema keys (database_connect: address / username) or the short forms
+    if "address" in db:
+        db.setdefault("host", db["address"])
+    if "username" in db:
+        db.setdefault("user", db["username"])
     db.setdefault("engine", "mysql")
     db.setdefault("host", env_head)
     db.setdefault("port", 3306 if db["engine"] == "mysql" else 5432)
@@ -316,7 +321,7 @@ class KongRuntime(ConfiguredRuntime):
 
     def files(self, c):
         cfg = c["cfg"]
-        db = _db_of(dict(cfg, database=dict({"engine": "postgresql"}, **(cfg.get("database") or {}))), c["head_ip"])
+        db = _db_of(dict(cfg, database=dict({"engine": "postgres"}, **(cfg.get("database") or {}))), c["head_ip"])
         conf = {"database": "postgres", "pg_host": db["host"], "pg_port": db["port"], "pg_user": db["user"],
                 "pg_password": db["password"], "pg_database": db.get("name", "kong"),
                 "proxy_listen": "0.0.0.0:8000", "admin_listen": f"{c['ip']}:8001"}

@@ -85,6 +85,37 @@ RUNTIMES: Dict[str, Dict[str, Any]] = {
     "zookeeper": dict(config="o"),
 }
 
+# keys the self-configuring runtimes add (runtime/configured*.py; node sizing overrides, rendered
+# file settings)                                                                            # +
+_NODE = dict(node_memory_mb="i", node_cpus="i")
+_ADDED: Dict[str, Dict[str, Any]] = {
+    "apisix": dict(etcd_hosts="a"),
+    "bind": dict(domain="s", upstream="a"),
+    "dnsmasq": dict(domain="s", upstream="a"),
+    "elasticsearch": dict(_NODE, master_nodes="i", data_dir="s", heap_mb="i", config="o"),
+    "flink": dict(_NODE, taskmanager_slots="i", taskmanager_memory_mb="i", jobmanager_memory_mb="i",
+                  parallelism="i", execution_target="s", state_backend="s", checkpoints_dir="s",
+                  high_availability_zookeeper="s"),
+    "kong": dict(config="o"),
+    "loadbalancer": dict(consul_address="s", use_consul="b"),
+    "metastore": dict(warehouse_dir="s", config="o"),
+    "minio": dict(access_key="s", secret_key="s", data_disks="i"),
+    "mount": dict(mount_path="s", storage="o"),
+    "nginx": dict(web_root="s"),
+    "pgbouncer": dict(postgres_host="s", postgres_port="port", databases="o", pool_mode="s", max_client_conn="i",
+                      default_pool_size="i"),
+    "pgpool": dict(num_init_children="i", user="s", primary_no_reads="b"),
+    "presto": dict(_NODE, jvm_max_memory_mb="i", query_max_memory_per_node_mb="i", query_max_memory_gb="i",
+                   environment="s", data_dir="s", hive="o"),
+    "ray": dict(_NODE, node_gpus="i", object_store_ratio="n", resources="o"),
+    "sshserver": dict(authorized_keys="s"),
+    "trino": dict(_NODE, jvm_max_memory_mb="i", query_max_memory_per_node_mb="i", query_max_memory_gb="i",
+                  environment="s", data_dir="s", hive="o", config="o"),
+    "xinetd": dict(services="o"),
+}
+for _rt, _keys in _ADDED.items():
+    RUNTIMES.setdefault(_rt, {}).update(_keys)
+
 SCALING = dict(scaling_policy_class="s", scaling_policy={"enum": ["scaling-with-resources", "scaling-with-load",
                                                                    "scaling-with-time"]},
                scaling_policy_by_node_type="o", scaling_step="i", scaling_resource="s", cpu_load_threshold="n",
