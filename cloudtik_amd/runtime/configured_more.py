@@ -228,6 +228,13 @@ class RayRuntime(ConfiguredRuntime):
     def stop_steps(self, head):
         return ["ray stop --force || true"]
 
+    def get_scaling_policy(self, cluster_config, head_ip):
+        from cloudtik_amd.runtime.ray_scaling import RayScalingPolicy
+        rc = (cluster_config.get("runtime") or {}).get("ray") or {}
+        if not (rc.get("auto_scaling") or (rc.get("scaling") or {}).get("auto_scaling")):
+            return None
+        return RayScalingPolicy(cluster_config, head_ip)
+
 
 # ----------------------------------------------------------------------------- MinIO
 class MinIORuntime(ConfiguredRuntime):

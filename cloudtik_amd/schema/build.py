@@ -107,7 +107,7 @@ _ADDED: Dict[str, Dict[str, Any]] = {
     "pgpool": dict(num_init_children="i", user="s", primary_no_reads="b"),
     "presto": dict(_NODE, jvm_max_memory_mb="i", query_max_memory_per_node_mb="i", query_max_memory_gb="i",
                    environment="s", data_dir="s", hive="o"),
-    "ray": dict(_NODE, node_gpus="i", object_store_ratio="n", resources="o"),
+    "ray": dict(_NODE, node_gpus="i", object_store_ratio="n", resources="o", auto_scaling="b"),
     "sshserver": dict(authorized_keys="s"),
     "trino": dict(_NODE, jvm_max_memory_mb="i", query_max_memory_per_node_mb="i", query_max_memory_gb="i",
                   environment="s", data_dir="s", hive="o", config="o"),
