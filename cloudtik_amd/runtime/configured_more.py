@@ -497,17 +497,35 @@ class SSHServerRuntime(ConfiguredRuntime):
 
 
 class XinetdRuntime(ConfiguredRuntime):
-    """xinetd services (e.g. the HAProxy / load-balancer health-check responders)."""
+    """xinetd services: the role-aware health checks of the cluster's replicated runtimes
+    (every runtime with a ``health_check_port``, runtime/common/health_check.py -- what HAProxy
+    probes to find the primary) plus any explicit ``services``."""
 
     spec = SPEC_BY_NAME["xinetd"]
 
+    def with_environment_variables(self, config, provider, node_id):
+        env = super().with_environment_variables(config, provider, node_id)
+        from cloudtik_amd.runtime.common.health_check import xinetd_services
+        checks = xinetd_services((config or {}).get("runtime") or {}, python="/usr/bin/python3")
+        if checks:
+            env["XINETD_HEALTH_CHECKS"] = json.dumps(checks, sort_keys=True)
+        return env
+
+    def ctx(self, head, env):
+        c = super().ctx(head, env)
+        c["health_checks"] = json.loads(env.get("XINETD_HEALTH_CHECKS") or "{}")
+        return c
+
     def files(self, c):
         out = {}
-        for name, s in sorted((c["cfg"].get("services") or {}).items()):
+        services = dict(c.get("health_checks") or {})
+        services.update(c["cfg"].get("services") or {})
+        for name, s in sorted(services.items()):
+            args = f"  server_args = {s['server_args']}\n" if s.get("server_args") else ""
             out[os.path.join(c["dir"], name)] = (
                 f"service {name}\n{{\n  type = UNLISTED\n  port = {int(s['port'])}\n  socket_type = stream\n"
                 f"  protocol = tcp\n  wait = no\n  user = {s.get('user', 'nobody')}\n  server = {s['server']}\n"
-                f"  only_from = {s.get('only_from', '0.0.0.0/0')}\n  disable = no\n}}\n")
+                f"{args}  only_from = {s.get('only_from', '0.0.0.0/0')}\n  disable = no\n}}\n")
         return out
 
     def configure_steps(self, head):

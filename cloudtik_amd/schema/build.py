@@ -112,6 +112,8 @@ _ADDED: Dict[str, Dict[str, Any]] = {
     "trino": dict(_NODE, jvm_max_memory_mb="i", query_max_memory_per_node_mb="i", query_max_memory_gb="i",
                   environment="s", data_dir="s", hive="o", config="o"),
     "xinetd": dict(services="o"),
+    "redis": dict(health_check_user="s"), "mysql": dict(health_check_user="s"),
+    "postgres": dict(health_check_user="s"),
 }
 for _rt, _keys in _ADDED.items():
     RUNTIMES.setdefault(_rt, {}).update(_keys)
