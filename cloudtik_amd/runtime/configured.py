@@ -343,13 +343,19 @@ class HAProxyRuntime(ConfiguredRuntime):
         cfg = c["cfg"]
         port = int(cfg.get("port", 80))
         mode = "http" if cfg.get("protocol", "http") == "http" else "tcp"
-        servers = (cfg.get("backend") or {}).get("servers") or []
+        backend = cfg.get("backend") or {}
+        servers = backend.get("servers") or []
         lines = ["global", "    maxconn 20000", "defaults", f"    mode {mode}", "    timeout connect 5s",
                  "    timeout client 60s", "    timeout server 60s",
                  "frontend cloudtik", f"    bind *:{port}", "    default_backend cloudtik-servers",
                  "backend cloudtik-servers", "    balance roundrobin"]
+        # role-aware routing: probe the runtime's health check (runtime/common/health_check.py),
+        # e.g. health_check_port 9201 + health_check_path /primary sends traffic to the primary only
+        hc_port = backend.get("health_check_port")
+        if hc_port:
+            lines.append(f"    option httpchk GET {backend.get('health_check_path', '/')}")
         for i, s in enumerate(servers):
-            lines.append(f"    server s{i} {s} check")
+            lines.append(f"    server s{i} {s} check" + (f" port {int(hc_port)}" if hc_port else ""))
         return {os.path.join(c["dir"], "haproxy.cfg"): "\n".join(lines) + "\n"}
 
     def configure_steps(self, head):

@@ -41,3 +41,10 @@ def test_xinetd_responder_and_runtime(tmp_path, monkeypatch):
     svc = files["xinetd/mysql-health-check"]
     assert "port = 9201" in svc and "server_args = -m cloudtik_amd.runtime.common.health_check mysql --port 3307" in svc
     assert list(files) == ["xinetd/mysql-health-check"]
+
+
+def test_haproxy_probes_the_role_health_check(tmp_path, monkeypatch):
+    cfg = {"backend": {"servers": ["10.0.0.12:3306", "10.0.0.13:3306"], "health_check_port": 9201,
+                       "health_check_path": "/primary"}, "protocol": "tcp", "port": 3306}
+    text = _render("haproxy", cfg, {}, head=True, monkeypatch=monkeypatch, tmp_path=tmp_path)["haproxy/haproxy.cfg"]
+    assert "option httpchk GET /primary" in text and "server s1 10.0.0.13:3306 check port 9201" in text
