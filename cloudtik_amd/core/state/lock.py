@@ -107,10 +107,11 @@ class LeaderElection:
         if self._thread:
             self._thread.join(timeout=5)
         if self._leader:
-            self.lock.release()
+            # stop acting as leader before the lock is handed over
             self._leader = False
             if self.on_demoted:
                 self.on_demoted()
+            self.lock.release()
 
 
 class ActiveStandbyService:

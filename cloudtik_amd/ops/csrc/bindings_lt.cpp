@@ -11,7 +11,9 @@
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/HIPContextLight.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <map>
+#include <vector>
 #include <mutex>
 #include <tuple>
 
@@ -154,6 +156,132 @@ bool lt_matmul(at::Tensor A, at::Tensor B, at::Tensor D, bool trans_a, bool tran
   return true;
 }
 
+// ---------------------------------------------------------------------------------------
+// Strided-batched D[b] = op(A[b]) @ op(B[b]) (beta 0) with the algorithm picked by TIMING every
+// solution hipBLASLt has for the problem (hipblaslt_ext::getAllAlgos + matmulIsAlgoSupported),
+// once per shape, on the real operands.  Used by the split-K weight-gradient GEMM
+// (ops/linear.py): PyTorch's TunableOp does not tune bf16 -> fp32 batched GEMMs, and the
+// heuristic's first pick for these transposed-A / fp32-out shapes is a depth-32 tile.
+// Candidates slower than 3x the best so far after one run are dropped without more timing.
+namespace {
+struct BPlan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, d = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  float ms = 0.f;
+  int n_tried = 0;
+  bool ok = false;
+};
+std::map<Key, BPlan> g_bplans;
+
+void set_batch(hipblasLtMatrixLayout_t l, int batch, int64_t stride) {
+  int32_t bc = batch;
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+  LT_CHECK(hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &stride,
+                                             sizeof(stride)));
+}
+}  // namespace
+
+// A, B, D: 2-D row-major views of batch 0; batch b's operands start stride_* elements later.
+// Returns the tuned algorithm's time in ms (first call) or 0, or -1 when nothing supports it.
+double lt_bmm_tuned(at::Tensor A, at::Tensor B, at::Tensor D, bool trans_a, bool trans_b, int64_t batch,
+                    int64_t stride_a, int64_t stride_b, int64_t stride_d, int64_t max_timed) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "lt_bmm_tuned: GPU tensors");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "lt_bmm_tuned: 2-D row-major operands");
+  const long M = D.size(0), N = D.size(1);
+  const long K = trans_a ? A.size(0) : A.size(1);
+  TORCH_CHECK((trans_a ? A.size(1) : A.size(0)) == M, "lt_bmm_tuned: A rows");
+  TORCH_CHECK((trans_b ? B.size(1) : B.size(0)) == K && (trans_b ? B.size(0) : B.size(1)) == N,
+              "lt_bmm_tuned: B shape");
+  TORCH_CHECK(batch >= 1, "lt_bmm_tuned: batch");
+  // the last batch's operands must lie inside the storage the views came from
+  auto span_ok = [&](const at::Tensor& t, int64_t stride) {
+    const int64_t last = (batch - 1) * stride + (t.size(0) - 1) * t.stride(0) + t.size(1);
+    return t.storage_offset() + last <= (int64_t)(t.storage().nbytes() / t.element_size());
+  };
+  TORCH_CHECK(span_ok(A, stride_a) && span_ok(B, stride_b) && span_ok(D, stride_d), "lt_bmm_tuned: batch span");
+  Key key{M, N, K, A.stride(0), B.stride(0), batch, D.stride(0), stride_a * 7 + stride_b * 13 + stride_d,
+          (long)dt(A) * 64 + (long)dt(D), (int)trans_a, (int)trans_b, -7, (int)dt(B), 0};
+  const size_t ws_size = at::cuda::getCUDABlasLtWorkspaceSize();
+  void* ws = at::cuda::getCUDABlasLtWorkspace();
+  hipblasLtHandle_t handle = at::cuda::getCurrentCUDABlasLtHandle();
+  hipStream_t stream = at::hip::getCurrentHIPStream().stream();
+  const float al = 1.f, be = 0.f;
+  BPlan* plan;
+  double tuned_ms = 0.0;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_bplans.find(key);
+    if (it == g_bplans.end()) {
+      BPlan p;
+      LT_CHECK(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+      hipblasOperation_t opa = trans_b ? HIPBLAS_OP_T : HIPBLAS_OP_N;   // swapped operands, as lt_matmul
+      hipblasOperation_t opb = trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opa, sizeof(opa)));
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opb, sizeof(opb)));
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt(B), trans_b ? K : N, trans_b ? N : K, B.stride(0)));
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.b, dt(A), trans_a ? M : K, trans_a ? K : M, A.stride(0)));
+      LT_CHECK(hipblasLtMatrixLayoutCreate(&p.d, dt(D), N, M, D.stride(0)));
+      set_batch(p.a, (int)batch, stride_b);
+      set_batch(p.b, (int)batch, stride_a);
+      set_batch(p.d, (int)batch, stride_d);
+      std::vector<hipblasLtMatmulHeuristicResult_t> all;
+      hipblaslt_ext::getAllAlgos(handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, opa, opb, dt(B), dt(A), dt(D),
+                                 dt(D), HIPBLAS_COMPUTE_32F, all);
+      hipEvent_t e0, e1;
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+      float best = 1e30f;
+      int timed = 0;
+      for (auto& r : all) {
+        if (max_timed > 0 && timed >= max_timed) break;
+        size_t need = 0;
+        if (hipblaslt_ext::matmulIsAlgoSupported(handle, p.desc, &al, p.a, p.b, &be, p.d, p.d, r.algo, need) !=
+                HIPBLAS_STATUS_SUCCESS || need > ws_size)
+          continue;
+        auto run = [&]() {
+          return hipblasLtMatmul(handle, p.desc, &al, B.data_ptr(), p.a, A.data_ptr(), p.b, &be, D.data_ptr(), p.d,
+                                 D.data_ptr(), p.d, &r.algo, ws, need, stream);
+        };
+        if (run() != HIPBLAS_STATUS_SUCCESS) continue;          // warm-up (and code-object load)
+        ++timed;
+        hipEventRecord(e0, stream);
+        run();
+        hipEventRecord(e1, stream);
+        hipEventSynchronize(e1);
+        float t1 = 0.f;
+        hipEventElapsedTime(&t1, e0, e1);
+        if (t1 > 3.f * best) continue;
+        hipEventRecord(e0, stream);
+        for (int i = 0; i < 3; ++i) run();
+        hipEventRecord(e1, stream);
+        hipEventSynchronize(e1);
+        float t3 = 0.f;
+        hipEventElapsedTime(&t3, e0, e1);
+        const float t = t3 / 3.f;
+        if (t < best) {
+          best = t;
+          p.algo = r.algo;
+          p.ws = need;
+          p.ok = true;
+        }
+      }
+      hipEventDestroy(e0);
+      hipEventDestroy(e1);
+      p.ms = p.ok ? best : 0.f;
+      p.n_tried = timed;
+      tuned_ms = p.ok ? best : -1.0;
+      it = g_bplans.emplace(key, p).first;
+    }
+    plan = &it->second;
+  }
+  if (!plan->ok) return -1.0;
+  LT_CHECK(hipblasLtMatmul(handle, plan->desc, &al, B.data_ptr(), plan->a, A.data_ptr(), plan->b, &be, D.data_ptr(),
+                           plan->d, D.data_ptr(), plan->d, &plan->algo, ws, plan->ws, stream));
+  return tuned_ms;
+}
+
 extern "C" int ct_gemm_nt(const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
                           void*, long, float*, hipStream_t);
 
@@ -188,4 +316,5 @@ bool gemm_nt(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumul
 void register_lt(pybind11::module& m) {
   m.def("gemm_nt", &gemm_nt, "hand-written MFMA GEMM A @ B^T with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
+  m.def("lt_bmm_tuned", &lt_bmm_tuned, "strided-batched hipBLASLt GEMM, algorithm picked by timing all solutions");
 }

@@ -27,6 +27,10 @@ _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 _WGRAD_STREAM = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM", "1") == "1"
 # weight-gradient GEMMs through the HIP gemm_tn kernel instead of hipBLASLt
 _HIP_WGRAD = os.environ.get("CLOUDTIK_AMD_WGRAD_KERNEL", "blas") == "hip"
+# split-K partial GEMMs through the binding's strided-batched hipBLASLt call whose algorithm is
+# chosen by timing every solution once per shape (torch.bmm's heuristic pick is not tuned:
+# TunableOp skips bf16 -> fp32 batched GEMMs)
+_LT_WGRAD = os.environ.get("CLOUDTIK_AMD_WGRAD_LT", "0") == "1"
 _streams = {}
 
 
@@ -104,6 +108,14 @@ def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> No
     from cloudtik_amd import ops
     dy2 = dy2.contiguous()
     x2 = x2.contiguous()
+    if _LT_WGRAD:
+        C = ops.require_native()
+        Ts = T // S
+        P = torch.empty(S, N, K, device=g.device, dtype=torch.float32)
+        # P[s] = dy2[s*Ts:(s+1)*Ts]^T @ x2[s*Ts:(s+1)*Ts]
+        if C.lt_bmm_tuned(dy2[:Ts], x2[:Ts], P[0], True, False, S, Ts * N, Ts * K, N * K, 0) >= 0:
+            C.splitk_reduce(P, g, True)
+            return
     P = torch.bmm(dy2.view(S, T // S, N).transpose(1, 2), x2.view(S, T // S, K), out_dtype=torch.float32)
     ops.require_native().splitk_reduce(P, g, True)
 

@@ -300,10 +300,11 @@ class ConsulLeaderElection:
         if self._thread:
             self._thread.join(5)
         if self._leader:
-            self.lock.release()
+            # stop acting as leader before the lock is handed over
             self._leader = False
             if self.on_demoted:
                 self.on_demoted()
+            self.lock.release()
 
 
 def service_dns_name(service: str, tag: Optional[str] = None, domain: str = "consul") -> str:

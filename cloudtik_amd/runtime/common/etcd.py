@@ -176,10 +176,11 @@ class EtcdLeaderElection:
         if self._thread:
             self._thread.join(5)
         if self._leader:
-            self.lock.release()
+            # stop acting as leader before the lock is handed over
             self._leader = False
             if self.on_demoted:
                 self.on_demoted()
+            self.lock.release()
 
 
 def leader_election(url: str, name: str, candidate_id: Optional[str] = None, ttl_s: int = 10, **kw):
