@@ -10,8 +10,15 @@ ZooKeeper, a metastore on MySQL ...) finds it in one of two places:
   ``cluster_operator._publish_services``); a ``<runtime>.<service>_service_selector`` in
   the runtime config narrows the candidates (clusters, features, names).
 
+* ``*_from_consul``    -- a Consul agent on the node knows every registered instance of the
+  service (healthy ones only), across clusters, selected by the same selector.
+
 Each helper returns the URI the consumer's config needs (``hdfs://h:8020``,
-``thrift://h:9083``, ``h1:2181,h2:2181`` ...) or ``None``.
+``thrift://h:9083``, ``h1:2181,h2:2181`` ...) or ``None``.  Discovery of a dependency is on
+unless the consumer sets ``<dependency>_service_discovery: false`` (then only the explicit
+URI in its config counts).  ``with_database_environment_variables`` turns the database a
+runtime uses (explicit ``database`` section, same cluster, Consul or workspace) into the
+``CLOUDTIK_DATABASE_*`` variables its scripts read.
 """
 from __future__ import annotations
 
@@ -74,7 +81,7 @@ def discover_runtime_service_addresses(global_variables, runtime_type: str, serv
 
 
 def _workspace_global_variables(config: Dict[str, Any]) -> Dict[str, str]:
-    from cloudtik_amd.providers.provider_factory import get_workspace_provider
+    from cloudtik_amd.core.provider_factory import get_workspace_provider
     try:
         wp = get_workspace_provider(config["provider"], config.get("workspace_name", "default"))
         return wp.subscribe_global_variables(config) or {}
@@ -146,14 +153,87 @@ def discover_database_on_head(config, head_ip: str) -> Optional[Dict[str, Any]]:
     return None
 
 
+def is_service_discovery(config: Dict[str, Any], consumer: Optional[str], runtime_type: str) -> bool:
+    """``<consumer>.<runtime_type>_service_discovery`` (default on)."""
+    if not consumer:
+        return True
+    rc = (config.get("runtime", {}) or {}).get(consumer, {}) or {}
+    return bool(rc.get(f"{runtime_type}_service_discovery", True))
+
+
+def discover_from_consul(runtime_type: str, config: Dict[str, Any], consumer: Optional[str] = None,
+                         consul_address: Optional[str] = None, client=None) -> Optional[str]:
+    """Healthy instances of the runtime's service known to the node's Consul agent."""
+    if runtime_type not in _KNOWN:
+        return None
+    import os
+    addr = consul_address or os.environ.get("CONSUL_HTTP_ADDR")
+    if client is None:
+        if not addr:
+            return None
+        from cloudtik_amd.runtime.common.consul import ConsulClient
+        client = ConsulClient(addr)
+    name, _, fmt = _KNOWN[runtime_type]
+    sel = _selector(config, consumer, runtime_type)
+    sel.pop("exclude_clusters", None)         # the same cluster's instances are fine through Consul
+    try:
+        insts = [i for i in client.select_services(sel) if i.get("name", "").endswith(name)]
+    except Exception:  # noqa: BLE001 - no agent on this node
+        return None
+    addrs = sorted(f"{i['host']}:{i['port']}" for i in insts)
+    return fmt(addrs) if addrs else None
+
+
 def discover_service(runtime_type: str, config: Dict[str, Any], head_ip: Optional[str] = None,
                      consumer: Optional[str] = None, global_variables=None,
-                     worker_ips: Optional[List[str]] = None):
-    """Same cluster first, then the workspace (the order the reference runtimes use)."""
+                     worker_ips: Optional[List[str]] = None, consul_address: Optional[str] = None):
+    """Same cluster first, then Consul (when an agent address is known), then the workspace
+    (the order the reference runtimes use); nothing when the consumer turned discovery of
+    this dependency off."""
+    if not is_service_discovery(config, consumer, runtime_type):
+        return None
     on_head: Callable = globals()[f"discover_{runtime_type}_on_head"]
     from_ws: Callable = globals()[f"discover_{runtime_type}_from_workspace"]
     if head_ip:
         r = on_head(config, head_ip) if runtime_type == "database" else on_head(config, head_ip, worker_ips)
         if r:
             return r
+    if runtime_type != "database":
+        r = discover_from_consul(runtime_type, config, consumer, consul_address)
+        if r:
+            return r
     return from_ws(config, consumer, global_variables)
+
+
+def discover_hdfs_name(config: Dict[str, Any], head_ip: Optional[str] = None, consumer: Optional[str] = None,
+                       global_variables=None) -> Optional[str]:
+    """The HDFS URI a consumer writes into fs.defaultFS: the HA nameservice
+    (``hdfs://<cluster>``) when the cluster's HDFS runs ``cluster_mode: ha_cluster``, else the
+    single NameNode's address."""
+    hdfs = (config.get("runtime", {}) or {}).get("hdfs", {}) or {}
+    if "hdfs" in _runtime_types(config) and hdfs.get("cluster_mode") == "ha_cluster":
+        return f"hdfs://{(hdfs.get('ha_cluster') or {}).get('name_service') or config.get('cluster_name', 'cloudtik')}"
+    return discover_service("hdfs", config, head_ip, consumer, global_variables)
+
+
+def with_database_environment_variables(config: Dict[str, Any], consumer: str, head_ip: Optional[str] = None,
+                                        global_variables=None) -> Dict[str, str]:
+    """``CLOUDTIK_DATABASE_{ENGINE,HOST,PORT,USERNAME,PASSWORD}`` for the consumer runtime's
+    database: its explicit ``database`` section, else discovery (same cluster, workspace)."""
+    rc = (config.get("runtime", {}) or {}).get(consumer, {}) or {}
+    db = dict(rc.get("database") or {})
+    if not db.get("address") and not db.get("host"):
+        found = None
+        if is_service_discovery(config, consumer, "database"):
+            found = (discover_database_on_head(config, head_ip) if head_ip else None) or \
+                discover_database_from_workspace(config, consumer, global_variables)
+        if not found:
+            return {}
+        db = dict(found, **{k: v for k, v in db.items() if v})
+    engine = db.get("engine", "mysql")
+    return {"CLOUDTIK_DATABASE_ENGINE": engine,
+            "CLOUDTIK_DATABASE_HOST": str(db.get("address") or db.get("host")),
+            "CLOUDTIK_DATABASE_PORT": str(db.get("port") or (3306 if engine == "mysql" else 5432)),
+            "CLOUDTIK_DATABASE_USERNAME": str(db.get("username") or db.get("user") or
+                                              ("root" if engine == "mysql" else "postgres")),
+            "CLOUDTIK_DATABASE_PASSWORD": str(db.get("password") or "cloudtik")}

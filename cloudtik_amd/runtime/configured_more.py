@@ -108,6 +108,9 @@ class MetastoreRuntime(ConfiguredRuntime):
     def with_environment_variables(self, config, provider, node_id):
         env = super().with_environment_variables(config, provider, node_id)
         env["METASTORE_URI"] = "thrift://$CLOUDTIK_HEAD_IP:9083"
+        # the backing database: explicit section, the cluster's MySQL / Postgres, or the workspace
+        from cloudtik_amd.runtime.common.discovery import with_database_environment_variables
+        env.update(with_database_environment_variables(config or {}, "metastore", "$CLOUDTIK_HEAD_IP"))
         return env
 
 

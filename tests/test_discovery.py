@@ -107,3 +107,42 @@ def test_discovery_from_workspace_and_on_head():
     assert disc.discover_zookeeper_on_head(own, "10.1.0.1", ["10.1.0.5"]) == "10.1.0.5:2181"
     assert disc.discover_service("hdfs", own, head_ip="10.1.0.1") == "hdfs://10.1.0.1:8020"
     assert disc.discover_service("metastore", own, head_ip="10.1.0.1", global_variables=gv) == "thrift://10.4.0.1:9083"
+
+
+def test_discovery_switches_consul_ha_name_and_database_env():
+    from cloudtik_amd.runtime.common import discovery as D
+
+    class FakeConsul:
+        def select_services(self, sel):
+            assert sel["runtimes"] == ["zookeeper"] and "exclude_clusters" not in sel
+            return [{"name": "c2-zookeeper", "host": "10.1.0.3", "port": 2181},
+                    {"name": "c2-zookeeper", "host": "10.1.0.2", "port": 2181}]
+
+    cfg = {"cluster_name": "c1", "runtime": {"types": ["kafka"], "kafka": {}}}
+    assert D.discover_from_consul("zookeeper", cfg, "kafka", client=FakeConsul()) == "10.1.0.2:2181,10.1.0.3:2181"
+    off = {"cluster_name": "c1", "runtime": {"types": ["kafka"], "kafka": {"zookeeper_service_discovery": False}}}
+    assert D.discover_service("zookeeper", off, "10.0.0.1", consumer="kafka", global_variables={}) is None
+    ha = {"cluster_name": "c1", "runtime": {"types": ["hdfs"], "hdfs": {"cluster_mode": "ha_cluster"}}}
+    assert D.discover_hdfs_name(ha) == "hdfs://c1"
+    single = {"cluster_name": "c1", "runtime": {"types": ["hdfs"]}}
+    assert D.discover_hdfs_name(single, "10.0.0.1") == "hdfs://10.0.0.1:8020"
+    on_head = {"cluster_name": "c1", "runtime": {"types": ["postgres", "metastore"], "metastore": {}}}
+    env = D.with_database_environment_variables(on_head, "metastore", "10.0.0.1", global_variables={})
+    assert env["CLOUDTIK_DATABASE_ENGINE"] == "postgres" and env["CLOUDTIK_DATABASE_HOST"] == "10.0.0.1"
+    assert env["CLOUDTIK_DATABASE_PORT"] == "5432" and env["CLOUDTIK_DATABASE_USERNAME"] == "postgres"
+    explicit = {"runtime": {"types": ["metastore"], "metastore": {"database": {
+        "engine": "mysql", "address": "db.example", "username": "hive", "password": "pw"}}}}
+    env = D.with_database_environment_variables(explicit, "metastore")
+    assert env["CLOUDTIK_DATABASE_HOST"] == "db.example" and env["CLOUDTIK_DATABASE_PORT"] == "3306"
+    assert D.with_database_environment_variables({"runtime": {"types": []}}, "metastore", global_variables={}) == {}
+
+
+def test_workspace_global_variables_through_the_provider(tmp_path, monkeypatch):
+    """_workspace_global_variables reaches the real workspace provider (local registry)."""
+    from cloudtik_amd.runtime.common import discovery as D
+    from cloudtik_amd.providers.local import workspace_provider as lwp
+    from cloudtik_amd.core.provider_factory import get_workspace_provider
+    monkeypatch.setattr(lwp, "STATE_DIR", str(tmp_path))
+    cfg = {"provider": {"type": "local"}, "workspace_name": "w", "cluster_name": "c1"}
+    get_workspace_provider(cfg["provider"], "w").publish_global_variables(cfg, {"service.c1.x": "{}"})
+    assert "service.c1.x" in D._workspace_global_variables(cfg)
