@@ -194,9 +194,20 @@ class DockerNodes:
         return args + [image, "sleep", "infinity"]
 
     def data_disks(self, node_id: str, node_config: Dict[str, Any], tags: Dict[str, str], seq: int) -> List[str]:
-        n = int(node_config.get("data_disks", 0) or 0)
+        """Host directories backing the node's data disks: ``data_disks`` is either a count
+        (directories under ``data_disk_root``) or, as in the reference's virtual configs, a
+        list of host disk roots -- one per-node directory on each."""
+        spec = node_config.get("data_disks") or 0
         owner = f"{self.cluster}-node-{seq}" if self.cfg.get("permanent_data_volumes") else node_id
-        return [os.path.join(self.disk_root, owner, f"disk_{k}") for k in range(1, n + 1)]
+        if isinstance(spec, (list, tuple)):
+            return [os.path.join(os.path.expanduser(root), owner) for root in spec]
+        return [os.path.join(self.disk_root, owner, f"disk_{k}") for k in range(1, int(spec) + 1)]
+
+    def stop_disks(self, node_id: str, node_config: Optional[Dict[str, Any]]) -> List[str]:
+        spec = (node_config or {}).get("data_disks")
+        if isinstance(spec, (list, tuple)):
+            return [os.path.join(os.path.expanduser(root), node_id) for root in spec]
+        return [os.path.join(self.disk_root, node_id)]
 
     def start(self, node_id: str, node_config, tags, alloc, seq: int) -> str:
         self.ensure_network()
@@ -213,9 +224,10 @@ class DockerNodes:
 
     def stop(self, node_id: str, node_config: Optional[Dict[str, Any]] = None, seq: int = 0):
         self._d("rm", "-f", node_id, check=False)
-        if not self.cfg.get("permanent_data_volumes"):
+        if not self.cfg.get("permanent_data_volumes") and self.cfg.get("data_disks.delete_on_termination", True):
             import shutil
-            shutil.rmtree(os.path.join(self.disk_root, node_id), ignore_errors=True)
+            for d in self.stop_disks(node_id, node_config):
+                shutil.rmtree(d, ignore_errors=True)
 
     def running(self) -> Dict[str, Dict[str, str]]:
         out = self._d("ps", "--filter", f"label=cloudtik-cluster-name={self.cluster}", "--format", "{{.Names}}",

@@ -148,9 +148,12 @@ class VirtualNodeProvider(NodeProvider):
                 nid = f"{self.cluster_name}-{seq}"
                 node = {"state": "running", "ip": f"{self.prefix}.{seq}", "tags": dict(tags),
                         "instance_type": node_config.get("instance_type", "virtual"),
-                        "gpu_ids": node_config.get("gpu_ids"), "seq": seq}
+                        "gpu_ids": node_config.get("gpu_ids"), "seq": seq, "node_config": node_config}
                 if self.containers is not None:
-                    res = node_config.get("resources") or {}
+                    # sizes: the reference's instance_type {CPU, memory, GPU} or resources
+                    res = dict(node_config.get("resources") or {})
+                    if isinstance(node_config.get("instance_type"), dict):
+                        res.update(node_config["instance_type"])
                     alloc_tab = st.setdefault("alloc", {})
                     alloc = self.containers.scheduler.allocate(
                         alloc_tab, int(node_config.get("gpus", res.get("GPU", 0)) or 0),
@@ -179,7 +182,7 @@ class VirtualNodeProvider(NodeProvider):
             if n:
                 n["state"] = "terminated"
                 if n.get("container") and self.containers is not None:
-                    self.containers.stop(n["container"], seq=n.get("seq", 0))
+                    self.containers.stop(n["container"], n.get("node_config"), seq=n.get("seq", 0))
                     st.get("alloc", {}).pop(node_id, None)
 
     # ------------------------------------------------------------------ execution
@@ -211,7 +214,7 @@ class VirtualNodeProvider(NodeProvider):
                 if self.containers is not None:
                     for nid, n in st.get("nodes", {}).items():
                         if n.get("container") and n.get("state") == "running":
-                            self.containers.stop(n["container"], seq=n.get("seq", 0))
+                            self.containers.stop(n["container"], n.get("node_config"), seq=n.get("seq", 0))
                 st["nodes"] = {}
                 st["alloc"] = {}
                 st["next_seq"] = 1

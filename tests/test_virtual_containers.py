@@ -118,3 +118,35 @@ def test_container_executor_runs_inside(tmp_path, monkeypatch):
     assert r.cmds[-1][:4] == ["docker", "exec", nid, "bash"]
     ex.run_rsync_up("/tmp/x", "/root/y/z")
     assert r.cmds[-1] == ["docker", "cp", "/tmp/x", f"{nid}:/root/y/z"]
+
+
+def test_reference_virtual_node_config_format(tmp_path, monkeypatch):
+    """The reference's virtual configs size nodes with instance_type {CPU, memory} and give
+    data_disks as host disk roots (examples/lab/config/*.yaml)."""
+    docker = FakeDocker()
+    p = _provider(tmp_path, monkeypatch, docker)
+    disks = tmp_path / "disks"
+    nc = {"instance_type": {"CPU": 4, "memory": "4G"}, "data_disks": [str(disks)], "data_dirs": [str(tmp_path / "share")]}
+    nid, node = next(iter(p.create_node(nc, {T.CLOUDTIK_TAG_NODE_KIND: "worker"}, 1).items()))
+    args = docker.containers[nid]["args"]
+    assert len(node["alloc"]["cpus"]) == 4 and _arg(args, "--memory") == ["4096m"]
+    assert f"{disks}/{nid}:/mnt/cloudtik/data_disk_1" in _arg(args, "-v") and (disks / nid).is_dir()
+    p.terminate_node(nid)
+    assert not (disks / nid).exists()
+
+
+@pytest.mark.skipif(not __import__("os").path.isdir("/root/reference/examples/lab/config"),
+                    reason="reference lab configs not present")
+def test_reference_lab_configs_bootstrap(tmp_path):
+    import glob
+    import os
+    from cloudtik_amd.core.cluster_config import load_cluster_config
+    src = "/root/reference/examples/lab/config"
+    for f in sorted(glob.glob(f"{src}/*.yaml")):
+        text = open(f).read().replace("{%user%}", "cloudtik")
+        dst = tmp_path / os.path.basename(f)
+        dst.write_text(text)
+    # the lab's inheritance (from: bootstrap / lab) resolves against its own directory
+    for f in sorted(tmp_path.glob("*.yaml")):
+        cfg = load_cluster_config(str(f))
+        assert cfg["provider"]["type"] == "virtual", f
