@@ -131,7 +131,14 @@ class ResNet(nn.Module):
             self.to(memory_format=torch.channels_last)
 
     def stem(self, x):
-        return F.max_pool2d(self.bn1(self.conv1(x)), 3, 2, 1)
+        y = self.conv1(x)
+        bn = self.bn1
+        if bn.relu and self.training and not bn.frozen:
+            # BN + ReLU + 3x3/2 max-pool in one pass (the full-resolution activation is never
+            # written; ops/functional.py batch_norm_relu_maxpool)
+            return ops.batch_norm_relu_maxpool(y, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                               training=True, momentum=bn.momentum, eps=bn.eps)
+        return F.max_pool2d(bn(y), 3, 2, 1)
 
     def features(self, x):
         """[C2, C3, C4, C5] (strides 4, 8, 16, 32)."""

@@ -407,6 +407,99 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// ResNet stem: y = maxpool3x3/s2/p1(relu(x * a + b)) in one pass over x -- the full-resolution
+// BN output is never written (nor read back by the pool): the BN backward recomputes its ReLU
+// mask from x (mode 2), and the pool backward needs only the argmax, kept as one byte per
+// element (window position kh*3+kw; ties go to the first maximum in row-major window order,
+// as PyTorch's kernel does).  One thread = one output pixel x 8 channels.
+__global__ __launch_bounds__(256) void bn_apply_pool_kernel(const bf16_t* __restrict__ x, const float* __restrict__ a,
+                                                            const float* __restrict__ b, bf16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ arg, int N, int H, int W, int CV,
+                                                            int OH, int OW) {
+  const long total = (long)N * OH * OW * CV;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const bool fixed = bn_fixed_cv(CV);
+  float av[8], bv[8];
+  if (fixed) { bn_load8(a, threadIdx.x % CV, av); bn_load8(b, threadIdx.x % CV, bv); }
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total; v += stride) {
+    const int cv = (int)(v % CV);
+    long t = v / CV;
+    const int ow = (int)(t % OW); t /= OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    if (!fixed) { bn_load8(a, cv, av); bn_load8(b, cv, bv); }
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = 2 * oh - 1 + kh;
+      if (h < 0 || h >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = 2 * ow - 1 + kw;
+        if (w < 0 || w >= W) continue;
+        const u16x8 xv = reinterpret_cast<const u16x8*>(x)[(((long)n * H + h) * W + w) * CV + cv];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // compare the bf16-rounded activation: the pooled value is the BN output as stored
+          const float t8 = bf2f(f2bf(fmaxf(bn_pre(bf2f(xv[j]), av[j], bv[j], 0.f), 0.f)));
+          if (t8 > best[j]) { best[j] = t8; bi[j] = (uint8_t)(kh * 3 + kw); }
+        }
+      }
+    }
+    u16x8 o;
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { o[j] = f2bf(best[j]); packed |= (uint64_t)bi[j] << (8 * j); }
+    reinterpret_cast<u16x8*>(y)[v] = o;
+    reinterpret_cast<uint64_t*>(arg)[v] = packed;
+  }
+}
+
+// dx[n,h,w,c] = sum of dy over the (<= 4) pooling windows whose argmax is (h, w): a gather, so
+// no zero-fill and no atomics; one thread = one input pixel x 8 channels.
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                             const uint8_t* __restrict__ arg,
+                                                             bf16_t* __restrict__ dx, int N, int H, int W, int CV,
+                                                             int OH, int OW) {
+  const long total = (long)N * H * W * CV;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total; v += stride) {
+    const int cv = (int)(v % CV);
+    long t = v / CV;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // windows o with 2o-1 <= h <= 2o+1
+    const int oh0 = h >> 1, oh1 = min((h + 1) >> 1, OH - 1);
+    const int ow0 = w >> 1, ow1 = min((w + 1) >> 1, OW - 1);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int kh = h - (2 * oh - 1);
+      if (kh < 0 || kh > 2) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int kw = w - (2 * ow - 1);
+        if (kw < 0 || kw > 2) continue;
+        const long o = (((long)n * OH + oh) * OW + ow) * CV + cv;
+        const uint64_t packed = reinterpret_cast<const uint64_t*>(arg)[o];
+        const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
+        const uint8_t pos = (uint8_t)(kh * 3 + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((packed >> (8 * j)) & 0xFF) == pos) acc[j] += bf2f(g[j]);
+      }
+    }
+    u16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = f2bf(acc[j]);
+    reinterpret_cast<u16x8*>(dx)[v] = out;
+  }
+}
+
 inline BnLayout bn_layout(int M, int C, int target_blocks) {
   BnLayout L;
   L.M = M; L.C = C; L.CV = C / 8;
@@ -476,6 +569,35 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
   const long tv = (long)M * (C / 8);
   BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, stat + 2 * C, stat + 3 * C,
                  (bf16_t*)y, tv, C / 8, relu);
+  return 0;
+}
+
+// ResNet stem: batch statistics of x, then y = maxpool3x3/s2/p1(relu(bn(x))) + byte argmax
+// (stat = float[4C] as ct_bn_fwd_train)
+extern "C" int ct_bn_fwd_train_pool(const void* x, const void* gamma, const void* beta, float* run_mean,
+                                    float* run_var, void* y, void* arg, float* part, float* stat, int N, int H, int W,
+                                    int C, int OH, int OW, float eps, float momentum, hipStream_t stream) {
+  const int M = N * H * W;
+  if (C % 8 || C / 8 > BN_RT || M <= 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  BnLayout L = bn_layout(M, C, bn_target_blocks());
+  const int nblk = bn_nblk(L);
+  bn_stats_kernel<<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
+  bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)2048 * C, nblk, L,
+                                                           (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                           eps, momentum, run_mean, run_var, stat,
+                                                           stat + C, stat + 2 * C, stat + 3 * C);
+  const long tv = (long)N * OH * OW * (C / 8);
+  bn_apply_pool_kernel<<<ew_grid(tv, 1), 256, 0, stream>>>((const bf16_t*)x, stat + 2 * C, stat + 3 * C, (bf16_t*)y,
+                                                           (uint8_t*)arg, N, H, W, C / 8, OH, OW);
+  return 0;
+}
+
+extern "C" int ct_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, int OH,
+                                 int OW, hipStream_t stream) {
+  if (C % 8 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  const long tv = (long)N * H * W * (C / 8);
+  maxpool3s2_bwd_kernel<<<ew_grid(tv, 1), 256, 0, stream>>>((const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, N, H,
+                                                            W, C / 8, OH, OW);
   return 0;
 }
 

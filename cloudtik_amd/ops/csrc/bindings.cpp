@@ -41,6 +41,9 @@ int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, co
 int ct_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, float*,
                     float*, int, int, float, float, int, hipStream_t);
 int ct_bn_apply(const void*, const void*, const float*, const float*, void*, int, int, int, hipStream_t);
+int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
+                         int, int, int, int, float, float, hipStream_t);
+int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
 int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, void*, void*, void*, void*, int,
               float*, float*, int, int, int, hipStream_t);
 int ct_attn_fwd(const void*, const long*, const void*, const long*, const void*, const long*, void*,
@@ -443,6 +446,42 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
   return {y, stat};
 }
 
+// ResNet stem: returns (y_pool [N, C, OH, OW] channels_last, argmax bytes [N, OH, OW, C] uint8, stat)
+std::vector<at::Tensor> bn_fwd_train_pool(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor run_mean,
+                                          at::Tensor run_var, double eps, double momentum) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "bn_fwd_train_pool: 4-D NHWC input");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_fwd_train_pool: C % 8 == 0, C <= 2048");
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  CHECK_F32(run_mean); CHECK_F32(run_var);
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto arg = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  auto stat = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
+  auto part = at::empty({2 * 2048 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_fwd_train_pool(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr<float>(),
+                                run_var.data_ptr<float>(), y.data_ptr(), arg.data_ptr(), part.data_ptr<float>(),
+                                stat.data_ptr<float>(), N, H, W, C, OH, OW, (float)eps, (float)momentum, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_fwd_train_pool: unsupported shape");
+  return {y, arg, stat};
+}
+
+// gradient of maxpool3x3/s2/p1 from the byte argmax: dx [N, C, H, W] channels_last
+at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W) {
+  at::Tensor dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dyc, "dy");
+  const int N = dyc.size(0), C = dyc.size(1), OH = dyc.size(2), OW = dyc.size(3);
+  TORCH_CHECK(arg.scalar_type() == at::kByte && arg.is_contiguous() && arg.numel() == dyc.numel(),
+              "maxpool3s2_bwd: argmax bytes");
+  TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && C % 8 == 0, "maxpool3s2_bwd: shape");
+  auto dx = at::empty({N, C, (long)H, (long)W}, dyc.options().memory_format(at::MemoryFormat::ChannelsLast));
+  int rc = ct_maxpool3s2_bwd(dyc.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, (int)H, (int)W, C, OH, OW,
+                             cur_stream());
+  TORCH_CHECK(rc == 0, "maxpool3s2_bwd: unsupported shape");
+  return dx;
+}
+
 at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, at::Tensor b, bool relu) {
   check_nhwc(x, "x");
   const int C = x.size(1);
@@ -527,6 +566,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd", &xent_fwd);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply", &bn_apply);
+  m.def("bn_fwd_train_pool", &bn_fwd_train_pool);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("attn_fwd_relbias", &attn_fwd_relbias);
   m.def("attn_fwd", &attn_fwd);

@@ -219,6 +219,52 @@ class _BNActFn(torch.autograd.Function):
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None
 
 
+def _bn_param_grads(wp, bp, gamma, x, stat, dy, y, mode, has_res):
+    """BN backward shared by the BN(+ReLU)(+pool) autograd functions: accumulates the affine
+    gradients straight into the flat gradient buffer when the parameters live there."""
+    flat = all(p is not None and p.grad is not None and getattr(p, "_ct_flat_grad", False)
+               and p.grad.is_contiguous() and p.grad.dtype == gamma.dtype for p in (wp, bp))
+    if flat:
+        dx, dres, _, _ = _C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, wp.grad, bp.grad)
+        for p in (wp, bp):
+            cb = getattr(p, "_ct_grad_ready", None)
+            if cb is not None:
+                cb(p)
+        return dx, dres, None, None
+    return tuple(_C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, None, None))
+
+
+class _BNReLUPoolFn(torch.autograd.Function):
+    """ResNet stem ``maxpool3x3/s2/p1(relu(bn(x)))`` (batchnorm.hip ``bn_apply_pool_kernel``):
+    the full-resolution BN output is never materialised; the backward gathers the pooled
+    gradient through the byte argmax and runs the BN backward with the ReLU mask recomputed
+    from x."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, run_mean, run_var, momentum, eps):
+        y, arg, stat = _C().bn_fwd_train_pool(x, gamma, beta, run_mean, run_var, eps, momentum)
+        ctx.save_for_backward(x, gamma, stat, arg)
+        ctx.params = (gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dyp):
+        x, gamma, stat, arg = ctx.saved_tensors
+        dy = _C().maxpool3s2_bwd(dyp, arg, x.shape[2], x.shape[3])
+        wp, bp = ctx.params
+        dx, _, dg, db = _bn_param_grads(wp, bp, gamma, x, stat, dy, None, 2, False)
+        return dx, dg, db, None, None, None, None
+
+
+def batch_norm_relu_maxpool(x, weight, bias, running_mean, running_var, training=True, momentum=0.1, eps=1e-5):
+    """``max_pool2d(relu(BatchNorm(x)), 3, 2, 1)`` -- fused on GPU in training (NHWC bf16)."""
+    if _native(x) and _bn_native_ok(x) and x.dim() == 4 and training:
+        return _BNReLUPoolFn.apply(x, weight, bias, running_mean, running_var, float(momentum), float(eps))
+    y = batch_norm_act(x, weight, bias, running_mean, running_var, relu=True, training=training,
+                       momentum=momentum, eps=eps)
+    return torch.nn.functional.max_pool2d(y, 3, 2, 1)
+
+
 class _BNAffineFn(torch.autograd.Function):
     """Frozen BatchNorm (running statistics) + residual + ReLU with autograd: the forward is
     the fused ``bn_apply`` HIP kernel; the backward is ``dy * relu_mask * scale`` (the affine

@@ -212,6 +212,46 @@ def test_batchnorm_act(cuda, C, HW, res):
         assert _rel(a, t.grad) < 2e-2
 
 
+@pytest.mark.parametrize("HW", [112, 37])
+@pytest.mark.parametrize("shift", [0.5, -1.0])      # -1.0: most activations ReLU to 0 -> many ties
+def test_bn_relu_maxpool_stem(cuda, HW, shift):
+    """Fused ResNet stem (bn_apply_pool_kernel + maxpool3s2_bwd_kernel) vs the unfused native
+    BN + PyTorch max_pool2d on the same bf16 tensors, and vs an fp32 reference."""
+    torch.manual_seed(1)
+    N, C = 4, 64
+    x0 = (torch.randn(N, C, HW, HW, device=cuda) + shift).bfloat16().contiguous(memory_format=torch.channels_last)
+    g0 = (1 + 0.1 * torch.randn(C, device=cuda)).bfloat16()
+    b0 = (0.1 * torch.randn(C, device=cuda)).bfloat16()
+    outs = []
+    for fused in (True, False):
+        x, g, b = (t.clone().requires_grad_() for t in (x0, g0, b0))
+        rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+        if fused:
+            y = ops.batch_norm_relu_maxpool(x, g, b, rm, rv, training=True)
+        else:
+            y = torch.nn.functional.max_pool2d(ops.batch_norm_act(x, g, b, rm, rv, relu=True, training=True), 3, 2, 1)
+        torch.manual_seed(2)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        outs.append((y.detach(), x.grad, g.grad, b.grad, rm, rv))
+    (yf, dxf, dgf, dbf, rmf, rvf), (yu, dxu, dgu, dbu, rmu, rvu) = outs
+    assert yf.shape == (N, C, (HW - 1) // 2 + 1, (HW - 1) // 2 + 1) and yf.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(yf, yu)                                  # same stats, same rounding, same max
+    assert torch.equal(rmf, rmu) and torch.equal(rvf, rvu)
+    assert _rel(dxf, dxu) < 1e-2 and _rel(dgf, dgu) < 1e-2 and _rel(dbf, dbu) < 1e-2
+    # fp32 reference
+    xr, gr, br = (t.detach().float().requires_grad_() for t in (x0, g0, b0))
+    yr = torch.nn.functional.max_pool2d(torch.relu(torch.nn.functional.batch_norm(
+        xr, torch.zeros(C, device=cuda), torch.ones(C, device=cuda), gr, br, True, 0.1, 1e-5)), 3, 2, 1)
+    yr.backward(dy.float())
+    assert _rel(yf, yr) < 1e-2
+    if shift > 0:
+        # with most activations ReLU'd to 0 the window maxima are near-ties whose winner
+        # differs between bf16 and fp32 activations, so the gradient routing is only
+        # comparable (exactly, above) against the same bf16 tensors
+        assert _rel(dxf, xr.grad) < 3e-2 and _rel(dgf, gr.grad) < 3e-2
+
+
 def test_linear_fused_wgrad(cuda):
     from cloudtik_amd.train.optim import FlatParamSpace
     torch.manual_seed(0)
