@@ -1,6 +1,7 @@
 // Bindings for RoPE, EmbeddingBag / interaction, detection ops and multi-tensor copy.
 // Host-side shape / dtype / alignment validation happens here, before any launch.
 #include <torch/extension.h>
+#include <cstring>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
@@ -32,6 +33,7 @@ int ct_rnnt_bwd(const void*, int, const int*, const int*, const int*, const floa
                 const float*, const float*, const float*, void*, int, int, int, int, int, hipStream_t);
 int ct_gemm_tn(const void*, long, const void*, long, void*, int, int, long, int, int, hipStream_t);
 int ct_mt_copy(const uint64_t*, const int64_t*, const int64_t*, int, long, void*, int, int, float, int, hipStream_t);
+int ct_mt_add(const int64_t*, int, int, hipStream_t);
 void* ct_loader_create(int, const void* const*, const long*, long, int, int, uint64_t, int, int, int, int, int, int);
 long ct_loader_num_batches(void*);
 void ct_loader_set_epoch(void*, long);
@@ -451,6 +453,41 @@ void mt_copy(std::vector<at::Tensor> tensors, at::Tensor flat, double scale, boo
   TORCH_CHECK(rc == 0, "mt_copy: too many tensors");
 }
 
+// dsts[t] += srcs[t] (same dtype, same strides, dense) for all t in one launch: chunks of
+// 64K elements, table (src, dst, n) per chunk staged through pinned memory
+void mt_add_(std::vector<at::Tensor> srcs, std::vector<at::Tensor> dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "mt_add_: list lengths differ");
+  if (srcs.empty()) return;
+  const auto dt = srcs[0].scalar_type();
+  TORCH_CHECK(dt == at::kFloat || dt == at::kBFloat16, "mt_add_: fp32 / bf16");
+  constexpr long CH = 65536;
+  std::vector<int64_t> tab;
+  for (size_t t = 0; t < srcs.size(); ++t) {
+    auto& a = srcs[t];
+    auto& b = dsts[t];
+    TORCH_CHECK(a.is_cuda() && b.is_cuda(), "mt_add_: GPU tensors");
+    TORCH_CHECK(a.scalar_type() == dt && b.scalar_type() == dt, "mt_add_: mixed dtypes");
+    bool same = a.sizes() == b.sizes();
+    for (int64_t d = 0; same && d < a.dim(); ++d)
+      if (a.size(d) > 1 && a.stride(d) != b.stride(d)) same = false;     // size-1 dims: any stride
+    TORCH_CHECK(same && a.is_non_overlapping_and_dense() && b.is_non_overlapping_and_dense(),
+                "mt_add_: src / dst layouts differ");
+    TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "mt_add_: alignment");
+    const long n = a.numel();
+    const long es = a.element_size();
+    for (long o = 0; o < n; o += CH) {
+      tab.push_back((int64_t)((uintptr_t)a.data_ptr() + o * es));
+      tab.push_back((int64_t)((uintptr_t)b.data_ptr() + o * es));
+      tab.push_back(std::min(CH, n - o));
+    }
+  }
+  auto host = at::empty({(long)tab.size()}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+  std::memcpy(host.data_ptr<int64_t>(), tab.data(), tab.size() * sizeof(int64_t));
+  auto dev = host.to(srcs[0].device(), /*non_blocking=*/true);
+  const int rc = ct_mt_add(dev.data_ptr<int64_t>(), (int)(tab.size() / 3), dt == at::kFloat ? 1 : 0, stream());
+  TORCH_CHECK(rc == 0, "mt_add_: too many chunks");
+}
+
 // ---------------------------------------------------------------- native loader
 // cols: CPU contiguous tensors whose dim 0 is the row; the Python wrapper keeps them alive
 int64_t loader_create(std::vector<at::Tensor> cols, int64_t batch, bool shuffle, int64_t seed, bool drop_last,
@@ -541,4 +578,5 @@ void register_ext(pybind11::module& m) {
   m.def("focal_fwd", &focal_fwd);
   m.def("focal_bwd", &focal_bwd);
   m.def("mt_copy", &mt_copy);
+  m.def("mt_add_", &mt_add_);
 }

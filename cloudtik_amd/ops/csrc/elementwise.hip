@@ -300,6 +300,41 @@ extern "C" int ct_splitk_reduce(const float* P, int S, long n, void* g, int accu
   return 0;
 }
 
+// ---------------------------------------------------------------- multi-tensor accumulate
+// dst_t += src_t for a list of (src, dst, n) chunks in ONE launch (block = chunk): the
+// deferred conv-weight gradients of train/optim.py FlatParamSpace land in the flat gradient
+// buffer with this instead of one AccumulateGrad add kernel per parameter.  Chunks start at
+// 16-byte-aligned element offsets; the tail of a chunk runs element-wise.
+template <typename T>
+__global__ void __launch_bounds__(256) mt_add_kernel(const int64_t* __restrict__ table) {
+  const T* src = reinterpret_cast<const T*>(table[3 * blockIdx.x]);
+  T* dst = reinterpret_cast<T*>(table[3 * blockIdx.x + 1]);
+  const long n = table[3 * blockIdx.x + 2];
+  constexpr int V = 16 / sizeof(T);
+  const long nv = n / V;
+  for (long i = threadIdx.x; i < nv; i += blockDim.x) {
+    if (sizeof(T) == 2) {
+      u16x8 a = reinterpret_cast<const u16x8*>(src)[i], b = reinterpret_cast<u16x8*>(dst)[i], o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(b[j]) + bf2f(a[j]));
+      reinterpret_cast<u16x8*>(dst)[i] = o;
+    } else {
+      f32x4 a = reinterpret_cast<const f32x4*>(src)[i], b = reinterpret_cast<f32x4*>(dst)[i];
+      reinterpret_cast<f32x4*>(dst)[i] = a + b;
+    }
+  }
+  for (long i = nv * V + threadIdx.x; i < n; i += blockDim.x)
+    dst[i] = from_f<T>(to_f<T>(dst[i]) + to_f<T>(src[i]));
+}
+
+extern "C" int ct_mt_add(const int64_t* table, int nchunks, int is_f32, hipStream_t stream) {
+  if (nchunks <= 0) return 0;
+  if (nchunks > 65535 * 32) return -1;
+  if (is_f32) mt_add_kernel<float><<<nchunks, 256, 0, stream>>>(table);
+  else mt_add_kernel<bf16_t><<<nchunks, 256, 0, stream>>>(table);
+  return 0;
+}
+
 // ---------------------------------------------------------------- multi-tensor pack / unpack
 // Gradient-bucket flatten for collectives (reference SSD distributed.py:13-48 and Horovod
 // tensor fusion, SURVEY.md §2.15 "Gradient bucket pack/scale/unpack"): tensor t (ptrs[t],

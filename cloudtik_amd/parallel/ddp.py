@@ -144,6 +144,7 @@ class GradBucketer:
 
     def _launch(self, b):
         from cloudtik_amd.ops.linear import grad_stream
+        self.space.flush_grads()            # deferred conv-weight grads -> flat buffer
         side = grad_stream()
         if self.p2p is not None and self._p2p_fits(b):
             # the one-shot kernel spins until the slowest rank reaches this bucket: give it
@@ -221,6 +222,7 @@ class GradBucketer:
     def accumulate_local(self):
         """fp32 mode: move this backward's gradients into the fp32 buffer (no communication)."""
         from cloudtik_amd.ops.linear import sync_grad_stream
+        self.space.flush_grads()
         if self.space.grad.is_cuda:
             sync_grad_stream()
         self.space.main_grad.add_(self.space.grad)
@@ -230,6 +232,7 @@ class GradBucketer:
         """Launch any bucket not yet launched (unused params / no overlap), then make the
         compute stream wait for every reduction.  Call before optimizer.step()."""
         from cloudtik_amd.ops.linear import sync_grad_stream
+        self.space.flush_grads()
         if self.world <= 1:
             if self.space.grad.is_cuda:
                 sync_grad_stream()

@@ -24,6 +24,7 @@ DLRM split-SGD).  On CPU the identical math runs in PyTorch.
 from __future__ import annotations
 
 import math
+from collections import OrderedDict
 from typing import Callable, Iterable, List, Optional, Sequence, Tuple
 
 import torch
@@ -55,10 +56,16 @@ def _flat_view(flat: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
     return flat.as_strided(like.shape, like.stride())
 
 
+def _same_order(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape and the same strides on every dim of size > 1 (``b`` dense => ``a`` dense
+    with the same element order)."""
+    return a.shape == b.shape and all(sa == sb for sa, sb, n in zip(a.stride(), b.stride(), a.shape) if n > 1)
+
+
 class FlatParamSpace:
     def __init__(self, params: Sequence[torch.nn.Parameter], names: Optional[Sequence[str]] = None,
                  grad_dtype: Optional[torch.dtype] = None, shard: Tuple[int, int] = (0, 1),
-                 align: int = ALIGN, reverse: bool = True):
+                 align: int = ALIGN, reverse: bool = True, defer_conv_grads: Optional[bool] = None):
         params = [p for p in params if p.requires_grad]
         assert params, "no trainable parameters"
         names = list(names) if names is not None else [f"p{i}" for i in range(len(params))]
@@ -89,6 +96,18 @@ class FlatParamSpace:
         dev = self.device
         self.model = torch.zeros(self.total, dtype=self.dtype, device=dev)
         self.grad = torch.zeros(self.total, dtype=self.grad_dtype, device=dev)
+        # Deferred conv-weight gradients: autograd's AccumulateGrad adds every conv weight
+        # gradient into a preset .grad with its own small kernel (53 launch-bound adds per
+        # ResNet-50 step).  Instead these parameters keep .grad unset, so AccumulateGrad just
+        # takes MIOpen's output tensor; a post-accumulate hook records the parameter and
+        # flush_grads() adds all recorded gradients into the flat buffer with ONE multi-tensor
+        # kernel (ops mt_add_) before anything reads the buffer (bucket launch, finish,
+        # optimizer step).
+        if defer_conv_grads is None:
+            import os
+            defer_conv_grads = os.environ.get("CLOUDTIK_AMD_DEFER_CONV_GRADS", "1") == "1"
+        self._deferred: "OrderedDict[int, torch.nn.Parameter]" = OrderedDict()
+        self._hooks = []
         with torch.no_grad():
             for p, o, n in zip(params, self.offsets, self.numels):
                 # keep each parameter's memory layout: a channels_last conv weight stays
@@ -97,8 +116,15 @@ class FlatParamSpace:
                 # NHWC activations sends the backward pass to the naive fallback kernels)
                 self.model[o:o + n].copy_(_memory_order(p.data).reshape(-1))
                 p.data = _flat_view(self.model[o:o + n], p)
-                p.grad = _flat_view(self.grad[o:o + n], p)
-                p._ct_flat_grad = True   # ops.linear may accumulate dW straight into it
+                view = _flat_view(self.grad[o:o + n], p)
+                if defer_conv_grads and dev.type == "cuda" and p.dim() == 4 and self.grad_dtype == self.dtype:
+                    p.grad = None
+                    p._ct_flat_view = view
+                    p._ct_flat_grad = False
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_deferred))
+                else:
+                    p.grad = view
+                    p._ct_flat_grad = True   # ops.linear may accumulate dW straight into it
         # fp32 gradient the optimizer reads instead of ``grad`` when a bucketer reduces /
         # accumulates in fp32 (parallel.GradBucketer(reduce_dtype=torch.float32))
         self.main_grad: Optional[torch.Tensor] = None
@@ -201,7 +227,37 @@ class FlatParamSpace:
             return self.local_grad
         return self.reduced_grad[self.shard_lo:self.shard_hi]
 
+    # ------------------------------------------------------------------ deferred grads
+    def _on_deferred(self, p):
+        self._deferred[id(p)] = p
+
+    def flush_grads(self):
+        """Add the recorded conv-weight gradients into the flat buffer (one launch) and
+        release them; a no-op when nothing is pending."""
+        if not self._deferred:
+            return
+        ps = [p for p in self._deferred.values() if p.grad is not None]
+        self._deferred.clear()
+        srcs, dsts = [], []
+        for p in ps:
+            g, v = p.grad, p._ct_flat_view
+            # same memory order (strides of size-1 dims do not matter: a 1x1 conv weight's
+            # gradient may come back NCHW-strided while the channels_last view is not)
+            if g.dtype == v.dtype and _same_order(g, v):
+                srcs.append(g)
+                dsts.append(v)
+            else:
+                v.add_(g)
+        if srcs:
+            from cloudtik_amd import ops
+            ops.require_native().mt_add_(srcs, dsts)
+        for p in ps:
+            p.grad = None
+
     def zero_grad(self):
+        for p in self._deferred.values():
+            p.grad = None
+        self._deferred.clear()
         self.grad.zero_()
         if self.main_grad is not None:
             self.main_grad.zero_()
@@ -350,6 +406,7 @@ class FusedLAMB(_FlatOptimizer):
     def step(self, closure=None):
         _sync_grads()
         loss = closure() if closure is not None else None
+        self.space.flush_grads()
         self.step_count += 1
         sp = self.space
         b1, b2 = self.betas
@@ -454,6 +511,7 @@ class FusedAdam(_FlatOptimizer):
     def step(self, closure=None):
         _sync_grads()
         loss = closure() if closure is not None else None
+        self.space.flush_grads()
         self.step_count += 1
         sp = self.space
         b1, b2 = self.betas
@@ -502,6 +560,7 @@ class FusedSGD(_FlatOptimizer):
     def step(self, closure=None):
         _sync_grads()
         loss = closure() if closure is not None else None
+        self.space.flush_grads()
         self.step_count += 1
         sp = self.space
         self._push_dyn()

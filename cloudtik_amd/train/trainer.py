@@ -160,6 +160,8 @@ class Trainer:
         return {k: t[i].item() / n for i, k in enumerate(keys)}
 
     def _clip(self):
+        if self.space is not None:
+            self.space.flush_grads()               # deferred conv-weight grads -> flat buffer
         g = self.space.shard_grad if self.space is not None else None
         if g is None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip_norm)

@@ -252,6 +252,43 @@ def test_bn_relu_maxpool_stem(cuda, HW, shift):
         assert _rel(dxf, xr.grad) < 3e-2 and _rel(dgf, gr.grad) < 3e-2
 
 
+def test_deferred_conv_grads_match_preset(cuda):
+    """FlatParamSpace(defer_conv_grads): conv-weight gradients taken from autograd and added
+    into the flat buffer by one multi-tensor kernel (mt_add_) give the same flat gradient and
+    the same SGD trajectory as preset .grad views, across gradient accumulation."""
+    from cloudtik_amd.train.optim import FlatParamSpace, FusedSGD
+
+    def make():
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Conv2d(16, 32, 3, padding=1, bias=False), torch.nn.ReLU(),
+                                torch.nn.Conv2d(32, 32, 1, bias=False), torch.nn.Flatten(),
+                                torch.nn.Linear(32 * 8 * 8, 10)).to(cuda).bfloat16()
+        return m.to(memory_format=torch.channels_last)
+
+    results = []
+    for defer in (False, True):
+        m = make()
+        sp = FlatParamSpace(list(m.parameters()), defer_conv_grads=defer)
+        opt = FusedSGD(sp.params, lr=0.05, momentum=0.9, space=sp)
+        convs = [p for p in sp.params if p.dim() == 4]
+        assert all((p.grad is None) == defer for p in convs)
+        for step in range(3):
+            for micro in range(2):                       # accumulation: second backward adds
+                torch.manual_seed(10 * step + micro)
+                x = torch.randn(8, 16, 8, 8, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+                m(x).float().pow(2).mean().backward()
+            if step == 0:
+                sp.flush_grads()
+                results.append(sp.grad.detach().float().clone())
+            opt.step()
+            opt.zero_grad()
+            assert not defer or all(p.grad is None for p in convs)
+        results.append(sp.model.detach().float().clone())
+    g0, w0, g1, w1 = results
+    assert torch.allclose(g0, g1, rtol=1e-2, atol=1e-3)
+    assert torch.allclose(w0, w1, rtol=1e-2, atol=1e-3)
+
+
 def test_linear_fused_wgrad(cuda):
     from cloudtik_amd.train.optim import FlatParamSpace
     torch.manual_seed(0)
