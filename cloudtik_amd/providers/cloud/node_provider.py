@@ -11,7 +11,8 @@ rest_providers.py, Aliyun and Huawei Cloud over their signed HTTP APIs in signed
 from __future__ import annotations
 
 import importlib
-from typing import Any, Dict, List
+import threading
+from typing import Any, Dict, List, Optional
 
 from cloudtik_amd.core import tags as T
 from cloudtik_amd.core.node_provider import NodeLaunchException, NodeProvider
@@ -25,73 +26,214 @@ def _require(module: str, provider: str):
                            "it is not available in this environment") from e
 
 
+TAG_BATCH_DELAY = 1.0     # seconds set_node_tags waits to batch concurrent updates
+
+
 class AWSNodeProvider(NodeProvider):
-    """EC2-backed nodes (reference providers/_private/aws/node_provider.py)."""
+    """EC2 instances as nodes (reference providers/_private/aws/node_provider.py).
+
+    * node tags are EC2 tags; ``set_node_tags`` calls from the updater threads of many nodes
+      are batched (one ``create_tags`` per distinct tag set every ``TAG_BATCH_DELAY``), as
+      a 100-node launch otherwise floods the EC2 API;
+    * ``create_node`` places instances in the workspace's private subnets (round-robin over
+      ``SubnetIds``, moving to the next subnet on capacity errors), with the workspace
+      security group and the head / worker instance profile (providers/cloud/workspace.py),
+      optional spot market, and ``data_disks`` as extra gp3 EBS volumes;
+    * boto3 is loaded lazily; ``provider._client_factory`` injects a client (tests).
+    """
+
+    CAPACITY_ERRORS = ("InsufficientInstanceCapacity", "InsufficientFreeAddressesInSubnet",
+                       "InsufficientCapacity", "Unsupported")
 
     def __init__(self, provider_config, cluster_name):
         super().__init__(provider_config, cluster_name)
-        boto3 = _require("boto3", "aws")
-        self.ec2 = boto3.resource("ec2", region_name=provider_config.get("region"))
-        self.client = self.ec2.meta.client
-        self._cache: Dict[str, Any] = {}
+        factory = provider_config.get("_client_factory")
+        if factory is None:
+            boto3 = _require("boto3", "aws")
+            factory = lambda svc: boto3.client(svc, region_name=provider_config.get("region"))  # noqa: E731
+        self.ec2 = factory("ec2")
+        self._nodes: Dict[str, Dict[str, Any]] = {}
+        self.tag_cache: Dict[str, Dict[str, str]] = {}
+        self._lock = threading.RLock()
+        self._pending_tags: Dict[str, Dict[str, str]] = {}
+        self._batch_timer: Optional[threading.Timer] = None
+        self._subnet_idx = 0
 
+    # ------------------------------------------------------------------ queries
     def _filters(self, tag_filters):
         f = [{"Name": "instance-state-name", "Values": ["pending", "running"]},
              {"Name": f"tag:{T.CLOUDTIK_TAG_CLUSTER_NAME}", "Values": [self.cluster_name]}]
         f += [{"Name": f"tag:{k}", "Values": [v]} for k, v in tag_filters.items()]
         return f
 
+    def _remember(self, inst: Dict[str, Any]):
+        nid = inst["InstanceId"]
+        self._nodes[nid] = inst
+        with self._lock:
+            tags = {t["Key"]: t["Value"] for t in inst.get("Tags") or []}
+            tags.update(self._pending_tags.get(nid, {}))     # not yet flushed updates win
+            self.tag_cache[nid] = tags
+
     def non_terminated_nodes(self, tag_filters):
-        nodes = list(self.ec2.instances.filter(Filters=self._filters(tag_filters)))
-        self._cache.update({n.id: n for n in nodes})
-        return [n.id for n in nodes]
+        out, token = [], None
+        while True:
+            kw = {"Filters": self._filters(tag_filters)}
+            if token:
+                kw["NextToken"] = token
+            r = self.ec2.describe_instances(**kw)
+            for res in r.get("Reservations", []):
+                for inst in res.get("Instances", []):
+                    self._remember(inst)
+                    out.append(inst["InstanceId"])
+            token = r.get("NextToken")
+            if not token:
+                return out
 
     def _node(self, node_id):
-        n = self._cache.get(node_id)
+        n = self._nodes.get(node_id)
         if n is None:
-            n = self.ec2.Instance(node_id)
-            self._cache[node_id] = n
+            r = self.ec2.describe_instances(InstanceIds=[node_id])
+            n = r["Reservations"][0]["Instances"][0]
+            self._remember(n)
         return n
 
     def is_running(self, node_id):
-        return self._node(node_id).state["Name"] == "running"
+        return self._node(node_id)["State"]["Name"] == "running"
 
     def is_terminated(self, node_id):
-        return self._node(node_id).state["Name"] not in ("running", "pending")
+        return self._node(node_id)["State"]["Name"] not in ("running", "pending")
 
     def node_tags(self, node_id):
-        return {t["Key"]: t["Value"] for t in (self._node(node_id).tags or [])}
+        with self._lock:
+            if node_id in self.tag_cache:
+                return dict(self.tag_cache[node_id])
+        self._node(node_id)
+        with self._lock:
+            return dict(self.tag_cache.get(node_id, {}))
 
     def external_ip(self, node_id):
-        return self._node(node_id).public_ip_address
+        return self._node(node_id).get("PublicIpAddress")
 
     def internal_ip(self, node_id):
-        return self._node(node_id).private_ip_address
+        return self._node(node_id).get("PrivateIpAddress")
+
+    # ------------------------------------------------------------------ tags (batched)
+    def set_node_tags(self, node_id, tags):
+        with self._lock:
+            self._pending_tags.setdefault(node_id, {}).update(tags)
+            self.tag_cache.setdefault(node_id, {}).update(tags)
+            if self._batch_timer is None:
+                self._batch_timer = threading.Timer(TAG_BATCH_DELAY, self._flush_tags)
+                self._batch_timer.daemon = True
+                self._batch_timer.start()
+
+    def _flush_tags(self):
+        with self._lock:
+            pending, self._pending_tags = self._pending_tags, {}
+            self._batch_timer = None
+        # one create_tags per distinct tag set
+        groups: Dict[tuple, List[str]] = {}
+        for nid, tags in pending.items():
+            groups.setdefault(tuple(sorted(tags.items())), []).append(nid)
+        self._create_tags({k: v for k, v in groups.items()})
+
+    def _create_tags(self, batch_updates: Dict[tuple, List[str]]):
+        for tag_items, node_ids in batch_updates.items():
+            self.ec2.create_tags(Resources=node_ids, Tags=[{"Key": k, "Value": v} for k, v in tag_items])
+
+    def flush_tags(self):
+        """Apply pending tag updates now (also before terminate)."""
+        with self._lock:
+            if self._batch_timer is not None:
+                self._batch_timer.cancel()
+        self._flush_tags()
+
+    # ------------------------------------------------------------------ launch
+    def _workspace_defaults(self):
+        """Subnets, security group and instance profiles of the cluster's workspace
+        (providers/cloud/workspace.py AWSWorkspace) for keys the config does not set."""
+        pc = self.provider_config
+        if pc.get("_workspace_filled") or not pc.get("workspace_name") or pc.get("use_working_vpc"):
+            return
+        pc["_workspace_filled"] = True
+        try:
+            from cloudtik_amd.providers.cloud.workspace import AWSWorkspace
+            ws = AWSWorkspace(pc, pc["workspace_name"], pc.get("_client_factory"))
+            sub = ws.ec2.describe_subnets(Filters=ws._filters([{"Name": "tag:cloudtik-subnet",
+                                                                  "Values": ["private"]}]))["Subnets"]
+            pc.setdefault("subnet_ids", [x["SubnetId"] for x in sub])
+            sg = ws._sg()
+            if sg:
+                pc.setdefault("security_group_ids", [sg])
+            pc.setdefault("head_instance_profile", ws.roles["head"])
+            pc.setdefault("worker_instance_profile", ws.roles["worker"])
+        except Exception as e:  # noqa: BLE001 - no workspace resources: launch with the config as given
+            import logging
+            logging.getLogger(__name__).warning("AWS workspace defaults unavailable: %s", e)
+
+    def _subnets(self, node_config) -> List[str]:
+        ids = node_config.get("SubnetIds") or ([node_config["SubnetId"]] if node_config.get("SubnetId") else [])
+        return list(ids or self.provider_config.get("subnet_ids", []))
 
     def create_node(self, node_config, tags, count):
-        conf = dict(node_config)
+        self._workspace_defaults()
+        conf = {k: v for k, v in node_config.items()
+                if k not in ("SubnetIds", "SubnetId", "data_disks", "spot", "instance_type")}
         tags = dict(tags, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name})
         conf.setdefault("TagSpecifications", []).append(
-            {"ResourceType": "instance", "Tags": [{"Key": k, "Value": v} for k, v in tags.items()]})
+            {"ResourceType": "instance", "Tags": [{"Key": k, "Value": str(v)} for k, v in tags.items()]})
         conf["MinCount"] = conf["MaxCount"] = count
-        if "instance_type" in conf:
-            conf["InstanceType"] = conf.pop("instance_type")
-        try:
-            created = self.ec2.create_instances(**conf)
-        except Exception as e:  # noqa: BLE001 -- botocore ClientError
-            raise NodeLaunchException(getattr(e, "response", {}).get("Error", {}).get("Code", "Unknown"), str(e))
-        return {n.id: n for n in created}
-
-    def set_node_tags(self, node_id, tags):
-        self.client.create_tags(Resources=[node_id], Tags=[{"Key": k, "Value": v} for k, v in tags.items()])
-        self._cache.pop(node_id, None)
+        if "instance_type" in node_config:
+            conf["InstanceType"] = node_config["instance_type"]
+        kind = tags.get(T.CLOUDTIK_TAG_NODE_KIND, "worker")
+        profile = self.provider_config.get(f"{kind}_instance_profile")
+        if profile and "IamInstanceProfile" not in conf:
+            conf["IamInstanceProfile"] = {"Name": profile}
+        sgs = self.provider_config.get("security_group_ids")
+        if sgs and "SecurityGroupIds" not in conf:
+            conf["SecurityGroupIds"] = list(sgs)
+        if node_config.get("spot"):
+            conf["InstanceMarketOptions"] = {"MarketType": "spot", "SpotOptions": {
+                "SpotInstanceType": "one-time", "InstanceInterruptionBehavior": "terminate"}}
+        disks = node_config.get("data_disks") or []
+        if disks:
+            conf["BlockDeviceMappings"] = list(conf.get("BlockDeviceMappings", [])) + [
+                {"DeviceName": f"/dev/sd{chr(ord('f') + i)}",
+                 "Ebs": {"VolumeSize": int(d.get("size", 200) if isinstance(d, dict) else d), "VolumeType": "gp3",
+                         "DeleteOnTermination": True}} for i, d in enumerate(disks)]
+        subnets = self._subnets(node_config)
+        attempts = subnets if subnets else [None]
+        last = None
+        for i in range(len(attempts)):
+            subnet = attempts[(self._subnet_idx + i) % len(attempts)]
+            if subnet:
+                conf["SubnetId"] = subnet
+            try:
+                r = self.ec2.run_instances(**conf)
+            except Exception as e:  # noqa: BLE001 -- botocore ClientError
+                code = getattr(e, "response", {}).get("Error", {}).get("Code", type(e).__name__)
+                last = NodeLaunchException(code, str(e))
+                if any(c in code for c in self.CAPACITY_ERRORS) and i + 1 < len(attempts):
+                    continue                                   # next subnet / availability zone
+                raise last
+            self._subnet_idx = (self._subnet_idx + i + 1) % max(1, len(attempts))
+            out = {}
+            for inst in r.get("Instances", []):
+                inst.setdefault("Tags", [{"Key": k, "Value": str(v)} for k, v in tags.items()])
+                self._remember(inst)
+                out[inst["InstanceId"]] = inst
+            return out
+        raise last
 
     def terminate_node(self, node_id):
-        self.client.terminate_instances(InstanceIds=[node_id])
+        self.terminate_nodes([node_id])
 
     def terminate_nodes(self, node_ids: List[str]):
         if node_ids:
-            self.client.terminate_instances(InstanceIds=list(node_ids))
+            self.flush_tags()
+            self.ec2.terminate_instances(InstanceIds=list(node_ids))
+            for n in node_ids:
+                self._nodes.pop(n, None)
 
 
 # GCP and Azure speak the clouds' REST APIs directly (no SDK needed): rest_providers.py
