@@ -141,14 +141,16 @@ class ScalingWithTime(ScalingWithResources):
         self.table = self._expand(c.get("scaling_time_table", {}) or {})
 
     def _seconds(self, spec: str) -> int:
+        """``[day ]HH:MM[:SS]`` -> seconds into the period (day: Mon..Sun weekly, 1..31
+        monthly)."""
         parts = spec.strip().split()
         day = 0
         if self.periodic == "weekly" and len(parts) == 2:
             day = WEEKDAYS.index(parts[0][:3].lower())
         elif self.periodic == "monthly" and len(parts) == 2:
             day = int(parts[0]) - 1
-        hh, mm = (parts[-1].split(":") + ["0"])[:2]
-        return day * 86400 + int(hh) * 3600 + int(mm) * 60
+        hh, mm, ss = (parts[-1].split(":") + ["0", "0"])[:3]
+        return day * 86400 + int(hh) * 3600 + int(mm) * 60 + int(ss)
 
     def _period(self) -> int:
         return {"daily": 86400, "weekly": 7 * 86400, "monthly": 31 * 86400}[self.periodic]
@@ -157,22 +159,60 @@ class ScalingWithTime(ScalingWithResources):
         wt = self._wtype()
         return int(self.config["available_node_types"].get(wt, {}).get("min_workers", 0)) if wt else 0
 
+    @property
+    def min_workers(self) -> int:
+        return self._min_workers()
+
+    @property
+    def scaling_time_table(self) -> List:
+        return self.table
+
     def _expand(self, table: Dict[str, Any]) -> List:
+        """Absolute counts, ``+n`` / ``-n`` / ``*f`` relative to the base (min_workers, or the
+        previous entry -- cyclically, so a leading relative entry follows the period's last
+        one); 0 means min_workers."""
         entries = sorted((self._seconds(k), v) for k, v in table.items())
-        out, prev = [], self._min_workers()
-        for sec, spec in entries:
-            base = self._min_workers() if self.math_base == "on-min-workers" else prev
-            s = str(spec).strip()
-            if s.startswith(("+", "-")):
-                n = base + int(float(s))
-            elif s.startswith("*"):
-                n = int(math.ceil(base * float(s[1:])))
-            else:
-                n = int(float(s))
-            n = max(0, n)
-            out.append((sec, n))
-            prev = n
+        mw = self._min_workers()
+
+        def resolve(prev):
+            out = []
+            for sec, spec in entries:
+                base = mw if self.math_base == "on-min-workers" else prev
+                s = str(spec).strip()
+                if s.startswith(("+", "-")):
+                    n = base + int(float(s))
+                elif s.startswith("*"):
+                    n = int(math.ceil(base * float(s[1:])))
+                else:
+                    n = int(float(s)) or mw
+                n = max(0, n)
+                out.append((sec, n))
+                prev = n
+            return out
+        out = resolve(mw)
+        if out and self.math_base != "on-min-workers":
+            out = resolve(out[-1][1])                # the period wraps: start from its last value
         return out
+
+    def _get_nodes_request(self, seconds: int) -> Optional[int]:
+        """Workers wanted ``seconds`` into the period (the last entry before it, wrapping)."""
+        if not self.table:
+            return None
+        current = self.table[-1][1]
+        for sec, n in self.table:
+            if sec <= seconds:
+                current = n
+        return current
+
+    def _get_resource_requests_at_seconds(self, seconds: int) -> List[Dict[str, float]]:
+        """The whole cluster's resource request at that point: the head plus the workers."""
+        n = self._get_nodes_request(seconds)
+        wt = self._wtype()
+        if n is None or wt is None:
+            return []
+        head = self.config.get("head_node_type")
+        reqs = [_node_bundle(self.config, head)] if head else []
+        return reqs + [_node_bundle(self.config, wt) for _ in range(n)]
 
     def nodes_at(self, t: Optional[float] = None) -> Optional[int]:
         if not self.table:
@@ -185,11 +225,7 @@ class ScalingWithTime(ScalingWithResources):
         else:
             now = 0
         now += lt.tm_hour * 3600 + lt.tm_min * 60 + lt.tm_sec
-        current = self.table[-1][1]                 # wraps from the previous period
-        for sec, n in self.table:
-            if sec <= now:
-                current = n
-        return current
+        return self._get_nodes_request(now)
 
     def requests(self, metrics) -> List[Dict[str, float]]:
         n = self.nodes_at()

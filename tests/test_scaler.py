@@ -208,7 +208,7 @@ def test_scaling_with_time_table():
                                  "scaling_time_table": {"08:00": "+3", "12:00": "*2", "20:00": 1}}
     p = ScalingWithTime(cfg, "h")
     t = time.mktime(time.strptime("2026-01-05 13:00", "%Y-%m-%d %H:%M"))
-    assert p.nodes_at(t) == 10                       # 2 + 3 = 5 at 08:00, *2 at 12:00
+    assert p.nodes_at(t) == 8                        # 1 (yesterday's 20:00) + 3 at 08:00, *2 at 12:00
     t = time.mktime(time.strptime("2026-01-05 07:00", "%Y-%m-%d %H:%M"))
     assert p.nodes_at(t) == 1                        # wraps from the previous day's 20:00 entry
 
