@@ -71,7 +71,32 @@ def include_runtime_for_selector(selector: Dict[str, Any], runtime: str) -> Dict
     return selector
 
 
+LABEL_CLUSTER, LABEL_RUNTIME, LABEL_SERVICE = "cloudtik-cluster", "cloudtik-runtime", "cloudtik-service"
+
+
+def service_tags(service: Dict[str, Any]) -> set:
+    """Implicit tags of a service record: ``cloudtik-c-<cluster>``, ``cloudtik-r-<runtime>``,
+    ``cloudtik-f-<feature>`` (the tags Consul registrations carry) plus explicit ``tags``."""
+    out = set(service.get("tags") or [])
+    if service.get("cluster"):
+        out.add(f"cloudtik-c-{service['cluster']}")
+    if service.get("service_type"):
+        out.add(f"cloudtik-r-{service['service_type']}")
+    out.update(f"cloudtik-f-{f}" for f in service.get("features") or [])
+    return out
+
+
+def service_labels(service: Dict[str, Any]) -> Dict[str, str]:
+    labels = {LABEL_CLUSTER: service.get("cluster"), LABEL_RUNTIME: service.get("service_type"),
+              LABEL_SERVICE: service.get("name")}
+    labels.update(service.get("labels") or {})
+    return {k: v for k, v in labels.items() if v is not None}
+
+
 def match_service(service: Dict[str, Any], selector: Optional[Dict[str, Any]]) -> bool:
+    """Selector keys (reference service_discovery/utils.py SERVICE_SELECTOR_*): services,
+    service_types / runtimes, clusters (+ exclude_* of each), tags (all required), features
+    (any), labels (all equal), exclude_labels (none equal)."""
     if not selector:
         return True
     for key, field in (("services", "name"), ("service_types", "service_type"),
@@ -79,12 +104,22 @@ def match_service(service: Dict[str, Any], selector: Optional[Dict[str, Any]]) -
         want = selector.get(key)
         if want and service.get(field) not in want:
             return False
-    ex = selector.get("exclude_clusters")
-    if ex and service.get("cluster") in ex:
-        return False
+        ex = selector.get(f"exclude_{key}")
+        if ex and service.get(field) in ex:
+            return False
     feats = selector.get("features")
     if feats and not set(feats) & set(service.get("features", [])):
         return False
+    tags = selector.get("tags")
+    if tags and not set(tags) <= service_tags(service):
+        return False
+    labels = service_labels(service)
+    for k, v in (selector.get("labels") or {}).items():
+        if labels.get(k) != v:
+            return False
+    for k, v in (selector.get("exclude_labels") or {}).items():
+        if labels.get(k) == v:
+            return False
     return True
 
 

@@ -154,7 +154,9 @@ DEFINITIONS = {
     "service_selector": {"type": "object", "properties": {
         "runtimes": {"type": "array", "items": {"type": "string"}}, "services": {"type": "array"},
         "tags": {"type": "array"}, "labels": {"type": "object"}, "exclude_runtimes": {"type": "array"},
-        "exclude_labels": {"type": "object"}, "clusters": {"type": "array"}, "exclude_clusters": {"type": "array"}},
+        "exclude_labels": {"type": "object"}, "clusters": {"type": "array"}, "exclude_clusters": {"type": "array"},
+        "exclude_services": {"type": "array"}, "service_types": {"type": "array"},             # +
+        "exclude_service_types": {"type": "array"}, "features": {"type": "array"}},            # +
         "additionalProperties": False},
     "database_connect": {"type": "object", "properties": {
         "engine": {"enum": ["mysql", "postgres"]}, "address": {"type": "string"}, "port": T["port"],

@@ -146,3 +146,30 @@ def test_workspace_global_variables_through_the_provider(tmp_path, monkeypatch):
     cfg = {"provider": {"type": "local"}, "workspace_name": "w", "cluster_name": "c1"}
     get_workspace_provider(cfg["provider"], "w").publish_global_variables(cfg, {"service.c1.x": "{}"})
     assert "service.c1.x" in D._workspace_global_variables(cfg)
+
+
+def test_service_selectors_tags_labels_and_exclusions():
+    """Selector semantics of the workspace registry (reference
+    tests/unit/runtime/test_service_discovery.py scenarios, over this registry's records)."""
+    from cloudtik_amd.core import service_discovery as sd
+    gv = {}
+    for cluster, rt, name, host in (("cluster-1", "runtime-1", "runtime-1", "127.0.0.1"),
+                                    ("cluster-1", "runtime-2", "runtime-2", "127.0.0.2"),
+                                    ("cluster-2", "runtime-1", "service-1", "127.0.0.3"),
+                                    ("cluster-2", "runtime-3", "service-1", "127.0.0.4")):
+        rec = {"name": name, "service_type": rt, "cluster": cluster, "port": 80}
+        gv[sd.service_global_key(cluster, f"{rt}-{name}")] = sd.encode_service_address(rec, host)
+
+    def hosts(sel):
+        return sorted(s["host"] for s in sd.discover_services(gv, sel))
+
+    assert hosts({"clusters": ["cluster-1"], "runtimes": ["runtime-1"]}) == ["127.0.0.1"]
+    assert hosts({"clusters": ["cluster-2"], "runtimes": ["runtime-1"], "services": ["service-1"]}) == ["127.0.0.3"]
+    assert hosts({"clusters": ["cluster-1"]}) == ["127.0.0.1", "127.0.0.2"]
+    assert hosts({"tags": ["cloudtik-c-cluster-2"]}) == ["127.0.0.3", "127.0.0.4"]
+    assert hosts({"labels": {"cloudtik-runtime": "runtime-1"}}) == ["127.0.0.1", "127.0.0.3"]
+    assert hosts({"exclude_labels": {"cloudtik-runtime": "runtime-1"}}) == ["127.0.0.2", "127.0.0.4"]
+    assert hosts({"exclude_runtimes": ["runtime-1", "runtime-2"]}) == ["127.0.0.4"]
+    assert hosts({"clusters": ["cluster-2"], "runtimes": ["runtime-3"], "services": ["service-1"],
+                  "tags": ["cloudtik-c-cluster-2"], "labels": {"cloudtik-runtime": "runtime-3"},
+                  "exclude_labels": {"cloudtik-runtime": "runtime-1"}}) == ["127.0.0.4"]
