@@ -65,6 +65,7 @@ __device__ __forceinline__ void bn_thread(const BnLayout& L, int& cv, int& rl) {
 }
 
 // per-block (mean, M2) over rows [b*R, (b+1)*R), 4 rows in flight per thread
+template <int U>
 __global__ __launch_bounds__(BN_RT) void bn_stats_kernel(const bf16_t* __restrict__ x, BnLayout L,
                                                          float* __restrict__ pmean,
                                                          float* __restrict__ pm2) {
@@ -79,12 +80,12 @@ __global__ __launch_bounds__(BN_RT) void bn_stats_kernel(const bf16_t* __restric
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
   if (rl < L.RPI) {
     int r = r0 + rl;
-    for (; r + 3 * L.RPI < r1; r += 4 * L.RPI) {
-      u16x8 v[4];
+    for (; r + (U - 1) * L.RPI < r1; r += U * L.RPI) {
+      u16x8 v[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const u16x8*>(x + (size_t)(r + u * L.RPI) * L.C)[cv];
+      for (int u = 0; u < U; ++u) v[u] = reinterpret_cast<const u16x8*>(x + (size_t)(r + u * L.RPI) * L.C)[cv];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) { const float f = bf2f(v[u][j]); s[j] += f; q[j] += f * f; }
     }
@@ -259,6 +260,7 @@ __device__ __forceinline__ void bn_mask8(const BnMask& mk, const u16x8& yv, cons
 }
 
 // per-block sums of dy' and dy'*xhat (dy' = masked dy), 4 rows in flight per thread
+template <int U>
 __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, BnMask mk, const bf16_t* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, BnLayout L, float* __restrict__ p1, float* __restrict__ p2) {
@@ -277,18 +279,18 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
   bn_mask_coef(mk, cv, fa, fb);
   if (rl < L.RPI) {
     int r = r0 + rl;
-    for (; r + 3 * L.RPI < r1; r += 4 * L.RPI) {
-      u16x8 g[4], xv[4], yv[4];
-      size_t o[4];
+    for (; r + (U - 1) * L.RPI < r1; r += U * L.RPI) {
+      u16x8 g[U], xv[U], yv[U];
+      size_t o[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         o[u] = (size_t)(r + u * L.RPI) * L.CV + cv;
         g[u] = reinterpret_cast<const u16x8*>(dy)[o[u]];
         xv[u] = reinterpret_cast<const u16x8*>(x)[o[u]];
         yv[u] = mk.mode == 1 ? reinterpret_cast<const u16x8*>(mk.y)[o[u]] : u16x8(0);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         bool on[8];
         bn_mask8(mk, yv[u], xv[u], fa, fb, on);
 #pragma unroll
@@ -543,6 +545,15 @@ static int bn_ew() {
     else KERNEL<1><<<ew_grid(GRIDWORK, 1), 256, 0, stream>>>(__VA_ARGS__);                   \
   } while (0)
 
+// rows in flight per thread in the reductions (CLOUDTIK_AMD_BN_UNROLL: 4 or 8)
+static int bn_unroll() {
+  static int n = [] {
+    const char* e = getenv("CLOUDTIK_AMD_BN_UNROLL");
+    return (e && atoi(e) >= 8) ? 8 : 4;
+  }();
+  return n;
+}
+
 // partial-block count of the reductions (CLOUDTIK_AMD_BN_BLOCKS, <= 2048; default 512)
 static int bn_target_blocks() {
   static int n = [] {
@@ -561,7 +572,8 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
   if (C % 8 || C / 8 > BN_RT || M <= 0) return -1;
   BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
-  bn_stats_kernel<<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
+  if (bn_unroll() == 8) bn_stats_kernel<8><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
+  else bn_stats_kernel<4><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
   bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)2048 * C, nblk, L,
                                                            (const bf16_t*)gamma, (const bf16_t*)beta,
                                                            eps, momentum, run_mean, run_var, stat,
@@ -581,7 +593,8 @@ extern "C" int ct_bn_fwd_train_pool(const void* x, const void* gamma, const void
   if (C % 8 || C / 8 > BN_RT || M <= 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
   BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
-  bn_stats_kernel<<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
+  if (bn_unroll() == 8) bn_stats_kernel<8><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
+  else bn_stats_kernel<4><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)x, L, part, part + (size_t)2048 * C);
   bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)2048 * C, nblk, L,
                                                            (const bf16_t*)gamma, (const bf16_t*)beta,
                                                            eps, momentum, run_mean, run_var, stat,
@@ -621,8 +634,12 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
   BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
   const BnMask mk{relu_mode, (const bf16_t*)y, stat + 2 * C, stat + 3 * C};
-  bn_bwd_reduce_kernel<<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
-                                                 part, part + (size_t)2048 * C);
+  if (bn_unroll() == 8)
+    bn_bwd_reduce_kernel<8><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
+                                                        part, part + (size_t)2048 * C);
+  else
+    bn_bwd_reduce_kernel<4><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
+                                                        part, part + (size_t)2048 * C);
   const int acc = (param_flags >> 1) & 1;   // bit 1: accumulate into dgamma / dbeta
   if (param_flags & 1)
     bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
