@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from cloudtik_amd import ops
+from cloudtik_amd.ops.conv1x1 import conv1x1
 
 
 class BatchNormAct(nn.Module):
@@ -92,10 +93,12 @@ class Bottleneck(nn.Module):
             self.down_bn = BatchNormAct(cout, relu=False, **kw)
 
     def forward(self, x):
-        idt = self.down_bn(self.down(x)) if self.down is not None else x
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=idt)
+        # 1x1 convs as NHWC GEMMs on GPU; conv1 hands out an alias of x for the residual /
+        # downsample branch so its dgrad GEMM absorbs that branch's gradient (ops/conv1x1.py)
+        out, x = conv1x1(x, self.conv1, keep_input=True)
+        idt = self.down_bn(conv1x1(x, self.down)) if self.down is not None else x
+        out = self.bn2(self.conv2(self.bn1(out)))
+        return self.bn3(conv1x1(out, self.conv3), residual=idt)
 
 
 class ResNet(nn.Module):

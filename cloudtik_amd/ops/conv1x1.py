@@ -1,0 +1,106 @@
+"""Stride-1 1x1 convolutions over NHWC activations as plain GEMMs, with the residual-gradient
+sum folded into the data-gradient GEMM.
+
+In channels_last a 1x1 stride-1 convolution is a GEMM over the ``[N*H*W, C]`` rows of the
+activation: ``Y = X W^T``, ``dX = dY W``, ``dW = dY^T X``.  Measured on MI355X over every
+1x1 shape of ResNet-50 at batch 256 (``bench/conv1x1_gemm_probe.py``,
+``profiles/r2/conv1x1_gemm.md``):
+
+* dgrad: hipBLASLt beats MIOpen's implicit-GEMM kernels once the output has >= 128 channels
+  (28x28 512->128: 0.085 vs 0.162 ms); MIOpen stays ahead for 64-channel outputs;
+* fwd: hipBLASLt is ahead for >= 1024 input channels, MIOpen's CK kernels below;
+* wgrad: the reduction runs over N*H*W (up to 802816) rows into a small output; MIOpen is
+  ahead at every shape (hipBLASLt's split-K path included), so it stays on MIOpen.
+
+``keep_input=True`` also returns an alias of ``x`` for the block's other consumer (the
+residual / downsample branch).  Autograd then sees ``x`` used once, and the backward adds the
+alias gradient into the data-gradient GEMM's output (hipBLASLt beta=1 on the freshly produced
+residual gradient) instead of autograd summing the two branch gradients with a separate
+elementwise kernel (16 such adds per ResNet-50 step).
+
+Parity: the reference trains torchvision's ``resnet50`` (nn.Conv2d everywhere;
+applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296); the
+module structure and state dict here are unchanged -- only the kernels differ.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+_ENABLED = os.environ.get("CLOUDTIK_AMD_CONV1X1_GEMM", "1") == "1"
+DGRAD_GEMM_MIN_CIN = 128
+FWD_GEMM_MIN_CIN = 1024
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> the [N*H*W, C] row view (a copy only if not NHWC-dense)."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _nchw(rows: torch.Tensor, N: int, H: int, W: int) -> torch.Tensor:
+    return rows.view(N, H, W, rows.shape[1]).permute(0, 3, 1, 2)
+
+
+def _conv_bwd(dy, x, w, mask):
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, mask)
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, keep_input):
+        ctx.save_for_backward(x, w)
+        ctx.keep = keep_input
+        N, C, H, W = x.shape
+        co = w.shape[0]
+        if C >= FWD_GEMM_MIN_CIN:
+            y = _nchw(torch.mm(_rows(x), w.reshape(co, C).t()), N, H, W)
+        else:
+            y = F.conv2d(x, w)
+        if keep_input:
+            return y, x.view_as(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, dx_other=None):
+        x, w = ctx.saved_tensors
+        N, C, H, W = x.shape
+        co = w.shape[0]
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dy2 = _rows(dy)
+            w2 = w.reshape(co, C)
+            if dx_other is not None and not torch.is_grad_enabled() and dx_other.dtype == dy.dtype \
+                    and dx_other.is_contiguous(memory_format=torch.channels_last):
+                # the other branch's gradient is a fresh tensor owned by this backward:
+                # accumulate the dgrad GEMM into it (beta = 1) -- no separate add kernel
+                dx = dx_other
+                _rows(dx).addmm_(dy2, w2)
+            else:
+                if C >= DGRAD_GEMM_MIN_CIN:
+                    dx = _nchw(torch.mm(dy2, w2), N, H, W)
+                else:
+                    dx = _conv_bwd(dy, x, w, [True, False, False])[0]
+                if dx_other is not None:
+                    dx = dx + dx_other
+        if ctx.needs_input_grad[1]:
+            dw = _conv_bwd(dy, x, w, [False, True, False])[1]
+        return dx, dw, None
+
+
+def conv1x1_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    return (_ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16
+            and conv.weight.dtype == x.dtype and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def conv1x1(x: torch.Tensor, conv: torch.nn.Conv2d, keep_input: bool = False):
+    """``conv(x)`` for a stride-1 1x1 bias-free conv over channels_last bf16 on GPU (GEMM
+    paths above); with ``keep_input`` returns ``(conv(x), x_alias)`` where ``x_alias`` must be
+    used in place of ``x`` by every other consumer.  Anything else falls back to ``conv(x)``."""
+    if not conv1x1_eligible(x, conv):
+        return (conv(x), x) if keep_input else conv(x)
+    return _Conv1x1Fn.apply(x, conv.weight, keep_input)

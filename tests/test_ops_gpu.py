@@ -289,6 +289,35 @@ def test_deferred_conv_grads_match_preset(cuda):
     assert torch.allclose(w0, w1, rtol=1e-2, atol=1e-3)
 
 
+def test_conv1x1_gemm_bottleneck(cuda, monkeypatch):
+    """ResNet bottlenecks with the 1x1 convs as NHWC GEMMs and the residual / downsample
+    gradient folded into conv1's dgrad GEMM (ops/conv1x1.py) match the stock MIOpen convs:
+    output, input gradient and every parameter gradient, for a stage-1-like block (64-channel
+    input: MIOpen dgrad) and a wide block (GEMM fwd + dgrad)."""
+    from cloudtik_amd.models.resnet import Bottleneck
+    from cloudtik_amd.ops import conv1x1 as C1
+
+    def run(enabled, cin, width, down, H):
+        monkeypatch.setattr(C1, "_ENABLED", enabled)
+        torch.manual_seed(0)
+        b = Bottleneck(cin, width, downsample=down, device=cuda, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            for m in b.modules():
+                if type(m).__name__ == "BatchNormAct":
+                    m.weight.fill_(0.7)             # bn3's zero-init would hide the main branch
+        x = torch.randn(8, cin, H, H, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+        x.requires_grad_()
+        y = b(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+        return [y.float(), x.grad.float()] + [p.grad.float() for p in b.parameters()]
+
+    for cin, width, down, H in ((64, 64, True, 14), (1024, 256, False, 7), (256, 128, True, 14)):
+        ref, got = run(False, cin, width, down, H), run(True, cin, width, down, H)
+        for a, b_ in zip(ref, got):
+            assert _rel(b_, a) < 2e-2, (cin, width, down)
+
+
 def test_linear_fused_wgrad(cuda):
     from cloudtik_amd.train.optim import FlatParamSpace
     torch.manual_seed(0)
