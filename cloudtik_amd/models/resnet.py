@@ -20,7 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from cloudtik_amd import ops
-from cloudtik_amd.ops.conv1x1 import conv1x1
+from cloudtik_amd.ops.conv1x1 import conv1x1, conv3x3
 
 
 class BatchNormAct(nn.Module):
@@ -68,7 +68,7 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = self.down_bn(self.down(x)) if self.down is not None else x
-        return self.bn2(self.conv2(self.bn1(self.conv1(x))), residual=idt)
+        return self.bn2(conv3x3(self.bn1(conv3x3(x, self.conv1)), self.conv2), residual=idt)
 
 
 class Bottleneck(nn.Module):
@@ -97,7 +97,7 @@ class Bottleneck(nn.Module):
         # downsample branch so its dgrad GEMM absorbs that branch's gradient (ops/conv1x1.py)
         out, x = conv1x1(x, self.conv1, keep_input=True)
         idt = self.down_bn(conv1x1(x, self.down)) if self.down is not None else x
-        out = self.bn2(self.conv2(self.bn1(out)))
+        out = self.bn2(conv3x3(self.bn1(out), self.conv2))
         return self.bn3(conv1x1(out, self.conv3), residual=idt)
 
 

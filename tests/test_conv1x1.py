@@ -81,3 +81,18 @@ def test_bottleneck_uses_alias_and_matches_plain_convs():
     ref = b.bn3(b.conv3(b.bn2(b.conv2(b.bn1(b.conv1(x))))), residual=b.down_bn(b.down(x)))
     torch.testing.assert_close(b(x), ref)
     assert not C1.conv1x1_eligible(x, b.conv1)        # CPU / fp32: stock conv
+
+
+def test_conv3x3_dgrad_as_forward_conv():
+    """3x3 stride-1 dgrad issued as conv2d(dY, flip(W)^T, pad 1) equals autograd's."""
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 6, 7, 7, generator=g).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(5, 6, 3, 3, generator=g).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(2, 5, 7, 7, generator=g)
+    x1, w1 = x.clone().requires_grad_(), w.clone().requires_grad_()
+    torch.nn.functional.conv2d(x1, w1, padding=1).backward(dy)
+    x2, w2 = x.clone().requires_grad_(), w.clone().requires_grad_()
+    y = C1._Conv3x3Fn.apply(x2, w2)
+    y.backward(dy)
+    torch.testing.assert_close(x2.grad, x1.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(w2.grad, w1.grad, rtol=1e-5, atol=1e-5)
