@@ -37,6 +37,10 @@ import torch.nn.functional as F
 
 _ENABLED = os.environ.get("CLOUDTIK_AMD_CONV1X1_GEMM", "1") == "1"
 _DGRAD_AS_FWD = os.environ.get("CLOUDTIK_AMD_CONV3X3_DGRAD_FWD", "1") == "1"
+# conv weight gradients on the gradient side stream (ops.linear.grad_stream), accumulated
+# straight into the flat gradient buffer: MIOpen's wgrad kernels (and their zero-fill / cast
+# helpers) overlap the bandwidth-bound BatchNorm backward and dgrad chain on the main stream
+_SIDE_WGRAD = os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_STREAM", "1") == "1"
 DGRAD_GEMM_MIN_CIN = 128
 FWD_GEMM_MIN_CIN = 1024
 
@@ -50,15 +54,46 @@ def _nchw(rows: torch.Tensor, N: int, H: int, W: int) -> torch.Tensor:
     return rows.view(N, H, W, rows.shape[1]).permute(0, 3, 1, 2)
 
 
-def _conv_bwd(dy, x, w, mask):
-    return torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, mask)
+def _conv_bwd(dy, x, w, mask, pad=0):
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1, mask)
+
+
+def _flat_target(wp):
+    """The flat-buffer gradient slice of parameter ``wp`` (train.optim.FlatParamSpace), if any."""
+    v = getattr(wp, "_ct_flat_view", None)        # deferred conv grads: .grad stays unset
+    if v is not None:
+        return v
+    if getattr(wp, "_ct_flat_grad", False) and wp.grad is not None:
+        return wp.grad
+    return None
+
+
+def _weight_grad(wp, dy, x, w, pad):
+    """MIOpen dW.  When the weight lives in a flat gradient buffer and the gradient side
+    stream is on, it is computed there and added into the buffer (returns None: autograd
+    never sees it, so the data-parallel bucketer is told via ``_ct_grad_ready``); otherwise
+    it is returned for AccumulateGrad."""
+    from cloudtik_amd.ops.linear import grad_stream
+    target = _flat_target(wp) if _SIDE_WGRAD else None
+    side = grad_stream() if target is not None else None
+    if side is None:
+        return _conv_bwd(dy, x, w, [False, True, False], pad)[1]
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        target.add_(_conv_bwd(dy, x, w, [False, True, False], pad)[1])
+    dy.record_stream(side)
+    x.record_stream(side)
+    cb = getattr(wp, "_ct_grad_ready", None)
+    if cb is not None:
+        cb(wp)
+    return None
 
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, keep_input):
         ctx.save_for_backward(x, w)
-        ctx.keep = keep_input
+        ctx.wp = w
         N, C, H, W = x.shape
         co = w.shape[0]
         if C >= FWD_GEMM_MIN_CIN:
@@ -93,7 +128,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 if dx_other is not None:
                     dx = dx + dx_other
         if ctx.needs_input_grad[1]:
-            dw = _conv_bwd(dy, x, w, [False, True, False])[1]
+            dw = _weight_grad(ctx.wp, dy, x, w, 0)
         return dx, dw, None
 
 
@@ -117,6 +152,7 @@ class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         ctx.save_for_backward(x, w)
+        ctx.wp = w
         return F.conv2d(x, w, padding=1)
 
     @staticmethod
@@ -128,8 +164,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
             dx = F.conv2d(dy, wt, padding=1)
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1]
+            dw = _weight_grad(ctx.wp, dy, x, w, 1)
         return dx, dw
 
 

@@ -162,6 +162,9 @@ class Trainer:
     def _clip(self):
         if self.space is not None:
             self.space.flush_grads()               # deferred conv-weight grads -> flat buffer
+            if self.space.grad.is_cuda:
+                from cloudtik_amd.ops.linear import sync_grad_stream
+                sync_grad_stream()                 # weight grads written on the side stream
         g = self.space.shard_grad if self.space is not None else None
         if g is None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.clip_norm)
