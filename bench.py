@@ -70,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--no-dropout", action="store_true")
     ap.add_argument("--conv-benchmark", action="store_true",
                     help="ResNet: let MIOpen search convolution solvers (torch.backends.cudnn.benchmark)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="auto: RCCL on GPU, gloo on CPU; gloo on GPU lets several ranks share "
+                         "one GPU (plumbing check of the GPU data-parallel path without RCCL)")
     ap.add_argument("--tunableop", default="use", choices=["off", "use", "tune"],
                     help="hipBLASLt solution selection via PyTorch TunableOp (results shipped in-tree)")
     return ap.parse_args(argv)
@@ -383,8 +386,8 @@ def main():
     import torch
     import torch.distributed as dist
     from cloudtik_amd.parallel import init_distributed
-    backend = "gloo" if args.device == "cpu" else None
-    rank, world, local, device = init_distributed(backend=backend)
+    backend = "gloo" if args.device == "cpu" else (None if args.dist_backend == "auto" else args.dist_backend)
+    rank, world, local, device = init_distributed(backend=backend, gpu=args.device == "cuda")
     if args.device == "cpu":
         device = torch.device("cpu")
     if world != args.gpus and rank == 0:

@@ -48,12 +48,18 @@ def env_local_world() -> int:
     return 1
 
 
-def init_distributed(backend: str = None, timeout_s: int = 1800):
+def init_distributed(backend: str = None, timeout_s: int = 1800, gpu: bool = None):
     """Initialise the default process group if WORLD_SIZE > 1 and bind this rank's GPU.
+
+    ``gpu`` (default: a GPU is present and the backend is not gloo) binds a GPU even under
+    gloo -- ranks that share one GPU exercise the GPU data-parallel path (bucketer, gradient
+    side stream, ZeRO-1) with gloo moving the CUDA tensors instead of RCCL.
 
     Returns (rank, world, local_rank, device)."""
     rank, world, local = env_rank_info()
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if gpu is None:
+        gpu = backend != "gloo"
+    use_gpu = torch.cuda.is_available() and gpu
     if use_gpu:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         device = torch.device("cuda", torch.cuda.current_device())

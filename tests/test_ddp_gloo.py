@@ -20,14 +20,23 @@ def _port():
 
 
 class Net(torch.nn.Module):
-    def __init__(self):
+    """``native``: the hidden layers go through ops.linear (weight gradient accumulated into the
+    flat buffer on the gradient side stream, readiness reported via _ct_grad_ready) -- the
+    path BERT's layers take on the GPU."""
+
+    def __init__(self, native=False):
         super().__init__()
+        self.native = native
         self.fc1 = torch.nn.Linear(16, 32)
         self.fc2 = torch.nn.Linear(32, 32)
         self.unused = torch.nn.Linear(8, 8)     # never receives a gradient
         self.head = torch.nn.Linear(32, 4)
 
     def forward(self, x):
+        if self.native:
+            from cloudtik_amd.ops.linear import linear
+            h = torch.relu(linear(x, self.fc1.weight, self.fc1.bias))
+            return self.head(torch.relu(linear(h, self.fc2.weight, self.fc2.bias)))
         return self.head(torch.relu(self.fc2(torch.relu(self.fc1(x)))))
 
 
@@ -39,21 +48,23 @@ def _data():
     return torch.randn(GLOBAL_B, 16, generator=g), torch.randint(0, 4, (GLOBAL_B,), generator=g)
 
 
-def _make(dtype):
+def _make(dtype, device="cpu"):
     torch.manual_seed(0)
-    return Net().to(dtype)
+    return Net(native=device == "cuda").to(dtype).to(device)
 
 
-def _worker(rank, world, port, accum, fp32_reduce, out):
+def _worker(rank, world, port, accum, fp32_reduce, out, device="cpu"):
     import torch.distributed as dist
     from contextlib import nullcontext
     from cloudtik_amd.parallel import GradBucketer, broadcast_flat_params
     from cloudtik_amd.train.optim import FlatParamSpace, FusedSGD
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if device == "cuda":
+        torch.cuda.set_device(0)             # every rank shares GPU 0; gloo moves the tensors
     try:
         dtype = torch.bfloat16 if fp32_reduce else torch.float32
-        model = _make(dtype)
+        model = _make(dtype, device)
         if rank:                                 # rank-local init differs: the broadcast must fix it
             with torch.no_grad():
                 for p in model.parameters():
@@ -66,7 +77,7 @@ def _worker(rank, world, port, accum, fp32_reduce, out):
         opt.grad_scale = ddp.grad_scale / accum
         X, Y = _data()
         n = GLOBAL_B // world
-        xs, ys = X[rank * n:(rank + 1) * n].to(dtype), Y[rank * n:(rank + 1) * n]
+        xs, ys = X[rank * n:(rank + 1) * n].to(dtype).to(device), Y[rank * n:(rank + 1) * n].to(device)
         m = n // accum
         for i in range(accum):
             ctx = ddp.no_sync() if i < accum - 1 else nullcontext()
@@ -75,9 +86,9 @@ def _worker(rank, world, port, accum, fp32_reduce, out):
                 loss.backward()
         ddp.finish()
         g = space.reduced_grad.float() * opt.grad_scale
-        grads = {nm: g[o:o + k].clone() for nm, o, k in zip(space.names, space.offsets, space.numels)}
+        grads = {nm: g[o:o + k].cpu().clone() for nm, o, k in zip(space.names, space.offsets, space.numels)}
         opt.step()
-        params = {nm: p.detach().float().reshape(-1).clone() for nm, p in named}
+        params = {nm: p.detach().float().reshape(-1).cpu().clone() for nm, p in named}
         out[rank] = (grads, params, len(ddp.buckets))
     finally:
         dist.destroy_process_group()
@@ -96,18 +107,20 @@ def _reference():
 
 @pytest.mark.parametrize("world,accum,fp32_reduce", [(2, 1, False), (2, 2, False), (4, 2, False), (2, 2, True),
                                                      (4, 1, True)])
-def test_gradbucketer_matches_full_batch(world, accum, fp32_reduce):
+def test_gradbucketer_matches_full_batch(world, accum, fp32_reduce, device="cpu"):
     port = _port()
     ctx = mp.get_context("spawn")
     with ctx.Manager() as mgr:
         out = mgr.dict()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, accum, fp32_reduce, out)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, accum, fp32_reduce, out, device))
+                 for r in range(world)]
         [p.start() for p in procs]
         [p.join(180) for p in procs]
         assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         res = dict(out)
     ref_g, ref_p = _reference()
-    tol = dict(rtol=3e-2, atol=3e-3) if fp32_reduce else dict(rtol=1e-5, atol=1e-6)
+    tol = dict(rtol=3e-2, atol=3e-3) if fp32_reduce else (dict(rtol=1e-5, atol=1e-6) if device == "cpu"
+                                                          else dict(rtol=1e-4, atol=1e-5))
     for r in range(world):
         grads, params, nb = res[r]
         assert nb > 2
@@ -117,3 +130,11 @@ def test_gradbucketer_matches_full_batch(world, accum, fp32_reduce):
         assert torch.count_nonzero(grads["unused.weight"]) == 0
     for n in ref_g:                              # bit-identical across ranks
         assert torch.equal(res[0][1][n], res[world - 1][1][n])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("accum,fp32_reduce", [(1, False), (2, False), (2, True)])
+def test_gradbucketer_matches_full_batch_gpu(accum, fp32_reduce):
+    """The GPU data-parallel path: two ranks on GPU 0, ops.linear weight gradients from the
+    side stream into the flat buffer, bucket launches from the readiness callbacks."""
+    test_gradbucketer_matches_full_batch(2, accum, fp32_reduce, device="cuda")
