@@ -87,7 +87,7 @@ def _use_native(*tensors) -> bool:
 
 # --------------------------------------------------------------------------- RNG streams
 class _DropoutRNG(threading.local):
-    """(seed, offset) pairs for the counter-based Philox dropout kernels.
+    """(seed, offset) pairs for the counter-based (hash) dropout kernels.
 
     Each dropout site draws a fresh 64-bit offset; the kernels regenerate the mask in
     backward from the same pair, so no mask is ever stored."""

@@ -2,8 +2,8 @@
 
 Used (a) as the CPU execution path and (b) as the fp32 oracle in the GPU numerics
 tests.  The dropout masks are bit-identical to the kernels': both evaluate the same
-counter-based Philox-4x32-7 stream (``common.h: dropout_bits8``), so a CPU run and a GPU
-run of the same model with the same seed drop the same elements.
+counter-based hash stream (``common.h: dropout_bits8``), so a CPU run and a GPU run of the
+same model with the same seed drop the same elements.
 """
 from __future__ import annotations
 
@@ -17,16 +17,22 @@ M32 = np.uint64(0xFFFFFFFF)
 ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
 
 
-def _philox4x32_7(c0, c1, c2, c3, k0, k1):
-    for _ in range(7):
-        p0 = np.uint64(0xD2511F53) * c0
-        p1 = np.uint64(0xCD9E8D57) * c2
-        hi0, lo0 = p0 >> np.uint64(32), p0 & M32
-        hi1, lo1 = p1 >> np.uint64(32), p1 & M32
-        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0), lo1, (hi0 ^ c3 ^ k1), lo0
-        k0 = (k0 + np.uint64(0x9E3779B9)) & M32
-        k1 = (k1 + np.uint64(0xBB67AE85)) & M32
-    return c0, c1, c2, c3
+def _mix32(x):
+    """common.h mix32 on uint64 arrays holding uint32 values."""
+    x = x ^ (x >> np.uint64(16))
+    x = (x * np.uint64(0x7FEB352D)) & M32
+    x = x ^ (x >> np.uint64(15))
+    x = (x * np.uint64(0x846CA68B)) & M32
+    return x ^ (x >> np.uint64(16))
+
+
+def _dropout_key(seed: int, offset: int) -> int:
+    def m(x):
+        return int(_mix32(np.array([x & 0xFFFFFFFF], dtype=np.uint64))[0])
+    k = m(((offset >> 32) + 0x632BE5AB) & 0xFFFFFFFF)
+    k = m(k ^ (offset & 0xFFFFFFFF))
+    k = m(k ^ ((seed >> 32) & 0xFFFFFFFF))
+    return m(k ^ (seed & 0xFFFFFFFF))
 
 
 def dropout_threshold(p: float) -> int:
@@ -35,23 +41,19 @@ def dropout_threshold(p: float) -> int:
 
 
 def dropout_keep_mask(n: int, p: float, seed: int, offset: int) -> torch.Tensor:
-    """Boolean keep-mask of ``n`` elements (n % 8 == 0), identical to the HIP kernels."""
+    """Boolean keep-mask of ``n`` elements (n % 8 == 0), identical to the HIP kernels
+    (common.h dropout_bits8: one 16-bit uniform per element from a hash of the pair counter)."""
     assert n % 8 == 0
+    seed &= 0xFFFFFFFFFFFFFFFF
+    offset &= 0xFFFFFFFFFFFFFFFF
     v = np.arange(n // 8, dtype=np.uint64)
-    seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
-    offset = np.uint64(offset & 0xFFFFFFFFFFFFFFFF)
-    k0 = np.full_like(v, seed & M32)
-    k1 = np.full_like(v, seed >> np.uint64(32))
-    c2 = np.full_like(v, offset & M32)
-    c3 = np.full_like(v, offset >> np.uint64(32))
-    c1 = (v >> np.uint64(31)) & M32
-    thr = np.uint64(dropout_threshold(p))
+    key = np.uint64(_dropout_key(seed, offset)) ^ _mix32((v >> np.uint64(30)) & M32)
+    t16 = np.uint64(dropout_threshold(p) >> 16)
     out = np.empty((n // 8, 8), dtype=bool)
-    for half in range(2):
-        c0 = (np.uint64(2) * v + np.uint64(half)) & M32
-        r = _philox4x32_7(c0, c1.copy(), c2.copy(), c3.copy(), k0.copy(), k1.copy())
-        for j in range(4):
-            out[:, half * 4 + j] = r[j] >= thr
+    for j in range(4):
+        r = _mix32((((v << np.uint64(2)) | np.uint64(j)) & M32) ^ key)
+        out[:, 2 * j] = (r & np.uint64(0xFFFF)) >= t16
+        out[:, 2 * j + 1] = (r >> np.uint64(16)) >= t16
     return torch.from_numpy(out.reshape(-1))
 
 

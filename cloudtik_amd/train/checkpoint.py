@@ -7,7 +7,7 @@ BERT's (commented-out) resume path, SURVEY.md §5 "checkpoint/resume").
 * writes go to ``step-<N>.tmp`` and are renamed only after every rank finished (barrier),
   so a crash never leaves a half-written "latest" checkpoint;
 * ``load_latest`` restores model, optimizer, scheduler and RNG (torch CPU/GPU + the
-  dropout Philox stream of cloudtik_amd.ops) and returns the metadata;
+  dropout hash stream of cloudtik_amd.ops) and returns the metadata;
 * only tensors / numbers / strings are stored, loaded with ``weights_only=True``;
 * ``save_async``: the device state is copied into reused pinned host buffers on a side HIP
   stream (the compute stream waits on that copy only, not on the host), and a writer thread

@@ -12,12 +12,29 @@ import torch.multiprocessing as mp
 from cloudtik_amd.ops import reference as R
 
 
-def test_philox_dropout_mask_deterministic_and_rate():
+def test_hash_dropout_mask_deterministic_and_rate():
     m1 = R.dropout_keep_mask(1 << 16, 0.1, seed=7, offset=0)
     m2 = R.dropout_keep_mask(1 << 16, 0.1, seed=7, offset=0)
     m3 = R.dropout_keep_mask(1 << 16, 0.1, seed=7, offset=1 << 16)
     assert torch.equal(m1, m2) and not torch.equal(m1, m3)
     assert abs(1 - m1.float().mean().item() - 0.1) < 0.01
+
+
+def test_hash_dropout_mask_statistics():
+    """Per-lane drop rates, independence of the two elements sharing one hash, and no
+    correlation between the streams of consecutive offsets (steps)."""
+    n, p = 1 << 20, 0.1
+    d = ~R.dropout_keep_mask(n, p, seed=11, offset=0)
+    lanes = d.view(-1, 8).float().mean(0)
+    assert torch.all((lanes - p).abs() < 0.004), lanes
+    pairs = d.view(-1, 2)
+    both = (pairs[:, 0] & pairs[:, 1]).float().mean().item()
+    assert abs(both - p * p) < 0.002, both
+    d2 = ~R.dropout_keep_mask(n, p, seed=11, offset=n)
+    assert abs((d & d2).float().mean().item() - p * p) < 0.002
+    # neighbouring 8-element vectors are independent too
+    v = d.view(-1, 8).any(1).float()
+    assert abs((v[1:] * v[:-1]).mean().item() - v.mean().item() ** 2) < 0.005
 
 
 def test_attention_dropout_mask_rate():
