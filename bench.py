@@ -62,7 +62,11 @@ def parse(argv=None):
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--max-pred", type=int, default=76,
                     help="masked-LM slots per sequence (reference phase-1: max_predictions_per_seq=76)")
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=64.0, help="BERT gradient bucket (MiB)")
+    ap.add_argument("--rn-bucket-mb", type=float, default=8.0,
+                    help="ResNet-50 gradient bucket (MiB): its 51 MB of bf16 gradients would be ONE "
+                         "64 MiB bucket, all-reduced only after the whole backward; 8 MiB gives 7 "
+                         "buckets that overlap the backward of the earlier stages")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="native path: fp32 = bf16 per-backward grads reduced / accumulated in fp32")
     ap.add_argument("--zero", action="store_true",
@@ -222,7 +226,7 @@ def build_resnet(args, rank, world, device, kind):
     opt = FusedSGD(space, lr=0.1, momentum=0.9, weight_decay=1e-4,
                    no_decay=lambda n: n.endswith("bias") or ".bn" in n or n.startswith("bn"))
     broadcast_flat_params(space)
-    ddp = GradBucketer(space, bucket_mb=args.bucket_mb,
+    ddp = GradBucketer(space, bucket_mb=args.rn_bucket_mb,
                        reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
                        mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale
