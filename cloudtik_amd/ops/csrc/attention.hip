@@ -203,20 +203,23 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
     l = l * alpha + ps;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { O0[i] *= alpha; O1[i] *= alpha; }
-    // dropout keep decisions packed into one register (bit 16t + i = register i of S_t),
-    // applied while packing to bf16: no second live copy of the probabilities
-    uint32_t keepbits = 0xFFFFFFFFu;
+    // dropout: one 32-bit hash per (even, odd) key pair, one 16-bit uniform each.  Dropped
+    // probabilities are zeroed in place (compare + select); the 1/(1-p) rescale is folded
+    // into the final 1/l normalisation (l is the pre-dropout row sum), so no per-element
+    // multiply.  (r >> 16) >= t16  <=>  r >= t16 << 16; (r & 0xFFFF) >= t16  <=>
+    // (r << 16) >= t16 << 16: one compare per element.
     if (DROP) {
       const uint32_t pbase = rb2 + (uint32_t)(kt * 32 + 2 * hh);
-      keepbits = 0;
+      const uint32_t thi = a.thr16 << 16;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int i = 0; i < 16; i += 2) {  // (i&3) in {0,2}: an even key and its odd partner
           const uint32_t pair = pbase + (uint32_t)(t * 16 + 4 * (i >> 2) + ((i & 3) >> 1));
           const uint32_t rr = hash_u32(pair ^ a.hash_base);
-          keepbits |= (uint32_t)((rr & 0xFFFFu) >= a.thr16) << (16 * t + i);
-          keepbits |= (uint32_t)((rr >> 16) >= a.thr16) << (16 * t + i + 1);
+          const bool k0 = (rr << 16) >= thi, k1 = rr >= thi;
+          if (t == 0) { S0[i] = k0 ? S0[i] : 0.f; S0[i + 1] = k1 ? S0[i + 1] : 0.f; }
+          else { S1[i] = k0 ? S1[i] : 0.f; S1[i + 1] = k1 ? S1[i + 1] : 0.f; }
         }
       }
     }
@@ -226,13 +229,8 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float p0 = S0[8 * s2 + j], p1 = S1[8 * s2 + j];
-        if (DROP) {
-          p0 = ((keepbits >> (8 * s2 + j)) & 1u) ? p0 * a.inv_keep : 0.f;
-          p1 = ((keepbits >> (16 + 8 * s2 + j)) & 1u) ? p1 * a.inv_keep : 0.f;
-        }
-        pf[0][s2][j] = (__bf16)p0;
-        pf[1][s2][j] = (__bf16)p1;
+        pf[0][s2][j] = (__bf16)S0[8 * s2 + j];
+        pf[1][s2][j] = (__bf16)S1[8 * s2 + j];
       }
     // O^T[d][q] += V^T[d][key] . P^T[key][q]; V^T fragments by transposed LDS reads
 #pragma unroll
@@ -251,7 +249,7 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
 #undef FWD_GLOAD
 #undef FWD_SWRITE
   l += __shfl_xor(l, 32, 64);
-  const float inv = l > 0.f ? 1.f / l : 0.f;
+  const float inv = l > 0.f ? (DROP ? a.inv_keep : 1.f) / l : 0.f;
   if (qvalid) {
     bf16_t* op = a.o + b * a.o_sb + h * a.o_sh + (long)qi * a.o_ss;
 #pragma unroll
