@@ -23,8 +23,7 @@ int ct_bias_act_bwd(const void*, const void*, const void*, void*, float*, void*,
 int ct_dropout(const void*, void*, long, float, uint64_t, uint64_t, hipStream_t);
 int ct_embed3_fwd(const int64_t*, const int64_t*, const void*, const void*, const void*, void*, int,
                   int, int, hipStream_t);
-int ct_embed3_bwd(const int64_t*, const int64_t*, const void*, float*, float*, float*, int, int,
-                  int, hipStream_t);
+int ct_embed3_bwd(const int64_t*, const int64_t*, const void*, float*, float*, float*, int, int, int, int, hipStream_t);
 int ct_cast(const void*, int, void*, int, long, float, int, hipStream_t);
 int ct_splitk_reduce(const float*, int, long, void*, int, hipStream_t);
 int ct_lamb(const void*, int, float*, float*, float*, void*, int, const int*, const long*,
@@ -235,10 +234,13 @@ void embed3_bwd(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor g,
                 c10::optional<at::Tensor> dT) {
   CHECK_IN(ids); CHECK_IN(g); CHECK_BF16(g);
   const int S = ids.size(1), N = g.size(-1), ntok = ids.numel();
+  TORCH_CHECK(ids.dim() == 2 && g.numel() == (int64_t)ntok * N, "embed3_bwd: g must be [ids.numel(), N]");
+  if (tt.has_value() && tt->defined()) TORCH_CHECK(tt->numel() == ntok, "embed3_bwd: token types shape");
+  if (dP.has_value() && dP->defined()) TORCH_CHECK(dP->size(0) >= S, "embed3_bwd: position table too short");
   for (auto* t : {&dW, &dP, &dT}) if (t->has_value() && (*t)->defined()) { CHECK_F32(**t); CHECK_IN(**t); TORCH_CHECK((*t)->size(1) == N); }
   ct_embed3_bwd(ids.data_ptr<int64_t>(), (tt.has_value() && tt->defined()) ? tt->data_ptr<int64_t>() : nullptr,
                 g.data_ptr(), (float*)optr_mut(dW), (float*)optr_mut(dP), (float*)optr_mut(dT), ntok, S,
-                N, cur_stream());
+                N, (dT.has_value() && dT->defined()) ? (int)dT->size(0) : 0, cur_stream());
 }
 
 void cast_into(at::Tensor x, at::Tensor y, double scale, bool accumulate) {
