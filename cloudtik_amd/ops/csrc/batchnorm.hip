@@ -259,11 +259,14 @@ __device__ __forceinline__ void bn_mask8(const BnMask& mk, const u16x8& yv, cons
   }
 }
 
-// per-block sums of dy' and dy'*xhat (dy' = masked dy), 4 rows in flight per thread
+// per-block sums of dy' and dy'*xhat (dy' = masked dy), 4 rows in flight per thread.
+// dmask (optional): dy' is also stored -- for a BN + residual-add + ReLU it IS the residual
+// branch's gradient, and the apply pass then reads dy' instead of dy and y.
 template <int U>
 __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
     const bf16_t* __restrict__ dy, BnMask mk, const bf16_t* __restrict__ x, const float* __restrict__ mean,
-    const float* __restrict__ invstd, BnLayout L, float* __restrict__ p1, float* __restrict__ p2) {
+    const float* __restrict__ invstd, BnLayout L, float* __restrict__ p1, float* __restrict__ p2,
+    bf16_t* __restrict__ dmask) {
   __shared__ float l1[BN_RT * 8];
   __shared__ float l2[BN_RT * 8];
   int cv, rl;
@@ -293,12 +296,15 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
       for (int u = 0; u < U; ++u) {
         bool on[8];
         bn_mask8(mk, yv[u], xv[u], fa, fb, on);
+        u16x8 od;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float d = on[j] ? bf2f(g[u][j]) : 0.f;
+          od[j] = on[j] ? g[u][j] : (unsigned short)0;
           s1[j] += d;
           s2[j] += d * (bf2f(xv[u][j]) - mu[j]) * is[j];
         }
+        if (dmask) reinterpret_cast<u16x8*>(dmask)[o[u]] = od;
       }
     }
     for (; r < r1; r += L.RPI) {
@@ -308,12 +314,15 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
       const u16x8 yv = mk.mode == 1 ? reinterpret_cast<const u16x8*>(mk.y)[o] : u16x8(0);
       bool on[8];
       bn_mask8(mk, yv, xv, fa, fb, on);
+      u16x8 od;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = on[j] ? bf2f(g[j]) : 0.f;
+        od[j] = on[j] ? g[j] : (unsigned short)0;
         s1[j] += d;
         s2[j] += d * (bf2f(xv[j]) - mu[j]) * is[j];
       }
+      if (dmask) reinterpret_cast<u16x8*>(dmask)[o] = od;
     }
   }
   bn_block_sum2(s1, s2, l1, l2, L.RPI, rl, L.CV);
@@ -634,12 +643,16 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
   BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
   const BnMask mk{relu_mode, (const bf16_t*)y, stat + 2 * C, stat + 3 * C};
+  // BN + residual add + ReLU: the reduction pass writes the masked gradient (= the residual
+  // branch's gradient, returned as dres) and the apply pass reads it back instead of dy and y:
+  // 7 instead of 8 activation-sized passes over the biggest ResNet tensors
+  bf16_t* dm = (relu_mode == 1 && dres) ? (bf16_t*)dres : nullptr;
   if (bn_unroll() == 8)
     bn_bwd_reduce_kernel<8><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
-                                                        part, part + (size_t)2048 * C);
+                                                        part, part + (size_t)2048 * C, dm);
   else
     bn_bwd_reduce_kernel<4><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
-                                                        part, part + (size_t)2048 * C);
+                                                        part, part + (size_t)2048 * C, dm);
   const int acc = (param_flags >> 1) & 1;   // bit 1: accumulate into dgamma / dbeta
   if (param_flags & 1)
     bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
@@ -650,7 +663,13 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
         part, part + (size_t)2048 * C, nblk, M, C, (const bf16_t*)gamma, stat, stat + C,
         (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
-  BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dy, mk, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
-                 (bf16_t*)dx, (bf16_t*)dres, tv, C / 8);
+  if (dm) {
+    const BnMask none{0, nullptr, nullptr, nullptr};
+    BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dm, none, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
+                   (bf16_t*)dx, (bf16_t*)nullptr, tv, C / 8);
+  } else {
+    BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dy, mk, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
+                   (bf16_t*)dx, (bf16_t*)dres, tv, C / 8);
+  }
   return 0;
 }
