@@ -96,11 +96,16 @@ def spawn_ranks(n: int) -> int:
     others are terminated (no rank is left blocked in a collective until the RCCL timeout).
     Returns the first non-zero exit code, else 0."""
     port = _free_port()
+    cpus = rank_cpus(n)
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CLOUDTIK_BENCH_CHILD="1")
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        pin = cpus.get(r)
+        if pin:
+            env["CLOUDTIK_BENCH_CPUS"] = ",".join(map(str, pin))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      preexec_fn=(lambda c=pin: os.sched_setaffinity(0, c)) if pin else None))
     rc = 0
     live = list(procs)
     while live:
@@ -121,6 +126,23 @@ def spawn_ranks(n: int) -> int:
                         q.kill()
         time.sleep(0.2)
     return rc if rc >= 0 else 128 - rc
+
+
+def rank_cpus(n: int):
+    """local rank -> cores of its GPU's NUMA node (runner/affinity.py), restricted to the cores
+    this process may use; {} when the topology is unknown or leaves a rank no core."""
+    try:
+        from cloudtik_amd.runner.affinity import rank_cpu_sets
+        allowed = os.sched_getaffinity(0)
+        out = {}
+        for r, cores in rank_cpu_sets(n).items():
+            c = sorted(set(cores) & allowed)
+            if not c:
+                return {}
+            out[r] = c
+        return out
+    except Exception:  # noqa: BLE001 - affinity is an optimisation, never a failure
+        return {}
 
 
 # ------------------------------------------------------------------ TunableOp
@@ -151,6 +173,54 @@ def setup_tunableop(mode, rank):
     if mode == "tune":
         tn.set_max_tuning_duration(60)
         tn.set_max_tuning_iterations(30)
+
+
+def bucket_plan(ddp):
+    """Gradient-bucket plan of a GradBucketer: count, sizes, collective, wire dtype."""
+    esize = ddp.space.grad.element_size() if not ddp.fp32 else 4
+    sizes = [(hi - lo) * esize for lo, hi, _ in ddp.buckets]
+    return {"buckets": len(sizes), "bytes_total": sum(sizes), "bytes_max": max(sizes) if sizes else 0,
+            "bytes_min": min(sizes) if sizes else 0,
+            "collective": "reduce_scatter+all_gather (ZeRO-1)" if ddp.zero else "all_reduce",
+            "overlap_with_backward": bool(ddp.overlap), "p2p_small_buckets": ddp.p2p is not None}
+
+
+def environment(device, world):
+    """Versions and state that decide performance on a fresh box (printed to stderr and
+    recorded in the JSON line)."""
+    import torch
+    import torch.distributed as dist
+    env = {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None)}
+    try:
+        from cloudtik_amd import ops
+        from cloudtik_amd.ops import miopen_solvers
+        env["native_ops"] = ops.native_available()
+        env["miopen_db"] = miopen_solvers.status()
+    except Exception as e:  # noqa: BLE001
+        env["ops_error"] = repr(e)[:200]
+    if device.type == "cuda":
+        p = torch.cuda.get_device_properties(device)
+        env["gpu"] = {"name": p.name, "arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
+                      "hbm_gib": round(p.total_memory / 2 ** 30, 1)}
+        try:
+            v = torch.cuda.nccl.version()
+            env["rccl"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001
+            env["rccl"] = None
+    env["nccl_env"] = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_"))}
+    if os.environ.get("CLOUDTIK_BENCH_CPUS"):
+        env["rank0_cpus"] = os.environ["CLOUDTIK_BENCH_CPUS"]
+    if dist.is_initialized():
+        # world size as seen by a real collective (not just the launcher's env)
+        t = torch.ones(1, device=device)
+        dist.all_reduce(t)
+        env["world_size_seen_by_collective"] = int(t.item())
+        # physical devices behind the ranks (gloo ranks may share one GPU)
+        ident = f"{socket.gethostname()}:{device.type}:{device.index if device.type == 'cuda' else os.getpid()}"
+        ids = [None] * world
+        dist.all_gather_object(ids, ident)
+        env["distinct_devices"] = len(set(ids)) if device.type == "cuda" else None
+    return env
 
 
 # ------------------------------------------------------------------ native builders
@@ -204,7 +274,7 @@ def build_bert(args, rank, world, device, kind):
                 unit="tokens/s", items_per_step=B * S,
                 metric="bert_large_pretrain_tokens_per_sec" if kind in ("bert-large", "tiny")
                 else "bert_base_pretrain_tokens_per_sec",
-                optimizer="fused LAMB (HIP)", impl="native")
+                optimizer="fused LAMB (HIP)", impl="native", plan=bucket_plan(ddp))
     return step, close, info
 
 
@@ -241,7 +311,7 @@ def build_resnet(args, rank, world, device, kind):
 
     info = dict(model="resnet50" if not tiny else "resnet-tiny", per_gpu_batch=B, seq_len=None,
                 unit="images/s", items_per_step=B, metric="resnet50_train_images_per_sec",
-                optimizer="fused SGD (HIP)", impl="native", image_size=R)
+                optimizer="fused SGD (HIP)", impl="native", image_size=R, plan=bucket_plan(ddp))
     return (lambda: ts(x, y)), ddp.remove, info
 
 
@@ -330,9 +400,33 @@ def build_resnet_eager(args, rank, world, device, kind):
 
 
 # ------------------------------------------------------------------ timing
-def timed(step, args, rank, world, device):
+def kernel_audit(step, device):
+    """One extra UNTIMED step under torch.profiler: how many GPU kernels ran, and how many of
+    them are MIOpen's naive convolution fallbacks (ConvDirectNaive*: 25-200 ms per call; a
+    correctly installed solver db never selects them).  {} if profiling is unavailable."""
+    import torch
+    if device.type != "cuda" or os.environ.get("CLOUDTIK_BENCH_AUDIT", "1") == "0":
+        return {}
+    try:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step()
+            torch.cuda.synchronize()
+        names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    except Exception as e:  # noqa: BLE001
+        return {"error": repr(e)[:200]}
+    naive = sorted({n for n in names if "naive" in n.lower()})
+    return {"kernels_per_step": len(names), "naive_conv_launches": sum("naive" in n.lower() for n in names),
+            "naive_conv_kernels": naive[:8]}
+
+
+def timed(step, args, rank, world, device, audit=False):
     """W warm-up steps, then K timed steps between barrier+sync brackets.  Returns
-    (max elapsed over ranks, per-rank elapsed list, last loss)."""
+    (max elapsed over ranks, per-rank elapsed list, last loss, per-step ms, audit).
+
+    Per-step times come from HIP events recorded between the steps on the compute stream
+    (no host synchronisation inside the timed loop); the headline is the host clock around
+    all K steps."""
     import torch
     import torch.distributed as dist
     from cloudtik_amd.parallel import barrier
@@ -347,38 +441,75 @@ def timed(step, args, rank, world, device):
     sync()
     if rank == 0:
         print(f"[bench] warm-up {args.warmup} step(s): {time.perf_counter() - tw:.1f}s", file=sys.stderr)
+    info = kernel_audit(step, device) if audit else {}
     barrier()
     sync()
+    cuda = device.type == "cuda"
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if cuda else []
+    stamps = []
     t0 = time.perf_counter()
     loss = None
-    for _ in range(args.steps):
+    if cuda:
+        events[0].record()
+    for i in range(args.steps):
         loss = step()
+        if cuda:
+            events[i + 1].record()
+        else:
+            stamps.append(time.perf_counter())
     barrier()
     sync()
     el = time.perf_counter() - t0
+    if cuda:
+        step_ms = [events[i].elapsed_time(events[i + 1]) for i in range(args.steps)]
+    else:
+        prev = [t0] + stamps[:-1]
+        step_ms = [(b - a) * 1e3 for a, b in zip(prev, stamps)]
     per_rank = [el]
     if dist.is_initialized():
         t = torch.tensor([el], dtype=torch.float64, device=device)
         out = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(out, t)
         per_rank = [float(o.item()) for o in out]
-    return max(per_rank), per_rank, float(loss.detach().float().item())
+    return max(per_rank), per_rank, float(loss.detach().float().item()), step_ms, info
+
+
+def mean_ci(xs):
+    """mean and 1.96 sigma (the reference protocol's ± band,
+    imagenet-resnet50-synthetic-pytorch-distributed.py:194-210)."""
+    import statistics
+    if not xs:
+        return None, None
+    m = statistics.fmean(xs)
+    return m, (1.96 * statistics.pstdev(xs) if len(xs) > 1 else 0.0)
 
 
 def run_one(build, args, rank, world, device, kind):
     import gc
     import torch
     step, close, info = build(args, rank, world, device, kind)
-    elapsed, per_rank, loss = timed(step, args, rank, world, device)
+    elapsed, per_rank, loss, step_ms, audit = timed(step, args, rank, world, device,
+                                                    audit=info["unit"] == "images/s")
+    if audit and rank == 0:
+        print(f"[bench] {info['model']} kernel audit (one untimed step): {json.dumps(audit)}", file=sys.stderr)
+    plan = info.pop("plan", None)
     close()
     del step
     gc.collect()
     if device.type == "cuda":
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    m, ci = mean_ci(step_ms)
+    # per-step throughput of the whole job (reference: mean img/s ± 1.96 sigma)
+    rates = [info["items_per_step"] * world / (t / 1e3) for t in step_ms if t > 0]
+    rm, rci = mean_ci(rates)
     info.update(elapsed=elapsed, ms=elapsed / args.steps * 1e3,
                 per_rank_ms=[round(e / args.steps * 1e3, 3) for e in per_rank],
-                value=info["items_per_step"] * world * args.steps / elapsed, loss=loss)
+                value=info["items_per_step"] * world * args.steps / elapsed, loss=loss,
+                step_ms=[round(t, 3) for t in step_ms], step_ms_mean=round(m, 3) if m else None,
+                step_ms_ci95=round(ci, 3) if ci is not None else None,
+                rate_mean=round(rm, 2) if rm else None, rate_ci95=round(rci, 2) if rci is not None else None,
+                audit=audit, plan=plan)
     return info
 
 
@@ -418,10 +549,13 @@ def main():
             r["eager_value"], r["eager_ms"] = e["value"], e["ms"]
         results.append(r)
 
-    if rank == 0 and device.type == "cuda" and args.tunableop != "off":
+    envinfo = environment(device, world)
+    if device.type == "cuda" and args.tunableop != "off":
         import torch.cuda.tunable as tn
-        print(f"[bench] TunableOp: {len(tn.get_results() or [])} tuned GEMM solutions in use "
-              f"({tn.get_filename()})", file=sys.stderr)
+        envinfo["tunableop"] = {"solutions": len(tn.get_results() or []), "file": tn.get_filename()}
+    if rank == 0:
+        print(f"[bench] environment: {json.dumps(envinfo)}", file=sys.stderr)
+    n_dev = envinfo.get("distinct_devices") or (world if device.type == "cuda" else 0)
     if rank == 0:
         head = results[0]
         base = BASELINE.get(head["model"])
@@ -434,15 +568,26 @@ def main():
             cfg.update(seq_len=head["seq_len"], max_pred=head["max_pred"],
                        sentences_per_sec=round(head["value"] / head["seq_len"], 2))
         out = {"metric": head["metric"], "value": round(head["value"], 2), "unit": head["unit"],
-               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "n_gpus": n_dev, "world_size": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(head["ms"], 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": (round(head["value"] / base, 4) if base else None),
                "dtype": "bf16" if device.type == "cuda" else "fp32",
                "data": "synthetic (one resident random batch per rank, re-used every step; random-init weights)",
                "config": cfg,
-               "world_size_seen_by_rccl": dist.get_world_size() if dist.is_initialized() else 1,
+               "world_size_seen_by_rccl": envinfo.get("world_size_seen_by_collective", 1)
+               if (dist.is_initialized() and dist.get_backend() == "nccl") else (1 if world == 1 else None),
                "backend": dist.get_backend() if dist.is_initialized() else None,
-               "per_rank_ms_per_step": head["per_rank_ms"]}
+               "per_rank_ms_per_step": head["per_rank_ms"],
+               "step_ms_mean": head["step_ms_mean"], "step_ms_ci95": head["step_ms_ci95"],
+               "value_mean_per_step": head["rate_mean"], "value_ci95": head["rate_ci95"],
+               "bucket_plan": head["plan"],
+               "env": {k: envinfo.get(k) for k in ("gpu", "rccl", "nccl_env", "rank0_cpus", "tunableop",
+                                                   "distinct_devices", "world_size_seen_by_collective")
+                       if envinfo.get(k) is not None},
+               "miopen_db": (envinfo.get("miopen_db") or {}).get("mode") if (envinfo.get("miopen_db") or {}).get(
+                   "installed") else "NOT INSTALLED"}
+        if device.type == "cuda" and n_dev != world:
+            out["note"] = f"{world} ranks shared {n_dev} GPU(s): plumbing check, not a scaling point"
         if "eager_value" in head:
             out["eager_value"] = round(head["eager_value"], 2)
             out["speedup_vs_eager"] = round(head["value"] / head["eager_value"], 3)
@@ -453,6 +598,11 @@ def main():
             out[f"{key}_per_gpu_batch"] = r["per_gpu_batch"]
             out[f"{key}_per_rank_ms_per_step"] = r["per_rank_ms"]
             out[f"{key}_loss_last_step"] = round(r["loss"], 4)
+            out[f"{key}_step_ms_mean"], out[f"{key}_step_ms_ci95"] = r["step_ms_mean"], r["step_ms_ci95"]
+            out[f"{key}_value_mean_per_step"], out[f"{key}_value_ci95"] = r["rate_mean"], r["rate_ci95"]
+            out[f"{key}_bucket_plan"] = r["plan"]
+            if r.get("audit"):
+                out[f"{key}_kernel_audit"] = {k: v for k, v in r["audit"].items() if k != "naive_conv_kernels"}
             if "eager_value" in r:
                 out[f"{key}_eager_value"] = round(r["eager_value"], 2)
                 out[f"{key}_speedup_vs_eager"] = round(r["value"] / r["eager_value"], 3)

@@ -22,40 +22,11 @@ import torch
 from . import reference as ref
 
 
-def _install_miopen_db():
-    """Point MIOpen at the solver database searched on MI355X for this framework's conv
-    shapes (ResNet-50 NHWC bf16 training; ``ops/miopen_db``), so immediate-mode convolution
-    uses the searched solvers (+10.7% ResNet-50 img/s) without a find step at start-up.
-    The shipped files are copied to a per-user cache directory first: MIOpen appends to its
-    user db, and the package directory may be read-only or shared by several ranks."""
-    if os.environ.get("MIOPEN_USER_DB_PATH") or os.environ.get("CLOUDTIK_AMD_MIOPEN_DB", "1") == "0":
-        return
-    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
-    if not os.path.isdir(src):
-        return
-    try:
-        import hashlib
-        import shutil
-        files = sorted(f for f in os.listdir(src) if f.endswith((".udb.txt", ".ufdb.txt")))
-        h = hashlib.sha1()
-        for f in files:
-            with open(os.path.join(src, f), "rb") as fh:
-                h.update(f.encode() + fh.read())
-        # keyed by the shipped content: an updated db in a new release gets a fresh directory
-        dst = os.path.join(os.path.expanduser(os.environ.get("XDG_CACHE_HOME", "~/.cache")), "cloudtik_amd",
-                           "miopen_db", h.hexdigest()[:12])
-        os.makedirs(dst, exist_ok=True)
-        for f in files:
-            if not os.path.exists(os.path.join(dst, f)):
-                tmp = os.path.join(dst, f".{f}.{os.getpid()}.tmp")
-                shutil.copyfile(os.path.join(src, f), tmp)
-                os.replace(tmp, os.path.join(dst, f))       # atomic: concurrent ranks never see a partial file
-        os.environ["MIOPEN_USER_DB_PATH"] = dst
-    except OSError:
-        pass
+from . import miopen_solvers as _miopen_db  # noqa: E402
 
-
-_install_miopen_db()
+# MIOpen solver records for this framework's conv shapes (see ops/miopen_solvers.py): installed
+# before anything creates a MIOpen handle; never silently skipped (bench.py prints status())
+_miopen_db.install()
 
 _C_ERR = None
 try:  # the extension is built in-tree (see ops/build.py)

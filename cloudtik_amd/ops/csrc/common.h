@@ -139,7 +139,10 @@ __device__ __forceinline__ uint32_t dropout_bits8(uint64_t seed, uint64_t offset
   uint32_t bits = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t r = mix32(((uint32_t)v << 2 | (uint32_t)j) ^ key);
+    // the key enters twice (add before the multiply, xor after it): with a plain
+    // mix32(ctr ^ key) two sites whose keys agree above the counter range would draw
+    // XOR-permuted copies of one stream
+    const uint32_t r = mix32((((uint32_t)v << 2 | (uint32_t)j) + key) * 0x9E3779B1u ^ key);
     bits |= (uint32_t)((r & 0xFFFFu) >= t16) << (2 * j);
     bits |= (uint32_t)((r >> 16) >= t16) << (2 * j + 1);
   }

@@ -51,7 +51,8 @@ def dropout_keep_mask(n: int, p: float, seed: int, offset: int) -> torch.Tensor:
     t16 = np.uint64(dropout_threshold(p) >> 16)
     out = np.empty((n // 8, 8), dtype=bool)
     for j in range(4):
-        r = _mix32((((v << np.uint64(2)) | np.uint64(j)) & M32) ^ key)
+        ctr = ((v << np.uint64(2)) | np.uint64(j)) & M32
+        r = _mix32(((((ctr + key) & M32) * np.uint64(0x9E3779B1)) & M32) ^ key)
         out[:, 2 * j] = (r & np.uint64(0xFFFF)) >= t16
         out[:, 2 * j + 1] = (r >> np.uint64(16)) >= t16
     return torch.from_numpy(out.reshape(-1))

@@ -138,6 +138,7 @@ class EtcdLeaderElection:
         self.lock = EtcdLock(client, f"leader/{name}", ttl_s, candidate_id)
         self.on_elected, self.on_demoted = on_elected, on_demoted
         self._leader = False
+        self._last_renew = 0.0
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
 
@@ -151,14 +152,26 @@ class EtcdLeaderElection:
     def leader(self) -> Optional[str]:
         return self.lock.owner()
 
-    def step(self) -> bool:
-        was = self._leader
-        self._leader = self.lock.renew() if was else self.lock.acquire(blocking=False)
-        if self._leader and not was and self.on_elected:
+    def _set(self, leader: bool):
+        was, self._leader = self._leader, leader
+        if leader:
+            self._last_renew = time.monotonic()
+        if leader and not was and self.on_elected:
             self.on_elected()
-        if was and not self._leader and self.on_demoted:
+        if was and not leader and self.on_demoted:
             self.on_demoted()
+
+    def step(self) -> bool:
+        self._set(self.lock.renew() if self._leader else self.lock.acquire(blocking=False))
         return self._leader
+
+    def _on_error(self):
+        """etcd unreachable.  The lease may expire on the server while we cannot renew it,
+        and another candidate then takes the lock: once the last successful renew is a lease
+        TTL old we stop acting as leader (never two leaders at once)."""
+        if self._leader and time.monotonic() - self._last_renew >= self.lock.ttl_s:
+            self.lock.lease = None          # expired server-side: re-acquire with a new lease
+            self._set(False)
 
     def start(self):
         def loop():
@@ -166,7 +179,7 @@ class EtcdLeaderElection:
                 try:
                     self.step()
                 except Exception:  # noqa: BLE001 - etcd briefly unreachable: retry
-                    pass
+                    self._on_error()
                 self._stop.wait(max(0.05, self.lock.ttl_s / 3))
         self._thread = threading.Thread(target=loop, daemon=True)
         self._thread.start()

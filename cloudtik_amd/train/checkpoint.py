@@ -1,8 +1,9 @@
 """Checkpoint / resume (reference: the transfer-learning models' checkpoint saving and
 BERT's (commented-out) resume path, SURVEY.md §5 "checkpoint/resume").
 
-* one directory per step: ``<dir>/step-<N>/`` with ``model.pt`` (rank 0), ``optim-rank<R>.pt``
-  (every rank: flat fp32 master + moments, so ZeRO-style sharded optimizer state round-trips),
+* one directory per step: ``<dir>/step-<N>/`` with ``model.pt`` (rank 0), ``optim.pt`` (rank 0:
+  the flat fp32 master + moments in the global layout -- ZeRO-1 shards are gathered -- which
+  restores at any world size) or ``optim-rank<R>.pt`` (per-rank shard-layout state),
   ``meta.json`` (step, epoch, world size, user metadata) and ``rng-rank<R>.pt``;
 * writes go to ``step-<N>.tmp`` and are renamed only after every rank finished (barrier),
   so a crash never leaves a half-written "latest" checkpoint;
@@ -74,7 +75,10 @@ class Checkpointer:
             if scheduler is not None and hasattr(scheduler, "state_dict"):
                 torch.save(scheduler.state_dict(), os.path.join(tmp, "scheduler.pt"))
         if optimizer is not None:
-            torch.save(_to_cpu(optimizer.state_dict()), os.path.join(tmp, f"optim-rank{rank}.pt"))
+            osd = optimizer.state_dict()          # collective under ZeRO-1: every rank calls it
+            name = _optim_file(osd, rank)
+            if name is not None:
+                torch.save(_to_cpu(osd), os.path.join(tmp, name))
         torch.save(_rng_state(), os.path.join(tmp, f"rng-rank{rank}.pt"))
         _barrier()
         if rank == 0:
@@ -127,8 +131,10 @@ class Checkpointer:
         if cuda:
             stream = torch.cuda.Stream()
             stream.wait_stream(torch.cuda.current_stream())
-        snap = {"model": model.state_dict() if rank == 0 else None,
-                "optim": optimizer.state_dict() if optimizer is not None else None}
+        osd = optimizer.state_dict() if optimizer is not None else None   # collective under ZeRO-1
+        if osd is not None and _optim_file(osd, rank) is None:
+            osd = None                          # rank 0 writes the global-layout state
+        snap = {"model": model.state_dict() if rank == 0 else None, "optim": osd}
         if stream is not None:
             snap = self._pinned_copy(snap, stream, "s")
             event = torch.cuda.Event()
@@ -152,7 +158,9 @@ class Checkpointer:
                     if sched is not None:
                         torch.save(sched, os.path.join(tmp, "scheduler.pt"))
                 if snap["optim"] is not None:
-                    torch.save(snap["optim"], os.path.join(tmp, f"optim-rank{rank}.pt"))
+                    name = _optim_file(snap["optim"], rank)
+                    if name is not None:
+                        torch.save(snap["optim"], os.path.join(tmp, name))
                 torch.save(rng, os.path.join(tmp, f"rng-rank{rank}.pt"))
                 open(os.path.join(tmp, f"done-rank{rank}"), "w").close()
                 if rank == 0:
@@ -190,12 +198,14 @@ class Checkpointer:
         sd = torch.load(os.path.join(d, "model.pt"), map_location=map_location, weights_only=True)
         model.load_state_dict(sd, strict=strict)
         if optimizer is not None:
-            p = os.path.join(d, f"optim-rank{rank}.pt")
+            p = os.path.join(d, "optim.pt")          # global layout: one file for any world size
             if not os.path.exists(p):
+                p = os.path.join(d, f"optim-rank{rank}.pt")
                 if meta["world_size"] != world:
-                    raise RuntimeError(f"checkpoint written by {meta['world_size']} ranks; resuming with {world} "
-                                       "needs an unsharded optimizer state")
-                raise FileNotFoundError(p)
+                    raise RuntimeError(f"checkpoint written by {meta['world_size']} ranks holds per-rank "
+                                       f"(shard-layout) optimizer state; it cannot resume at {world} ranks")
+                if not os.path.exists(p):
+                    raise FileNotFoundError(p)
             optimizer.load_state_dict(torch.load(p, map_location=map_location, weights_only=True))
         if scheduler is not None and os.path.exists(os.path.join(d, "scheduler.pt")):
             scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=True))
@@ -226,6 +236,14 @@ class PendingSave:
         if self.error is not None:
             raise self.error
         return self.path
+
+
+def _optim_file(osd, rank: int) -> Optional[str]:
+    """File name of this rank's optimizer state, or None when another rank writes it: a
+    global-layout flat state (identical on every rank) is written once, by rank 0."""
+    if isinstance(osd, dict) and osd.get("flat_layout") == "global":
+        return "optim.pt" if rank == 0 else None
+    return f"optim-rank{rank}.pt"
 
 
 def _to_cpu(obj):

@@ -84,6 +84,7 @@ class FlatParamSpace:
             self.offsets.append(off)
             self.numels.append(p.numel())
             off += ((p.numel() + align - 1) // align) * align
+        self.used = off                  # world-size independent: the parameters' extent
         rank, world = shard
         self.rank, self.world = rank, world
         # pad total so every shard is an aligned equal slice
@@ -349,30 +350,59 @@ class _FlatOptimizer(torch.optim.Optimizer):
             self.dyn.copy_(host)
 
     def state_dict(self):
-        """Flat optimizer state in the GLOBAL layout (ZeRO-1 shards are gathered), so a
-        checkpoint restores onto any sharding / world size."""
+        """Flat optimizer state in the GLOBAL layout (ZeRO-1 shards are gathered).
+
+        Parameter offsets inside the flat space depend only on the parameter list and the
+        alignment, never on the world size (only the tail padding of ``total`` does), so a
+        global-layout state restores onto any sharding / world size: ``load_state_dict``
+        re-pads it to the current ``total`` and cuts this rank's pieces out of it.  The
+        parameter table is stored with it and checked on load."""
         sd = super().state_dict()
         sp = self.space
         flat = dict(self._flat_state())
         if sp.master is not None:      # fp32 master shard (the bf16 model alone loses bits)
             flat["master"] = sp.master
-        sd["flat"] = {k: (sp.full_of(v) if sp.sharded else v) for k, v in flat.items()}
-        sd["flat_layout"] = "global" if sp.sharded else ("shard" if sp.world > 1 else "global")
+        if sp.sharded or sp.world == 1:
+            sd["flat"] = {k: (sp.full_of(v) if sp.sharded else v) for k, v in flat.items()}
+            sd["flat_layout"] = "global"
+        else:                          # a contiguous shard that no gather function can rebuild
+            sd["flat"] = flat
+            sd["flat_layout"] = "shard"
+        sd["flat_params"] = {"offsets": list(sp.offsets), "numels": list(sp.numels),
+                             "used": sp.used, "world": sp.world}
         sd["step_count"] = self.step_count
         return sd
 
     def load_state_dict(self, sd):
+        """Restore the flat state.  The weights themselves come from the MODEL's state dict
+        (parameters are views of ``space.model``), loaded before this: the shard-local copies
+        derived from it (ZeRO-1 ``local_model``, the fp32 ``master``) are refreshed here
+        first, then the saved fp32 master (if any) overrides the bf16-rounded refresh."""
         sd = dict(sd)
         flat = sd.pop("flat", {})
         layout = sd.pop("flat_layout", "shard")
+        table = sd.pop("flat_params", None)
         self.step_count = sd.pop("step_count", 0)
         super().load_state_dict(sd)
         sp = self.space
+        if table is not None and (list(table["offsets"]) != list(sp.offsets)
+                                  or list(table["numels"]) != list(sp.numels)):
+            raise ValueError("optimizer state was saved for a different parameter list")
+        if layout == "shard" and table is not None and table["world"] != sp.world:
+            raise ValueError(f"shard-layout optimizer state of world size {table['world']} cannot be "
+                             f"restored at world size {sp.world}")
+        sp.sync_master_from_model()
         for k, v in flat.items():
             dst = sp.master if k == "master" else getattr(self, k)
             v = v.to(dst.device)
-            if layout == "global" and v.numel() == sp.total and dst.numel() != sp.total:
-                v = sp.local_of(v)
+            if layout == "global":
+                if v.numel() != sp.total:          # saved at another world size: re-pad the tail
+                    full = torch.zeros(sp.total, dtype=v.dtype, device=v.device)
+                    n = min(sp.used, v.numel())
+                    full[:n].copy_(v[:n])
+                    v = full
+                if dst.numel() != sp.total:
+                    v = sp.local_of(v)
             dst.copy_(v)
 
     def _flat_state(self):

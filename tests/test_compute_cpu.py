@@ -248,3 +248,20 @@ def test_new_op_references_cpu():
     assert abs(ra.item() - 7.5) < 1e-4   # mean of a linear ramp over the box
     fl = ops.sigmoid_focal_loss(torch.zeros(2, 3), torch.tensor([1, 0]))
     assert fl.item() > 0
+
+
+def test_dropout_sites_with_close_keys_are_independent(monkeypatch):
+    """Two dropout sites whose stream keys differ only in low bits must not draw permuted
+    copies of one mask (mix32(ctr ^ key) would: site2[c] == site1[c ^ (k1 ^ k2)])."""
+    import numpy as np
+    n, p = 1 << 16, 0.5
+    k1 = 0x12345670
+    masks = []
+    for k in (k1, k1 ^ 0x5):
+        monkeypatch.setattr(R, "_dropout_key", lambda s, o, k=k: k)
+        masks.append(R.dropout_keep_mask(n, p, seed=1, offset=0).numpy().reshape(-1, 2))
+    m1, m2 = masks                                    # [pair counter, 2] 16-bit uniforms per hash
+    ctr = np.arange(m1.shape[0])
+    permuted = m1[(ctr ^ 0x5) % m1.shape[0]]
+    assert (permuted == m2).mean() < 0.6              # independent: ~0.5 agreement per element
+    assert abs((m1 == m2).mean() - 0.5) < 0.02

@@ -143,3 +143,41 @@ def test_leader_election_and_factory(etcd):
     e2.resign()
     with pytest.raises(ValueError):
         leader_election("zk://x:1", "n")
+
+
+def test_leader_demotes_itself_when_etcd_unreachable(etcd):
+    """A leader that cannot renew for a lease TTL stops acting as leader (its lease expires on
+    the server and another candidate takes over): never two leaders at once."""
+    _, c, port = etcd
+    ev = []
+    cut = threading.Event()
+    partitioned = EtcdClient(f"127.0.0.1:{port}")
+    real_post = partitioned._post
+
+    def post(path, body):
+        if cut.is_set():
+            raise OSError("gateway unreachable")
+        return real_post(path, body)
+
+    partitioned._post = post
+    e1 = EtcdLeaderElection(partitioned, "svc", "n1", ttl_s=1, on_elected=lambda: ev.append("n1+"),
+                            on_demoted=lambda: ev.append("n1-"))
+    e2 = EtcdLeaderElection(c, "svc", "n2", ttl_s=1, on_elected=lambda: ev.append("n2+"))
+    e1.start()
+    deadline = time.time() + 5
+    while not e1.is_leader() and time.time() < deadline:
+        time.sleep(0.02)
+    assert e1.is_leader()
+    cut.set()
+    t_cut = time.time()
+    while e1.is_leader() and time.time() < deadline + 5:
+        time.sleep(0.02)
+    assert not e1.is_leader() and time.time() - t_cut < 2.5
+    e2.start()
+    while not e2.is_leader() and time.time() < deadline + 10:
+        time.sleep(0.02)
+    assert e2.is_leader()
+    assert ev.index("n1-") < ev.index("n2+")              # demoted before the other took over
+    cut.clear()
+    e1.resign()
+    e2.resign()

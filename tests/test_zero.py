@@ -81,11 +81,17 @@ def _worker(rank, world, port, kind, dtype, out):
         _steps(m2, opt2, ddp2, rank, dtype, range(2))
         ck = (sp2.model.clone(), opt2.state_dict())
         m3, sp3, opt3, ddp3 = _build(kind, dtype, rank, world, zero=True)
-        sp3.model.copy_(ck[0])
-        sp3.sync_master_from_model()
-        opt3.load_state_dict(ck[1])
+        sp3.model.copy_(ck[0])                 # what Checkpointer.load's model.load_state_dict does
+        opt3.load_state_dict(ck[1])            # must refresh local_model / master itself
         _steps(m3, opt3, ddp3, rank, dtype, range(2, 3))
         res["resumed"] = _real(sp3, sp3.model)
+        if rank == 0:                          # for the world-size-change check in the parent
+            res["ckpt_model"] = ck[0].clone()
+            res["ckpt_state"] = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in ck[1].items()
+                                 if k in ("flat", "flat_layout", "flat_params", "step_count")}
+            res["ckpt_state"]["full"] = opt2.state_dict()
+        else:
+            opt2.state_dict()                  # collective: every rank takes part
         out[rank] = res
     finally:
         dist.destroy_process_group()
@@ -110,3 +116,60 @@ def test_zero1_matches_unsharded(kind, world, dtype):
         for k, v in res[r]["plain_state"].items():
             torch.testing.assert_close(res[r]["zero_state"][k], v, **tol, msg=k)
     assert torch.equal(res[0]["zero"], res[world - 1]["zero"])
+    # the global-layout state restores unsharded at world size 1 (other tail padding)
+    from cloudtik_amd.train.optim import FlatParamSpace
+    m1, sp1, opt1, _ = _build(kind, dtype, 0, 1, zero=False)
+    assert sp1.total != res[0]["ckpt_model"].numel() or world == 1 or sp1.total % world == 0
+    n = min(sp1.total, res[0]["ckpt_model"].numel())
+    sp1.model[:n].copy_(res[0]["ckpt_model"][:n])
+    opt1.load_state_dict(res[0]["ckpt_state"]["full"])
+    saved = res[0]["ckpt_state"]["flat"]
+    for k, v in opt1.state_dict()["flat"].items():
+        torch.testing.assert_close(_real(sp1, v), _real(sp1, saved[k][:sp1.used].float()
+                                   if saved[k].numel() >= sp1.used else saved[k]), rtol=0, atol=0, msg=k)
+    assert isinstance(sp1, FlatParamSpace)
+
+
+def _trainer_worker(rank, world, port, ckdir, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from cloudtik_amd.train.trainer import Trainer
+    g = torch.Generator().manual_seed(5 + rank)
+    x = torch.randn(96, 20, generator=g)
+    y = torch.randint(0, 5, (96,), generator=g)
+    batches = [(x[i:i + 16], y[i:i + 16]) for i in range(0, 96, 16)]
+    try:
+        def run(epochs, ck, seed):
+            torch.manual_seed(seed)
+            m = torch.nn.Sequential(torch.nn.Linear(20, 48), torch.nn.GELU(), torch.nn.Linear(48, 5))
+            t = Trainer(m, "adamw", lr=1e-2, weight_decay=0.01, train_loader=batches, epochs=epochs, log_every=0,
+                        checkpoint_dir=ck, zero=True, bucket_mb=0.002)
+            assert t.space.sharded and t.space.master is None        # fp32: no master copy
+            t.fit()
+            return {k: v.detach().clone() for k, v in t.model.state_dict().items()}
+        straight = run(2, None, 0)
+        run(1, ckdir, 0)                       # checkpoint at the end of epoch 0
+        resumed = run(2, ckdir, 123)           # other init: the checkpoint must overwrite it
+        out[rank] = {"straight": straight, "resumed": resumed}
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_trainer_zero1_resume_fp32(tmp_path):
+    """Trainer(zero=True) with fp32 parameters (no master copy) resumes from its checkpoint
+    and ends on the same weights as an uninterrupted run."""
+    port = _port()
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as mgr:
+        out = mgr.dict()
+        procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, str(tmp_path), out)) for r in range(2)]
+        [p.start() for p in procs]
+        [p.join(240) for p in procs]
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        res = dict(out)
+    assert os.path.exists(os.path.join(str(tmp_path), "step-6", "optim.pt"))
+    for r in range(2):
+        for k, v in res[r]["straight"].items():
+            torch.testing.assert_close(res[r]["resumed"][k], v, rtol=1e-6, atol=1e-7, msg=k)
