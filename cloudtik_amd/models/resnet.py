@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from cloudtik_amd import ops
+from cloudtik_amd.ops import conv as igemm
 from cloudtik_amd.ops.conv1x1 import conv1x1, conv3x3
 
 
@@ -93,8 +94,16 @@ class Bottleneck(nn.Module):
             self.down_bn = BatchNormAct(cout, relu=False, **kw)
 
     def forward(self, x):
-        # 1x1 convs as NHWC GEMMs on GPU; conv1 hands out an alias of x for the residual /
-        # downsample branch so its dgrad GEMM absorbs that branch's gradient (ops/conv1x1.py)
+        if igemm.ENABLED and igemm.eligible(x, self.conv1.weight, (1, 1), (0, 0)):
+            # every conv on the in-tree implicit-GEMM MFMA kernels (ops/conv.py); conv1 hands
+            # out an alias of x for the residual / downsample branch so its data-gradient
+            # epilogue absorbs that branch's gradient
+            out, x = igemm.conv2d(x, self.conv1, keep_input=True)
+            idt = self.down_bn(igemm.conv2d(x, self.down)) if self.down is not None else x
+            out = self.bn2(igemm.conv2d(self.bn1(out), self.conv2))
+            return self.bn3(igemm.conv2d(out, self.conv3), residual=idt)
+        # MIOpen path (CLOUDTIK_AMD_CONV_IGEMM=0, CPU): 1x1 convs as NHWC GEMMs, conv1's dgrad
+        # GEMM absorbs the residual branch's gradient (ops/conv1x1.py)
         out, x = conv1x1(x, self.conv1, keep_input=True)
         idt = self.down_bn(conv1x1(x, self.down)) if self.down is not None else x
         out = self.bn2(conv3x3(self.bn1(out), self.conv2))

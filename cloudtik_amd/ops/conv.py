@@ -1,0 +1,268 @@
+"""Convolutions on the in-tree implicit-GEMM MFMA kernels (csrc/conv.hip) instead of MIOpen.
+
+Why: MIOpen's immediate mode picks its solver per problem from a user find-db.  On a fresh
+node without the right records it either searches (~60 s of warm-up for ResNet-50) or falls
+back to naive kernels (25-200 ms per call); the driver measured ResNet-50 at 1,111 img/s on
+such a node against 10,149 on a warm one.  These kernels have no solver state: the same code
+runs on every box.
+
+Every convolution is planned as ``Y[m, n] = sum_t sum_c X[pixel(m) + tap_t, c] W'[n, t*Ci + c]``
+over NHWC (channels_last) bf16 tensors:
+
+* forward: row grid = output pixels, taps = (r - pad, s - pad) at input stride ``stride``;
+* data gradient, stride 1: X = dY, taps = (pad - r, pad - s), W' = W transposed to
+  [Ci][R][S][Co] (no flip needed: the tap carries the sign);
+* data gradient, stride > 1: one launch per output-pixel phase (h mod s, w mod s), with the
+  filter taps that reach that phase (a phase no tap reaches is zero-filled);
+* weight gradient: a TN implicit GEMM over the pixels (both NHWC operands are pixel-major),
+  split-K with fp32 slabs summed by ``splitk_reduce``.
+
+The forward epilogue can also emit per-tile BatchNorm statistics (``stats=True``): the
+BatchNorm that follows the conv then skips its statistics pass over the output.
+
+Parity: torchvision ``nn.Conv2d`` semantics (bias-free, groups=1, dilation=1) as the
+reference trains them (applications/ai/quickstart/models/image_recognition/pytorch/common/
+main.py:276-296); tests compare against ``F.conv2d`` in fp32.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+ENABLED = os.environ.get("CLOUDTIK_AMD_CONV_IGEMM", "1") == "1"
+_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_CFG", "-1"))
+
+
+def _C():
+    from cloudtik_amd import ops
+    return ops.require_native()
+
+
+def eligible(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation=(1, 1), groups=1) -> bool:
+    """Shapes the kernels take: NHWC bf16 on GPU, Ci and Co multiples of 64, taps within
+    [-8, 7], at most 16 taps per launch."""
+    if not (ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    co, ci, R, S = w.shape
+    if groups != 1 or tuple(dilation) != (1, 1) or ci % 64 or co % 64 or R * S > 16 or x.shape[1] != ci:
+        return False
+    ph, pw = padding
+    if max(R - 1 - ph, S - 1 - pw, ph, pw) > 7:
+        return False
+    return x.is_contiguous(memory_format=torch.channels_last)
+
+
+def out_size(h, k, s, p):
+    return (h + 2 * p - k) // s + 1
+
+
+# ------------------------------------------------------------------ plans
+def fwd_plan(x_shape, w_shape, stride, padding):
+    N, ci, H, W = x_shape
+    co, _, R, S = w_shape
+    sh, sw = stride
+    ph, pw = padding
+    Ho, Wo = out_size(H, R, sh, ph), out_size(W, S, sw, pw)
+    taps = []
+    for r in range(R):
+        for s in range(S):
+            taps += [r - ph, s - pw]
+    geo = [Ho, Wo, sh, sw, Ho, Wo, 1, 1, 0, 0, co, N * Ho * Wo]
+    return geo, taps, (N, co, Ho, Wo)
+
+
+def weight_rows(w: torch.Tensor) -> torch.Tensor:
+    """[Co, R*S*Ci] rows of a conv weight (a view when the weight is channels_last)."""
+    co = w.shape[0]
+    return w.permute(0, 2, 3, 1).reshape(co, -1)
+
+
+def dgrad_phases(x_shape, w_shape, stride, padding):
+    """Per output-pixel phase (a, b) of dX: (row-grid size, taps (dy, dx) into dY, filter taps (r, s))."""
+    N, ci, H, W = x_shape
+    co, _, R, S = w_shape
+    sh, sw = stride
+    ph, pw = padding
+    out = []
+    for a in range(sh):
+        for b in range(sw):
+            Hr, Wr = (H - a + sh - 1) // sh, (W - b + sw - 1) // sw
+            if Hr <= 0 or Wr <= 0:
+                continue
+            taps, rs = [], []
+            for r in range(R):
+                if (a + ph - r) % sh:
+                    continue
+                for s in range(S):
+                    if (b + pw - s) % sw:
+                        continue
+                    taps += [(a + ph - r) // sh, (b + pw - s) // sw]
+                    rs.append((r, s))
+            out.append(((a, b), (Hr, Wr), taps, rs))
+    return out
+
+
+# ------------------------------------------------------------------ launches
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), padding=(0, 0), out: Optional[torch.Tensor] = None,
+             accumulate: bool = False, stats: bool = False):
+    """Y = conv2d(x, w) (NHWC bf16).  With ``stats`` also returns (mean, biased var) per output
+    channel of the bf16 Y, from the epilogue's tile partials."""
+    geo, taps, shape = fwd_plan(x.shape, w.shape, tuple(stride), tuple(padding))
+    N, co, Ho, Wo = shape
+    if out is None:
+        out = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
+    C = _C()
+    part = None
+    if stats:
+        bm = C.conv_igemm_tile_m(_CFG, co, geo[11], len(taps) // 2 * (x.shape[1] // 64))
+        part = torch.empty(((geo[11] + bm - 1) // bm) * 2 * co, device=x.device, dtype=torch.float32)
+    ok = C.conv_igemm(x, weight_rows(w).contiguous(), out, geo, taps, accumulate, part, _CFG)
+    if not ok:
+        raise RuntimeError(f"conv_igemm rejected x{tuple(x.shape)} w{tuple(w.shape)} s{stride} p{padding}")
+    if not stats:
+        return out
+    mean = torch.empty(co, device=x.device, dtype=torch.float32)
+    var = torch.empty_like(mean)
+    C.bn_partials_finalize(part, bm, geo[11], mean, var)
+    return out, mean, var
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), padding=(0, 0),
+               out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """dX of conv2d(x, w) for the NHWC bf16 gradient dy; ``accumulate`` adds into ``out``."""
+    N, ci, H, W = x_shape
+    co, _, R, S = w.shape
+    phases = dgrad_phases(x_shape, w.shape, tuple(stride), tuple(padding))
+    empty_phase = any(not rs for _, _, _, rs in phases)
+    if out is None:
+        out = torch.empty((N, ci, H, W), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        if empty_phase and not accumulate:
+            out.zero_()
+    elif empty_phase and not accumulate:
+        out.zero_()
+    C = _C()
+    wt = w.permute(1, 2, 3, 0)                      # [Ci, R, S, Co]
+    sh, sw = stride
+    for (a, b), (Hr, Wr), taps, rs in phases:
+        if not rs:
+            continue
+        if len(rs) == R * S:
+            wm = wt.reshape(ci, -1).contiguous()
+        else:
+            wm = torch.stack([wt[:, r, s, :] for r, s in rs], 1).reshape(ci, -1).contiguous()
+        geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
+        if not C.conv_igemm(dy, wm, out, geo, taps, accumulate, None, _CFG):
+            raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)} w{tuple(w.shape)}")
+    return out
+
+
+_WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
+_WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256)}
+PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
+
+
+def wgrad_plan(M: int, co: int, nn: int, cfg: int):
+    """(splits, rows per split): about 2048 workgroups, each split a multiple of 32 pixels
+    and at least 256 deep, the fp32 partials capped at PARTIAL_BYTES."""
+    bm, bn = _WG_TILES[cfg]
+    tiles = (co // bm) * (nn // bn)
+    splits = max(1, min(512 // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
+    rows = ((M + splits - 1) // splits + 31) // 32 * 32
+    return (M + rows - 1) // rows, rows
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=(1, 1), padding=(0, 0),
+               out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """dW of conv2d(x, w) (NHWC bf16 dy, x) as a channels_last bf16 [Co, Ci, R, S] tensor;
+    ``out`` (same memory layout, e.g. a flat-buffer gradient view) receives it, added when
+    ``accumulate``."""
+    co, ci, R, S = w_shape
+    taps = []
+    for r in range(R):
+        for s in range(S):
+            taps += [r - padding[0], s - padding[1]]
+    nn = R * S * ci
+    M = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    C = _C()
+    cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
+    splits, rows = wgrad_plan(M, co, nn, cfg)
+    part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)
+    if not C.conv_wgrad(dy, x, part, taps, [stride[0], stride[1], rows], splits, cfg):
+        raise RuntimeError(f"conv_wgrad rejected dy{tuple(dy.shape)} x{tuple(x.shape)} w{tuple(w_shape)}")
+    if out is None:
+        out = torch.empty(w_shape, device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        accumulate = False
+    flat = out.permute(0, 2, 3, 1).reshape(-1) if out.dim() == 4 else out.reshape(-1)
+    if splits <= 16:
+        C.splitk_reduce(part.view(splits, -1), flat, accumulate)
+    else:                                   # many slabs: parallel over the slabs too
+        C.splitk_reduce_wide(part, splits, flat, accumulate)
+    return out
+
+
+def _weight_grad(wp, dy, x, w_shape, stride, padding):
+    """dW.  When the weight lives in a flat gradient buffer (train.optim.FlatParamSpace) and the
+    gradient side stream is on, the split-K reduce ADDS it straight into its buffer slice on the
+    side stream (returns None: autograd never sees it, the data-parallel bucketer is told through
+    ``_ct_grad_ready``); otherwise it is returned for AccumulateGrad."""
+    from cloudtik_amd.ops.conv1x1 import _SIDE_WGRAD, _flat_target
+    from cloudtik_amd.ops.linear import grad_stream
+    target = _flat_target(wp) if _SIDE_WGRAD else None
+    side = grad_stream() if target is not None else None
+    if target is None or not target.is_contiguous(memory_format=torch.channels_last) or target.dtype != dy.dtype:
+        return conv_wgrad(dy, x, w_shape, stride, padding)
+    if side is None:
+        conv_wgrad(dy, x, w_shape, stride, padding, out=target, accumulate=True)
+    else:
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            conv_wgrad(dy, x, w_shape, stride, padding, out=target, accumulate=True)
+        dy.record_stream(side)
+        x.record_stream(side)
+    cb = getattr(wp, "_ct_grad_ready", None)
+    if cb is not None:
+        cb(wp)
+    return None
+
+
+class ConvFn(torch.autograd.Function):
+    """conv2d on the implicit-GEMM kernels.  ``keep_input`` also returns an alias of x for the
+    block's other consumer (the residual / downsample branch): autograd then sees x used once
+    and the data gradient of this conv is accumulated INTO the other branch's gradient by the
+    kernel's epilogue (no separate add pass)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, padding, keep_input):
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.padding = stride, padding
+        ctx.wp = w
+        y = conv_fwd(x, w, stride, padding)
+        return (y, x.view_as(x)) if keep_input else y
+
+    @staticmethod
+    def backward(ctx, dy, dx_other=None):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if (dx_other is not None and not torch.is_grad_enabled() and dx_other.dtype == dy.dtype
+                    and dx_other.is_contiguous(memory_format=torch.channels_last)):
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding, out=dx_other, accumulate=True)
+            else:
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding)
+                if dx_other is not None:
+                    dx = dx + dx_other
+        if ctx.needs_input_grad[1]:
+            dw = _weight_grad(ctx.wp, dy, x, tuple(w.shape), ctx.stride, ctx.padding)
+        return dx, dw, None, None, None
+
+
+def conv2d(x: torch.Tensor, conv: torch.nn.Conv2d, keep_input: bool = False):
+    """``conv(x)`` on the implicit-GEMM kernels when eligible, else ``conv(x)``; with
+    ``keep_input`` returns ``(conv(x), x_alias)`` (see ConvFn)."""
+    if conv.bias is not None or not eligible(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups):
+        return (conv(x), x) if keep_input else conv(x)
+    return ConvFn.apply(x, conv.weight, tuple(conv.stride), tuple(conv.padding), keep_input)

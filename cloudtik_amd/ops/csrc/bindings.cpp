@@ -541,6 +541,7 @@ void register_graph(pybind11::module& m); // bindings_graph.cpp
 void register_deform(pybind11::module& m); // bindings_deform.cpp
 void register_p2p(pybind11::module& m);    // bindings_p2p.cpp
 void register_lt(pybind11::module& m);     // bindings_lt.cpp
+void register_conv(pybind11::module& m);   // bindings_conv.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "cloudtik_amd CDNA4 (gfx950) op library";
@@ -549,6 +550,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_deform(m);
   register_p2p(m);
   register_lt(m);
+  register_conv(m);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);

@@ -1,0 +1,116 @@
+// Bindings for the implicit-GEMM convolution kernels (csrc/conv.hip).  Shapes, layouts and
+// alignment are validated here; the plan (row grid, taps, output addressing) comes from
+// ops/conv.py.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+#include <vector>
+
+extern "C" {
+int ct_conv_igemm(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
+                  int, int, int, int, const int*, int, float*, int, hipStream_t);
+int ct_conv_igemm_rows(int, int, int, int);
+int ct_conv_igemm_tile_m(int);
+int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
+int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
+                  int, int, hipStream_t);
+int ct_conv_wgrad_cfg(int, int, int);
+int ct_splitk_reduce_wide(const float*, int, long, void*, int, float*, hipStream_t);
+}
+
+// X: NHWC-dense bf16 [Nb, Hi, Wi, Ci] (any logical NCHW/NHWC view whose memory is NHWC);
+// W: [Co, T*Ci] bf16 row-major; Y: bf16 memory written at the planned addresses.
+// geo = {Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, M}; taps = {dy0, dx0, dy1, dx1, ...}.
+// part (optional, fp32 [tiles, 2, Co]) receives per-tile BatchNorm (mean, M2) of Y.
+bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> geo, std::vector<int64_t> taps,
+                bool accumulate, c10::optional<at::Tensor> part, int64_t cfg) {
+  TORCH_CHECK(X.is_cuda() && W.is_cuda() && Y.is_cuda(), "conv_igemm: GPU tensors");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 && Y.scalar_type() == at::kBFloat16,
+              "conv_igemm: bf16 tensors");
+  TORCH_CHECK(X.dim() == 4 && X.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm: X must be NHWC-dense");
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "conv_igemm: W must be [Co, T*Ci] row-major");
+  TORCH_CHECK(geo.size() == 12 && taps.size() % 2 == 0, "conv_igemm: plan");
+  const int Ci = (int)X.size(1), Hi = (int)X.size(2), Wi = (int)X.size(3);
+  const int T = (int)taps.size() / 2, Co = (int)W.size(0);
+  TORCH_CHECK(W.size(1) == (int64_t)T * Ci, "conv_igemm: W columns != taps * Ci");
+  const long M = geo[11];
+  // every output address the plan produces must lie inside Y (checked on the host before launch)
+  const long Nb = X.size(0);
+  TORCH_CHECK(M > 0 && M <= Nb * geo[0] * geo[1], "conv_igemm: rows exceed the row grid");
+  const long last_y = (geo[0] - 1) * geo[6] + geo[8], last_x = (geo[1] - 1) * geo[7] + geo[9];
+  TORCH_CHECK(geo[8] >= 0 && geo[9] >= 0 && last_y < geo[4] && last_x < geo[5], "conv_igemm: output grid");
+  TORCH_CHECK((((Nb - 1) * geo[4] + last_y) * geo[5] + last_x) * geo[10] + Co <= Y.numel(), "conv_igemm: Y too small");
+  std::vector<int> tp(taps.begin(), taps.end());
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    const int cfg_r = ct_conv_igemm_rows((int)cfg, Co, (int)M, T * (Ci / 64));
+    const int bm = ct_conv_igemm_tile_m(cfg_r);
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                part->numel() >= (M + bm - 1) / bm * 2 * Co, "conv_igemm: part buffer");
+    pp = part->data_ptr<float>();
+  }
+  const int rc = ct_conv_igemm(X.data_ptr(), Hi, Wi, Ci, W.data_ptr(), Y.data_ptr(), (int)geo[0], (int)geo[1],
+                               (int)geo[2], (int)geo[3], (int)geo[4], (int)geo[5], (int)geo[6], (int)geo[7],
+                               (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), accumulate ? 1 : 0, pp,
+                               (int)cfg, at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
+int64_t conv_igemm_tile_m(int64_t cfg, int64_t Co, int64_t M, int64_t KT) {
+  return ct_conv_igemm_tile_m(ct_conv_igemm_rows((int)cfg, (int)Co, (int)M, (int)KT));
+}
+
+void bn_partials_finalize(at::Tensor part, int64_t rows_per_tile, int64_t M, at::Tensor mean, at::Tensor var) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(), "bn_partials_finalize");
+  const int C = (int)mean.numel();
+  const int tiles = (int)((M + rows_per_tile - 1) / rows_per_tile);
+  TORCH_CHECK(part.numel() >= (long)tiles * 2 * C && var.numel() == C && mean.scalar_type() == at::kFloat &&
+              var.scalar_type() == at::kFloat && mean.is_contiguous() && var.is_contiguous(), "bn_partials_finalize");
+  TORCH_CHECK(ct_bn_partials_finalize(part.data_ptr<float>(), tiles, (int)rows_per_tile, (int)M, C,
+                                      mean.data_ptr<float>(), var.data_ptr<float>(),
+                                      at::hip::getCurrentHIPStream().stream()) == 0, "bn_partials_finalize launch");
+}
+
+// fp32 partials P[splits, Co, T*Ci] of the weight gradient; DY: NHWC-dense [Nb, Co, Hr, Wr]
+// (the conv output grid), X: NHWC-dense input.  geo = {sy, sx, rows_per_split}.
+bool conv_wgrad(at::Tensor DY, at::Tensor X, at::Tensor P, std::vector<int64_t> taps, std::vector<int64_t> geo,
+                int64_t splits, int64_t cfg) {
+  TORCH_CHECK(DY.is_cuda() && X.is_cuda() && P.is_cuda(), "conv_wgrad: GPU tensors");
+  TORCH_CHECK(DY.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16 && P.scalar_type() == at::kFloat,
+              "conv_wgrad: dtypes");
+  TORCH_CHECK(DY.dim() == 4 && X.dim() == 4 && DY.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              X.is_contiguous(at::MemoryFormat::ChannelsLast) && P.is_contiguous(), "conv_wgrad: layouts");
+  TORCH_CHECK(geo.size() == 3 && taps.size() % 2 == 0 && DY.size(0) == X.size(0), "conv_wgrad: plan");
+  const int T = (int)taps.size() / 2, Ci = (int)X.size(1), Co = (int)DY.size(1);
+  const long M = DY.size(0) * DY.size(2) * DY.size(3);
+  TORCH_CHECK(P.numel() >= splits * (long)Co * T * Ci, "conv_wgrad: partial buffer");
+  std::vector<int> tp(taps.begin(), taps.end());
+  const int rc = ct_conv_wgrad(DY.data_ptr(), X.data_ptr(), (int)X.size(2), (int)X.size(3), Ci, (int)DY.size(2),
+                               (int)DY.size(3), (int)geo[0], (int)geo[1], Co, (int)M, T, tp.data(),
+                               P.data_ptr<float>(), (int)splits, (int)geo[2], (int)cfg,
+                               at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
+int64_t conv_wgrad_cfg(int64_t cfg, int64_t Co, int64_t NN) { return ct_conv_wgrad_cfg((int)cfg, (int)Co, (int)NN); }
+
+// out (bf16, n elements, contiguous) (+)= sum of the S fp32 slabs of P [S * n]
+void splitk_reduce_wide(at::Tensor P, int64_t S, at::Tensor out, bool accumulate) {
+  TORCH_CHECK(P.is_cuda() && P.scalar_type() == at::kFloat && P.is_contiguous(), "splitk_reduce_wide: P");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kBFloat16 && out.is_contiguous(), "splitk_reduce_wide: out");
+  const long n = out.numel();
+  TORCH_CHECK(P.numel() >= S * n, "splitk_reduce_wide: P too small");
+  auto ws = at::empty({n + (n + 1023) / 1024 + 4}, P.options());
+  TORCH_CHECK(ct_splitk_reduce_wide(P.data_ptr<float>(), (int)S, n, out.data_ptr(), accumulate ? 1 : 0,
+                                    ws.data_ptr<float>(), at::hip::getCurrentHIPStream().stream()) == 0,
+              "splitk_reduce_wide launch");
+}
+
+void register_conv(pybind11::module& m) {
+  m.def("splitk_reduce_wide", &splitk_reduce_wide, "sum of many fp32 split-K slabs into bf16 (+=)");
+  m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient: fp32 split-K partials");
+  m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
+  m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
+  m.def("conv_igemm_tile_m", &conv_igemm_tile_m, "rows per tile of the chosen conv configuration");
+  m.def("bn_partials_finalize", &bn_partials_finalize, "Chan merge of per-tile (mean, M2) -> mean, var");
+}

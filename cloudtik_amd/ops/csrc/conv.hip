@@ -1,0 +1,646 @@
+// Implicit-GEMM convolution over NHWC bf16 activations for gfx950 (MFMA 16x16x32, fp32 acc).
+//
+// One kernel family serves every convolution of the ResNet family that is not a plain GEMM:
+//     Y[m, n] = sum_{t < T, c < Ci} X[pixel(m) + tap(t), c] * W[n, t * Ci + c]
+// where row m walks a "row grid" (b, y, x) and tap t adds a (dy, dx) pixel offset:
+//   * forward conv:            row grid = output pixels, pixel = (y*sy, x*sx), taps = (r - pad, s - pad);
+//   * data gradient, stride 1: X = dY, taps = (pad - r, pad - s), W = the flipped, transposed filter;
+//   * data gradient, stride 2: one launch per output-pixel parity class, row grid = that class,
+//                              taps = the filter taps that reach it (ops/conv.py builds the plan).
+// Out-of-image taps read a zero page, so padding costs no branch in the K loop.
+//
+// Structure (MI355X_MICROARCH.md / cdna_hip_programming.md §5):
+//   * BM x BN output tile per workgroup, K walked 64 channels of one tap at a time (BK = 64);
+//   * both operands staged global -> LDS with global_load_lds_dwordx4 (16 B per lane): each
+//     A row is one pixel's 64 channels (128 B) -- a per-lane gathered address, which is what
+//     LDS-DMA allows (the LDS side is lane-linear, the global side is per lane); the 16-B
+//     chunks of a row are XOR-swizzled on the SOURCE side so ds_read_b128 fragment reads are
+//     conflict-free;
+//   * an NS-slot LDS ring with NS-1 stages in flight, a counted vmcnt and one raw s_barrier per
+//     K-step (the DMA spans the barrier; one stage in flight is latency-bound);
+//   * blockIdx -> tile through the bijective XCD remap with N-tiles fastest, so the blocks that
+//     share an A panel (the expensive gathered operand) run on one XCD's L2;
+//   * epilogue: the bf16 tile is re-laid through LDS so each lane stores 16 contiguous bytes
+//     (whole rows per wave), optional accumulate (Y += result), and optionally the per-tile
+//     BatchNorm statistics of
+//     the bf16 output (mean and M2 per channel over the tile's rows, merged by Chan's formula
+//     in ct_bn_partials_finalize) -- the separate statistics pass over the conv output goes away.
+// Reference workload: torchvision ResNet-50 training, channels_last bf16
+// (applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296).
+#include "common.h"
+
+namespace ct {
+
+typedef __attribute__((ext_vector_type(8))) short cv_s16x8;
+typedef __attribute__((address_space(3))) cv_s16x8 cv_lds_s16x8;
+typedef __attribute__((address_space(3))) void cv_lds_void;
+
+__device__ __attribute__((aligned(256))) uint32_t cv_zero_page[64];   // zero-initialised: OOB source
+
+constexpr int CV_MAXT = 16;
+
+struct ConvArgs {
+  const bf16_t* X;      // gathered operand, NHWC [Nb, Hi, Wi, Ci]
+  const bf16_t* W;      // [Co][T * Ci], k contiguous
+  bf16_t* Y;            // output
+  float* part;          // EPI 1: [mtiles][2][Co] per-tile (mean, M2)
+  int Hi, Wi, Ci;
+  int Hr, Wr;           // row grid: m = (b * Hr + y) * Wr + x
+  int sy, sx;           // input pixel = (y * sy + dy_t, x * sx + dx_t)
+  int Ho, Wo, oys, oxs, oy0, ox0, ldy;   // output pixel = (y * oys + oy0, x * oxs + ox0), row stride ldy
+  int Co, M, T;
+  int accumulate;
+  unsigned long long tdy, tdx;           // 16 taps x 4 bits, biased by 8
+};
+
+__device__ __forceinline__ int cv_swz(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void cv_glds16(const void* g, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(cv_lds_void*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
+}
+
+__device__ __forceinline__ cv_s16x8 cv_frag(const char* img, int r0, int ks, int lane) {
+  const int row = r0 + (lane & 15);
+  const int kc = ks * 4 + (lane >> 4);
+  return *(const cv_lds_s16x8*)(img + row * 128 + ((kc ^ cv_swz(row)) << 4));
+}
+
+__device__ __forceinline__ void cv_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void cv_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `rem` later stages (G glds each) are outstanding
+template <int G, int NS>
+__device__ __forceinline__ void cv_wait_stage(int rem) {
+  if constexpr (NS >= 4) {
+    if (rem >= 2) { cv_vm<2 * G>(); return; }
+  }
+  if constexpr (NS >= 3) {
+    if (rem >= 1) { cv_vm<G>(); return; }
+  }
+  cv_vm<0>();
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int MINB, int EPI>
+__global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int IA = BM / (8 * NW), IB = BN / (8 * NW), G = IA + IB;
+  static_assert(IA * 8 * NW == BM && IB * 8 * NW == BN, "tile / wave mismatch");
+  static_assert(NS >= 2 && NS <= 4 && NS * STAGE <= 160 * 1024, "LDS ring");
+  __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE];   // the only LDS object
+
+  const int ntn = a.Co / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = L / ntn, tn = L % ntn;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int HW = a.Hr * a.Wr;
+
+  // ---- per-lane gather descriptors: the A rows this lane stages (fixed for the whole K loop)
+  int pix[IA], iy0[IA], ix0[IA];
+  unsigned gca[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = (wave * IA + j) * 8 + (lane >> 3);
+    const int m = m0 + row;
+    gca[j] = (unsigned)((lane & 7) ^ cv_swz(row)) * 8u;
+    if (m < a.M) {
+      const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+      iy0[j] = y * a.sy;
+      ix0[j] = x * a.sx;
+      pix[j] = ((b * a.Hi + iy0[j]) * a.Wi + ix0[j]) * a.Ci;
+    } else {
+      iy0[j] = -(1 << 20);
+      ix0[j] = 0;
+      pix[j] = 0;
+    }
+  }
+  const long ldw = (long)a.T * a.Ci;
+  const bf16_t* wrow[IB];
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int row = (wave * IB + j) * 8 + (lane >> 3);
+    wrow[j] = a.W + (long)(n0 + row) * ldw + ((lane & 7) ^ cv_swz(row)) * 8;
+  }
+  const int cpt = a.Ci >> 6;                // 64-channel chunks per tap
+  const int KT = a.T * cpt;
+
+  auto stage = [&](int kt, int slot) {
+    const int t = kt / cpt, c0 = (kt - t * cpt) << 6;
+    const int dy = (int)((a.tdy >> (4 * t)) & 15) - 8, dx = (int)((a.tdx >> (4 * t)) & 15) - 8;
+    const int toff = (dy * a.Wi + dx) * a.Ci + c0;
+    char* As = lds + slot * STAGE;
+    char* Bs = As + BM * 128;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int iy = iy0[j] + dy, ix = ix0[j] + dx;
+      const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      const void* src = ok ? (const void*)(a.X + (long)(pix[j] + toff) + gca[j]) : (const void*)cv_zero_page;
+      cv_glds16(src, As + (wave * IA + j) * 1024);
+    }
+    const long k0 = (long)t * a.Ci + c0;
+#pragma unroll
+    for (int j = 0; j < IB; ++j) cv_glds16(wrow[j] + k0, Bs + (wave * IB + j) * 1024);
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < KT) stage(s, s);
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = KT - 1 - kt;          // stages issued after kt (capped by the ring)
+    cv_wait_stage<G, NS>(ahead < NS - 2 ? ahead : NS - 2);
+    cv_bar();
+    if (kt + NS - 1 < KT) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* As = lds + (kt % NS) * STAGE;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      cv_s16x8 fa[MI], fb[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = cv_frag(As, wm * WM + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = cv_frag(Bs, wn * WN + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb[j], (bf16x8_t)fa[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue.  acc[i][j][r] = Y[row wm*WM + 16 i + (lane & 15)][col wn*WN + 16 j + 4 (lane >> 4) + r]
+  // of the tile.  The bf16 tile goes through LDS so that every lane then stores 16 contiguous
+  // bytes and a wave writes whole rows: 8-byte stores of the MFMA layout (4 channels of 16
+  // rows per instruction) made the epilogue store-issue-bound.
+  constexpr int OROW = BN * 2 + 16;                // padded LDS row: 2-way at most on the b64 writes
+  static_assert(BM * OROW + WGM * BN * 4 <= NS * STAGE, "epilogue LDS");
+  char* ot = lds;
+  float* red = (float*)(lds + BM * OROW);          // [WGM][BN] statistics scratch
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  cv_bar();                                        // every wave is done reading the ring
+  bool rv[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int row = wm * WM + 16 * i + (lane & 15);
+    rv[i] = m0 + row < a.M;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      u16x4 out;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        out[r] = f2bf(acc[i][j][r]);
+        if constexpr (EPI == 1) acc[i][j][r] = rv[i] ? bf2f(out[r]) : 0.f;   // what BatchNorm will read
+      }
+      *(u16x4*)(ot + row * OROW + (wn * WN + 16 * j + 4 * (lane >> 4)) * 2) = out;
+    }
+  }
+  if constexpr (EPI == 1) {
+    // per-tile column mean and M2 from the registers (two passes: numerically like Welford)
+    const int nrows = min(BM, a.M - m0);
+    float cs[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) v += acc[i][j][r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
+      }
+    __syncthreads();
+    float mean[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
+        float sum = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) sum += red[w * BN + c];
+        mean[j][r] = sum / (float)nrows;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const float d = acc[i][j][r] - mean[j][r];
+          q += rv[i] ? d * d : 0.f;
+        }
+        cs[j][r] = q;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cs[j][r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
+      }
+    __syncthreads();
+    if (wm == 0 && (lane & 15) == 0) {
+      float* pm = a.part + (long)tm * 2 * a.Co;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
+          float q = 0.f;
+#pragma unroll
+          for (int w = 0; w < WGM; ++w) q += red[w * BN + c];
+          pm[n0 + c] = mean[j][r];
+          pm[a.Co + n0 + c] = q;
+        }
+    }
+  }
+  __syncthreads();
+  // coalesced copy-out: row-major 16-B chunks, BN / 8 lanes per row
+  constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;
+  const int cc = tid % CPR;
+#pragma unroll 4
+  for (int row = tid / CPR; row < BM; row += RPP) {
+    const int m = m0 + row;
+    if (m >= a.M) break;
+    const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+    bf16_t* yp = a.Y + ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+    u16x8 v = *(const u16x8*)(ot + row * OROW + cc * 16);
+    if (a.accumulate) {
+      const u16x8 old = *(const u16x8*)yp;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(old[e]));
+    }
+    *(u16x8*)yp = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight gradient: dW[co][t * Ci + c] = sum_m dY[m][co] * X[pixel(m) + tap_t][c]
+// a "TN" GEMM whose reduction runs over the pixels (the row index of both NHWC operands):
+//   * BK = 32 pixels per stage; both tiles are staged row-major ([pixel][channel], as in memory)
+//     by LDS-DMA and the MFMA fragments, which need 8 consecutive pixels per lane, are read with
+//     ds_read_b64_tr_b16 (the transposing LDS read) -- no transpose pass;
+//   * the X tile is gathered per 16-byte chunk: the chunk's column fixes its tap, the row fixes
+//     the pixel, tracked incrementally per lane (+32 pixels per stage) instead of divided out;
+//   * split-K over pixel ranges (the output is small, the reduction is up to 800k pixels deep);
+//     fp32 partial slabs [split][co][t * Ci + c] are summed by ct_splitk_reduce.
+struct WgradArgs {
+  const bf16_t* DY;     // [M][Co]
+  const bf16_t* X;      // NHWC [Nb, Hi, Wi, Ci]
+  float* P;             // [splits][Co][NN]
+  int Hi, Wi, Ci, Hr, Wr, sy, sx;
+  int Co, NN, M, T, rows_per_split;
+  unsigned long long tdy, tdx;
+};
+
+template <int LPR>
+__device__ __forceinline__ int wg_swz(int r) {
+  if constexpr (LPR == 8) return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+  else return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
+}
+
+typedef __attribute__((ext_vector_type(4))) short wg_s16x4;
+typedef __attribute__((address_space(3))) wg_s16x4 wg_lds_s16x4;
+
+// 16 columns [col0, col0 + 16) x 32 pixels of a row-major image with ROWB-byte rows: lane l gets
+// column (l & 15), pixels 8 (l >> 4) .. + 8
+template <int ROWB>
+__device__ __forceinline__ cv_s16x8 wg_frag(const char* img, int col0, int lane) {
+  constexpr int LPR = ROWB / 16;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 8 * g + q, r1 = r0 + 4;
+  const int ch = (col0 >> 3) + (p >> 1);
+  const char* a0 = img + r0 * ROWB + ((ch ^ wg_swz<LPR>(r0)) << 4) + ((p & 1) << 3);
+  const char* a1 = img + r1 * ROWB + ((ch ^ wg_swz<LPR>(r1)) << 4) + ((p & 1) << 3);
+  const wg_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((wg_lds_s16x4*)a0);
+  const wg_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((wg_lds_s16x4*)a1);
+  return cv_s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BMC, int BNC, int WGM, int WGN, int NS>
+__global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs a) {
+  constexpr int NW = WGM * WGN, BK = 32;
+  constexpr int ROWA = BMC * 2, ROWB = BNC * 2, LPA = ROWA / 16, LPB = ROWB / 16;
+  constexpr int TA = BK * ROWA, TB = BK * ROWB, STG = TA + TB;
+  constexpr int GA = TA / (1024 * NW), GB = TB / (1024 * NW), G = GA + GB;
+  constexpr int RPA = 64 / LPA, RPB = 64 / LPB;          // rows per DMA instruction
+  constexpr int WM = BMC / WGM, WN = BNC / WGN, MI = WM / 16, NJ = WN / 16;
+  static_assert(GA * 1024 * NW == TA && GB * 1024 * NW == TB, "wgrad tile / waves");
+  static_assert(NS * STG <= 160 * 1024 && NS >= 2 && NS <= 4, "wgrad ring");
+  __shared__ __attribute__((aligned(1024))) char lds[NS * STG];
+
+  const int tiles_n = a.NN / BNC, tiles = (a.Co / BMC) * tiles_n;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, tile = L % tiles;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int c0 = tm * BMC, n0 = tn * BNC;
+  const int kbeg = split * a.rows_per_split;
+  const int kend = min(a.M, kbeg + a.rows_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  // A rows (dY): row r of the stage = pixel kbeg + 32 s + r; fixed column chunk per instruction
+  int ra[GA];
+  unsigned ga_off[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int r = (wave * GA + j) * RPA + lane / LPA;
+    ra[j] = r;
+    ga_off[j] = (unsigned)(c0 + (((lane % LPA) ^ wg_swz<LPA>(r)) << 3));
+  }
+  // B rows (gathered X): per instruction the lane's chunk column -> tap, channel; the pixel
+  // (b, y, x) of its row is tracked incrementally
+  int rb[GB], bb[GB], yb[GB], xb[GB], dyb[GB], dxb[GB], cib[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int r = (wave * GB + j) * RPB + lane / LPB;
+    rb[j] = r;
+    const int n = n0 + (((lane % LPB) ^ wg_swz<LPB>(r)) << 3);
+    const int t = n / a.Ci;
+    cib[j] = n - t * a.Ci;
+    dyb[j] = (int)((a.tdy >> (4 * t)) & 15) - 8;
+    dxb[j] = (int)((a.tdx >> (4 * t)) & 15) - 8;
+    const int m = kbeg + r, HW = a.Hr * a.Wr;
+    bb[j] = m / HW;
+    const int rem = m - bb[j] * HW;
+    yb[j] = rem / a.Wr;
+    xb[j] = rem - yb[j] * a.Wr;
+  }
+
+  auto stage = [&](int s, int slot) {
+    char* As = lds + slot * STG;
+    char* Bs = As + TA;
+    const int kb = kbeg + s * BK;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int m = kb + ra[j];
+      const void* src = m < kend ? (const void*)(a.DY + (long)m * a.Co + ga_off[j]) : (const void*)cv_zero_page;
+      cv_glds16(src, As + (wave * GA + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int m = kb + rb[j];
+      const int iy = yb[j] * a.sy + dyb[j], ix = xb[j] * a.sx + dxb[j];
+      const bool ok = m < kend && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      const void* src = ok ? (const void*)(a.X + ((long)(bb[j] * a.Hi + iy) * a.Wi + ix) * a.Ci + cib[j])
+                           : (const void*)cv_zero_page;
+      cv_glds16(src, Bs + (wave * GB + j) * 1024);
+      // advance this row's pixel by one stage (BK pixels)
+      int x = xb[j] + BK, y = yb[j], b = bb[j];
+      while (x >= a.Wr) { x -= a.Wr; ++y; }
+      while (y >= a.Hr) { y -= a.Hr; ++b; }
+      xb[j] = x; yb[j] = y; bb[j] = b;
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = nk - 1 - kt;
+    cv_wait_stage<G, NS>(ahead < NS - 2 ? ahead : NS - 2);
+    cv_bar();
+    if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* As = lds + (kt % NS) * STG;
+    const char* Bs = As + TA;
+    cv_s16x8 fa[MI], fb[NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = wg_frag<ROWA>(As, wm * WM + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) fb[j] = wg_frag<ROWB>(Bs, wn * WN + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb[j], (bf16x8_t)fa[i], acc[i][j], 0, 0, 0);
+  }
+  // acc[i][j][r] = dW[c0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]
+  float* P = a.P + (long)split * a.Co * a.NN;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const long row = c0 + wm * WM + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      *(f32x4*)(P + row * a.NN + n0 + wn * WN + 16 * j + 4 * (lane >> 4)) = acc[i][j];
+  }
+}
+
+template <int BMC, int BNC, int WGM, int WGN, int NS>
+static int wg_launch(const WgradArgs& a, int splits, hipStream_t s) {
+  const long blocks = (long)(a.Co / BMC) * (a.NN / BNC) * splits;
+  if (blocks > (1L << 30)) return 5;
+  conv_wgrad_kernel<BMC, BNC, WGM, WGN, NS><<<(int)blocks, 64 * WGM * WGN, 0, s>>>(a);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+// Chan merge of per-tile (mean, M2) partials -> per-channel mean and biased variance, in
+// fp64 (tiles x channels is small).  One thread per channel.
+__global__ void bn_partials_finalize_kernel(const float* __restrict__ part, int tiles, int rows_per_tile, int M,
+                                            int C, float* __restrict__ mean_out, float* __restrict__ var_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int t = 0; t < tiles; ++t) {
+    const double nb = (double)min(rows_per_tile, M - t * rows_per_tile);
+    const double mb = part[(long)t * 2 * C + c], qb = part[(long)t * 2 * C + C + c];
+    const double nn = n + nb, d = mb - mean;
+    mean += d * nb / nn;
+    m2 += qb + d * d * n * nb / nn;
+    n = nn;
+  }
+  mean_out[c] = (float)mean;
+  var_out[c] = (float)(m2 / n);
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int MINB>
+static int cv_launch(const ConvArgs& a, int epi, hipStream_t s) {
+  const long tiles = (long)ceil_div(a.M, BM) * (a.Co / BN);
+  if (tiles > (1L << 30)) return 5;
+  if (epi == 1)
+    conv_igemm_kernel<BM, BN, WGM, WGN, NS, MINB, 1><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(a);
+  else
+    conv_igemm_kernel<BM, BN, WGM, WGN, NS, MINB, 0><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(a);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+}  // namespace ct
+
+using namespace ct;
+
+// tile configurations (BM x BN, waves, LDS ring slots, workgroups per CU):
+//   0: 256x64  4w NS3      1: 256x128 8w NS3      2: 128x128 4w NS4      3: 128x64 4w NS4
+//   4: 256x64  4w NS2 x2   5: 128x128 4w NS2 x2   6: 256x64  8w NS3      7: 128x64 4w NS2 x2
+//   8: 128x64  4w NS2 x3   9: 64x128  4w NS2 x3
+// -1 = pick by shape: short reductions (<= 4 K-steps of 64) want two workgroups per CU so one
+// tile's epilogue overlaps another's loads; long ones want the deeper ring.
+extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
+  // measured on MI355X over every ResNet-50 shape at batch 256 (bench/conv_igemm_probe.py,
+  // profiles/r3/conv_igemm.md): small tiles with 2-3 workgroups per CU win everywhere; the
+  // 1-workgroup configurations (deeper ring) never do
+  (void)M;
+  (void)KT;
+  if (cfg < 0) cfg = Co % 128 ? 8 : (Co == 128 ? 9 : 5);
+  return cfg;
+}
+
+extern "C" int ct_conv_igemm_tile_m(int cfg) {
+  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : (cfg == 9 ? 64 : 128);
+}
+
+// Y = implicit-GEMM conv (see the file comment).  `taps` = T (dy, dx) pairs in [-8, 7].
+// Returns nonzero (launching nothing) on an unsupported shape.
+extern "C" int ct_conv_igemm(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
+                             int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M,
+                             int T, const int* taps, int accumulate, float* part, int cfg, hipStream_t stream) {
+  if (Ci <= 0 || Ci % 64 || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT) return 1;
+  if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 7) || ldy % 4) return 3;
+  ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
+             Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull};
+  for (int t = 0; t < T; ++t) {
+    const int dy = taps[2 * t], dx = taps[2 * t + 1];
+    if (dy < -8 || dy > 7 || dx < -8 || dx > 7) return 4;
+    a.tdy |= (unsigned long long)(dy + 8) << (4 * t);
+    a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
+  }
+  const int epi = part ? 1 : 0;
+  cfg = ct_conv_igemm_rows(cfg, Co, M, T * (Ci / 64));
+  if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9) && Co % 128) return 2;
+  switch (cfg) {
+    case 0: return cv_launch<256, 64, 4, 1, 3, 1>(a, epi, stream);
+    case 1: return cv_launch<256, 128, 4, 2, 3, 1>(a, epi, stream);
+    case 2: return cv_launch<128, 128, 2, 2, 4, 1>(a, epi, stream);
+    case 3: return cv_launch<128, 64, 2, 2, 4, 1>(a, epi, stream);
+    case 4: return cv_launch<256, 64, 4, 1, 2, 2>(a, epi, stream);
+    case 5: return cv_launch<128, 128, 2, 2, 2, 2>(a, epi, stream);
+    case 6: return cv_launch<256, 64, 8, 1, 3, 1>(a, epi, stream);
+    case 7: return cv_launch<128, 64, 2, 2, 2, 2>(a, epi, stream);
+    case 8: return cv_launch<128, 64, 2, 2, 2, 3>(a, epi, stream);
+    case 9: return cv_launch<64, 128, 1, 4, 2, 3>(a, epi, stream);
+    default: return 6;
+  }
+}
+
+extern "C" int ct_bn_partials_finalize(const float* part, int tiles, int rows_per_tile, int M, int C, float* mean,
+                                       float* var, hipStream_t stream) {
+  bn_partials_finalize_kernel<<<ceil_div(C, 256), 256, 0, stream>>>(part, tiles, rows_per_tile, M, C, mean, var);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+// Sum of S fp32 slabs [S][n] into a bf16 vector (+= when accumulate), parallel over the slabs
+// as well: block (x, y) adds slabs [32 y, 32 y + 32) of elements [1024 x, 1024 x + 1024) into an
+// fp32 accumulator with atomics (at most S / 32 adders per address), and the last block of each
+// column (arrival ticket) converts that element range to bf16.
+__global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restrict__ P, int S, long n, float* acc,
+                                                         unsigned* tickets, bf16_t* __restrict__ out, int accumulate) {
+  const long e = (long)blockIdx.x * 1024 + threadIdx.x * 4;
+  const int s0 = blockIdx.y * 32, s1 = min(S, s0 + 32);
+  if (e + 3 < n) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int s = s0; s < s1; ++s) v += *(const f32x4*)(P + (long)s * n + e);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) atomicAdd(acc + e + r, v[r]);
+  } else {
+    for (long i = e; i < n && i < e + 4; ++i) {
+      float v = 0.f;
+      for (int s = s0; s < s1; ++s) v += P[(long)s * n + i];
+      atomicAdd(acc + i, v);
+    }
+  }
+  // publish: every wave's atomics are done before the ticket (agent-scope release/acquire)
+  __shared__ unsigned last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (long i = e; i < n && i < e + 4; ++i) {
+    const float v = __hip_atomic_load(acc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[i] = f2bf(accumulate ? v + bf2f(out[i]) : v);
+  }
+}
+
+// wgrad tile configurations: 0 = 64x64 (4 waves 2x2), 1 = 64x128 (2x2), 2 = 128x128 (2x2),
+// 3 = 128x256 (8 waves 2x4); -1 = the largest that divides (Co, T*Ci)
+extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
+  if (cfg >= 0) return cfg;
+  if (Co % 128 == 0 && NN % 128 == 0) return 2;      // 128 x 128 was fastest at every such shape
+  return 0;
+}
+
+// workspace: n fp32 + ceil(n / 1024) tickets, zeroed here
+extern "C" int ct_splitk_reduce_wide(const float* P, int S, long n, void* out, int accumulate, float* ws,
+                                     hipStream_t stream) {
+  if (S < 1 || n < 1) return 1;
+  const long cols = (n + 1023) / 1024;
+  unsigned* tickets = (unsigned*)(ws + n);
+  if (hipMemsetAsync(ws, 0, n * sizeof(float) + cols * sizeof(unsigned), stream) != hipSuccess) return 7;
+  dim3 grid((unsigned)cols, (unsigned)((S + 31) / 32));
+  splitk_wide_kernel<<<grid, 256, 0, stream>>>(P, S, n, ws, tickets, (bf16_t*)out, accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+// fp32 partials P[splits][Co][T*Ci] of dW; rows_per_split must be a multiple of 32.
+extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int Ci, int Hr, int Wr, int sy, int sx,
+                             int Co, int M, int T, const int* taps, float* P, int splits, int rows_per_split, int cfg,
+                             hipStream_t stream) {
+  if (Ci <= 0 || Ci % 64 || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT || splits < 1) return 1;
+  if (rows_per_split % 32 || (long)rows_per_split * splits < M) return 2;
+  if (((uintptr_t)DY & 15) || ((uintptr_t)X & 15) || ((uintptr_t)P & 15)) return 3;
+  WgradArgs a{(const bf16_t*)DY, (const bf16_t*)X, P, Hi, Wi, Ci, Hr, Wr, sy, sx, Co, T * Ci, M, T, rows_per_split,
+              0ull, 0ull};
+  for (int t = 0; t < T; ++t) {
+    const int dy = taps[2 * t], dx = taps[2 * t + 1];
+    if (dy < -8 || dy > 7 || dx < -8 || dx > 7) return 4;
+    a.tdy |= (unsigned long long)(dy + 8) << (4 * t);
+    a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
+  }
+  cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
+  if ((cfg >= 2 && Co % 128) || (cfg == 3 && a.NN % 256) || (cfg >= 1 && a.NN % 128)) return 2;
+  switch (cfg) {
+    case 0: return wg_launch<64, 64, 2, 2, 4>(a, splits, stream);
+    case 1: return wg_launch<64, 128, 2, 2, 4>(a, splits, stream);
+    case 2: return wg_launch<128, 128, 2, 2, 4>(a, splits, stream);
+    case 3: return wg_launch<128, 256, 2, 4, 4>(a, splits, stream);
+    default: return 6;
+  }
+}

@@ -29,7 +29,9 @@ def _run(*extra):
 @pytest.mark.parametrize("zero", [False, True])
 def test_bench_two_ranks_share_one_gpu(zero):
     r = _run(*(["--zero"] if zero else []))
-    assert r["n_gpus"] == 2 and r["world_size_seen_by_rccl"] == 2 and r["backend"] == "gloo"
+    # two ranks, ONE physical GPU: n_gpus counts devices, the world size comes from a collective
+    assert r["n_gpus"] == 1 and r["world_size"] == 2 and r["backend"] == "gloo" and "note" in r
+    assert r["env"]["world_size_seen_by_collective"] == 2 and r["env"]["distinct_devices"] == 1
     assert r["dtype"] == "bf16" and r["config"]["zero1"] is zero
     assert len(r["per_rank_ms_per_step"]) == 2 and len(r["resnet50_per_rank_ms_per_step"]) == 2
     assert r["value"] > 0 and r["resnet50_images_per_sec"] > 0

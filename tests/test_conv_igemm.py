@@ -1,0 +1,150 @@
+"""Implicit-GEMM convolution plans (ops/conv.py) and kernels (csrc/conv.hip).
+
+CPU: the row-grid / tap plans are executed by a plain-PyTorch emulation of the kernel's
+addressing (gather rows by tap, zero outside the image, GEMM, scatter rows to the planned
+output pixels) and compared with F.conv2d and its autograd gradients -- this pins the plan
+logic (forward taps, stride-1 data-gradient taps, stride-2 phase decomposition) without a GPU.
+
+GPU: the HIP kernels against an fp32 reference: forward (+ BatchNorm tile statistics), data
+gradient (plain and accumulated into a residual gradient), weight gradient (split-K slabs,
+both reduce paths), and a ResNet-50 bottleneck fwd + bwd against the MIOpen path."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cloudtik_amd.ops import conv as CV
+
+
+def _emulate(X, Wm, geo, taps, Y):
+    """The kernel's addressing in PyTorch: X NCHW fp32, Wm [N, T*Ci], Y NCHW fp32 (written)."""
+    Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, M = geo
+    Nb, Ci, Hi, Wi = X.shape
+    T = len(taps) // 2
+    xs = X.permute(0, 2, 3, 1)                                  # NHWC
+    b = torch.arange(Nb).view(-1, 1, 1).expand(Nb, Hr, Wr).reshape(-1)
+    y = torch.arange(Hr).view(1, -1, 1).expand(Nb, Hr, Wr).reshape(-1)
+    x = torch.arange(Wr).view(1, 1, -1).expand(Nb, Hr, Wr).reshape(-1)
+    cols = []
+    for t in range(T):
+        iy, ix = y * sy + taps[2 * t], x * sx + taps[2 * t + 1]
+        ok = (iy >= 0) & (iy < Hi) & (ix >= 0) & (ix < Wi)
+        g = torch.zeros(b.numel(), Ci)
+        g[ok] = xs[b[ok], iy[ok], ix[ok]]
+        cols.append(g)
+    A = torch.cat(cols, 1)                                      # [M, T*Ci]
+    out = A @ Wm.t()                                            # [M, N]
+    Yn = Y.permute(0, 2, 3, 1)
+    Yn[b, y * oys + oy0, x * oxs + ox0] = out
+
+
+@pytest.mark.parametrize("k,s", [(1, 1), (3, 1), (1, 2), (3, 2), (5, 2), (7, 2)])
+def test_plans_match_conv2d_and_its_gradients(k, s):
+    torch.manual_seed(k * 10 + s)
+    N, ci, co, H = 2, 3, 5, 9
+    pad = k // 2
+    x = torch.randn(N, ci, H, H, requires_grad=True)
+    w = torch.randn(co, ci, k, k, requires_grad=True)
+    ref = F.conv2d(x, w, stride=s, padding=pad)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    # forward plan
+    geo, taps, shape = CV.fwd_plan(x.shape, w.shape, (s, s), (pad, pad))
+    Y = torch.zeros(shape)
+    _emulate(x.detach(), w.detach().permute(0, 2, 3, 1).reshape(co, -1), geo, taps, Y)
+    torch.testing.assert_close(Y, ref.detach(), rtol=1e-4, atol=1e-4)
+    # data-gradient phases
+    dX = torch.zeros_like(x)
+    wt = w.detach().permute(1, 2, 3, 0)
+    for (a, b), (Hr, Wr), tp, rs in CV.dgrad_phases(x.shape, w.shape, (s, s), (pad, pad)):
+        if not rs:
+            continue
+        wm = torch.stack([wt[:, r, q, :] for r, q in rs], 1).reshape(ci, -1)
+        _emulate(dy, wm, [Hr, Wr, 1, 1, H, H, s, s, a, b, ci, N * Hr * Wr], tp, dX)
+    torch.testing.assert_close(dX, x.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_wgrad_plan_covers_every_pixel():
+    for M in (100, 12544, 802816):
+        for co, nn, cfg in ((64, 576, 0), (512, 4608, 2), (2048, 1024, 2)):
+            splits, rows = CV.wgrad_plan(M, co, nn, cfg)
+            assert rows % 32 == 0 and splits * rows >= M and (splits - 1) * rows < M
+            assert splits * co * nn * 4 <= max(CV.PARTIAL_BYTES, co * nn * 4)
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci,co,H,k,s", [(64, 64, 14, 3, 1), (128, 256, 9, 1, 1), (64, 128, 15, 3, 2),
+                                         (256, 64, 8, 1, 2), (128, 128, 7, 3, 1), (64, 192, 11, 3, 1)])
+def test_kernels_match_fp32_reference(cuda, ci, co, H, k, s):
+    torch.manual_seed(ci + co + H)
+    pad = k // 2
+    x = _nhwc(torch.randn(3, ci, H, H, device=cuda).to(torch.bfloat16))
+    w = _nhwc((torch.randn(co, ci, k, k, device=cuda) * (2.0 / (ci * k * k)) ** 0.5).to(torch.bfloat16))
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    ref = F.conv2d(xr, wr, stride=s, padding=pad)
+    dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
+    ref.backward(dy.float())
+    y, mean, var = CV.conv_fwd(x, w, (s, s), (pad, pad), stats=True)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 1e-2
+    yb = y.float()
+    torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(var, yb.var((0, 2, 3), unbiased=False), rtol=1e-3, atol=1e-6)
+    dx = CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad))
+    assert _rel(dx, xr.grad) < 1e-2
+    other = _nhwc(torch.randn(x.shape, device=cuda).to(torch.bfloat16))
+    acc = CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad), out=other.clone(), accumulate=True)
+    assert _rel(acc, xr.grad + other.float()) < 1e-2
+    dw = CV.conv_wgrad(dy, x, w.shape, (s, s), (pad, pad))
+    assert dw.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(dw, wr.grad) < 1e-2
+    # many split-K slabs (the parallel reduce) and accumulation into an existing gradient
+    old = CV.PARTIAL_BYTES
+    try:
+        base = _nhwc(torch.randn(w.shape, device=cuda).to(torch.bfloat16))
+        dw2 = CV.conv_wgrad(dy, x, w.shape, (s, s), (pad, pad), out=base.clone(), accumulate=True)
+        assert _rel(dw2, wr.grad + base.float()) < 1e-2
+    finally:
+        CV.PARTIAL_BYTES = old
+
+
+@pytest.mark.gpu
+def test_wide_reduce_many_slabs(cuda):
+    from cloudtik_amd import ops
+    P = torch.randn(300, 5000, device=cuda)
+    out = torch.randn(5000, device=cuda).to(torch.bfloat16)
+    ref = P.sum(0) + out.float()
+    ops.require_native().splitk_reduce_wide(P.reshape(-1), 300, out, True)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("down,stride", [(True, 1), (True, 2), (False, 1)])
+def test_bottleneck_matches_miopen_path(cuda, down, stride, monkeypatch):
+    from cloudtik_amd.models.resnet import Bottleneck
+    torch.manual_seed(0)
+    cin = 64 if down else 256
+    blk = Bottleneck(cin, 64, stride, downsample=down, device=cuda, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    x0 = _nhwc(torch.randn(4, cin, 16, 16, device=cuda).to(torch.bfloat16))
+
+    def run(enabled):
+        monkeypatch.setattr(CV, "ENABLED", enabled)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+        return y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
+
+    y1, gx1, gp1 = run(True)
+    y0, gx0, gp0 = run(False)
+    assert _rel(y1, y0) < 2e-2 and _rel(gx1, gx0) < 3e-2
+    for a, b in zip(gp1, gp0):
+        assert _rel(a, b) < 3e-2
