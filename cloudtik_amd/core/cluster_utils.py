@@ -105,7 +105,22 @@ def create_updater(config: Dict[str, Any], provider, node_id: str, is_head: bool
         use_internal_ip=not is_head or config["provider"].get("use_internal_ips", False),
         docker_config=config.get("docker"), restart_only=restart_only, for_recovery=for_recovery,
         environment_variables=node_environment(config, provider, node_id, head_ip, is_head),
-        call_context=call_context, ready_timeout=ready_timeout)
+        call_context=call_context, ready_timeout=ready_timeout,
+        shared_memory_ratio=shared_memory_ratio(config, nt))
+
+
+def shared_memory_ratio(config: Dict[str, Any], node_type: Optional[str]) -> float:
+    """/dev/shm share of a container's memory: the largest any enabled runtime asks for
+    (Runtime.get_runtime_shared_memory_ratio), or docker.shared_memory_ratio."""
+    ratio = float((config.get("docker") or {}).get("shared_memory_ratio", 0.0) or 0.0)
+    from cloudtik_amd.core.runtime_factory import get_runtime, get_runtime_types
+    rc = config.get("runtime") or {}
+    for name in get_runtime_types(config):
+        try:
+            ratio = max(ratio, float(get_runtime(name, rc).get_runtime_shared_memory_ratio(rc, config, node_type) or 0))
+        except Exception:  # noqa: BLE001 - a runtime without the hook
+            continue
+    return ratio
 
 
 def get_head_node(provider, cluster_name: str) -> Optional[str]:

@@ -331,15 +331,88 @@ class SSHCommandExecutor(CommandExecutor):
 
 
 # ---------------------------------------------------------------------------------- docker
+# bootstrap files are copied into the container, never bind-mounted: docker bind-mounts the
+# inode, so a config rewritten on the host (new file, rename) would go stale inside
+BOOTSTRAP_MOUNTS = ("~/cloudtik_bootstrap_config.yaml", "~/cloudtik_bootstrap_key.pem")
+
+
+def docker_host_mount_location(cluster_name: str) -> str:
+    """Host directory that holds the bind-mounted file_mounts of a cluster's containers."""
+    return f"/tmp/cloudtik_docker_mounts/{cluster_name}"
+
+
 class DockerCommandExecutor(CommandExecutor):
-    def __init__(self, call_context, host_executor: CommandExecutor, docker_config: Dict[str, Any]):
+    """Runs node commands inside the cluster container on a host reached by ``host_executor``
+    (reference core/_private/command_executor/docker_command_executor.py, run_init :326).
+
+    * ``run_init``: pulls the image (``pull_before_run``, default true; otherwise only when
+      missing), checks a running container for drift -- a different image or file_mounts it
+      does not bind-mount -- and restarts it then; a container is started only once the files
+      are synced (``sync_run_yet``), with the file_mounts bind-mounted from the host mount
+      location, ROCm device pass-through and /dev/shm sized from the runtime's ratio; the
+      bootstrap config / key are copied in.  Returns whether a ``docker run`` was executed.
+    * rsync goes to the host mount location (the bind mount makes it visible inside); paths
+      that are not bind-mounted are copied into the running container.
+    """
+
+    def __init__(self, call_context, host_executor: CommandExecutor, docker_config: Dict[str, Any],
+                 cluster_name: str = "default"):
         super().__init__(call_context)
         self.host = host_executor
         self.docker_config = docker_config or {}
         self.container_name = self.docker_config.get("container_name", "cloudtik-ai")
         self.docker_cmd = self.docker_config.get("docker_cmd", "docker")
+        self.cluster_name = cluster_name
         self.initialized = False
+        self.home_dir: Optional[str] = None
+        self.bind_mounts: Dict[str, str] = {}
 
+    # ------------------------------------------------------------------ helpers
+    def _host(self, cmd, with_output=False, silent=True):
+        return self.host.run(cmd, with_output=with_output, run_env="host", silent=silent)
+
+    def image(self, as_head: bool) -> Optional[str]:
+        return self.docker_config.get("head_image" if as_head else "worker_image") or self.docker_config.get("image")
+
+    def _out(self, cmd) -> str:
+        out = self._host(cmd, with_output=True)
+        return out.decode() if isinstance(out, (bytes, bytearray)) else (out or "")
+
+    def is_container_running(self) -> bool:
+        out = self._out(f"{self.docker_cmd} inspect -f '{{{{.State.Running}}}}' {self.container_name} || true")
+        return "true" in out.lower() and "no such object" not in out.lower()
+
+    def expand_user(self, path: str) -> str:
+        if path.startswith("~"):
+            if self.home_dir is None:
+                self.home_dir = self._out(f"{self.docker_cmd} exec {self.container_name} printenv HOME").strip() \
+                    or "/root"
+            return self.home_dir + path[1:]
+        return path
+
+    def host_mount_path(self, remote: str) -> str:
+        return docker_host_mount_location(self.cluster_name) + "/" + remote.lstrip("~/").lstrip("/")
+
+    def restart_needed(self, image: str, mounts: Dict[str, str]) -> bool:
+        """A running container with another image or without some requested bind mounts."""
+        running_image = self._out(f"{self.docker_cmd} inspect -f '{{{{.Config.Image}}}}' {self.container_name}").strip()
+        if running_image and running_image != image:
+            logger.warning("container %s runs image %s instead of %s: restarting it", self.container_name,
+                           running_image, image)
+            return True
+        raw = self._out(f"{self.docker_cmd} inspect -f '{{{{json .Mounts}}}}' {self.container_name}").strip()
+        try:
+            active = {m["Destination"].strip("/") for m in json.loads(raw or "[]")}
+        except (ValueError, KeyError, TypeError):
+            return False
+        wanted = {self.expand_user(r).strip("/") for r in mounts}
+        missing = wanted - active
+        if missing:
+            logger.warning("container %s lacks file mounts %s: restarting it", self.container_name, sorted(missing))
+            return True
+        return False
+
+    # ------------------------------------------------------------------ CommandExecutor
     def run(self, cmd=None, timeout=120, exit_on_fail=False, port_forward=None, with_output=False,
             environment_variables=None, run_env="auto", ssh_options_override_ssh_key="",
             shutdown_after_run=False, cmd_to_print=None, silent=False):
@@ -355,25 +428,34 @@ class DockerCommandExecutor(CommandExecutor):
         return self.host.run(inner, timeout, exit_on_fail, port_forward, with_output, None, "host",
                              ssh_options_override_ssh_key, shutdown_after_run, inner_shown, silent)
 
+    def _bind_mounted(self, target: str) -> bool:
+        t = target.rstrip("/")
+        return any(t == r.rstrip("/") or t.startswith(r.rstrip("/") + "/") for r in self.bind_mounts)
+
     def run_rsync_up(self, source, target, options=None):
-        staging = f"/tmp/cloudtik_docker_staging{target}"
+        staging = self.host_mount_path(target)
+        self._host(f"mkdir -p {shlex.quote(os.path.dirname(staging.rstrip('/')))}")
         self.host.run_rsync_up(source, staging, options)
-        self.host.run(f"{self.docker_cmd} exec {self.container_name} mkdir -p {shlex.quote(os.path.dirname(target.rstrip('/')))} && "
-                      f"{self.docker_cmd} cp {shlex.quote(staging)} {self.container_name}:{shlex.quote(target)}",
-                      run_env="host", silent=True)
+        if self.initialized and not self._bind_mounted(target) and self.is_container_running():
+            dst = self.expand_user(target)
+            self._host(f"{self.docker_cmd} exec {self.container_name} mkdir -p "
+                       f"{shlex.quote(os.path.dirname(dst.rstrip('/')))} && "
+                       f"{self.docker_cmd} cp {shlex.quote(staging)} {self.container_name}:{shlex.quote(dst)}")
 
     def run_rsync_down(self, source, target, options=None):
-        staging = f"/tmp/cloudtik_docker_staging{source}"
-        self.host.run(f"mkdir -p {shlex.quote(os.path.dirname(staging.rstrip('/')))} && "
-                      f"{self.docker_cmd} cp {self.container_name}:{shlex.quote(source)} {shlex.quote(staging)}",
-                      run_env="host", silent=True)
+        staging = self.host_mount_path(source)
+        self._host(f"mkdir -p {shlex.quote(os.path.dirname(staging.rstrip('/')))} && "
+                   f"{self.docker_cmd} cp {self.container_name}:{shlex.quote(self.expand_user(source))} "
+                   f"{shlex.quote(staging)}")
         self.host.run_rsync_down(staging, target, options)
 
     def remote_shell_command_str(self):
         return self.host.remote_shell_command_str().strip() + f" -tt -- {self.docker_cmd} exec -it {self.container_name} /bin/bash\n"
 
     def rocm_run_options(self, as_head: bool) -> List[str]:
-        """GPU pass-through flags when the host exposes /dev/kfd (AMD ROCm)."""
+        """GPU pass-through flags when the host exposes /dev/kfd (AMD ROCm); the reference's
+        nvidia-container-runtime detection (docker_command_executor.py:475-497) has no role
+        on MI355X."""
         if self.docker_config.get("disable_automatic_runtime_detection"):
             return []
         try:
@@ -396,28 +478,61 @@ class DockerCommandExecutor(CommandExecutor):
         except Exception:  # noqa: BLE001
             return []
 
+    def _pull(self, image: str):
+        if self.docker_config.get("pull_before_run", True):
+            self._host(f"{self.docker_cmd} pull {image}")
+        else:
+            self._host(f"{self.docker_cmd} image inspect {image} 1> /dev/null 2>&1 || {self.docker_cmd} pull {image}")
+
     def run_init(self, *, as_head, file_mounts, shared_memory_ratio, sync_run_yet):
-        image = self.docker_config.get("head_image" if as_head else "worker_image") or self.docker_config.get("image")
+        image = self.image(as_head)
         if not image:
             return None
-        running = self.host.run(f"{self.docker_cmd} inspect -f '{{{{.State.Running}}}}' {self.container_name} || true",
-                                with_output=True, run_env="host")
-        if running and running.strip() == b"true":
-            self.initialized = True
-            return True
-        opts = list(self.docker_config.get("run_options", [])) + \
-            list(self.docker_config.get("head_run_options" if as_head else "worker_run_options", []))
-        opts += ["--ipc=host", "--net=host", "--cap-add=NET_ADMIN", "--cap-add=SYS_NICE"]
-        opts += self.rocm_run_options(as_head) + self.shm_run_options(shared_memory_ratio)
-        mounts = " ".join(f"-v {shlex.quote(d)}:{shlex.quote(d)}" for d in (file_mounts or {}))
-        cmd = f"{self.docker_cmd} run --rm --name {self.container_name} -d -it {mounts} " \
-              f"{' '.join(opts)} {image} bash"
-        self.host.run(cmd, run_env="host")
+        self._pull(image)
+        mounts = {r: l for r, l in (file_mounts or {}).items() if r not in BOOTSTRAP_MOUNTS}
+        self.bind_mounts = mounts
+        running = self.initialized or self.is_container_running()
+        restart = running and self.restart_needed(image, mounts)
+        if restart:
+            self._host(f"{self.docker_cmd} stop {self.container_name} > /dev/null || true")
+            self.initialized = False
+        docker_run = False
+        if not running or restart:
+            if not sync_run_yet:
+                # start after the file sync: docker would create missing mount sources as root
+                return True
+            opts = list(self.docker_config.get("run_options", [])) + \
+                list(self.docker_config.get("head_run_options" if as_head else "worker_run_options", []))
+            opts += [f"--ipc={self.docker_config.get('ipc_mode') or 'host'}",
+                     f"--net={self.docker_config.get('network') or 'host'}",
+                     "--cap-add=NET_ADMIN", "--cap-add=SYS_NICE"]
+            if self.docker_config.get("cpus"):
+                opts.append(f"--cpus={self.docker_config['cpus']}")
+            if self.docker_config.get("memory"):
+                opts.append(f"--memory={self.docker_config['memory']}")
+            opts += self.rocm_run_options(as_head) + self.shm_run_options(shared_memory_ratio)
+            binds = " ".join(f"-v {shlex.quote(self.host_mount_path(r))}:{shlex.quote(r.replace('~/', '/root/'))}"
+                             for r in sorted(mounts))
+            labels = " ".join(f"-l {shlex.quote(f'{k}={v}')}" for k, v in
+                              (self.docker_config.get("labels") or {}).items())
+            self._host(f"{self.docker_cmd} run --rm --name {self.container_name} -d -it {binds} {labels} "
+                       f"-e CLOUDTIK_CLUSTER_NAME={shlex.quote(self.cluster_name)} {' '.join(opts)} {image} bash")
+            docker_run = True
+            self.home_dir = None
         self.initialized = True
-        return True
+        # bootstrap files: copied in explicitly (see BOOTSTRAP_MOUNTS)
+        for b in BOOTSTRAP_MOUNTS:
+            if b in (file_mounts or {}):
+                if not sync_run_yet:
+                    self.host.run_rsync_up(file_mounts[b], self.host_mount_path(b))
+                dst = self.expand_user(b)
+                self._host(f"{self.docker_cmd} cp {shlex.quote(self.host_mount_path(b))} "
+                           f"{self.container_name}:{shlex.quote(dst)}")
+        return docker_run
 
     def run_terminate(self):
-        self.host.run(f"{self.docker_cmd} stop {self.container_name} || true", run_env="host", silent=True)
+        self._host(f"{self.docker_cmd} stop {self.container_name} > /dev/null || true")
+        self.initialized = False
 
     def bootstrap_data_disks(self):
         return self.host.bootstrap_data_disks()
@@ -480,6 +595,7 @@ def create_default_command_executor(call_context, log_prefix, node_id, provider,
     else:
         host = SSHCommandExecutor(call_context, log_prefix, node_id, provider, auth_config,
                                   cluster_name, process_runner, use_internal_ip)
-    if docker_config and docker_config.get("enabled") and docker_config.get("image"):
-        return DockerCommandExecutor(call_context, host, docker_config)
+    if docker_config and docker_config.get("enabled") and (
+            docker_config.get("image") or docker_config.get("head_image") or docker_config.get("worker_image")):
+        return DockerCommandExecutor(call_context, host, docker_config, cluster_name)
     return host

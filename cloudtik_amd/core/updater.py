@@ -47,7 +47,7 @@ class NodeUpdater:
                  docker_config: Optional[Dict[str, Any]] = None, restart_only: bool = False,
                  for_recovery: bool = False, environment_variables: Optional[Dict[str, Any]] = None,
                  call_context: Optional[CallContext] = None, ready_timeout: float = None,
-                 command_timeout: Optional[float] = None):
+                 command_timeout: Optional[float] = None, shared_memory_ratio: float = 0.0):
         self.node_id = node_id
         self.provider = provider
         self.provider_config = provider_config
@@ -68,6 +68,7 @@ class NodeUpdater:
         self.call_context = call_context or CallContext()
         self.ready_timeout = ready_timeout if ready_timeout is not None else C.CLOUDTIK_NODE_START_WAIT_S
         self.command_timeout = command_timeout
+        self.shared_memory_ratio = shared_memory_ratio
         self.log_prefix = f"NodeUpdater: {node_id}: "
         self.executor = provider.get_command_executor(
             self.call_context, self.log_prefix, node_id, auth_config, cluster_name, process_runner,
@@ -153,6 +154,15 @@ class NodeUpdater:
         tags = self.provider.node_tags(self.node_id)
         runtime_unchanged = (self.runtime_hash is not None
                              and tags.get(T.CLOUDTIK_TAG_RUNTIME_CONFIG) == self.runtime_hash)
+        if runtime_unchanged:
+            # a node resumed from the stopped-node cache keeps its runtime hash, but its
+            # container is gone: a container (re)start invalidates the hash, so the
+            # initialization and setup commands run again inside the new container
+            # (reference node_updater.py:456-466)
+            if self.executor.run_init(as_head=self.is_head_node, file_mounts=self.file_mounts,
+                                      shared_memory_ratio=self.shared_memory_ratio, sync_run_yet=False):
+                runtime_unchanged = False
+                self.restart_only = False
         mounts_unchanged = (self.file_mounts_contents_hash is None
                             or tags.get(T.CLOUDTIK_TAG_FILE_MOUNTS_CONTENTS) == self.file_mounts_contents_hash)
         env = self.get_update_environment_variables()
@@ -164,6 +174,9 @@ class NodeUpdater:
                 self.exec_commands("start", self.start_commands, env)
             return
 
+        self._stage("data_disks")
+        self._set_status(T.STATUS_BOOTSTRAPPING_DATA_DISKS)
+        self.executor.bootstrap_data_disks()
         self._stage("sync_files")
         self._set_status(T.STATUS_SYNCING_FILES)
         self.sync_file_mounts()
@@ -173,6 +186,9 @@ class NodeUpdater:
         if not self.restart_only or self.for_recovery:
             self._stage("initialization")
             self.exec_commands("initialization", self.initialization_commands, env)
+            # container runtime: started here, after the files are synced
+            self.executor.run_init(as_head=self.is_head_node, file_mounts=self.file_mounts,
+                                   shared_memory_ratio=self.shared_memory_ratio, sync_run_yet=True)
             self._stage("setup")
             self.exec_commands("setup", self.setup_commands, env)
             self._stage("bootstrap")

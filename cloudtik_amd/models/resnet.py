@@ -98,10 +98,11 @@ class Bottleneck(nn.Module):
             # every conv on the in-tree implicit-GEMM MFMA kernels (ops/conv.py); conv1 hands
             # out an alias of x for the residual / downsample branch so its data-gradient
             # epilogue absorbs that branch's gradient
-            out, x = igemm.conv2d(x, self.conv1, keep_input=True)
-            idt = self.down_bn(igemm.conv2d(x, self.down)) if self.down is not None else x
-            out = self.bn2(igemm.conv2d(self.bn1(out), self.conv2))
-            return self.bn3(igemm.conv2d(out, self.conv3), residual=idt)
+            st = self.training and not self.bn1.frozen      # BatchNorm statistics from the conv epilogues
+            out, x = igemm.conv2d(x, self.conv1, keep_input=True, bn_stats=st)
+            idt = self.down_bn(igemm.conv2d(x, self.down, bn_stats=st)) if self.down is not None else x
+            out = self.bn2(igemm.conv2d(self.bn1(out), self.conv2, bn_stats=st))
+            return self.bn3(igemm.conv2d(out, self.conv3, bn_stats=st), residual=idt)
         # MIOpen path (CLOUDTIK_AMD_CONV_IGEMM=0, CPU): 1x1 convs as NHWC GEMMs, conv1's dgrad
         # GEMM absorbs the residual branch's gradient (ops/conv1x1.py)
         out, x = conv1x1(x, self.conv1, keep_input=True)
@@ -143,7 +144,7 @@ class ResNet(nn.Module):
             self.to(memory_format=torch.channels_last)
 
     def stem(self, x):
-        y = self.conv1(x)
+        y = igemm.stem_conv(x, self.conv1)
         bn = self.bn1
         if bn.relu and self.training and not bn.frozen:
             # BN + ReLU + 3x3/2 max-pool in one pass (the full-resolution activation is never

@@ -107,21 +107,25 @@ def dgrad_phases(x_shape, w_shape, stride, padding):
 
 # ------------------------------------------------------------------ launches
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), padding=(0, 0), out: Optional[torch.Tensor] = None,
-             accumulate: bool = False, stats: bool = False):
+             accumulate: bool = False, stats: bool = False, partials: bool = False):
     """Y = conv2d(x, w) (NHWC bf16).  With ``stats`` also returns (mean, biased var) per output
-    channel of the bf16 Y, from the epilogue's tile partials."""
+    channel of the bf16 Y, from the epilogue's tile partials; with ``partials`` the raw
+    partials instead: (Y, part, rows_per_tile), part = means [tiles][Co] then M2 [tiles][Co]
+    (what ops.batch_norm_act consumes when Y carries them as ``Y._ct_bn_part``)."""
     geo, taps, shape = fwd_plan(x.shape, w.shape, tuple(stride), tuple(padding))
     N, co, Ho, Wo = shape
     if out is None:
         out = torch.empty(shape, device=x.device, dtype=x.dtype, memory_format=torch.channels_last)
     C = _C()
     part = None
-    if stats:
+    if stats or partials:
         bm = C.conv_igemm_tile_m(_CFG, co, geo[11], len(taps) // 2 * (x.shape[1] // 64))
         part = torch.empty(((geo[11] + bm - 1) // bm) * 2 * co, device=x.device, dtype=torch.float32)
     ok = C.conv_igemm(x, weight_rows(w).contiguous(), out, geo, taps, accumulate, part, _CFG)
     if not ok:
         raise RuntimeError(f"conv_igemm rejected x{tuple(x.shape)} w{tuple(w.shape)} s{stride} p{padding}")
+    if partials:
+        return out, part, bm
     if not stats:
         return out
     mean = torch.empty(co, device=x.device, dtype=torch.float32)
@@ -235,11 +239,17 @@ class ConvFn(torch.autograd.Function):
     kernel's epilogue (no separate add pass)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, padding, keep_input):
+    def forward(ctx, x, w, stride, padding, keep_input, bn_stats=False):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding = stride, padding
         ctx.wp = w
-        y = conv_fwd(x, w, stride, padding)
+        if bn_stats:
+            # the epilogue reduces the BatchNorm statistics of y per tile; the BatchNorm that
+            # consumes y picks them up instead of re-reading y for a statistics pass
+            y, part, rows = conv_fwd(x, w, stride, padding, partials=True)
+            y._ct_bn_part = (part, rows)
+        else:
+            y = conv_fwd(x, w, stride, padding)
         return (y, x.view_as(x)) if keep_input else y
 
     @staticmethod
@@ -257,12 +267,115 @@ class ConvFn(torch.autograd.Function):
                     dx = dx + dx_other
         if ctx.needs_input_grad[1]:
             dw = _weight_grad(ctx.wp, dy, x, tuple(w.shape), ctx.stride, ctx.padding)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv2d(x: torch.Tensor, conv: torch.nn.Conv2d, keep_input: bool = False):
+BN_STATS = os.environ.get("CLOUDTIK_AMD_CONV_BN_STATS", "1") == "1"
+
+
+def conv2d(x: torch.Tensor, conv: torch.nn.Conv2d, keep_input: bool = False, bn_stats: bool = False):
     """``conv(x)`` on the implicit-GEMM kernels when eligible, else ``conv(x)``; with
-    ``keep_input`` returns ``(conv(x), x_alias)`` (see ConvFn)."""
+    ``keep_input`` returns ``(conv(x), x_alias)`` (see ConvFn); ``bn_stats``: the output feeds a
+    training-mode BatchNorm, so the epilogue also reduces its statistics."""
     if conv.bias is not None or not eligible(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups):
         return (conv(x), x) if keep_input else conv(x)
-    return ConvFn.apply(x, conv.weight, tuple(conv.stride), tuple(conv.padding), keep_input)
+    return ConvFn.apply(x, conv.weight, tuple(conv.stride), tuple(conv.padding), keep_input,
+                        bool(bn_stats and BN_STATS))
+
+
+# ------------------------------------------------------------------ the stem (Ci = 3)
+def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    """ResNet's 7x7/2 stem over an RGB bf16 image batch on GPU (any 3-channel conv with
+    R, S <= 8 works: the kernel's pixel-chunk mode)."""
+    w = conv.weight
+    return (ENABLED and x.is_cuda and x.dim() == 4 and x.shape[1] <= 8 and w.dtype == torch.bfloat16
+            and not x.requires_grad
+            and x.dtype == torch.bfloat16 and conv.bias is None and conv.groups == 1
+            and tuple(conv.dilation) == (1, 1) and w.shape[2] <= 7 and w.shape[3] <= 8 and w.shape[0] % 64 == 0
+            and max(conv.padding) <= 7)
+
+
+def to_nhwc8(x: torch.Tensor) -> torch.Tensor:
+    """[N, C<=8, H, W] -> NHWC with the channels zero-padded to 8 (16 bytes per pixel), returned
+    as the logical [N, 8, H, W] channels_last view the kernels take."""
+    n, c, h, w = x.shape
+    return F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous().permute(0, 3, 1, 2)
+
+
+def _stem_taps(R, pad):
+    taps = []
+    for r in range(R):
+        taps += [r - pad[0], -pad[1]]          # the K-step's 8 pixels start at x*s - pad
+    return taps
+
+
+def stem_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Co, C, R, S] -> [Co, R * 64]: column r*64 + s*8 + c = w[co, c, r, s] (zero-padded)."""
+    co, c, R, S = w.shape
+    wp = torch.zeros(co, R, 8, 8, device=w.device, dtype=w.dtype)
+    wp[:, :, :S, :c] = w.permute(0, 2, 3, 1)
+    return wp.reshape(co, R * 64)
+
+
+def stem_fwd(x8: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+    n, _, H, W = x8.shape
+    co, c, R, S = w.shape
+    Ho, Wo = out_size(H, R, stride[0], padding[0]), out_size(W, S, stride[1], padding[1])
+    out = torch.empty((n, co, Ho, Wo), device=x8.device, dtype=x8.dtype, memory_format=torch.channels_last)
+    geo = [Ho, Wo, stride[0], stride[1], Ho, Wo, 1, 1, 0, 0, co, n * Ho * Wo]
+    if not _C().conv_igemm(x8, stem_weight(w), out, geo, _stem_taps(R, padding), False, None, _CFG):
+        raise RuntimeError(f"conv_igemm (stem) rejected x{tuple(x8.shape)} w{tuple(w.shape)}")
+    return out
+
+
+def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding) -> torch.Tensor:
+    co, c, R, S = w_shape
+    nn = R * 64
+    M = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    C = _C()
+    cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
+    splits, rows = wgrad_plan(M, co, nn, cfg)
+    part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)
+    if not C.conv_wgrad(dy, x8, part, _stem_taps(R, padding), [stride[0], stride[1], rows], splits, cfg):
+        raise RuntimeError(f"conv_wgrad (stem) rejected dy{tuple(dy.shape)} x{tuple(x8.shape)}")
+    full = torch.empty(co * nn, device=dy.device, dtype=dy.dtype)
+    if splits <= 16:
+        C.splitk_reduce(part.view(splits, -1), full, False)
+    else:
+        C.splitk_reduce_wide(part, splits, full, False)
+    return full.view(co, R, 8, 8)[:, :, :S, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+
+
+class StemFn(torch.autograd.Function):
+    """conv2d of a <= 8-channel image batch (no input gradient: it is the network input)."""
+
+    @staticmethod
+    def forward(ctx, x8, w, stride, padding):
+        ctx.save_for_backward(x8)
+        ctx.stride, ctx.padding, ctx.w_shape = stride, padding, tuple(w.shape)
+        ctx.wp = w
+        return stem_fwd(x8, w, stride, padding)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x8,) = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = stem_wgrad(dy, x8, ctx.w_shape, ctx.stride, ctx.padding)
+            from cloudtik_amd.ops.conv1x1 import _flat_target
+            target = _flat_target(ctx.wp)
+            if target is not None:                    # straight into the flat gradient buffer
+                target.add_(dw)
+                cb = getattr(ctx.wp, "_ct_grad_ready", None)
+                if cb is not None:
+                    cb(ctx.wp)
+                dw = None
+        return None, dw, None, None
+
+
+def stem_conv(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
+    """``conv(x)`` for the image-batch stem on the kernels' pixel-chunk mode when eligible."""
+    if not stem_eligible(x, conv):
+        return conv(x)
+    return StemFn.apply(to_nhwc8(x), conv.weight, tuple(conv.stride), tuple(conv.padding))

@@ -593,6 +593,25 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
   return 0;
 }
 
+// Training forward whose statistics were produced by the PRODUCER of x: per-tile means
+// [tiles][C] and M2 [tiles][C] over rows_per_tile rows each (the implicit-GEMM conv epilogue,
+// conv.hip).  Only the finalize and the apply pass run: x is read once instead of twice.
+extern "C" int ct_bn_fwd_train_given(const void* x, const void* res, const void* gamma, const void* beta,
+                                     float* run_mean, float* run_var, void* y, const float* part, int tiles,
+                                     int rows_per_tile, float* stat, int M, int C, float eps, float momentum,
+                                     int relu, hipStream_t stream) {
+  if (C % 8 || M <= 0 || tiles <= 0 || (long)tiles * rows_per_tile < M) return -1;
+  BnLayout L{M, C, C / 8, 1, rows_per_tile};
+  bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)tiles * C, tiles, L,
+                                                           (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                           eps, momentum, run_mean, run_var, stat,
+                                                           stat + C, stat + 2 * C, stat + 3 * C);
+  const long tv = (long)M * (C / 8);
+  BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, stat + 2 * C, stat + 3 * C,
+                 (bf16_t*)y, tv, C / 8, relu);
+  return 0;
+}
+
 // ResNet stem: batch statistics of x, then y = maxpool3x3/s2/p1(relu(bn(x))) + byte argmax
 // (stat = float[4C] as ct_bn_fwd_train)
 extern "C" int ct_bn_fwd_train_pool(const void* x, const void* gamma, const void* beta, float* run_mean,

@@ -40,6 +40,8 @@ int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, co
 int ct_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, float*,
                     float*, int, int, float, float, int, hipStream_t);
 int ct_bn_apply(const void*, const void*, const float*, const float*, void*, int, int, int, hipStream_t);
+int ct_bn_fwd_train_given(const void*, const void*, const void*, const void*, float*, float*, void*, const float*, int,
+                          int, float*, int, int, float, float, int, hipStream_t);
 int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
                          int, int, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
@@ -448,6 +450,29 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
   return {y, stat};
 }
 
+// bn_fwd_train with the statistics already reduced per tile by x's producer (conv epilogue):
+// part = means [tiles][C] then M2 [tiles][C], tiles = ceil(M / rows_per_tile)
+std::vector<at::Tensor> bn_fwd_train_given(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma,
+                                           at::Tensor beta, at::Tensor run_mean, at::Tensor run_var, at::Tensor part,
+                                           int64_t rows_per_tile, double eps, double momentum, bool relu) {
+  check_nhwc(x, "x");
+  const int C = x.size(1);
+  const long M = nhwc_rows(x);
+  if (res.has_value() && res->defined()) { check_nhwc(*res, "residual"); TORCH_CHECK(res->sizes() == x.sizes()); }
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  CHECK_F32(run_mean); CHECK_F32(run_var); CHECK_IN(part); CHECK_F32(part);
+  const long tiles = (M + rows_per_tile - 1) / rows_per_tile;
+  TORCH_CHECK(part.numel() >= 2 * tiles * C, "bn_fwd_train_given: part buffer");
+  auto y = at::empty_like(x);
+  auto stat = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_fwd_train_given(x.data_ptr(), optr(res), gamma.data_ptr(), beta.data_ptr(),
+                                 run_mean.data_ptr<float>(), run_var.data_ptr<float>(), y.data_ptr(),
+                                 part.data_ptr<float>(), (int)tiles, (int)rows_per_tile, stat.data_ptr<float>(),
+                                 (int)M, C, (float)eps, (float)momentum, relu ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_fwd_train_given: unsupported C=", C);
+  return {y, stat};
+}
+
 // ResNet stem: returns (y_pool [N, C, OH, OW] channels_last, argmax bytes [N, OH, OW, C] uint8, stat)
 std::vector<at::Tensor> bn_fwd_train_pool(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor run_mean,
                                           at::Tensor run_var, double eps, double momentum) {
@@ -570,6 +595,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_fwd", &xent_fwd);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_apply", &bn_apply);
+  m.def("bn_fwd_train_given", &bn_fwd_train_given);
   m.def("bn_fwd_train_pool", &bn_fwd_train_pool);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd);

@@ -32,7 +32,8 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
   TORCH_CHECK(geo.size() == 12 && taps.size() % 2 == 0, "conv_igemm: plan");
   const int Ci = (int)X.size(1), Hi = (int)X.size(2), Wi = (int)X.size(3);
   const int T = (int)taps.size() / 2, Co = (int)W.size(0);
-  TORCH_CHECK(W.size(1) == (int64_t)T * Ci, "conv_igemm: W columns != taps * Ci");
+  const int cw = Ci == 8 ? 64 : Ci;           // stem (pixel-chunk) mode: 64 weight columns per tap
+  TORCH_CHECK(W.size(1) == (int64_t)T * cw, "conv_igemm: W columns != taps * Ci");
   const long M = geo[11];
   // every output address the plan produces must lie inside Y (checked on the host before launch)
   const long Nb = X.size(0);
@@ -43,7 +44,7 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
   std::vector<int> tp(taps.begin(), taps.end());
   float* pp = nullptr;
   if (part.has_value() && part->defined()) {
-    const int cfg_r = ct_conv_igemm_rows((int)cfg, Co, (int)M, T * (Ci / 64));
+    const int cfg_r = ct_conv_igemm_rows((int)cfg, Co, (int)M, T * (cw / 64));
     const int bm = ct_conv_igemm_tile_m(cfg_r);
     TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() &&
                 part->numel() >= (M + bm - 1) / bm * 2 * Co, "conv_igemm: part buffer");
@@ -83,7 +84,7 @@ bool conv_wgrad(at::Tensor DY, at::Tensor X, at::Tensor P, std::vector<int64_t> 
   TORCH_CHECK(geo.size() == 3 && taps.size() % 2 == 0 && DY.size(0) == X.size(0), "conv_wgrad: plan");
   const int T = (int)taps.size() / 2, Ci = (int)X.size(1), Co = (int)DY.size(1);
   const long M = DY.size(0) * DY.size(2) * DY.size(3);
-  TORCH_CHECK(P.numel() >= splits * (long)Co * T * Ci, "conv_wgrad: partial buffer");
+  TORCH_CHECK(P.numel() >= splits * (long)Co * T * (Ci == 8 ? 64 : Ci), "conv_wgrad: partial buffer");
   std::vector<int> tp(taps.begin(), taps.end());
   const int rc = ct_conv_wgrad(DY.data_ptr(), X.data_ptr(), (int)X.size(2), (int)X.size(3), Ci, (int)DY.size(2),
                                (int)DY.size(3), (int)geo[0], (int)geo[1], Co, (int)M, T, tp.data(),

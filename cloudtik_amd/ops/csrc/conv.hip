@@ -43,7 +43,7 @@ struct ConvArgs {
   const bf16_t* X;      // gathered operand, NHWC [Nb, Hi, Wi, Ci]
   const bf16_t* W;      // [Co][T * Ci], k contiguous
   bf16_t* Y;            // output
-  float* part;          // EPI 1: [mtiles][2][Co] per-tile (mean, M2)
+  float* part;          // EPI 1: per-tile means [mtiles][Co], then M2 [mtiles][Co]
   int Hi, Wi, Ci;
   int Hr, Wr;           // row grid: m = (b * Hr + y) * Wr + x
   int sy, sx;           // input pixel = (y * sy + dy_t, x * sx + dx_t)
@@ -51,6 +51,8 @@ struct ConvArgs {
   int Co, M, T;
   int accumulate;
   unsigned long long tdy, tdx;           // 16 taps x 4 bits, biased by 8
+  int cpt;              // K-steps (of 64 weight columns) per tap: Ci / 64, or 1 in pixel-chunk mode
+  int pixchunk;         // stem mode: Ci = 8, the 8 chunks of a K-step are 8 consecutive pixels
 };
 
 __device__ __forceinline__ int cv_swz(int r) { return (r >> 1) & 7; }
@@ -110,13 +112,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   const int HW = a.Hr * a.Wr;
 
   // ---- per-lane gather descriptors: the A rows this lane stages (fixed for the whole K loop)
-  int pix[IA], iy0[IA], ix0[IA];
+  int pix[IA], iy0[IA], ix0[IA], gpx[IA];
   unsigned gca[IA];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
     const int row = (wave * IA + j) * 8 + (lane >> 3);
     const int m = m0 + row;
-    gca[j] = (unsigned)((lane & 7) ^ cv_swz(row)) * 8u;
+    const int gc = (lane & 7) ^ cv_swz(row);
+    gca[j] = (unsigned)gc * 8u;                    // element offset of the chunk
+    gpx[j] = a.pixchunk ? gc : 0;                  // stem: the chunk is a pixel step along x
     if (m < a.M) {
       const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
       iy0[j] = y * a.sy;
@@ -128,14 +132,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
       pix[j] = 0;
     }
   }
-  const long ldw = (long)a.T * a.Ci;
+  const long ldw = (long)a.T * a.cpt * 64;
   const bf16_t* wrow[IB];
 #pragma unroll
   for (int j = 0; j < IB; ++j) {
     const int row = (wave * IB + j) * 8 + (lane >> 3);
     wrow[j] = a.W + (long)(n0 + row) * ldw + ((lane & 7) ^ cv_swz(row)) * 8;
   }
-  const int cpt = a.Ci >> 6;                // 64-channel chunks per tap
+  const int cpt = a.cpt;                    // 64-column K-steps per tap
   const int KT = a.T * cpt;
 
   auto stage = [&](int kt, int slot) {
@@ -146,12 +150,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
     char* Bs = As + BM * 128;
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
-      const int iy = iy0[j] + dy, ix = ix0[j] + dx;
+      const int iy = iy0[j] + dy, ix = ix0[j] + dx + gpx[j];
       const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
       const void* src = ok ? (const void*)(a.X + (long)(pix[j] + toff) + gca[j]) : (const void*)cv_zero_page;
       cv_glds16(src, As + (wave * IA + j) * 1024);
     }
-    const long k0 = (long)t * a.Ci + c0;
+    const long k0 = (long)t * cpt * 64 + c0;
 #pragma unroll
     for (int j = 0; j < IB; ++j) cv_glds16(wrow[j] + k0, Bs + (wave * IB + j) * 1024);
   };
@@ -264,7 +268,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
       }
     __syncthreads();
     if (wm == 0 && (lane & 15) == 0) {
-      float* pm = a.part + (long)tm * 2 * a.Co;
+      // part = means [tiles_m][Co], then M2 [tiles_m][Co] (the layout bn_finalize_kernel reads)
+      const long tiles_m = (a.M + BM - 1) / BM;
+      float* pm = a.part + (long)tm * a.Co;
+      float* pq = a.part + (tiles_m + tm) * (long)a.Co;
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -274,7 +281,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
 #pragma unroll
           for (int w = 0; w < WGM; ++w) q += red[w * BN + c];
           pm[n0 + c] = mean[j][r];
-          pm[a.Co + n0 + c] = q;
+          pq[n0 + c] = q;
         }
     }
   }
@@ -315,6 +322,8 @@ struct WgradArgs {
   int Hi, Wi, Ci, Hr, Wr, sy, sx;
   int Co, NN, M, T, rows_per_split;
   unsigned long long tdy, tdx;
+  int Cw;               // weight columns per tap (= Ci, or 64 in pixel-chunk mode)
+  int pixchunk;         // stem: column c of a tap = pixel step c / 8, channel c % 8 (Ci = 8)
 };
 
 template <int LPR>
@@ -375,14 +384,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
   }
   // B rows (gathered X): per instruction the lane's chunk column -> tap, channel; the pixel
   // (b, y, x) of its row is tracked incrementally
-  int rb[GB], bb[GB], yb[GB], xb[GB], dyb[GB], dxb[GB], cib[GB];
+  int rb[GB], bb[GB], yb[GB], xb[GB], dyb[GB], dxb[GB], cib[GB], pxb[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int r = (wave * GB + j) * RPB + lane / LPB;
     rb[j] = r;
     const int n = n0 + (((lane % LPB) ^ wg_swz<LPB>(r)) << 3);
-    const int t = n / a.Ci;
-    cib[j] = n - t * a.Ci;
+    const int t = n / a.Cw;
+    const int c = n - t * a.Cw;
+    cib[j] = a.pixchunk ? (c & 7) : c;
+    pxb[j] = a.pixchunk ? (c >> 3) : 0;
     dyb[j] = (int)((a.tdy >> (4 * t)) & 15) - 8;
     dxb[j] = (int)((a.tdx >> (4 * t)) & 15) - 8;
     const int m = kbeg + r, HW = a.Hr * a.Wr;
@@ -405,7 +416,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const int m = kb + rb[j];
-      const int iy = yb[j] * a.sy + dyb[j], ix = xb[j] * a.sx + dxb[j];
+      const int iy = yb[j] * a.sy + dyb[j], ix = xb[j] * a.sx + dxb[j] + pxb[j];
       const bool ok = m < kend && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
       const void* src = ok ? (const void*)(a.X + ((long)(bb[j] * a.Hi + iy) * a.Wi + ix) * a.Ci + cib[j])
                            : (const void*)cv_zero_page;
@@ -473,7 +484,7 @@ __global__ void bn_partials_finalize_kernel(const float* __restrict__ part, int 
   double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int t = 0; t < tiles; ++t) {
     const double nb = (double)min(rows_per_tile, M - t * rows_per_tile);
-    const double mb = part[(long)t * 2 * C + c], qb = part[(long)t * 2 * C + C + c];
+    const double mb = part[(long)t * C + c], qb = part[((long)tiles + t) * C + c];
     const double nn = n + nb, d = mb - mean;
     mean += d * nb / nn;
     m2 += qb + d * d * n * nb / nn;
@@ -523,10 +534,11 @@ extern "C" int ct_conv_igemm_tile_m(int cfg) {
 extern "C" int ct_conv_igemm(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
                              int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M,
                              int T, const int* taps, int accumulate, float* part, int cfg, hipStream_t stream) {
-  if (Ci <= 0 || Ci % 64 || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT) return 1;
+  if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT) return 1;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 7) || ldy % 4) return 3;
+  const int pixchunk = Ci == 8;            // the stem: NHWC8 input, 8 pixels per K-step
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
-             Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull};
+             Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk};
   for (int t = 0; t < T; ++t) {
     const int dy = taps[2 * t], dx = taps[2 * t + 1];
     if (dy < -8 || dy > 7 || dx < -8 || dx > 7) return 4;
@@ -534,7 +546,7 @@ extern "C" int ct_conv_igemm(const void* X, int Hi, int Wi, int Ci, const void* 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   const int epi = part ? 1 : 0;
-  cfg = ct_conv_igemm_rows(cfg, Co, M, T * (Ci / 64));
+  cfg = ct_conv_igemm_rows(cfg, Co, M, T * a.cpt);
   if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9) && Co % 128) return 2;
   switch (cfg) {
     case 0: return cv_launch<256, 64, 4, 1, 3, 1>(a, epi, stream);
@@ -623,11 +635,13 @@ extern "C" int ct_splitk_reduce_wide(const float* P, int S, long n, void* out, i
 extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int Ci, int Hr, int Wr, int sy, int sx,
                              int Co, int M, int T, const int* taps, float* P, int splits, int rows_per_split, int cfg,
                              hipStream_t stream) {
-  if (Ci <= 0 || Ci % 64 || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT || splits < 1) return 1;
+  if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT || splits < 1)
+    return 1;
   if (rows_per_split % 32 || (long)rows_per_split * splits < M) return 2;
   if (((uintptr_t)DY & 15) || ((uintptr_t)X & 15) || ((uintptr_t)P & 15)) return 3;
-  WgradArgs a{(const bf16_t*)DY, (const bf16_t*)X, P, Hi, Wi, Ci, Hr, Wr, sy, sx, Co, T * Ci, M, T, rows_per_split,
-              0ull, 0ull};
+  const int pixchunk = Ci == 8, Cw = pixchunk ? 64 : Ci;
+  WgradArgs a{(const bf16_t*)DY, (const bf16_t*)X, P, Hi, Wi, Ci, Hr, Wr, sy, sx, Co, T * Cw, M, T, rows_per_split,
+              0ull, 0ull, Cw, pixchunk};
   for (int t = 0; t < T; ++t) {
     const int dy = taps[2 * t], dx = taps[2 * t + 1];
     if (dy < -8 || dy > 7 || dx < -8 || dx > 7) return 4;

@@ -190,7 +190,13 @@ def cross_entropy_fused(x, W, b, labels, V=None, ignore_index=-100, label_smooth
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, run_mean, run_var, relu, momentum, eps):
-        y, stat = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu)
+        given = getattr(x, "_ct_bn_part", None)
+        if given is not None:
+            # statistics already reduced per tile by the conv that produced x (ops/conv.py)
+            y, stat = _C().bn_fwd_train_given(x, residual, gamma, beta, run_mean, run_var, given[0], given[1],
+                                              eps, momentum, relu)
+        else:
+            y, stat = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu)
         has_res = residual is not None
         # ReLU mask for the backward: without a residual it is recomputed from x and the
         # forward's affine coefficients (stat), so y is neither saved nor re-read

@@ -39,6 +39,10 @@ class AWSNodeProvider(NodeProvider):
       ``SubnetIds``, moving to the next subnet on capacity errors), with the workspace
       security group and the head / worker instance profile (providers/cloud/workspace.py),
       optional spot market, and ``data_disks`` as extra gp3 EBS volumes;
+    * stopped-node caching (``cache_stopped_nodes``, default true, reference aws
+      node_provider.py:63,233,530): terminating a node STOPS it (spot instances, which cannot
+      be stopped, are terminated); a launch first restarts stopped nodes of the same cluster,
+      node kind, node type and launch hash, re-tagged, and creates only the remainder;
     * boto3 is loaded lazily; ``provider._client_factory`` injects a client (tests).
     """
 
@@ -58,6 +62,7 @@ class AWSNodeProvider(NodeProvider):
         self._pending_tags: Dict[str, Dict[str, str]] = {}
         self._batch_timer: Optional[threading.Timer] = None
         self._subnet_idx = 0
+        self.cache_stopped_nodes = bool(provider_config.get("cache_stopped_nodes", True))
 
     # ------------------------------------------------------------------ queries
     def _filters(self, tag_filters):
@@ -175,7 +180,43 @@ class AWSNodeProvider(NodeProvider):
         ids = node_config.get("SubnetIds") or ([node_config["SubnetId"]] if node_config.get("SubnetId") else [])
         return list(ids or self.provider_config.get("subnet_ids", []))
 
+    def _reuse_stopped(self, tags, count) -> Dict[str, Any]:
+        """Restart up to ``count`` stopped nodes launched from the same configuration."""
+        keys = (T.CLOUDTIK_TAG_NODE_KIND, T.CLOUDTIK_TAG_LAUNCH_CONFIG, T.CLOUDTIK_TAG_USER_NODE_TYPE)
+        filters = [{"Name": "instance-state-name", "Values": ["stopped", "stopping"]},
+                   {"Name": f"tag:{T.CLOUDTIK_TAG_CLUSTER_NAME}", "Values": [self.cluster_name]}]
+        filters += [{"Name": f"tag:{k}", "Values": [tags[k]]} for k in keys if k in tags]
+        found = []
+        for res in self.ec2.describe_instances(Filters=filters).get("Reservations", []):
+            found += res.get("Instances", [])
+        found = sorted(found, key=lambda i: i["InstanceId"])[:count]
+        if not found:
+            return {}
+        ids = [i["InstanceId"] for i in found]
+        self.ec2.start_instances(InstanceIds=ids)
+        # the reused nodes take the new launch's tags (status, node seq id, ...)
+        self.ec2.create_tags(Resources=ids, Tags=[{"Key": k, "Value": str(v)} for k, v in tags.items()])
+        out = {}
+        for inst in found:
+            cur = {t["Key"]: t["Value"] for t in inst.get("Tags") or []}
+            cur.update({k: str(v) for k, v in tags.items()})
+            inst = dict(inst, Tags=[{"Key": k, "Value": v} for k, v in cur.items()], State={"Name": "pending"})
+            self._remember(inst)
+            out[inst["InstanceId"]] = inst
+        return out
+
     def create_node(self, node_config, tags, count):
+        reused: Dict[str, Any] = {}
+        if self.cache_stopped_nodes:
+            reused = self._reuse_stopped(dict(tags, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name}), count)
+            count -= len(reused)
+            if count <= 0:
+                return reused
+        out = self._launch(node_config, tags, count)
+        out.update(reused)
+        return out
+
+    def _launch(self, node_config, tags, count):
         self._workspace_defaults()
         conf = {k: v for k, v in node_config.items()
                 if k not in ("SubnetIds", "SubnetId", "data_disks", "spot", "instance_type")}
@@ -229,11 +270,21 @@ class AWSNodeProvider(NodeProvider):
         self.terminate_nodes([node_id])
 
     def terminate_nodes(self, node_ids: List[str]):
-        if node_ids:
-            self.flush_tags()
-            self.ec2.terminate_instances(InstanceIds=list(node_ids))
-            for n in node_ids:
-                self._nodes.pop(n, None)
+        if not node_ids:
+            return
+        self.flush_tags()
+        terminate, stop = list(node_ids), []
+        if self.cache_stopped_nodes:
+            # spot instances cannot be stopped: those are terminated
+            spot = {n for n in node_ids if self._node(n).get("InstanceLifecycle") == "spot"}
+            stop = [n for n in node_ids if n not in spot]
+            terminate = [n for n in node_ids if n in spot]
+        if stop:
+            self.ec2.stop_instances(InstanceIds=stop)
+        if terminate:
+            self.ec2.terminate_instances(InstanceIds=terminate)
+        for n in node_ids:
+            self._nodes.pop(n, None)
 
 
 # GCP and Azure speak the clouds' REST APIs directly (no SDK needed): rest_providers.py

@@ -11,12 +11,30 @@ from cloudtik_amd.core.node_provider import NodeLaunchException, NodeProvider
 
 
 class MockProcessRunner:
-    """Records commands; ``fail_cmds`` substrings make a command fail."""
+    """Records commands; ``fail_cmds`` substrings make a command fail; ``respond_to_call``
+    gives canned outputs to commands that capture output (reference test_cloudtik.py:91-205)."""
 
     def __init__(self, fail_cmds: Optional[List[str]] = None):
         self.calls: List[str] = []
         self.fail_cmds = list(fail_cmds or [])
         self.lock = threading.Lock()
+        self.responses: Dict[str, List[str]] = {}
+
+    def respond_to_call(self, pattern: str, outputs: List[str]):
+        """The next commands containing ``pattern`` that capture output get ``outputs`` in order
+        (the last one repeats)."""
+        self.responses[pattern] = list(outputs)
+
+    def output_for(self, cmd: str) -> bytes:
+        with self.lock:
+            for pat, outs in self.responses.items():
+                if pat in cmd and outs:
+                    return (outs.pop(0) if len(outs) > 1 else outs[0]).encode()
+        return b""
+
+    def clear_history(self):
+        with self.lock:
+            self.calls.clear()
 
     def record(self, node_id: str, cmd: str):
         with self.lock:
@@ -39,7 +57,7 @@ class MockCommandExecutor(CommandExecutor):
             shutdown_after_run=False, cmd_to_print=None, silent=False):
         if cmd:
             self.runner.record(self.node_id, cmd)
-        return b"" if with_output else None
+        return self.runner.output_for(cmd or "") if with_output else None
 
     def run_rsync_up(self, source, target, options=None):
         self.runner.record(self.node_id, f"rsync-up {source} {target}")
@@ -57,6 +75,9 @@ class MockProvider(NodeProvider):
         w = MockProvider._worlds.setdefault(cluster_name, {"nodes": {}, "next": 0, "lock": threading.RLock(),
                                                            "runner": MockProcessRunner(), "fail_launch": set()})
         self.world = w
+        # stop instead of terminate, reuse stopped nodes on launch (the reference MockProvider's
+        # cache_stopped, test_cloudtik.py:207)
+        self.cache_stopped = bool(provider_config.get("cache_stopped_nodes", False))
 
     @classmethod
     def reset(cls, cluster_name: Optional[str] = None):
@@ -76,14 +97,15 @@ class MockProvider(NodeProvider):
     def non_terminated_nodes(self, tag_filters):
         with self.world["lock"]:
             return sorted((nid for nid, n in self.world["nodes"].items()
-                           if n["state"] != "terminated" and all(n["tags"].get(k) == v for k, v in tag_filters.items())),
+                           if n["state"] not in ("terminated", "stopped")
+                           and all(n["tags"].get(k) == v for k, v in tag_filters.items())),
                           key=lambda x: int(x.split("-")[-1]))
 
     def is_running(self, node_id):
         return self.world["nodes"].get(node_id, {}).get("state") == "running"
 
     def is_terminated(self, node_id):
-        return self.world["nodes"].get(node_id, {}).get("state", "terminated") == "terminated"
+        return self.world["nodes"].get(node_id, {}).get("state", "terminated") in ("terminated", "stopped")
 
     def node_tags(self, node_id):
         return dict(self.world["nodes"].get(node_id, {}).get("tags", {}))
@@ -101,6 +123,18 @@ class MockProvider(NodeProvider):
             raise NodeLaunchException("InsufficientCapacity", f"no capacity for {itype}")
         out = {}
         with self.world["lock"]:
+            if self.cache_stopped:
+                from cloudtik_amd.core import tags as T
+                keys = (T.CLOUDTIK_TAG_NODE_KIND, T.CLOUDTIK_TAG_LAUNCH_CONFIG, T.CLOUDTIK_TAG_USER_NODE_TYPE)
+                for nid in sorted(self.world["nodes"], key=lambda x: int(x.split("-")[-1])):
+                    n = self.world["nodes"][nid]
+                    if count <= 0:
+                        break
+                    if n["state"] == "stopped" and all(n["tags"].get(k) == tags.get(k) for k in keys):
+                        n["state"] = "running"
+                        n["tags"].update(tags)
+                        out[nid] = n
+                        count -= 1
             for _ in range(count):
                 i = self.world["next"]
                 self.world["next"] += 1
@@ -117,8 +151,13 @@ class MockProvider(NodeProvider):
     def terminate_node(self, node_id):
         with self.world["lock"]:
             if node_id in self.world["nodes"]:
-                self.world["nodes"][node_id]["state"] = "terminated"
+                self.world["nodes"][node_id]["state"] = "stopped" if self.cache_stopped else "terminated"
 
     def get_command_executor(self, call_context, log_prefix, node_id, auth_config, cluster_name, process_runner,
                              use_internal_ip, docker_config=None):
-        return MockCommandExecutor(call_context, node_id, self.runner)
+        host = MockCommandExecutor(call_context, node_id, self.runner)
+        if docker_config and docker_config.get("enabled") and (
+                docker_config.get("image") or docker_config.get("head_image") or docker_config.get("worker_image")):
+            from cloudtik_amd.core.executor import DockerCommandExecutor
+            return DockerCommandExecutor(call_context, host, docker_config, cluster_name)
+        return host

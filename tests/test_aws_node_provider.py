@@ -38,7 +38,11 @@ class FakeEC2:
         return {"Instances": out}
 
     def describe_instances(self, Filters=None, InstanceIds=None, NextToken=None):
-        rows = [i for i in self.instances.values() if i["State"]["Name"] in ("pending", "running")]
+        states = ("pending", "running")
+        for f in Filters or []:
+            if f["Name"] == "instance-state-name":
+                states = tuple(f["Values"])
+        rows = [i for i in self.instances.values() if i["State"]["Name"] in states]
         if InstanceIds:
             rows = [self.instances[i] for i in InstanceIds]
         for f in Filters or []:
@@ -59,6 +63,15 @@ class FakeEC2:
     def terminate_instances(self, InstanceIds):
         for i in InstanceIds:
             self.instances[i]["State"]["Name"] = "terminated"
+
+    def stop_instances(self, InstanceIds):
+        for i in InstanceIds:
+            self.instances[i]["State"]["Name"] = "stopped"
+
+    def start_instances(self, InstanceIds):
+        for i in InstanceIds:
+            assert self.instances[i]["State"]["Name"] == "stopped"
+            self.instances[i]["State"]["Name"] = "pending"
 
 
 def _provider(fake, **cfg):
@@ -109,3 +122,35 @@ def test_all_subnets_full_raises_launch_exception():
     fake = FakeEC2(full_subnets={"subnet-a", "subnet-b"})
     with pytest.raises(NodeLaunchException):
         _provider(fake).create_node({"SubnetIds": ["subnet-a", "subnet-b"]}, {}, 1)
+
+
+def test_stopped_node_caching_reuses_matching_nodes():
+    """cache_stopped_nodes (reference aws node_provider.py:63,233,530): terminate stops the
+    instance; the next launch with the same launch hash / node type restarts it (re-tagged)
+    and creates only what is missing; spot instances are terminated, never stopped."""
+    fake = FakeEC2()
+    p = _provider(fake)
+    tags = {T.CLOUDTIK_TAG_NODE_KIND: "worker", T.CLOUDTIK_TAG_LAUNCH_CONFIG: "h1",
+            T.CLOUDTIK_TAG_USER_NODE_TYPE: "gpu.8x"}
+    ids = sorted(p.create_node({"instance_type": "m5.large"}, dict(tags, **{T.CLOUDTIK_TAG_NODE_STATUS: "up-to-date"}), 2))
+    p.terminate_nodes(ids)
+    assert all(fake.instances[i]["State"]["Name"] == "stopped" for i in ids)
+    assert p.non_terminated_nodes({}) == []
+    # another launch hash: no reuse
+    other = p.create_node({"instance_type": "m5.large"}, dict(tags, **{T.CLOUDTIK_TAG_LAUNCH_CONFIG: "h2"}), 1)
+    assert not set(other) & set(ids)
+    # same launch config: both stopped nodes come back, one new instance is created
+    n_before = fake.n
+    got = p.create_node({"instance_type": "m5.large"}, dict(tags, **{T.CLOUDTIK_TAG_NODE_STATUS: "uninitialized"}), 3)
+    assert set(ids) <= set(got) and len(got) == 3 and fake.n == n_before + 1
+    assert all(p.node_tags(i)[T.CLOUDTIK_TAG_NODE_STATUS] == "uninitialized" for i in ids)
+    assert {t["Key"]: t["Value"] for t in fake.instances[ids[0]]["Tags"]}[T.CLOUDTIK_TAG_NODE_STATUS] == "uninitialized"
+    # spot: terminated even with caching on
+    fake.instances[ids[0]]["InstanceLifecycle"] = "spot"
+    p._nodes.pop(ids[0], None)
+    p.terminate_nodes([ids[0]])
+    assert fake.instances[ids[0]]["State"]["Name"] == "terminated"
+    # caching off: terminate
+    q = _provider(fake, cache_stopped_nodes=False)
+    q.terminate_nodes([ids[1]])
+    assert fake.instances[ids[1]]["State"]["Name"] == "terminated"

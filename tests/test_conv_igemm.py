@@ -76,7 +76,8 @@ def _nhwc(t):
 
 
 def _rel(a, b):
-    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+    # (zero_init BatchNorm: some gradients are exactly zero in both paths)
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-6)).item()
 
 
 @pytest.mark.gpu
@@ -148,3 +149,51 @@ def test_bottleneck_matches_miopen_path(cuda, down, stride, monkeypatch):
     assert _rel(y1, y0) < 2e-2 and _rel(gx1, gx0) < 3e-2
     for a, b in zip(gp1, gp0):
         assert _rel(a, b) < 3e-2
+
+
+def test_stem_pixel_chunk_plan_matches_conv2d():
+    """Stem mode: NHWC8 input, one K-step per filter row = 8 consecutive pixels x 8 channels."""
+    torch.manual_seed(3)
+    N, H, co = 2, 12, 64
+    x = torch.randn(N, 3, H, H)
+    w = torch.randn(co, 3, 7, 7)
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    x8 = CV.to_nhwc8(x)                                        # [N, 8, H, W] channels_last
+    assert x8.shape == (N, 8, H, H) and x8.is_contiguous(memory_format=torch.channels_last)
+    Wm = CV.stem_weight(w)                                     # [co, 7 * 64]
+    taps = CV._stem_taps(7, (3, 3))
+    Ho = CV.out_size(H, 7, 2, 3)
+    xs = x8.permute(0, 2, 3, 1)
+    b = torch.arange(N).view(-1, 1, 1).expand(N, Ho, Ho).reshape(-1)
+    y = torch.arange(Ho).view(1, -1, 1).expand(N, Ho, Ho).reshape(-1)
+    xx = torch.arange(Ho).view(1, 1, -1).expand(N, Ho, Ho).reshape(-1)
+    cols = []
+    for t in range(7):
+        for p in range(8):                                     # chunk p = pixel step p
+            iy, ix = 2 * y + taps[2 * t], 2 * xx + taps[2 * t + 1] + p
+            ok = (iy >= 0) & (iy < H) & (ix >= 0) & (ix < H)
+            g = torch.zeros(b.numel(), 8)
+            g[ok] = xs[b[ok], iy[ok], ix[ok]]
+            cols.append(g)
+    out = (torch.cat(cols, 1) @ Wm.t()).view(N, Ho, Ho, co).permute(0, 3, 1, 2)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_stem_kernels_match_fp32_reference(cuda):
+    torch.manual_seed(5)
+    x = torch.randn(4, 3, 40, 40, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = _nhwc((torch.randn(64, 3, 7, 7, device=cuda) * 0.1).to(torch.bfloat16))
+    wr = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wr, stride=2, padding=3)
+    dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
+    ref.backward(dy.float())
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(cuda, torch.bfloat16)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+    assert CV.stem_eligible(x, conv)
+    y = CV.stem_conv(x, conv)
+    assert _rel(y, ref) < 1e-2
+    x8 = CV.to_nhwc8(x)
+    dw = CV.stem_wgrad(dy, x8, w.shape, (2, 2), (3, 3))
+    assert _rel(dw, wr.grad) < 1e-2

@@ -303,3 +303,106 @@ def test_scaling_by_node_type_routes_metrics_and_bundles():
     assert sum(1 for r in reqs if r.get("GPU") == 8) == 2               # time table: 2 GPU nodes
     assert sum(1 for r in reqs if r.get("CPU") == 64 and "GPU" not in r) == 1   # load 0.94 > 0.5: +1 step
     assert set(st.node_resource_states) == {"n1", "n2", "n3"}
+
+
+def _docker(c):
+    c["docker"] = {"enabled": True, "image": "cloudtik/ai-rocm:latest", "container_name": "cloudtik-ai"}
+    c["provider"]["cache_stopped_nodes"] = True
+    c["available_node_types"]["cpu.small"].update(min_workers=1, max_workers=1)
+
+
+def test_setup_commands_with_stopped_node_caching_docker(state):
+    """Reference tests/unit/test_cloudtik.py:1507: with docker, a node restarted from the
+    stopped-node cache keeps its runtime hash but its container is gone, so the container is
+    started again (docker run) and the initialization + setup commands run again inside it."""
+    name = "sc-docker-cache"
+    cfg, provider, scaler = _setup(name, state, _docker)
+    runner = provider.runner
+    scaler.update()
+    (w,) = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    cmds = runner.commands_for(w)
+    assert any(c.startswith("docker pull cloudtik/ai-rocm:latest") for c in cmds)
+    assert any(c.startswith("docker run") and "cloudtik/ai-rocm:latest" in c for c in cmds)
+    setup_cmds = [c for c in cmds if "docker exec" in c and "runtime install ai" in c]
+    assert setup_cmds                                    # setup ran INSIDE the container
+    rh = provider.node_tags(w)[T.CLOUDTIK_TAG_RUNTIME_CONFIG]
+
+    # stop the node (cached, not terminated); the scaler relaunches it from the cache
+    provider.terminate_node(w)
+    assert _workers(provider, name) == []
+    runner.clear_history()
+    scaler.update()
+    (w2,) = _workers(provider, name)
+    assert w2 == w                                      # the SAME node came back
+    cmds = runner.commands_for(w)
+    assert any(c.startswith("docker run") for c in cmds)
+    assert any("docker exec" in c and "runtime install ai" in c for c in cmds)
+    assert provider.node_tags(w)[T.CLOUDTIK_TAG_RUNTIME_CONFIG] == rh
+    assert provider.node_tags(w)[T.CLOUDTIK_TAG_NODE_STATUS] == T.STATUS_UP_TO_DATE
+
+    # container still running with the right image and mounts: nothing is re-run
+    runner.respond_to_call(".State.Running", ["true"])
+    runner.respond_to_call(".Config.Image", ["cloudtik/ai-rocm:latest"])
+    runner.respond_to_call("json .Mounts", ["[]"])
+    runner.clear_history()
+    from cloudtik_amd.core.cluster_utils import create_updater
+    u = create_updater(cfg, provider, w, is_head=False, head_ip="10.0.0.1")
+    u.run()
+    cmds = runner.commands_for(w)
+    assert u.exitcode == 0 and not any(c.startswith("docker run") for c in cmds)
+    assert not any("runtime install ai" in c for c in cmds)
+
+
+def test_docker_container_restarted_when_image_changes(state):
+    name = "sc-docker-image"
+    cfg, provider, scaler = _setup(name, state, _docker)
+    runner = provider.runner
+    scaler.update()
+    (w,) = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    runner.respond_to_call(".State.Running", ["true"])
+    runner.respond_to_call(".Config.Image", ["cloudtik/ai-rocm:old"])     # drifted
+    runner.respond_to_call("json .Mounts", ["[]"])
+    runner.clear_history()
+    from cloudtik_amd.core.cluster_utils import create_updater
+    u = create_updater(cfg, provider, w, is_head=False, head_ip="10.0.0.1")
+    u.run()
+    cmds = runner.commands_for(w)
+    assert u.exitcode == 0
+    stop = [i for i, c in enumerate(cmds) if c.startswith("docker stop cloudtik-ai")]
+    run = [i for i, c in enumerate(cmds) if c.startswith("docker run")]
+    assert stop and run and stop[0] < run[0]
+    assert any("docker exec" in c and "runtime install ai" in c for c in cmds)
+
+
+def test_docker_file_mounts_bind_mounted_and_pull_policy(state, tmp_path):
+    name = "sc-docker-mounts"
+    src = tmp_path / "data"
+    src.mkdir()
+
+    def mut(c):
+        _docker(c)
+        c["file_mounts"] = {"/root/test-folder": str(src)}
+        c["docker"]["pull_before_run"] = False
+
+    cfg, provider, scaler = _setup(name, state, mut)
+    runner = provider.runner
+    scaler.update()
+    (w,) = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    cmds = runner.commands_for(w)
+    host_loc = f"/tmp/cloudtik_docker_mounts/{name}/root/test-folder"
+    assert any(c.startswith("rsync-up") and host_loc in c for c in cmds)       # synced to the host location
+    run = [c for c in cmds if c.startswith("docker run")][0]
+    assert f"-v {host_loc}:/root/test-folder" in run                          # bind-mounted into the container
+    assert any("image inspect cloudtik/ai-rocm:latest" in c and "|| docker pull" in c for c in cmds)
+    assert not any(c.startswith("docker pull") for c in cmds)
+    # a running container that lacks a requested mount is restarted
+    runner.respond_to_call(".State.Running", ["true"])
+    runner.respond_to_call(".Config.Image", ["cloudtik/ai-rocm:latest"])
+    runner.respond_to_call("json .Mounts", ['[{"Destination": "/some/other"}]'])
+    runner.clear_history()
+    from cloudtik_amd.core.cluster_utils import create_updater
+    u = create_updater(cfg, provider, w, is_head=False, head_ip="10.0.0.1")
+    u.run()
+    cmds = runner.commands_for(w)
+    assert u.exitcode == 0 and any(c.startswith("docker stop") for c in cmds) and any(
+        c.startswith("docker run") for c in cmds)
