@@ -120,7 +120,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), padding=(0, 0), ou
     part = None
     if stats or partials:
         bm = C.conv_igemm_tile_m(_CFG, co, geo[11], len(taps) // 2 * (x.shape[1] // 64))
-        part = torch.empty(((geo[11] + bm - 1) // bm) * 2 * co, device=x.device, dtype=torch.float32)
+        tiles = (geo[11] + bm - 1) // bm
+        # + room for the first-level merge of the BatchNorm finalize (batchnorm.hip)
+        part = torch.empty((tiles + (tiles + 63) // 64) * 2 * co, device=x.device, dtype=torch.float32)
     ok = C.conv_igemm(x, weight_rows(w).contiguous(), out, geo, taps, accumulate, part, _CFG)
     if not ok:
         raise RuntimeError(f"conv_igemm rejected x{tuple(x.shape)} w{tuple(w.shape)} s{stride} p{padding}")
@@ -166,6 +168,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
 _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256)}
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
+WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
 
 
 def wgrad_plan(M: int, co: int, nn: int, cfg: int):
@@ -173,7 +176,7 @@ def wgrad_plan(M: int, co: int, nn: int, cfg: int):
     and at least 256 deep, the fp32 partials capped at PARTIAL_BYTES."""
     bm, bn = _WG_TILES[cfg]
     tiles = (co // bm) * (nn // bn)
-    splits = max(1, min(512 // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
+    splits = max(1, min(WGRAD_BLOCKS // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
     rows = ((M + splits - 1) // splits + 31) // 32 * 32
     return (M + rows - 1) // rows, rows
 

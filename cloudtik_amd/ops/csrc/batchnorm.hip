@@ -593,6 +593,47 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
   return 0;
 }
 
+// First-level Chan merge of per-tile (mean, M2) partials: block (g, cb) merges tiles
+// [g * GROUP, (g + 1) * GROUP) of channels [64 cb, 64 cb + 64) -- one lane per channel, the 4
+// waves take interleaved tiles and are merged through LDS -- into one (mean, M2) partial of
+// GROUP * rows_per_tile rows.  The conv epilogue emits one partial per 128-row tile (6272 for a
+// ResNet-50 layer-1 conv); the single-block-per-64-channels finalize read them serially.
+constexpr int BN_MERGE_GROUP = 64;
+__global__ __launch_bounds__(256) void bn_partials_merge_kernel(const float* __restrict__ pmean,
+                                                               const float* __restrict__ pm2, int tiles,
+                                                               int rows_per_tile, int M, int C,
+                                                               float* __restrict__ omean, float* __restrict__ om2) {
+  __shared__ float sn[4][64], sm[4][64], sq[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane, g = blockIdx.x;
+  const int t0 = g * BN_MERGE_GROUP, t1 = min(tiles, t0 + BN_MERGE_GROUP);
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  if (c < C) {
+    for (int t = t0 + w; t < t1; t += 4) {
+      const float nb = (float)min(rows_per_tile, M - t * rows_per_tile);
+      const float mb = pmean[(size_t)t * C + c], qb = pm2[(size_t)t * C + c];
+      const float nn = n + nb, d = mb - mean;
+      mean += d * nb / nn;
+      m2 += qb + d * d * n * nb / nn;
+      n = nn;
+    }
+  }
+  sn[w][lane] = n; sm[w][lane] = mean; sq[w][lane] = m2;
+  __syncthreads();
+  if (w != 0 || c >= C) return;
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const float nb = sn[k][lane];
+    if (nb <= 0.f) continue;
+    const float nn = n + nb, d = sm[k][lane] - mean;
+    mean += d * nb / nn;
+    m2 += sq[k][lane] + d * d * n * nb / nn;
+    n = nn;
+  }
+  omean[(size_t)g * C + c] = mean;
+  om2[(size_t)g * C + c] = m2;
+}
+
 // Training forward whose statistics were produced by the PRODUCER of x: per-tile means
 // [tiles][C] and M2 [tiles][C] over rows_per_tile rows each (the implicit-GEMM conv epilogue,
 // conv.hip).  Only the finalize and the apply pass run: x is read once instead of twice.
@@ -601,6 +642,17 @@ extern "C" int ct_bn_fwd_train_given(const void* x, const void* res, const void*
                                      int rows_per_tile, float* stat, int M, int C, float eps, float momentum,
                                      int relu, hipStream_t stream) {
   if (C % 8 || M <= 0 || tiles <= 0 || (long)tiles * rows_per_tile < M) return -1;
+  if (tiles > 2 * BN_MERGE_GROUP) {
+    // merge groups of tiles first, into the tail of the partial buffer (means at
+    // part + 2 tiles C, then the M2 rows): the finalize then reads at most 2 * GROUP partials
+    const int groups = ceil_div(tiles, BN_MERGE_GROUP);
+    float* om = const_cast<float*>(part) + (size_t)2 * tiles * C;
+    bn_partials_merge_kernel<<<dim3(groups, ceil_div(C, 64)), 256, 0, stream>>>(
+        part, part + (size_t)tiles * C, tiles, rows_per_tile, M, C, om, om + (size_t)groups * C);
+    part = om;
+    tiles = groups;
+    rows_per_tile *= BN_MERGE_GROUP;
+  }
   BnLayout L{M, C, C / 8, 1, rows_per_tile};
   bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)tiles * C, tiles, L,
                                                            (const bf16_t*)gamma, (const bf16_t*)beta,

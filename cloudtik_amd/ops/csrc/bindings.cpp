@@ -462,7 +462,9 @@ std::vector<at::Tensor> bn_fwd_train_given(at::Tensor x, c10::optional<at::Tenso
   TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
   CHECK_F32(run_mean); CHECK_F32(run_var); CHECK_IN(part); CHECK_F32(part);
   const long tiles = (M + rows_per_tile - 1) / rows_per_tile;
-  TORCH_CHECK(part.numel() >= 2 * tiles * C, "bn_fwd_train_given: part buffer");
+  // the tail holds the first-level merge (ct_bn_fwd_train_given) when there are many tiles
+  TORCH_CHECK(part.numel() >= 2 * (tiles + (tiles > 128 ? (tiles + 63) / 64 : 0)) * C,
+              "bn_fwd_train_given: part buffer");
   auto y = at::empty_like(x);
   auto stat = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
   int rc = ct_bn_fwd_train_given(x.data_ptr(), optr(res), gamma.data_ptr(), beta.data_ptr(),
