@@ -63,13 +63,16 @@ def aliyun_sign(params: Dict[str, str], secret: str, method: str = "GET") -> str
     return base64.b64encode(mac).decode()
 
 
-def aliyun_transport(endpoint: str, ak: str, sk: str, timeout_s: float = 60.0) -> Callable[[str, Dict], Dict]:
+def aliyun_transport(endpoint: str, ak: str, sk: str, timeout_s: float = 60.0,
+                     version: str = _ECS_VERSION) -> Callable[[str, Dict], Dict]:
+    """RPC caller of one product (``endpoint`` + API ``version``: ECS 2014-05-26, VPC
+    2016-04-28, RAM 2015-05-01)."""
     import requests
     session = requests.Session()
 
     def call(action: str, params: Dict[str, Any]) -> Dict[str, Any]:
         q = {k: str(v) for k, v in params.items()}
-        q.update(Action=action, Format="JSON", Version=_ECS_VERSION, AccessKeyId=ak, SignatureMethod="HMAC-SHA1",
+        q.update(Action=action, Format="JSON", Version=version, AccessKeyId=ak, SignatureMethod="HMAC-SHA1",
                  SignatureVersion="1.0", SignatureNonce=uuid.uuid4().hex,
                  Timestamp=_dt.datetime.now(_dt.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"))
         q["Signature"] = aliyun_sign(q, sk)

@@ -5,8 +5,10 @@ A managed bucket / database belongs to a workspace: these providers run only the
 steps of the workspace's step plan (providers/cloud/workspace.py) -- GCS bucket / Cloud SQL,
 ADLS Gen2 account + container / MySQL flexible server, S3 bucket / RDS -- so ``cloudtik
 storage create`` and ``cloudtik workspace create`` with ``managed_cloud_storage`` build the
-same resource.  Aliyun / Huawei Cloud storage is not managed here: the hdfs / minio / mysql /
-postgres runtimes serve those clusters."""
+same resource; Aliyun / Huawei Cloud manage an OSS / OBS bucket the same way
+(providers/cloud/signed_workspace.py; reference aliyun/storage_provider.py,
+huaweicloud/storage_provider.py).  Neither of those two clouds has a managed database in the
+reference: the mysql / postgres runtimes serve their clusters."""
 from __future__ import annotations
 
 from cloudtik_amd.core.provider_api import DatabaseProvider, StorageProvider
@@ -23,6 +25,9 @@ class _ManagedSteps:
                                       f"{'hdfs or minio' if self.KIND == 'storage' else 'mysql or postgres'} runtime")
         flags = {"managed_cloud_storage": self.KIND == "storage", "managed_cloud_database": self.KIND == "database"}
         steps = [s for s in plan.steps(dict(config.get("provider", {}), **flags)) if s.managed == self.KIND]
+        if not steps:
+            raise NotImplementedError(f"managed {self.KIND} on {self.provider_config.get('type')}: use the "
+                                      f"{'hdfs or minio' if self.KIND == 'storage' else 'mysql or postgres'} runtime")
         return plan, WorkspaceBuilder(steps, log=lambda m: print(f"[{self.KIND}] {m}", flush=True))
 
     def create(self, config):

@@ -20,7 +20,10 @@ Clouds:
   user-assigned identities + role assignments, ADLS Gen2 storage account + container,
   MySQL flexible server);
 * AWS over boto3 clients (VPC, subnets, internet gateway, NAT gateway, route tables,
-  security group, IAM roles + instance profiles, S3 bucket, RDS instance).
+  security group, IAM roles + instance profiles, S3 bucket, RDS instance);
+* Aliyun and Huawei Cloud over their signed HTTP APIs (providers/cloud/signed_workspace.py:
+  VPC, VSwitch / subnet, NAT gateway + EIP + SNAT, security group, RAM roles / IAM agencies,
+  OSS / OBS bucket).
 """
 from __future__ import annotations
 
@@ -709,6 +712,12 @@ def cloud_workspace(provider_config: Dict[str, Any], workspace_name: str, transp
         return AzureWorkspace(provider_config, workspace_name, call)
     if t == "aws":
         return AWSWorkspace(provider_config, workspace_name, transport or provider_config.get("_client_factory"))
+    if t == "aliyun":
+        from cloudtik_amd.providers.cloud.signed_workspace import AliyunWorkspace
+        return AliyunWorkspace(provider_config, workspace_name, transport)
+    if t == "huaweicloud":
+        from cloudtik_amd.providers.cloud.signed_workspace import HuaweiCloudWorkspace
+        return HuaweiCloudWorkspace(provider_config, workspace_name, transport)
     if t == "kubernetes":
         from cloudtik_amd.providers.kubernetes.workspace import Kubectl, KubernetesWorkspace
         kubectl = provider_config.get("_kubectl") or Kubectl(provider_config.get("kubectl"))

@@ -7,7 +7,8 @@ workspace is declared on an existing network (``provider.use_working_vpc`` /
 ``use_existing_network``) -- then only the registry below is set up.  The workspace-wide
 service registry (publish / subscribe global variables) is the same shared JSON state for
 every provider type, so service discovery between clusters of one workspace is provider
-independent.  Aliyun / Huawei Cloud workspaces run on existing networks; a Kubernetes
+independent.  Aliyun / Huawei Cloud workspaces are step plans over the clouds' signed APIs
+(providers/cloud/signed_workspace.py); a Kubernetes
 workspace is its namespace, service accounts and RBAC plus the EKS / GKE / AKS workload
 identity of the pods (providers/kubernetes/workspace.py)."""
 from __future__ import annotations
