@@ -31,7 +31,6 @@ int ct_rnnt_fwd(const void*, int, const int*, const int*, const int*, float*, fl
                 int, int, int, hipStream_t);
 int ct_rnnt_bwd(const void*, int, const int*, const int*, const int*, const float*, const float*, const float*,
                 const float*, const float*, const float*, void*, int, int, int, int, int, hipStream_t);
-int ct_gemm_tn(const void*, long, const void*, long, void*, int, int, long, int, int, hipStream_t);
 int ct_mt_copy(const uint64_t*, const int64_t*, const int64_t*, int, long, void*, int, int, float, int, hipStream_t);
 int ct_mt_add(const int64_t*, int, int, hipStream_t);
 void* ct_loader_create(int, const void* const*, const long*, long, int, int, uint64_t, int, int, int, int, int, int);
@@ -220,22 +219,6 @@ at::Tensor nms_segmented(at::Tensor boxes, at::Tensor seg_offsets, double thr, d
 // out[M, N] (+)= A[T, M]^T B[T, N] (bf16 operands, fp32 accumulation).  mode 0: out is fp32
 // [splits, M, N] partials; 1: bf16 out += result; 2: bf16 out = result.  Returns false (and
 // launches nothing) for shapes the kernel does not tile (M, N % 256, T % (64 * splits)).
-bool gemm_tn(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, int64_t mode) {
-  XCHECK_CUDA(A); XCHECK_CUDA(B); XCHECK_CUDA(out);
-  XCHECK_DT(A, at::kBFloat16); XCHECK_DT(B, at::kBFloat16);
-  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(0) == B.size(0), "gemm_tn: A [T, M], B [T, N]");
-  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && out.is_contiguous(), "gemm_tn: row-major operands");
-  const long T = A.size(0), M = A.size(1), N = B.size(1);
-  if (mode == 0) {
-    XCHECK_DT(out, at::kFloat);
-    TORCH_CHECK(out.numel() == splits * M * N, "gemm_tn: partials must be [splits, M, N]");
-  } else {
-    XCHECK_DT(out, at::kBFloat16);
-    TORCH_CHECK(out.numel() == M * N && splits == 1, "gemm_tn: out must be [M, N] with one split");
-  }
-  return ct_gemm_tn(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), out.data_ptr(), (int)M, (int)N, T,
-                    (int)splits, (int)mode, stream()) == 0;
-}
 
 void check_rois(const at::Tensor& feat, const at::Tensor& rois) {
   XCHECK_IN(feat); XCHECK_IN(rois); XCHECK_DT(rois, at::kFloat);
@@ -566,7 +549,6 @@ void register_ext(pybind11::module& m) {
   m.def("interact_bwd", &interact_bwd);
   m.def("nms_sorted", &nms_sorted);
   m.def("nms_segmented", &nms_segmented);
-  m.def("gemm_tn", &gemm_tn);
   m.def("roi_align_fwd", &roi_align_fwd);
   m.def("roi_align_bwd", &roi_align_bwd);
   m.def("roi_align_nhwc_fwd", &roi_align_nhwc_fwd);

@@ -313,7 +313,31 @@ bool gemm_nt(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumul
   return rc == 0;
 }
 
+extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, hipStream_t);
+
+// out[M,N] = A[K,M]^T @ B[K,N] through the MFMA kernel's weight-gradient layout: splits > 1 ->
+// out is fp32 [splits, M, N] (partial slabs); splits == 1 -> bf16 [M, N] (+)= result.
+bool gemm_tn2(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool accumulate) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && out.is_cuda(), "gemm_tn2: GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_tn2: bf16 operands");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B), "gemm_tn2: 2-D row-major operands");
+  const long K = A.size(0), M = A.size(1), N = B.size(1);
+  TORCH_CHECK(B.size(0) == K, "gemm_tn2: K mismatch");
+  long ldo = 0;
+  if (splits > 1) {
+    TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 3 && out.size(0) == splits &&
+                out.size(1) == M && out.size(2) == N, "gemm_tn2: fp32 [splits, M, N] slabs");
+  } else {
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16 && rowmajor_ok(out) && out.size(0) == M && out.size(1) == N,
+                "gemm_tn2: bf16 [M, N] out");
+    ldo = out.stride(0);
+  }
+  return ct_gemm_tn2(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), out.data_ptr(), ldo, (int)M, (int)N, K,
+                     (int)splits, accumulate ? 1 : 0, at::hip::getCurrentHIPStream().stream()) == 0;
+}
+
 void register_lt(pybind11::module& m) {
+  m.def("gemm_tn2", &gemm_tn2, "weight-gradient GEMM A^T @ B (token-major operands) on the MFMA kernel");
   m.def("gemm_nt", &gemm_nt, "hand-written MFMA GEMM A @ B^T with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
   m.def("lt_bmm_tuned", &lt_bmm_tuned, "strided-batched hipBLASLt GEMM, algorithm picked by timing all solutions");

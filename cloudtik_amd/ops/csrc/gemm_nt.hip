@@ -19,9 +19,14 @@
 //   * exactly one half-tile DMA (2 glds per wave) and one counted vmcnt(8) per phase, four
 //     halves in flight; fragment reads 12 / 4 / 8 / 0 per phase (schedule: nt_stage_slot);
 //   * the MFMA is issued as B-fragment x A-fragment, so each lane ends up with 4 consecutive
-//     output COLUMNS of one row: 8-byte stores, and the bias / aux vectors load 8 bytes too;
+//     output COLUMNS of one row; a permlane16 swap between column blocks turns them into 8
+//     consecutive columns for 16-byte stores (nt_pair_swap);
 //   * blockIdx -> tile goes through the bijective XCD remap; N-tiles vary fastest so the
 //     blocks resident on one XCD share A panels in its L2.
+//   * staging through registers (global_load_dwordx4 + ds_write_b128 a few phases later) was
+//     measured 10 % slower than the LDS-DMA once the DMA's bases are wave-uniform SGPRs.
+// The same kernel runs the weight-gradient layout (TN: both operands token-major, transposing
+// LDS reads, split-K into fp32 slabs; ct_gemm_tn2).
 // Reference: the BERT encoder FFN (HF BertIntermediate + BertOutput).
 #include "common.h"
 #include <cstdlib>
@@ -37,7 +42,7 @@ constexpr int NT_ROWB = NT_BK * 2;        // 128 B per LDS image row
 constexpr int NT_HALF = 128 * NT_ROWB;    // 16 KiB: 128 rows of one operand
 constexpr int NT_BUF = 4 * NT_HALF;       // 64 KiB per K-tile buffer
 
-enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2 };
+enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2, NT_EPI_F32_SLAB = 3 };
 
 struct NtArgs {
   const bf16_t* A;
@@ -46,7 +51,9 @@ struct NtArgs {
   const bf16_t* bias;   // EPI 1: [N]; EPI 2 (optional): added to aux before gelu'
   bf16_t* aux;          // EPI 1: pre-activation out; EPI 2: pre-activation in
   float* dbias;         // EPI 2: [N] fp32, accumulated with atomics (may be null)
+  float* P;             // EPI 3: fp32 split-K slabs [splits][M][N]
   long lda, ldb, ldd, ldaux;
+  long tsplit;          // TN: reduction length per split
   int M, N, K;
   int accumulate;       // EPI 0: D += result
 };
@@ -86,6 +93,44 @@ __device__ __forceinline__ nt_s16x8 nt_frag(const char* img, int r0, int ks, int
   return *(const nt_lds_s16x8*)(img + row * NT_ROWB + ((kc ^ nt_swz(row)) << 4));
 }
 
+// ---- TN layout (weight gradients: D[M, N] = A[K, M]^T B[K, N], K = tokens is the row index of
+// both operands).  A half-tile image is 64 k-rows x 128 columns (256 B rows): the same 16 KiB
+// and the same column sets per half as the NT images' rows, so the phase schedule, the
+// fragment indices and the epilogue are shared; only staging and fragment reads differ.
+// Fragments need 8 consecutive k per lane: two ds_read_b64_tr_b16 (gfx950's transposing LDS
+// read) per 16 x 32 fragment.  Chunk swizzle of 256-B row r: rows r..r+3 and r+8..r+11 land in
+// 8 distinct 32-B bank slots for the transposing reads.
+constexpr int TN_ROWB = 256;
+__device__ __forceinline__ int tn_swz(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
+
+typedef __attribute__((ext_vector_type(4))) short tn_s16x4;
+typedef __attribute__((address_space(3))) tn_s16x4 tn_lds_s16x4;
+
+// fragment of image columns [c0, c0 + 16) x k [32 ks, 32 ks + 32): lane l gets column
+// c0 + (l & 15), k 32 ks + 8 (l >> 4) .. + 8 -- the nt_frag lane layout
+__device__ __forceinline__ nt_s16x8 tn_frag(const char* img, int c0, int ks, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = 32 * ks + 8 * g + q, r1 = r0 + 4;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const char* a0 = img + r0 * TN_ROWB + ((ch ^ tn_swz(r0)) << 4) + ((p & 1) << 3);
+  const char* a1 = img + r1 * TN_ROWB + ((ch ^ tn_swz(r1)) << 4) + ((p & 1) << 3);
+  const tn_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tn_lds_s16x4*)a0);
+  const tn_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tn_lds_s16x4*)a1);
+  return nt_s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// per-lane byte offset of a TN staging piece (4 image rows of 256 B = one glds): lane l fills
+// LDS chunk (l & 15) of row 4 piece + (l >> 4) with global chunk (l & 15) ^ swizzle; the
+// swizzle depends on the piece only through (piece >> 1) & 1 = wave & 1.  Image chunk c ->
+// operand column: A halves hold tile columns {0-63, 128-191} (+64 for A1), B halves the
+// first (B0) or second (B1) 32 of each 64-column wave block.
+__device__ __forceinline__ unsigned tn_lane_off(long ld, int wave, int lane, bool isA) {
+  const int q = lane >> 4;
+  const int c = (lane & 15) ^ tn_swz(q + 8 * (wave & 1));
+  const int col = isA ? (c < 8 ? c * 8 : 128 + (c - 8) * 8) : (c >> 2) * 64 + (c & 3) * 8;
+  return (unsigned)((q * ld + col) * 2);
+}
+
 __device__ __forceinline__ void nt_bar() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
@@ -116,20 +161,39 @@ __device__ __forceinline__ void nt_mma_end() {
 // landed, and it is first read 5 phases after its issue (one phase after the wait, as the
 // barrier offset between the wave groups requires); a half is restaged >= 2 phases after its
 // last read (WAR for the group that runs ahead).
-__device__ __forceinline__ void nt_stage_slot(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B,
-                                              long ldb, long m0, long n0, long k0, int slot, char* dst, int wave,
-                                              int lane) {
+struct NtCtx {
+  const bf16_t* A;
+  const bf16_t* B;
+  long lda, ldb, m0, n0, kbase;   // kbase: first k of this split (TN)
+  char* lds;
+  int wave, lane, ra, rb;
+  unsigned offa0, offa1, offb0, offb1;   // per-lane staging offsets (NT: by piece parity; TN: A / B)
+};
+
+template <bool TN>
+__device__ __forceinline__ void nt_stage_slot(const NtCtx& c, long k0, int slot, char* dst) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int piece = wave * 2 + i;                      // image rows piece*8 .. +8
+    const int piece = c.wave * 2 + i;
     const bf16_t* base;
     unsigned off;
-    if (slot == 0 || slot == 3) {                        // A0 / A1
-      base = A + (m0 + ((piece >> 3) << 7) + (slot == 3 ? 64 : 0) + (piece & 7) * 8) * lda + k0;
-      off = nt_lane_off(lda, i, lane);
-    } else {                                             // B0 / B1
-      base = B + (n0 + ((piece >> 2) << 6) + (slot == 2 ? 32 : 0) + (piece & 3) * 8) * ldb + k0;
-      off = nt_lane_off(ldb, i, lane);
+    if constexpr (!TN) {
+      if (slot == 0 || slot == 3) {                        // A0 / A1: image rows piece*8 .. +8
+        base = c.A + (c.m0 + ((piece >> 3) << 7) + (slot == 3 ? 64 : 0) + (piece & 7) * 8) * c.lda + k0;
+        off = i ? c.offa1 : c.offa0;
+      } else {                                             // B0 / B1
+        base = c.B + (c.n0 + ((piece >> 2) << 6) + (slot == 2 ? 32 : 0) + (piece & 3) * 8) * c.ldb + k0;
+        off = i ? c.offb1 : c.offb0;
+      }
+    } else {
+      const long krow = c.kbase + k0 + piece * 4;          // image rows 4 piece .. + 4
+      if (slot == 0 || slot == 3) {
+        base = c.A + krow * c.lda + c.m0 + (slot == 3 ? 64 : 0);
+        off = c.offa0;
+      } else {
+        base = c.B + krow * c.ldb + c.n0 + (slot == 2 ? 32 : 0);
+        off = c.offb0;
+      }
     }
     nt_glds16s(base, off, dst + piece * 1024);
   }
@@ -139,14 +203,6 @@ template <int N>
 __device__ __forceinline__ void nt_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-
-struct NtCtx {
-  const bf16_t* A;
-  const bf16_t* B;
-  long lda, ldb, m0, n0;
-  char* lds;
-  int wave, lane, ra, rb;
-};
 
 // one 16-MFMA quadrant: acc[I0 + i][J0 + j] += A-frags fa[QM] x B-frags fb[QN]
 template <int I0, int J0>
@@ -162,12 +218,17 @@ __device__ __forceinline__ void nt_quad(f32x4 (&acc)[8][4], const nt_s16x8 (&fa)
 }
 
 // half with virtual index v (see above) -> its buffer slot
+template <bool TN>
 __device__ __forceinline__ void nt_stage_v(const NtCtx& c, int v) {
   const int T = (v + 6) >> 2, slot = (v + 6) & 3;
-  nt_stage_slot(c.A, c.lda, c.B, c.ldb, c.m0, c.n0, (long)T * NT_BK, slot,
-                c.lds + (T & 1) * NT_BUF + slot * NT_HALF, c.wave, c.lane);
+  nt_stage_slot<TN>(c, (long)T * NT_BK, slot, c.lds + (T & 1) * NT_BUF + slot * NT_HALF);
 }
 
+template <bool TN>
+__device__ __forceinline__ nt_s16x8 nt_fragment(const char* img, int r0, int ks, int lane) {
+  if constexpr (TN) return tn_frag(img, r0, ks, lane);
+  else return nt_frag(img, r0, ks, lane);
+}
 
 // DMA plan of one K-tile t (POS: 0 steady, 1 = K-tile nk-2, 2 = the last K-tile): phase q
 // issues half v = 4t + q (virtual index, slot order A0 B0 B1 A1) and waits vmcnt(8) in steady
@@ -182,7 +243,7 @@ struct NtPlan {
   }
 };
 
-template <int POS, int DIAG>
+template <int POS, int DIAG, bool TN>
 __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][4], nt_s16x8 (&fa)[2][4][2],
                                          nt_s16x8 (&fb)[2][2][2]) {
   const char* buf = c.lds + (t & 1) * NT_BUF;
@@ -190,7 +251,7 @@ __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][
   constexpr bool DMA = DIAG == 0 || DIAG == 3;
   using P = NtPlan<POS>;
 #define NT_PHASE_TAIL(Q, I0, J0, FA, FB)                                             \
-  if constexpr (DMA && P::issue(Q)) nt_stage_v(c, 4 * t + Q);                        \
+  if constexpr (DMA && P::issue(Q)) nt_stage_v<TN>(c, 4 * t + Q);                    \
   if constexpr (WAIT) nt_vm<P::wait(Q)>();                                           \
   if constexpr (BAR) nt_mma_begin(); else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
   nt_quad<I0, J0>(acc, FA, FB);                                                      \
@@ -199,33 +260,60 @@ __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = nt_frag(buf + 1 * NT_HALF, c.rb + j * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = nt_fragment<TN>(buf + 1 * NT_HALF, c.rb + j * 16, ks, c.lane);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fa[0][i][ks] = nt_frag(buf + 0 * NT_HALF, c.ra + i * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fa[0][i][ks] = nt_fragment<TN>(buf + 0 * NT_HALF, c.ra + i * 16, ks, c.lane);
   NT_PHASE_TAIL(0, 0, 0, fa[0], fb[0])
   // ---- q1: B1 fragments
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = nt_frag(buf + 2 * NT_HALF, c.rb + j * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = nt_fragment<TN>(buf + 2 * NT_HALF, c.rb + j * 16, ks, c.lane);
   NT_PHASE_TAIL(1, 0, 2, fa[0], fb[1])
   // ---- q2: A1 fragments
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fa[1][i][ks] = nt_frag(buf + 3 * NT_HALF, c.ra + i * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fa[1][i][ks] = nt_fragment<TN>(buf + 3 * NT_HALF, c.ra + i * 16, ks, c.lane);
   NT_PHASE_TAIL(2, 4, 2, fa[1], fb[1])
   // ---- q3: no fragment reads
   NT_PHASE_TAIL(3, 4, 0, fa[1], fb[0])
 #undef NT_PHASE_TAIL
 }
 
+// 16-B stores from the MFMA layout: lane l holds 4 consecutive columns 16 j + 4 (l >> 4) .. + 3
+// of row (l & 15) in block j; v_permlane16_swap exchanges the odd 16-lane rows of block j with
+// the even rows of block j + 1, after which lane l holds 8 consecutive columns
+// 8 ((l >> 4) >> 1) .. + 7 of block j + ((l >> 4) & 1) -- one dwordx4 store instead of two
+// dwordx2 (the epilogue store tail is store-issue bound: MI355X_MICROARCH.md, attention epilogue
+// row; cdna_hip_programming.md T21).  Each store instruction then writes 16 rows x 64
+// contiguous bytes.
+__device__ __forceinline__ u16x8 nt_pair_swap(u16x4 x, u16x4 y) {
+  const uint2 xv = __builtin_bit_cast(uint2, x), yv = __builtin_bit_cast(uint2, y);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(xv.x, yv.x, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(xv.y, yv.y, false, false);
+  // after the swap this lane holds (s0[0], s1[0]) = columns c .. c+3, (s0[1], s1[1]) = c+4 .. c+7
+  const uint4 v = {s0[0], s1[0], s0[1], s1[1]};
+  return __builtin_bit_cast(u16x8, v);
+}
+
 // epilogue over one wave's accumulators: acc[i][j][r] holds D[mrow + 16i][ncol + 16j + r]
+// (ncol includes this lane's 4 (lane >> 4)); math in that layout, stores after the swap.
+// EPI 3 (fp32 split-K slab, row stride N): the lane's 4 columns are one 16-B store already.
 template <int EPI, bool BGRAD, int NJ>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[8][NJ], long mrow, long ncol,
-                                            int lane) {
+                                            int lane, int split) {
+  static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
+  if constexpr (EPI == NT_EPI_F32_SLAB) {
+    float* P = a.P + (long)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) *(f32x4*)(P + (mrow + i * 16) * a.N + ncol + j * 16) = acc[i][j];
+    return;
+  }
   float bv[NJ][4] = {};
   if (EPI == NT_EPI_BIAS_GELU_AUX || (EPI == NT_EPI_DGELU_BGRAD && a.bias)) {
 #pragma unroll
@@ -240,43 +328,48 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+  // column of this lane's 16-B chunk after the swap, relative to block 0 of the pair
+  const int g = lane >> 4;
+  const long scol = (ncol - 4 * g) + 16 * (g & 1) + 8 * (g >> 1);
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const long m = mrow + i * 16;
+    u16x4 out[NJ], pre[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const long n = ncol + j * 16;
-      bf16_t* dp = a.D + m * a.ldd + n;
-      u16x4 out;
       if constexpr (EPI == NT_EPI_PLAIN) {
         if (a.accumulate) {
-          const u16x4 old = *(const u16x4*)dp;
+          const u16x4 old = *(const u16x4*)(a.D + m * a.ldd + n);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r] + bf2f(old[r]));
+          for (int r = 0; r < 4; ++r) out[j][r] = f2bf(acc[i][j][r] + bf2f(old[r]));
         } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) out[r] = f2bf(acc[i][j][r]);
+          for (int r = 0; r < 4; ++r) out[j][r] = f2bf(acc[i][j][r]);
         }
       } else if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) {
-        u16x4 pre;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = acc[i][j][r] + bv[j][r];
-          pre[r] = f2bf(v);
-          out[r] = f2bf(gelu_erf(v));
+          pre[j][r] = f2bf(v);
+          out[j][r] = f2bf(gelu_erf(v));
         }
-        *(u16x4*)(a.aux + m * a.ldaux + n) = pre;
       } else {
         const u16x4 z = *(const u16x4*)(a.aux + m * a.ldaux + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float g = acc[i][j][r] * gelu_erf_grad(bf2f(z[r]) + bv[j][r]);
-          out[r] = f2bf(g);
-          if constexpr (BGRAD) cs[j][r] += g;
+          const float gg = acc[i][j][r] * gelu_erf_grad(bf2f(z[r]) + bv[j][r]);
+          out[j][r] = f2bf(gg);
+          if constexpr (BGRAD) cs[j][r] += gg;
         }
       }
-      *(u16x4*)dp = out;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; j += 2) {
+      const long n = scol + j * 16;
+      *(u16x8*)(a.D + m * a.ldd + n) = nt_pair_swap(out[j], out[j + 1]);
+      if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) *(u16x8*)(a.aux + m * a.ldaux + n) = nt_pair_swap(pre[j], pre[j + 1]);
     }
   }
   if constexpr (EPI == NT_EPI_DGELU_BGRAD && BGRAD) {
@@ -298,18 +391,31 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
 
 // DIAG (timing diagnostics only, wrong results): 1 = no DMA / vmcnt in the K loop (MFMA + LDS
 // reads + barriers), 2 = additionally no barriers (MFMA + LDS reads), 3 = DMA issued but never
-// waited for in the K loop
-template <int EPI, bool BGRAD, int DIAG = 0>
+// waited for in the K loop.  TN: the weight-gradient layout (blockIdx -> (split, tile)).
+template <int EPI, bool BGRAD, int DIAG = 0, bool TN = false>
 __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * NT_BUF];    // 128 KiB, the only LDS object
   const int tiles_n = a.N / NT_BN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = (a.M / NT_BM) * tiles_n;
+  int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = TN ? L / tiles : 0;
+  L -= split * tiles;
   const int tm = L / tiles_n, tn = L % tiles_n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: staging bases in SGPRs
   const int wr = wave >> 2, wc = wave & 3;
   const long m0 = (long)tm * NT_BM, n0 = (long)tn * NT_BN;
-  const int nk = a.K / NT_BK;
-  const NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, lds, wave, lane, wr * 64, wc * 32};
+  const int nk = (TN ? (int)a.tsplit : a.K) / NT_BK;
+  NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, (long)split * a.tsplit, lds, wave, lane, wr * 64, wc * 32, 0, 0, 0, 0};
+  if constexpr (TN) {
+    c.offa0 = c.offa1 = tn_lane_off(a.lda, wave, lane, true);
+    c.offb0 = c.offb1 = tn_lane_off(a.ldb, wave, lane, false);
+  } else {
+    c.offa0 = nt_lane_off(a.lda, 0, lane);
+    c.offa1 = nt_lane_off(a.lda, 1, lane);
+    c.offb0 = nt_lane_off(a.ldb, 0, lane);
+    c.offb1 = nt_lane_off(a.ldb, 1, lane);
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -322,10 +428,10 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
 
   // prologue: halves -6 .. -1 (all of K-tile 0, A0 + B0 of K-tile 1); wait for tile 0's A0, B0
 #pragma unroll
-  for (int v = -6; v < -2; ++v) nt_stage_v(c, v);
+  for (int v = -6; v < -2; ++v) nt_stage_v<TN>(c, v);
   if (nk > 1) {
-    nt_stage_v(c, -2);
-    nt_stage_v(c, -1);
+    nt_stage_v<TN>(c, -2);
+    nt_stage_v<TN>(c, -1);
     nt_vm<8>();
   } else {
     nt_vm<4>();
@@ -336,16 +442,16 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   // steady state: every phase issues one half and keeps 4 in flight; the last two K-tiles
   // drain (halves beyond 4 nk - 7 do not exist)
   int t = 0;
-  for (; t < nk - 2; ++t) nt_ktile<0, DIAG>(c, t, acc, fa, fb);
+  for (; t < nk - 2; ++t) nt_ktile<0, DIAG, TN>(c, t, acc, fa, fb);
   if (nk >= 2) {
-    nt_ktile<1, DIAG>(c, t, acc, fa, fb);
+    nt_ktile<1, DIAG, TN>(c, t, acc, fa, fb);
     ++t;
   }
-  nt_ktile<2, DIAG>(c, t, acc, fa, fb);
+  nt_ktile<2, DIAG, TN>(c, t, acc, fa, fb);
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 
   // acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
-  nt_epilogue<EPI, BGRAD, 4>(a, acc, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + (lane >> 4) * 4, lane);
+  nt_epilogue<EPI, BGRAD, 4>(a, acc, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + (lane >> 4) * 4, lane, split);
 }
 
 }  // namespace ct
@@ -360,15 +466,15 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
                           int epi, int accumulate, const void* bias, void* aux, long ldaux, float* dbias,
                           hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % NT_BM || N % NT_BN || K % NT_BK) return 1;
-  if (lda % 8 || ldb % 8 || ldd % 4 || lda < K || ldb < K || ldd < N) return 2;
-  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 7)) return 3;
+  if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < K || ldd < N) return 2;
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 15)) return 3;
   if (epi == 1 && (!bias || !aux || ((uintptr_t)bias & 7))) return 4;
-  if ((epi == 1 || epi == 2) && (!aux || ((uintptr_t)aux & 7) || ldaux % 4 || ldaux < N)) return 4;
+  if ((epi == 1 || epi == 2) && (!aux || ((uintptr_t)aux & 15) || ldaux % 8 || ldaux < N)) return 4;
   if (bias && ((uintptr_t)bias & 7)) return 4;
   const long blocks = (long)(M / NT_BM) * (N / NT_BN);
   if (blocks > (1L << 30)) return 5;
-  NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias,
-           lda, ldb, ldd, ldaux, M, N, K, accumulate};
+  NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias, nullptr,
+           lda, ldb, ldd, ldaux, 0, M, N, K, accumulate};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
   if (diag == 1) { gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
   if (diag == 2) { gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
@@ -382,5 +488,24 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
       break;
     default: return 6;
   }
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+// Weight-gradient layout: D[M,N] = A[K,M]^T . B[K,N] (row-major, K = tokens; lda >= M, ldb >= N).
+// splits > 1: fp32 partial slabs P[splits][M][N] (reduced by ct_splitk_reduce*); splits == 1:
+// bf16 out (+)= result (accumulate), row stride ldo.  Nonzero (nothing launched) when the
+// shape / alignment is unsupported.
+extern "C" int ct_gemm_tn2(const void* A, long lda, const void* B, long ldb, void* out, long ldo, int M, int N,
+                           long K, int splits, int accumulate, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || M % NT_BM || N % NT_BN) return 1;
+  if (K % ((long)splits * NT_BK)) return 2;
+  if (lda % 8 || ldb % 8 || lda < M || ldb < N || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return 3;
+  if (((uintptr_t)out & 15) || (splits == 1 && (ldo % 8 || ldo < N))) return 4;
+  const long blocks = (long)(M / NT_BM) * (N / NT_BN) * splits;
+  if (blocks > (1L << 30)) return 5;
+  NtArgs a{(const bf16_t*)A, (const bf16_t*)B, splits == 1 ? (bf16_t*)out : nullptr, nullptr, nullptr, nullptr,
+           splits > 1 ? (float*)out : nullptr, lda, ldb, ldo, 0, K / splits, M, N, (int)(K / splits), accumulate};
+  if (splits > 1) gemm_nt_kernel<NT_EPI_F32_SLAB, false, 0, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+  else gemm_nt_kernel<NT_EPI_PLAIN, false, 0, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }

@@ -25,8 +25,10 @@ _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 # gradients -- the bucketed all-reduce and the optimizer -- order themselves after this
 # stream via ``grad_stream_event()`` / ``sync_grad_stream()``.
 _WGRAD_STREAM = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM", "1") == "1"
-# weight-gradient GEMMs through the HIP gemm_tn kernel instead of hipBLASLt
-_HIP_WGRAD = os.environ.get("CLOUDTIK_AMD_WGRAD_KERNEL", "blas") == "hip"
+# weight-gradient GEMMs through the MFMA kernel's TN layout (csrc/gemm_nt.hip, ct_gemm_tn2)
+# instead of hipBLASLt's batched split-K GEMM: 13-17 % faster per BERT-large layer
+# (bench/gemm_tn2_probe.py); "blas" restores hipBLASLt
+_HIP_WGRAD = os.environ.get("CLOUDTIK_AMD_WGRAD_KERNEL", "hip") == "hip"
 # split-K partial GEMMs through the binding's strided-batched hipBLASLt call whose algorithm is
 # chosen by timing every solution once per shape (torch.bmm's heuristic pick is not tuned:
 # TunableOp skips bf16 -> fp32 batched GEMMs)
@@ -85,23 +87,44 @@ def splitk_factor(T: int, N: int, K: int) -> int:
     return S
 
 
+def tn2_splits(T: int, N: int, K: int, cus: int = 256) -> int:
+    """Split factor for the MFMA wgrad kernel: the fewest splits that minimise the number of
+    256-workgroup waves per unit of work, ceil(tiles * S / cus) / S (qkv 48 tiles -> 16,
+    proj 16 -> 16, FFN 64 -> 4), keeping >= 512 tokens per split; slab reduction cost grows
+    with S, so ties go to the smaller S."""
+    tiles = (N // 256) * (K // 256)
+    best, best_cost = 1, None
+    for S in (1, 2, 4, 8, 16, 32):
+        if T % (64 * S) or (S > 1 and T // S < 512):
+            continue
+        cost = -(-tiles * S // cus) / S
+        if best_cost is None or cost < best_cost - 1e-12:
+            best, best_cost = S, cost
+    return best
+
+
 def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
-    """g += dy2^T x2 (bf16 g, fp32 accumulation).  Split-K as one batched GEMM with fp32
-    partials + one fused reduce-accumulate HIP kernel when the plain GEMM under-fills the
-    GPU; otherwise hipBLASLt's beta=1 epilogue does the accumulation."""
+    """g += dy2^T x2 (bf16 g, fp32 accumulation).  The MFMA kernel's TN layout with split-K
+    fp32 slabs + one fused reduce-accumulate kernel (or, unsplit, accumulating straight into
+    g); otherwise hipBLASLt's batched split-K GEMM, or its beta=1 epilogue when one split
+    fills the GPU."""
     T, N = dy2.shape
     K = x2.shape[1]
-    S = splitk_factor(T, N, K) if (g.is_cuda and g.dtype == torch.bfloat16 and g.is_contiguous()) else 1
-    if _HIP_WGRAD and S > 1 and N % 256 == 0 and K % 256 == 0 and T % (64 * S) == 0:
-        # hand-written MFMA kernel (csrc/gemm.hip): fp32 slabs straight from the [T, N] / [T, K]
-        # operands through transposing LDS reads; parity with hipBLASLt on the BERT shapes
-        # (bench/gemm_tn_probe.py), so opt-in
+    if (_HIP_WGRAD and g.is_cuda and g.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16
+            and N % 256 == 0 and K % 256 == 0 and T % 64 == 0):
         from cloudtik_amd import ops
         C = ops.require_native()
-        P = torch.empty(S, N, K, device=g.device, dtype=torch.float32)
-        if C.gemm_tn(dy2.contiguous(), x2.contiguous(), P, S, 0):
-            C.splitk_reduce(P, g, True)
-            return
+        S = tn2_splits(T, N, K)
+        dy2c, x2c = dy2.contiguous(), x2.contiguous()
+        if S == 1:
+            if C.gemm_tn2(dy2c, x2c, g, 1, True):
+                return
+        else:
+            P = torch.empty(S, N, K, device=g.device, dtype=torch.float32)
+            if C.gemm_tn2(dy2c, x2c, P, S, False):
+                C.splitk_reduce(P, g, True)
+                return
+    S = splitk_factor(T, N, K) if (g.is_cuda and g.dtype == torch.bfloat16 and g.is_contiguous()) else 1
     if S == 1:
         g.addmm_(dy2.t(), x2)
         return

@@ -39,8 +39,27 @@ def _C():
 _FUSED_FFN_DGRAD = os.environ.get("CLOUDTIK_AMD_FUSED_FFN_DGRAD", "0") == "1"
 
 
+# FFN1 forward through the same GEMM with the bias + GELU epilogue: h = gelu(x W1^T + b1) and the
+# biased pre-activation kept for backward, instead of hipBLASLt + a bias_act_fwd pass
+_FUSED_FFN_FWD = os.environ.get("CLOUDTIK_AMD_FUSED_FFN_FWD", "0") == "1"
+
+
+def _fused_ffn1(C, x2, W1, b1f):
+    """(zb, h): zb = x2 W1^T + b1f (kept), h = gelu(zb).  None when unsupported."""
+    T, H = x2.shape
+    F = W1.shape[0]
+    if T % 256 or F % 256 or H % 64 or b1f.dtype != torch.bfloat16:
+        return None
+    zb = torch.empty(T, F, device=x2.device, dtype=x2.dtype)
+    h = torch.empty_like(zb)
+    if not C.gemm_nt(x2, W1, h, 1, False, b1f, zb, None):
+        return None
+    return zb, h
+
+
 def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f):
-    """dz = (df @ W2) * gelu'(z + b1f); db1f += column sums of dz.  None when unsupported."""
+    """dz = (df @ W2) * gelu'(z [+ b1f]); db1f += column sums of dz (b1f None: z already
+    holds the bias).  None when unsupported."""
     T, F = z.shape
     if T % 256 or F % 256 or df.shape[1] % 64:
         return None
@@ -145,13 +164,17 @@ class _FFNBlockFn(torch.autograd.Function):
         C = _C()
         B, S, H = x1.shape
         x2 = x1.reshape(B * S, H)
-        z = torch.mm(x2, W1.t())
-        h = C.bias_act_fwd(z, b1f, 1)
+        fused = _fused_ffn1(C, x2, W1, b1f) if _FUSED_FFN_FWD else None
+        if fused is not None:
+            z, h = fused                        # z includes the bias
+        else:
+            z = torch.mm(x2, W1.t())
+            h = C.bias_act_fwd(z, b1f, 1)
         f = torch.mm(h, W2.t())
         y, s, mean, rstd = C.layernorm_fwd(f, b2f, x2, g2, b2, eps, False, p_hid, seed_h, off_h)
         ctx.save_for_backward(x2, z, h, s, mean, rstd)
         ctx.params = (W1, b1f, W2, b2f, g2, b2)
-        ctx.cfg = (B, S, H, p_hid, seed_h, off_h)
+        ctx.cfg = (B, S, H, p_hid, seed_h, off_h, fused is not None)
         return y.view(B, S, H)
 
     @staticmethod
@@ -159,7 +182,8 @@ class _FFNBlockFn(torch.autograd.Function):
         C = _C()
         x2, z, h, s, mean, rstd = ctx.saved_tensors
         W1, b1f, W2, b2f, g2, b2 = ctx.params
-        B, S, H, p_hid, seed_h, off_h = ctx.cfg
+        B, S, H, p_hid, seed_h, off_h, z_biased = ctx.cfg
+        zbias = None if z_biased else b1f       # the bias gelu' still has to add to z
         dy2 = dy.reshape(B * S, H).contiguous()
         dg2, fg2 = _vec_grad_out(g2)
         db2, fb2 = _vec_grad_out(b2)
@@ -172,10 +196,10 @@ class _FFNBlockFn(torch.autograd.Function):
         _ready(*[p for p, f in ((g2, fg2), (b2, fb2), (b2f, fb2f)) if f])
         dW2 = _wgrad(W2, df, h)
         db1f, fb1f = _vec_grad_out(b1f)
-        dz = _fused_ffn_dgrad(C, df.contiguous(), W2, z, b1f, db1f) if _FUSED_FFN_DGRAD else None
+        dz = _fused_ffn_dgrad(C, df.contiguous(), W2, z, zbias, db1f) if _FUSED_FFN_DGRAD else None
         if dz is None:
             dh = torch.mm(df, W2)
-            dz = C.bias_act_bwd_into(dh, z, b1f, 1, db1f, True)
+            dz = C.bias_act_bwd_into(dh, z, zbias, 1, db1f, True)
         if fb1f:
             _ready(b1f)
         dW1 = _wgrad(W1, dz, x2)

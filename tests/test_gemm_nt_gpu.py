@@ -90,6 +90,10 @@ def test_gemm_nt_strided_operands_and_refusals():
     D = torch.empty(512, 256, device="cuda", dtype=torch.bfloat16)
     assert C.gemm_nt(A, B, D, 0, False, None, None, None)
     _close(D, A.float() @ B.float().t())
+    Dw = torch.zeros(512, 384, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nt(A, B, Dw[:, 64:320], 0, False, None, None, None)            # ldd = 384, offset
+    _close(Dw[:, 64:320], A.float() @ B.float().t())
+    assert not Dw[:, :64].any() and not Dw[:, 320:].any()                       # nothing outside D
     bad = torch.empty(500, 256, device="cuda", dtype=torch.bfloat16)
     assert not C.gemm_nt(_rand(500, 256), B, bad, 0, False, None, None, None)     # M % 256
     assert not C.gemm_nt(_rand(256, 96), _rand(256, 96), torch.empty(256, 256, device="cuda",
@@ -110,3 +114,44 @@ def test_gemm_nt_operands_spanning_4gb_addresses():
     assert C.gemm_nt(A2, B, D, 0, False, None, None, None)
     _close(D, A2.float() @ B.float().t())
     del A2, big
+
+
+# ---- weight-gradient layout (ct_gemm_tn2): out = A[K,M]^T B[K,N], token-major operands
+@pytest.mark.parametrize("M,N,K,S", [(256, 256, 64, 1), (512, 256, 128, 1), (256, 768, 192, 1),
+                                     (768, 512, 1024, 1), (256, 256, 512, 8), (512, 768, 2048, 4),
+                                     (1024, 256, 768, 3)])
+def test_gemm_tn2_matches_fp32(M, N, K, S):
+    C = _C()
+    A, B = _rand(K, M, seed=M + K), _rand(K, N, seed=N + 7 * K, scale=K ** -0.5)
+    ref = A.float().t() @ B.float()
+    if S == 1:
+        D = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        assert C.gemm_tn2(A, B, D, 1, False)
+        _close(D, ref)
+        D0 = _rand(M, N, seed=3)
+        D1 = D0.clone()
+        assert C.gemm_tn2(A, B, D1, 1, True)
+        _close(D1, ref + D0.float())
+    else:
+        P = torch.full((S, M, N), float("nan"), device="cuda")
+        assert C.gemm_tn2(A, B, P, S, False)
+        torch.testing.assert_close(P.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
+        # each slab is its own K range
+        Ks = K // S
+        torch.testing.assert_close(P[1], A[Ks:2 * Ks].float().t() @ B[Ks:2 * Ks].float(), rtol=2e-3,
+                                   atol=2e-3 * ref.abs().max().item())
+
+
+def test_gemm_tn2_strided_operands_and_refusals():
+    C = _C()
+    big = _rand(256, 640, seed=21)
+    A = big[:, 128:384]                  # lda = 640, column offset
+    B = _rand(256, 512, seed=22)
+    D = torch.zeros(256, 768, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_tn2(A, B, D[:, 128:640], 1, False)                       # ldo = 768
+    _close(D[:, 128:640], A.float().t() @ B.float())
+    assert not D[:, :128].any() and not D[:, 640:].any()
+    assert not C.gemm_tn2(_rand(96, 256), _rand(96, 256), torch.empty(256, 256, device="cuda",
+                                                                      dtype=torch.bfloat16), 1, False)   # K % 64
+    assert not C.gemm_tn2(_rand(256, 256), _rand(256, 256), torch.empty(3, 256, 256, device="cuda"), 3,
+                          False)                                                     # K % (S * 64)

@@ -241,26 +241,34 @@ def test_bn_grads_accumulate_into_flat_buffer(cuda):
     assert set(id(p) for p in space.params) <= set(seen)
 
 
-@pytest.mark.parametrize("splits,mode", [(1, 2), (1, 1), (3, 0)])
-def test_gemm_tn_weight_gradient(cuda, splits, mode):
-    """HIP MFMA dW kernel (csrc/gemm.hip): C[M,N] (+)= A[T,M]^T B[T,N] vs an fp32 reference,
-    asymmetric operands (a row/col swap fails), split-K fp32 slabs and bf16 accumulate."""
+@pytest.mark.parametrize("splits,acc", [(1, False), (1, True), (3, False)])
+def test_gemm_tn_weight_gradient(cuda, splits, acc):
+    """MFMA dW kernel (csrc/gemm_nt.hip, TN layout): C[M,N] (+)= A[T,M]^T B[T,N] vs an fp32
+    reference, asymmetric operands (a row/col swap fails), split-K fp32 slabs and bf16
+    accumulate; then the wgrad entry point (ops.linear.wgrad_accumulate) on the same data."""
+    import importlib
     from cloudtik_amd import ops
+    L = importlib.import_module("cloudtik_amd.ops.linear")     # (ops.linear is the function)
     C = ops.require_native()
     g = torch.Generator().manual_seed(3)
     T, M, N = 64 * 3 * 4, 512, 768
     A = (torch.randn(T, M, generator=g) + torch.arange(M) / M).bfloat16().to(cuda)
     B = (torch.randn(T, N, generator=g) - torch.arange(N)[None, :] / N).bfloat16().to(cuda)
     ref = A.float().t() @ B.float()
-    if mode == 0:
+    if splits > 1:
         out = torch.empty(splits, M, N, device=cuda)
-        assert C.gemm_tn(A, B, out, splits, 0)
+        assert C.gemm_tn2(A, B, out, splits, False)
         torch.testing.assert_close(out.sum(0), ref, atol=2e-3, rtol=1e-4)
     else:
         base = torch.randn(M, N, generator=g).bfloat16().to(cuda)
         out = base.clone()
-        assert C.gemm_tn(A, B, out, 1, mode)
-        want = ref + (base.float() if mode == 1 else 0)
+        assert C.gemm_tn2(A, B, out, 1, acc)
+        want = ref + (base.float() if acc else 0)
         torch.testing.assert_close(out.float(), want, atol=0.5, rtol=1e-2)
     # unsupported shapes are refused, not launched
-    assert not C.gemm_tn(A[:, :500], B, torch.empty(1, 500, N, device=cuda), 1, 0)
+    assert not C.gemm_tn2(A[:, :500], B, torch.empty(2, 500, N, device=cuda), 2, False)
+    # the weight-gradient entry point accumulates the same product into a bf16 gradient
+    grad = torch.randn(M, N, generator=g).bfloat16().to(cuda)
+    want = ref + grad.float()
+    L.wgrad_accumulate(grad, A, B)
+    torch.testing.assert_close(grad.float(), want, atol=0.5, rtol=1e-2)

@@ -397,13 +397,25 @@ def test_wgrad_splitk_accumulate(cuda, N, K):
     assert _rel(g2, ref) < 5e-3
 
 
-@pytest.mark.parametrize("p,fused", [(0.0, False), (0.1, False), (0.1, True)])
-def test_bert_layer_blocks_match_composed(cuda, p, fused, monkeypatch):
+@pytest.mark.parametrize("p,fused,fused_fwd", [(0.0, False, False), (0.1, False, False), (0.1, True, False),
+                                              (0.1, False, True), (0.1, True, True)])
+def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, monkeypatch):
     """Hand-scheduled block backward == composed-op autograd (same dropout streams); `fused`
-    routes the FFN dgrad through the MFMA GEMM with the dGELU + bias-gradient epilogue."""
+    routes the FFN dgrad through the MFMA GEMM with the dGELU + bias-gradient epilogue,
+    `fused_fwd` the FFN1 forward through it with the bias + GELU epilogue (the kept
+    pre-activation then already holds the bias)."""
     from cloudtik_amd.models.bert import BertConfig, BertLayer
     from cloudtik_amd.ops import transformer as T
     monkeypatch.setattr(T, "_FUSED_FFN_DGRAD", fused)
+    monkeypatch.setattr(T, "_FUSED_FFN_FWD", fused_fwd)
+    if fused_fwd:
+        fwd_calls = []
+        orig_fwd = T._fused_ffn1
+        def spy_fwd(*a):
+            r = orig_fwd(*a)
+            fwd_calls.append(r is not None)
+            return r
+        monkeypatch.setattr(T, "_fused_ffn1", spy_fwd)
     if fused:
         calls = []
         orig_fused = T._fused_ffn_dgrad
@@ -445,6 +457,8 @@ def test_bert_layer_blocks_match_composed(cuda, p, fused, monkeypatch):
     assert _rel(g_blocks, sp.grad.float()) < 2e-2
     if fused:
         assert calls and all(calls), "fused FFN dgrad path not taken"
+    if fused_fwd:
+        assert fwd_calls and all(fwd_calls), "fused FFN1 forward path not taken"
 
 
 @pytest.mark.parametrize("name", ["adamw", "lamb"])
