@@ -216,9 +216,9 @@ def _weight_grad(wp, dy, x, w_shape, stride, padding):
     side stream (returns None: autograd never sees it, the data-parallel bucketer is told through
     ``_ct_grad_ready``); otherwise it is returned for AccumulateGrad."""
     from cloudtik_amd.ops.conv1x1 import _SIDE_WGRAD, _flat_target
-    from cloudtik_amd.ops.linear import grad_stream
+    from cloudtik_amd.ops.linear import side_grad_stream
     target = _flat_target(wp) if _SIDE_WGRAD else None
-    side = grad_stream() if target is not None else None
+    side = side_grad_stream() if target is not None else None
     if target is None or not target.is_contiguous(memory_format=torch.channels_last) or target.dtype != dy.dtype:
         return conv_wgrad(dy, x, w_shape, stride, padding)
     if side is None:

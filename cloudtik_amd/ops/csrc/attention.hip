@@ -332,6 +332,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
   const int nq = (a.Sq + 31) / 32;
   const bool single_block = gridDim.x == 1;
+  // 16-byte dQ stores need 8-element strides and a 16-byte aligned base
+  const bool dq16 = ((a.dq_ss | a.dq_sb | a.dq_sh) & 7) == 0 && (((uintptr_t)a.dq) & 15) == 0;
   const int dt_q = w & 1, kh = w >> 1;  // this wave's share of the dQ product
 
   // Q / dO / lse / delta tiles are register-prefetched one q-tile ahead (issued before the
@@ -477,13 +479,25 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     __syncthreads();   // (B2) red visible; staged tile t+1 visible for the next iteration
     if (kh == 0) {
       const int d = dt_q * 32 + r;
-      if (single_block && qb + 32 <= a.Sq) {
-        // whole tile in range (every q-tile when Sq % 32 == 0): no per-element exec-mask
-        // branches around the 16 stores
+      if (single_block && qb + 32 <= a.Sq && dq16) {
+        // whole tile in range (every q-tile when Sq % 32 == 0).  The lane holds 16 queries of
+        // one d; re-layout through this wave's own 4 KiB of `red` (its reads of it are done:
+        // LDS executes a wave's accesses in order) as fp32 [32 q][32 d], then 16-byte bf16
+        // stores of 8 consecutive d: 2 stores per lane instead of 16 two-byte ones
+        float v[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          dqbase[q * (int)a.dq_ss + d] = f2bf((acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale);
+        for (int i = 0; i < 16; ++i) v[i] = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
+        float* stg = red + dt_q * 1024;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) stg[((i & 3) + 8 * (i >> 2) + 4 * hh) * 32 + r] = v[i];
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) {
+          const int cidx = lane + 64 * c2, qr = cidx >> 2, seg = cidx & 3;
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + qr * 32 + seg * 8);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + qr * 32 + seg * 8 + 4);
+          const u16x8 o = {f2bf(lo[0]), f2bf(lo[1]), f2bf(lo[2]), f2bf(lo[3]),
+                           f2bf(hi[0]), f2bf(hi[1]), f2bf(hi[2]), f2bf(hi[3])};
+          *reinterpret_cast<u16x8*>(dqbase + (qb + qr) * (int)a.dq_ss + dt_q * 32 + seg * 8) = o;
         }
       } else {
 #pragma unroll

@@ -283,19 +283,18 @@ double lt_bmm_tuned(at::Tensor A, at::Tensor B, at::Tensor D, bool trans_a, bool
 }
 
 extern "C" int ct_gemm_nt(const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
-                          void*, long, float*, hipStream_t);
+                          void*, long, float*, int, hipStream_t);
 
-// D[M,N] = A[M,K] @ B[N,K]^T through the hand-written MFMA kernel (csrc/gemm_nt.hip) with
-// epilogue 0 plain (accumulate: D +=), 1 bias + GELU keeping aux = pre-activation, 2 dGELU
-// with aux = pre-activation and dbias += column sums.  False when the shape is unsupported.
-bool gemm_nt(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumulate, c10::optional<at::Tensor> bias,
-             c10::optional<at::Tensor> aux, c10::optional<at::Tensor> dbias) {
+// shared checks + launch of gemm_nt / gemm_nn (b_kn: B stored [K, N])
+static bool gemm_nt_impl(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumulate,
+                         c10::optional<at::Tensor> bias, c10::optional<at::Tensor> aux, c10::optional<at::Tensor> dbias,
+                         bool b_kn) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "gemm_nt: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
               D.scalar_type() == at::kBFloat16, "gemm_nt: bf16 operands");
   TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "gemm_nt: 2-D row-major operands");
-  const long M = A.size(0), K = A.size(1), N = B.size(0);
-  TORCH_CHECK(B.size(1) == K && D.size(0) == M && D.size(1) == N, "gemm_nt: shape mismatch");
+  const long M = A.size(0), K = A.size(1), N = b_kn ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_kn ? B.size(0) : B.size(1)) == K && D.size(0) == M && D.size(1) == N, "gemm_nt: shape mismatch");
   const bool hb = bias.has_value() && bias->defined(), ha = aux.has_value() && aux->defined(),
              hd = dbias.has_value() && dbias->defined();
   if (hb) TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
@@ -309,8 +308,22 @@ bool gemm_nt(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumul
   int rc = ct_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0), (int)M,
                       (int)N, (int)K, (int)epi, accumulate ? 1 : 0, hb ? bias->data_ptr() : nullptr,
                       ha ? aux->data_ptr() : nullptr, ha ? aux->stride(0) : 0,
-                      hd ? dbias->data_ptr<float>() : nullptr, at::hip::getCurrentHIPStream().stream());
+                      hd ? dbias->data_ptr<float>() : nullptr, b_kn ? 1 : 0, at::hip::getCurrentHIPStream().stream());
   return rc == 0;
+}
+
+// D[M,N] = A[M,K] @ B[N,K]^T through the hand-written MFMA kernel (csrc/gemm_nt.hip) with
+// epilogue 0 plain (accumulate: D +=), 1 bias + GELU keeping aux = pre-activation, 2 dGELU
+// with aux = pre-activation and dbias += column sums.  False when the shape is unsupported.
+bool gemm_nt(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumulate, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> aux, c10::optional<at::Tensor> dbias) {
+  return gemm_nt_impl(A, B, D, epi, accumulate, bias, aux, dbias, false);
+}
+
+// the same with B stored [K, N] (D = A @ B: a data gradient straight from an [out, in] weight)
+bool gemm_nn(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumulate, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> aux, c10::optional<at::Tensor> dbias) {
+  return gemm_nt_impl(A, B, D, epi, accumulate, bias, aux, dbias, true);
 }
 
 extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, hipStream_t);
@@ -339,6 +352,7 @@ bool gemm_tn2(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool a
 void register_lt(pybind11::module& m) {
   m.def("gemm_tn2", &gemm_tn2, "weight-gradient GEMM A^T @ B (token-major operands) on the MFMA kernel");
   m.def("gemm_nt", &gemm_nt, "hand-written MFMA GEMM A @ B^T with fused epilogues");
+  m.def("gemm_nn", &gemm_nn, "hand-written MFMA GEMM A @ B (B stored [K, N]) with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
   m.def("lt_bmm_tuned", &lt_bmm_tuned, "strided-batched hipBLASLt GEMM, algorithm picked by timing all solutions");
 }

@@ -170,26 +170,34 @@ struct NtCtx {
   unsigned offa0, offa1, offb0, offb1;   // per-lane staging offsets (NT: by piece parity; TN: A / B)
 };
 
-template <bool TN>
+// operand layouts: LAY 0 = NT (A [M,K], B [N,K]), 1 = TN (A [K,M], B [K,N]; weight gradients),
+// 2 = NN (A [M,K], B [K,N]; data gradients straight from the [out, in] weight)
+template <int LAY> struct NtLay {
+  static constexpr bool AT = LAY == 1;    // A stored k-major (transposing staging / reads)
+  static constexpr bool BT = LAY >= 1;    // B stored k-major
+};
+
+template <int LAY>
 __device__ __forceinline__ void nt_stage_slot(const NtCtx& c, long k0, int slot, char* dst) {
+  using Ly = NtLay<LAY>;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int piece = c.wave * 2 + i;
+    const long krow = c.kbase + k0 + piece * 4;            // k-major images: rows 4 piece .. + 4
     const bf16_t* base;
     unsigned off;
-    if constexpr (!TN) {
-      if (slot == 0 || slot == 3) {                        // A0 / A1: image rows piece*8 .. +8
+    if (slot == 0 || slot == 3) {                          // A0 / A1
+      if constexpr (!Ly::AT) {                             // image rows piece*8 .. +8
         base = c.A + (c.m0 + ((piece >> 3) << 7) + (slot == 3 ? 64 : 0) + (piece & 7) * 8) * c.lda + k0;
         off = i ? c.offa1 : c.offa0;
-      } else {                                             // B0 / B1
-        base = c.B + (c.n0 + ((piece >> 2) << 6) + (slot == 2 ? 32 : 0) + (piece & 3) * 8) * c.ldb + k0;
-        off = i ? c.offb1 : c.offb0;
-      }
-    } else {
-      const long krow = c.kbase + k0 + piece * 4;          // image rows 4 piece .. + 4
-      if (slot == 0 || slot == 3) {
+      } else {
         base = c.A + krow * c.lda + c.m0 + (slot == 3 ? 64 : 0);
         off = c.offa0;
+      }
+    } else {                                               // B0 / B1
+      if constexpr (!Ly::BT) {
+        base = c.B + (c.n0 + ((piece >> 2) << 6) + (slot == 2 ? 32 : 0) + (piece & 3) * 8) * c.ldb + k0;
+        off = i ? c.offb1 : c.offb0;
       } else {
         base = c.B + krow * c.ldb + c.n0 + (slot == 2 ? 32 : 0);
         off = c.offb0;
@@ -218,15 +226,15 @@ __device__ __forceinline__ void nt_quad(f32x4 (&acc)[8][4], const nt_s16x8 (&fa)
 }
 
 // half with virtual index v (see above) -> its buffer slot
-template <bool TN>
+template <int LAY>
 __device__ __forceinline__ void nt_stage_v(const NtCtx& c, int v) {
   const int T = (v + 6) >> 2, slot = (v + 6) & 3;
-  nt_stage_slot<TN>(c, (long)T * NT_BK, slot, c.lds + (T & 1) * NT_BUF + slot * NT_HALF);
+  nt_stage_slot<LAY>(c, (long)T * NT_BK, slot, c.lds + (T & 1) * NT_BUF + slot * NT_HALF);
 }
 
-template <bool TN>
+template <bool KMAJOR>
 __device__ __forceinline__ nt_s16x8 nt_fragment(const char* img, int r0, int ks, int lane) {
-  if constexpr (TN) return tn_frag(img, r0, ks, lane);
+  if constexpr (KMAJOR) return tn_frag(img, r0, ks, lane);
   else return nt_frag(img, r0, ks, lane);
 }
 
@@ -243,7 +251,7 @@ struct NtPlan {
   }
 };
 
-template <int POS, int DIAG, bool TN>
+template <int POS, int DIAG, int LAY>
 __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][4], nt_s16x8 (&fa)[2][4][2],
                                          nt_s16x8 (&fb)[2][2][2]) {
   const char* buf = c.lds + (t & 1) * NT_BUF;
@@ -251,7 +259,7 @@ __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][
   constexpr bool DMA = DIAG == 0 || DIAG == 3;
   using P = NtPlan<POS>;
 #define NT_PHASE_TAIL(Q, I0, J0, FA, FB)                                             \
-  if constexpr (DMA && P::issue(Q)) nt_stage_v<TN>(c, 4 * t + Q);                    \
+  if constexpr (DMA && P::issue(Q)) nt_stage_v<LAY>(c, 4 * t + Q);                   \
   if constexpr (WAIT) nt_vm<P::wait(Q)>();                                           \
   if constexpr (BAR) nt_mma_begin(); else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
   nt_quad<I0, J0>(acc, FA, FB);                                                      \
@@ -260,23 +268,23 @@ __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = nt_fragment<TN>(buf + 1 * NT_HALF, c.rb + j * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = nt_fragment<NtLay<LAY>::BT>(buf + 1 * NT_HALF, c.rb + j * 16, ks, c.lane);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fa[0][i][ks] = nt_fragment<TN>(buf + 0 * NT_HALF, c.ra + i * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fa[0][i][ks] = nt_fragment<NtLay<LAY>::AT>(buf + 0 * NT_HALF, c.ra + i * 16, ks, c.lane);
   NT_PHASE_TAIL(0, 0, 0, fa[0], fb[0])
   // ---- q1: B1 fragments
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = nt_fragment<TN>(buf + 2 * NT_HALF, c.rb + j * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = nt_fragment<NtLay<LAY>::BT>(buf + 2 * NT_HALF, c.rb + j * 16, ks, c.lane);
   NT_PHASE_TAIL(1, 0, 2, fa[0], fb[1])
   // ---- q2: A1 fragments
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fa[1][i][ks] = nt_fragment<TN>(buf + 3 * NT_HALF, c.ra + i * 16, ks, c.lane);
+    for (int ks = 0; ks < 2; ++ks) fa[1][i][ks] = nt_fragment<NtLay<LAY>::AT>(buf + 3 * NT_HALF, c.ra + i * 16, ks, c.lane);
   NT_PHASE_TAIL(2, 4, 2, fa[1], fb[1])
   // ---- q3: no fragment reads
   NT_PHASE_TAIL(3, 4, 0, fa[1], fb[0])
@@ -391,28 +399,35 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
 
 // DIAG (timing diagnostics only, wrong results): 1 = no DMA / vmcnt in the K loop (MFMA + LDS
 // reads + barriers), 2 = additionally no barriers (MFMA + LDS reads), 3 = DMA issued but never
-// waited for in the K loop.  TN: the weight-gradient layout (blockIdx -> (split, tile)).
-template <int EPI, bool BGRAD, int DIAG = 0, bool TN = false>
+// waited for in the K loop.  LAY: operand layouts (NtLay); 1 = TN weight gradients with
+// blockIdx -> (split, tile).
+template <int EPI, bool BGRAD, int DIAG = 0, int LAY = 0>
 __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
+  using Ly = NtLay<LAY>;
+  constexpr bool SPLIT = LAY == 1;
   __shared__ __attribute__((aligned(1024))) char lds[2 * NT_BUF];    // 128 KiB, the only LDS object
   const int tiles_n = a.N / NT_BN;
   const int tiles = (a.M / NT_BM) * tiles_n;
   int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = TN ? L / tiles : 0;
+  const int split = SPLIT ? L / tiles : 0;
   L -= split * tiles;
   const int tm = L / tiles_n, tn = L % tiles_n;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: staging bases in SGPRs
   const int wr = wave >> 2, wc = wave & 3;
   const long m0 = (long)tm * NT_BM, n0 = (long)tn * NT_BN;
-  const int nk = (TN ? (int)a.tsplit : a.K) / NT_BK;
-  NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, (long)split * a.tsplit, lds, wave, lane, wr * 64, wc * 32, 0, 0, 0, 0};
-  if constexpr (TN) {
+  const int nk = (SPLIT ? (int)a.tsplit : a.K) / NT_BK;
+  NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, SPLIT ? (long)split * a.tsplit : 0L, lds, wave, lane, wr * 64, wc * 32,
+          0, 0, 0, 0};
+  if constexpr (Ly::AT) {
     c.offa0 = c.offa1 = tn_lane_off(a.lda, wave, lane, true);
-    c.offb0 = c.offb1 = tn_lane_off(a.ldb, wave, lane, false);
   } else {
     c.offa0 = nt_lane_off(a.lda, 0, lane);
     c.offa1 = nt_lane_off(a.lda, 1, lane);
+  }
+  if constexpr (Ly::BT) {
+    c.offb0 = c.offb1 = tn_lane_off(a.ldb, wave, lane, false);
+  } else {
     c.offb0 = nt_lane_off(a.ldb, 0, lane);
     c.offb1 = nt_lane_off(a.ldb, 1, lane);
   }
@@ -428,10 +443,10 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
 
   // prologue: halves -6 .. -1 (all of K-tile 0, A0 + B0 of K-tile 1); wait for tile 0's A0, B0
 #pragma unroll
-  for (int v = -6; v < -2; ++v) nt_stage_v<TN>(c, v);
+  for (int v = -6; v < -2; ++v) nt_stage_v<LAY>(c, v);
   if (nk > 1) {
-    nt_stage_v<TN>(c, -2);
-    nt_stage_v<TN>(c, -1);
+    nt_stage_v<LAY>(c, -2);
+    nt_stage_v<LAY>(c, -1);
     nt_vm<8>();
   } else {
     nt_vm<4>();
@@ -442,12 +457,12 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   // steady state: every phase issues one half and keeps 4 in flight; the last two K-tiles
   // drain (halves beyond 4 nk - 7 do not exist)
   int t = 0;
-  for (; t < nk - 2; ++t) nt_ktile<0, DIAG, TN>(c, t, acc, fa, fb);
+  for (; t < nk - 2; ++t) nt_ktile<0, DIAG, LAY>(c, t, acc, fa, fb);
   if (nk >= 2) {
-    nt_ktile<1, DIAG, TN>(c, t, acc, fa, fb);
+    nt_ktile<1, DIAG, LAY>(c, t, acc, fa, fb);
     ++t;
   }
-  nt_ktile<2, DIAG, TN>(c, t, acc, fa, fb);
+  nt_ktile<2, DIAG, LAY>(c, t, acc, fa, fb);
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 
   // acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
@@ -463,10 +478,10 @@ using namespace ct;
 //   2: D = result * gelu'(aux [+ bias]), dbias += column sums (bias, dbias may be null).
 // Returns nonzero (and launches nothing) when the shape / alignment is not supported.
 extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void* D, long ldd, int M, int N, int K,
-                          int epi, int accumulate, const void* bias, void* aux, long ldaux, float* dbias,
+                          int epi, int accumulate, const void* bias, void* aux, long ldaux, float* dbias, int b_kn,
                           hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % NT_BM || N % NT_BN || K % NT_BK) return 1;
-  if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < K || ldd < N) return 2;
+  if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < (b_kn ? N : K) || ldd < N) return 2;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 15)) return 3;
   if (epi == 1 && (!bias || !aux || ((uintptr_t)bias & 7))) return 4;
   if ((epi == 1 || epi == 2) && (!aux || ((uintptr_t)aux & 15) || ldaux % 8 || ldaux < N)) return 4;
@@ -476,18 +491,27 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias, nullptr,
            lda, ldb, ldd, ldaux, 0, M, N, K, accumulate};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
-  if (diag == 1) { gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
-  if (diag == 2) { gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
-  if (diag == 3) { gemm_nt_kernel<0, false, 3><<<(int)blocks, NT_THREADS, 0, stream>>>(a); return 0; }
+  if (diag && !b_kn) {
+    if (diag == 1) gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+    else if (diag == 2) gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+    else gemm_nt_kernel<0, false, 3><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+    return 0;
+  }
+#define NT_LAUNCH(E, BG)                                                                  \
+  do {                                                                                    \
+    if (b_kn) gemm_nt_kernel<E, BG, 0, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a);     \
+    else gemm_nt_kernel<E, BG, 0, 0><<<(int)blocks, NT_THREADS, 0, stream>>>(a);          \
+  } while (0)
   switch (epi) {
-    case 0: gemm_nt_kernel<0, false><<<(int)blocks, NT_THREADS, 0, stream>>>(a); break;
-    case 1: gemm_nt_kernel<1, false><<<(int)blocks, NT_THREADS, 0, stream>>>(a); break;
+    case 0: NT_LAUNCH(0, false); break;
+    case 1: NT_LAUNCH(1, false); break;
     case 2:
-      if (dbias) gemm_nt_kernel<2, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
-      else gemm_nt_kernel<2, false><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+      if (dbias) NT_LAUNCH(2, true);
+      else NT_LAUNCH(2, false);
       break;
     default: return 6;
   }
+#undef NT_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
@@ -505,7 +529,7 @@ extern "C" int ct_gemm_tn2(const void* A, long lda, const void* B, long ldb, voi
   if (blocks > (1L << 30)) return 5;
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, splits == 1 ? (bf16_t*)out : nullptr, nullptr, nullptr, nullptr,
            splits > 1 ? (float*)out : nullptr, lda, ldb, ldo, 0, K / splits, M, N, (int)(K / splits), accumulate};
-  if (splits > 1) gemm_nt_kernel<NT_EPI_F32_SLAB, false, 0, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
-  else gemm_nt_kernel<NT_EPI_PLAIN, false, 0, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+  if (splits > 1) gemm_nt_kernel<NT_EPI_F32_SLAB, false, 0, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+  else gemm_nt_kernel<NT_EPI_PLAIN, false, 0, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }

@@ -59,10 +59,40 @@ def sync_grad_stream() -> None:
         torch.cuda.current_stream().wait_stream(s)
 
 
+_end_of_backward_sync_queued = False
+
+
+def _join_grad_stream():
+    """Autograd final callback: the streams that read gradients after ``backward()`` returns
+    wait (on the GPU, no host sync) for every weight gradient issued on the side stream, so a
+    plain ``param.grad`` read -- clipping, logging, a test -- never races the side stream."""
+    global _end_of_backward_sync_queued
+    _end_of_backward_sync_queued = False
+    s = _streams.get(torch.cuda.current_device())
+    if s is None:
+        return
+    cur = torch.cuda.current_stream()
+    cur.wait_stream(s)
+    default = torch.cuda.default_stream()
+    if default != cur:
+        default.wait_stream(s)
+
+
+def side_grad_stream():
+    """``grad_stream()`` for work issued from inside a backward pass: the first call of a
+    backward also queues the end-of-backward join (``_join_grad_stream``)."""
+    global _end_of_backward_sync_queued
+    s = grad_stream()
+    if s is not None and not _end_of_backward_sync_queued and torch._C._current_graph_task_id() != -1:
+        torch.autograd.Variable._execution_engine.queue_callback(_join_grad_stream)
+        _end_of_backward_sync_queued = True
+    return s
+
+
 def wgrad_on_side_stream(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
     """Issue ``g += dy2^T x2`` on the gradient side stream; False if disabled."""
-    s = grad_stream()
-    if s is None or not g.is_cuda:
+    s = side_grad_stream() if g.is_cuda else None
+    if s is None:
         return False
     cur = torch.cuda.current_stream()
     s.wait_stream(cur)                       # dY / X produced (and grad zeroed) on the main stream

@@ -3,7 +3,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/ab_wgrad"; mkdir -p "$OUT"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_nt_gpu.py "tests/test_ops2_gpu.py::test_gemm_tn_weight_gradient" "tests/test_ops_gpu.py::test_bert_layer_blocks_match_composed" > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_nt_gpu.py "tests/test_ops2_gpu.py::test_gemm_tn_weight_gradient" "tests/test_ops_gpu.py::test_bert_layer_blocks_match_composed" ${EXTRA_TESTS:-} > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
 tail -2 "$OUT/tests.log"
 for r in 1 2; do
   for cfg in ${CFGS:-hip:11 blas:11 hip:00}; do

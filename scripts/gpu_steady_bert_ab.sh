@@ -14,5 +14,5 @@ prof() {  # name delim -- cmd...
   rm -rf "$OUT/$name"
   head -3 "$OUT/$name.md"
 }
-CLOUDTIK_AMD_FUSED_FFN_FWD=0 CLOUDTIK_AMD_FUSED_FFN_DGRAD=0 prof bert_large_unfused lamb_stage1 -- python3 -u "$R/bench.py" --model bert-large --steps 8 --warmup 4 \
- && CLOUDTIK_AMD_FUSED_FFN_FWD=1 CLOUDTIK_AMD_FUSED_FFN_DGRAD=1 prof bert_large_fused lamb_stage1 -- python3 -u "$R/bench.py" --model bert-large --steps 8 --warmup 4
+CLOUDTIK_AMD_WGRAD_STREAM=${WS:-1} CLOUDTIK_AMD_FUSED_FFN_FWD=0 CLOUDTIK_AMD_FUSED_FFN_DGRAD=0 prof bert_large_unfused${TAG:-} lamb_stage1 -- python3 -u "$R/bench.py" --model bert-large --steps 8 --warmup 4 \
+ && CLOUDTIK_AMD_WGRAD_STREAM=${WS:-1} CLOUDTIK_AMD_FUSED_FFN_FWD=1 CLOUDTIK_AMD_FUSED_FFN_DGRAD=1 prof bert_large_fused${TAG:-} lamb_stage1 -- python3 -u "$R/bench.py" --model bert-large --steps 8 --warmup 4

@@ -155,3 +155,25 @@ def test_gemm_tn2_strided_operands_and_refusals():
                                                                       dtype=torch.bfloat16), 1, False)   # K % 64
     assert not C.gemm_tn2(_rand(256, 256), _rand(256, 256), torch.empty(3, 256, 256, device="cuda"), 3,
                           False)                                                     # K % (S * 64)
+
+
+# ---- NN layout (gemm_nn): D = A[M,K] @ B[K,N], B read in place from an [out, in] weight
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (2048, 1024, 1024)])
+def test_gemm_nn_plain_and_dgelu(M, N, K):
+    C = _C()
+    A, B = _rand(M, K, seed=M), _rand(K, N, seed=N, scale=K ** -0.5)
+    ref = A.float() @ B.float()
+    D = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nn(A, B, D, 0, False, None, None, None)
+    _close(D, ref)
+    aux = _rand(M, N, seed=5)
+    bias = _rand(N, seed=6, scale=0.1)
+    db = torch.zeros(N, device="cuda")
+    assert C.gemm_nn(A, B, D, 2, False, bias, aux, db)
+    want = ref * _gelu_grad(aux.float() + bias.float())
+    _close(D, want)
+    torch.testing.assert_close(db, want.sum(0), rtol=2e-3, atol=2e-2 * max(1.0, want.abs().sum(0).max().item() / M))
+    # strided B (a column slice of a wider weight)
+    Bw = _rand(K, N + 128, seed=7)
+    assert C.gemm_nn(A, Bw[:, 128:], D, 0, False, None, None, None)
+    _close(D, A.float() @ Bw[:, 128:].float())
