@@ -617,14 +617,22 @@ class Booster:
                               dm.w.to(dev) if dm.w is not None else torch.ones(en, device=dev)))
         metrics = p.eval_metric or [self._default_metric()]
         # row sampling on the device (no per-round host->device copy); the feature mask is
-        # drawn on the host from a seed shared by every rank so all ranks agree on it
-        gen = torch.Generator(device=dev).manual_seed(p.seed + (dist.get_rank() if _dist_on() else 0))
-        fgen = torch.Generator(device="cpu").manual_seed(p.seed)        # same feature mask on every rank
+        # drawn on the host from a seed shared by every rank so all ranks agree on it.  Both
+        # are re-seeded from the GLOBAL round index (trees already in the model count), so
+        # training in several calls -- the checkpoint segments of elastic training -- draws
+        # exactly what one call would
+        rank = dist.get_rank() if _dist_on() else 0
+        gen = torch.Generator(device=dev)
+        fgen = torch.Generator(device="cpu")
         K = self.objective.n_outputs
         F = bins.shape[0]
+        start_round = self.num_trees // K
         new_trees: List[Tuple[torch.Tensor, ...]] = []
         best_score, best_it, history = None, None, {}
         for it in range(num_boost_round):
+            rnd = start_round + it
+            gen.manual_seed((p.seed * 1_000_003 + rank * 7_919 + rnd) & 0x7FFFFFFFFFFFFFFF)
+            fgen.manual_seed((p.seed * 1_000_003 + rnd) & 0x7FFFFFFFFFFFFFFF)
             if p.subsample < 1:
                 sampled = torch.rand(n, device=dev, generator=gen) < p.subsample
             else:
@@ -657,7 +665,7 @@ class Booster:
                 if not _dist_on() or dist.get_rank() == 0:
                     print(f"[{it}]\t{msg}", flush=True)
             if callback:
-                callback(it, scores)
+                callback(rnd, scores)
             if early_stopping_rounds and eval_sets:
                 key = f"{eval_sets[-1][0]}-{metrics[-1]}"
                 s = scores[key]

@@ -3,7 +3,11 @@ xgboost/modeling/run.py:98-330 with the same options and YAML configs).
 
 Single process by default; for data-parallel training launch it with ``cloudtik-run -np N``
 (one rank per GPU, torch.distributed env:// rendezvous): each rank takes an equal row shard
-of the training split and histograms are all-reduced per tree level.
+of the training split and histograms are all-reduced per tree level.  ``--num-actors N``
+without a launcher runs the fault-tolerant driver (elastic.py): N actor processes, a model
+checkpoint every ``--checkpoint-frequency`` rounds, ``--max-actor-restarts`` restarts per
+actor and, with ``--elastic-training``, up to ``--max-failed-actors`` actors dropped
+(reference RayParams, xgboost/modeling/run.py:90-106).
 """
 from __future__ import annotations
 
@@ -58,11 +62,25 @@ def parse_args(argv=None):
     a("--predict-output", "--predict_output")
     a("--target-col", "--target_col")
     a("--data-api", "--data_api", default="pandas")
-    a("--num-actors", "--num_actors", type=int, default=1, help="use cloudtik-run -np N instead")
+    a("--num-actors", "--num_actors", type=int, default=1,
+      help="> 1: fault-tolerant actor processes from this driver (or launch with cloudtik-run -np N)")
     a("--cpus-per-actor", "--cpus_per_actor", type=int, default=0)
     a("--gpus-per-actor", "--gpus_per_actor", type=int, default=0)
     a("--device", default=None)
+    a("--elastic-training", "--elastic_training", action="store_true")
+    a("--max-failed-actors", "--max_failed_actors", type=int, default=0)
+    a("--max-actor-restarts", "--max_actor_restarts", type=int, default=0)
+    a("--checkpoint-frequency", "--checkpoint_frequency", type=int, default=5)
     return ap.parse_args(argv)
+
+
+def _parquet_shard(path, target, ignore, actor_id, num_actors):
+    """Elastic actor shard: rows actor_id::num_actors of the processed training split."""
+    import pandas as pd
+    from cloudtik_amd.modeling.gbdt import DMatrix
+    from cloudtik_amd.modeling.gbdt.data import feature_frame
+    X, y = feature_frame(pd.read_parquet(path), target, ignore)
+    return DMatrix(X.iloc[actor_id::num_actors], y.iloc[actor_id::num_actors])
 
 
 def run(args) -> Dict[str, Any]:
@@ -111,9 +129,28 @@ def run(args) -> Dict[str, Any]:
                 Xe, ye = feature_frame(splits[name], target, ignore)
                 evals.append((DMatrix(Xe, ye), name))
         t0 = time.time()
-        booster = Booster(params, device=device).train(
-            DMatrix(Xtr, ytr), int(tparams.get("num_boost_round", 100)), evals,
-            tparams.get("early_stopping_rounds"), tparams.get("verbose_eval", False))
+        rounds = int(tparams.get("num_boost_round", 100))
+        if args.num_actors > 1 and world == 1:
+            # fault-tolerant multi-actor training from this driver process
+            import functools
+            from cloudtik_amd.modeling.gbdt.elastic import ElasticParams, train_elastic
+            train_path = os.path.join(processed, "train.parquet")
+            if not os.path.exists(train_path):
+                os.makedirs(processed, exist_ok=True)
+                splits["train"].to_parquet(train_path)
+            ep = ElasticParams(num_actors=args.num_actors, elastic_training=args.elastic_training,
+                               max_failed_actors=args.max_failed_actors,
+                               max_actor_restarts=args.max_actor_restarts,
+                               checkpoint_frequency=args.checkpoint_frequency,
+                               checkpoint_dir=os.path.join(args.output_dir, "checkpoints"),
+                               device="cuda" if device.startswith("cuda") else "cpu")
+            booster, report = train_elastic(params, functools.partial(_parquet_shard, train_path, target, ignore),
+                                            rounds, ep, log=lambda m: print(f"[elastic] {m}", flush=True))
+            result["elastic"] = report
+        else:
+            booster = Booster(params, device=device).train(
+                DMatrix(Xtr, ytr), rounds, evals,
+                tparams.get("early_stopping_rounds"), tparams.get("verbose_eval", False))
         if device.startswith("cuda"):
             torch.cuda.synchronize()
         result["train_seconds"] = time.time() - t0
