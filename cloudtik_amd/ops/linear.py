@@ -74,7 +74,7 @@ def _join_grad_stream():
     cur = torch.cuda.current_stream()
     cur.wait_stream(s)
     default = torch.cuda.default_stream()
-    if default != cur:
+    if default != cur and not torch.cuda.is_current_stream_capturing():
         default.wait_stream(s)
 
 

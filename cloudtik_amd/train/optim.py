@@ -332,15 +332,29 @@ class _FlatOptimizer(torch.optim.Optimizer):
             raise ValueError("fused flat optimizers need one learning rate across groups")
         return float(next(iter(lrs)))
 
-    def _push_dyn(self, b1=None, b2=None):
+    def _dyn_values(self, b1, b2):
         t = self.step_count
         bc1 = 1.0 / (1.0 - b1 ** t) if b1 is not None else 1.0
         bc2 = 1.0 / (1.0 - b2 ** t) if b2 is not None else 1.0
+        return [self._lr(), self.grad_scale, bc1, bc2]
+
+    def _push_dyn(self, b1=None, b2=None):
+        if self.dyn.is_cuda and torch.cuda.is_current_stream_capturing():
+            # hipGraph capture (train.graph_step): the captured copy node re-reads ONE fixed
+            # pinned slot at every replay; graph_step_prepare() rewrites it between replays
+            if getattr(self, "_graph_host", None) is None:
+                raise RuntimeError("call graph_capture_begin() before capturing an optimizer step "
+                                   "(pinned memory cannot be allocated while a stream captures)")
+            self._graph_betas = (b1, b2)
+            self._graph_replays = 0
+            self._graph_host.copy_(torch.tensor(self._dyn_values(b1, b2), dtype=torch.float32))
+            self.dyn.copy_(self._graph_host, non_blocking=True)
+            return
         i = self._dyn_slot = (self._dyn_slot + 1) % _DYN_SLOTS
         host, ev = self._dyn_ring[i], self._dyn_events[i]
         if ev is not None:
             ev.synchronize()
-        host.copy_(torch.tensor([self._lr(), self.grad_scale, bc1, bc2], dtype=torch.float32))
+        host.copy_(torch.tensor(self._dyn_values(b1, b2), dtype=torch.float32))
         if self.dyn.is_cuda:
             self.dyn.copy_(host, non_blocking=True)
             if ev is None:
@@ -348,6 +362,32 @@ class _FlatOptimizer(torch.optim.Optimizer):
             ev.record()
         else:
             self.dyn.copy_(host)
+
+    def graph_capture_begin(self):
+        """Allocate the pinned scalar slot a captured step's copy node reads (before capture)."""
+        if self.dyn.is_cuda and getattr(self, "_graph_host", None) is None:
+            self._graph_host = torch.zeros(4, dtype=torch.float32, pin_memory=True)
+            self._graph_done = torch.cuda.Event()
+
+    def graph_step_prepare(self):
+        """Before replaying a captured training step (the capture itself ran no kernels): count
+        the step and put its scalars (lr, grad scale, bias corrections) where the graph's copy
+        node reads them.  The slot is only rewritten -- after the previous replay finished with
+        it -- when a value changes (never for a constant-lr SGD)."""
+        if getattr(self, "_graph_host", None) is None:
+            return
+        if self._graph_replays > 0:
+            self.step_count += 1
+        self._graph_replays += 1
+        vals = torch.tensor(self._dyn_values(*self._graph_betas), dtype=torch.float32)
+        if not torch.equal(vals, self._graph_host):
+            self._graph_done.synchronize()
+            self._graph_host.copy_(vals)
+
+    def graph_step_done(self):
+        """After a replay was launched: mark where the host slot is free again."""
+        if getattr(self, "_graph_host", None) is not None:
+            self._graph_done.record()
 
     def state_dict(self):
         """Flat optimizer state in the GLOBAL layout (ZeRO-1 shards are gathered).
