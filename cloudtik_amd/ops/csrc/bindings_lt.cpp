@@ -326,11 +326,13 @@ bool gemm_nn(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumul
   return gemm_nt_impl(A, B, D, epi, accumulate, bias, aux, dbias, true);
 }
 
-extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, hipStream_t);
+extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, float*,
+                           hipStream_t);
 
 // out[M,N] = A[K,M]^T @ B[K,N] through the MFMA kernel's weight-gradient layout: splits > 1 ->
 // out is fp32 [splits, M, N] (partial slabs); splits == 1 -> bf16 [M, N] (+)= result.
-bool gemm_tn2(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool accumulate) {
+static bool gemm_tn2_impl(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool accumulate,
+                          float* biasg) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && out.is_cuda(), "gemm_tn2: GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_tn2: bf16 operands");
   TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B), "gemm_tn2: 2-D row-major operands");
@@ -346,11 +348,23 @@ bool gemm_tn2(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool a
     ldo = out.stride(0);
   }
   return ct_gemm_tn2(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), out.data_ptr(), ldo, (int)M, (int)N, K,
-                     (int)splits, accumulate ? 1 : 0, at::hip::getCurrentHIPStream().stream()) == 0;
+                     (int)splits, accumulate ? 1 : 0, biasg, at::hip::getCurrentHIPStream().stream()) == 0;
+}
+
+bool gemm_tn2(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool accumulate) {
+  return gemm_tn2_impl(A, B, out, splits, accumulate, nullptr);
+}
+
+// the same, also writing biasg[s][m] = sum over split s's K range of A[k][m] (fp32 [splits, M])
+bool gemm_tn2_bias(at::Tensor A, at::Tensor B, at::Tensor out, int64_t splits, bool accumulate, at::Tensor biasg) {
+  TORCH_CHECK(biasg.is_cuda() && biasg.scalar_type() == at::kFloat && biasg.is_contiguous() &&
+              biasg.numel() == splits * A.size(1), "gemm_tn2_bias: fp32 [splits, M] bias partials");
+  return gemm_tn2_impl(A, B, out, splits, accumulate, biasg.data_ptr<float>());
 }
 
 void register_lt(pybind11::module& m) {
   m.def("gemm_tn2", &gemm_tn2, "weight-gradient GEMM A^T @ B (token-major operands) on the MFMA kernel");
+  m.def("gemm_tn2_bias", &gemm_tn2_bias, "gemm_tn2 + per-split column sums of A (bias gradient)");
   m.def("gemm_nt", &gemm_nt, "hand-written MFMA GEMM A @ B^T with fused epilogues");
   m.def("gemm_nn", &gemm_nn, "hand-written MFMA GEMM A @ B (B stored [K, N]) with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");

@@ -62,6 +62,15 @@ __device__ __forceinline__ void cv_glds16(const void* g, const char* lds_wave_ba
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
 }
 
+// LDS-DMA addressed as a wave-uniform 64-bit base (SGPRs) + a per-lane 32-bit byte offset
+__device__ __forceinline__ void cv_glds16s(const void* sbase, unsigned voff, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(cv_lds_void*)lds_wave_base);
+  const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)sbase) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)sbase >> 32)) << 32);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
+               : "memory", "m0");
+}
+
 __device__ __forceinline__ cv_s16x8 cv_frag(const char* img, int r0, int ks, int lane) {
   const int row = r0 + (lane & 15);
   const int kc = ks * 4 + (lane >> 4);
@@ -106,7 +115,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   const int ntn = a.Co / BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = L / ntn, tn = L % ntn;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: weight bases in SGPRs
   const int wm = wave / WGN, wn = wave % WGN;
   const int m0 = tm * BM, n0 = tn * BN;
   const int HW = a.Hr * a.Wr;
@@ -133,12 +143,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
     }
   }
   const long ldw = (long)a.T * a.cpt * 64;
-  const bf16_t* wrow[IB];
+  // weight rows: the 8-row group g = wave * IB + j of staging instruction j starts at a
+  // wave-uniform row; the lane's row q = lane >> 3 inside it and its swizzled chunk are a
+  // 32-bit byte offset.  The swizzle of row 8 g + q, (4 g + (q >> 1)) & 7, depends on the group
+  // only through its parity.
+  const bf16_t* wbase[IB];
+  unsigned woff[2];
 #pragma unroll
-  for (int j = 0; j < IB; ++j) {
-    const int row = (wave * IB + j) * 8 + (lane >> 3);
-    wrow[j] = a.W + (long)(n0 + row) * ldw + ((lane & 7) ^ cv_swz(row)) * 8;
-  }
+  for (int par = 0; par < 2; ++par)
+    woff[par] = (unsigned)(((lane >> 3) * ldw + (((lane & 7) ^ ((4 * par + ((lane >> 3) >> 1)) & 7)) * 8)) * 2);
+#pragma unroll
+  for (int j = 0; j < IB; ++j) wbase[j] = a.W + (long)(n0 + (wave * IB + j) * 8) * ldw;
   const int cpt = a.cpt;                    // 64-column K-steps per tap
   const int KT = a.T * cpt;
 
@@ -157,7 +172,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
     }
     const long k0 = (long)t * cpt * 64 + c0;
 #pragma unroll
-    for (int j = 0; j < IB; ++j) cv_glds16(wrow[j] + k0, Bs + (wave * IB + j) * 1024);
+    for (int j = 0; j < IB; ++j) cv_glds16s(wbase[j] + k0, woff[(wave * IB + j) & 1], Bs + (wave * IB + j) * 1024);
   };
 
   f32x4 acc[MI][NJ];

@@ -12,6 +12,7 @@ then never sees a weight gradient, the data-parallel bucketer is notified explic
 from __future__ import annotations
 
 import os
+from typing import Optional
 
 import torch
 import torch.nn.functional as F
@@ -89,15 +90,17 @@ def side_grad_stream():
     return s
 
 
-def wgrad_on_side_stream(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
-    """Issue ``g += dy2^T x2`` on the gradient side stream; False if disabled."""
+def wgrad_on_side_stream(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
+                         dbias: Optional[torch.Tensor] = None) -> bool:
+    """Issue ``g += dy2^T x2`` (and ``dbias += column sums of dy2``) on the gradient side
+    stream; False if disabled."""
     s = side_grad_stream() if g.is_cuda else None
     if s is None:
         return False
     cur = torch.cuda.current_stream()
     s.wait_stream(cur)                       # dY / X produced (and grad zeroed) on the main stream
     with torch.cuda.stream(s):
-        wgrad_accumulate(g, dy2, x2)
+        wgrad_accumulate(g, dy2, x2, dbias)
     dy2.record_stream(s)
     x2.record_stream(s)
     return True
@@ -133,11 +136,23 @@ def tn2_splits(T: int, N: int, K: int, cus: int = 256) -> int:
     return best
 
 
-def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
-    """g += dy2^T x2 (bf16 g, fp32 accumulation).  The MFMA kernel's TN layout with split-K
-    fp32 slabs + one fused reduce-accumulate kernel (or, unsplit, accumulating straight into
-    g); otherwise hipBLASLt's batched split-K GEMM, or its beta=1 epilogue when one split
-    fills the GPU."""
+def _bias_colsum(dbias: torch.Tensor, dy2: torch.Tensor) -> None:
+    """dbias += column sums of dy2 (fp32 accumulation)."""
+    if dbias.is_cuda and dbias.dtype == torch.bfloat16 and dbias.is_contiguous() and dy2.shape[1] % 8 == 0:
+        from cloudtik_amd import ops
+        ops.require_native().bias_act_bwd_into(dy2.contiguous(), dy2.contiguous(), None, 0, dbias, False)
+    else:
+        dbias.add_(dy2.float().sum(0).to(dbias.dtype))
+
+
+def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
+                     dbias: Optional[torch.Tensor] = None) -> None:
+    """g += dy2^T x2 (bf16 g, fp32 accumulation); with ``dbias``, also dbias += column sums of
+    dy2 (the bias gradient).  The MFMA kernel's TN layout with split-K fp32 slabs + one fused
+    reduce-accumulate kernel (or, unsplit, accumulating straight into g), the bias sums coming
+    out of the same kernel (one extra MFMA per A fragment against an all-ones operand);
+    otherwise hipBLASLt's batched split-K GEMM, or its beta=1 epilogue when one split fills
+    the GPU, plus a column-sum kernel for the bias."""
     T, N = dy2.shape
     K = x2.shape[1]
     if (_HIP_WGRAD and g.is_cuda and g.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16
@@ -146,14 +161,21 @@ def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> No
         C = ops.require_native()
         S = tn2_splits(T, N, K)
         dy2c, x2c = dy2.contiguous(), x2.contiguous()
-        if S == 1:
-            if C.gemm_tn2(dy2c, x2c, g, 1, True):
-                return
-        else:
-            P = torch.empty(S, N, K, device=g.device, dtype=torch.float32)
-            if C.gemm_tn2(dy2c, x2c, P, S, False):
-                C.splitk_reduce(P, g, True)
-                return
+        fuse_bias = dbias is not None and dbias.dtype == torch.bfloat16 and dbias.is_contiguous()
+        bP = torch.empty(S, N, device=g.device, dtype=torch.float32) if fuse_bias else None
+        out = g if S == 1 else torch.empty(S, N, K, device=g.device, dtype=torch.float32)
+        ok = (C.gemm_tn2_bias(dy2c, x2c, out, S, S == 1, bP) if fuse_bias
+              else C.gemm_tn2(dy2c, x2c, out, S, S == 1))
+        if ok:
+            if S > 1:
+                C.splitk_reduce(out, g, True)
+            if fuse_bias:
+                C.splitk_reduce(bP, dbias, True)
+            elif dbias is not None:
+                _bias_colsum(dbias, dy2)
+            return
+    if dbias is not None:
+        _bias_colsum(dbias, dy2)
     S = splitk_factor(T, N, K) if (g.is_cuda and g.dtype == torch.bfloat16 and g.is_contiguous()) else 1
     if S == 1:
         g.addmm_(dy2.t(), x2)

@@ -89,12 +89,16 @@ def _ready(*params):
             cb(p)
 
 
-def _wgrad(p, dy2, x2):
-    """dW = dy2^T x2, accumulated into the flat buffer when possible."""
+def _wgrad(p, dy2, x2, bias=None):
+    """dW = dy2^T x2, accumulated into the flat buffer when possible.  With ``bias`` (a flat
+    parameter), its gradient -- the column sums of dy2 -- comes out of the same GEMM."""
     if _flat(p):
-        if not wgrad_on_side_stream(p.grad, dy2, x2):
-            wgrad_accumulate(p.grad, dy2, x2)
+        db = bias.grad if bias is not None else None
+        if not wgrad_on_side_stream(p.grad, dy2, x2, db):
+            wgrad_accumulate(p.grad, dy2, x2, db)
         _ready(p)
+        if bias is not None:
+            _ready(bias)
         return None
     return dy2.t() @ x2
 
@@ -154,10 +158,13 @@ class _AttnBlockFn(torch.autograd.Function):
         C.attn_bwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, do, d5[:, :, 0], d5[:, :, 1], d5[:, :, 2],
                    kb if has_kb else None, lse, scale, p_attn, seed_a, off_a, False)
         dbq, fbq = _vec_grad_out(bqkv)
-        C.bias_act_bwd_into(dqkv, dqkv, None, 0, dbq, False)   # column sum of dqkv
-        if fbq:
-            _ready(bqkv)
-        dWqkv = _wgrad(Wqkv, dqkv, x2)
+        if fbq and _flat(Wqkv):
+            dWqkv = _wgrad(Wqkv, dqkv, x2, bias=bqkv)          # bias grad fused into the wgrad GEMM
+        else:
+            C.bias_act_bwd_into(dqkv, dqkv, None, 0, dbq, False)   # column sum of dqkv
+            if fbq:
+                _ready(bqkv)
+            dWqkv = _wgrad(Wqkv, dqkv, x2)
         dx = ds.addmm_(dqkv, Wqkv)        # residual grad fused: in-place beta=1 epilogue, no C copy
         return (dx.view(B, S, H), dWqkv, None if fbq else dbq, dWo, None if fbo else dbo,
                 None if fg1 else dg1, None if fb1 else db1, None, None, None, None, None,

@@ -177,3 +177,24 @@ def test_gemm_nn_plain_and_dgelu(M, N, K):
     Bw = _rand(K, N + 128, seed=7)
     assert C.gemm_nn(A, Bw[:, 128:], D, 0, False, None, None, None)
     _close(D, A.float() @ Bw[:, 128:].float())
+
+
+@pytest.mark.parametrize("M,N,K,S", [(512, 256, 256, 1), (768, 512, 2048, 4), (3072, 1024, 8192, 16)])
+def test_gemm_tn2_bias_column_sums(M, N, K, S):
+    """gemm_tn2_bias: the weight-gradient product plus per-split column sums of A (the bias
+    gradient) from the extra all-ones MFMA; the product itself is unchanged."""
+    C = _C()
+    A, B = _rand(K, M, seed=M + 1), _rand(K, N, seed=N + 2, scale=K ** -0.5)
+    ref = A.float().t() @ B.float()
+    bP = torch.full((S, M), float("nan"), device="cuda")
+    if S == 1:
+        D = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        assert C.gemm_tn2_bias(A, B, D, 1, True, bP)
+        _close(D, ref)
+    else:
+        P = torch.empty(S, M, N, device="cuda")
+        assert C.gemm_tn2_bias(A, B, P, S, False, bP)
+        torch.testing.assert_close(P.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
+    Ks = K // S
+    want = A.float().view(S, Ks, M).sum(1)
+    torch.testing.assert_close(bP, want, rtol=1e-3, atol=1e-2)
