@@ -180,15 +180,24 @@ struct NtCtx {
 template <int Q, int I0>
 __device__ __forceinline__ void nt_quad_bias(f32x4 (&accb)[2], const nt_s16x8 (&fa)[4][2], int biasw) {
   if (biasw < 0 || (biasw >> 2) != (I0 >> 2)) return;          // rows 0-3 in q0, 4-7 in q2
-  const int i0 = biasw & 3;                                      // 0 or 2 within fa
   nt_s16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;           // bf16 1.0
+  // fragment indices must stay compile-time: a runtime index into fa would put the whole
+  // fragment array in scratch memory
+  if ((biasw & 3) == 0) {
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-      accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)ones, (bf16x8_t)fa[i0 + t][ks], accb[t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t)
+        accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)ones, (bf16x8_t)fa[t][ks], accb[t], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        accb[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)ones, (bf16x8_t)fa[2 + t][ks], accb[t], 0, 0, 0);
+  }
 }
 
 // operand layouts: LAY 0 = NT (A [M,K], B [N,K]), 1 = TN (A [K,M], B [K,N]; weight gradients),

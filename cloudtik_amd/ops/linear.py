@@ -17,6 +17,8 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+# bias gradients out of the MFMA weight-gradient GEMM (extra all-ones MFMA; ops/csrc/gemm_nt.hip)
+_WGRAD_BIAS_FUSE = os.environ.get("CLOUDTIK_AMD_WGRAD_BIAS_FUSE", "1") == "1"
 # split-K for weight-gradient GEMMs: 0 disables, otherwise the maximum split factor
 _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 
@@ -161,7 +163,8 @@ def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
         C = ops.require_native()
         S = tn2_splits(T, N, K)
         dy2c, x2c = dy2.contiguous(), x2.contiguous()
-        fuse_bias = dbias is not None and dbias.dtype == torch.bfloat16 and dbias.is_contiguous()
+        fuse_bias = (_WGRAD_BIAS_FUSE and dbias is not None and dbias.dtype == torch.bfloat16
+                     and dbias.is_contiguous())
         bP = torch.empty(S, N, device=g.device, dtype=torch.float32) if fuse_bias else None
         out = g if S == 1 else torch.empty(S, N, K, device=g.device, dtype=torch.float32)
         ok = (C.gemm_tn2_bias(dy2c, x2c, out, S, S == 1, bP) if fuse_bias
