@@ -25,9 +25,12 @@
 //   * S = Q.K^T and dP = dO.V^T are computed with the key on the lane, so P and dS are
 //     already the B operands of dV^T += dO^T.P and dK^T += Q^T.dS (Q^T, dO^T by
 //     transposed LDS reads); only dS crosses LDS (once) for dQ = dS.K.
-//   * dQ: reduced across the workgroup's waves in LDS; stored directly (bf16) when one
-//     workgroup covers all keys (S <= 128, the BERT phase-1 case), otherwise accumulated
-//     with fp32 atomics in the full-rate 2x128-byte shape and converted by a tiny kernel.
+//   * dQ: each wave owns 16 queries x 32 d of the q-tile and sums over all 128 keys itself
+//     (16x16x32 MFMAs on transposed reads of dS^T and K: no cross-wave reduction); the
+//     q-tile inputs and dS^T are double-buffered, so each q-tile takes ONE barrier.  Stored
+//     directly (bf16, 16-byte stores after a permlane16 swap) when one workgroup covers all
+//     keys (S <= 128, the BERT phase-1 case), otherwise accumulated with fp32 atomics and
+//     converted by a tiny kernel.
 //   * attention-prob dropout regenerated from a counter hash (nothing stored).
 #include "common.h"
 
@@ -280,17 +283,19 @@ struct AttnBwdArgs {
 
 template <bool DROP, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
-  // LDS: Q tile 4K | dO tile 4K | K block 16K | dS 8K | dQ pair-reduce 8K | lse, delta
-  // LDS: Q tile 4K | dO tile 4K | K block 16K | V block 16K | dS^T 8K | dQ pair-reduce 8K | lse, delta
-  __shared__ __attribute__((aligned(16))) char smem[4096 + 4096 + 16384 + 16384 + 8192 + 8192 + 256];
+  // LDS: Q tiles 2 x 4K | dO tiles 2 x 4K | K block 16K | V block 16K | dS^T 2 x 8K | lse, delta 2 x 256 B
+  // The per-q-tile inputs (Q, dO, lse, delta) and dS^T are double-buffered, so one barrier per
+  // q-tile orders everything: tile t+2 is staged into the buffers tile t has just released, and
+  // dQ needs no cross-wave reduction (each wave owns 16 queries x 32 d of the tile's dQ and sums
+  // over all 128 keys itself).
+  __shared__ __attribute__((aligned(16))) char smem[8192 + 8192 + 16384 + 16384 + 16384 + 512];
   char* Qs = smem;
-  char* dOs = smem + 4096;
-  char* Ks = smem + 8192;
-  char* Vs = smem + 24576;
-  char* dSs = smem + 40960;
-  float* red = reinterpret_cast<float*>(smem + 49152);
-  float* lse_s = reinterpret_cast<float*>(smem + 57344);
-  float* delta_s = lse_s + 32;
+  char* dOs = smem + 8192;
+  char* Ks = smem + 16384;
+  char* Vs = smem + 32768;
+  char* dSs = smem + 49152;
+  float* lse_s = reinterpret_cast<float*>(smem + 65536);      // [2][32]
+  float* delta_s = lse_s + 64;                                // [2][32]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   const bf16_t* vp = a.v + b * a.v_sb + h * a.v_sh;
   // K and V blocks (128 keys) into LDS: row reads give the B operands of S = Q K^T and
   // dP = dO V^T (re-read per q-tile instead of pinning 32 VGPRs), transposed reads of K
-  // give dQ's B operand
+  // give dQ's operand
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i;
@@ -334,11 +339,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   const bool single_block = gridDim.x == 1;
   // 16-byte dQ stores need 8-element strides and a 16-byte aligned base
   const bool dq16 = ((a.dq_ss | a.dq_sb | a.dq_sh) & 7) == 0 && (((uintptr_t)a.dq) & 15) == 0;
-  const int dt_q = w & 1, kh = w >> 1;  // this wave's share of the dQ product
+  // this wave's share of the tile's dQ: queries 16 (w & 1) .. +16, d 32 (w >> 1) .. +32
+  const int dq_q0 = 16 * (w & 1), dq_d0 = 32 * (w >> 1);
+  // 16x16x32 fragment lane roles (transposing reads): g = lane >> 4 picks 8 keys, q4 / p4 a
+  // row / 4-column group inside them
+  const int fg = lane >> 4, fq = (lane & 15) >> 2, fp = lane & 3;
 
-  // Q / dO / lse / delta tiles are register-prefetched one q-tile ahead (issued before the
-  // tile's MFMAs, written to LDS after the mid barrier): 2 barriers per q-tile, and the
-  // global-load latency of tile t+1 hides under the compute of tile t.
+  // Q / dO / lse / delta tiles are register-prefetched two q-tiles ahead (issued before the
+  // tile's MFMAs, written to LDS after its barrier into the buffer it has just released)
   const int prow = tid >> 3, pch = tid & 7;
   // delta = rowsum(dO * O) is computed here (no separate kernel): each thread prefetches
   // the O chunk matching its dO chunk; the 8 threads of a row reduce at staging time
@@ -356,32 +364,42 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
       pL = ok2_ ? a.lse[(long)bh * a.Sq + (qb_) + tid] : INFINITY;                          \
     }                                                                                       \
   }
-#define BWD_STAGE()                                                                         \
+#define BWD_STAGE(buf_)                                                                     \
   {                                                                                         \
-    *reinterpret_cast<u16x8*>(Qs + swz(prow, pch)) = pQ;                                    \
-    *reinterpret_cast<u16x8*>(dOs + swz(prow, pch)) = pdO;                                  \
-    if (tid < 32) lse_s[tid] = pL;                                                          \
+    *reinterpret_cast<u16x8*>(Qs + (buf_) * 4096 + swz(prow, pch)) = pQ;                    \
+    *reinterpret_cast<u16x8*>(dOs + (buf_) * 4096 + swz(prow, pch)) = pdO;                  \
+    if (tid < 32) lse_s[(buf_) * 32 + tid] = pL;                                            \
     float dd_ = 0.f;                                                                        \
     _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) dd_ += bf2f(pdO[j_]) * bf2f(pO[j_]);  \
     dd_ += __shfl_xor(dd_, 1, 64);                                                          \
     dd_ += __shfl_xor(dd_, 2, 64);                                                          \
     dd_ += __shfl_xor(dd_, 4, 64);                                                          \
-    if (pch == 0) delta_s[prow] = dd_;                                                      \
+    if (pch == 0) delta_s[(buf_) * 32 + prow] = dd_;                                        \
   }
   BWD_PREFETCH(0);
-  BWD_STAGE();
+  BWD_STAGE(0);
+  if (nq > 1) {
+    BWD_PREFETCH(32);
+    BWD_STAGE(1);
+  }
   __syncthreads();
 
   for (int qt = 0; qt < nq; ++qt) {
     const int qb = qt * 32;
-    if (qt + 1 < nq) BWD_PREFETCH(qb + 32);
+    const int buf = qt & 1;
+    if (qt + 2 < nq) BWD_PREFETCH(qb + 64);
+    const char* Qt = Qs + buf * 4096;
+    const char* dOt = dOs + buf * 4096;
+    const float* lse_t = lse_s + buf * 32;
+    const float* delta_t = delta_s + buf * 32;
+    char* dSt = dSs + buf * 8192;
     f32x16 S, dP;
 #pragma unroll
     for (int i = 0; i < 16; ++i) { S[i] = 0.f; dP[i] = 0.f; }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      S = mfma32(lds_b128(Qs + swz(r, 2 * s + hh)), lds_b128(Ks + swz(krow, 2 * s + hh)), S);
-      dP = mfma32(lds_b128(dOs + swz(r, 2 * s + hh)), lds_b128(Vs + swz(krow, 2 * s + hh)), dP);
+      S = mfma32(lds_b128(Qt + swz(r, 2 * s + hh)), lds_b128(Ks + swz(krow, 2 * s + hh)), S);
+      dP = mfma32(lds_b128(dOt + swz(r, 2 * s + hh)), lds_b128(Vs + swz(krow, 2 * s + hh)), dP);
     }
     // dropout keep bits: the pair (even key, odd key) shares one hash; the two lanes of a
     // pair (lane ^ 1) each hash 8 of the 16 query rows and swap halves with one DPP move
@@ -406,8 +424,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     // reg i <-> query row qrow(i) = (i&3) + 8(i>>2) + 4hh of this tile; column = key_l
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_s + 8 * g + 4 * hh);
-      const f32x4 D4 = *reinterpret_cast<const f32x4*>(delta_s + 8 * g + 4 * hh);
+      const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_t + 8 * g + 4 * hh);
+      const f32x4 D4 = *reinterpret_cast<const f32x4*>(delta_t + 8 * g + 4 * hh);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int i = 4 * g + j;
@@ -433,10 +451,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const int qr = 16 * s2 + 4 * hh + trow;
-      const bf16x8_t ado0 = cat_tr(lds_tr(dOs + swz_e(qr, tcol)), lds_tr(dOs + swz_e(qr + 8, tcol)));
-      const bf16x8_t ado1 = cat_tr(lds_tr(dOs + swz_e(qr, 32 + tcol)), lds_tr(dOs + swz_e(qr + 8, 32 + tcol)));
-      const bf16x8_t aq0 = cat_tr(lds_tr(Qs + swz_e(qr, tcol)), lds_tr(Qs + swz_e(qr + 8, tcol)));
-      const bf16x8_t aq1 = cat_tr(lds_tr(Qs + swz_e(qr, 32 + tcol)), lds_tr(Qs + swz_e(qr + 8, 32 + tcol)));
+      const bf16x8_t ado0 = cat_tr(lds_tr(dOt + swz_e(qr, tcol)), lds_tr(dOt + swz_e(qr + 8, tcol)));
+      const bf16x8_t ado1 = cat_tr(lds_tr(dOt + swz_e(qr, 32 + tcol)), lds_tr(dOt + swz_e(qr + 8, 32 + tcol)));
+      const bf16x8_t aq0 = cat_tr(lds_tr(Qt + swz_e(qr, tcol)), lds_tr(Qt + swz_e(qr + 8, tcol)));
+      const bf16x8_t aq1 = cat_tr(lds_tr(Qt + swz_e(qr, 32 + tcol)), lds_tr(Qt + swz_e(qr + 8, 32 + tcol)));
       dV0 = mfma32(ado0, pf[s2], dV0);
       dV1 = mfma32(ado1, pf[s2], dV1);
       dK0 = mfma32(aq0, dsf[s2], dK0);
@@ -446,7 +464,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     // each lane owns one key row and 4 runs of 4 consecutive queries -> 4 ds_write_b64
     {
       const int key = w * 32 + r;
-      char* rowp = dSs + key * 64;
+      char* rowp = dSt + key * 64;
       const int sw = (key >> 1) & 7;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -455,64 +473,48 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
         *reinterpret_cast<u16x4*>(rowp + ((c ^ sw) << 3)) = v;
       }
     }
-    __syncthreads();   // (B1) every wave is done reading Qs / dOs / lse / delta of this tile
-    if (qt + 1 < nq) BWD_STAGE();
-    // dQ[q][d] partial = dS[q][kh*64 .. +64] . K[kh*64 .. +64][dt_q*32 .. +32]
-    // A (dS, q on the lane) by transposed reads of dS^T; B (K columns) by transposed reads
-    f32x16 acc;
+    __syncthreads();   // the ONLY barrier of the tile: dS^T complete; this tile's Q / dO / lse /
+                       // delta buffers free; tile t+1's staged buffers visible
+    if (qt + 2 < nq) BWD_STAGE(buf);
+    // dQ[q][d] = sum over the 128 keys of dS[q][key] K[key][d], 16x16x32 MFMAs issued as
+    // (K^T fragment, dS fragment): the lane ends up with 4 consecutive d of one query.  Both
+    // fragments (8 consecutive keys per lane) come from transposing reads of [key][.] images.
+    f32x4 dq0 = {0.f, 0.f, 0.f, 0.f}, dq1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    const int qcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;   // 4 queries this lane addresses
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kr = kh * 64 + 16 * s + 8 * hh + trow;
-      const int r0 = kr, r1 = kr + 4;
-      const bf16x8_t aa = cat_tr(lds_tr(dSs + r0 * 64 + ((((qcol >> 2)) ^ ((r0 >> 1) & 7)) << 3)),
-                                 lds_tr(dSs + r1 * 64 + ((((qcol >> 2)) ^ ((r1 >> 1) & 7)) << 3)));
-      const bf16x8_t bb = cat_tr(lds_tr(Ks + swz_e(kr, dt_q * 32 + tcol)), lds_tr(Ks + swz_e(kr + 4, dt_q * 32 + tcol)));
-      acc = mfma32(aa, bb, acc);
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr0 = 32 * ks + 8 * fg + fq, kr1 = kr0 + 4;
+      const int qc = (dq_q0 >> 2) + fp;        // 8-byte chunk of queries dq_q0 + 4 fp .. + 3
+      const bf16x8_t sf = cat_tr(lds_tr(dSt + kr0 * 64 + ((qc ^ ((kr0 >> 1) & 7)) << 3)),
+                                 lds_tr(dSt + kr1 * 64 + ((qc ^ ((kr1 >> 1) & 7)) << 3)));
+      const bf16x8_t kf0 = cat_tr(lds_tr(Ks + swz_e(kr0, dq_d0 + 4 * fp)), lds_tr(Ks + swz_e(kr1, dq_d0 + 4 * fp)));
+      const bf16x8_t kf1 = cat_tr(lds_tr(Ks + swz_e(kr0, dq_d0 + 16 + 4 * fp)),
+                                  lds_tr(Ks + swz_e(kr1, dq_d0 + 16 + 4 * fp)));
+      dq0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf0, sf, dq0, 0, 0, 0);
+      dq1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf1, sf, dq1, 0, 0, 0);
     }
-    if (kh == 1) {
+    // dq0[rr] = dQ[q = dq_q0 + (lane & 15)][d = dq_d0 + 4 (lane >> 4) + rr], dq1 the same +16
+    const int q = qb + dq_q0 + (lane & 15);
+    if (single_block && dq16 && qb + 32 <= a.Sq) {
+      const u16x4 o0 = {f2bf(dq0[0] * a.scale), f2bf(dq0[1] * a.scale), f2bf(dq0[2] * a.scale), f2bf(dq0[3] * a.scale)};
+      const u16x4 o1 = {f2bf(dq1[0] * a.scale), f2bf(dq1[1] * a.scale), f2bf(dq1[2] * a.scale), f2bf(dq1[3] * a.scale)};
+      // permlane16 swap of the two d blocks: lane group g gets 8 consecutive d
+      const uint2 xv = __builtin_bit_cast(uint2, o0), yv = __builtin_bit_cast(uint2, o1);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(xv.x, yv.x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(xv.y, yv.y, false, false);
+      const uint4 v = {s0[0], s1[0], s0[1], s1[1]};
+      const int d = dq_d0 + 16 * (fg & 1) + 8 * (fg >> 1);
+      *reinterpret_cast<uint4*>(dqbase + q * (int)a.dq_ss + d) = v;
+    } else if (q < a.Sq) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) red[(dt_q * 16 + i) * 64 + lane] = acc[i];
-    }
-    __syncthreads();   // (B2) red visible; staged tile t+1 visible for the next iteration
-    if (kh == 0) {
-      const int d = dt_q * 32 + r;
-      if (single_block && qb + 32 <= a.Sq && dq16) {
-        // whole tile in range (every q-tile when Sq % 32 == 0).  The lane holds 16 queries of
-        // one d; re-layout through this wave's own 4 KiB of `red` (its reads of it are done:
-        // LDS executes a wave's accesses in order) as fp32 [32 q][32 d], then 16-byte bf16
-        // stores of 8 consecutive d: 2 stores per lane instead of 16 two-byte ones
-        float v[16];
+      for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
-        float* stg = red + dt_q * 1024;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) stg[((i & 3) + 8 * (i >> 2) + 4 * hh) * 32 + r] = v[i];
-#pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2) {
-          const int cidx = lane + 64 * c2, qr = cidx >> 2, seg = cidx & 3;
-          const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + qr * 32 + seg * 8);
-          const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + qr * 32 + seg * 8 + 4);
-          const u16x8 o = {f2bf(lo[0]), f2bf(lo[1]), f2bf(lo[2]), f2bf(lo[3]),
-                           f2bf(hi[0]), f2bf(hi[1]), f2bf(hi[2]), f2bf(hi[3])};
-          *reinterpret_cast<u16x8*>(dqbase + (qb + qr) * (int)a.dq_ss + dt_q * 32 + seg * 8) = o;
+        for (int rr = 0; rr < 4; ++rr) {
+          const int d = dq_d0 + 16 * t2 + 4 * fg + rr;
+          const float val = (t2 ? dq1[rr] : dq0[rr]) * a.scale;
+          if (single_block) dqbase[q * (int)a.dq_ss + d] = f2bf(val);
+          else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int q = qb + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const float val = (acc[i] + red[(dt_q * 16 + i) * 64 + lane]) * a.scale;
-          if (q < a.Sq) {
-            if (single_block) dqbase[q * (int)a.dq_ss + d] = f2bf(val);
-            else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
-          }
-        }
-      }
     }
-    // no trailing barrier: the next tile's dS / red writes happen after its (B1), which
-    // every wave reaches only after finishing these reads
   }
 #undef BWD_PREFETCH
 #undef BWD_STAGE
