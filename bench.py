@@ -462,10 +462,13 @@ def timed(step, args, rank, world, device, audit=False):
     loss = None
     if cuda:
         events[0].record()
+    host = []                       # host-side issue time of each step (no sync inside the loop)
     for i in range(args.steps):
+        th = time.perf_counter()
         loss = step()
         if cuda:
             events[i + 1].record()
+            host.append((time.perf_counter() - th) * 1e3)
         else:
             stamps.append(time.perf_counter())
     barrier()
@@ -482,6 +485,9 @@ def timed(step, args, rank, world, device, audit=False):
         out = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(out, t)
         per_rank = [float(o.item()) for o in out]
+    if host:
+        # a host issue time close to the GPU step time means the step is launch / host bound
+        info = dict(info or {}, host_issue_ms_mean=round(sum(host) / len(host), 3))
     return max(per_rank), per_rank, float(loss.detach().float().item()), step_ms, info
 
 
@@ -501,9 +507,11 @@ def run_one(build, args, rank, world, device, kind):
     step, close, info = build(args, rank, world, device, kind)
     elapsed, per_rank, loss, step_ms, audit = timed(step, args, rank, world, device,
                                                     audit=info["unit"] == "images/s")
+    host_ms = audit.pop("host_issue_ms_mean", None) if audit else None
     if audit and rank == 0:
         print(f"[bench] {info['model']} kernel audit (one untimed step): {json.dumps(audit)}", file=sys.stderr)
     plan = info.pop("plan", None)
+    info["host_issue_ms"] = host_ms
     close()
     del step
     gc.collect()
@@ -594,6 +602,7 @@ def main():
                "step_ms_mean": head["step_ms_mean"], "step_ms_ci95": head["step_ms_ci95"],
                "value_mean_per_step": head["rate_mean"], "value_ci95": head["rate_ci95"],
                "bucket_plan": head["plan"],
+               "host_issue_ms_per_step": head.get("host_issue_ms"),
                "env": {k: envinfo.get(k) for k in ("gpu", "rccl", "nccl_env", "rank0_cpus", "tunableop",
                                                    "distinct_devices", "world_size_seen_by_collective")
                        if envinfo.get(k) is not None},
@@ -614,6 +623,7 @@ def main():
             out[f"{key}_step_ms_mean"], out[f"{key}_step_ms_ci95"] = r["step_ms_mean"], r["step_ms_ci95"]
             out[f"{key}_value_mean_per_step"], out[f"{key}_value_ci95"] = r["rate_mean"], r["rate_ci95"]
             out[f"{key}_bucket_plan"] = r["plan"]
+            out[f"{key}_host_issue_ms_per_step"] = r.get("host_issue_ms")
             if "hip_graph" in r:
                 out[f"{key}_hip_graph"] = r["hip_graph"]
             if r.get("audit"):

@@ -136,6 +136,67 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), padding=(0, 0), ou
     return out, mean, var
 
 
+class _DgradWeights:
+    """The data-gradient weight matrices ([Ci, taps * Co], taps flipped per phase) of every
+    conv weight that lives in one parameter storage (train.optim.FlatParamSpace), rebuilt by
+    ONE gather kernel per backward pass instead of one transposing copy per conv and phase
+    (56 small launches on the critical path of a ResNet-50 backward).
+
+    Weights change only between backward passes (optimizer steps), so the matrices are
+    refreshed at the first data gradient of each backward (a new autograd graph task); a key
+    first seen mid-backward is gathered on its own and joins the batched gather from the next
+    pass.  Outside a backward pass (direct calls) nothing is cached."""
+
+    def __init__(self):
+        self.groups = {}          # storage ptr -> dict(keys, idx, buf, flat, task, slices)
+
+    @staticmethod
+    def _index(w, rs):
+        co, ci, R, S = w.shape
+        wi = torch.arange(w.storage_offset(), w.storage_offset() + w.numel(), device=w.device).view(co, R, S, ci)
+        wti = wi.permute(3, 1, 2, 0)                            # [Ci, R, S, Co] of storage indices
+        if len(rs) == R * S:
+            return wti.reshape(ci, -1).contiguous()
+        return torch.stack([wti[:, r, q, :] for r, q in rs], 1).reshape(ci, -1).contiguous()
+
+    def get(self, w: torch.Tensor, rs) -> Optional[torch.Tensor]:
+        task = torch._C._current_graph_task_id()
+        if task == -1 or not w.is_contiguous(memory_format=torch.channels_last):
+            return None
+        st = w.untyped_storage()
+        g = self.groups.get(st.data_ptr())
+        if g is None:
+            flat = torch.empty(0, dtype=w.dtype, device=w.device).set_(st)
+            g = self.groups[st.data_ptr()] = {"keys": {}, "idx": None, "buf": None, "flat": flat, "task": None}
+        key = (w.storage_offset(), tuple(w.shape), tuple(rs))
+        if key not in g["keys"]:
+            idx = self._index(w, rs)
+            g["keys"][key] = idx
+            g["idx"] = None                                      # rebuild the batched index next pass
+            return torch.index_select(g["flat"], 0, idx.view(-1)).view(idx.shape)
+        if g["idx"] is None:
+            # batched layout: every key's matrix back to back in one buffer
+            parts, off, slices = [], 0, {}
+            for k, idx in g["keys"].items():
+                slices[k] = (off, idx.shape)
+                parts.append(idx.view(-1))
+                off += idx.numel()
+            g["idx"] = torch.cat(parts)
+            g["buf"] = torch.empty(off, dtype=w.dtype, device=w.device)
+            g["slices"] = slices
+            g["task"] = None
+        if g["task"] != task:
+            torch.index_select(g["flat"], 0, g["idx"], out=g["buf"])
+            g["task"] = task
+        off, shape = g["slices"][key]
+        n = shape[0] * shape[1]
+        return g["buf"][off:off + n].view(shape)
+
+
+_DGRAD_W = _DgradWeights()
+_DGRAD_W_CACHE = os.environ.get("CLOUDTIK_AMD_CONV_DGRAD_WCACHE", "1") == "1"
+
+
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), padding=(0, 0),
                out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
     """dX of conv2d(x, w) for the NHWC bf16 gradient dy; ``accumulate`` adds into ``out``."""
@@ -155,10 +216,12 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
     for (a, b), (Hr, Wr), taps, rs in phases:
         if not rs:
             continue
-        if len(rs) == R * S:
-            wm = wt.reshape(ci, -1).contiguous()
-        else:
-            wm = torch.stack([wt[:, r, s, :] for r, s in rs], 1).reshape(ci, -1).contiguous()
+        wm = _DGRAD_W.get(w, rs) if _DGRAD_W_CACHE else None
+        if wm is None:
+            if len(rs) == R * S:
+                wm = wt.reshape(ci, -1).contiguous()
+            else:
+                wm = torch.stack([wt[:, r, s, :] for r, s in rs], 1).reshape(ci, -1).contiguous()
         geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
         if not C.conv_igemm(dy, wm, out, geo, taps, accumulate, None, _CFG):
             raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)} w{tuple(w.shape)}")

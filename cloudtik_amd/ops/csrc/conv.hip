@@ -630,7 +630,12 @@ __global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restric
 // 3 = 128x256 (8 waves 2x4); -1 = the largest that divides (Co, T*Ci)
 extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   if (cfg >= 0) return cfg;
-  if (Co % 128 == 0 && NN % 128 == 0) return 2;      // 128 x 128 was fastest at every such shape
+  // per-shape probe over every ResNet-50 conv (profiles/r3/conv_wgrad_cfg.md): the 8-wave
+  // 128 x 256 tile wins wherever it divides (l4.c2 357 -> 146 us, l3.c2 183 -> 111 us), then
+  // 128 x 128, then 64 x 128 for 64-channel outputs (l1.c1 163 -> 128 us)
+  if (Co % 128 == 0 && NN % 256 == 0) return 3;
+  if (Co % 128 == 0 && NN % 128 == 0) return 2;
+  if (NN % 128 == 0) return 1;
   return 0;
 }
 

@@ -82,7 +82,8 @@ def _rel(a, b):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ci,co,H,k,s", [(64, 64, 14, 3, 1), (128, 256, 9, 1, 1), (64, 128, 15, 3, 2),
-                                         (256, 64, 8, 1, 2), (128, 128, 7, 3, 1), (64, 192, 11, 3, 1)])
+                                         (256, 64, 8, 1, 2), (128, 128, 7, 3, 1), (64, 192, 11, 3, 1),
+                                         (256, 128, 8, 3, 1), (512, 256, 7, 1, 2)])
 def test_kernels_match_fp32_reference(cuda, ci, co, H, k, s):
     torch.manual_seed(ci + co + H)
     pad = k // 2
@@ -197,3 +198,39 @@ def test_stem_kernels_match_fp32_reference(cuda):
     x8 = CV.to_nhwc8(x)
     dw = CV.stem_wgrad(dy, x8, w.shape, (2, 2), (3, 3))
     assert _rel(dw, wr.grad) < 1e-2
+
+
+def test_dgrad_weight_cache_matches_direct_transposes():
+    """_DgradWeights: per-phase [Ci, taps*Co] matrices of channels_last weights living in one
+    flat storage, built per key on first sight and by one batched gather from the next
+    backward pass on, equal the direct permute/stack copies."""
+    flat = torch.randn(5000)
+    w = flat[64:64 + 8 * 4 * 9].view(8, 3, 3, 4).permute(0, 3, 1, 2)      # channels_last view
+    assert w.is_contiguous(memory_format=torch.channels_last)
+    cache = CV._DgradWeights()
+    full_rs = [(r, q) for r in range(3) for q in range(3)]
+    sub_rs = [(0, 0), (2, 1)]
+    got = []
+
+    class Probe(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 1
+
+        @staticmethod
+        def backward(ctx, g):
+            got.append((cache.get(w, full_rs).clone(), cache.get(w, sub_rs).clone()))
+            return g
+
+    x = torch.ones(2, requires_grad=True)
+    for step in range(3):
+        Probe.apply(x).sum().backward()
+        if step == 1:
+            with torch.no_grad():
+                flat.mul_(2.0)                   # "optimizer step": the next pass must refresh
+    wt = w.permute(1, 2, 3, 0)                    # current (doubled) weights
+    for i, (full, sub) in enumerate(got):
+        scale = 0.5 if i < 2 else 1.0            # passes 0 and 1 ran before the update
+        torch.testing.assert_close(full, wt.reshape(4, -1) * scale)
+        torch.testing.assert_close(sub, torch.stack([wt[:, 0, 0, :], wt[:, 2, 1, :]], 1).reshape(4, -1) * scale)
+    assert cache.get(w, full_rs) is None        # outside a backward pass nothing is cached
