@@ -197,22 +197,63 @@ _DGRAD_W = _DgradWeights()
 _DGRAD_W_CACHE = os.environ.get("CLOUDTIK_AMD_CONV_DGRAD_WCACHE", "1") == "1"
 
 
+BN_BWD_FUSE = os.environ.get("CLOUDTIK_AMD_CONV_BN_BWD_FUSE", "1") == "1"
+
+
+class BnBwdLink:
+    """Hand-off between a BatchNorm + ReLU (mask recomputed from its input, ops.functional
+    ``_BNActFn`` mode 2) and the conv that consumes its output.  The conv's data gradient IS the
+    BatchNorm's incoming gradient, so the conv epilogue (conv.hip EPI 2) masks it and reduces the
+    BatchNorm-backward sums per tile; ``pending`` carries those partials to the BatchNorm's
+    backward, which then skips its own reduction pass over dy and x.  The gradient tensor's
+    identity and version are recorded so a gradient that autograd summed with another consumer's
+    (or modified) is never paired with stale partials."""
+
+    __slots__ = ("x", "stat", "pending")
+
+    def __init__(self, x: torch.Tensor, stat: torch.Tensor):
+        self.x = x
+        self.stat = stat
+        self.pending = None
+
+    def take(self, dy: torch.Tensor):
+        """The partials for ``dy`` (part, tiles, rows), or None."""
+        p, self.pending = self.pending, None
+        if p is None or dy.data_ptr() != p[3] or dy._version != p[4]:
+            return None
+        return p[:3]
+
+
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), padding=(0, 0),
-               out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
-    """dX of conv2d(x, w) for the NHWC bf16 gradient dy; ``accumulate`` adds into ``out``."""
+               out: Optional[torch.Tensor] = None, accumulate: bool = False, bn: Optional[BnBwdLink] = None):
+    """dX of conv2d(x, w) for the NHWC bf16 gradient dy; ``accumulate`` adds into ``out``.
+
+    ``bn``: x is the output of that BatchNorm + ReLU; dX is returned ReLU-masked and the
+    BatchNorm-backward partial sums are left in ``bn.pending`` (see BnBwdLink)."""
     N, ci, H, W = x_shape
     co, _, R, S = w.shape
     phases = dgrad_phases(x_shape, w.shape, tuple(stride), tuple(padding))
     empty_phase = any(not rs for _, _, _, rs in phases)
+    C = _C()
+    bn_plan = None
+    if bn is not None and not accumulate and bn.x.shape == tuple(x_shape) and co % 64 == 0:
+        tiles = []
+        for _, (Hr, Wr), taps, rs in phases:
+            if rs:
+                m = N * Hr * Wr
+                bm = C.conv_igemm_tile_m(_CFG, ci, m, len(taps) // 2 * (co // 64))
+                tiles.append((m + bm - 1) // bm)
+        rows = sum(tiles)
+        bn_plan = (torch.empty(2 * rows * ci, device=dy.device, dtype=torch.float32), rows)
     if out is None:
         out = torch.empty((N, ci, H, W), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
         if empty_phase and not accumulate:
             out.zero_()
     elif empty_phase and not accumulate:
         out.zero_()
-    C = _C()
     wt = w.permute(1, 2, 3, 0)                      # [Ci, R, S, Co]
     sh, sw = stride
+    tile0 = 0
     for (a, b), (Hr, Wr), taps, rs in phases:
         if not rs:
             continue
@@ -223,8 +264,19 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
             else:
                 wm = torch.stack([wt[:, r, s, :] for r, s in rs], 1).reshape(ci, -1).contiguous()
         geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
+        if bn_plan is not None:
+            part, rows = bn_plan
+            if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, bn.stat, part, tile0, rows):
+                bm = C.conv_igemm_tile_m(_CFG, ci, geo[11], len(taps) // 2 * (co // 64))
+                tile0 += (geo[11] + bm - 1) // bm
+                continue
+            if tile0:
+                raise RuntimeError("conv_igemm_bn rejected a later phase of a supported data gradient")
+            bn_plan = None                          # configuration without the fused epilogue
         if not C.conv_igemm(dy, wm, out, geo, taps, accumulate, None, _CFG):
             raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)} w{tuple(w.shape)}")
+    if bn_plan is not None:
+        bn.pending = (bn_plan[0], tile0, bn_plan[1], out.data_ptr(), out._version)
     return out
 
 
@@ -309,6 +361,8 @@ class ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.padding = stride, padding
         ctx.wp = w
+        # x = the output of a BatchNorm + ReLU: its backward reduction runs in our dgrad epilogue
+        ctx.bn_link = getattr(x, "_ct_bn_bwd", None) if (BN_BWD_FUSE and not keep_input) else None
         if bn_stats:
             # the epilogue reduces the BatchNorm statistics of y per tile; the BatchNorm that
             # consumes y picks them up instead of re-reading y for a statistics pass
@@ -328,7 +382,8 @@ class ConvFn(torch.autograd.Function):
                     and dx_other.is_contiguous(memory_format=torch.channels_last)):
                 dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding, out=dx_other, accumulate=True)
             else:
-                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding)
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding,
+                                bn=ctx.bn_link if dx_other is None else None)
                 if dx_other is not None:
                     dx = dx + dx_other
         if ctx.needs_input_grad[1]:

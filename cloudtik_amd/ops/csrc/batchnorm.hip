@@ -744,3 +744,50 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
   }
   return 0;
 }
+
+// first-level sum of per-tile BatchNorm-backward partials (the conv data-gradient epilogue's,
+// conv.hip EPI 2: thousands of tile rows): rows [64 g, 64 g + 64) of p1 / p2 -> row g of
+// q1 / q2.  One thread per (group, channel), coalesced over channels.
+__global__ __launch_bounds__(256) void bn_bwd_partials_sum_kernel(const float* __restrict__ p1,
+                                                                 const float* __restrict__ p2, int tiles, int C,
+                                                                 float* __restrict__ q1, float* __restrict__ q2) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int t0 = blockIdx.x * 64, t1 = min(tiles, t0 + 64);
+  float a = 0.f, b = 0.f;
+#pragma unroll 8
+  for (int t = t0; t < t1; ++t) {
+    a += p1[(size_t)t * C + c];
+    b += p2[(size_t)t * C + c];
+  }
+  q1[(size_t)blockIdx.x * C + c] = a;
+  q2[(size_t)blockIdx.x * C + c] = b;
+}
+
+// BatchNorm (+ ReLU) backward whose reduction was done by the producer of dy (conv.hip EPI 2):
+// dym = the already-masked gradient, p1 / p2 = per-tile sums [tiles][C] (p2 = p1 + p2off).
+// work = float[2 * ceil(tiles / 64) * C + 3 * C] scratch.
+extern "C" int ct_bn_bwd_given(const void* dym, const void* x, const void* gamma, const float* stat, void* dx,
+                               void* dgamma, void* dbeta, int param_flags, const float* p1, long p2off, int tiles,
+                               float* work, int M, int C, hipStream_t stream) {
+  if (C % 8 || C > 2048 || M <= 0 || tiles <= 0) return -1;
+  const int G = (tiles + 63) / 64;
+  float* q1 = work;
+  float* q2 = work + (size_t)G * C;
+  float* coef = q2 + (size_t)G * C;
+  bn_bwd_partials_sum_kernel<<<dim3(G, ceil_div(C, 256)), 256, 0, stream>>>(p1, p1 + p2off, tiles, C, q1, q2);
+  const int acc = (param_flags >> 1) & 1;
+  if (param_flags & 1)
+    bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
+        q1, q2, G, M, C, (const bf16_t*)gamma, stat, stat + C, (float*)dgamma, (float*)dbeta, coef, coef + C,
+        coef + 2 * C, acc);
+  else
+    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
+        q1, q2, G, M, C, (const bf16_t*)gamma, stat, stat + C, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C,
+        coef + 2 * C, acc);
+  const long tv = (long)M * (C / 8);
+  const BnMask none{0, nullptr, nullptr, nullptr};
+  BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dym, none, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
+                 (bf16_t*)dx, (bf16_t*)nullptr, tv, C / 8);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}

@@ -45,6 +45,8 @@ int ct_bn_fwd_train_given(const void*, const void*, const void*, const void*, fl
 int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
                          int, int, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
+int ct_bn_bwd_given(const void*, const void*, const void*, const float*, void*, void*, void*, int, const float*, long,
+                    int, float*, int, int, hipStream_t);
 int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, void*, void*, void*, void*, int,
               float*, float*, int, int, int, hipStream_t);
 int ct_attn_fwd(const void*, const long*, const void*, const long*, const void*, const long*, void*,
@@ -563,6 +565,40 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::T
   return {dx, dres, dgamma, dbeta};
 }
 
+// BatchNorm (+ ReLU) backward from the reduction done by the conv that produced dy
+// (conv_igemm_bn): dym = the masked gradient, part = float[2 * rows * C] per-tile sums (first
+// `tiles` rows of each half).  Returns (dx, dgamma, dbeta).
+std::vector<at::Tensor> bn_bwd_given(at::Tensor dym, at::Tensor x, at::Tensor gamma, at::Tensor stat, at::Tensor part,
+                                     int64_t tiles, int64_t rows, c10::optional<at::Tensor> dgamma_acc,
+                                     c10::optional<at::Tensor> dbeta_acc) {
+  check_nhwc(x, "x");
+  check_nhwc(dym, "dym");
+  const int C = x.size(1);
+  const long M = nhwc_rows(x);
+  TORCH_CHECK(dym.sizes() == x.sizes() && dym.strides() == x.strides(), "bn_bwd_given: dym / x layout");
+  TORCH_CHECK(C <= 2048 && stat.numel() == 4 * (long)C, "bn_bwd_given: stat must be float[4C], C <= 2048");
+  CHECK_F32(stat);
+  CHECK_F32(part);
+  TORCH_CHECK(tiles > 0 && tiles <= rows && part.numel() >= 2 * rows * C, "bn_bwd_given: part buffer");
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined();
+  if (acc) {
+    TORCH_CHECK(dbeta_acc.has_value() && dbeta_acc->defined(), "bn_bwd_given: dgamma_acc needs dbeta_acc");
+    TORCH_CHECK(dgamma_acc->is_contiguous() && dbeta_acc->is_contiguous() && dgamma_acc->numel() == C &&
+                dbeta_acc->numel() == C && dgamma_acc->scalar_type() == gamma.scalar_type() &&
+                dbeta_acc->scalar_type() == gamma.scalar_type(), "bn_bwd_given: bad accumulate targets");
+  }
+  auto dx = at::empty_like(x);
+  auto dgamma = acc ? *dgamma_acc : at::empty_like(gamma), dbeta = acc ? *dbeta_acc : at::empty_like(gamma);
+  const long G = (tiles + 63) / 64;
+  auto work = at::empty({2 * G * C + 3 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_bwd_given(dym.data_ptr(), x.data_ptr(), gamma.data_ptr(), stat.data_ptr<float>(), dx.data_ptr(),
+                           dgamma.data_ptr(), dbeta.data_ptr(),
+                           (gamma.scalar_type() == at::kFloat ? 1 : 0) | (acc ? 2 : 0), part.data_ptr<float>(),
+                           rows * C, (int)tiles, work.data_ptr<float>(), (int)M, C, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_bwd_given: unsupported C=", C);
+  return {dx, dgamma, dbeta};
+}
+
 void register_ext(pybind11::module& m);   // bindings_ext.cpp
 void register_graph(pybind11::module& m); // bindings_graph.cpp
 void register_deform(pybind11::module& m); // bindings_deform.cpp
@@ -601,6 +637,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_train_pool", &bn_fwd_train_pool);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd_given", &bn_bwd_given);
   m.def("attn_fwd_relbias", &attn_fwd_relbias);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -9,6 +9,9 @@
 extern "C" {
 int ct_conv_igemm(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
                   int, int, int, int, const int*, int, float*, int, hipStream_t);
+int ct_conv_igemm_bn(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
+                     int, int, int, int, const int*, int, int, const void*, const float*, float*, long, int,
+                     hipStream_t);
 int ct_conv_igemm_rows(int, int, int, int);
 int ct_conv_igemm_tile_m(int);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
@@ -54,6 +57,47 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
                                (int)geo[2], (int)geo[3], (int)geo[4], (int)geo[5], (int)geo[6], (int)geo[7],
                                (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), accumulate ? 1 : 0, pp,
                                (int)cfg, at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
+// Data gradient feeding a BatchNorm + ReLU backward (mask recomputed from the BatchNorm input
+// bnx): Y = the masked gradient, per-tile sums of dy' and dy' * xhat into part rows
+// [tile0, tile0 + tiles) and part rows [rows + tile0, ...) (rows = the buffer's tile capacity).
+// Returns false (nothing launched) on an unsupported configuration.
+bool conv_igemm_bn(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> geo, std::vector<int64_t> taps,
+                   bool accumulate, int64_t cfg, at::Tensor bnx, at::Tensor stat, at::Tensor part, int64_t tile0,
+                   int64_t rows) {
+  TORCH_CHECK(X.is_cuda() && W.is_cuda() && Y.is_cuda() && bnx.is_cuda(), "conv_igemm_bn: GPU tensors");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 &&
+              Y.scalar_type() == at::kBFloat16 && bnx.scalar_type() == at::kBFloat16, "conv_igemm_bn: bf16 tensors");
+  TORCH_CHECK(X.dim() == 4 && X.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm_bn: X must be NHWC-dense");
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "conv_igemm_bn: W must be [Co, T*Ci] row-major");
+  TORCH_CHECK(geo.size() == 12 && taps.size() % 2 == 0, "conv_igemm_bn: plan");
+  // the BatchNorm input must share Y's memory layout exactly (same shape, both NHWC-dense)
+  TORCH_CHECK(Y.dim() == 4 && Y.is_contiguous(at::MemoryFormat::ChannelsLast) && bnx.sizes() == Y.sizes() &&
+              bnx.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm_bn: bnx / Y layout");
+  const int Ci = (int)X.size(1), Hi = (int)X.size(2), Wi = (int)X.size(3);
+  const int T = (int)taps.size() / 2, Co = (int)W.size(0);
+  TORCH_CHECK(Ci % 64 == 0 && W.size(1) == (int64_t)T * Ci, "conv_igemm_bn: W columns != taps * Ci");
+  TORCH_CHECK(Y.size(1) == Co && geo[10] == Co, "conv_igemm_bn: Y channels");
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.is_contiguous() && stat.numel() == 4L * Co,
+              "conv_igemm_bn: stat must be float[4 Co]");
+  const long M = geo[11];
+  const long Nb = X.size(0);
+  TORCH_CHECK(M > 0 && M <= Nb * geo[0] * geo[1], "conv_igemm_bn: rows exceed the row grid");
+  const long last_y = (geo[0] - 1) * geo[6] + geo[8], last_x = (geo[1] - 1) * geo[7] + geo[9];
+  TORCH_CHECK(geo[8] >= 0 && geo[9] >= 0 && last_y < geo[4] && last_x < geo[5], "conv_igemm_bn: output grid");
+  TORCH_CHECK((((Nb - 1) * geo[4] + last_y) * geo[5] + last_x) * geo[10] + Co <= Y.numel(), "conv_igemm_bn: Y too small");
+  const int bm = ct_conv_igemm_tile_m(ct_conv_igemm_rows((int)cfg, Co, (int)M, T * (Ci / 64)));
+  const long tiles = (M + bm - 1) / bm;
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && tile0 >= 0 &&
+              tile0 + tiles <= rows && part.numel() >= 2 * rows * Co, "conv_igemm_bn: part buffer");
+  std::vector<int> tp(taps.begin(), taps.end());
+  const int rc = ct_conv_igemm_bn(X.data_ptr(), Hi, Wi, Ci, W.data_ptr(), Y.data_ptr(), (int)geo[0], (int)geo[1],
+                                  (int)geo[2], (int)geo[3], (int)geo[4], (int)geo[5], (int)geo[6], (int)geo[7],
+                                  (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), accumulate ? 1 : 0,
+                                  (int)cfg, bnx.data_ptr(), stat.data_ptr<float>(), part.data_ptr<float>(), rows * Co,
+                                  (int)tile0, at::hip::getCurrentHIPStream().stream());
   return rc == 0;
 }
 
@@ -112,6 +156,7 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient: fp32 split-K partials");
   m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
   m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
+  m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
   m.def("conv_igemm_tile_m", &conv_igemm_tile_m, "rows per tile of the chosen conv configuration");
   m.def("bn_partials_finalize", &bn_partials_finalize, "Chan merge of per-tile (mean, M2) -> mean, var");
 }

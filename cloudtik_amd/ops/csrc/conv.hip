@@ -53,6 +53,12 @@ struct ConvArgs {
   unsigned long long tdy, tdx;           // 16 taps x 4 bits, biased by 8
   int cpt;              // K-steps (of 64 weight columns) per tap: Ci / 64, or 1 in pixel-chunk mode
   int pixchunk;         // stem mode: Ci = 8, the 8 chunks of a K-step are 8 consecutive pixels
+  // EPI 2 (data gradient feeding a BatchNorm + ReLU backward, mask recomputed from x):
+  const bf16_t* bnx;    // the BatchNorm's input, at the same addresses as Y
+  const float* bnstat;  // its forward float[4 Co]: mean, invstd, a, b (y = relu(a x + b))
+  float* bnp;           // per-tile sums of dy' and dy' * xhat: rows [bntile0 + tm][Co], the
+  long bnp2;            //   second set bnp2 floats further
+  int bntile0;
 };
 
 __device__ __forceinline__ int cv_swz(int r) { return (r >> 1) & 7; }
@@ -304,19 +310,75 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   // coalesced copy-out: row-major 16-B chunks, BN / 8 lanes per row
   constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;
   const int cc = tid % CPR;
+  // EPI 2: the BatchNorm backward's reduction pass rides on the copy-out.  This thread's 8
+  // channels are fixed over its rows: it masks dy with the ReLU mask recomputed from the
+  // BatchNorm input (what bn_bwd_reduce_kernel mode 2 does), stores the masked dy' and sums
+  // dy' and dy' * xhat -- the separate pass re-reading dy and x goes away.
+  float bmu[8], bis[8], bfa[8], bfb[8], s1[8], s2[8];
+  if constexpr (EPI == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = n0 + cc * 8 + e;
+      bmu[e] = a.bnstat[c];
+      bis[e] = a.bnstat[a.Co + c];
+      bfa[e] = a.bnstat[2 * a.Co + c];
+      bfb[e] = a.bnstat[3 * a.Co + c];
+      s1[e] = 0.f;
+      s2[e] = 0.f;
+    }
+  }
 #pragma unroll 4
   for (int row = tid / CPR; row < BM; row += RPP) {
     const int m = m0 + row;
     if (m >= a.M) break;
     const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
-    bf16_t* yp = a.Y + ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+    const long yo = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+    bf16_t* yp = a.Y + yo;
     u16x8 v = *(const u16x8*)(ot + row * OROW + cc * 16);
     if (a.accumulate) {
       const u16x8 old = *(const u16x8*)yp;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(old[e]));
     }
+    if constexpr (EPI == 2) {
+      const u16x8 xv = *(const u16x8*)(a.bnx + yo);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xf = bf2f(xv[e]);
+        const bool on = bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
+        if (!on) v[e] = 0;
+        const float d = bf2f(v[e]);
+        s1[e] += d;
+        s2[e] += d * (xf - bmu[e]) * bis[e];
+      }
+    }
     *(u16x8*)yp = v;
+  }
+  if constexpr (EPI == 2) {
+    // column sums over the tile: [RPP][BN] per set in the (now free) LDS, then one thread per
+    // column adds the RPP row slots
+    static_assert(2 * RPP * BN * 4 <= NS * STAGE, "EPI 2 reduction LDS");
+    float* r1 = (float*)lds;
+    float* r2 = r1 + RPP * BN;
+    __syncthreads();                               // every lane is done reading ot
+    const int slot = tid / CPR;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      r1[slot * BN + cc * 8 + e] = s1[e];
+      r2[slot * BN + cc * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 64 * NW) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll 8
+      for (int q = 0; q < RPP; ++q) {
+        t1 += r1[q * BN + c];
+        t2 += r2[q * BN + c];
+      }
+      float* p = a.bnp + (long)(a.bntile0 + tm) * a.Co + n0 + c;
+      p[0] = t1;
+      p[a.bnp2] = t2;
+    }
   }
 }
 
@@ -509,13 +571,16 @@ __global__ void bn_partials_finalize_kernel(const float* __restrict__ part, int 
   var_out[c] = (float)(m2 / n);
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS, int MINB>
+template <int BM, int BN, int WGM, int WGN, int NS, int MINB, bool WITH_BN = false>
 static int cv_launch(const ConvArgs& a, int epi, hipStream_t s) {
   const long tiles = (long)ceil_div(a.M, BM) * (a.Co / BN);
   if (tiles > (1L << 30)) return 5;
   if (epi == 1)
     conv_igemm_kernel<BM, BN, WGM, WGN, NS, MINB, 1><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(a);
-  else
+  else if (epi == 2) {
+    if constexpr (WITH_BN) conv_igemm_kernel<BM, BN, WGM, WGN, NS, MINB, 2><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(a);
+    else return 6;
+  } else
     conv_igemm_kernel<BM, BN, WGM, WGN, NS, MINB, 0><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
@@ -546,23 +611,74 @@ extern "C" int ct_conv_igemm_tile_m(int cfg) {
 
 // Y = implicit-GEMM conv (see the file comment).  `taps` = T (dy, dx) pairs in [-8, 7].
 // Returns nonzero (launching nothing) on an unsupported shape.
+// EPI 2 arguments of ct_conv_igemm_bn (NULL bnx: a plain launch)
+struct ConvBnBwd {
+  const void* bnx;
+  const float* bnstat;
+  float* bnp;
+  long bnp2;
+  int tile0;
+};
+
+static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
+                           int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M, int T,
+                           const int* taps, int accumulate, float* part, int cfg, const ConvBnBwd* bn,
+                           hipStream_t stream);
+
 extern "C" int ct_conv_igemm(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
                              int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M,
                              int T, const int* taps, int accumulate, float* part, int cfg, hipStream_t stream) {
+  return conv_igemm_impl(X, Hi, Wi, Ci, W, Y, Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, taps,
+                         accumulate, part, cfg, nullptr, stream);
+}
+
+// data gradient whose output feeds a BatchNorm + ReLU backward (mask from x): Y = masked dy,
+// per-tile sums of dy' and dy' * xhat into bnp rows [tile0, tile0 + tiles) (and bnp + bnp2)
+extern "C" int ct_conv_igemm_bn(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
+                                int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M,
+                                int T, const int* taps, int accumulate, int cfg, const void* bnx, const float* bnstat,
+                                float* bnp, long bnp2, int tile0, hipStream_t stream) {
+  if (!bnx || !bnstat || !bnp || ((uintptr_t)bnx & 15) || ((uintptr_t)Y & 15) || ldy % 8) return 8;
+  const ConvBnBwd bn{bnx, bnstat, bnp, bnp2, tile0};
+  return conv_igemm_impl(X, Hi, Wi, Ci, W, Y, Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, taps,
+                         accumulate, nullptr, cfg, &bn, stream);
+}
+
+static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
+                           int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M, int T,
+                           const int* taps, int accumulate, float* part, int cfg, const ConvBnBwd* bn,
+                           hipStream_t stream) {
   if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT) return 1;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 7) || ldy % 4) return 3;
   const int pixchunk = Ci == 8;            // the stem: NHWC8 input, 8 pixels per K-step
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
-             Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk};
+             Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk,
+             nullptr, nullptr, nullptr, 0, 0};
+  if (bn) {
+    a.bnx = (const bf16_t*)bn->bnx;
+    a.bnstat = bn->bnstat;
+    a.bnp = bn->bnp;
+    a.bnp2 = bn->bnp2;
+    a.bntile0 = bn->tile0;
+  }
   for (int t = 0; t < T; ++t) {
     const int dy = taps[2 * t], dx = taps[2 * t + 1];
     if (dy < -8 || dy > 7 || dx < -8 || dx > 7) return 4;
     a.tdy |= (unsigned long long)(dy + 8) << (4 * t);
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
-  const int epi = part ? 1 : 0;
+  const int epi = bn ? 2 : (part ? 1 : 0);
   cfg = ct_conv_igemm_rows(cfg, Co, M, T * a.cpt);
   if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9) && Co % 128) return 2;
+  if (epi == 2) {
+    // the default (shape-picked) configurations only: the others are not instantiated with EPI 2
+    switch (cfg) {
+      case 5: return cv_launch<128, 128, 2, 2, 2, 2, true>(a, epi, stream);
+      case 8: return cv_launch<128, 64, 2, 2, 2, 3, true>(a, epi, stream);
+      case 9: return cv_launch<64, 128, 1, 4, 2, 3, true>(a, epi, stream);
+      default: return 6;
+    }
+  }
   switch (cfg) {
     case 0: return cv_launch<256, 64, 4, 1, 3, 1>(a, epi, stream);
     case 1: return cv_launch<256, 128, 4, 2, 3, 1>(a, epi, stream);

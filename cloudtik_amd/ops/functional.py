@@ -204,6 +204,12 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, y if mode == 1 else None, gamma, stat)
         ctx.params = (gamma, beta)
         ctx.cfg = (mode, has_res)
+        ctx.bn_link = None
+        if mode == 2 and x.dim() == 4:
+            # a conv consuming y may run our backward reduction in its dgrad epilogue (ops/conv.py)
+            from cloudtik_amd.ops.conv import BnBwdLink
+            ctx.bn_link = BnBwdLink(x, stat)
+            y._ct_bn_bwd = ctx.bn_link
         return y
 
     @staticmethod
@@ -213,6 +219,19 @@ class _BNActFn(torch.autograd.Function):
         wp, bp = ctx.params
         flat = all(p is not None and p.grad is not None and getattr(p, "_ct_flat_grad", False)
                    and p.grad.is_contiguous() and p.grad.dtype == gamma.dtype for p in (wp, bp))
+        given = ctx.bn_link.take(dy) if ctx.bn_link is not None else None
+        if given is not None and dy.is_contiguous(memory_format=torch.channels_last):
+            # dy arrives ReLU-masked with its reduction done by the conv's dgrad epilogue
+            part, tiles, rows = given
+            if flat:
+                dx, _, _ = _C().bn_bwd_given(dy, x, gamma, stat, part, tiles, rows, wp.grad, bp.grad)
+                for p in (wp, bp):
+                    cb = getattr(p, "_ct_grad_ready", None)
+                    if cb is not None:
+                        cb(p)
+                return dx, None, None, None, None, None, None, None, None
+            dx, dg, db = _C().bn_bwd_given(dy, x, gamma, stat, part, tiles, rows, None, None)
+            return dx, dg, db, None, None, None, None, None, None
         if flat:
             # accumulate straight into the flat gradient buffer (no AccumulateGrad kernels)
             dx, dres, _, _ = _C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, wp.grad, bp.grad)

@@ -27,7 +27,8 @@ def main():
     rows = []
     with open(a.csv) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            sid = r.get("Stream_Id") or r.get("Queue_Id") or "0"
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], sid))
     rows.sort()
     marks = [i for i, r in enumerate(rows) if a.delim in r[2]]
     # the optimizer may be split over several launches per step: keep the first of each run
@@ -38,15 +39,33 @@ def main():
     win = rows[lo:hi]
     tot = defaultdict(float)
     cnt = defaultdict(int)
-    for s, e, n in win:
+    per_stream = defaultdict(float)
+    for s, e, n, sid in win:
+        per_stream[sid] += (e - s) / 1e3
         tot[n] += (e - s) / 1e3
         cnt[n] += 1
+    # wall time with at least one kernel running (union of the kernel intervals)
+    cover, cur_s, cur_e = 0.0, None, None
+    for s, e, _n, _sid in sorted(win):
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                cover += (cur_e - cur_s) / 1e3
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        cover += (cur_e - cur_s) / 1e3
     busy = sum(tot.values()) / a.steps
     span = (rows[starts[-1]][1] - rows[starts[-a.steps - 1]][1]) / 1e3 / a.steps
     print(f"## {a.title or a.csv}\n")
     print(f"Steady state over the last {a.steps} steps (cut at `{a.delim}`): GPU-busy {busy / 1e3:.2f} ms "
           f"per step, step span {span / 1e3:.2f} ms ({100 * busy / span:.0f}% busy), "
           f"{len(win) / a.steps:.0f} kernels per step.\n")
+    if len(per_stream) > 1:
+        parts = ", ".join(f"stream {k}: {v / a.steps / 1e3:.2f} ms" for k, v in
+                          sorted(per_stream.items(), key=lambda kv: -kv[1]))
+        print(f"Per stream kernel time per step: {parts}; wall time with >= 1 kernel running "
+              f"{cover / a.steps / 1e3:.2f} ms per step.\n")
     print("| kernel | ms/step | calls/step | % busy |\n|---|---:|---:|---:|")
     for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
         short = n if len(n) <= 100 else n[:97] + "..."

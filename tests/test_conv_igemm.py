@@ -152,6 +152,46 @@ def test_bottleneck_matches_miopen_path(cuda, down, stride, monkeypatch):
         assert _rel(a, b) < 3e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("down,stride", [(True, 2), (False, 1)])
+def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, monkeypatch):
+    """conv.hip EPI 2: the BatchNorm + ReLU backward reduction done in the consuming conv's
+    data-gradient epilogue (bn1 -> conv2 incl. the stride-2 phase plan, bn2 -> conv3) gives the
+    gradients of the separate reduction pass, and actually runs."""
+    from cloudtik_amd import ops
+    from cloudtik_amd.models.resnet import Bottleneck
+    torch.manual_seed(1)
+    cin = 64 if down else 256
+    blk = Bottleneck(cin, 64, stride, downsample=down, device=cuda, dtype=torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    x0 = _nhwc(torch.randn(4, cin, 20, 20, device=cuda).to(torch.bfloat16))
+    C = ops.require_native()
+    calls = {"n": 0}
+    orig = C.bn_bwd_given
+
+    def counted(*a):
+        calls["n"] += 1
+        return orig(*a)
+
+    monkeypatch.setattr(C, "bn_bwd_given", counted)
+
+    def run(fuse):
+        monkeypatch.setattr(CV, "BN_BWD_FUSE", fuse)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+        return x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
+
+    gx1, gp1 = run(True)
+    assert calls["n"] == 2                       # bn1 and bn2
+    gx0, gp0 = run(False)
+    assert calls["n"] == 2
+    assert _rel(gx1, gx0) < 1e-2
+    for a, b in zip(gp1, gp0):
+        assert _rel(a, b) < 1e-2
+
+
 def test_stem_pixel_chunk_plan_matches_conv2d():
     """Stem mode: NHWC8 input, one K-step per filter row = 8 consecutive pixels x 8 channels."""
     torch.manual_seed(3)
