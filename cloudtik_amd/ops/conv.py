@@ -209,11 +209,12 @@ class BnBwdLink:
     identity and version are recorded so a gradient that autograd summed with another consumer's
     (or modified) is never paired with stale partials."""
 
-    __slots__ = ("x", "stat", "pending")
+    __slots__ = ("x", "stat", "mode", "pending")
 
-    def __init__(self, x: torch.Tensor, stat: torch.Tensor):
+    def __init__(self, x: torch.Tensor, stat: torch.Tensor, mode: int):
         self.x = x
         self.stat = stat
+        self.mode = mode            # 2: mask recomputed from x; 1: mask read from the BN output
         self.pending = None
 
     def take(self, dy: torch.Tensor):
@@ -225,18 +226,21 @@ class BnBwdLink:
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), padding=(0, 0),
-               out: Optional[torch.Tensor] = None, accumulate: bool = False, bn: Optional[BnBwdLink] = None):
+               out: Optional[torch.Tensor] = None, accumulate: bool = False, bn: Optional[BnBwdLink] = None,
+               bn_y: Optional[torch.Tensor] = None):
     """dX of conv2d(x, w) for the NHWC bf16 gradient dy; ``accumulate`` adds into ``out``.
 
-    ``bn``: x is the output of that BatchNorm + ReLU; dX is returned ReLU-masked and the
-    BatchNorm-backward partial sums are left in ``bn.pending`` (see BnBwdLink)."""
+    ``bn``: x is the output of that BatchNorm + ReLU; dX (after the accumulate) is returned
+    ReLU-masked and the BatchNorm-backward partial sums are left in ``bn.pending`` (see
+    BnBwdLink).  ``bn_y`` = x itself, the mask source of a BatchNorm with a residual add."""
     N, ci, H, W = x_shape
     co, _, R, S = w.shape
     phases = dgrad_phases(x_shape, w.shape, tuple(stride), tuple(padding))
     empty_phase = any(not rs for _, _, _, rs in phases)
     C = _C()
     bn_plan = None
-    if bn is not None and not accumulate and bn.x.shape == tuple(x_shape) and co % 64 == 0:
+    if bn is not None and (bn.mode == 2 or bn_y is not None) and not (accumulate and empty_phase) \
+            and bn.x.shape == tuple(x_shape) and co % 64 == 0:
         tiles = []
         for _, (Hr, Wr), taps, rs in phases:
             if rs:
@@ -266,7 +270,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
         geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
         if bn_plan is not None:
             part, rows = bn_plan
-            if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, bn.stat, part, tile0, rows):
+            if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, bn_y if bn.mode == 1 else None,
+                               bn.stat, part, tile0, rows):
                 bm = C.conv_igemm_tile_m(_CFG, ci, geo[11], len(taps) // 2 * (co // 64))
                 tile0 += (geo[11] + bm - 1) // bm
                 continue
@@ -362,7 +367,7 @@ class ConvFn(torch.autograd.Function):
         ctx.stride, ctx.padding = stride, padding
         ctx.wp = w
         # x = the output of a BatchNorm + ReLU: its backward reduction runs in our dgrad epilogue
-        ctx.bn_link = getattr(x, "_ct_bn_bwd", None) if (BN_BWD_FUSE and not keep_input) else None
+        ctx.bn_link = getattr(x, "_ct_bn_bwd", None) if BN_BWD_FUSE else None
         if bn_stats:
             # the epilogue reduces the BatchNorm statistics of y per tile; the BatchNorm that
             # consumes y picks them up instead of re-reading y for a statistics pass
@@ -380,10 +385,12 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if (dx_other is not None and not torch.is_grad_enabled() and dx_other.dtype == dy.dtype
                     and dx_other.is_contiguous(memory_format=torch.channels_last)):
-                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding, out=dx_other, accumulate=True)
+                # (a BatchNorm with a residual add: x is its output, the ReLU mask source)
+                dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding, out=dx_other, accumulate=True,
+                                bn=ctx.bn_link, bn_y=x)
             else:
                 dx = conv_dgrad(dy, w, x.shape, ctx.stride, ctx.padding,
-                                bn=ctx.bn_link if dx_other is None else None)
+                                bn=ctx.bn_link if dx_other is None else None, bn_y=x)
                 if dx_other is not None:
                     dx = dx + dx_other
         if ctx.needs_input_grad[1]:

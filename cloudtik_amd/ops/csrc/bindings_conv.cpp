@@ -10,8 +10,8 @@ extern "C" {
 int ct_conv_igemm(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
                   int, int, int, int, const int*, int, float*, int, hipStream_t);
 int ct_conv_igemm_bn(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
-                     int, int, int, int, const int*, int, int, const void*, const float*, float*, long, int,
-                     hipStream_t);
+                     int, int, int, int, const int*, int, int, const void*, const void*, const float*, float*, long,
+                     int, hipStream_t);
 int ct_conv_igemm_rows(int, int, int, int);
 int ct_conv_igemm_tile_m(int);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
@@ -60,13 +60,14 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
   return rc == 0;
 }
 
-// Data gradient feeding a BatchNorm + ReLU backward (mask recomputed from the BatchNorm input
-// bnx): Y = the masked gradient, per-tile sums of dy' and dy' * xhat into part rows
-// [tile0, tile0 + tiles) and part rows [rows + tile0, ...) (rows = the buffer's tile capacity).
+// Data gradient feeding a BatchNorm + ReLU backward (ReLU mask read from its output bny, or
+// recomputed from its input bnx): Y = the masked gradient (after the accumulate), per-tile sums
+// of dy' and dy' * xhat into part rows [tile0, tile0 + tiles) and [rows + tile0, ...) (rows =
+// the buffer's tile capacity).
 // Returns false (nothing launched) on an unsupported configuration.
 bool conv_igemm_bn(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> geo, std::vector<int64_t> taps,
-                   bool accumulate, int64_t cfg, at::Tensor bnx, at::Tensor stat, at::Tensor part, int64_t tile0,
-                   int64_t rows) {
+                   bool accumulate, int64_t cfg, at::Tensor bnx, c10::optional<at::Tensor> bny, at::Tensor stat,
+                   at::Tensor part, int64_t tile0, int64_t rows) {
   TORCH_CHECK(X.is_cuda() && W.is_cuda() && Y.is_cuda() && bnx.is_cuda(), "conv_igemm_bn: GPU tensors");
   TORCH_CHECK(X.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 &&
               Y.scalar_type() == at::kBFloat16 && bnx.scalar_type() == at::kBFloat16, "conv_igemm_bn: bf16 tensors");
@@ -76,6 +77,10 @@ bool conv_igemm_bn(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t
   // the BatchNorm input must share Y's memory layout exactly (same shape, both NHWC-dense)
   TORCH_CHECK(Y.dim() == 4 && Y.is_contiguous(at::MemoryFormat::ChannelsLast) && bnx.sizes() == Y.sizes() &&
               bnx.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm_bn: bnx / Y layout");
+  const bool has_y = bny.has_value() && bny->defined();
+  if (has_y)
+    TORCH_CHECK(bny->is_cuda() && bny->scalar_type() == at::kBFloat16 && bny->sizes() == Y.sizes() &&
+                bny->is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm_bn: bny / Y layout");
   const int Ci = (int)X.size(1), Hi = (int)X.size(2), Wi = (int)X.size(3);
   const int T = (int)taps.size() / 2, Co = (int)W.size(0);
   TORCH_CHECK(Ci % 64 == 0 && W.size(1) == (int64_t)T * Ci, "conv_igemm_bn: W columns != taps * Ci");
@@ -96,7 +101,7 @@ bool conv_igemm_bn(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t
   const int rc = ct_conv_igemm_bn(X.data_ptr(), Hi, Wi, Ci, W.data_ptr(), Y.data_ptr(), (int)geo[0], (int)geo[1],
                                   (int)geo[2], (int)geo[3], (int)geo[4], (int)geo[5], (int)geo[6], (int)geo[7],
                                   (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), accumulate ? 1 : 0,
-                                  (int)cfg, bnx.data_ptr(), stat.data_ptr<float>(), part.data_ptr<float>(), rows * Co,
+                                  (int)cfg, bnx.data_ptr(), has_y ? bny->data_ptr() : nullptr, stat.data_ptr<float>(), part.data_ptr<float>(), rows * Co,
                                   (int)tile0, at::hip::getCurrentHIPStream().stream());
   return rc == 0;
 }

@@ -55,6 +55,8 @@ struct ConvArgs {
   int pixchunk;         // stem mode: Ci = 8, the 8 chunks of a K-step are 8 consecutive pixels
   // EPI 2 (data gradient feeding a BatchNorm + ReLU backward, mask recomputed from x):
   const bf16_t* bnx;    // the BatchNorm's input, at the same addresses as Y
+  const bf16_t* bny;    // its output (ReLU mask source when it had a residual add), or null:
+                        //   mask recomputed from x
   const float* bnstat;  // its forward float[4 Co]: mean, invstd, a, b (y = relu(a x + b))
   float* bnp;           // per-tile sums of dy' and dy' * xhat: rows [bntile0 + tm][Co], the
   long bnp2;            //   second set bnp2 floats further
@@ -342,10 +344,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
     }
     if constexpr (EPI == 2) {
       const u16x8 xv = *(const u16x8*)(a.bnx + yo);
+      const u16x8 yv = a.bny ? *(const u16x8*)(a.bny + yo) : u16x8(0);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xf = bf2f(xv[e]);
-        const bool on = bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
+        const bool on = a.bny ? bf2f(yv[e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
         if (!on) v[e] = 0;
         const float d = bf2f(v[e]);
         s1[e] += d;
@@ -614,6 +617,7 @@ extern "C" int ct_conv_igemm_tile_m(int cfg) {
 // EPI 2 arguments of ct_conv_igemm_bn (NULL bnx: a plain launch)
 struct ConvBnBwd {
   const void* bnx;
+  const void* bny;
   const float* bnstat;
   float* bnp;
   long bnp2;
@@ -636,10 +640,11 @@ extern "C" int ct_conv_igemm(const void* X, int Hi, int Wi, int Ci, const void* 
 // per-tile sums of dy' and dy' * xhat into bnp rows [tile0, tile0 + tiles) (and bnp + bnp2)
 extern "C" int ct_conv_igemm_bn(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
                                 int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M,
-                                int T, const int* taps, int accumulate, int cfg, const void* bnx, const float* bnstat,
-                                float* bnp, long bnp2, int tile0, hipStream_t stream) {
-  if (!bnx || !bnstat || !bnp || ((uintptr_t)bnx & 15) || ((uintptr_t)Y & 15) || ldy % 8) return 8;
-  const ConvBnBwd bn{bnx, bnstat, bnp, bnp2, tile0};
+                                int T, const int* taps, int accumulate, int cfg, const void* bnx, const void* bny,
+                                const float* bnstat, float* bnp, long bnp2, int tile0, hipStream_t stream) {
+  if (!bnx || !bnstat || !bnp || ((uintptr_t)bnx & 15) || ((uintptr_t)bny & 15) || ((uintptr_t)Y & 15) || ldy % 8)
+    return 8;
+  const ConvBnBwd bn{bnx, bny, bnstat, bnp, bnp2, tile0};
   return conv_igemm_impl(X, Hi, Wi, Ci, W, Y, Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, taps,
                          accumulate, nullptr, cfg, &bn, stream);
 }
@@ -653,9 +658,10 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   const int pixchunk = Ci == 8;            // the stem: NHWC8 input, 8 pixels per K-step
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
              Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk,
-             nullptr, nullptr, nullptr, 0, 0};
+             nullptr, nullptr, nullptr, nullptr, 0, 0};
   if (bn) {
     a.bnx = (const bf16_t*)bn->bnx;
+    a.bny = (const bf16_t*)bn->bny;
     a.bnstat = bn->bnstat;
     a.bnp = bn->bnp;
     a.bnp2 = bn->bnp2;

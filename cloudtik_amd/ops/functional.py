@@ -205,10 +205,10 @@ class _BNActFn(torch.autograd.Function):
         ctx.params = (gamma, beta)
         ctx.cfg = (mode, has_res)
         ctx.bn_link = None
-        if mode == 2 and x.dim() == 4:
+        if mode != 0 and x.dim() == 4:
             # a conv consuming y may run our backward reduction in its dgrad epilogue (ops/conv.py)
             from cloudtik_amd.ops.conv import BnBwdLink
-            ctx.bn_link = BnBwdLink(x, stat)
+            ctx.bn_link = BnBwdLink(x, stat, mode)
             y._ct_bn_bwd = ctx.bn_link
         return y
 
@@ -229,9 +229,10 @@ class _BNActFn(torch.autograd.Function):
                     cb = getattr(p, "_ct_grad_ready", None)
                     if cb is not None:
                         cb(p)
-                return dx, None, None, None, None, None, None, None, None
+                # with a residual add the masked dy IS the residual branch's gradient
+                return dx, None, None, (dy if has_res else None), None, None, None, None, None
             dx, dg, db = _C().bn_bwd_given(dy, x, gamma, stat, part, tiles, rows, None, None)
-            return dx, dg, db, None, None, None, None, None, None
+            return dx, dg, db, (dy if has_res else None), None, None, None, None, None
         if flat:
             # accumulate straight into the flat gradient buffer (no AccumulateGrad kernels)
             dx, dres, _, _ = _C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, wp.grad, bp.grad)

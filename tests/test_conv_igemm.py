@@ -156,14 +156,17 @@ def test_bottleneck_matches_miopen_path(cuda, down, stride, monkeypatch):
 @pytest.mark.parametrize("down,stride", [(True, 2), (False, 1)])
 def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, monkeypatch):
     """conv.hip EPI 2: the BatchNorm + ReLU backward reduction done in the consuming conv's
-    data-gradient epilogue (bn1 -> conv2 incl. the stride-2 phase plan, bn2 -> conv3) gives the
-    gradients of the separate reduction pass, and actually runs."""
+    data-gradient epilogue gives the gradients of the separate reduction pass, and actually runs:
+    bn1 -> conv2 (incl. the stride-2 phase plan) and bn2 -> conv3 (mask recomputed from x), and
+    block 1's bn3 (residual add, mask read from y) -> block 2's conv1, whose data gradient
+    accumulates into the residual gradient."""
     from cloudtik_amd import ops
     from cloudtik_amd.models.resnet import Bottleneck
     torch.manual_seed(1)
     cin = 64 if down else 256
-    blk = Bottleneck(cin, 64, stride, downsample=down, device=cuda, dtype=torch.bfloat16).to(
-        memory_format=torch.channels_last)
+    kw = dict(device=cuda, dtype=torch.bfloat16)
+    blk = torch.nn.Sequential(Bottleneck(cin, 64, stride, downsample=down, **kw),
+                              Bottleneck(256, 64, 1, downsample=False, **kw)).to(memory_format=torch.channels_last)
     x0 = _nhwc(torch.randn(4, cin, 20, 20, device=cuda).to(torch.bfloat16))
     C = ops.require_native()
     calls = {"n": 0}
@@ -184,9 +187,9 @@ def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, monkeypatch
         return x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
 
     gx1, gp1 = run(True)
-    assert calls["n"] == 2                       # bn1 and bn2
+    assert calls["n"] == 5                       # bn1, bn2 of both blocks, bn3 of the first
     gx0, gp0 = run(False)
-    assert calls["n"] == 2
+    assert calls["n"] == 5
     assert _rel(gx1, gx0) < 1e-2
     for a, b in zip(gp1, gp0):
         assert _rel(a, b) < 1e-2
