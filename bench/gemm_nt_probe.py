@@ -61,8 +61,11 @@ def main():
     dz = torch.empty(T, F, device="cuda", dtype=bf)
     t_fus = timeit(lambda: C.gemm_nt(df, W2t, dz, 2, False, None, aux, db))
     t_tr = timeit(lambda: W2.t().contiguous())
+    t_nn = timeit(lambda: C.gemm_nn(df, W2, dz, 2, False, b1, z, db))
+    t_nn0 = timeit(lambda: C.gemm_nn(df, W2, dz, 0, False, None, None, None))
     print(json.dumps({"case": "ffn_dgrad_dgelu_bgrad", "unfused_us": round(t_unf, 1), "fused_us": round(t_fus, 1),
-                      "w2_transpose_us": round(t_tr, 1)}), flush=True)
+                      "w2_transpose_us": round(t_tr, 1), "nn_fused_us": round(t_nn, 1),
+                      "nn_plain_us": round(t_nn0, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -18,8 +18,9 @@ MI355X-first structure of one encoder layer (bf16 activations/weights, fp32 stat
 
 so every bias gradient is folded into a LayerNorm / bias-GELU backward kernel and there is
 no permute/contiguous copy anywhere in the layer.  The vocabulary is padded to a multiple
-of 64 rows (aligned 16-byte vector access in the fused cross-entropy kernel); padded rows
-never receive tokens and are masked out of the softmax.
+of 256 rows (aligned 16-byte vector access in the fused cross-entropy kernel, and whole
+256-row tiles for the decoder's weight-gradient GEMM); padded rows never receive tokens and
+are masked out of the softmax.
 """
 from __future__ import annotations
 
@@ -46,7 +47,7 @@ class BertConfig:
     type_vocab_size: int = 2
     layer_norm_eps: float = 1e-12
     initializer_range: float = 0.02
-    pad_vocab_multiple: int = 64
+    pad_vocab_multiple: int = 256
     dense_seq_output: bool = True
 
     @property

@@ -42,7 +42,7 @@ constexpr int NT_ROWB = NT_BK * 2;        // 128 B per LDS image row
 constexpr int NT_HALF = 128 * NT_ROWB;    // 16 KiB: 128 rows of one operand
 constexpr int NT_BUF = 4 * NT_HALF;       // 64 KiB per K-tile buffer
 
-enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2, NT_EPI_F32_SLAB = 3 };
+enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2, NT_EPI_F32_SLAB = 3, NT_EPI_NONE = 4 };
 
 struct NtArgs {
   const bf16_t* A;
@@ -345,6 +345,17 @@ template <int EPI, bool BGRAD, int NJ>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[8][NJ], long mrow, long ncol,
                                             int lane, int split) {
   static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
+  if constexpr (EPI == NT_EPI_NONE) {
+    // timing diagnostic (CLOUDTIK_AMD_GEMM_DIAG=4): the K loop without the epilogue's memory
+    // traffic; the never-taken store keeps the accumulators live
+    f32x4 t = acc[0][0];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) t += acc[i][j];
+    if (a.accumulate == 0x5EED) *(f32x4*)(a.P ? a.P : (float*)a.D) = t;
+    return;
+  }
   if constexpr (EPI == NT_EPI_F32_SLAB) {
     float* P = a.P + (long)split * a.M * a.N;
 #pragma unroll
@@ -531,6 +542,11 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias, nullptr,
            nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, accumulate};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
+  if (diag == 4) {
+    if (b_kn) gemm_nt_kernel<NT_EPI_NONE, false, 0, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+    else gemm_nt_kernel<NT_EPI_NONE, false, 0, 0><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+    return 0;
+  }
   if (diag && !b_kn) {
     if (diag == 1) gemm_nt_kernel<0, false, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
     else if (diag == 2) gemm_nt_kernel<0, false, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
@@ -571,6 +587,11 @@ extern "C" int ct_gemm_tn2(const void* A, long lda, const void* B, long ldb, voi
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, splits == 1 ? (bf16_t*)out : nullptr, nullptr, nullptr, nullptr,
            splits > 1 ? (float*)out : nullptr, biasg, lda, ldb, ldo, 0, K / splits, M, N, (int)(K / splits),
            accumulate};
+  static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
+  if (diag == 4) {
+    gemm_nt_kernel<NT_EPI_NONE, false, 0, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
+    return 0;
+  }
   if (biasg) {
     if (splits > 1) gemm_nt_kernel<NT_EPI_F32_SLAB, false, 0, 1, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
     else gemm_nt_kernel<NT_EPI_PLAIN, false, 0, 1, true><<<(int)blocks, NT_THREADS, 0, stream>>>(a);

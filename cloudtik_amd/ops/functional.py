@@ -165,7 +165,19 @@ class _LinearXentFn(torch.autograd.Function):
     def backward(ctx, g):
         x, W, dlogits = ctx.saved_tensors
         dx = torch.matmul(dlogits, W) * g.to(dlogits.dtype)
-        dW = torch.matmul(dlogits.t(), x) * g.to(dlogits.dtype)
+        dW = None
+        import importlib
+        _lin = importlib.import_module("cloudtik_amd.ops.linear")   # (ops.linear is also a function)
+        if (_lin._HIP_WGRAD and dlogits.dtype == torch.bfloat16 and W.shape[0] % 256 == 0
+                and x.shape[1] % 256 == 0 and x.shape[0] % 64 == 0):
+            # decoder weight gradient on the MFMA kernel's TN layout (the vocabulary is padded to
+            # a multiple of 256 for it): one split fills ~2 waves of the GPU, bf16 out directly
+            dW = torch.empty_like(W)
+            if not _C().gemm_tn2(dlogits, x.contiguous(), dW, 1, False):
+                dW = None
+        if dW is None:
+            dW = torch.matmul(dlogits.t(), x)
+        dW = dW * g.to(dlogits.dtype)
         db = dlogits.sum(0, dtype=torch.float32).mul_(g).to(dlogits.dtype) if ctx.has_b else None
         return dx, dW, db, None, None, None, None
 
