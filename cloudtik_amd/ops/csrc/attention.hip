@@ -33,6 +33,8 @@
 //     converted by a tiny kernel.
 //   * attention-prob dropout regenerated from a counter hash (nothing stored).
 #include "common.h"
+#include <cstdlib>
+#include <type_traits>
 
 namespace ct {
 
@@ -267,6 +269,203 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   }
 }
 
+
+// Pipelined persistent forward (no relative bias): a workgroup walks work items blockIdx.x,
+// + gridDim.x, ... (item = q-block + nqb * (batch * H + head)) and runs ONE flat loop over the
+// K/V tiles of all of them.  The K/V (+ key bias) of flat tile f + 2 are loaded into one of two
+// register staging sets at step f and written to LDS at the end of step f + 1, so every load
+// has two tile computations to land (the one-set kernel above gives it one).  Measured SLOWER
+// than the one-item kernel (75.5 vs 65.9 us on BERT-large shapes): the hardware dispatcher
+// already overlaps one workgroup's loads with another's MFMAs, and the persistent walk only
+// adds loop-carried state (199 VGPRs, 2 waves/SIMD).  Kept as an opt-in (CLOUDTIK_AMD_ATTN_FWD_PIPE=1)
+// for long sequences, where items have many tiles.  The next item's Q fragments
+// are loaded at the first tile of the current item.  The loop is unrolled by two so the
+// staging set is a compile-time choice (a runtime index would put the sets in scratch).
+template <bool DROP, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_kernel(AttnFwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + 2 * 64 * 4];
+  float* kbias_lds = reinterpret_cast<float*>(smem + 32768);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int nqb = (a.Sq + 127) / 128;
+  const int nitems = nqb * a.B * a.H;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= nitems) return;
+  const float LOG2E = 1.4426950408889634f;
+  const int srow = tid >> 3, sch = tid & 7;
+  const int nt = (a.Sk + 63) / 64;
+  const int my_items = (nitems - (int)blockIdx.x + G - 1) / G;
+  const int nflat = my_items * nt;
+  const int trow = (lane >> 2) & 3;
+  const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
+
+  u16x8 k0s[2], v0s[2], k1s[2], v1s[2];
+  float b0s = 0.f, b1s = 0.f;
+  auto gload = [&](int f, u16x8 (&K)[2], u16x8 (&V)[2], float& Bv) {
+    const int it = (int)blockIdx.x + (f / nt) * G, kt = f % nt;
+    const int bh = it / nqb, b = bh / a.H, h = bh % a.H;
+    const bf16_t* kp = a.k + b * a.k_sb + h * a.k_sh;
+    const bf16_t* vp = a.v + b * a.v_sb + h * a.v_sh;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = kt * 64 + srow + 32 * i;
+      const bool ok = key < a.Sk;
+      K[i] = ok ? *reinterpret_cast<const u16x8*>(kp + (key * (int)a.k_ss + sch * 8)) : u16x8(0);
+      V[i] = ok ? *reinterpret_cast<const u16x8*>(vp + (key * (int)a.v_ss + sch * 8)) : u16x8(0);
+    }
+    if (tid < 64) {
+      const int kk = kt * 64 + tid;
+      Bv = kk < a.Sk ? (a.kbias ? a.kbias[b * a.kb_sb + kk] * LOG2E : 0.f) : -INFINITY;
+    }
+  };
+  auto swrite = [&](int buf, const u16x8 (&K)[2], const u16x8 (&V)[2], float Bv) {
+    char* kb = smem + buf * 16384;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<u16x8*>(kb + swz(srow + 32 * i, sch)) = K[i];
+      *reinterpret_cast<u16x8*>(kb + 8192 + swz(srow + 32 * i, sch)) = V[i];
+    }
+    if (tid < 64) kbias_lds[buf * 64 + tid] = Bv;
+  };
+  auto qload = [&](int it, bf16x8_t (&Q)[4]) {
+    const int bh = it / nqb, b = bh / a.H, h = bh % a.H;
+    const int qi = (it % nqb) * 128 + w * 32 + r;
+    const bf16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (long)qi * a.q_ss;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) Q[s] = gload_frag(qp + 16 * s + 8 * hh, qi < a.Sq);
+  };
+
+  bf16x8_t qf[4], qn[4];
+  qload(blockIdx.x, qf);
+  gload(0, k0s, v0s, b0s);
+  if (nflat > 1) gload(1, k1s, v1s, b1s);
+  swrite(0, k0s, v0s, b0s);
+  __syncthreads();
+
+  f32x16 O0, O1;
+  float m = -INFINITY, l = 0.f;
+
+  // one flat step: compute tile f from LDS buffer P (f % 2 == P), K/V of tile f + 2 into
+  // staging set P, tile f + 1 (staging set 1 - P) into buffer 1 - P at the end
+  auto step = [&](int f, u16x8 (&Kp)[2], u16x8 (&Vp)[2], float& Bp, const u16x8 (&Kq)[2],
+                  const u16x8 (&Vq)[2], const float& Bq, int P) {
+    if (f + 2 < nflat) gload(f + 2, Kp, Vp, Bp);
+    const int fi = f / nt, kt = f - fi * nt;
+    const int item = (int)blockIdx.x + fi * G;
+    const int bh = item / nqb;
+    const int qi = (item % nqb) * 128 + w * 32 + r;
+    if (kt == 0) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { O0[i] = 0.f; O1[i] = 0.f; }
+      m = -INFINITY;
+      l = 0.f;
+      if (fi + 1 < my_items) qload(item + G, qn);
+    }
+    const char* Kb = smem + P * 16384;
+    const char* Vb = Kb + 8192;
+    f32x16 S0, S1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { S0[i] = 0.f; S1[i] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      S0 = mfma32(lds_b128(Kb + swz(r, 2 * s + hh)), qf[s], S0);
+      S1 = mfma32(lds_b128(Kb + swz(32 + r, 2 * s + hh)), qf[s], S1);
+    }
+    const float* kbt = kbias_lds + P * 64 + 4 * hh;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bb0 = *reinterpret_cast<const f32x4*>(kbt + 8 * g);
+      const f32x4 bb1 = *reinterpret_cast<const f32x4*>(kbt + 32 + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * g + j;
+        float x0 = fmaf(S0[i], a.scale_log2, bb0[j]);
+        float x1 = fmaf(S1[i], a.scale_log2, bb1[j]);
+        if (CAUSAL) {
+          const int key0 = kt * 64 + 8 * g + 4 * hh + j;
+          if (key0 > qi) x0 = -INFINITY;
+          if (key0 + 32 > qi) x1 = -INFINITY;
+        }
+        S0[i] = x0; S1[i] = x1;
+        mx = fmaxf(mx, fmaxf(x0, x1));
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float msub = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = __builtin_amdgcn_exp2f(m - msub);
+    m = m_new;
+    float ps = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      S0[i] = __builtin_amdgcn_exp2f(S0[i] - msub);
+      S1[i] = __builtin_amdgcn_exp2f(S1[i] - msub);
+      ps += S0[i] + S1[i];
+    }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { O0[i] *= alpha; O1[i] *= alpha; }
+    if (DROP) {   // the dropout stream of the one-item kernel above, element for element
+      const uint32_t rb2 = (uint32_t)((((uint64_t)bh * a.Sq + qi) * (uint64_t)a.Sk) >> 1);
+      const uint32_t pbase = rb2 + (uint32_t)(kt * 32 + 2 * hh);
+      const uint32_t thi = a.thr16 << 16;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const uint32_t pair = pbase + (uint32_t)(t * 16 + 4 * (i >> 2) + ((i & 3) >> 1));
+          const uint32_t rr = hash_u32(pair ^ a.hash_base);
+          const bool k0 = (rr << 16) >= thi, k1 = rr >= thi;
+          if (t == 0) { S0[i] = k0 ? S0[i] : 0.f; S0[i + 1] = k1 ? S0[i + 1] : 0.f; }
+          else { S1[i] = k0 ? S1[i] : 0.f; S1[i + 1] = k1 ? S1[i + 1] : 0.f; }
+        }
+      }
+    }
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pf[0][s2][j] = (__bf16)S0[8 * s2 + j];
+        pf[1][s2][j] = (__bf16)S1[8 * s2 + j];
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int kb = t * 32 + 16 * s2 + 4 * hh + trow;
+        const bf16x8_t a0 = cat_tr(lds_tr(Vb + swz_e(kb, tcol)), lds_tr(Vb + swz_e(kb + 8, tcol)));
+        const bf16x8_t a1 = cat_tr(lds_tr(Vb + swz_e(kb, 32 + tcol)), lds_tr(Vb + swz_e(kb + 8, 32 + tcol)));
+        O0 = mfma32(a0, pf[t][s2], O0);
+        O1 = mfma32(a1, pf[t][s2], O1);
+      }
+    if (kt == nt - 1) {
+      float lt = l + __shfl_xor(l, 32, 64);
+      const float inv = lt > 0.f ? (DROP ? a.inv_keep : 1.f) / lt : 0.f;
+      if (qi < a.Sq) {
+        const int b = bh / a.H, h = bh % a.H;
+        bf16_t* op = a.o + b * a.o_sb + h * a.o_sh + (long)qi * a.o_ss;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = 8 * g + 4 * hh;
+          u16x4 v0 = {f2bf(O0[4 * g] * inv), f2bf(O0[4 * g + 1] * inv), f2bf(O0[4 * g + 2] * inv), f2bf(O0[4 * g + 3] * inv)};
+          u16x4 v1 = {f2bf(O1[4 * g] * inv), f2bf(O1[4 * g + 1] * inv), f2bf(O1[4 * g + 2] * inv), f2bf(O1[4 * g + 3] * inv)};
+          *reinterpret_cast<u16x4*>(op + d) = v0;
+          *reinterpret_cast<u16x4*>(op + 32 + d) = v1;
+        }
+        if (hh == 0 && a.lse) a.lse[(long)bh * a.Sq + qi] = lt > 0.f ? m + log2f(lt) : INFINITY;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[s] = qn[s];
+    }
+    if (f + 1 < nflat) swrite(1 - P, Kq, Vq, Bq);
+    __syncthreads();
+  };
+  for (int f = 0; f < nflat; f += 2) {
+    step(f, k0s, v0s, b0s, k1s, v1s, b1s, 0);
+    if (f + 1 < nflat) step(f + 1, k1s, v1s, b1s, k0s, v0s, b0s, 1);
+  }
+}
 
 struct AttnBwdArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* dO; const bf16_t* o;
@@ -566,6 +765,35 @@ static void drop_params(float p, uint64_t seed, uint64_t offset, uint32_t* thr16
   *base = host_hash_u32(s_lo ^ (s_hi * 0x85EBCA6Bu) ^ (o_lo * 0xC2B2AE35u));
 }
 
+// Multiprocessor count of the current device (cached per device id).
+static int attn_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// Persistent grid of a kernel with `per_cu` resident workgroups per CU over `nitems` work
+// items: every workgroup takes ceil(nitems / slots) items and the grid is the fewest
+// workgroups that need no more rounds than that.  CLOUDTIK_AMD_ATTN_PERSIST=0: one
+// workgroup per item.
+static int attn_persistent_grid(long nitems, int per_cu) {
+  static const int on = [] {
+    const char* e = getenv("CLOUDTIK_AMD_ATTN_PERSIST");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || nitems <= 0) return (int)nitems;
+  const long slots = (long)attn_cu_count() * per_cu;
+  if (nitems <= slots) return (int)nitems;
+  const long rounds = (nitems + slots - 1) / slots;
+  return (int)((nitems + rounds - 1) / rounds);
+}
+
 // strides: [batch, seq, head] in elements for each tensor; head_dim must be 64 (contiguous)
 // the kernels index rows inside one (batch, head) slice with 32-bit offsets
 static inline bool fits32(long rows, long row_stride) { return rows * row_stride + 64 < (1L << 31); }
@@ -599,6 +827,23 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
     return e ? atoi(e) : 0;
   }();
   const int wpe = (wpe_env >= 1 && wpe_env <= 3) ? wpe_env : (p_drop > 0.f ? 3 : 2);
+  static const int pipe = [] {
+    // opt-in: measured slower than the one-item kernel on BERT-large shapes (B 256, S 128,
+    // p 0.1: 75.5 us persistent / 84.9 us one item per workgroup vs 65.9 us;
+    // profiles/r3/attention_persistent_ab.md)
+    const char* e = getenv("CLOUDTIK_AMD_ATTN_FWD_PIPE");
+    return e ? atoi(e) : 0;
+  }();
+  if (pipe) {
+    const long nitems = (long)((Sq + 127) / 128) * B * H;
+    if (nitems > (1L << 30)) return -6;
+    const int g1 = attn_persistent_grid(nitems, 2);
+    if (drop && causal) attn_fwd_pipe_kernel<true, true><<<g1, 256, 0, stream>>>(a);
+    else if (drop) attn_fwd_pipe_kernel<true, false><<<g1, 256, 0, stream>>>(a);
+    else if (causal) attn_fwd_pipe_kernel<false, true><<<g1, 256, 0, stream>>>(a);
+    else attn_fwd_pipe_kernel<false, false><<<g1, 256, 0, stream>>>(a);
+    return 0;
+  }
 #define CT_ATTN_FWD(W)                                                                          \
   if (drop && causal) attn_fwd_d64_kernel<true, true, false, W><<<grid, 256, 0, stream>>>(a);    \
   else if (drop) attn_fwd_d64_kernel<true, false, false, W><<<grid, 256, 0, stream>>>(a);        \
