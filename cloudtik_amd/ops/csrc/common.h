@@ -90,6 +90,48 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return fmaf(x * 0.3989422804014327f, e, gelu_cdf_e(x, e));
 }
 
+// The same GELU / GELU' on element PAIRS, batched over NP pairs, for GEMM epilogues (the
+// matrix cores are idle there).  float2 arithmetic lowers to
+// v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two lanes' worth of fp32 per instruction); the
+// batch is computed stage by stage (all arguments, then all v_rcp / v_exp, then the
+// polynomials) so the transcendental results are not consumed by the very next instruction
+// (the scalar form left ~2 s_nop per element for those hazards).  exp(-x^2/2) is
+// exp2(x * (x * -log2(e)/2)).  Same formula and constants as gelu_cdf_e.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+template <int NP, bool GRAD>
+__device__ __forceinline__ void gelu2_batch(const f32x2 (&x)[NP], f32x2 (&y)[NP]) {
+  const float kE = -0.5f * 1.4426950408889634f;
+  f32x2 d[NP], e[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const f32x2 ax = {fabsf(x[p][0]), fabsf(x[p][1])};
+    d[p] = __builtin_elementwise_fma(ax, (f32x2)(0.3275911f * 0.70710678118654752f), (f32x2)(1.f));
+    e[p] = x[p] * (x[p] * kE);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    d[p] = f32x2{__builtin_amdgcn_rcpf(d[p][0]), __builtin_amdgcn_rcpf(d[p][1])};
+    e[p] = f32x2{__builtin_amdgcn_exp2f(e[p][0]), __builtin_amdgcn_exp2f(e[p][1])};
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const f32x2 t = d[p];
+    f32x2 q = __builtin_elementwise_fma(t, (f32x2)(1.061405429f), (f32x2)(-1.453152027f));
+    q = __builtin_elementwise_fma(q, t, (f32x2)(1.421413741f));
+    q = __builtin_elementwise_fma(q, t, (f32x2)(-0.284496736f));
+    q = __builtin_elementwise_fma(q, t, (f32x2)(0.254829592f));
+    q = q * t;
+    const f32x2 ea = __builtin_elementwise_fma(-q, e[p], (f32x2)(1.f));          // erf(|x| / sqrt 2)
+    const f32x2 s = {copysignf(ea[0], x[p][0]), copysignf(ea[1], x[p][1])};
+    const f32x2 cdf = __builtin_elementwise_fma(s, (f32x2)(0.5f), (f32x2)(0.5f));
+    if constexpr (GRAD)
+      y[p] = __builtin_elementwise_fma(x[p] * 0.3989422804014327f, e[p], cdf);
+    else
+      y[p] = x[p] * cdf;
+  }
+}
+
 // Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): consecutive logical tiles land on the same XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
