@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=32768)
     a = ap.parse_args()
     from cloudtik_amd import ops
-    from cloudtik_amd.ops.linear import splitk_factor
+    from cloudtik_amd.ops.linear import splitk_factor, tn2_splits
     C = ops.require_native()
     T = a.tokens
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -41,8 +41,9 @@ def main():
         ref = dy.float().t() @ x.float()
         fl = 2 * T * N * K
         row = {"case": name, "N": N, "K": K}
-        for S in sorted({splitk_factor(T, N, K), 2, 4, 8, 16}):
-            if T % (S * 64):
+        row["tn2_splits_chosen"] = tn2_splits(T, N, K)
+        for S in sorted({splitk_factor(T, N, K), tn2_splits(T, N, K), 2, 4, 5, 6, 8, 16}):
+            if T // 64 < S:
                 continue
             P = torch.empty(S, N, K, device="cuda")
             t_gemm = timeit(lambda: C.gemm_tn2(dy, x, P, S, False))

@@ -54,7 +54,8 @@ struct NtArgs {
   float* P;             // EPI 3: fp32 split-K slabs [splits][M][N]
   float* biasg;         // TN (BIASG): fp32 [splits][M] column sums of A over this split's K
   long lda, ldb, ldd, ldaux;
-  long tsplit;          // TN: reduction length per split
+  long tsplit;          // TN: number of split-K slices (the K-tiles are dealt out as evenly as
+                        // possible: the first (K / 64) % splits slices get one K-tile more)
   int M, N, K;
   int accumulate;       // EPI 0: D += result
 };
@@ -477,8 +478,14 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: staging bases in SGPRs
   const int wr = wave >> 2, wc = wave & 3;
   const long m0 = (long)tm * NT_BM, n0 = (long)tn * NT_BN;
-  const int nk = (SPLIT ? (int)a.tsplit : a.K) / NT_BK;
-  NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, SPLIT ? (long)split * a.tsplit : 0L, lds, wave, lane, wr * 64, wc * 32,
+  // split-K (TN): the K / 64 K-tiles dealt out over the slices, so any slice count works (e.g.
+  // 5 slices of the 512 K-tiles of a 32768-token weight gradient: 48 tiles x 5 = 240 workgroups,
+  // one wave, a third of the fp32 slab traffic of 16 power-of-two slices)
+  const int kt_all = a.K / NT_BK;
+  const int kt_q = SPLIT ? kt_all / (int)a.tsplit : kt_all, kt_r = SPLIT ? kt_all % (int)a.tsplit : 0;
+  const int nk = kt_q + (split < kt_r ? 1 : 0);
+  const long kfirst = SPLIT ? (long)(split * kt_q + min(split, kt_r)) * NT_BK : 0L;
+  NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, kfirst, lds, wave, lane, wr * 64, wc * 32,
           0, 0, 0, 0, (BIASG && tn == 0) ? 2 * wc : -1};
   f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   if constexpr (Ly::AT) {
@@ -590,7 +597,8 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
-// Weight-gradient layout: D[M,N] = A[K,M]^T . B[K,N] (row-major, K = tokens; lda >= M, ldb >= N).
+// Weight-gradient layout: D[M,N] = A[K,M]^T . B[K,N] (row-major, K = tokens; lda >= M, ldb >= N;
+// K % 64 == 0, any 1 <= splits <= K / 64).
 // splits > 1: fp32 partial slabs P[splits][M][N] (reduced by ct_splitk_reduce*); splits == 1:
 // bf16 out (+)= result (accumulate), row stride ldo.  biasg (optional, fp32 [splits][M]): the
 // column sums of A per split (the bias gradient when A is dY).  Nonzero (nothing launched)
@@ -598,13 +606,13 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
 extern "C" int ct_gemm_tn2(const void* A, long lda, const void* B, long ldb, void* out, long ldo, int M, int N,
                            long K, int splits, int accumulate, float* biasg, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || M % NT_BM || N % NT_BN) return 1;
-  if (K % ((long)splits * NT_BK)) return 2;
+  if (K % NT_BK || K / NT_BK < splits || K > (1L << 30)) return 2;
   if (lda % 8 || ldb % 8 || lda < M || ldb < N || ((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return 3;
   if (((uintptr_t)out & 15) || (splits == 1 && (ldo % 8 || ldo < N))) return 4;
   const long blocks = (long)(M / NT_BM) * (N / NT_BN) * splits;
   if (blocks > (1L << 30)) return 5;
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, splits == 1 ? (bf16_t*)out : nullptr, nullptr, nullptr, nullptr,
-           splits > 1 ? (float*)out : nullptr, biasg, lda, ldb, ldo, 0, K / splits, M, N, (int)(K / splits),
+           splits > 1 ? (float*)out : nullptr, biasg, lda, ldb, ldo, 0, (long)splits, M, N, (int)K,
            accumulate};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
   if (diag == 4) {

@@ -123,17 +123,24 @@ def splitk_factor(T: int, N: int, K: int) -> int:
 
 
 def tn2_splits(T: int, N: int, K: int, cus: int = 256) -> int:
-    """Split factor for the MFMA wgrad kernel: the fewest splits that minimise the number of
-    256-workgroup waves per unit of work, ceil(tiles * S / cus) / S (qkv 48 tiles -> 16,
-    proj 16 -> 16, FFN 64 -> 4), keeping >= 512 tokens per split; slab reduction cost grows
-    with S, so ties go to the smaller S."""
+    """Split factor for the MFMA wgrad kernel (any S: the kernel deals the T / 64 K-tiles out
+    over the slices).  Modelled time = K loop + fp32 slab round trip:
+      loop(S) = t_full * waves(S) * cus / (tiles * S), waves = ceil(tiles * S / cus), with
+      t_full the loop time at a perfect spread (2 N K T at ~1.3 PF/s, measured K-loop rate);
+      slab(S) = S * tiles * 256 KiB * 2 (written, read back by the reduce) at ~5 TB/s (0 at S=1).
+    BERT-large: qkv 48 tiles -> 5 (240 workgroups, one wave; 16 power-of-two slices cost 3x the
+    slab bytes), proj 16 tiles -> 16, FFN 64 tiles -> 4.  >= 512 tokens per slice."""
     tiles = (N // 256) * (K // 256)
+    if tiles <= 0 or T % 64:
+        return 1
+    t_full = 2.0 * N * K * T / 1.3e15
     best, best_cost = 1, None
-    for S in (1, 2, 4, 8, 16, 32):
-        if T % (64 * S) or (S > 1 and T // S < 512):
+    for S in range(1, 33):
+        if S > 1 and (T // S < 512 or T // 64 < S):
             continue
-        cost = -(-tiles * S // cus) / S
-        if best_cost is None or cost < best_cost - 1e-12:
+        waves = -(-tiles * S // cus)
+        cost = t_full * waves * cus / (tiles * S) + (S * tiles * 262144 * 2 / 5e12 if S > 1 else 0.0)
+        if best_cost is None or cost < best_cost * (1 - 1e-9):
             best, best_cost = S, cost
     return best
 

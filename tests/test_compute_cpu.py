@@ -268,13 +268,13 @@ def test_dropout_sites_with_close_keys_are_independent(monkeypatch):
 
 
 def test_wgrad_split_choice_fills_whole_waves():
-    """tn2_splits (ops/linear.py): the fewest splits minimising 256-workgroup waves per unit of
-    work -- BERT-large qkv 48 tiles -> 16 (3 full waves), proj 16 -> 16, FFN 64 -> 4 -- and never
-    fewer than 512 tokens per split or a token count the 64-row K-tile does not divide."""
+    """tn2_splits (ops/linear.py): K loop (256-workgroup waves) + fp32 slab round trip --
+    BERT-large qkv 48 tiles -> 5 (240 workgroups in one wave, a third of the slab bytes of 16),
+    proj 16 -> 16, FFN 64 -> 4 -- and never fewer than 512 tokens per split."""
     import importlib
     L = importlib.import_module("cloudtik_amd.ops.linear")
     T = 32768
-    assert L.tn2_splits(T, 3072, 1024) == 16
+    assert L.tn2_splits(T, 3072, 1024) == 5
     assert L.tn2_splits(T, 1024, 1024) == 16
     assert L.tn2_splits(T, 4096, 1024) == 4 and L.tn2_splits(T, 1024, 4096) == 4
     assert L.tn2_splits(T, 8192, 8192) == 1                     # 1024 tiles: already 4 full waves
@@ -283,4 +283,4 @@ def test_wgrad_split_choice_fills_whole_waves():
     for T_ in (4096, 32768, 65536):
         for N, K in ((1024, 1024), (3072, 1024), (4096, 1024), (768, 3072)):
             S = L.tn2_splits(T_, N, K)
-            assert T_ % (64 * S) == 0 and (S == 1 or T_ // S >= 512)
+            assert T_ // 64 >= S and (S == 1 or T_ // S >= 512)

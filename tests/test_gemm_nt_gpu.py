@@ -116,10 +116,23 @@ def test_gemm_nt_operands_spanning_4gb_addresses():
     del A2, big
 
 
+def _split_ranges(K, S):
+    """K range of each split-K slice: the K / 64 K-tiles dealt out, the first (K/64) % S
+    slices one K-tile longer (ct_gemm_tn2)."""
+    q, r = divmod(K // 64, S)
+    out, k = [], 0
+    for s in range(S):
+        n = (q + (1 if s < r else 0)) * 64
+        out.append((k, k + n))
+        k += n
+    return out
+
+
 # ---- weight-gradient layout (ct_gemm_tn2): out = A[K,M]^T B[K,N], token-major operands
 @pytest.mark.parametrize("M,N,K,S", [(256, 256, 64, 1), (512, 256, 128, 1), (256, 768, 192, 1),
                                      (768, 512, 1024, 1), (256, 256, 512, 8), (512, 768, 2048, 4),
-                                     (1024, 256, 768, 3)])
+                                     (1024, 256, 768, 3), (768, 256, 320, 3), (512, 512, 2048, 5),
+                                     (256, 256, 192, 3)])
 def test_gemm_tn2_matches_fp32(M, N, K, S):
     C = _C()
     A, B = _rand(K, M, seed=M + K), _rand(K, N, seed=N + 7 * K, scale=K ** -0.5)
@@ -136,10 +149,10 @@ def test_gemm_tn2_matches_fp32(M, N, K, S):
         P = torch.full((S, M, N), float("nan"), device="cuda")
         assert C.gemm_tn2(A, B, P, S, False)
         torch.testing.assert_close(P.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
-        # each slab is its own K range
-        Ks = K // S
-        torch.testing.assert_close(P[1], A[Ks:2 * Ks].float().t() @ B[Ks:2 * Ks].float(), rtol=2e-3,
-                                   atol=2e-3 * ref.abs().max().item())
+        # each slab is its own K range (uneven when S does not divide the K-tile count)
+        for s_, (k0, k1) in enumerate(_split_ranges(K, S)):
+            torch.testing.assert_close(P[s_], A[k0:k1].float().t() @ B[k0:k1].float(), rtol=2e-3,
+                                       atol=2e-3 * ref.abs().max().item())
 
 
 def test_gemm_tn2_strided_operands_and_refusals():
@@ -153,8 +166,8 @@ def test_gemm_tn2_strided_operands_and_refusals():
     assert not D[:, :128].any() and not D[:, 640:].any()
     assert not C.gemm_tn2(_rand(96, 256), _rand(96, 256), torch.empty(256, 256, device="cuda",
                                                                       dtype=torch.bfloat16), 1, False)   # K % 64
-    assert not C.gemm_tn2(_rand(256, 256), _rand(256, 256), torch.empty(3, 256, 256, device="cuda"), 3,
-                          False)                                                     # K % (S * 64)
+    assert not C.gemm_tn2(_rand(128, 256), _rand(128, 256), torch.empty(3, 256, 256, device="cuda"), 3,
+                          False)                                      # fewer K-tiles (2) than splits
 
 
 # ---- NN layout (gemm_nn): D = A[M,K] @ B[K,N], B read in place from an [out, in] weight
@@ -179,7 +192,8 @@ def test_gemm_nn_plain_and_dgelu(M, N, K):
     _close(D, A.float() @ Bw[:, 128:].float())
 
 
-@pytest.mark.parametrize("M,N,K,S", [(512, 256, 256, 1), (768, 512, 2048, 4), (3072, 1024, 8192, 16)])
+@pytest.mark.parametrize("M,N,K,S", [(512, 256, 256, 1), (768, 512, 2048, 4), (3072, 1024, 8192, 16),
+                                     (3072, 1024, 8192, 5)])
 def test_gemm_tn2_bias_column_sums(M, N, K, S):
     """gemm_tn2_bias: the weight-gradient product plus per-split column sums of A (the bias
     gradient) from the extra all-ones MFMA; the product itself is unchanged."""
@@ -195,6 +209,5 @@ def test_gemm_tn2_bias_column_sums(M, N, K, S):
         P = torch.empty(S, M, N, device="cuda")
         assert C.gemm_tn2_bias(A, B, P, S, False, bP)
         torch.testing.assert_close(P.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
-    Ks = K // S
-    want = A.float().view(S, Ks, M).sum(1)
+    want = torch.stack([A[k0:k1].float().sum(0) for k0, k1 in _split_ranges(K, S)])
     torch.testing.assert_close(bP, want, rtol=1e-3, atol=1e-2)
