@@ -96,9 +96,14 @@ class GradBucketer:
         self._enabled = True
         self._hooks = []
         if self.overlap:
-            for p in space.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-                p._ct_grad_ready = self._on_grad   # fused-wgrad GEMMs (ops.linear) report here
+            self._register_hooks()
+
+    def _register_hooks(self):
+        if self._hooks:
+            return
+        for p in self.space.params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            p._ct_grad_ready = self._on_grad   # fused-wgrad GEMMs (ops.linear) report here
 
     # ------------------------------------------------------------------ ZeRO-1 layout
     def _build_uniform_buckets(self, cap):
