@@ -92,6 +92,7 @@ class GradBucketer:
         self._pending = [len(m) for _, _, m in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._next = 0
+        self._reported = set()
         self._works = []
         self._enabled = True
         self._hooks = []
@@ -139,6 +140,14 @@ class GradBucketer:
     def _on_grad(self, p):
         if not self._enabled:
             return
+        # a parameter reports ONCE per backward: the fused paths that accumulate straight into
+        # the flat buffer call _ct_grad_ready themselves, and autograd then still runs the
+        # parameter's post-accumulate hook (with no gradient of its own) -- counted twice, the
+        # second report would complete a bucket before its last member's gradient landed and
+        # the all-reduce would miss it (tests/test_bucket_ready_gpu.py)
+        if id(p) in self._reported:
+            return
+        self._reported.add(id(p))
         for b in self.param_bucket[id(p)]:
             self._pending[b] -= 1
             if self._pending[b] == 0:
@@ -239,6 +248,7 @@ class GradBucketer:
         from cloudtik_amd.ops.linear import sync_grad_stream
         self.space.flush_grads()
         if self.world <= 1:
+            self._reset()
             if self.space.grad.is_cuda:
                 sync_grad_stream()
             if self.fp32:
@@ -260,9 +270,14 @@ class GradBucketer:
                 buf.record_stream(torch.cuda.current_stream()) if buf.is_cuda else None
                 dst.copy_(buf)
         self._works.clear()
+        self._reset()
+
+    def _reset(self):
+        """Per-backward bookkeeping back to 'nothing reported'."""
         self._pending = [len(m) for _, _, m in self.buckets]
         self._ready = [False] * len(self.buckets)
         self._next = 0
+        self._reported = set()
 
     @property
     def grad_scale(self) -> float:
