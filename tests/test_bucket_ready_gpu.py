@@ -66,3 +66,53 @@ def test_buckets_launch_once_with_final_gradients(bucket_mb):
             space.zero_grad()
     finally:
         ddp.remove()
+
+
+@pytest.mark.parametrize("bucket_mb", [0.25, 8.0])
+def test_resnet_buckets_launch_once_with_final_gradients(bucket_mb):
+    """The same on the ResNet path: conv weight gradients added into the flat buffer on the
+    side stream or deferred until flush_grads(), BN affine gradients from fused kernels."""
+    import torch.nn.functional as F
+    from cloudtik_amd.models.resnet import resnet18_like_small
+    from cloudtik_amd.parallel import GradBucketer
+    from cloudtik_amd.train.optim import FlatParamSpace
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    model = resnet18_like_small(device=dev)
+    model.train()
+    named = list(model.named_parameters())
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    ddp = GradBucketer(space, bucket_mb=bucket_mb)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(4, 3, 32, 32, generator=g).to(device=dev, dtype=next(model.parameters()).dtype)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), generator=g).to(dev)
+    launched = {}
+
+    def record(b):
+        space.flush_grads()                           # what _launch does before the collective
+        torch.cuda.synchronize()
+        lo, hi, _ = ddp.buckets[b]
+        launched.setdefault(b, []).append(space.grad[lo:hi].clone())
+
+    ddp._launch = record
+    ddp._register_hooks()
+    try:
+        for _ in range(2):
+            launched.clear()
+            F.cross_entropy(model(x).float(), y).backward()
+            space.flush_grads()
+            torch.cuda.synchronize()
+            bad = []
+            for b, (lo, hi, mem) in enumerate(ddp.buckets):
+                got = launched.get(b, [])
+                if len(got) != 1:
+                    bad.append(f"bucket {b}: launched {len(got)} times")
+                elif not torch.equal(got[0], space.grad[lo:hi]):
+                    bad.append(f"bucket {b} ({[space.names[i] for i in mem][:3]}...): launched early")
+            assert not bad, "\n".join(bad)
+            ddp.finish()
+            space.zero_grad()
+    finally:
+        ddp.remove()
