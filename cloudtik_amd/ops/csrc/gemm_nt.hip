@@ -380,6 +380,16 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
   // column of this lane's 16-B chunk after the swap, relative to block 0 of the pair
   const int g = lane >> 4;
   const long scol = (ncol - 4 * g) + 16 * (g & 1) + 8 * (g >> 1);
+  // dGELU: the pre-activation rows are loaded two rows ahead of their use (a ring of two
+  // row buffers, compile-time indexed in the unrolled row loop); loaded at the row itself,
+  // every row waited a full memory latency (vmcnt(0) before each row's math)
+  u16x4 zq[2][NJ];
+  if constexpr (EPI == NT_EPI_DGELU_BGRAD) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) zq[i][j] = *(const u16x4*)(a.aux + (mrow + i * 16) * a.ldaux + ncol + j * 16);
+  }
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -421,14 +431,20 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
               out[j][2 * h + e] = f2bf(gv[2 * j + h][e]);
             }
       } else {
-        // dGELU: scalar form (the packed-pair form measured no faster here: 366 vs 349 us per
-        // BERT-large FFN dgrad; this epilogue reads z and writes dz at HBM rate)
+        // dGELU: scalar form (the packed-pair form measured no faster: 366 vs 349 us per
+        // BERT-large FFN dgrad)
+        u16x4 z[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) z[j] = zq[i & 1][j];
+        if (i + 2 < 8) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) zq[i & 1][j] = *(const u16x4*)(a.aux + (m + 32) * a.ldaux + ncol + j * 16);
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const u16x4 z = *(const u16x4*)(a.aux + m * a.ldaux + ncol + j * 16);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float gg = acc[i][j][r] * gelu_erf_grad(bf2f(z[r]) + bv[j][r]);
+            const float gg = acc[i][j][r] * gelu_erf_grad(bf2f(z[j][r]) + bv[j][r]);
             out[j][r] = f2bf(gg);
             if constexpr (BGRAD) cs[2 * j + (r >> 1)][r & 1] += gg;
           }
