@@ -342,9 +342,39 @@ __device__ __forceinline__ u16x8 nt_pair_swap(u16x4 x, u16x4 y) {
 // epilogue over one wave's accumulators: acc[i][j][r] holds D[mrow + 16i][ncol + 16j + r]
 // (ncol includes this lane's 4 (lane >> 4)); math in that layout, stores after the swap.
 // EPI 3 (fp32 split-K slab, row stride N): the lane's 4 columns are one 16-B store already.
+// Epilogue operands loaded ahead of their use: the bias columns before the K loop (the
+// epilogue used to open with these loads and wait a full memory latency, once per tile; the
+// K loop's counted vmcnt waits stay correct -- the loads are older than the DMA they wait
+// for, so they are simply waited for too) and the dGELU pre-activation rows two rows ahead
+// inside the epilogue.  Issuing the first two rows before the last K-tile as well measured
+// slower (343 vs 338 us per BERT-large FFN dgrad): the last K-tile's waits then cover them.
+template <int NJ>
+struct NtEpiPre {
+  u16x4 bias[NJ];
+  u16x4 z[2][NJ];
+};
+
+template <int EPI, int NJ>
+__device__ __forceinline__ void nt_preload_bias(const NtArgs& a, long ncol, NtEpiPre<NJ>& pre) {
+  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) pre.bias[j] = a.bias ? *(const u16x4*)(a.bias + ncol + j * 16) : u16x4(0);
+  }
+}
+
+template <int EPI, int NJ>
+__device__ __forceinline__ void nt_preload_z(const NtArgs& a, long mrow, long ncol, NtEpiPre<NJ>& pre) {
+  if constexpr (EPI == NT_EPI_DGELU_BGRAD) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) pre.z[i][j] = *(const u16x4*)(a.aux + (mrow + i * 16) * a.ldaux + ncol + j * 16);
+  }
+}
+
 template <int EPI, bool BGRAD, int NJ>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[8][NJ], long mrow, long ncol,
-                                            int lane, int split) {
+                                            int lane, int split, NtEpiPre<NJ>& pre) {
   static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
   if constexpr (EPI == NT_EPI_NONE) {
     // timing diagnostic (CLOUDTIK_AMD_GEMM_DIAG=4): the K loop without the epilogue's memory
@@ -366,13 +396,11 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
     return;
   }
   float bv[NJ][4] = {};
-  if (EPI == NT_EPI_BIAS_GELU_AUX || (EPI == NT_EPI_DGELU_BGRAD && a.bias)) {
+  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const u16x4 b = *(const u16x4*)(a.bias + ncol + j * 16);
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[j][r] = bf2f(b[r]);
-    }
+      for (int r = 0; r < 4; ++r) bv[j][r] = bf2f(pre.bias[j][r]);
   }
   f32x2 cs[2 * NJ];   // dGELU column sums, packed pairs: (block j, columns 2h, 2h + 1)
 #pragma unroll
@@ -381,15 +409,10 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
   const int g = lane >> 4;
   const long scol = (ncol - 4 * g) + 16 * (g & 1) + 8 * (g >> 1);
   // dGELU: the pre-activation rows are loaded two rows ahead of their use (a ring of two
-  // row buffers, compile-time indexed in the unrolled row loop); loaded at the row itself,
-  // every row waited a full memory latency (vmcnt(0) before each row's math)
-  u16x4 zq[2][NJ];
-  if constexpr (EPI == NT_EPI_DGELU_BGRAD) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) zq[i][j] = *(const u16x4*)(a.aux + (mrow + i * 16) * a.ldaux + ncol + j * 16);
-  }
+  // row buffers, compile-time indexed in the unrolled row loop; rows 0 and 1 by
+  // nt_preload_z); loaded at the row itself, every row waited a full memory latency
+  auto& zq = pre.z;
+  nt_preload_z<EPI, NJ>(a, mrow, ncol, pre);
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -522,6 +545,11 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // this lane's epilogue coordinates: rows m0 + wr*128 + 16i + (lane & 15), columns
+  // n0 + wc*64 + 16j + 4(lane >> 4) + r
+  const long emrow = m0 + wr * 128 + (lane & 15), encol = n0 + wc * 64 + (lane >> 4) * 4;
+  NtEpiPre<4> epre;
+  nt_preload_bias<EPI, 4>(a, encol, epre);
 
   nt_s16x8 fa[2][4][2];   // [qm][frag][ks]: A rows wr*128 + qm*64 + 16 frag
   nt_s16x8 fb[2][2][2];   // [qn][frag][ks]: B rows wc*64 + qn*32 + 16 frag
@@ -551,7 +579,7 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 
   // acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
-  nt_epilogue<EPI, BGRAD, 4>(a, acc, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + (lane >> 4) * 4, lane, split);
+  nt_epilogue<EPI, BGRAD, 4>(a, acc, emrow, encol, lane, split, epre);
   if constexpr (BIASG) {
     // accb[t] row block 2 wc + t: every column holds the row sum; lanes 0-15 hold rows 0-15
     if (c.biasw >= 0 && lane < 16) {
