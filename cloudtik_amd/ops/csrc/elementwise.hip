@@ -321,6 +321,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
     }
+    // unrolled so several slabs' loads are in flight per thread (a rolled loop waits one
+    // memory latency per slab)
+#pragma unroll 4
     for (int s = 0; s < S; ++s) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(P + s * n + v * 8);
       const f32x4 b = *reinterpret_cast<const f32x4*>(P + s * n + v * 8 + 4);
