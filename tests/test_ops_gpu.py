@@ -525,3 +525,36 @@ def test_batchnorm_repeat_and_relu_modes(cuda, C):
     assert torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1])
     ref_mean = xs[1].float().mean(dim=(0, 2, 3))
     assert _rel(outs[1][1][:C], ref_mean) < 1e-4
+
+
+@pytest.mark.parametrize("V,ld", [(1000, 1024), (30522, 30720), (12000, 12000), (40000, 40000)])
+@pytest.mark.parametrize("smooth", [0.0, 0.1])
+def test_xent_kernel_matches_fp32(cuda, V, ld, smooth):
+    """xent_fwd (in place, gradient written over the logits): loss rows, log-sum-exp and
+    (softmax - onehot) * scale against an fp32 reference, padded columns zero.  Rows up to 32768
+    columns run the register-resident kernel (one read of the row), wider rows the two-pass one
+    (40000)."""
+    from cloudtik_amd import ops as _ops
+    C = _ops.require_native()
+    torch.manual_seed(1)
+    R = 37
+    logits = (3 * torch.randn(R, ld, device=cuda)).bfloat16()
+    labels = torch.randint(0, V, (R,), device=cuda)
+    labels[::5] = -100
+    labels[1] = V - 1                                   # the last real column
+    ref = logits.float()[:, :V]
+    lse_ref = torch.logsumexp(ref, 1)
+    valid = labels != -100
+    scale = torch.tensor([1.0 / valid.sum().item()], device=cuda)
+    buf = logits.clone()
+    loss, lse = C.xent_fwd(buf, buf, V, labels, scale, -100, smooth)
+    torch.cuda.synchronize()
+    logp = ref - lse_ref[:, None]
+    nll = -logp.gather(1, labels.clamp_min(0)[:, None])[:, 0]
+    want_loss = torch.where(valid, (1 - smooth) * nll - smooth * logp.mean(1), torch.zeros_like(nll))
+    torch.testing.assert_close(lse, lse_ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(loss, want_loss, rtol=1e-3, atol=2e-3)
+    onehot = torch.nn.functional.one_hot(labels.clamp_min(0), V).float()
+    g = (logp.exp() - smooth / V - (1 - smooth) * onehot) * scale * valid[:, None].float()
+    torch.testing.assert_close(buf.float()[:, :V], g, rtol=2e-2, atol=2e-4)
+    assert buf.float()[:, V:].abs().max().item() == 0.0 if ld > V else True
