@@ -111,6 +111,8 @@ def test_linear_cross_entropy(cuda, R):
     assert _rel(x.grad, xr.grad) < 3e-2
     assert _rel(W.grad[:V], Wr.grad[:V]) < 3e-2
     assert W.grad[V:].abs().max().item() == 0.0
+    assert _rel(b.grad[:V], br.grad[:V]) < 3e-2           # 320 rows: from the TN kernel's all-ones MFMA
+    assert b.grad[V:].abs().max().item() == 0.0
 
 
 @pytest.mark.parametrize("S", [128, 64, 200, 512])
