@@ -26,6 +26,7 @@ int ct_embed3_fwd(const int64_t*, const int64_t*, const void*, const void*, cons
 int ct_embed3_bwd(const int64_t*, const int64_t*, const void*, float*, float*, float*, int, int, int, int, hipStream_t);
 int ct_cast(const void*, int, void*, int, long, float, int, hipStream_t);
 int ct_splitk_reduce(const float*, int, long, void*, int, hipStream_t);
+int ct_splitk_reduce_clear(float*, int, long, void*, int, hipStream_t);
 int ct_lamb(const void*, int, float*, float*, float*, void*, int, const int*, const long*,
             const int*, int, const int*, int, const float*, const float*, float, float, float, int,
             int, float*, float*, int, hipStream_t);
@@ -259,6 +260,15 @@ void splitk_reduce(at::Tensor partials, at::Tensor g, bool accumulate) {
   TORCH_CHECK(g.numel() % 8 == 0, "splitk_reduce: numel must be a multiple of 8");
   TORCH_CHECK(ct_splitk_reduce(partials.data_ptr<float>(), (int)partials.size(0), g.numel(), g.data_ptr(),
                                accumulate ? 1 : 0, cur_stream()) == 0);
+}
+
+// the same, and the partials are zeroed once read (persistent accumulation buffers)
+void splitk_reduce_clear(at::Tensor partials, at::Tensor g, bool accumulate) {
+  CHECK_IN(partials); CHECK_F32(partials); CHECK_IN(g); CHECK_BF16(g);
+  TORCH_CHECK(partials.dim() >= 2 && partials[0].numel() == g.numel(), "splitk_reduce_clear: shape mismatch");
+  TORCH_CHECK(g.numel() % 8 == 0, "splitk_reduce_clear: numel must be a multiple of 8");
+  TORCH_CHECK(ct_splitk_reduce_clear(partials.data_ptr<float>(), (int)partials.size(0), g.numel(), g.data_ptr(),
+                                     accumulate ? 1 : 0, cur_stream()) == 0, "splitk_reduce_clear failed");
 }
 
 // ---------------------------------------------------------------- optimizers
@@ -625,6 +635,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed3_bwd", &embed3_bwd);
   m.def("cast_into", &cast_into);
   m.def("splitk_reduce", &splitk_reduce);
+  m.def("splitk_reduce_clear", &splitk_reduce_clear);
   m.def("lamb_step", &lamb_step);
   m.def("adam_step", &adam_step);
   m.def("sgd_step", &sgd_step);

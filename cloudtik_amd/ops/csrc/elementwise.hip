@@ -308,8 +308,11 @@ extern "C" int ct_embed3_bwd(const int64_t* ids, const int64_t* tt, const void* 
 // g[i] = bf16( (accumulate ? g[i] : 0) + sum_s P[s*n + i] ) -- the second half of a split-K
 // weight-gradient GEMM (the partials come from one batched hipBLASLt GEMM with fp32 output).
 // One pass: 8 elements per thread, S fp32 float4 pairs + one bf16x8 load/store.
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, int S, long nv,
-                                                            bf16_t* __restrict__ g, int accumulate) {
+// clear: the partials are zeroed after they are read (a persistent fp32 accumulation buffer --
+// the fused FFN dgrad's bias-gradient atomics -- is then ready for its next use without a fill
+// kernel)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(float* __restrict__ P, int S, long nv,
+                                                            bf16_t* __restrict__ g, int accumulate, int clear) {
   const long n = nv * 8;
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nv; v += (long)gridDim.x * blockDim.x) {
     float acc[8];
@@ -329,6 +332,10 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       const f32x4 b = *reinterpret_cast<const f32x4*>(P + s * n + v * 8 + 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += b[j]; }
+      if (clear) {
+        *reinterpret_cast<f32x4*>(P + s * n + v * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(P + s * n + v * 8 + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     u16x8 o;
 #pragma unroll
@@ -340,7 +347,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 extern "C" int ct_splitk_reduce(const float* P, int S, long n, void* g, int accumulate, hipStream_t stream) {
   if (n % 8) return -1;
   const long nv = n / 8;
-  splitk_reduce_kernel<<<grid_for(nv), 256, 0, stream>>>(P, S, nv, (bf16_t*)g, accumulate);
+  splitk_reduce_kernel<<<grid_for(nv), 256, 0, stream>>>(const_cast<float*>(P), S, nv, (bf16_t*)g, accumulate, 0);
+  return 0;
+}
+
+extern "C" int ct_splitk_reduce_clear(float* P, int S, long n, void* g, int accumulate, hipStream_t stream) {
+  if (n % 8) return -1;
+  const long nv = n / 8;
+  splitk_reduce_kernel<<<grid_for(nv), 256, 0, stream>>>(P, S, nv, (bf16_t*)g, accumulate, 1);
   return 0;
 }
 

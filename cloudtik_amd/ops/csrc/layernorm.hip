@@ -260,27 +260,32 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
 
 // Up to three column sums in ONE launch (blockIdx.y picks the (partials, output) pair):
 // the LayerNorm backward's dgamma / dbeta / dbias reductions are tiny (a few MB) and were
-// three back-to-back launch latencies.
+// three back-to-back launch latencies.  Block = 16 columns x 16 row-lanes (256 threads), so a
+// 1024-wide reduction spreads over 3 x 64 workgroups (at 64 columns per 1024-thread block it
+// ran on 48 CUs), and each lane keeps 8 independent loads in flight: the kernel is a chain of
+// memory latencies, not bandwidth (9 MB per call).
 struct Colsum3 { const float* part[3]; void* out[3]; };
 
 template <typename OUT>
-__global__ __launch_bounds__(1024) void colsum3_kernel(Colsum3 c, int P, int N, int accumulate) {
-  __shared__ float red[16][64];
+__global__ __launch_bounds__(256) void colsum3_kernel(Colsum3 c, int P, int N, int accumulate) {
+  __shared__ float red[16][16];
   const float* __restrict__ part = c.part[blockIdx.y];
   OUT* __restrict__ out = reinterpret_cast<OUT*>(c.out[blockIdx.y]);
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + cl;
-  float t = 0.f;
+  const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (col < N) {
     int p = rl;
-    for (; p + 48 < P; p += 64) {
-      const float a = part[(size_t)p * N + col], b = part[(size_t)(p + 16) * N + col];
-      const float d = part[(size_t)(p + 32) * N + col], e = part[(size_t)(p + 48) * N + col];
-      t += (a + b) + (d + e);
+    for (; p + 112 < P; p += 128) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(p + 16 * u) * N + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] += v[u];
     }
-    for (; p < P; p += 16) t += part[(size_t)p * N + col];
+    for (; p < P; p += 16) t[0] += part[(size_t)p * N + col];
   }
-  red[rl][cl] = t;
+  red[rl][cl] = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
   __syncthreads();
   if (rl == 0 && col < N) {
     float s = 0.f;
@@ -299,9 +304,9 @@ static int colsum_multi(const float* const* parts, void* const* outs, int n, int
                         int accumulate, hipStream_t stream) {
   Colsum3 c{};
   for (int i = 0; i < n; ++i) { c.part[i] = parts[i]; c.out[i] = outs[i]; }
-  const dim3 grid(ceil_div(N, 64), n);
-  if (out_fp32) colsum3_kernel<float><<<grid, 1024, 0, stream>>>(c, P, N, accumulate);
-  else colsum3_kernel<bf16_t><<<grid, 1024, 0, stream>>>(c, P, N, accumulate);
+  const dim3 grid(ceil_div(N, 16), n);
+  if (out_fp32) colsum3_kernel<float><<<grid, 256, 0, stream>>>(c, P, N, accumulate);
+  else colsum3_kernel<bf16_t><<<grid, 256, 0, stream>>>(c, P, N, accumulate);
   return 0;
 }
 

@@ -60,6 +60,21 @@ def _fused_ffn1(C, x2, W1, b1f):
     return zb, h
 
 
+# fp32 bias-gradient accumulators of the fused FFN dgrad, one per (device, width), kept
+# zeroed between uses: the reduce that moves the sums into the bf16 gradient clears them
+# (splitk_reduce_clear), so no fill kernel runs per layer.  Uses are stream-ordered on the
+# main stream.
+_DB_ACC = {}
+
+
+def _zeroed_acc(device, F):
+    key = (device, F)
+    t = _DB_ACC.get(key)
+    if t is None:
+        t = _DB_ACC[key] = torch.zeros(F, device=device, dtype=torch.float32)
+    return t
+
+
 def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f):
     """dz = (df @ W2) * gelu'(z [+ b1f]); db1f += column sums of dz (b1f None: z already
     holds the bias).  W2 [H, F] is read in place as the [K, N] operand (gemm_nn: no transposed
@@ -69,11 +84,12 @@ def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f):
     if T % 256 or F % 256 or df.shape[1] % 64:
         return None
     dz = torch.empty_like(z)
-    db = torch.zeros(F, device=z.device, dtype=torch.float32)
+    direct = db1f.dtype == torch.bfloat16 and db1f.is_contiguous()
+    db = _zeroed_acc(z.device, F) if direct else torch.zeros(F, device=z.device, dtype=torch.float32)
     if not C.gemm_nn(df, W2, dz, 2, False, b1f, z, db):
         return None
-    if db1f.dtype == torch.bfloat16 and db1f.is_contiguous():
-        C.splitk_reduce(db.view(1, F), db1f, True)
+    if direct:
+        C.splitk_reduce_clear(db.view(1, F), db1f, True)
     else:
         db1f.add_(db)
     return dz
