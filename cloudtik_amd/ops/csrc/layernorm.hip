@@ -110,15 +110,19 @@ struct LnBwdArgs {
   int M, N; uint32_t thresh; float scale; uint64_t seed, offset;
 };
 
-template <int MAXV, bool RMS, bool EXTRA>
+// DBIAS: also the column sums of dx (the gradient of the bias folded into the forward's
+// prologue); off when the consumer computes them instead (the projection's weight-gradient
+// GEMM sums its dY operand with an all-ones MFMA: ops/transformer.py) -- 16 fewer registers
+// and adds per row, a third fewer partials
+template <int MAXV, bool RMS, bool EXTRA, bool DBIAS>
 __global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
   const int N = a.N, nvec = N >> 3;
   const bool drop = a.thresh != 0;
-  const bool want_dbias = a.dbias_part != nullptr;
-  float dg[MAXV][8], db[MAXV][8], dbi[MAXV][8];
+  constexpr bool want_dbias = DBIAS;
+  float dg[MAXV][8], db[MAXV][8], dbi[DBIAS ? MAXV : 1][8];
   u16x8 gb[MAXV];                    // gamma kept packed (bf16): 4 VGPRs per 8 columns
   const u16x8* g8 = reinterpret_cast<const u16x8*>(a.gamma);
 #pragma unroll
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
     const int c = lane + i * 64;
     gb[i] = c < nvec ? g8[c] : u16x8(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; }
+    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; if (DBIAS) dbi[i][j] = 0.f; }
   }
   // Software pipeline: the s / dy / dextra rows (and mean, rstd) of the NEXT row are in
   // flight while this row's reductions and stores run -- the kernel is latency bound with
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
           o[j] = f2bf(t);
           float tx = drop ? (((keep >> j) & 1u) ? t * a.scale : 0.f) : t;
           od[j] = f2bf(tx);
-          dbi[i][j] += tx;
+          if constexpr (DBIAS) dbi[i][j] += tx;
         }
         if (a.ds) reinterpret_cast<u16x8*>(a.ds + (size_t)row * N)[c] = o;
         if (a.dx) reinterpret_cast<u16x8*>(a.dx + (size_t)row * N)[c] = od;
@@ -212,7 +216,7 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
         for (int j = 0; j < 8; ++j) {
           const int col = c * 8 + j;
           if (c < nvec && col >= base && col < base + 512)
-            red[wid][col - base] = pass == 0 ? dg[i][j] : (pass == 1 ? db[i][j] : dbi[i][j]);
+            red[wid][col - base] = pass == 0 ? dg[i][j] : (pass == 1 ? db[i][j] : dbi[DBIAS ? i : 0][j]);
         }
       }
       __syncthreads();
@@ -367,17 +371,20 @@ extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, co
   a.scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed; a.offset = offset;
   const int mv = (N / 8 + 63) / 64;
-#define CT_LNB(MV) case MV:                                                                  \
-    if (rms) { if (a.dextra) ln_bwd_kernel<MV, true, true><<<grid, 256, 0, stream>>>(a);          \
-               else ln_bwd_kernel<MV, true, false><<<grid, 256, 0, stream>>>(a); }                  \
-    else { if (a.dextra) ln_bwd_kernel<MV, false, true><<<grid, 256, 0, stream>>>(a);             \
-           else ln_bwd_kernel<MV, false, false><<<grid, 256, 0, stream>>>(a); }                     \
+#define CT_LNB2(MV, DB)                                                                       \
+    if (rms) { if (a.dextra) ln_bwd_kernel<MV, true, true, DB><<<grid, 256, 0, stream>>>(a);       \
+               else ln_bwd_kernel<MV, true, false, DB><<<grid, 256, 0, stream>>>(a); }               \
+    else { if (a.dextra) ln_bwd_kernel<MV, false, true, DB><<<grid, 256, 0, stream>>>(a);          \
+           else ln_bwd_kernel<MV, false, false, DB><<<grid, 256, 0, stream>>>(a); }
+#define CT_LNB(MV) case MV:                                                                   \
+    if (a.dbias_part) { CT_LNB2(MV, true) } else { CT_LNB2(MV, false) }                         \
     break;
   switch (mv) {
     CT_LNB(1) CT_LNB(2) CT_LNB(3) CT_LNB(4)
     default: return -1;
   }
 #undef CT_LNB
+#undef CT_LNB2
   const float* parts[3];
   void* outs[3];
   int n = 0;
