@@ -335,6 +335,14 @@ class SparkRuntime(_HadoopFamily):
         env["HADOOP_CONF_DIR"] = "$RUNTIME_PATH/hadoop/etc/hadoop"
         if rc.get("hive_metastore_uri"):
             env["SPARK_METASTORE_URI"] = str(rc["hive_metastore_uri"])
+        # SQL optimizations (runtime/hadoop/spark_optimizations.py) and user properties
+        # (runtime.spark.config), rendered into spark-defaults.conf on every node
+        from cloudtik_amd.runtime.hadoop.spark_optimizations import render_properties, spark_optimization_properties
+        opt = spark_optimization_properties(self.spec.version, rc.get("optimizations"),
+                                            bool(rc.get("optimized_build", False)))
+        lines = [ln for ln in render_properties(opt).split("\n") if ln]
+        lines += [f"{k:<38} {v}" for k, v in (rc.get("config") or {}).items()]
+        env["SPARK_EXTRA_PROPERTIES"] = ";;".join(lines)     # one line in the exported environment
         return env
 
     def conf_values(self, facts, env):
@@ -349,7 +357,8 @@ class SparkRuntime(_HadoopFamily):
                 "spark.sql.warehouse.dir": f"{base}/spark-warehouse",
                 "spark.hadoop.hive.metastore.properties":
                     (f"spark.hadoop.hive.metastore.uris        {ms}\nspark.sql.catalogImplementation        hive"
-                     if ms else "")}
+                     if ms else ""),
+                "spark.extra.properties": "\n".join(env.get("SPARK_EXTRA_PROPERTIES", "").split(";;"))}
 
     def start_steps(self, head):
         if not head:

@@ -77,7 +77,8 @@ RUNTIMES: Dict[str, Dict[str, Any]] = {
     "ray": dict(scaling="o"),
     "redis": dict(port="port", cluster_mode={"enum": ["none", "replication", "sharding"]}, password="s",
                   health_check_port="port", replication="o", sharding="o"),
-    "spark": dict(_METASTORE, config="o", spark_executor_resource="o"),                          # + sizing
+    "spark": dict(_METASTORE, config="o", spark_executor_resource="o",                           # + sizing
+                  optimizations={"type": ["object", "array", "string", "boolean"]}, optimized_build="b"),  # +
     "sshserver": dict(port="port"),
     "trino": dict(_METASTORE, catalogs="o"),
     "yarn": dict(scaling={"$ref": "#/definitions/yarn_scaling"}, yarn_resource_memory_ratio="n",
