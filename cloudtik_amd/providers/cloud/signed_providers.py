@@ -98,7 +98,13 @@ def _tag_params(tags: Dict[str, str]) -> Dict[str, str]:
 class AliyunNodeProvider(NodeProvider):
     """ECS instances as nodes; node id = instance id; tags = ECS tags (at most 20 per
     DescribeInstances filter, so the cluster-name tag filters server-side and the rest are
-    checked on the returned tags)."""
+    checked on the returned tags).
+
+    Stopped-node caching (``cache_stopped_nodes``, default true as in the reference
+    aliyun node_provider.py:50,213,357): terminating STOPS pay-as-you-go instances
+    (``StopInstances`` in StopCharging mode) and deletes spot ones; a launch first restarts
+    (``StartInstances``) stopped instances of the same cluster, node kind, node type and
+    launch hash, re-tagged with the new launch's tags, and runs only the remainder."""
 
     def __init__(self, provider_config, cluster_name, transport=None):
         super().__init__(provider_config, cluster_name)
@@ -108,6 +114,7 @@ class AliyunNodeProvider(NodeProvider):
             transport = aliyun_transport(provider_config.get("endpoint", f"ecs.{self.region}.aliyuncs.com"), ak, sk)
         self._call = transport or provider_config["_transport"]
         self._cache: Dict[str, Dict[str, Any]] = {}
+        self.cache_stopped_nodes = bool(provider_config.get("cache_stopped_nodes", True))
 
     @staticmethod
     def _tags_of(inst) -> Dict[str, str]:
@@ -160,8 +167,45 @@ class AliyunNodeProvider(NodeProvider):
         ips = (n.get("PublicIpAddress") or {}).get("IpAddress") or []
         return ips[0] if ips else None
 
+    def _reuse_stopped(self, tags, count) -> Dict[str, Any]:
+        """Restart up to ``count`` stopped instances launched from the same configuration."""
+        keys = (T.CLOUDTIK_TAG_CLUSTER_NAME, T.CLOUDTIK_TAG_NODE_KIND, T.CLOUDTIK_TAG_LAUNCH_CONFIG,
+                T.CLOUDTIK_TAG_USER_NODE_TYPE)
+        want = {k: tags[k] for k in keys if k in tags}
+        insts = self._describe(dict(_tag_params(want), Status="Stopped"))
+        found = sorted((i for i in insts if i.get("Status") == "Stopped"
+                        and all(self._tags_of(i).get(k) == v for k, v in want.items())),
+                       key=lambda i: i["InstanceId"])[:count]
+        if not found:
+            return {}
+        ids = [i["InstanceId"] for i in found]
+        self._call("StartInstances", dict(_indexed("InstanceId", ids), RegionId=self.region))
+        self._call("TagResources", dict(_tag_params({k: str(v) for k, v in tags.items()}),
+                                        RegionId=self.region, ResourceType="instance",
+                                        **_indexed("ResourceId", ids)))
+        out = {}
+        for inst in found:
+            cur = self._tags_of(inst)
+            cur.update({k: str(v) for k, v in tags.items()})
+            inst = dict(inst, Status="Starting",
+                        Tags={"Tag": [{"TagKey": k, "TagValue": v} for k, v in cur.items()]})
+            self._cache[inst["InstanceId"]] = inst
+            out[inst["InstanceId"]] = inst
+        return out
+
     def create_node(self, node_config, tags, count):
         tags = dict(tags, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name})
+        reused: Dict[str, Any] = {}
+        if self.cache_stopped_nodes:
+            reused = self._reuse_stopped(tags, count)
+            count -= len(reused)
+            if count <= 0:
+                return reused
+        out = self._run(node_config, tags, count)
+        out.update(reused)
+        return out
+
+    def _run(self, node_config, tags, count):
         params: Dict[str, Any] = {"RegionId": self.region, "Amount": count,
                                   "InstanceName": f"{self.cluster_name}-{tags.get(T.CLOUDTIK_TAG_NODE_KIND, 'node')}"}
         for key in ("InstanceType", "ImageId", "SecurityGroupId", "VSwitchId", "ZoneId", "KeyPairName",
@@ -185,11 +229,23 @@ class AliyunNodeProvider(NodeProvider):
         self.terminate_nodes([node_id])
 
     def terminate_nodes(self, node_ids: List[str]):
-        for i in range(0, len(node_ids), 100):  # DeleteInstances takes at most 100 ids
-            chunk = node_ids[i:i + 100]
-            self._call("DeleteInstances", dict(_indexed("InstanceId", chunk), RegionId=self.region, Force="true"))
-            for nid in chunk:
-                self._cache.pop(nid, None)
+        if not node_ids:
+            return
+        delete, stop = list(node_ids), []
+        if self.cache_stopped_nodes:
+            # spot instances are reclaimed by the cloud when stopped: those are deleted
+            spot = {n for n in node_ids
+                    if self._node(n).get("SpotStrategy", "NoSpot") not in ("NoSpot", "")}
+            stop = [n for n in node_ids if n not in spot]
+            delete = [n for n in node_ids if n in spot]
+        for i in range(0, len(stop), 100):     # StopInstances / DeleteInstances take at most 100 ids
+            self._call("StopInstances", dict(_indexed("InstanceId", stop[i:i + 100]), RegionId=self.region,
+                                             StoppedMode="StopCharging"))
+        for i in range(0, len(delete), 100):
+            self._call("DeleteInstances", dict(_indexed("InstanceId", delete[i:i + 100]), RegionId=self.region,
+                                               Force="true"))
+        for nid in node_ids:
+            self._cache.pop(nid, None)
 
 
 # -------------------------------------------------------------------------- Huawei Cloud
@@ -241,6 +297,7 @@ class HuaweiCloudNodeProvider(NodeProvider):
             transport = huawei_transport(ak, sk)
         self._call = transport or provider_config["_transport"]
         self._cache: Dict[str, Dict[str, Any]] = {}
+        self.cache_stopped_nodes = bool(provider_config.get("cache_stopped_nodes", True))
 
     def _url(self, path: str, version: str = "v1") -> str:
         host = self.provider_config.get("endpoint", f"ecs.{self.region}.myhuaweicloud.com")

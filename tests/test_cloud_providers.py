@@ -245,14 +245,27 @@ class FakeAliyunECS:
                 sel = [x for x in sel if x["InstanceId"] in want]
             sel = [x for x in sel if all({t["TagKey"]: t["TagValue"] for t in x["Tags"]["Tag"]}.get(k) == v
                                          for k, v in tags.items())]
+            if "Status" in params:
+                sel = [x for x in sel if x["Status"] == params["Status"]]
             ps, pn = int(params["PageSize"]), int(params["PageNumber"])
             return {"Instances": {"Instance": sel[(pn - 1) * ps:pn * ps]}, "TotalCount": len(sel)}
         if action == "TagResources":
             assert params["ResourceType"] == "instance"
-            inst = self.inst[params["ResourceId.1"]]
-            cur = {t["TagKey"]: t["TagValue"] for t in inst["Tags"]["Tag"]}
-            cur.update(tags)
-            inst["Tags"]["Tag"] = [{"TagKey": k, "TagValue": v} for k, v in cur.items()]
+            for iid in self._indexed(params, "ResourceId"):
+                inst = self.inst[iid]
+                cur = {t["TagKey"]: t["TagValue"] for t in inst["Tags"]["Tag"]}
+                cur.update(tags)
+                inst["Tags"]["Tag"] = [{"TagKey": k, "TagValue": v} for k, v in cur.items()]
+            return {}
+        if action == "StopInstances":
+            assert params["StoppedMode"] == "StopCharging"
+            for iid in self._indexed(params, "InstanceId"):
+                self.inst[iid]["Status"] = "Stopped"
+            return {}
+        if action == "StartInstances":
+            for iid in self._indexed(params, "InstanceId"):
+                assert self.inst[iid]["Status"] == "Stopped"
+                self.inst[iid]["Status"] = "Starting"
             return {}
         if action == "DeleteInstances":
             assert params["Force"] == "true"
@@ -281,6 +294,34 @@ def test_aliyun_provider_contract():
     p.terminate_nodes(list(made))
     assert p.non_terminated_nodes({}) == [] and len(other.non_terminated_nodes({})) == 1
     assert p.is_terminated(a)
+
+
+def test_aliyun_stopped_node_caching():
+    """Reference aliyun node_provider.py:213,357: terminate stops, launch restarts matching
+    stopped instances first (same node type + launch hash), spot instances are deleted."""
+    api = FakeAliyunECS()
+    p = AliyunNodeProvider({"region": "cn-hangzhou", "_transport": api}, "c1")
+    wt = {T.CLOUDTIK_TAG_NODE_KIND: "worker", T.CLOUDTIK_TAG_USER_NODE_TYPE: "gpu",
+          T.CLOUDTIK_TAG_LAUNCH_CONFIG: "h1"}
+    made = sorted(p.create_node({"InstanceType": "ecs.gn8"}, wt, 3))
+    api.inst[made[2]]["SpotStrategy"] = "SpotAsPriceGo"
+    p.terminate_nodes(made)
+    assert api.inst[made[0]]["Status"] == api.inst[made[1]]["Status"] == "Stopped"
+    assert made[2] not in api.inst                                  # spot: deleted
+    assert p.non_terminated_nodes({}) == []
+    # a different launch hash does not reuse them
+    other = p.create_node({"InstanceType": "ecs.gn8"}, dict(wt, **{T.CLOUDTIK_TAG_LAUNCH_CONFIG: "h2"}), 1)
+    assert not set(other) & set(made)
+    # same configuration: both stopped ones restart, re-tagged, one more is run
+    again = p.create_node({"InstanceType": "ecs.gn8"}, dict(wt, **{T.CLOUDTIK_TAG_NODE_STATUS: "pending"}), 3)
+    assert len(again) == 3 and set(made[:2]) <= set(again)
+    assert all(api.inst[i]["Status"] == "Starting" for i in made[:2])
+    assert p.node_tags(made[0])[T.CLOUDTIK_TAG_NODE_STATUS] == "pending"
+    assert sum(1 for a, _ in api.calls if a == "RunInstances") == 3
+    # caching off: terminate deletes
+    q = AliyunNodeProvider({"region": "cn-hangzhou", "_transport": api, "cache_stopped_nodes": False}, "c1")
+    q.terminate_nodes(list(again))
+    assert not set(again) & set(api.inst)
 
 
 class FakeHuaweiECS:
