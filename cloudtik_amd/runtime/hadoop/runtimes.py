@@ -14,6 +14,7 @@ import os
 from typing import Any, Dict, List, Optional
 
 from cloudtik_amd.runtime.catalog import SPEC_BY_NAME, CatalogRuntime
+from cloudtik_amd.runtime.hadoop import cloud_storage
 from cloudtik_amd.runtime.common.runtime_base import render_conf_file
 
 CONF_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conf")
@@ -174,10 +175,25 @@ def _proxyuser(user: str) -> str:
                      for k in ("hosts", "groups"))
 
 
+def _credential_file(facts) -> str:
+    return os.path.join(facts["home"], "etc", "hadoop", cloud_storage.CREDENTIAL_STORE)
+
+
 def _core_values(facts, env, default_fs: str) -> Dict[str, Any]:
+    props, secrets = cloud_storage.cloud_storage_conf(env)
     return {"fs.default.name": default_fs,
             "hadoop.tmp.dir": os.path.join(facts["home"], "tmp"),
-            "hadoop.proxyuser.properties": _proxyuser(facts["user"])}
+            "hadoop.proxyuser.properties": _proxyuser(facts["user"]),
+            "cloud.storage.properties": cloud_storage.properties_xml(
+                props, _credential_file(facts) if secrets else "")}
+
+
+def _credential_steps(runtime, head) -> List[str]:
+    """Secrets of the cloud storage connector into the JCEKS store core-site points at."""
+    env = runtime.node_env(head)
+    _, secrets = cloud_storage.cloud_storage_conf(env)
+    facts = runtime.node_facts(head, env)
+    return cloud_storage.credential_commands(secrets, facts["home"], _credential_file(facts))
 
 
 class HadoopRuntime(_HadoopFamily):
@@ -187,15 +203,20 @@ class HadoopRuntime(_HadoopFamily):
     templates = {"core-site.xml": "core-site.xml"}
 
     def conf_values(self, facts, env):
-        fs = env.get("HADOOP_DEFAULT_FS") or env.get("HDFS_NAMENODE_URI") or f"file://{facts['home']}/data"
+        fs = (env.get("HADOOP_DEFAULT_FS") or env.get("HDFS_NAMENODE_URI")
+              or cloud_storage.cloud_storage_uri(env) or f"file://{facts['home']}/data")
         return _core_values(facts, env, fs)
 
     def with_environment_variables(self, config, provider, node_id):
         env = super().with_environment_variables(config, provider, node_id)
+        env.update(cloud_storage.export_cloud_storage_env((config or {}).get("provider", {})))
         rc = (config or {}).get("runtime", {}).get("hadoop", {}) or {}
         if rc.get("default_storage"):
             env["HADOOP_DEFAULT_FS"] = str(rc["default_storage"])
         return env
+
+    def configure_steps(self, head):
+        return super().configure_steps(head) + _credential_steps(self, head)
 
 
 class HdfsRuntime(_HadoopFamily):
@@ -215,6 +236,7 @@ class HdfsRuntime(_HadoopFamily):
 
     def with_environment_variables(self, config, provider, node_id):
         env = super().with_environment_variables(config, provider, node_id)
+        env.update(cloud_storage.export_cloud_storage_env((config or {}).get("provider", {})))
         rc = (config or {}).get("runtime", {}).get("hdfs", {}) or {}
         env["HDFS_DFS_REPLICATION"] = str(rc.get("dfs_replication", 1))
         env["HDFS_DFS_BLOCKSIZE"] = str(rc.get("dfs_blocksize", 268435456))
@@ -235,6 +257,9 @@ class HdfsRuntime(_HadoopFamily):
             "dfs.namenode.http-address": f"{head}:{HDFS_HTTP_PORT}",
         })
         return vals
+
+    def configure_steps(self, head):
+        return super().configure_steps(head) + _credential_steps(self, head)
 
     def start_steps(self, head):
         if not head:

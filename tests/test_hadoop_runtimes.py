@@ -171,3 +171,104 @@ def test_yarn_job_waiter_until_idle():
     with pytest.raises(TimeoutError):
         YarnJobWaiter({}, fetch=lambda p: {"clusterMetrics": {"appsPending": 1, "appsRunning": 0}},
                       interval=0).wait_for_completion("n", "cmd", timeout=0)
+
+
+# ---------------------------------------------------------------- cloud storage in core-site
+from cloudtik_amd.runtime.hadoop import HadoopRuntime  # noqa: E402
+from cloudtik_amd.runtime.hadoop import cloud_storage as cs  # noqa: E402
+
+
+def _with_storage(provider):
+    cfg = _cluster(types=("hadoop",))
+    cfg["provider"] = provider
+    return cfg
+
+
+def test_hadoop_core_site_aws_keys_go_to_credential_store(node_env, monkeypatch):
+    """Reference hadoop-cloud-credential.sh update_credential_config_for_aws: the access key
+    in core-site, the secret only in the JCEKS store core-site points at."""
+    cfg = _with_storage({"type": "aws", "storage": {"aws_s3_storage": {
+        "s3.bucket": "b1", "s3.access.key.id": "AKIA1", "s3.secret.access.key": "s3cr3t"}}})
+    rt = HadoopRuntime({})
+    _export(rt, cfg, monkeypatch, node_env)
+    path = rt.render(head=True)["core-site.xml"]
+    core = _props(path)
+    assert core["fs.defaultFS"] == "s3a://b1"
+    assert core["fs.s3a.access.key"] == "AKIA1"
+    assert core["hadoop.security.credential.provider.path"].startswith("jceks://file@" + str(node_env))
+    assert "s3cr3t" not in open(path).read()
+    steps = rt.configure_steps(True)
+    assert any("credential create fs.s3a.secret.key -value s3cr3t" in s for s in steps)
+
+
+def test_hadoop_core_site_instance_identities(node_env, monkeypatch):
+    # no keys: instance profile, or web identity on EKS
+    props, secrets = cs.cloud_storage_conf({"AWS_CLOUD_STORAGE": "true"})
+    assert props["fs.s3a.aws.credentials.provider"].endswith("InstanceProfileCredentialsProvider") and not secrets
+    props, _ = cs.cloud_storage_conf({"AWS_CLOUD_STORAGE": "true", "AWS_WEB_IDENTITY": "true"})
+    assert props["fs.s3a.aws.credentials.provider"].endswith("WebIdentityTokenCredentialsProvider")
+
+
+def test_azure_workload_identity_token_provider(node_env, monkeypatch):
+    """N7 patch 0001: on AKS the projected pod identity feeds WorkloadIdentityTokenProvider
+    (tenant, client id, authority, federated token file), all via the credential store."""
+    env = cs.export_cloud_storage_env({"type": "azure", "tenant_id": "t0", "storage": {"azure_cloud_storage": {
+        "azure.storage.type": "datalake", "azure.storage.account": "acct", "azure.container": "c"}}})
+    assert cs.cloud_storage_uri(env) == "abfs://c@acct.dfs.core.windows.net"
+    props, secrets = cs.cloud_storage_conf(env)
+    assert props["fs.azure.account.oauth.provider.type"].endswith(".MsiTokenProvider")
+    assert secrets == {"fs.azure.account.oauth2.msi.tenant": "t0"}
+    env.update(AZURE_WORKLOAD_IDENTITY="true", AZURE_TENANT_ID="t1", AZURE_CLIENT_ID="cid",
+               AZURE_FEDERATED_TOKEN_FILE="/var/run/secrets/azure/tokens/azure-identity-token",
+               AZURE_AUTHORITY_HOST="https://login.microsoftonline.com/")
+    props, secrets = cs.cloud_storage_conf(env)
+    assert props["fs.azure.account.auth.type"] == "OAuth"
+    assert props["fs.azure.account.oauth.provider.type"] == \
+        "org.apache.hadoop.fs.azurebfs.oauth2.WorkloadIdentityTokenProvider"
+    assert secrets["fs.azure.account.oauth2.msi.tenant"] == "t1"
+    assert secrets["fs.azure.account.oauth2.client.id"] == "cid"
+    assert secrets["fs.azure.account.oauth2.token.file"].endswith("azure-identity-token")
+    assert "fs.azure.account.oauth2.msi.authority" in secrets
+    # an account key wins over identities
+    props, secrets = cs.cloud_storage_conf(dict(env, AZURE_ACCOUNT_KEY="k=="))
+    assert props["fs.azure.account.auth.type"] == "SharedKey"
+    assert secrets == {"fs.azure.account.key.acct.dfs.core.windows.net": "k=="}
+
+
+def test_aliyun_ecs_ram_role_and_huawei_agency(node_env, monkeypatch):
+    """N7 patch 0002: without OSS keys the ECS RAM role provider reads the role name from
+    fs.oss.ecs.ramRoleName; Huawei Cloud uses the ECS agency provider."""
+    env = cs.export_cloud_storage_env({"type": "aliyun", "region": "cn-hangzhou",
+                                       "storage": {"aliyun_oss_storage": {"oss.bucket": "ob"}}})
+    env["ALIYUN_ECS_RAM_ROLE_NAME"] = "cloudtik-worker-role"
+    props, secrets = cs.cloud_storage_conf(env)
+    assert props["fs.oss.credentials.provider"].endswith("AliyunEcsRamRoleCredentialsProvider")
+    assert props["fs.oss.endpoint"] == "oss-cn-hangzhou-internal.aliyuncs.com"
+    assert secrets == {"fs.oss.ecs.ramRoleName": "cloudtik-worker-role"}
+    assert cs.cloud_storage_uri(env) == "oss://ob"
+    keyed = dict(env, ALIYUN_OSS_ACCESS_KEY_ID="id", ALIYUN_OSS_ACCESS_KEY_SECRET="sk")
+    props, secrets = cs.cloud_storage_conf(keyed)
+    assert "fs.oss.credentials.provider" not in props and secrets["fs.oss.accessKeySecret"] == "sk"
+    hw = cs.export_cloud_storage_env({"type": "huaweicloud", "region": "cn-north-4",
+                                      "storage": {"huaweicloud_obs_storage": {"obs.bucket": "hb"}}})
+    props, secrets = cs.cloud_storage_conf(hw)
+    assert props["fs.obs.security.provider"] == "com.obs.services.EcsObsCredentialsProvider"
+    assert props["fs.obs.endpoint"] == "obs.cn-north-4.myhuaweicloud.com" and not secrets
+    # no cloud storage: nothing rendered, no credential steps
+    rt = HadoopRuntime({})
+    _export(rt, _cluster(types=("hadoop",)), monkeypatch, node_env)
+    core = _props(rt.render(head=True)["core-site.xml"])
+    assert "hadoop.security.credential.provider.path" not in core
+    assert not any("credential create" in s for s in rt.configure_steps(True))
+
+
+def test_kubernetes_cloud_provider_identities():
+    env = cs.export_cloud_storage_env({"type": "kubernetes", "cloud_provider": {
+        "type": "azure", "storage": {"azure_cloud_storage": {"azure.storage.account": "a", "azure.container": "c"}}}})
+    assert env["AZURE_WORKLOAD_IDENTITY"] == "true" and cs.cloud_storage_kind(env) == "azure"
+    props, _ = cs.cloud_storage_conf(dict(env, AZURE_CLIENT_ID="x"))
+    assert props["fs.azure.account.oauth.provider.type"].endswith("WorkloadIdentityTokenProvider")
+    env = cs.export_cloud_storage_env({"type": "kubernetes", "cloud_provider": {
+        "type": "aws", "storage": {"aws_s3_storage": {"s3.bucket": "b"}}}})
+    props, _ = cs.cloud_storage_conf(env)
+    assert props["fs.s3a.aws.credentials.provider"].endswith("WebIdentityTokenCredentialsProvider")
