@@ -452,7 +452,9 @@ def timed(step, args, rank, world, device, audit=False):
     sync()
     if rank == 0:
         print(f"[bench] warm-up {args.warmup} step(s): {time.perf_counter() - tw:.1f}s", file=sys.stderr)
-    info = kernel_audit(step, device) if audit else {}
+    # nothing may sit between warm-up and the timed loop: the profiler-based kernel audit
+    # runs AFTER the timed region (round 3: a torch.profiler session placed here left one
+    # timed ResNet step blocked ~4.7 s on the host on a fresh box)
     barrier()
     sync()
     cuda = device.type == "cuda"
@@ -485,10 +487,14 @@ def timed(step, args, rank, world, device, audit=False):
         out = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(out, t)
         per_rank = [float(o.item()) for o in out]
+    info = {}
     if host:
         # a host issue time close to the GPU step time means the step is launch / host bound
-        info = dict(info or {}, host_issue_ms_mean=round(sum(host) / len(host), 3))
-    return max(per_rank), per_rank, float(loss.detach().float().item()), step_ms, info
+        info = dict(host_issue_ms_mean=round(sum(host) / len(host), 3), host_ms=[round(h, 3) for h in host])
+    loss_v = float(loss.detach().float().item())
+    if audit:
+        info.update(kernel_audit(step, device))
+    return max(per_rank), per_rank, loss_v, step_ms, info
 
 
 def mean_ci(xs):
@@ -508,10 +514,12 @@ def run_one(build, args, rank, world, device, kind):
     elapsed, per_rank, loss, step_ms, audit = timed(step, args, rank, world, device,
                                                     audit=info["unit"] == "images/s")
     host_ms = audit.pop("host_issue_ms_mean", None) if audit else None
+    host_arr = audit.pop("host_ms", None) if audit else None
     if audit and rank == 0:
         print(f"[bench] {info['model']} kernel audit (one untimed step): {json.dumps(audit)}", file=sys.stderr)
     plan = info.pop("plan", None)
     info["host_issue_ms"] = host_ms
+    info["host_ms"] = host_arr
     close()
     del step
     gc.collect()
@@ -603,6 +611,7 @@ def main():
                "value_mean_per_step": head["rate_mean"], "value_ci95": head["rate_ci95"],
                "bucket_plan": head["plan"],
                "host_issue_ms_per_step": head.get("host_issue_ms"),
+               "step_ms": head["step_ms"], "host_ms": head.get("host_ms"),
                "env": {k: envinfo.get(k) for k in ("gpu", "rccl", "nccl_env", "rank0_cpus", "tunableop",
                                                    "distinct_devices", "world_size_seen_by_collective")
                        if envinfo.get(k) is not None},
@@ -624,6 +633,7 @@ def main():
             out[f"{key}_value_mean_per_step"], out[f"{key}_value_ci95"] = r["rate_mean"], r["rate_ci95"]
             out[f"{key}_bucket_plan"] = r["plan"]
             out[f"{key}_host_issue_ms_per_step"] = r.get("host_issue_ms")
+            out[f"{key}_step_ms"], out[f"{key}_host_ms"] = r["step_ms"], r.get("host_ms")
             if "hip_graph" in r:
                 out[f"{key}_hip_graph"] = r["hip_graph"]
             if r.get("audit"):

@@ -366,6 +366,7 @@ class DockerCommandExecutor(CommandExecutor):
         self.initialized = False
         self.home_dir: Optional[str] = None
         self.bind_mounts: Dict[str, str] = {}
+        self._image_homes: Dict[str, str] = {}
 
     # ------------------------------------------------------------------ helpers
     def _host(self, cmd, with_output=False, silent=True):
@@ -382,12 +383,30 @@ class DockerCommandExecutor(CommandExecutor):
         out = self._out(f"{self.docker_cmd} inspect -f '{{{{.State.Running}}}}' {self.container_name} || true")
         return "true" in out.lower() and "no such object" not in out.lower()
 
+    def image_home(self, image: str) -> str:
+        """$HOME of the image's default user, read once per image BEFORE the container runs:
+        ``~/`` file mounts are bind-mounted there (an image whose user is not root, e.g. the
+        reference base image's /home/cloudtik, would otherwise get them under /root)."""
+        if image not in self._image_homes:
+            out = self._out(f"{self.docker_cmd} run --rm --entrypoint printenv {image} HOME || true")
+            lines = [ln.strip() for ln in out.splitlines() if ln.strip().startswith("/")]
+            self._image_homes[image] = lines[-1] if lines else "/root"
+        return self._image_homes[image]
+
     def expand_user(self, path: str) -> str:
         if path.startswith("~"):
             if self.home_dir is None:
                 self.home_dir = self._out(f"{self.docker_cmd} exec {self.container_name} printenv HOME").strip() \
                     or "/root"
             return self.home_dir + path[1:]
+        return path
+
+    @staticmethod
+    def _under_home(path: str, home: str) -> str:
+        if path == "~":
+            return home
+        if path.startswith("~/"):
+            return home.rstrip("/") + "/" + path[2:]
         return path
 
     def host_mount_path(self, remote: str) -> str:
@@ -405,7 +424,9 @@ class DockerCommandExecutor(CommandExecutor):
             active = {m["Destination"].strip("/") for m in json.loads(raw or "[]")}
         except (ValueError, KeyError, TypeError):
             return False
-        wanted = {self.expand_user(r).strip("/") for r in mounts}
+        # where THIS image's docker run would bind them (the same home as the -v targets)
+        home = self.image_home(image) if any(r.startswith("~") for r in mounts) else None
+        wanted = {self._under_home(r, home).strip("/") for r in mounts}
         missing = wanted - active
         if missing:
             logger.warning("container %s lacks file mounts %s: restarting it", self.container_name, sorted(missing))
@@ -511,14 +532,15 @@ class DockerCommandExecutor(CommandExecutor):
             if self.docker_config.get("memory"):
                 opts.append(f"--memory={self.docker_config['memory']}")
             opts += self.rocm_run_options(as_head) + self.shm_run_options(shared_memory_ratio)
-            binds = " ".join(f"-v {shlex.quote(self.host_mount_path(r))}:{shlex.quote(r.replace('~/', '/root/'))}"
+            home = self.image_home(image) if any(r.startswith("~") for r in mounts) else None
+            binds = " ".join(f"-v {shlex.quote(self.host_mount_path(r))}:{shlex.quote(self._under_home(r, home))}"
                              for r in sorted(mounts))
             labels = " ".join(f"-l {shlex.quote(f'{k}={v}')}" for k, v in
                               (self.docker_config.get("labels") or {}).items())
             self._host(f"{self.docker_cmd} run --rm --name {self.container_name} -d -it {binds} {labels} "
                        f"-e CLOUDTIK_CLUSTER_NAME={shlex.quote(self.cluster_name)} {' '.join(opts)} {image} bash")
             docker_run = True
-            self.home_dir = None
+            self.home_dir = self._image_homes.get(image)
         self.initialized = True
         # bootstrap files: copied in explicitly (see BOOTSTRAP_MOUNTS)
         for b in BOOTSTRAP_MOUNTS:

@@ -183,16 +183,19 @@ class NodeUpdater:
         if runtime_unchanged and not self.for_recovery and not self.restart_only:
             return  # only file contents changed
         self._set_status(T.STATUS_SETTING_UP)
-        if not self.restart_only or self.for_recovery:
+        if not runtime_unchanged or self.for_recovery:
+            # a changed runtime hash always re-runs the initialization commands and starts the
+            # container (after the files are synced); restart_only drops only the setup /
+            # bootstrap commands (reference node_updater.py:467-537)
             self._stage("initialization")
             self.exec_commands("initialization", self.initialization_commands, env)
-            # container runtime: started here, after the files are synced
             self.executor.run_init(as_head=self.is_head_node, file_mounts=self.file_mounts,
                                    shared_memory_ratio=self.shared_memory_ratio, sync_run_yet=True)
-            self._stage("setup")
-            self.exec_commands("setup", self.setup_commands, env)
-            self._stage("bootstrap")
-            self.exec_commands("bootstrap", self.bootstrap_commands, env)
+            if not self.restart_only or self.for_recovery:
+                self._stage("setup")
+                self.exec_commands("setup", self.setup_commands, env)
+                self._stage("bootstrap")
+                self.exec_commands("bootstrap", self.bootstrap_commands, env)
         self._stage("start")
         self.exec_commands("start", self.start_commands, env)
 

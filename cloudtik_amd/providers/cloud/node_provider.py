@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import importlib
 import threading
+import time
 from typing import Any, Dict, List, Optional
 
 from cloudtik_amd.core import tags as T
@@ -27,6 +28,8 @@ def _require(module: str, provider: str):
 
 
 TAG_BATCH_DELAY = 1.0     # seconds set_node_tags waits to batch concurrent updates
+STOPPING_WAIT_S = 300.0   # how long a launch waits for a 'stopping' cached node to stop
+STOPPING_POLL_S = 5.0
 
 
 class AWSNodeProvider(NodeProvider):
@@ -189,7 +192,14 @@ class AWSNodeProvider(NodeProvider):
         found = []
         for res in self.ec2.describe_instances(Filters=filters).get("Reservations", []):
             found += res.get("Instances", [])
-        found = sorted(found, key=lambda i: i["InstanceId"])[:count]
+        # prefer instances that are already stopped; a 'stopping' one is usable only once
+        # EC2 reports it stopped (StartInstances on it fails with IncorrectInstanceState and
+        # would fail the whole scale-up; reference aws node_provider.py:280-287 waits too)
+        found = sorted(found, key=lambda i: (i["State"]["Name"] != "stopped", i["InstanceId"]))[:count]
+        stopping = [i["InstanceId"] for i in found if i["State"]["Name"] != "stopped"]
+        if stopping:
+            ready = self._wait_stopped(stopping)
+            found = [i for i in found if i["State"]["Name"] == "stopped" or i["InstanceId"] in ready]
         if not found:
             return {}
         ids = [i["InstanceId"] for i in found]
@@ -204,6 +214,28 @@ class AWSNodeProvider(NodeProvider):
             self._remember(inst)
             out[inst["InstanceId"]] = inst
         return out
+
+    def _wait_stopped(self, ids, timeout=None, poll=None):
+        """Poll until the given 'stopping' instances are 'stopped'; returns the ids that got
+        there within ``timeout`` (the rest are left alone and new instances are launched)."""
+        timeout = STOPPING_WAIT_S if timeout is None else timeout
+        poll = STOPPING_POLL_S if poll is None else poll
+        deadline = time.time() + timeout
+        pending = set(ids)
+        done = set()
+        while pending:
+            resp = self.ec2.describe_instances(InstanceIds=sorted(pending))
+            for res in resp.get("Reservations", []):
+                for inst in res.get("Instances", []):
+                    if inst["State"]["Name"] == "stopped":
+                        done.add(inst["InstanceId"])
+                    elif inst["State"]["Name"] != "stopping":      # terminated / started elsewhere
+                        pending.discard(inst["InstanceId"])
+            pending -= done
+            if not pending or time.time() >= deadline:
+                break
+            time.sleep(poll)
+        return done
 
     def create_node(self, node_config, tags, count):
         reused: Dict[str, Any] = {}

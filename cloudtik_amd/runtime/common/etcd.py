@@ -32,10 +32,10 @@ class EtcdClient:
         self.base = endpoint if endpoint.startswith("http") else f"http://{endpoint}"
         self.timeout = timeout
 
-    def _post(self, path: str, body: Dict[str, Any]) -> Dict[str, Any]:
+    def _post(self, path: str, body: Dict[str, Any], timeout: Optional[float] = None) -> Dict[str, Any]:
         req = urllib.request.Request(f"{self.base}/v3/{path}", data=json.dumps(body).encode(), method="POST",
                                      headers={"Content-Type": "application/json"})
-        with urllib.request.urlopen(req, timeout=self.timeout) as r:
+        with urllib.request.urlopen(req, timeout=timeout or self.timeout) as r:
             return json.loads(r.read() or b"{}")
 
     # ---------------------------------------------------------------- KV
@@ -45,8 +45,8 @@ class EtcdClient:
             body["lease"] = lease
         self._post("kv/put", body)
 
-    def get(self, key: str) -> Optional[bytes]:
-        kvs = self._post("kv/range", {"key": _b64(key)}).get("kvs") or []
+    def get(self, key: str, timeout: Optional[float] = None) -> Optional[bytes]:
+        kvs = self._post("kv/range", {"key": _b64(key)}, timeout=timeout).get("kvs") or []
         return _unb64(kvs[0].get("value")) if kvs else None
 
     def get_prefix(self, prefix: str) -> Dict[str, bytes]:
@@ -76,8 +76,8 @@ class EtcdClient:
     def lease_grant(self, ttl_s: int) -> str:
         return str(self._post("lease/grant", {"TTL": int(ttl_s)})["ID"])
 
-    def lease_keepalive(self, lease: str) -> bool:
-        r = self._post("lease/keepalive", {"ID": lease})
+    def lease_keepalive(self, lease: str, timeout: Optional[float] = None) -> bool:
+        r = self._post("lease/keepalive", {"ID": lease}, timeout=timeout)
         return int((r.get("result") or r).get("TTL", 0) or 0) > 0
 
     def lease_revoke(self, lease: str):
@@ -106,9 +106,9 @@ class EtcdLock:
                 return False
             time.sleep(poll)
 
-    def renew(self) -> bool:
-        return self.lease is not None and self.c.lease_keepalive(self.lease) and \
-            self.c.get(self.key) == self.owner_id.encode()
+    def renew(self, timeout: Optional[float] = None) -> bool:
+        return self.lease is not None and self.c.lease_keepalive(self.lease, timeout=timeout) and \
+            self.c.get(self.key, timeout=timeout) == self.owner_id.encode()
 
     def release(self) -> bool:
         ok = self.c.delete_if_value(self.key, self.owner_id)
@@ -131,47 +131,76 @@ class EtcdLock:
 
 class EtcdLeaderElection:
     """Leader election on an EtcdLock (same interface as runtime/common/consul.py
-    ``ConsulLeaderElection``: step / start / resign / is_leader / leader)."""
+    ``ConsulLeaderElection``: step / start / resign / is_leader / leader).
+
+    Leadership is time-bounded: the server starts a lease's TTL when it HANDLES a keepalive,
+    so the only safe local lower bound of the expiry is the time the keepalive was SENT.  A
+    leader therefore stops acting as leader at ``sent + ttl - margin``, where the margin
+    covers one loop poll plus the two RPC timeouts of a renew (keepalive + owner check), so
+    the demotion lands before the server can expire the lease and hand the lock to another
+    candidate -- even when an etcd call hangs (every call carries an explicit timeout, and
+    ``is_leader()`` checks the deadline itself instead of trusting the loop)."""
 
     def __init__(self, client: EtcdClient, name: str, candidate_id: Optional[str] = None, ttl_s: int = 10,
-                 on_elected=None, on_demoted=None):
+                 on_elected=None, on_demoted=None, clock=time.monotonic):
         self.lock = EtcdLock(client, f"leader/{name}", ttl_s, candidate_id)
         self.on_elected, self.on_demoted = on_elected, on_demoted
+        self.clock = clock
+        self.poll_s = max(0.05, ttl_s / 5)
+        self.rpc_timeout_s = max(0.05, ttl_s / 7)
+        self.margin_s = self.poll_s + 2 * self.rpc_timeout_s
         self._leader = False
-        self._last_renew = 0.0
+        self._last_renew = 0.0          # send time of the last renew / acquire that succeeded
         self._stop = threading.Event()
+        self._mu = threading.Lock()
         self._thread: Optional[threading.Thread] = None
 
     @property
     def candidate_id(self) -> str:
         return self.lock.owner_id
 
+    def deadline(self) -> float:
+        """Local time after which this node must no longer act as leader."""
+        return self._last_renew + self.lock.ttl_s - self.margin_s
+
     def is_leader(self) -> bool:
+        if self._leader and self.clock() >= self.deadline():
+            self._expire()
         return self._leader
 
     def leader(self) -> Optional[str]:
         return self.lock.owner()
 
-    def _set(self, leader: bool):
-        was, self._leader = self._leader, leader
-        if leader:
-            self._last_renew = time.monotonic()
+    def _set(self, leader: bool, sent: Optional[float] = None):
+        with self._mu:
+            was, self._leader = self._leader, leader
+            if leader and sent is not None:
+                self._last_renew = sent
         if leader and not was and self.on_elected:
             self.on_elected()
         if was and not leader and self.on_demoted:
             self.on_demoted()
 
+    def _expire(self):
+        """The lease may already be gone server-side: stop leading, re-acquire with a new lease."""
+        self.lock.lease = None
+        self._set(False)
+
     def step(self) -> bool:
-        self._set(self.lock.renew() if self._leader else self.lock.acquire(blocking=False))
+        if self._leader and self.clock() >= self.deadline():
+            self._expire()
+        sent = self.clock()
+        if self._leader:
+            ok = self.lock.renew(timeout=self.rpc_timeout_s)
+        else:
+            ok = self.lock.acquire(blocking=False)
+        self._set(ok, sent)
         return self._leader
 
     def _on_error(self):
-        """etcd unreachable.  The lease may expire on the server while we cannot renew it,
-        and another candidate then takes the lock: once the last successful renew is a lease
-        TTL old we stop acting as leader (never two leaders at once)."""
-        if self._leader and time.monotonic() - self._last_renew >= self.lock.ttl_s:
-            self.lock.lease = None          # expired server-side: re-acquire with a new lease
-            self._set(False)
+        """etcd unreachable: keep leading only until the send-time deadline."""
+        if self._leader and self.clock() >= self.deadline():
+            self._expire()
 
     def start(self):
         def loop():
@@ -180,7 +209,10 @@ class EtcdLeaderElection:
                     self.step()
                 except Exception:  # noqa: BLE001 - etcd briefly unreachable: retry
                     self._on_error()
-                self._stop.wait(max(0.05, self.lock.ttl_s / 3))
+                wait = self.poll_s
+                if self._leader:
+                    wait = min(wait, max(0.0, self.deadline() - self.clock()))
+                self._stop.wait(max(0.01, wait))
         self._thread = threading.Thread(target=loop, daemon=True)
         self._thread.start()
 

@@ -137,13 +137,26 @@ def cloud_storage_uri(env: Dict[str, Any]) -> str:
 
 def cloud_storage_conf(env: Dict[str, Any]) -> Tuple[Dict[str, str], Dict[str, str]]:
     """(core-site properties, credential-store secrets) for the node's cloud storage."""
+    props, secrets, _ = _storage_conf(env)
+    return props, secrets
+
+
+def cloud_storage_secret_vars(env: Dict[str, Any]) -> Dict[str, str]:
+    """credential-store alias -> NAME of the node environment variable holding its value
+    (the configure steps reference the variable, never the secret itself)."""
+    return _storage_conf(env)[2]
+
+
+def _storage_conf(env: Dict[str, Any]) -> Tuple[Dict[str, str], Dict[str, str], Dict[str, str]]:
     kind = cloud_storage_kind(env)
     props: Dict[str, str] = {}
     secrets: Dict[str, str] = {}
+    sources: Dict[str, str] = {}
 
     def secret(name, var):
         if env.get(var):
             secrets[name] = str(env[var])
+            sources[name] = var
 
     if kind == "aws":
         if env.get("AWS_S3_ACCESS_KEY_ID"):
@@ -178,16 +191,17 @@ def cloud_storage_conf(env: Dict[str, Any]) -> Tuple[Dict[str, str], Dict[str, s
             props["fs.azure.account.oauth.provider.type"] = _ABFS_OAUTH + (
                 "WorkloadIdentityTokenProvider" if workload else "MsiTokenProvider")
             tenant, client = env.get("AZURE_MANAGED_IDENTITY_TENANT_ID"), env.get("AZURE_MANAGED_IDENTITY_CLIENT_ID")
+            tenant_var, client_var = "AZURE_MANAGED_IDENTITY_TENANT_ID", "AZURE_MANAGED_IDENTITY_CLIENT_ID"
             if workload:
                 # the pod's projected identity (AKS workload identity webhook) wins
-                tenant = env.get("AZURE_TENANT_ID") or tenant
-                client = env.get("AZURE_CLIENT_ID") or client
+                if env.get("AZURE_TENANT_ID"):
+                    tenant_var = "AZURE_TENANT_ID"
+                if env.get("AZURE_CLIENT_ID"):
+                    client_var = "AZURE_CLIENT_ID"
                 secret("fs.azure.account.oauth2.msi.authority", "AZURE_AUTHORITY_HOST")
                 secret("fs.azure.account.oauth2.token.file", "AZURE_FEDERATED_TOKEN_FILE")
-            if tenant:
-                secrets["fs.azure.account.oauth2.msi.tenant"] = str(tenant)
-            if client:
-                secrets["fs.azure.account.oauth2.client.id"] = str(client)
+            secret("fs.azure.account.oauth2.msi.tenant", tenant_var)
+            secret("fs.azure.account.oauth2.client.id", client_var)
     elif kind == "aliyun":
         props["fs.oss.impl"] = "org.apache.hadoop.fs.aliyun.oss.AliyunOSSFileSystem"
         if env.get("ALIYUN_OSS_INTERNAL_ENDPOINT"):
@@ -206,7 +220,7 @@ def cloud_storage_conf(env: Dict[str, Any]) -> Tuple[Dict[str, str], Dict[str, s
             props["fs.obs.security.provider"] = "com.obs.services.EcsObsCredentialsProvider"
         secret("fs.obs.access.key", "HUAWEICLOUD_OBS_ACCESS_KEY")
         secret("fs.obs.secret.key", "HUAWEICLOUD_OBS_SECRET_KEY")
-    return props, secrets
+    return props, secrets, sources
 
 
 def properties_xml(props: Dict[str, str], credential_file: str = "") -> str:
@@ -218,13 +232,19 @@ def properties_xml(props: Dict[str, str], credential_file: str = "") -> str:
                      for k, v in items.items())
 
 
-def credential_commands(secrets: Dict[str, str], hadoop_home: str, credential_file: str) -> List[str]:
-    """``hadoop credential create`` per secret into a fresh store (rewritten every configure)."""
-    if not secrets:
+def credential_commands(secret_vars: Dict[str, str], hadoop_home: str, credential_file: str) -> List[str]:
+    """``hadoop credential create`` per secret into a fresh store (rewritten every configure).
+
+    ``secret_vars`` maps each alias to the NAME of the environment variable that holds it; the
+    commands expand ``"$VAR"`` when they run (the steps run with the node environment), so no
+    secret value appears in a step string, a failed step's error message or a log."""
+    if not secret_vars:
         return []
     store = f"jceks://file@{credential_file}"
     cmds = [f"rm -f {shlex.quote(credential_file)}"]
-    for name, value in secrets.items():
+    for name, var in secret_vars.items():
+        if not var.replace("_", "").isalnum():
+            raise ValueError(f"not an environment variable name: {var!r}")
         cmds.append(f"{shlex.quote(hadoop_home + '/bin/hadoop')} credential create {shlex.quote(name)} "
-                    f"-value {shlex.quote(value)} -provider {shlex.quote(store)} > /dev/null")
+                    f"-value \"${var}\" -provider {shlex.quote(store)} > /dev/null")
     return cmds

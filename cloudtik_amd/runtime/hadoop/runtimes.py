@@ -191,9 +191,9 @@ def _core_values(facts, env, default_fs: str) -> Dict[str, Any]:
 def _credential_steps(runtime, head) -> List[str]:
     """Secrets of the cloud storage connector into the JCEKS store core-site points at."""
     env = runtime.node_env(head)
-    _, secrets = cloud_storage.cloud_storage_conf(env)
+    secret_vars = cloud_storage.cloud_storage_secret_vars(env)
     facts = runtime.node_facts(head, env)
-    return cloud_storage.credential_commands(secrets, facts["home"], _credential_file(facts))
+    return cloud_storage.credential_commands(secret_vars, facts["home"], _credential_file(facts))
 
 
 class HadoopRuntime(_HadoopFamily):

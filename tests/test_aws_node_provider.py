@@ -154,3 +154,35 @@ def test_stopped_node_caching_reuses_matching_nodes():
     q = _provider(fake, cache_stopped_nodes=False)
     q.terminate_nodes([ids[1]])
     assert fake.instances[ids[1]]["State"]["Name"] == "terminated"
+
+
+def test_stopping_node_is_waited_for_before_start(monkeypatch):
+    """A cached node still 'stopping' is started only after EC2 reports it 'stopped'
+    (StartInstances on a stopping instance fails); one that never stops is skipped and a
+    new instance launched instead (reference aws node_provider.py:280-287)."""
+    monkeypatch.setattr(NP, "STOPPING_POLL_S", 0.01)
+    fake = FakeEC2()
+    p = _provider(fake)
+    tags = {T.CLOUDTIK_TAG_NODE_KIND: "worker", T.CLOUDTIK_TAG_LAUNCH_CONFIG: "h1",
+            T.CLOUDTIK_TAG_USER_NODE_TYPE: "gpu.8x"}
+    ids = sorted(p.create_node({"instance_type": "m5.large"}, dict(tags), 2))
+    p.terminate_nodes(ids)
+    fake.instances[ids[0]]["State"]["Name"] = "stopping"
+    fake.instances[ids[1]]["State"]["Name"] = "stopping"
+    polls = {"n": 0}
+    orig = fake.describe_instances
+
+    def describe(Filters=None, InstanceIds=None, NextToken=None):
+        if InstanceIds:
+            polls["n"] += 1
+            if polls["n"] == 3:                       # ids[0] finishes stopping on the 3rd poll
+                fake.instances[ids[0]]["State"]["Name"] = "stopped"
+        return orig(Filters=Filters, InstanceIds=InstanceIds, NextToken=NextToken)
+    fake.describe_instances = describe
+    monkeypatch.setattr(NP, "STOPPING_WAIT_S", 0.2)
+    n_before = fake.n
+    got = p.create_node({"instance_type": "m5.large"}, dict(tags), 2)
+    assert ids[0] in got and ids[1] not in got            # never started while stopping
+    assert fake.instances[ids[0]]["State"]["Name"] == "pending"
+    assert fake.instances[ids[1]]["State"]["Name"] == "stopping"
+    assert fake.n == n_before + 1 and len(got) == 2

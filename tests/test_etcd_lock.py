@@ -181,3 +181,44 @@ def test_leader_demotes_itself_when_etcd_unreachable(etcd):
     cut.clear()
     e1.resign()
     e2.resign()
+
+
+def test_demotion_deadline_uses_send_time_and_precedes_server_expiry():
+    """The renew's SEND time bounds the server-side lease start, so the leader must step
+    down at sent + ttl - margin, strictly before the server can expire the lease -- also
+    when the renew RPC itself is slow or hangs (fake clock, stub lock)."""
+    now = [100.0]
+
+    class StubLock:
+        ttl_s, owner_id, lease = 10, "n1", "L1"
+
+        def __init__(self):
+            self.calls = []
+
+        def acquire(self, blocking=True):
+            now[0] += 0.5                         # the acquire RPC takes 0.5 s
+            return True
+
+        def renew(self, timeout=None):
+            self.calls.append(timeout)
+            now[0] += 2.0                         # a slow keepalive round trip
+            return True
+
+        def owner(self):
+            return "n1"
+
+    e = EtcdLeaderElection.__new__(EtcdLeaderElection)
+    EtcdLeaderElection.__init__(e, EtcdClient("127.0.0.1:1"), "x", "n1", ttl_s=10, clock=lambda: now[0])
+    e.lock = StubLock()
+    sent = now[0]
+    assert e.step() and e._last_renew == sent            # the send time, not the reply time
+    sent = now[0]
+    assert e.step() and e._last_renew == sent
+    assert e.lock.calls == [e.rpc_timeout_s]              # renew carries an explicit timeout
+    server_expiry = sent + e.lock.ttl_s                    # earliest possible server-side expiry
+    # etcd now unreachable: the leader stays only until its deadline, before server expiry
+    assert e.deadline() < server_expiry - e.poll_s
+    now[0] = e.deadline() - 0.01
+    assert e.is_leader()
+    now[0] = e.deadline()
+    assert not e.is_leader() and e.lock.lease is None

@@ -198,7 +198,8 @@ def test_hadoop_core_site_aws_keys_go_to_credential_store(node_env, monkeypatch)
     assert core["hadoop.security.credential.provider.path"].startswith("jceks://file@" + str(node_env))
     assert "s3cr3t" not in open(path).read()
     steps = rt.configure_steps(True)
-    assert any("credential create fs.s3a.secret.key -value s3cr3t" in s for s in steps)
+    assert any('credential create fs.s3a.secret.key -value "$AWS_S3_SECRET_ACCESS_KEY"' in s for s in steps)
+    assert not any("s3cr3t" in s for s in steps)          # the value never enters a step string
 
 
 def test_hadoop_core_site_instance_identities(node_env, monkeypatch):

@@ -406,3 +406,60 @@ def test_docker_file_mounts_bind_mounted_and_pull_policy(state, tmp_path):
     cmds = runner.commands_for(w)
     assert u.exitcode == 0 and any(c.startswith("docker stop") for c in cmds) and any(
         c.startswith("docker run") for c in cmds)
+
+
+def test_docker_home_mounts_follow_image_user(state, tmp_path):
+    """'~/' file mounts land in the IMAGE user's home (a non-root image: /home/cloudtik), and
+    the drift check compares against the same place, so an up-to-date container is not
+    restarted on the next update (reference docker_command_executor.py reads $HOME first)."""
+    name = "sc-docker-home"
+    src = tmp_path / "cfg"
+    src.mkdir()
+
+    def mut(c):
+        _docker(c)
+        c["file_mounts"] = {"~/conf": str(src)}
+
+    cfg, provider, scaler = _setup(name, state, mut)
+    runner = provider.runner
+    runner.respond_to_call("--entrypoint printenv", ["/home/cloudtik"])
+    scaler.update()
+    (w,) = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    cmds = runner.commands_for(w)
+    run = [c for c in cmds if c.startswith("docker run") and "--name" in c][0]
+    assert f"-v /tmp/cloudtik_docker_mounts/{name}/conf:/home/cloudtik/conf" in run
+    assert "/root/conf" not in run
+    # the running container has the mount at /home/cloudtik/conf: no restart
+    runner.respond_to_call(".State.Running", ["true"])
+    runner.respond_to_call(".Config.Image", ["cloudtik/ai-rocm:latest"])
+    runner.respond_to_call("json .Mounts", ['[{"Destination": "/home/cloudtik/conf"}]'])
+    runner.clear_history()
+    from cloudtik_amd.core.cluster_utils import create_updater
+    u = create_updater(cfg, provider, w, is_head=False, head_ip="10.0.0.1", restart_only=True)
+    provider.set_node_tags(w, {T.CLOUDTIK_TAG_FILE_MOUNTS_CONTENTS: "changed"})
+    u.run()
+    cmds = runner.commands_for(w)
+    assert u.exitcode == 0 and not any(c.startswith("docker stop") for c in cmds)
+
+
+def test_restart_only_with_changed_runtime_hash_starts_container(state):
+    """restart_only drops only the setup commands: when the runtime hash changed and the
+    container is not running, the initialization commands and the docker run still happen
+    before the start commands (reference node_updater.py:467-537)."""
+    name = "sc-docker-restart-only"
+    cfg, provider, scaler = _setup(name, state, _docker)
+    runner = provider.runner
+    scaler.update()
+    (w,) = _workers(provider, name, T.STATUS_UP_TO_DATE)
+    provider.set_node_tags(w, {T.CLOUDTIK_TAG_RUNTIME_CONFIG: "old-hash"})
+    runner.respond_to_call(".State.Running", ["false"])
+    runner.clear_history()
+    from cloudtik_amd.core.cluster_utils import create_updater
+    u = create_updater(cfg, provider, w, is_head=False, head_ip="10.0.0.1", restart_only=True)
+    u.run()
+    cmds = runner.commands_for(w)
+    assert u.exitcode == 0
+    run = [i for i, c in enumerate(cmds) if c.startswith("docker run") and "--name" in c]
+    start = [i for i, c in enumerate(cmds) if "docker exec" in c and "node start" in c]
+    assert run and start and run[0] < start[0]
+    assert not any("docker exec" in c and "runtime install ai" in c for c in cmds)   # no setup
