@@ -279,7 +279,7 @@ def build_bert(args, rank, world, device, kind):
                 unit="tokens/s", items_per_step=B * S,
                 metric="bert_large_pretrain_tokens_per_sec" if kind in ("bert-large", "tiny")
                 else "bert_base_pretrain_tokens_per_sec",
-                optimizer="fused LAMB (HIP)", impl="native", plan=bucket_plan(ddp))
+                optimizer="fused LAMB (HIP)", impl="native", plan=bucket_plan(ddp), bucketer=ddp)
     return step, close, info
 
 
@@ -322,7 +322,7 @@ def build_resnet(args, rank, world, device, kind):
     info = dict(model="resnet50" if not tiny else "resnet-tiny", per_gpu_batch=B, seq_len=None,
                 unit="images/s", items_per_step=B, metric="resnet50_train_images_per_sec",
                 optimizer="fused SGD (HIP)", impl="native", image_size=R, plan=bucket_plan(ddp),
-                hip_graph=bool(graph))
+                hip_graph=bool(graph), bucketer=None if graph else ddp)
     return step, ddp.remove, info
 
 
@@ -431,7 +431,22 @@ def kernel_audit(step, device):
             "naive_conv_kernels": naive[:8]}
 
 
-def timed(step, args, rank, world, device, audit=False):
+def bucket_timeline(step, bucketer, device):
+    """One extra UNTIMED step with the bucketer's trace on: when each gradient bucket's
+    collective was issued relative to the end of backward (ms; negative = overlapped)."""
+    import torch
+    if bucketer is None or device.type != "cuda" or bucketer.world <= 1:
+        return None
+    bucketer.trace = True
+    try:
+        step()
+        torch.cuda.synchronize()
+        return [{"bucket": b, "bytes": n, "ms_vs_backward_end": t} for b, n, t in bucketer.timeline()]
+    finally:
+        bucketer.trace = False
+
+
+def timed(step, args, rank, world, device, audit=False, bucketer=None):
     """W warm-up steps, then K timed steps between barrier+sync brackets.  Returns
     (max elapsed over ranks, per-rank elapsed list, last loss, per-step ms, audit).
 
@@ -491,9 +506,19 @@ def timed(step, args, rank, world, device, audit=False):
     if host:
         # a host issue time close to the GPU step time means the step is launch / host bound
         info = dict(host_issue_ms_mean=round(sum(host) / len(host), 3), host_ms=[round(h, 3) for h in host])
+    if dist.is_initialized() and world > 1:
+        # every rank's per-step GPU times (the max over ranks is the headline; a straggler
+        # rank or step shows up here)
+        t = torch.tensor(step_ms, dtype=torch.float64, device=device)
+        outs = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        info["per_rank_step_ms"] = [[round(float(x), 3) for x in o.tolist()] for o in outs]
     loss_v = float(loss.detach().float().item())
     if audit:
         info.update(kernel_audit(step, device))
+    tl = bucket_timeline(step, bucketer, device)
+    if tl is not None:
+        info["bucket_timeline"] = tl
     return max(per_rank), per_rank, loss_v, step_ms, info
 
 
@@ -511,10 +536,14 @@ def run_one(build, args, rank, world, device, kind):
     import gc
     import torch
     step, close, info = build(args, rank, world, device, kind)
+    bucketer = info.pop("bucketer", None)
     elapsed, per_rank, loss, step_ms, audit = timed(step, args, rank, world, device,
-                                                    audit=info["unit"] == "images/s")
+                                                    audit=info["unit"] == "images/s", bucketer=bucketer)
+    del bucketer
     host_ms = audit.pop("host_issue_ms_mean", None) if audit else None
     host_arr = audit.pop("host_ms", None) if audit else None
+    info["per_rank_step_ms"] = audit.pop("per_rank_step_ms", None) if audit else None
+    info["bucket_timeline"] = audit.pop("bucket_timeline", None) if audit else None
     if audit and rank == 0:
         print(f"[bench] {info['model']} kernel audit (one untimed step): {json.dumps(audit)}", file=sys.stderr)
     plan = info.pop("plan", None)
@@ -612,6 +641,7 @@ def main():
                "bucket_plan": head["plan"],
                "host_issue_ms_per_step": head.get("host_issue_ms"),
                "step_ms": head["step_ms"], "host_ms": head.get("host_ms"),
+               "per_rank_step_ms": head.get("per_rank_step_ms"), "bucket_timeline": head.get("bucket_timeline"),
                "env": {k: envinfo.get(k) for k in ("gpu", "rccl", "nccl_env", "rank0_cpus", "tunableop",
                                                    "distinct_devices", "world_size_seen_by_collective")
                        if envinfo.get(k) is not None},
@@ -634,6 +664,10 @@ def main():
             out[f"{key}_bucket_plan"] = r["plan"]
             out[f"{key}_host_issue_ms_per_step"] = r.get("host_issue_ms")
             out[f"{key}_step_ms"], out[f"{key}_host_ms"] = r["step_ms"], r.get("host_ms")
+            if r.get("per_rank_step_ms"):
+                out[f"{key}_per_rank_step_ms"] = r["per_rank_step_ms"]
+            if r.get("bucket_timeline"):
+                out[f"{key}_bucket_timeline"] = r["bucket_timeline"]
             if "hip_graph" in r:
                 out[f"{key}_hip_graph"] = r["hip_graph"]
             if r.get("audit"):

@@ -96,6 +96,11 @@ class GradBucketer:
         self._works = []
         self._enabled = True
         self._hooks = []
+        # bucket timeline (CUDA, opt-in per step): an event where each bucket's collective is
+        # issued and one where backward ended (finish() entry) -> launch times relative to it
+        self.trace = False
+        self._trace_ev: List = []
+        self._trace_end = None
         if self.overlap:
             self._register_hooks()
 
@@ -182,6 +187,10 @@ class GradBucketer:
             self._launch_on_current(b)
 
     def _launch_on_current(self, b):
+        if self.trace and self.space.grad.is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._trace_ev.append((b, ev))
         lo, hi, _ = self.buckets[b]
         t = self.space.grad[lo:hi]
         if self.zero:
@@ -246,6 +255,9 @@ class GradBucketer:
         """Launch any bucket not yet launched (unused params / no overlap), then make the
         compute stream wait for every reduction.  Call before optimizer.step()."""
         from cloudtik_amd.ops.linear import sync_grad_stream
+        if self.trace and self.space.grad.is_cuda:
+            self._trace_end = torch.cuda.Event(enable_timing=True)
+            self._trace_end.record()
         self.space.flush_grads()
         if self.world <= 1:
             self._reset()
@@ -278,6 +290,21 @@ class GradBucketer:
         self._ready = [False] * len(self.buckets)
         self._next = 0
         self._reported = set()
+
+    def timeline(self):
+        """After a traced step has finished on the GPU: [(bucket, bytes, ms)] -- when each
+        bucket's collective was issued relative to the end of backward (negative = it
+        overlapped backward).  Clears the trace."""
+        out = []
+        if self._trace_end is not None:
+            self._trace_end.synchronize()
+            esize = 4 if self.fp32 else self.space.grad.element_size()
+            for b, ev in self._trace_ev:
+                ev.synchronize()
+                lo, hi, _ = self.buckets[b]
+                out.append((b, (hi - lo) * esize, round(self._trace_end.elapsed_time(ev), 3)))
+        self._trace_ev, self._trace_end = [], None
+        return out
 
     @property
     def grad_scale(self) -> float:
