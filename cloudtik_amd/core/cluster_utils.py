@@ -43,6 +43,9 @@ def node_tags(config: Dict[str, Any], node_type: str, kind: str, seq_id: Optiona
         T.CLOUDTIK_TAG_NODE_STATUS: T.STATUS_UNINITIALIZED,
         T.CLOUDTIK_TAG_LAUNCH_CONFIG: launch_hash(config, node_type, provider),
         T.CLOUDTIK_TAG_NODE_NAME: f"cloudtik-{config['cluster_name']}-{kind}",
+        # the workspace the node belongs to: the workspace registry (global variables as
+        # head-node tags) lists the heads of all its clusters by this tag
+        T.CLOUDTIK_TAG_WORKSPACE_NAME: config.get("workspace_name") or "default",
     }
     if seq_id is not None:
         t[T.CLOUDTIK_TAG_NODE_SEQ_ID] = str(seq_id)

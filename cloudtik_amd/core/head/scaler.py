@@ -59,10 +59,11 @@ class NodeAvailabilityTracker:
 
 class NodeLauncher(threading.Thread):
     def __init__(self, provider, config, node_type: str, count: int, tracker: NodeAvailabilityTracker,
-                 pending: Counter, lock: threading.Lock):
+                 pending: Counter, lock: threading.Lock, extra_tags: Optional[Dict[str, str]] = None):
         super().__init__(daemon=True, name=f"launcher-{node_type}")
         self.provider, self.config = provider, config
         self.node_type, self.count = node_type, count
+        self.extra_tags = dict(extra_tags or {})      # e.g. the quorum a joining node enters
         self.tracker, self.pending, self.lock = tracker, pending, lock
         self.error: Optional[BaseException] = None
 
@@ -73,6 +74,7 @@ class NodeLauncher(threading.Thread):
                 with self.lock:
                     seq = next_seq_id(self.provider, self.config["cluster_name"])
                 tags = node_tags(self.config, self.node_type, T.NODE_KIND_WORKER, seq, self.provider)
+                tags.update(self.extra_tags)
                 self.provider.create_node_with_resources(nt.get("node_config", {}), tags, 1,
                                                          nt.get("resources", {}))
             self.tracker.record_success(self.node_type)
@@ -114,7 +116,7 @@ class ClusterScaler:
         self.last_update_time = None
         from cloudtik_amd.core.head.quorum_manager import QuorumManager
         from cloudtik_amd.core.head.scaling_policies import create_scaling_policy
-        self.quorum = QuorumManager(config, provider)
+        self.quorum = QuorumManager(config, provider, state_client)
         self.policy = create_scaling_policy(config, self.head_ip, metrics_source=self.node_metrics)
         self.policy_requests: List[Dict[str, float]] = []
 
@@ -178,7 +180,7 @@ class ClusterScaler:
         self.scheduler.reset_config(config["available_node_types"], config.get("max_workers", 0),
                                     config["head_node_type"], opts.get("upscaling_speed", 1.0))
         self.idle_timeout_s = 60.0 * float(opts.get("idle_timeout_minutes", 5))
-        self.quorum.reset(config)
+        self.quorum.reset(config, self.provider)
         if self.policy is not None:
             self.policy.reset(config)
 
@@ -205,6 +207,8 @@ class ClusterScaler:
         workers = self.workers()
         tags = {n: self.provider.node_tags(n) for n in workers}
         types = self.config["available_node_types"]
+        with self.launch_lock:
+            self.quorum.update(workers, tags, dict(+self.pending_launches))
 
         # 3) terminations
         to_terminate: Dict[str, str] = {}
@@ -213,6 +217,9 @@ class ClusterScaler:
             nt = t.get(T.CLOUDTIK_TAG_USER_NODE_TYPE)
             if nt not in types:
                 to_terminate[n] = "unknown node type"
+                continue
+            if self.quorum.terminate_for_quorum(nt, n):
+                to_terminate[n] = "member of a quorum that lost its majority"
                 continue
             from cloudtik_amd.core.cluster_utils import launch_hash
             if t.get(T.CLOUDTIK_TAG_LAUNCH_CONFIG) != launch_hash(self.config, nt, self.provider):
@@ -233,6 +240,7 @@ class ClusterScaler:
             self.updaters.pop(n, None)
         if to_terminate:
             self.provider.terminate_nodes(list(to_terminate))
+            self.quorum.remove_terminating(list(to_terminate))
             workers = [n for n in workers if n not in to_terminate]
 
         # 4) launches
@@ -248,18 +256,28 @@ class ClusterScaler:
             dict(existing), launching, self.resource_demands(), self._free_resources(unused),
             self.cluster_requests(), running_count=len(workers))
         unavailable = self.tracker.unavailable()
-        for nt, cnt in to_launch.items():
+        for nt, cnt in self._prioritize_launch(to_launch).items():
             if nt in unavailable:
                 continue
-            self._launch(nt, cnt)
+            allowed, qid = self.quorum.is_launch_allowed(nt)
+            if not allowed:
+                continue
+            if qid:
+                cnt = 1                    # a running quorum grows one joining node at a time
+            self._launch(nt, cnt, self.quorum.launch_tags(qid))
         self.infeasible = infeasible
 
-        # 5) updates + recovery (quorum runtimes: set up only a complete initial membership)
+        # 5) updates + recovery; held back while a constrained node type (quorum runtimes)
+        # lacks its minimal membership
         workers = self.workers()
         to_replace = []
-        may_update = set(self.quorum.updatable(
-            [n for n in workers if self.provider.node_tags(n).get(T.CLOUDTIK_TAG_NODE_STATUS) == T.STATUS_UNINITIALIZED
-             or self.provider.node_tags(n).get(T.CLOUDTIK_TAG_QUORUM_ID)]))
+        if self.quorum.enabled:
+            with self.launch_lock:
+                pending = dict(+self.pending_launches)
+            self.quorum.update(workers, {}, pending)
+        if self.quorum.wait_for_update():
+            self.publish_status()
+            return
         for n in workers:
             t = self.provider.node_tags(n)
             status = t.get(T.CLOUDTIK_TAG_NODE_STATUS)
@@ -273,8 +291,7 @@ class ClusterScaler:
             if u is not None:
                 continue
             if status == T.STATUS_UNINITIALIZED:
-                if n in may_update:
-                    self._spawn_updater(n, recovery=False)
+                self._spawn_updater(n, recovery=False)
             elif status == T.STATUS_UP_TO_DATE and self.state is not None:
                 beat = hb.get(n) or hb.get(self.provider.internal_ip(n) or "")
                 last = (beat or {}).get("last_heartbeat_time")
@@ -336,13 +353,24 @@ class ClusterScaler:
                 else:
                     keep += 1
 
-    def _launch(self, node_type: str, count: int):
+    def _prioritize_launch(self, to_launch: Dict[str, int]) -> Dict[str, int]:
+        """Only the node types of the lowest ``launch_priority`` value launch this round
+        (reference cluster_scaler.py:671 _prioritize_launch): storage / coordination types
+        come up before the compute types that discover them."""
+        if len(to_launch) <= 1:
+            return dict(to_launch)
+        types = self.config["available_node_types"]
+        prio = {nt: int((types.get(nt) or {}).get("launch_priority", 0) or 0) for nt in to_launch}
+        best = min(prio.values())
+        return {nt: c for nt, c in to_launch.items() if prio[nt] == best}
+
+    def _launch(self, node_type: str, count: int, extra_tags: Optional[Dict[str, str]] = None):
         count = min(count, C.CLOUDTIK_MAX_LAUNCH_BATCH * 4)
         with self.launch_lock:
             self.pending_launches[node_type] += count
-        self._log(f"launching {count} x {node_type}")
+        self._log(f"launching {count} x {node_type}" + (" (quorum join)" if extra_tags else ""))
         launcher = NodeLauncher(self.provider, self.config, node_type, count, self.tracker,
-                                self.pending_launches, self.launch_lock)
+                                self.pending_launches, self.launch_lock, extra_tags)
         if self.synchronous:
             launcher.run()
         else:

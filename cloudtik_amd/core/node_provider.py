@@ -7,7 +7,9 @@ identified by opaque string ids; all control-plane state about a node lives in i
 """
 from __future__ import annotations
 
+import contextlib
 import copy
+import threading
 from typing import Any, Dict, List, Optional
 
 
@@ -32,6 +34,38 @@ class NodeProvider:
     # ------------------------------------------------------------------ queries
     def non_terminated_nodes(self, tag_filters: Dict[str, str]) -> List[str]:
         raise NotImplementedError
+
+    # A provider instance is bound to one cluster: its listing filters on the cluster-name tag.
+    # The workspace registry needs the head nodes of EVERY cluster of a workspace (reference
+    # providers/_private/aws/workspace_provider.py:57-91 _get_workspace_head_nodes): inside
+    # ``workspace_scope()`` the cloud providers drop the cluster filter (thread-local, so a
+    # scaler thread sharing the instance keeps its own scope).
+    _scope = threading.local()
+
+    @contextlib.contextmanager
+    def workspace_scope(self):
+        prev = getattr(self._scope, "all_clusters", False)
+        self._scope.all_clusters = True
+        try:
+            yield
+        finally:
+            self._scope.all_clusters = prev
+
+    def cluster_filter(self) -> Dict[str, str]:
+        """The cluster-name tag filter this instance lists with ({} in a workspace scope)."""
+        if getattr(self._scope, "all_clusters", False):
+            return {}
+        from cloudtik_amd.core import tags as T
+        return {T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name}
+
+    def workspace_head_nodes(self, workspace_name: str) -> Dict[str, Dict[str, str]]:
+        """Running head nodes of every cluster in ``workspace_name``: {key: tags}.  The keys
+        are opaque (a head of another cluster may not be addressable through this instance)."""
+        from cloudtik_amd.core import tags as T
+        with self.workspace_scope():
+            ids = self.non_terminated_nodes({T.CLOUDTIK_TAG_WORKSPACE_NAME: workspace_name,
+                                             T.CLOUDTIK_TAG_NODE_KIND: T.NODE_KIND_HEAD})
+            return {i: self.node_tags(i) for i in ids}
 
     def is_running(self, node_id: str) -> bool:
         raise NotImplementedError

@@ -49,6 +49,7 @@ _WORKSPACE_PROVIDERS = {
     "aliyun": _lazy("cloudtik_amd.providers.cloud.workspace_provider", "CloudWorkspaceProvider"),
     "huaweicloud": _lazy("cloudtik_amd.providers.cloud.workspace_provider", "CloudWorkspaceProvider"),
     "kubernetes": _lazy("cloudtik_amd.providers.cloud.workspace_provider", "CloudWorkspaceProvider"),
+    "mock": _lazy("cloudtik_amd.providers.local.workspace_provider", "LocalWorkspaceProvider"),
 }
 
 _STORAGE_PROVIDERS = {

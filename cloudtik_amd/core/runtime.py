@@ -66,7 +66,9 @@ class Runtime:
     def get_runtime_services(self, cluster_config: Dict[str, Any]):
         return {}
 
-    def get_node_constraints(self, cluster_config: Dict[str, Any]):
+    def get_node_constraints(self, cluster_config: Dict[str, Any], node_type: Optional[str] = None):
+        """None, or (needs minimal nodes before setup, forms a quorum, quorum can grow) for the
+        given worker node type (reference core/runtime.py:193)."""
         return None
 
     def node_constraints_reached(self, cluster_config, node_type, head_info, nodes_info, quorum_id=None):

@@ -69,9 +69,8 @@ class AWSNodeProvider(NodeProvider):
 
     # ------------------------------------------------------------------ queries
     def _filters(self, tag_filters):
-        f = [{"Name": "instance-state-name", "Values": ["pending", "running"]},
-             {"Name": f"tag:{T.CLOUDTIK_TAG_CLUSTER_NAME}", "Values": [self.cluster_name]}]
-        f += [{"Name": f"tag:{k}", "Values": [v]} for k, v in tag_filters.items()]
+        f = [{"Name": "instance-state-name", "Values": ["pending", "running"]}]
+        f += [{"Name": f"tag:{k}", "Values": [v]} for k, v in dict(self.cluster_filter(), **tag_filters).items()]
         return f
 
     def _remember(self, inst: Dict[str, Any]):
@@ -178,6 +177,27 @@ class AWSNodeProvider(NodeProvider):
         except Exception as e:  # noqa: BLE001 - no workspace resources: launch with the config as given
             import logging
             logging.getLogger(__name__).warning("AWS workspace defaults unavailable: %s", e)
+
+    # ------------------------------------------------------------------ SSH key pair
+    def key_pair_exists(self, name: str) -> bool:
+        try:
+            return bool(self.ec2.describe_key_pairs(KeyNames=[name]).get("KeyPairs"))
+        except Exception as e:  # noqa: BLE001 - botocore ClientError InvalidKeyPair.NotFound
+            code = getattr(e, "response", {}).get("Error", {}).get("Code", "")
+            if code == "InvalidKeyPair.NotFound":
+                return False
+            raise
+
+    def create_key_pair(self, name: str) -> str:
+        return self.ec2.create_key_pair(KeyName=name)["KeyMaterial"]
+
+    @staticmethod
+    def bootstrap_config(cluster_config):
+        """Key pair for the updater's SSH (reference aws/config.py:3868)."""
+        from cloudtik_amd.providers.cloud import keypairs
+        p = AWSNodeProvider(cluster_config["provider"], cluster_config.get("cluster_name", "default"))
+        return keypairs.configure_cloud_key_pair(cluster_config, "aws", cluster_config["provider"]["region"],
+                                                 p.key_pair_exists, p.create_key_pair)
 
     def _subnets(self, node_config) -> List[str]:
         ids = node_config.get("SubnetIds") or ([node_config["SubnetId"]] if node_config.get("SubnetId") else [])

@@ -72,6 +72,12 @@ def gcp_label(v: str) -> str:
 class GCPNodeProvider(NodeProvider):
     """Compute Engine instances as nodes; node id = instance name; tags = labels."""
 
+    @staticmethod
+    def bootstrap_config(cluster_config):
+        """SSH public key into the instances' metadata (reference gcp/config.py:2678,3478)."""
+        from cloudtik_amd.providers.cloud import keypairs
+        return keypairs.configure_gcp_key_pair(cluster_config)
+
     def __init__(self, provider_config, cluster_name, transport: Optional[Transport] = None):
         super().__init__(provider_config, cluster_name)
         self.project = provider_config["project_id"]
@@ -104,8 +110,8 @@ class GCPNodeProvider(NodeProvider):
         return op
 
     def non_terminated_nodes(self, tag_filters):
-        flt = [f'labels.{gcp_label(T.CLOUDTIK_TAG_CLUSTER_NAME)} = "{gcp_label(self.cluster_name)}"']
-        flt += [f'labels.{gcp_label(k)} = "{gcp_label(v)}"' for k, v in tag_filters.items()]
+        flt = [f'labels.{gcp_label(k)} = "{gcp_label(v)}"'
+               for k, v in dict(self.cluster_filter(), **tag_filters).items()]
         items, token = [], None
         while True:
             params = {"filter": " AND ".join(f"({f})" for f in flt)}
@@ -203,6 +209,12 @@ class AzureNodeProvider(NodeProvider):
     """ARM virtual machines as nodes; node id = VM name; tags = VM tags.  Each VM gets its
     own NIC (``<vm>-nic``) on ``provider.subnet_id`` and, with ``use_public_ip``, a public IP."""
 
+    @staticmethod
+    def bootstrap_config(cluster_config):
+        """adminUsername + SSH public key in the VMs' osProfile (reference _azure/config.py:4068)."""
+        from cloudtik_amd.providers.cloud import keypairs
+        return keypairs.configure_azure_key_pair(cluster_config)
+
     def __init__(self, provider_config, cluster_name, transport: Optional[Transport] = None):
         super().__init__(provider_config, cluster_name)
         self.sub = provider_config["subscription_id"]
@@ -226,7 +238,7 @@ class AzureNodeProvider(NodeProvider):
         return self._rg("Microsoft.Compute", "virtualMachines", name)
 
     def non_terminated_nodes(self, tag_filters):
-        want = dict(tag_filters, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name})
+        want = dict(tag_filters, **self.cluster_filter())
         vms, url, params = [], self._vm_url(), {"api-version": _VM_API}
         while url:
             page = self._call("GET", url, params, None)

@@ -120,6 +120,21 @@ class AliyunNodeProvider(NodeProvider):
     def _tags_of(inst) -> Dict[str, str]:
         return {t["TagKey"]: t.get("TagValue", "") for t in (inst.get("Tags") or {}).get("Tag", [])}
 
+    def key_pair_exists(self, name: str) -> bool:
+        r = self._call("DescribeKeyPairs", {"RegionId": self.region, "KeyPairName": name})
+        return any(k.get("KeyPairName") == name for k in (r.get("KeyPairs") or {}).get("KeyPair", []))
+
+    def create_key_pair(self, name: str) -> str:
+        return self._call("CreateKeyPair", {"RegionId": self.region, "KeyPairName": name})["PrivateKeyBody"]
+
+    @staticmethod
+    def bootstrap_config(cluster_config):
+        """ECS key pair for the updater's SSH (reference aliyun/config.py:2153)."""
+        from cloudtik_amd.providers.cloud import keypairs
+        p = AliyunNodeProvider(cluster_config["provider"], cluster_config.get("cluster_name", "default"))
+        return keypairs.configure_cloud_key_pair(cluster_config, "aliyun", p.region, p.key_pair_exists,
+                                                 p.create_key_pair)
+
     def _describe(self, extra: Dict[str, Any]) -> List[Dict[str, Any]]:
         out, page = [], 1
         while True:
@@ -131,7 +146,9 @@ class AliyunNodeProvider(NodeProvider):
             page += 1
 
     def non_terminated_nodes(self, tag_filters):
-        insts = self._describe(_tag_params({T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name}))
+        scope = self.cluster_filter() or {k: v for k, v in tag_filters.items()
+                                          if k == T.CLOUDTIK_TAG_WORKSPACE_NAME}
+        insts = self._describe(_tag_params(scope))
         live = [i for i in insts if i.get("Status") in ("Pending", "Starting", "Running")]
         self._cache.update({i["InstanceId"]: i for i in live})
         return [i["InstanceId"] for i in live
@@ -303,6 +320,29 @@ class HuaweiCloudNodeProvider(NodeProvider):
         host = self.provider_config.get("endpoint", f"ecs.{self.region}.myhuaweicloud.com")
         return f"https://{host}/{version}/{self.project}/cloudservers{path}"
 
+    def _kps_url(self, name: str = "") -> str:
+        host = self.provider_config.get("kps_endpoint", f"kps.{self.region}.myhuaweicloud.com")
+        return f"https://{host}/v3/{self.project}/keypairs" + (f"/{name}" if name else "")
+
+    def key_pair_exists(self, name: str) -> bool:
+        try:
+            return bool(self._call("GET", self._kps_url(name), None, None).get("keypair"))
+        except CloudAPIError as e:
+            if e.status == 404:
+                return False
+            raise
+
+    def create_key_pair(self, name: str) -> str:
+        return self._call("POST", self._kps_url(), None, {"keypair": {"name": name}})["keypair"]["private_key"]
+
+    @staticmethod
+    def bootstrap_config(cluster_config):
+        """KPS key pair for the updater's SSH (reference huaweicloud/config.py:1876)."""
+        from cloudtik_amd.providers.cloud import keypairs
+        p = HuaweiCloudNodeProvider(cluster_config["provider"], cluster_config.get("cluster_name", "default"))
+        return keypairs.configure_cloud_key_pair(cluster_config, "huaweicloud", p.region, p.key_pair_exists,
+                                                 p.create_key_pair)
+
     @staticmethod
     def _tags_of(srv) -> Dict[str, str]:
         out = {}
@@ -312,7 +352,7 @@ class HuaweiCloudNodeProvider(NodeProvider):
         return out
 
     def non_terminated_nodes(self, tag_filters):
-        want = dict(tag_filters, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name})
+        want = dict(tag_filters, **self.cluster_filter())
         servers, offset = [], 1
         while True:
             page = self._call("GET", self._url("/detail"), {"limit": 100, "offset": offset}, None)
@@ -364,7 +404,8 @@ class HuaweiCloudNodeProvider(NodeProvider):
     def create_node(self, node_config, tags, count):
         tags = dict(tags, **{T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name})
         server = json.loads(json.dumps(node_config.get("server", {})))
-        for key, dst in (("flavor", "flavorRef"), ("image_id", "imageRef"), ("vpc_id", "vpcid")):
+        for key, dst in (("flavor", "flavorRef"), ("image_id", "imageRef"), ("vpc_id", "vpcid"),
+                         ("key_name", "key_name")):
             if key in node_config:
                 server[dst] = node_config[key]
         if "subnet_id" in node_config:

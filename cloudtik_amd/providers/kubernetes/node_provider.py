@@ -58,7 +58,7 @@ class KubernetesNodeProvider(NodeProvider):
         return json.loads(self._k("get", "pod", node_id, "-o", "json"))
 
     def non_terminated_nodes(self, tag_filters):
-        sel = {T.CLOUDTIK_TAG_CLUSTER_NAME: self.cluster_name}
+        sel = self.cluster_filter()
         sel.update(tag_filters)
         return [p["metadata"]["name"] for p in self._pods(sel)
                 if p.get("status", {}).get("phase") in ("Pending", "Running")

@@ -112,6 +112,27 @@ class LocalNodeProvider(NodeProvider):
         super().__init__(provider_config, cluster_name)
         self.scheduler = LocalScheduler(provider_config, cluster_name)
 
+    def workspace_head_nodes(self, workspace_name):
+        """Every local cluster keeps its node state in its own file of the state directory
+        (the same host serves as head of several clusters, so node ids -- host IPs -- repeat
+        across clusters): scan them all; keys are ``<cluster>/<ip>``."""
+        out = {}
+        try:
+            files = sorted(f for f in os.listdir(STATE_DIR) if f.endswith(".json") and not f.startswith("workspace-"))
+        except OSError:
+            return out
+        for f in files:
+            try:
+                nodes = FileStateStore(os.path.join(STATE_DIR, f)).get_nodes()
+            except (OSError, ValueError):
+                continue
+            for ip, n in nodes.items():
+                tags = n.get("tags", {})
+                if n.get("state") != "terminated" and tags.get(T.CLOUDTIK_TAG_NODE_KIND) == T.NODE_KIND_HEAD and \
+                        tags.get(T.CLOUDTIK_TAG_WORKSPACE_NAME) == workspace_name:
+                    out[f"{f[:-5]}/{ip}"] = dict(tags)
+        return out
+
     def non_terminated_nodes(self, tag_filters):
         return self.scheduler.get_non_terminated_nodes(tag_filters)
 

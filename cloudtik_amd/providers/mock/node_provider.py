@@ -86,6 +86,18 @@ class MockProvider(NodeProvider):
         else:
             cls._worlds.pop(cluster_name, None)
 
+    def workspace_head_nodes(self, workspace_name):
+        from cloudtik_amd.core import tags as T
+        out = {}
+        for cname, w in sorted(MockProvider._worlds.items()):
+            with w["lock"]:
+                for nid, n in w["nodes"].items():
+                    t = n["tags"]
+                    if n["state"] not in ("terminated", "stopped") and t.get(T.CLOUDTIK_TAG_NODE_KIND) == "head" \
+                            and t.get(T.CLOUDTIK_TAG_WORKSPACE_NAME) == workspace_name:
+                        out[f"{cname}/{nid}"] = dict(t)
+        return out
+
     @property
     def runner(self) -> MockProcessRunner:
         return self.world["runner"]

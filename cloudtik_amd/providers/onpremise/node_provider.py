@@ -49,7 +49,8 @@ class OnPremiseNodeProvider(NodeProvider):
         self.client = SimulatorClient(addr)
 
     def non_terminated_nodes(self, tag_filters):
-        return self.client.call("non_terminated_nodes", cluster_name=self.cluster_name, tag_filters=tag_filters)
+        return self.client.call("non_terminated_nodes", cluster_name=self.cluster_name if self.cluster_filter() else None,
+                                tag_filters=tag_filters)
 
     def is_running(self, node_id):
         return self.client.call("is_running", node_id=node_id)

@@ -57,7 +57,8 @@ class PoolScheduler:
     def non_terminated_nodes(self, cluster_name: str, tag_filters: Dict[str, str]) -> List[str]:
         out = []
         for ip, n in self.store.get_nodes().items():
-            if n["state"] == "allocated" and n["cluster"] == cluster_name and \
+            # cluster_name None: every cluster of the pool (workspace-wide head listing)
+            if n["state"] == "allocated" and (cluster_name is None or n["cluster"] == cluster_name) and \
                     all(n["tags"].get(k) == v for k, v in (tag_filters or {}).items()):
                 out.append(ip)
         return sorted(out)

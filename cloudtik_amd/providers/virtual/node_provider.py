@@ -100,6 +100,26 @@ class VirtualNodeProvider(NodeProvider):
     def _nodes(self):
         return self.store.get_nodes()
 
+    def workspace_head_nodes(self, workspace_name):
+        """Heads of every virtual cluster on this host (one state directory per cluster)."""
+        from cloudtik_amd.core import tags as T
+        base = os.path.join(_state_dir(), "virtual")
+        out = {}
+        try:
+            names = sorted(os.listdir(base))
+        except OSError:
+            return out
+        for cname in names:
+            path = os.path.join(base, cname, "nodes.json")
+            if not os.path.exists(path):
+                continue
+            for nid, n in FileStateStore(path).get_nodes().items():
+                t = n.get("tags", {})
+                if n.get("state") == "running" and t.get(T.CLOUDTIK_TAG_NODE_KIND) == T.NODE_KIND_HEAD and \
+                        t.get(T.CLOUDTIK_TAG_WORKSPACE_NAME) == workspace_name:
+                    out[f"{cname}/{nid}"] = dict(t)
+        return out
+
     def non_terminated_nodes(self, tag_filters):
         out = []
         for nid, n in self._nodes().items():

@@ -326,6 +326,30 @@ class CatalogRuntime(RuntimeBase):
             return None
         return QUORUM_CONSTRAINTS.get(self.name, (True, True, True))
 
+    def node_constraints_reached(self, cluster_config, node_type, head_info, nodes_info, quorum_id=None):
+        """Called on the head when the node type's minimal membership (or a quorum join) is
+        complete: the ensemble -- member addresses in sequence order -- is registered in the
+        workspace registry as ``<cluster>-<runtime>-ensemble`` so other clusters discover the
+        servers of THIS quorum (reference zookeeper/utils.py:66 _handle_node_constraints_reached)."""
+        if not self.spec.services:
+            return None
+        members = sorted(nodes_info.values(), key=lambda i: i.get("node_seq_id", 0))
+        hosts = [m["node_ip"] for m in members if m.get("node_ip")]
+        svc = self.spec.services[0]
+        rec = sd.define_runtime_service(self.name, f"{svc.name}-ensemble", svc.port, svc.protocol, svc.node_kind,
+                                        svc.scope, list(svc.features), svc.metrics)
+        rec.update(quorum_id=quorum_id, node_type=node_type)
+        key = sd.service_global_key(cluster_config.get("cluster_name", "default"), f"{self.name}-ensemble")
+        gv = {key: sd.encode_service_address(rec, hosts[0] if hosts else None, hosts)}
+        try:
+            from cloudtik_amd.core.provider_factory import get_workspace_provider
+            get_workspace_provider(cluster_config["provider"], cluster_config.get("workspace_name", "default")) \
+                .publish_global_variables(cluster_config, gv)
+        except Exception as e:  # noqa: BLE001 - discovery falls back to the members' tags
+            import logging
+            logging.getLogger(__name__).warning("%s: could not register the ensemble: %s", self.name, e)
+        return gv
+
     def get_logs(self):
         return dict(self.spec.logs)
 

@@ -138,14 +138,78 @@ def test_discovery_switches_consul_ha_name_and_database_env():
 
 
 def test_workspace_global_variables_through_the_provider(tmp_path, monkeypatch):
-    """_workspace_global_variables reaches the real workspace provider (local registry)."""
+    """The registry is head-node tags behind the node provider (reference
+    providers/_private/local/workspace_provider.py:54-80): a service published by cluster c1's
+    head is discovered from ANOTHER CLI home (fresh workspace-provider instance, own state dir)
+    through the provider, a long value survives the tag-size split, and the entries vanish
+    with the head."""
     from cloudtik_amd.runtime.common import discovery as D
     from cloudtik_amd.providers.local import workspace_provider as lwp
-    from cloudtik_amd.core.provider_factory import get_workspace_provider
+    from cloudtik_amd.core import tags as T
+    from cloudtik_amd.core.provider_factory import get_workspace_provider, get_node_provider
+    from cloudtik_amd.providers.mock.node_provider import MockProvider
+    MockProvider.reset()
+    monkeypatch.setattr(lwp, "STATE_DIR", str(tmp_path / "home1"))
+    pc = {"type": "mock"}
+    heads = {}
+    for c, ws in (("c1", "w"), ("c2", "w"), ("c3", "other")):
+        p = get_node_provider(pc, c, use_cache=False)
+        heads[c] = next(iter(p.create_node({}, {T.CLOUDTIK_TAG_CLUSTER_NAME: c, T.CLOUDTIK_TAG_NODE_KIND: "head",
+                                                T.CLOUDTIK_TAG_WORKSPACE_NAME: ws}, 1)))
+    long_value = '{"hosts": [' + ",".join(f'"10.0.{i // 250}.{i % 250}"' for i in range(60)) + "]}"
+    cfg1 = {"provider": pc, "workspace_name": "w", "cluster_name": "c1"}
+    get_workspace_provider(pc, "w").publish_global_variables(cfg1, {"service.c1.x": "{}", "service.c1.big": long_value})
+    get_workspace_provider(pc, "w").publish_global_variables(
+        {"provider": pc, "workspace_name": "w", "cluster_name": "c2"}, {"service.c2.y": "{}"})
+    get_workspace_provider(pc, "other").publish_global_variables(
+        {"provider": pc, "workspace_name": "other", "cluster_name": "c3"}, {"service.c3.z": "{}"})
+    tags = get_node_provider(pc, "c1", use_cache=False).node_tags(heads["c1"])
+    assert all(len(v) <= lwp.TAG_VALUE_MAX for k, v in tags.items() if k.startswith("x-"))
+    # a second CLI home: nothing shared but the provider
+    monkeypatch.setattr(lwp, "STATE_DIR", str(tmp_path / "home2"))
+    cfg_other_host = {"provider": pc, "workspace_name": "w", "cluster_name": "c9"}
+    gv = D._workspace_global_variables(cfg_other_host)
+    assert gv["service.c1.x"] == "{}" and gv["service.c2.y"] == "{}" and gv["service.c1.big"] == long_value
+    assert "service.c3.z" not in gv                            # another workspace
+    assert sorted(get_workspace_provider(pc, "w").list_clusters(cfg_other_host)) == ["c1", "c2"]
+    get_node_provider(pc, "c1", use_cache=False).terminate_node(heads["c1"])
+    gv = D._workspace_global_variables(cfg_other_host)
+    assert "service.c1.x" not in gv and "service.c2.y" in gv
+    MockProvider.reset()
+
+
+def test_local_provider_workspace_heads_span_cluster_state_files(tmp_path, monkeypatch):
+    """Local clusters keep one state file each and share this host as head: the workspace
+    listing scans every file (the same IP heads several clusters)."""
+    from cloudtik_amd.core import tags as T
+    from cloudtik_amd.providers.local import node_provider as lnp, workspace_provider as lwp
+    monkeypatch.setattr(lnp, "STATE_DIR", str(tmp_path))
     monkeypatch.setattr(lwp, "STATE_DIR", str(tmp_path))
-    cfg = {"provider": {"type": "local"}, "workspace_name": "w", "cluster_name": "c1"}
-    get_workspace_provider(cfg["provider"], "w").publish_global_variables(cfg, {"service.c1.x": "{}"})
-    assert "service.c1.x" in D._workspace_global_variables(cfg)
+    pc = {"type": "local", "nodes": ["10.1.0.1"]}
+    for c in ("a", "b"):
+        p = lnp.LocalNodeProvider(pc, c)
+        (h,) = p.create_node({}, {T.CLOUDTIK_TAG_CLUSTER_NAME: c, T.CLOUDTIK_TAG_NODE_KIND: "head",
+                                  T.CLOUDTIK_TAG_WORKSPACE_NAME: "w"}, 1)
+        lwp.LocalWorkspaceProvider(pc, "w").publish_global_variables(
+            {"provider": pc, "cluster_name": c}, {f"service.{c}.s": c})
+    heads = lnp.LocalNodeProvider(pc, "zz").workspace_head_nodes("w")
+    assert sorted(heads) == ["a/10.1.0.1", "b/10.1.0.1"]
+    gv = lwp.LocalWorkspaceProvider(pc, "w").subscribe_global_variables({"provider": pc, "cluster_name": "zz"})
+    assert gv == {"service.a.s": "a", "service.b.s": "b"}
+
+
+def test_cloud_listing_drops_cluster_filter_only_in_workspace_scope():
+    """EC2 filters: the cluster tag in normal listings, the workspace + head tags inside
+    workspace_scope (how a cloud provider finds every head of a workspace)."""
+    from cloudtik_amd.core import tags as T
+    from cloudtik_amd.providers.cloud import node_provider as NP
+    p = NP.AWSNodeProvider({"region": "nowhere", "_client_factory": lambda svc: None}, "c1")
+    names = {f["Name"] for f in p._filters({})}
+    assert f"tag:{T.CLOUDTIK_TAG_CLUSTER_NAME}" in names
+    with p.workspace_scope():
+        f = p._filters({T.CLOUDTIK_TAG_WORKSPACE_NAME: "w"})
+    assert {x["Name"] for x in f} == {"instance-state-name", f"tag:{T.CLOUDTIK_TAG_WORKSPACE_NAME}"}
+    assert f"tag:{T.CLOUDTIK_TAG_CLUSTER_NAME}" in {x["Name"] for x in p._filters({})}
 
 
 def test_service_selectors_tags_labels_and_exclusions():

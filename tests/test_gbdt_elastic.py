@@ -63,8 +63,10 @@ def test_elastic_training_continues_without_the_failed_actor(tmp_path):
 def test_failure_without_elasticity_or_past_the_limit_raises(tmp_path):
     with pytest.raises(RuntimeError, match="elastic_training is off"):
         _run(tmp_path, "rigid", fail_at={0: 1})
+    # past the limit: one lost actor with max_failed_actors=0 (two simultaneous failures are
+    # not deterministic -- the driver tears the group down at the FIRST exit it sees)
     with pytest.raises(RuntimeError, match="actors lost"):
-        _run(tmp_path, "toomany", elastic_training=True, max_failed_actors=1, fail_at={0: 1, 2: 1})
+        _run(tmp_path, "toomany", elastic_training=True, max_failed_actors=0, fail_at={2: 1})
 
 
 def test_run_workflow_with_elastic_actors(tmp_path):

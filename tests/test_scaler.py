@@ -222,6 +222,8 @@ def test_quorum_runtime_sets_up_complete_membership(state):
         c["available_node_types"]["cpu.small"].update(min_workers=3)
         c["options"]["upscaling_speed"] = 0.1        # launches trickle in: max(5,...) still caps at 3 here
     cfg, provider, scaler = _setup(name, state, mutate)
+    provider.create_node({}, {T.CLOUDTIK_TAG_CLUSTER_NAME: name, T.CLOUDTIK_TAG_NODE_KIND: "head",
+                              T.CLOUDTIK_TAG_WORKSPACE_NAME: "default"}, 1)
     # launch only 2 first by shrinking min_workers, nothing may be set up
     scaler.config["available_node_types"]["cpu.small"]["min_workers"] = 2
     scaler.scheduler.node_types["cpu.small"]["min_workers"] = 2
@@ -236,7 +238,113 @@ def test_quorum_runtime_sets_up_complete_membership(state):
     assert len(ws) == 3
     qids = {provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_ID] for w in ws}
     assert len(qids) == 1
-    assert all(provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_JOIN] == T.QUORUM_JOIN_STATUS_SUCCESS for w in ws)
+    # the initial members form the quorum directly (no join); the runtime got the membership
+    assert not any(T.CLOUDTIK_TAG_QUORUM_JOIN in provider.node_tags(w) for w in ws)
+    (note,) = scaler.quorum.notifications
+    assert note["runtimes"] == ["zookeeper"] and sorted(note["members"]) == sorted(ws)
+    assert note["quorum_id"] == next(iter(qids))
+    # the zookeeper runtime registered this ensemble in the workspace registry (head tags)
+    from cloudtik_amd.core.provider_factory import get_workspace_provider
+    from cloudtik_amd.core import service_discovery as sd
+    gv = get_workspace_provider(cfg["provider"], "default").subscribe_global_variables(cfg)
+    rec = sd.decode_service_address(gv[sd.service_global_key(name, "zookeeper-ensemble")])
+    assert sorted(rec["hosts"]) == sorted(provider.internal_ip(w) for w in ws) and rec["quorum_id"] in qids
+
+
+def _zk_types(c, zk_min=3, extra=None):
+    """A dedicated ZooKeeper node type (its own runtime section) next to compute types."""
+    c["available_node_types"]["zk.node"] = {"node_config": {"instance_type": "m.zk"}, "resources": {"CPU": 4},
+                                            "min_workers": zk_min, "max_workers": 5, "launch_priority": 0,
+                                            "runtime": {"types": ["zookeeper"]}}
+    c["available_node_types"]["cpu.small"].update(min_workers=2, launch_priority=1)
+    c["max_workers"] = 20
+    c.setdefault("options", {})["launch_with_strong_priority"] = True
+    if extra:
+        extra(c)
+
+
+def _by_type(provider, name, nt):
+    return [w for w in _workers(provider, name) if provider.node_tags(w)[T.CLOUDTIK_TAG_USER_NODE_TYPE] == nt]
+
+
+def test_per_node_type_quorum_gates_other_types(state, monkeypatch):
+    """Reference quorum_manager.py:299,341,430: the constraint is per node type (only zk.node
+    runs ZooKeeper); with launch_with_strong_priority the compute type launches only once every
+    zk node is up to date; the runtime hook receives head + member info and the quorum id."""
+    from cloudtik_amd.runtime.catalog import CatalogRuntime
+    seen = []
+    monkeypatch.setattr(CatalogRuntime, "node_constraints_reached",
+                        lambda self, cfg, nt, head, nodes, quorum_id=None: seen.append((self.name, nt, head, nodes,
+                                                                                        quorum_id)))
+    name = "sc-quorum-types"
+    cfg, provider, scaler = _setup(name, state, _zk_types)
+    assert set(scaler.quorum.constraints) == {"zk.node"}
+    c = scaler.quorum.constraints["zk.node"]
+    assert (c.minimal, c.quorum, c.scalable, c.runtimes) == (3, True, True, ["zookeeper"])
+    scaler.update()
+    zk = _by_type(provider, name, "zk.node")
+    assert len(zk) == 3 and not _by_type(provider, name, "cpu.small")      # compute waits (priority)
+    assert all(provider.node_tags(w)[T.CLOUDTIK_TAG_NODE_STATUS] == T.STATUS_UP_TO_DATE for w in zk)
+    (rt, nt, head, nodes, qid), = seen
+    assert rt == "zookeeper" and nt == "zk.node" and sorted(nodes) == sorted(zk) and qid
+    assert head["node_seq_id"] == T.CLOUDTIK_TAG_HEAD_NODE_SEQ_ID
+    assert all(nodes[w]["node_ip"] == provider.internal_ip(w) and nodes[w]["quorum_id"] == qid for w in zk)
+    assert json.loads(state.kv_get(b"cluster_nodes_info_zk.node", namespace="cluster")).keys() == set(zk)
+    # strong priority: while a zk node is not up to date, compute may not launch
+    provider.set_node_tags(zk[0], {T.CLOUDTIK_TAG_NODE_STATUS: T.STATUS_SETTING_UP})
+    scaler.quorum.update(_workers(provider, name), {}, {})
+    assert scaler.quorum.is_launch_allowed("cpu.small") == (False, None)
+    provider.set_node_tags(zk[0], {T.CLOUDTIK_TAG_NODE_STATUS: T.STATUS_UP_TO_DATE})
+    scaler.update()
+    assert len(_by_type(provider, name, "cpu.small")) == 2
+    assert not any(T.CLOUDTIK_TAG_QUORUM_ID in provider.node_tags(w) for w in _by_type(provider, name, "cpu.small"))
+
+
+def test_scalable_quorum_grows_one_joining_node_at_a_time(state, monkeypatch):
+    from cloudtik_amd.runtime.catalog import CatalogRuntime
+    seen = []
+    monkeypatch.setattr(CatalogRuntime, "node_constraints_reached",
+                        lambda self, cfg, nt, head, nodes, quorum_id=None: seen.append((sorted(nodes), quorum_id)))
+    name = "sc-quorum-join"
+    cfg, provider, scaler = _setup(name, state, _zk_types)
+    scaler.update()
+    zk = sorted(_by_type(provider, name, "zk.node"))
+    qid = provider.node_tags(zk[0])[T.CLOUDTIK_TAG_QUORUM_ID]
+    provider.terminate_node(zk[0])                          # 2 of 3 left: the quorum keeps its majority
+    scaler.update()
+    now = sorted(_by_type(provider, name, "zk.node"))
+    (joiner,) = set(now) - set(zk)
+    t = provider.node_tags(joiner)
+    assert t[T.CLOUDTIK_TAG_QUORUM_ID] == qid                # joined the running quorum
+    assert t[T.CLOUDTIK_TAG_QUORUM_JOIN] == T.QUORUM_JOIN_STATUS_SUCCESS
+    assert seen[-1] == (sorted(now), qid)                    # runtime told about the new member set
+    # while a join is in progress no second node launches
+    provider.set_node_tags(joiner, {T.CLOUDTIK_TAG_QUORUM_JOIN: T.QUORUM_JOIN_STATUS_INIT})
+    scaler.quorum.update(_workers(provider, name), {}, {})
+    assert scaler.quorum.is_launch_allowed("zk.node") == (False, None)
+
+
+def test_unscalable_quorum_lost_majority_is_replaced(state, monkeypatch):
+    """MinIO-like quorum (not scalable): members of a quorum below its majority are terminated
+    (terminate_for_quorum) and a fresh quorum forms on new nodes; a healthy non-scalable quorum
+    launches nothing."""
+    from cloudtik_amd.runtime import catalog
+    monkeypatch.setitem(catalog.QUORUM_CONSTRAINTS, "zookeeper", (True, True, False))
+    name = "sc-quorum-minio"
+    cfg, provider, scaler = _setup(name, state, _zk_types)
+    scaler.update()
+    zk = sorted(_by_type(provider, name, "zk.node"))
+    qid = provider.node_tags(zk[0])[T.CLOUDTIK_TAG_QUORUM_ID]
+    provider.terminate_node(zk[0])
+    scaler.update()                      # majority kept, not scalable: no replacement launched
+    assert sorted(_by_type(provider, name, "zk.node")) == zk[1:]
+    provider.terminate_node(zk[1])       # 1 of 3: the quorum lost its majority
+    scaler.update()                      # the last member goes; the scheduler relaunches 3
+    scaler.update()
+    now = _by_type(provider, name, "zk.node")
+    assert zk[2] not in now and len(now) == 3
+    qids = {provider.node_tags(w)[T.CLOUDTIK_TAG_QUORUM_ID] for w in now}
+    assert len(qids) == 1 and qids != {qid}
 
 
 def test_unhealthy_gpu_node_is_replaced(state, monkeypatch):
