@@ -6,6 +6,8 @@ import json
 import os
 
 import click
+
+from cloudtik_amd.cli.dump_options import dump_options
 import yaml
 
 DEFAULT_BOOTSTRAP_CONFIG = "~/cloudtik_bootstrap_config.yaml"
@@ -201,11 +203,16 @@ def process_status():
 
 @head.command(name="cluster-dump")
 @click.option("--output", "-o", default=None)
-@click.option("--no-logs", is_flag=True, default=False)
-def cluster_dump(output, no_logs):
-    """Collect cluster info, state and logs into a tarball."""
+@click.option("--hosts", default=None, help="Only these nodes (IPs or node ids, comma separated).")
+@click.option("--head-only", is_flag=True, default=False)
+@click.option("--silent", is_flag=True, default=False)
+@dump_options
+def cluster_dump(output, hosts, head_only, silent, params):
+    """Collect every node's logs, debug state, packages, processes and GPU state (in parallel)."""
     from cloudtik_amd.core import cluster_operator as op
-    click.echo(op.cluster_dump(_cfg_file(), output, not no_logs))
+    out = op.cluster_dump(_cfg_file(), output, hosts=hosts, head_only=head_only, params=params, on_head=True)
+    if not silent:
+        click.echo(out)
 
 
 @head.command(name="debug-status")

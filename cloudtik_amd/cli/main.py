@@ -22,6 +22,8 @@ import sys
 
 import click
 
+from cloudtik_amd.cli.dump_options import dump_options
+
 from cloudtik_amd.core import constants as C
 
 
@@ -407,12 +409,15 @@ def health_check(cluster_config_file, with_details, cluster_name):
 @cli.command(name="cluster-dump")
 @click.argument("cluster_config_file")
 @click.option("--output", "-o", default=None)
-@click.option("--no-logs", is_flag=True, default=False)
+@click.option("--hosts", default=None, help="Only these nodes (IPs or node ids, comma separated).")
+@click.option("--head-only", is_flag=True, default=False)
 @_cluster_name
-def cluster_dump(cluster_config_file, output, no_logs, cluster_name):
-    """Collect info, state and logs of the cluster into a tarball."""
+@dump_options
+def cluster_dump(cluster_config_file, output, hosts, head_only, cluster_name, params):
+    """Collect logs, debug state, packages, processes and GPU state of the cluster's nodes."""
     from cloudtik_amd.core import cluster_operator as op
-    click.echo(op.cluster_dump(cluster_config_file, output, not no_logs, cluster_name))
+    click.echo(op.cluster_dump(cluster_config_file, output, override_cluster_name=cluster_name, hosts=hosts,
+                               head_only=head_only, params=params))
 
 
 cli.add_command(cluster_dump, name="cluster_dump")

@@ -11,6 +11,8 @@ import time
 
 import click
 
+from cloudtik_amd.cli.dump_options import dump_options
+
 from cloudtik_amd.core import constants as C
 
 DEFAULT_BOOTSTRAP_CONFIG = "~/cloudtik_bootstrap_config.yaml"
@@ -130,14 +132,14 @@ def wait_for_port(port, host, timeout, free):
 
 @node.command()
 @click.option("--output", "-o", default=None)
-def dump(output):
-    """Tar this node's session logs."""
-    import tarfile
-    from cloudtik_amd.core import services
-    output = output or f"cloudtik-node-dump-{time.strftime('%Y%m%d-%H%M%S')}.tar.gz"
-    with tarfile.open(output, "w:gz") as t:
-        t.add(services.logs_dir(), arcname="logs")
-    click.echo(output)
+@click.option("--silent", is_flag=True, default=False)
+@dump_options
+def dump(output, silent, params):
+    """Archive this node's logs, debug state, pip packages, processes and GPU state."""
+    from cloudtik_amd.core.cluster_dump import collect_local
+    out = collect_local(params, output or f"cloudtik-node-dump-{time.strftime('%Y%m%d-%H%M%S')}.tar.gz")
+    if not silent:
+        click.echo(out)
 
 
 @node.command(name="service-daemon")

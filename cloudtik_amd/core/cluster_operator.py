@@ -549,29 +549,35 @@ def health_check(config, with_details: bool = False) -> Dict[str, Any]:
 
 
 def cluster_dump(config_file, output: Optional[str] = None, include_logs: bool = True,
-                 override_cluster_name: Optional[str] = None) -> str:
-    """Collect cluster info, state tables and the session logs of every node into a tarball."""
+                 override_cluster_name: Optional[str] = None, hosts: Optional[str] = None,
+                 head_only: bool = False, params=None, on_head: bool = False) -> str:
+    """Collect logs, debug state, pip packages, processes and GPU state of the cluster's nodes
+    into one tarball (core/cluster_dump.py).  ``on_head`` (``cloudtik head cluster-dump``), or
+    a head that is this very host: collect here.  Otherwise the collection runs on the head
+    (``cloudtik head cluster-dump``, which reaches the workers) and its archive is copied back
+    (reference cluster_operator.py dump_cluster -> get_archive_from_head_node)."""
+    from cloudtik_amd.core import cluster_dump as cd
     config = _config(config_file, override_cluster_name)
     provider = _provider(config)
-    output = output or f"cloudtik-dump-{config['cluster_name']}-{time.strftime('%Y%m%d-%H%M%S')}.tar.gz"
-    tmp = tempfile.mkdtemp(prefix="cloudtik-dump-")
-    with open(os.path.join(tmp, "cluster_info.json"), "w") as f:
-        json.dump(get_cluster_info(config), f, indent=1, default=str)
+    params = params or cd.DumpParameters(logs=include_logs)
+    head = get_head_node(provider, config["cluster_name"])
+    if on_head or head is None or cd._is_local(provider.internal_ip(head) or ""):
+        return cd.dump_cluster(config, provider, params, output, hosts=hosts, head_only=head_only)
+    name = config["cluster_name"]
+    output = os.path.expanduser(output or os.path.join(os.getcwd(), f"{name}_{time.strftime('%Y-%m-%d_%H-%M-%S')}.tar.gz"))
+    remote = f"/tmp/cloudtik_cluster_dump_{name}_{os.getpid()}.tar.gz"
+    cmd = ["cloudtik", "head", "cluster-dump", "--silent", "--output", remote] + params.node_flags()
+    if hosts:
+        cmd += ["--hosts", shlex.quote(hosts)]
+    if head_only:
+        cmd.append("--head-only")
+    ex = _executor(config, provider, head)
+    ex.run(" ".join(cmd), timeout=1800, environment_variables=node_environment(config, provider, head, None, True))
+    ex.run_rsync_down(remote, output)
     try:
-        with open(os.path.join(tmp, "health.json"), "w") as f:
-            json.dump(health_check(config, with_details=True), f, indent=1, default=str)
-    except Exception as e:  # noqa: BLE001
-        logger.warning("health check failed: %s", e)
-    if include_logs:
-        for n in provider.non_terminated_nodes({T.CLOUDTIK_TAG_CLUSTER_NAME: config["cluster_name"]}):
-            d = os.path.join(tmp, "nodes", provider.internal_ip(n) or n)
-            os.makedirs(d, exist_ok=True)
-            try:
-                _executor(config, provider, n).run_rsync_down("~/.cloudtik/session/logs", d)
-            except (ProcessRunnerError, OSError) as e:
-                logger.warning("could not fetch logs of %s: %s", n, e)
-    with tarfile.open(output, "w:gz") as tar:
-        tar.add(tmp, arcname=os.path.basename(output).split(".tar")[0])
+        ex.run(f"rm -f {shlex.quote(remote)}", timeout=60)
+    except (ProcessRunnerError, OSError):
+        pass
     return output
 
 

@@ -105,7 +105,12 @@ class ClusterController:
                 raise
             dt = time.time() - t0
             try:
-                self.metrics.observe(self.scaler.summary(), dt)
+                summary = self.scaler.summary()
+                self.metrics.observe(summary, dt)
+                # the last round's scaler state for `cloudtik cluster-dump` (debug_state.txt)
+                from cloudtik_amd.core.cluster_dump import write_debug_state
+                write_debug_state(dict(summary, update_seconds=round(dt, 3),
+                                       quorum=getattr(self.scaler.quorum, "notifications", [])[-10:]))
             except Exception:  # noqa: BLE001
                 pass
             rounds += 1
