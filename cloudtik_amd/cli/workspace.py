@@ -36,7 +36,11 @@ def create(workspace_config_file, yes):
 def delete(workspace_config_file, delete_managed_storage, delete_managed_database, yes):
     """Delete a workspace."""
     from cloudtik_amd.core import workspace as ws
-    ws.delete_workspace(_load(workspace_config_file), delete_managed_storage, delete_managed_database)
+    try:
+        ws.delete_workspace(_load(workspace_config_file), delete_managed_storage, delete_managed_database,
+                            confirm=None if yes else (lambda q: click.confirm(q, default=False)))
+    except (ws.WorkspaceInUse, RuntimeError) as e:
+        raise click.ClickException(str(e))
     click.echo("workspace deleted")
 
 

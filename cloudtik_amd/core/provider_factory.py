@@ -41,7 +41,7 @@ _NODE_PROVIDERS = {
 
 _WORKSPACE_PROVIDERS = {
     "local": _lazy("cloudtik_amd.providers.local.workspace_provider", "LocalWorkspaceProvider"),
-    "onpremise": _lazy("cloudtik_amd.providers.local.workspace_provider", "LocalWorkspaceProvider"),
+    "onpremise": _lazy("cloudtik_amd.providers.onpremise.workspace_provider", "OnPremiseWorkspaceProvider"),
     "virtual": _lazy("cloudtik_amd.providers.local.workspace_provider", "LocalWorkspaceProvider"),
     "aws": _lazy("cloudtik_amd.providers.cloud.workspace_provider", "CloudWorkspaceProvider"),
     "gcp": _lazy("cloudtik_amd.providers.cloud.workspace_provider", "CloudWorkspaceProvider"),

@@ -33,10 +33,41 @@ def create_workspace(config: Dict[str, Any]):
     return cfg
 
 
-def delete_workspace(config: Dict[str, Any], delete_managed_storage=False, delete_managed_database=False):
+class WorkspaceInUse(RuntimeError):
+    pass
+
+
+def delete_workspace(config: Dict[str, Any], delete_managed_storage=False, delete_managed_database=False,
+                     confirm=None):
+    """Delete the workspace, refusing while it still serves something (reference
+    workspace_operator.py:58-112): a complete workspace with running clusters, or managed
+    databases that are not being deleted with it.  ``confirm(question) -> bool`` is asked
+    last (the CLI prompts unless --yes); a refusal aborts."""
     cfg = prepare_workspace_config(config)
-    get_workspace_provider(cfg["provider"], cfg["workspace_name"]).delete_workspace(
-        cfg, delete_managed_storage, delete_managed_database)
+    name = cfg["workspace_name"]
+    p = get_workspace_provider(cfg["provider"], name)
+    existence = p.check_workspace_existence(cfg)
+    if existence == Existence.NOT_EXIST:
+        raise RuntimeError(f"workspace {name} does not exist")
+    if existence == Existence.COMPLETED:
+        running = p.list_clusters(cfg) or {}
+        if running:
+            raise WorkspaceInUse(f"workspace {name} has running clusters ({', '.join(sorted(running))}): "
+                                 f"stop them first")
+    if cfg.get("managed_cloud_storage"):
+        logger.warning("the managed cloud storage of workspace %s %s", name,
+                       "and ALL its data will be deleted" if delete_managed_storage else "is kept")
+    if cfg.get("managed_cloud_database") and not delete_managed_database:
+        try:
+            dbs = p.list_databases(cfg) or {}
+        except NotImplementedError:
+            dbs = {}
+        if dbs:
+            raise WorkspaceInUse(f"workspace {name} has managed databases ({', '.join(sorted(dbs))}): delete them "
+                                 f"first or pass --delete-managed-database")
+    if confirm is not None and not confirm(f"Delete workspace {name}?"):
+        raise RuntimeError("aborted")
+    p.delete_workspace(cfg, delete_managed_storage, delete_managed_database)
 
 
 def update_workspace(config: Dict[str, Any]):

@@ -43,10 +43,9 @@ class SimulatorClient:
 class OnPremiseNodeProvider(NodeProvider):
     def __init__(self, provider_config, cluster_name):
         super().__init__(provider_config, cluster_name)
-        addr = provider_config.get("cloud_simulator_address")
-        if not addr:
-            raise ValueError("onpremise provider needs provider.cloud_simulator_address")
-        self.client = SimulatorClient(addr)
+        from cloudtik_amd.providers.onpremise.simulator import simulator_address
+        # configured, or discovered from the process file of a simulator on this machine
+        self.client = SimulatorClient(simulator_address(provider_config.get("cloud_simulator_address")))
 
     def non_terminated_nodes(self, tag_filters):
         return self.client.call("non_terminated_nodes", cluster_name=self.cluster_name if self.cluster_filter() else None,

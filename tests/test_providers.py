@@ -21,8 +21,9 @@ def _port():
 
 
 @pytest.fixture
-def simulator(tmp_path):
+def simulator(tmp_path, monkeypatch):
     from cloudtik_amd.providers.onpremise.simulator import serve
+    monkeypatch.setenv("CLOUDTIK_SIMULATOR_PROCESS_FILE", str(tmp_path / "sim.json"))
     pool = {"instance_types": {"mi355x-8gpu": {"CPU": 128, "GPU": 8, "accelerator_type:MI355X": 8},
                                "cpu-node": {"CPU": 64}},
             "nodes": [{"ip": "10.1.0.1", "instance_type": "mi355x-8gpu"},
@@ -60,6 +61,53 @@ def test_onpremise_provider_pool(simulator):
            "available_node_types": {"w": {"node_config": {"instance_type": "cpu-node"}}}}
     OnPremiseNodeProvider.fillout_available_node_types_resources(cfg)
     assert cfg["available_node_types"]["w"]["resources"] == {"CPU": 64}
+
+
+def test_simulator_reload_workspaces_discovery_and_shutdown(simulator, tmp_path, monkeypatch):
+    """Reference cloudtik_cloud_simulator.py:196-227 / cloud_simulator_scheduler.py:146-158 /
+    onpremise/config.py:20-50: the pool is reloaded in place (new hosts free, removed free hosts
+    gone, removed allocated hosts drain), workspaces live in the simulator, providers find the
+    simulator through its process file, and --shutdown stops it."""
+    from cloudtik_amd.core.workspace import Existence
+    from cloudtik_amd.providers.onpremise import simulator as S
+    from cloudtik_amd.providers.onpremise.node_provider import OnPremiseNodeProvider
+    from cloudtik_amd.providers.onpremise.workspace_provider import OnPremiseWorkspaceProvider
+    # discovery: no address configured -> the process file of the running simulator
+    assert S.discover_simulator() == simulator
+    pa = OnPremiseNodeProvider({"type": "onpremise"}, "a")
+    (nid,) = pa.create_node({"instance_type": "mi355x-8gpu"}, {T.CLOUDTIK_TAG_NODE_KIND: "head",
+                                                               T.CLOUDTIK_TAG_WORKSPACE_NAME: "w1"}, 1)
+    # workspaces
+    wp = OnPremiseWorkspaceProvider({"type": "onpremise"}, "w1")
+    assert wp.check_workspace_existence({}) == Existence.NOT_EXIST
+    wp.create_workspace({})
+    assert wp.check_workspace_existence({}) == Existence.COMPLETED
+    assert S.request(None, "list_workspaces") == ["w1"]
+    with pytest.raises(RuntimeError, match="running clusters"):
+        wp.delete_workspace({})
+    # reload: 10.1.0.2 (free) and 10.1.0.1 (allocated to cluster a) leave, 10.1.0.9 joins
+    pool = {"instance_types": {"mi355x-8gpu": {"CPU": 128, "GPU": 8}, "cpu-node": {"CPU": 64}},
+            "nodes": [{"ip": "10.1.0.3", "instance_type": "cpu-node"},
+                      {"ip": "10.1.0.9", "instance_type": "mi355x-8gpu"}]}
+    (tmp_path / "pool.yaml").write_text(yaml.safe_dump(pool))
+    S.main(["--reload", "--bind-address", simulator.split(":")[0], "--port", simulator.split(":")[1]])
+    st = S.request(None, "pool_status")
+    assert st["total"] == 3 and st["draining"] == [nid] and st["free"] == 2
+    (n2,) = OnPremiseNodeProvider({"type": "onpremise"}, "b").create_node({"instance_type": "mi355x-8gpu"}, {}, 1)
+    assert n2 == "10.1.0.9"                                 # never a draining host
+    pa.terminate_node(nid)                                  # the draining host leaves the pool
+    assert S.request(None, "pool_status")["total"] == 2
+    wp.delete_workspace({})
+    assert wp.check_workspace_existence({}) == Existence.NOT_EXIST
+    # shutdown over the API
+    S.main(["--shutdown"])
+    import time
+    deadline = time.time() + 5
+    while time.time() < deadline and os.path.exists(str(tmp_path / "sim.json")):
+        time.sleep(0.05)
+    assert not os.path.exists(str(tmp_path / "sim.json"))
+    with pytest.raises(Exception):
+        S.request(simulator, "pool_status")
 
 
 FAKE_KUBECTL = r'''#!/usr/bin/env python3
