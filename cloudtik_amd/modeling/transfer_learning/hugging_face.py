@@ -224,9 +224,18 @@ class HuggingFaceTextClassificationModel:
 
     def train(self, dataset, epochs: int = 1, batch_size: int = 32, lr: float = 2e-5, eval_dataset=None,
               weight_decay: float = 0.01, checkpoint_dir: Optional[str] = None, seed: int = 0,
-              max_steps: Optional[int] = None, log_every: int = 50, warmup_steps: int = 0):
+              max_steps: Optional[int] = None, log_every: int = 50, warmup_steps: int = 0,
+              distributed: bool = False, nnodes: int = 1, nproc_per_node: int = 1, hosts: Optional[str] = None,
+              hostfile: Optional[str] = None, shared_dir: Optional[str] = None, launcher: Optional[str] = None):
         """Fine-tune with the framework Trainer (data parallel when launched with several
-        ranks).  ``dataset`` is a torch Dataset of dicts or a HuggingFaceTextClassificationDataset."""
+        ranks).  ``dataset`` is a torch Dataset of dicts or a HuggingFaceTextClassificationDataset.
+        ``distributed=True`` launches the ranks itself (modeling/transfer_learning/distributed.py)."""
+        if distributed:
+            from cloudtik_amd.modeling.transfer_learning.distributed import fit_distributed
+            return fit_distributed(self, dataset, dict(
+                epochs=epochs, batch_size=batch_size, lr=lr, eval_dataset=eval_dataset, weight_decay=weight_decay,
+                checkpoint_dir=checkpoint_dir, seed=seed, max_steps=max_steps, log_every=log_every,
+                warmup_steps=warmup_steps), nnodes, nproc_per_node, hosts, hostfile, shared_dir, launcher)
         import torch.distributed as dist
         from cloudtik_amd.train.trainer import Trainer
         torch.manual_seed(seed)

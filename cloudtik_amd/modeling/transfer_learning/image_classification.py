@@ -97,7 +97,17 @@ class ImageClassificationModel:
     def train(self, dataset: Dataset, epochs: int = 1, batch_size: int = 32, lr: float = 1e-3,
               eval_dataset: Optional[Dataset] = None, optimizer: str = "adamw", weight_decay: float = 0.0,
               checkpoint_dir: Optional[str] = None, seed: int = 0, max_steps: Optional[int] = None,
-              log_every: int = 50) -> List[Dict[str, float]]:
+              log_every: int = 50, distributed: bool = False, nnodes: int = 1, nproc_per_node: int = 1,
+              hosts: Optional[str] = None, hostfile: Optional[str] = None, shared_dir: Optional[str] = None,
+              launcher: Optional[str] = None) -> List[Dict[str, float]]:
+        """Fine-tune; ``distributed=True`` launches ``nnodes`` x ``nproc_per_node`` ranks through
+        cloudtik-run from here (modeling/transfer_learning/distributed.py)."""
+        if distributed:
+            from cloudtik_amd.modeling.transfer_learning.distributed import fit_distributed
+            return fit_distributed(self, dataset, dict(
+                epochs=epochs, batch_size=batch_size, lr=lr, eval_dataset=eval_dataset, optimizer=optimizer,
+                weight_decay=weight_decay, checkpoint_dir=checkpoint_dir, seed=seed, max_steps=max_steps,
+                log_every=log_every), nnodes, nproc_per_node, hosts, hostfile, shared_dir, launcher)
         from cloudtik_amd.train.trainer import Trainer
         self.classes = self.classes or getattr(dataset, "classes", None)
         tr = Trainer(self.model, optimizer=optimizer, lr=lr, weight_decay=weight_decay,

@@ -65,7 +65,15 @@ class TextClassificationModel:
     def train(self, dataset: Dataset, epochs: int = 1, batch_size: int = 32, lr: float = 2e-5,
               eval_dataset: Optional[Dataset] = None, optimizer: str = "adamw", weight_decay: float = 0.01,
               checkpoint_dir: Optional[str] = None, seed: int = 0, max_steps: Optional[int] = None,
-              log_every: int = 50) -> List[Dict[str, float]]:
+              log_every: int = 50, distributed: bool = False, nnodes: int = 1, nproc_per_node: int = 1,
+              hosts: Optional[str] = None, hostfile: Optional[str] = None, shared_dir: Optional[str] = None,
+              launcher: Optional[str] = None) -> List[Dict[str, float]]:
+        if distributed:
+            from cloudtik_amd.modeling.transfer_learning.distributed import fit_distributed
+            return fit_distributed(self, dataset, dict(
+                epochs=epochs, batch_size=batch_size, lr=lr, eval_dataset=eval_dataset, optimizer=optimizer,
+                weight_decay=weight_decay, checkpoint_dir=checkpoint_dir, seed=seed, max_steps=max_steps,
+                log_every=log_every), nnodes, nproc_per_node, hosts, hostfile, shared_dir, launcher)
         import torch.distributed as dist
         from cloudtik_amd.train.trainer import Trainer
         self.classes = self.classes or getattr(dataset, "classes", None)

@@ -1,7 +1,9 @@
 """Distributed job runner (``cloudtik-run``) and the function-call API.
 
-``run(fn, args, num_proc=...)`` runs a Python function on every rank of a local or
-multi-host job and returns the per-rank results (reference runtime/ai/runner/util/
+``run_command(cmd, nnodes=..., nproc_per_node=..., hosts=...)`` launches a command on every
+rank exactly as ``cloudtik-run`` would (reference runtime/ai/runner/__init__.py:139-187) and
+returns its exit code.  ``run(fn, args, num_proc=...)`` runs a Python function on every rank
+of a local or multi-host job and returns the per-rank results (reference runtime/ai/runner/util/
 func_call.py + run_func.py + codec.py: the function is serialized with cloudpickle,
 each rank executes it under the launcher's env:// rank environment and writes its result
 back).  Only files this process wrote are deserialized.
@@ -16,6 +18,41 @@ import tempfile
 from typing import Any, Callable, List, Optional
 
 from cloudtik_amd.runner.distributor import Distributor
+
+
+def run_command(command, num_proc: int = 0, nnodes: int = 0, nproc_per_node: int = 0, hosts: Optional[str] = None,
+                hostfile: Optional[str] = None, launcher: Optional[str] = None, master_addr: Optional[str] = None,
+                master_port: int = 29500, module: bool = False, no_python: bool = False,
+                max_restarts: int = 0, env: Optional[dict] = None, extra_args: Optional[List[str]] = None) -> int:
+    """Run ``command`` (a script / module and its arguments, list or string) on every rank;
+    same launcher selection, rank environment and restarts as the ``cloudtik-run`` CLI."""
+    import shlex
+    from cloudtik_amd.runner.launch import main as launch_main
+    cmd = shlex.split(command) if isinstance(command, str) else [str(c) for c in command]
+    if not cmd:
+        raise ValueError("empty command")
+    argv = ["--num-proc", str(num_proc), "--nnodes", str(nnodes), "--nproc-per-node", str(nproc_per_node),
+            "--master-port", str(master_port), "--max-restarts", str(max_restarts)]
+    if hosts:
+        argv += ["--hosts", hosts]
+    if hostfile:
+        argv += ["--hostfile", hostfile]
+    if launcher:
+        argv += ["--launcher", launcher]
+    if master_addr:
+        argv += ["--master-addr", master_addr]
+    if module:
+        argv.append("-m")
+    if no_python:
+        argv.append("--no-python")
+    argv += list(extra_args or [])
+    old = dict(os.environ)
+    os.environ.update({k: str(v) for k, v in (env or {}).items()})
+    try:
+        return launch_main(argv + cmd)
+    finally:
+        os.environ.clear()
+        os.environ.update(old)
 
 
 def run(fn: Callable, args: tuple = (), kwargs: Optional[dict] = None, num_proc: int = 0,
