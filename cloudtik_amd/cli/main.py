@@ -164,12 +164,17 @@ def exec_cmd(cluster_config_file, cmd, node_ip, all_nodes, start, run_env, clust
 @click.argument("script_args", nargs=-1, type=click.UNPROCESSED)
 @click.option("--node-ip", default=None)
 @click.option("--job-waiter", default=None)
+@click.option("--runtime-options", default=None,
+              help="Options for the runtime's runner, e.g. the AI runtime's cloudtik-run: "
+                   "\"--nproc-per-node 8 --max-restarts 2\" (reference scripts.py submit).")
 @_cluster_name
-def submit(cluster_config_file, script, script_args, node_ip, job_waiter, cluster_name):
+def submit(cluster_config_file, script, script_args, node_ip, job_waiter, runtime_options, cluster_name):
     """Upload a script to the cluster and run it (python / bash / ...)."""
+    import shlex
     from cloudtik_amd.core import cluster_operator as op
     try:
-        op.submit_and_exec(cluster_config_file, script, list(script_args), node_ip, job_waiter, cluster_name)
+        op.submit_and_exec(cluster_config_file, script, list(script_args), node_ip, job_waiter, cluster_name,
+                           runtime_options=shlex.split(runtime_options) if runtime_options else None)
     except Exception as e:  # noqa: BLE001
         _fail(str(e))
 

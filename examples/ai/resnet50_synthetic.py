@@ -25,6 +25,23 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 
+def native_libraries():
+    """The framework's native shared objects mapped into this process (/proc/self/maps)."""
+    import cloudtik_amd
+    root = os.path.dirname(os.path.dirname(os.path.abspath(cloudtik_amd.__file__)))
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split()[-1] if len(line.split()) >= 6 else ""
+                if path.endswith(".so") and "cloudtik_amd" in path and os.path.realpath(path).startswith(
+                        os.path.realpath(root)):
+                    out.add(os.path.relpath(os.path.realpath(path), os.path.realpath(root)))
+    except OSError:
+        pass
+    return sorted(out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch-size", type=int, default=32)
@@ -35,6 +52,9 @@ def main():
     ap.add_argument("--horovod", action="store_true")
     ap.add_argument("--fp16-allreduce", action="store_true")
     ap.add_argument("--use-adasum", action="store_true")
+    ap.add_argument("--report-json", default=None,
+                    help="each rank writes <path>.rank<R>: its device binding, the native HIP libraries "
+                         "mapped into the process, the last loss and its img/s (end-to-end checks)")
     args = ap.parse_args()
 
     from cloudtik_amd.models.resnet import resnet18_like_small, resnet50
@@ -81,14 +101,16 @@ def main():
         ts = ResNetTrainStep(model, opt, ddp)
 
         def step():
-            ts(data, target)
+            return ts(data, target)
 
     def log(s):
         if rank == 0:
             print(s, flush=True)
 
+    last = {}
+
     def benchmark_step():
-        step()
+        last["loss"] = step()
         if gpu:
             torch.cuda.synchronize()
 
@@ -105,6 +127,15 @@ def main():
     mean, conf = np.mean(img_secs), 1.96 * np.std(img_secs)
     log(f"Img/sec per {'GPU' if gpu else 'CPU'}: {mean:.1f} +-{conf:.1f}")
     log(f"Total img/sec on {world} {'GPU' if gpu else 'CPU'}(s): {world * mean:.1f} +-{world * conf:.1f}")
+    if args.report_json:
+        import json
+        loss = last.get("loss")
+        with open(f"{args.report_json}.rank{rank}", "w") as f:
+            json.dump({"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
+                       "device": str(device), "device_name": torch.cuda.get_device_name(device) if gpu else None,
+                       "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
+                       "native_libraries": native_libraries(), "img_per_sec": float(mean),
+                       "loss": float(loss.detach().float()) if torch.is_tensor(loss) else None}, f)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
