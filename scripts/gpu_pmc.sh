@@ -8,7 +8,7 @@ TAG=$1; MODEL=$2; RE=${3:-.}
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-export CLOUDTIK_AMD_WGRAD_STREAM=0
+export CLOUDTIK_AMD_WGRAD_STREAM=0 CLOUDTIK_BENCH_AUDIT=0
 ARGS="--model $MODEL --steps 2 --warmup 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex "$RE" --output-format csv -d "$OUT/tr" -o tr -- python3 "$R/bench.py" $ARGS > "$OUT/tr.log" 2>&1 || { tail -5 "$OUT/tr.log"; exit 1; }
 i=0
