@@ -83,6 +83,7 @@ def main():
           "igemm dgrad us | calls |")
     print("|---|---|---|---:|---:|---:|---:|---:|")
     tot = {"mi_f": 0.0, "ig_f": 0.0, "mi_d": 0.0, "ig_d": 0.0}
+    roofs = []
     for name, ci, co, H, k, s, calls in SHAPES:
         errs = check(ci, co, H, k, s, dev)
         pad = k // 2
@@ -127,6 +128,16 @@ def main():
         tot["mi_d"] += mi_d * calls
         tot["ig_f"] += auto_f * calls
         tot["ig_d"] += auto_d * calls
+        # roofline: minimum HBM bytes (read X, W once, write Y) at 6 TB/s vs bf16 MFMA at 2.5 PF
+        Ho = (H + 2 * pad - k) // s + 1
+        fl = 2.0 * a.batch * Ho * Ho * co * ci * k * k
+        by = 2.0 * (a.batch * H * H * ci + co * ci * k * k + a.batch * Ho * Ho * co)
+        roof = max(by / 6e12, fl / 2.5e15) * 1e6
+        roofs.append({"conv": name, "roofline_us": round(roof, 1), "fwd_us": round(auto_f, 1),
+                      "dgrad_us": round(auto_d, 1), "wgrad_us": round(ig_w, 1), "fwd_tflops": round(fl / auto_f / 1e6),
+                      "fwd_TBs": round(by / auto_f / 1e6, 2), "fwd_pct_roofline": round(100 * roof / auto_f),
+                      "dgrad_pct_roofline": round(100 * roof / auto_d), "wgrad_pct_roofline": round(100 * roof / ig_w),
+                      "calls": calls})
         print(f"| {name} | {ci}->{co} {H}x{H} k{k} s{s} | {errs[0]:.1e} / {errs[1]:.1e} / {errs[2]:.1e} / "
               f"{errs[3]:.1e} | {mi_f:.1f} | {auto_f:.1f} (best {best_f[0]:.1f} c{best_f[1]}) | {mi_d:.1f} | "
               f"{auto_d:.1f} (best {best_d[0]:.1f} c{best_d[1]}) | {calls} |", flush=True)
@@ -135,6 +146,15 @@ def main():
     print(f"\nper ResNet-50 step (auto cfg): MIOpen fwd {tot['mi_f'] / 1e3:.2f} ms, igemm fwd {tot['ig_f'] / 1e3:.2f} ms; "
           f"MIOpen dgrad {tot['mi_d'] / 1e3:.2f} ms, igemm dgrad {tot['ig_d'] / 1e3:.2f} ms; "
           f"MIOpen wgrad {tot['mi_w'] / 1e3:.2f} ms, igemm wgrad {tot['ig_w'] / 1e3:.2f} ms")
+    print("\n| conv | roofline us | fwd us (% roof, TF/s, TB/s) | dgrad us (% roof) | wgrad us (% roof) | calls |")
+    print("|---|---:|---:|---:|---:|---:|")
+    for r in roofs:
+        print(f"| {r['conv']} | {r['roofline_us']} | {r['fwd_us']} ({r['fwd_pct_roofline']}%, {r['fwd_tflops']}, "
+              f"{r['fwd_TBs']}) | {r['dgrad_us']} ({r['dgrad_pct_roofline']}%) | {r['wgrad_us']} "
+              f"({r['wgrad_pct_roofline']}%) | {r['calls']} |")
+    w = sum(r["calls"] * r["roofline_us"] for r in roofs)
+    print(f"\nper step: roofline {3 * w / 1e3:.2f} ms for fwd+dgrad+wgrad vs igemm "
+          f"{(tot['ig_f'] + tot['ig_d'] + tot['ig_w']) / 1e3:.2f} ms")
 
 
 if __name__ == "__main__":

@@ -326,6 +326,29 @@ bool gemm_nn(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumul
   return gemm_nt_impl(A, B, D, epi, accumulate, bias, aux, dbias, true);
 }
 
+extern "C" int ct_gemm_nt_stream(const void*, long, const void*, long, void*, long, int, int, int, int, const void*,
+                                 int, int, int, hipStream_t);
+
+// Streamed persistent MFMA GEMM (one workgroup per CU walks its output tiles with one
+// continuous K-tile DMA stream): D = A @ B^T (b_kn: B stored [K, N], D = A @ B) [+ bias[N]].
+bool gemm_nt_stream(at::Tensor A, at::Tensor B, at::Tensor D, c10::optional<at::Tensor> bias, bool b_kn,
+                    int64_t wgs, bool accumulate) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "gemm_nt_stream: GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+              D.scalar_type() == at::kBFloat16, "gemm_nt_stream: bf16 operands");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "gemm_nt_stream: 2-D row-major operands");
+  const long M = A.size(0), K = A.size(1), N = b_kn ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_kn ? B.size(0) : B.size(1)) == K && D.size(0) == M && D.size(1) == N,
+              "gemm_nt_stream: shape mismatch");
+  const bool hb = bias.has_value() && bias->defined();
+  if (hb) TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                      "gemm_nt_stream: bias");
+  int rc = ct_gemm_nt_stream(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0),
+                             (int)M, (int)N, (int)K, hb ? 5 : 0, hb ? bias->data_ptr() : nullptr, b_kn ? 1 : 0,
+                             (int)wgs, accumulate ? 1 : 0, at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
 extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, float*,
                            hipStream_t);
 
@@ -366,6 +389,9 @@ void register_lt(pybind11::module& m) {
   m.def("gemm_tn2", &gemm_tn2, "weight-gradient GEMM A^T @ B (token-major operands) on the MFMA kernel");
   m.def("gemm_tn2_bias", &gemm_tn2_bias, "gemm_tn2 + per-split column sums of A (bias gradient)");
   m.def("gemm_nt", &gemm_nt, "hand-written MFMA GEMM A @ B^T with fused epilogues");
+  m.def("gemm_nt_stream", &gemm_nt_stream, "streamed persistent MFMA GEMM A @ B^T / A @ B (+ bias)",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("D"), pybind11::arg("bias") = pybind11::none(), pybind11::arg("b_kn") = false,
+        pybind11::arg("wgs") = 0, pybind11::arg("accumulate") = false);
   m.def("gemm_nn", &gemm_nn, "hand-written MFMA GEMM A @ B (B stored [K, N]) with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
   m.def("lt_bmm_tuned", &lt_bmm_tuned, "strided-batched hipBLASLt GEMM, algorithm picked by timing all solutions");

@@ -29,6 +29,7 @@
 // LDS reads, split-K into fp32 slabs; ct_gemm_tn2).
 // Reference: the BERT encoder FFN (HF BertIntermediate + BertOutput).
 #include "common.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace ct {
@@ -42,7 +43,8 @@ constexpr int NT_ROWB = NT_BK * 2;        // 128 B per LDS image row
 constexpr int NT_HALF = 128 * NT_ROWB;    // 16 KiB: 128 rows of one operand
 constexpr int NT_BUF = 4 * NT_HALF;       // 64 KiB per K-tile buffer
 
-enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2, NT_EPI_F32_SLAB = 3, NT_EPI_NONE = 4 };
+enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2, NT_EPI_F32_SLAB = 3, NT_EPI_NONE = 4,
+       NT_EPI_BIAS = 5 };
 
 struct NtArgs {
   const bf16_t* A;
@@ -356,7 +358,7 @@ struct NtEpiPre {
 
 template <int EPI, int NJ>
 __device__ __forceinline__ void nt_preload_bias(const NtArgs& a, long ncol, NtEpiPre<NJ>& pre) {
-  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD) {
+  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_BIAS) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) pre.bias[j] = a.bias ? *(const u16x4*)(a.bias + ncol + j * 16) : u16x4(0);
   }
@@ -396,7 +398,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
     return;
   }
   float bv[NJ][4] = {};
-  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD) {
+  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_BIAS) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -418,7 +420,13 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
   for (int i = 0; i < 8; ++i) {
     const long m = mrow + i * 16;
     u16x4 out[NJ], pre[NJ];
-    if constexpr (EPI == NT_EPI_PLAIN) {
+    if constexpr (EPI == NT_EPI_BIAS) {
+      // D = result + bias (the forward Linear: QKV / attention output / FFN2 projections)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[j][r] = f2bf(acc[i][j][r] + bv[j][r]);
+    } else if constexpr (EPI == NT_EPI_PLAIN) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const long n = ncol + j * 16;
@@ -590,9 +598,226 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Streamed persistent variant (forward / data-gradient GEMMs, NT and NN layouts).
+//
+// One workgroup per CU walks several output tiles (w, w + P, w + 2P, ... in the XCD-remapped
+// tile order), and its K-tiles form ONE continuous stream: the half-tile DMAs of the next
+// output tile are issued by the last phases of the current one exactly as within a tile, so
+// the next tile's operands land while this tile's epilogue stores run (the epilogue of one
+// wave group also overlaps the other group's MFMA phase: the groups run one barrier apart).
+// Nothing else changes: same phases, same LDS images and swizzles, same counted vmcnt waits
+// (epilogue stores / bias loads are younger than the in-flight DMAs, so "all but the N youngest
+// vector-memory ops" only ever waits for MORE than the pipeline needs).  The one-tile kernel
+// pays a workgroup launch, a cold prologue (first DMA latency) and an idle epilogue per tile:
+// at K = 1024 (16 K-tiles) that is a large share of the tile.
+struct NtStream {
+  int nk;            // K-tiles per output tile
+  int total_k;       // K-tiles of this workgroup's whole stream
+  int tiles_n, tiles, P, wg;
+  __device__ __forceinline__ void tile_origin(int j, long& m0, long& n0) const {
+    const int L = xcd_remap(j * P + wg, tiles);
+    m0 = (long)(L / tiles_n) * NT_BM;
+    n0 = (long)(L % tiles_n) * NT_BN;
+  }
+};
+
+// DMA cursor: the (output tile, K-tile, slot) of the next half to stage, advanced one slot per
+// staging call (the phases issue halves in stream order).  Wave-uniform, lives in SGPRs.
+struct NtCursor {
+  int j, k, slot, G;
+  long m0, n0;
+};
+
+template <int LAY>
+__device__ __forceinline__ void nt_stage_cursor(const NtCtx& c, const NtStream& st, NtCursor& cur) {
+  using Ly = NtLay<LAY>;
+  static_assert(!Ly::AT, "streamed kernel: NT / NN layouts only");
+  if (cur.G < st.total_k) {
+    char* dst = c.lds + (cur.G & 1) * NT_BUF + cur.slot * NT_HALF;
+    const long k0 = (long)cur.k * NT_BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = c.wave * 2 + i;
+      const bf16_t* base;
+      unsigned off;
+      if (cur.slot == 0 || cur.slot == 3) {
+        base = c.A + (cur.m0 + ((piece >> 3) << 7) + (cur.slot == 3 ? 64 : 0) + (piece & 7) * 8) * c.lda + k0;
+        off = i ? c.offa1 : c.offa0;
+      } else if constexpr (!Ly::BT) {
+        base = c.B + (cur.n0 + ((piece >> 2) << 6) + (cur.slot == 2 ? 32 : 0) + (piece & 3) * 8) * c.ldb + k0;
+        off = i ? c.offb1 : c.offb0;
+      } else {
+        base = c.B + (k0 + piece * 4) * c.ldb + cur.n0 + (cur.slot == 2 ? 32 : 0);
+        off = c.offb0;
+      }
+      nt_glds16s(base, off, dst + piece * 1024);
+    }
+  }
+  // advance: slot -> K-tile -> output tile
+  if (++cur.slot == 4) {
+    cur.slot = 0;
+    ++cur.G;
+    if (++cur.k == st.nk) {
+      cur.k = 0;
+      ++cur.j;
+      if (cur.G < st.total_k) st.tile_origin(cur.j, cur.m0, cur.n0);
+    }
+  }
+}
+
+template <int POS, int LAY>
+__device__ __forceinline__ void nt_ktile_stream(const NtCtx& c, const NtStream& st, NtCursor& cur, int t,
+                                                f32x4 (&acc)[8][4], nt_s16x8 (&fa)[2][4][2], nt_s16x8 (&fb)[2][2][2]) {
+  const char* buf = c.lds + (t & 1) * NT_BUF;
+  using P = NtPlan<POS>;
+#define NT_SPHASE_TAIL(Q, I0, J0, FA, FB)                          \
+  if constexpr (P::issue(Q)) nt_stage_cursor<LAY>(c, st, cur);     \
+  nt_vm<P::wait(Q)>();                                             \
+  nt_mma_begin();                                                  \
+  nt_quad<I0, J0>(acc, FA, FB);                                    \
+  nt_mma_end();
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb[0][j][ks] = nt_fragment<NtLay<LAY>::BT>(buf + 1 * NT_HALF, c.rb + j * 16, ks, c.lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fa[0][i][ks] = nt_fragment<false>(buf + 0 * NT_HALF, c.ra + i * 16, ks, c.lane);
+  NT_SPHASE_TAIL(0, 0, 0, fa[0], fb[0])
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb[1][j][ks] = nt_fragment<NtLay<LAY>::BT>(buf + 2 * NT_HALF, c.rb + j * 16, ks, c.lane);
+  NT_SPHASE_TAIL(1, 0, 2, fa[0], fb[1])
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fa[1][i][ks] = nt_fragment<false>(buf + 3 * NT_HALF, c.ra + i * 16, ks, c.lane);
+  NT_SPHASE_TAIL(2, 4, 2, fa[1], fb[1])
+  NT_SPHASE_TAIL(3, 4, 0, fa[1], fb[0])
+#undef NT_SPHASE_TAIL
+}
+
+template <int EPI, int LAY>
+__global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_stream_kernel(NtArgs a, int P) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * NT_BUF];    // 128 KiB, the only LDS object
+  const int tiles_n = a.N / NT_BN;
+  const int tiles = (a.M / NT_BM) * tiles_n;
+  const int wg = blockIdx.x;
+  const int my_tiles = wg < tiles ? (tiles - wg + P - 1) / P : 0;
+  const int nk = a.K / NT_BK;
+  NtStream st{nk, my_tiles * nk, tiles_n, tiles, P, wg};
+  if (my_tiles == 0) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  NtCtx c{a.A, a.B, a.lda, a.ldb, 0, 0, 0, lds, wave, lane, wr * 64, wc * 32, 0, 0, 0, 0, -1};
+  c.offa0 = nt_lane_off(a.lda, 0, lane);
+  c.offa1 = nt_lane_off(a.lda, 1, lane);
+  if constexpr (NtLay<LAY>::BT) {
+    c.offb0 = c.offb1 = tn_lane_off(a.ldb, wave, lane, false);
+  } else {
+    c.offb0 = nt_lane_off(a.ldb, 0, lane);
+    c.offb1 = nt_lane_off(a.ldb, 1, lane);
+  }
+  NtCursor cur{0, 0, 0, 0, 0, 0};
+  st.tile_origin(0, cur.m0, cur.n0);
+  long m0 = cur.m0, n0 = cur.n0;      // origin of the tile being multiplied
+  int jt = 0, kin = 0;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  NtEpiPre<4> epre;
+  nt_preload_bias<EPI, 4>(a, n0 + wc * 64 + (lane >> 4) * 4, epre);
+  nt_s16x8 fa[2][4][2];
+  nt_s16x8 fb[2][2][2];
+
+  // prologue: the first K-tile and half of the second (six halves), as in the one-tile kernel
+#pragma unroll
+  for (int v = 0; v < 6; ++v) nt_stage_cursor<LAY>(c, st, cur);
+  if (st.total_k > 1) nt_vm<8>(); else nt_vm<4>();
+  nt_bar();
+  if (wr == 1) nt_bar();                                 // group 1 runs one barrier behind
+
+  // after each K-tile: when an output tile is complete, store it (the next tile's DMAs are
+  // already in flight), clear the accumulators and load the next tile's bias
+  auto finish_k = [&]() {
+    if (++kin != nk) return;
+    const long emrow = m0 + wr * 128 + (lane & 15), encol = n0 + wc * 64 + (lane >> 4) * 4;
+    nt_epilogue<EPI, false, 4>(a, acc, emrow, encol, lane, 0, epre);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kin = 0;
+    if (++jt < my_tiles) {
+      st.tile_origin(jt, m0, n0);
+      nt_preload_bias<EPI, 4>(a, n0 + wc * 64 + (lane >> 4) * 4, epre);
+    }
+  };
+  // steady state, then the two draining K-tiles of the whole stream (one ktile variant per
+  // loop: branching between variants inside one loop body spills the fragment registers)
+  const int T = st.total_k;
+  int t = 0;
+  for (; t < T - 2; ++t) {
+    nt_ktile_stream<0, LAY>(c, st, cur, t, acc, fa, fb);
+    finish_k();
+  }
+  if (T >= 2) {
+    nt_ktile_stream<1, LAY>(c, st, cur, t, acc, fa, fb);
+    finish_k();
+    ++t;
+  }
+  nt_ktile_stream<2, LAY>(c, st, cur, t, acc, fa, fb);
+  finish_k();
+  if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
+}
+
 }  // namespace ct
 
 using namespace ct;
+
+static int nt_cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// Streamed persistent GEMM: D[M,N] (+)= A[M,K] . B^T (b_kn = 0: B [N,K]; 1: B [K,N]) with
+// epilogue 0 (plain; accumulate: D += result) or 5 (+ bias[N]).  One workgroup per CU (or fewer when
+// there are fewer tiles).  Nonzero (nothing launched) when unsupported.
+extern "C" int ct_gemm_nt_stream(const void* A, long lda, const void* B, long ldb, void* D, long ldd, int M, int N,
+                                 int K, int epi, const void* bias, int b_kn, int wgs, int accumulate,
+                                 hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % NT_BM || N % NT_BN || K % NT_BK) return 1;
+  if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < (b_kn ? N : K) || ldd < N) return 2;
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 15)) return 3;
+  if (epi != 0 && epi != 5) return 6;
+  if (epi == 5 && (!bias || ((uintptr_t)bias & 7))) return 4;
+  const long tiles = (long)(M / NT_BM) * (N / NT_BN);
+  if (tiles > (1L << 30)) return 5;
+  const int P = (int)std::min<long>(tiles, wgs > 0 ? wgs : nt_cu_count());
+  if (accumulate && epi != 0) return 6;
+  NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, nullptr, nullptr, nullptr,
+           nullptr, lda, ldb, ldd, 0, 0, M, N, K, accumulate ? 1 : 0};
+  if (epi == 5) {
+    if (b_kn) gemm_nt_stream_kernel<NT_EPI_BIAS, 2><<<P, NT_THREADS, 0, stream>>>(a, P);
+    else gemm_nt_stream_kernel<NT_EPI_BIAS, 0><<<P, NT_THREADS, 0, stream>>>(a, P);
+  } else {
+    if (b_kn) gemm_nt_stream_kernel<NT_EPI_PLAIN, 2><<<P, NT_THREADS, 0, stream>>>(a, P);
+    else gemm_nt_stream_kernel<NT_EPI_PLAIN, 0><<<P, NT_THREADS, 0, stream>>>(a, P);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
 
 // D[M,N] = A[M,K] . B[N,K]^T (row-major, K-contiguous operands) with epilogue `epi`:
 //   0: plain (accumulate: D += result); 1: aux = result + bias, D = gelu(aux);
@@ -605,6 +830,7 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < (b_kn ? N : K) || ldd < N) return 2;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 15)) return 3;
   if (epi == 1 && (!bias || !aux || ((uintptr_t)bias & 7))) return 4;
+  if (epi == 5 && (!bias || ((uintptr_t)bias & 7))) return 4;
   if ((epi == 1 || epi == 2) && (!aux || ((uintptr_t)aux & 15) || ldaux % 8 || ldaux < N)) return 4;
   if (bias && ((uintptr_t)bias & 7)) return 4;
   const long blocks = (long)(M / NT_BM) * (N / NT_BN);
@@ -635,6 +861,7 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
       if (dbias) NT_LAUNCH(2, true);
       else NT_LAUNCH(2, false);
       break;
+    case 5: NT_LAUNCH(5, false); break;
     default: return 6;
   }
 #undef NT_LAUNCH

@@ -95,6 +95,35 @@ def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f):
     return dz
 
 
+# Plain forward / data-gradient GEMMs through the streamed persistent MFMA kernel
+# (csrc/gemm_nt.hip gemm_nt_stream_kernel: one workgroup per CU, one continuous K-tile DMA
+# stream across its tiles, epilogue stores overlapped with the next tile's loads) instead of
+# hipBLASLt.  Comma list of sites (qkv, wo, ffn2, do, dx_attn, dx_ffn), "all" or "" (none);
+# bench/gemm_stream_probe.py measures each shape against hipBLASLt.
+_STREAM_SITES = os.environ.get("CLOUDTIK_AMD_STREAM_GEMM", "")
+_STREAM_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _STREAM_SITES == "all"
+                 else {t for t in _STREAM_SITES.split(",") if t})
+
+
+def _stream_mm(site, A, B, b_kn, bias=None, out=None):
+    """A [M,K] . B^T (b_kn False: B [N,K]) or A . B (b_kn True: B [K,N]) [+ bias], or
+    ``out += A . B`` when ``out`` is given.  None when the site is not routed or the shape
+    is outside the kernel's tiling (M, N multiples of 256, K of 64)."""
+    if site not in _STREAM_SITES:
+        return None
+    M, K = A.shape
+    N = B.shape[1] if b_kn else B.shape[0]
+    if M % 256 or N % 256 or K % 64 or not A.is_contiguous() or not B.is_contiguous():
+        return None
+    if bias is not None and (bias.dtype != torch.bfloat16 or not bias.is_contiguous()):
+        return None
+    acc = out is not None
+    D = out if acc else torch.empty(M, N, device=A.device, dtype=A.dtype)
+    if not _C().gemm_nt_stream(A, B, D, bias, b_kn, 0, acc):
+        return None
+    return D
+
+
 def _flat(p) -> bool:
     return p.grad is not None and getattr(p, "_ct_flat_grad", False)
 
@@ -135,13 +164,17 @@ class _AttnBlockFn(torch.autograd.Function):
         B, S, H = x.shape
         D = H // nh
         x2 = x.reshape(B * S, H)
-        qkv = torch.addmm(bqkv, x2, Wqkv.t())
+        qkv = _stream_mm("qkv", x2, Wqkv, False, bias=bqkv)
+        if qkv is None:
+            qkv = torch.addmm(bqkv, x2, Wqkv.t())
         v5 = qkv.view(B, S, 3, nh, D)
         o = torch.empty(B, S, nh, D, dtype=x.dtype, device=x.device)
         scale = 1.0 / math.sqrt(D)
         lse = C.attn_fwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], o, key_bias, scale, p_attn,
                          seed_a, off_a, False)
-        a = torch.mm(o.view(B * S, H), Wo.t())
+        a = _stream_mm("wo", o.view(B * S, H), Wo, False)
+        if a is None:
+            a = torch.mm(o.view(B * S, H), Wo.t())
         y, s, mean, rstd = C.layernorm_fwd(a, bo, x2, g1, b1, eps, False, p_hid, seed_h, off_h)
         ctx.save_for_backward(x2, qkv, o, lse, s, mean, rstd,
                               key_bias if key_bias is not None else torch.empty(0))
@@ -171,7 +204,10 @@ class _AttnBlockFn(torch.autograd.Function):
         _ready(*[p for p, f in ((g1, fg1), (b1, fb1), (bo, fbo)) if f])
         o2 = o.view(B * S, H)
         dWo = _wgrad(Wo, da, o2)
-        do = torch.mm(da, Wo).view(B, S, nh, D)
+        do = _stream_mm("do", da, Wo, True)
+        if do is None:
+            do = torch.mm(da, Wo)
+        do = do.view(B, S, nh, D)
         dqkv = torch.empty_like(qkv)
         v5 = qkv.view(B, S, 3, nh, D)
         d5 = dqkv.view(B, S, 3, nh, D)
@@ -185,7 +221,9 @@ class _AttnBlockFn(torch.autograd.Function):
             if fbq:
                 _ready(bqkv)
             dWqkv = _wgrad(Wqkv, dqkv, x2)
-        dx = ds.addmm_(dqkv, Wqkv)        # residual grad fused: in-place beta=1 epilogue, no C copy
+        dx = _stream_mm("dx_attn", dqkv, Wqkv, True, out=ds)
+        if dx is None:
+            dx = ds.addmm_(dqkv, Wqkv)    # residual grad fused: in-place beta=1 epilogue, no C copy
         return (dx.view(B, S, H), dWqkv, None if fbq else dbq, dWo, None if fbo else dbo,
                 None if fg1 else dg1, None if fb1 else db1, None, None, None, None, None,
                 None, None, None, None)
@@ -203,7 +241,9 @@ class _FFNBlockFn(torch.autograd.Function):
         else:
             z = torch.mm(x2, W1.t())
             h = C.bias_act_fwd(z, b1f, 1)
-        f = torch.mm(h, W2.t())
+        f = _stream_mm("ffn2", h, W2, False)
+        if f is None:
+            f = torch.mm(h, W2.t())
         y, s, mean, rstd = C.layernorm_fwd(f, b2f, x2, g2, b2, eps, False, p_hid, seed_h, off_h)
         ctx.save_for_backward(x2, z, h, s, mean, rstd)
         ctx.params = (W1, b1f, W2, b2f, g2, b2)
@@ -236,7 +276,9 @@ class _FFNBlockFn(torch.autograd.Function):
         if fb1f:
             _ready(b1f)
         dW1 = _wgrad(W1, dz, x2)
-        dx = ds.addmm_(dz, W1)
+        dx = _stream_mm("dx_ffn", dz, W1, True, out=ds)
+        if dx is None:
+            dx = ds.addmm_(dz, W1)
         return (dx.view(B, S, H), dW1, None if fb1f else db1f, dW2, None if fb2f else db2f,
                 None if fg2 else dg2, None if fb2 else db2, None, None, None, None)
 

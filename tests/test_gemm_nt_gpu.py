@@ -211,3 +211,35 @@ def test_gemm_tn2_bias_column_sums(M, N, K, S):
         torch.testing.assert_close(P.sum(0), ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
     want = torch.stack([A[k0:k1].float().sum(0) for k0, k1 in _split_ranges(K, S)])
     torch.testing.assert_close(bP, want, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K,wgs", [(256, 256, 64, 0), (512, 256, 128, 1), (1024, 768, 192, 5),
+                                       (2048, 1024, 1024, 0), (1536, 512, 320, 3), (4096, 3072, 1024, 0)])
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_nt_stream_matches_reference(M, N, K, wgs, b_kn):
+    """Streamed persistent kernel: every workgroup walks several output tiles with one DMA
+    stream (wgs < tiles forces several tiles per workgroup, including uneven tails and single
+    K-tile streams); NT and NN (B stored [K, N]) layouts, with and without bias."""
+    C = _C()
+    A = _rand(M, K, seed=11)
+    B = _rand(K, N, scale=K ** -0.5, seed=12) if b_kn else _rand(N, K, scale=K ** -0.5, seed=12)
+    bias = _rand(N, scale=0.5, seed=13)
+    ref = A.float() @ (B.float() if b_kn else B.float().t())
+    D = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nt_stream(A, B, D, None, b_kn, wgs)
+    torch.cuda.synchronize()
+    _close(D, ref)
+    D.fill_(float("nan"))
+    assert C.gemm_nt_stream(A, B, D, bias, b_kn, wgs)
+    _close(D, ref + bias.float())
+    base = _rand(M, N, seed=14)
+    D2 = base.clone()
+    assert C.gemm_nt_stream(A, B, D2, None, b_kn, wgs, True)            # D += A B
+    _close(D2, ref + base.float())
+
+
+def test_gemm_nt_stream_refuses_unsupported():
+    C = _C()
+    A, B = _rand(300, 64), _rand(256, 64)
+    D = torch.empty(300, 256, device="cuda", dtype=torch.bfloat16)
+    assert not C.gemm_nt_stream(A, B, D, None, False, 0)

@@ -400,9 +400,10 @@ def test_wgrad_splitk_accumulate(cuda, N, K):
     assert _rel(g2, ref) < 5e-3
 
 
-@pytest.mark.parametrize("p,fused,fused_fwd", [(0.0, False, False), (0.1, False, False), (0.1, True, False),
-                                              (0.1, False, True), (0.1, True, True)])
-def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, monkeypatch):
+@pytest.mark.parametrize("p,fused,fused_fwd,stream", [(0.0, False, False, False), (0.1, False, False, False),
+                                                     (0.1, True, False, False), (0.1, False, True, False),
+                                                     (0.1, True, True, False), (0.1, True, True, True)])
+def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, stream, monkeypatch):
     """Hand-scheduled block backward == composed-op autograd (same dropout streams); `fused`
     routes the FFN dgrad through the MFMA GEMM with the dGELU + bias-gradient epilogue,
     `fused_fwd` the FFN1 forward through it with the bias + GELU epilogue (the kept
@@ -411,6 +412,16 @@ def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, monkeypatch
     from cloudtik_amd.ops import transformer as T
     monkeypatch.setattr(T, "_FUSED_FFN_DGRAD", fused)
     monkeypatch.setattr(T, "_FUSED_FFN_FWD", fused_fwd)
+    stream_sites = []
+    if stream:                             # every plain fwd / dgrad GEMM through the streamed kernel
+        monkeypatch.setattr(T, "_STREAM_SITES", {"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"})
+        orig_stream = T._stream_mm
+        def spy_stream(site, *a, **k):
+            r = orig_stream(site, *a, **k)
+            if r is not None:
+                stream_sites.append(site)
+            return r
+        monkeypatch.setattr(T, "_stream_mm", spy_stream)
     if fused_fwd:
         fwd_calls = []
         orig_fwd = T._fused_ffn1
@@ -462,6 +473,8 @@ def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, monkeypatch
         assert calls and all(calls), "fused FFN dgrad path not taken"
     if fused_fwd:
         assert fwd_calls and all(fwd_calls), "fused FFN1 forward path not taken"
+    if stream:
+        assert set(stream_sites) == {"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"}, stream_sites
 
 
 @pytest.mark.parametrize("name", ["adamw", "lamb"])
