@@ -14,6 +14,7 @@ int ct_conv_igemm_bn(const void*, int, int, int, const void*, void*, int, int, i
                      int, hipStream_t);
 int ct_conv_igemm_rows(int, int, int, int);
 int ct_conv_igemm_tile_m(int);
+void ct_conv_stream_set_cus(int);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
 int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
                   int, int, hipStream_t);
@@ -162,6 +163,8 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
   m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
   m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
+  m.def("conv_stream_set_cus", [](int64_t cus) { ct_conv_stream_set_cus((int)cus); },
+        "streamed conv kernels: persistent workgroups = cus x per-CU count (0: the device's CUs)");
   m.def("conv_igemm_tile_m", &conv_igemm_tile_m, "rows per tile of the chosen conv configuration");
   m.def("bn_partials_finalize", &bn_partials_finalize, "Chan merge of per-tile (mean, M2) -> mean, var");
 }

@@ -28,6 +28,7 @@
 // Reference workload: torchvision ResNet-50 training, channels_last bf16
 // (applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296).
 #include "common.h"
+#include <algorithm>
 
 namespace ct {
 
@@ -386,6 +387,328 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
 }
 
 // ------------------------------------------------------------------------------------------
+// Streamed persistent variant of conv_igemm_kernel.  Grid = WPC workgroups per CU (or fewer
+// when there are fewer tiles); workgroup w walks the tiles w, w + P, w + 2P, ... of the
+// XCD-remapped tile order, and its K-steps form ONE stream over (tile, K-step): the LDS ring
+// keeps NS - 1 stages in flight ACROSS tile boundaries, so the next tile's first stages land
+// while this tile's epilogue runs.  A 1x1 convolution over 64 channels has ONE K-step per tile
+// and the one-tile kernel pays a cold DMA latency plus an idle epilogue for each.
+//   * the gather descriptors (pixel bases of the A rows, weight row bases) belong to the tile
+//     the DMA cursor is in, recomputed when the cursor crosses a tile boundary;
+//   * the epilogue re-lays the bf16 tile through the ring slot the tile's last K-step just
+//     read (free until the next step's barrier + issue; 16-B chunks XOR-swizzled by row instead
+//     of the padded rows of the one-tile kernel, so the image fits the slot exactly);
+//   * epilogue stores and loads are younger than the in-flight DMAs: the counted vmcnt waits
+//     of the following K-steps only ever wait for more than they need.
+template <int BM, int BN, int WGM, int WGN, int NS, int WPC, int EPI>
+__global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvArgs a, int P) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int IA = BM / (8 * NW), IB = BN / (8 * NW), G = IA + IB;
+  constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;         // copy-out: 16-B chunks per row, rows per pass
+  constexpr int REDB = EPI == 1 ? WGM * BN * 4 : 16;
+  static_assert(IA * 8 * NW == BM && IB * 8 * NW == BN, "tile / wave mismatch");
+  static_assert(NS >= 2 && NS <= 4 && WPC * (NS * STAGE + REDB) <= 160 * 1024, "LDS ring");
+  static_assert(BM * BN * 2 <= STAGE && (CPR == 8 || CPR == 16), "epilogue image in one ring slot");
+  static_assert(EPI != 2 || 2 * RPP * BN * 4 <= STAGE, "EPI 2 reduction in one ring slot");
+  __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE + REDB];
+
+  const int ntn = a.Co / BN;
+  const int tiles = ((a.M + BM - 1) / BM) * ntn;
+  const int wg = blockIdx.x;
+  if (wg >= tiles) return;
+  const int my_tiles = (tiles - wg + P - 1) / P;
+  const int KT = a.T * a.cpt;
+  const int total = my_tiles * KT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int HW = a.Hr * a.Wr;
+  const long ldw = (long)a.T * a.cpt * 64;
+  const int cpt = a.cpt;
+
+  // tile-invariant parts of the gather: the lane's rows inside the tile and their swizzled chunk
+  int gpx[IA];
+  unsigned gca[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = (wave * IA + j) * 8 + (lane >> 3);
+    const int gc = (lane & 7) ^ cv_swz(row);
+    gca[j] = (unsigned)gc * 8u;
+    gpx[j] = a.pixchunk ? gc : 0;
+  }
+  unsigned woff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par)
+    woff[par] = (unsigned)(((lane >> 3) * ldw + (((lane & 7) ^ ((4 * par + ((lane >> 3) >> 1)) & 7)) * 8)) * 2);
+
+  // DMA cursor: tile index cj of this workgroup's sequence, K-step ck inside it, stream index cg
+  int cj = 0, ck = 0, cg = 0;
+  int pix[IA], iy0[IA], ix0[IA];
+  const bf16_t* wbase[IB];
+  auto cursor_tile = [&](int j) {
+    const int L = xcd_remap(j * P + wg, tiles);
+    const int m0 = (L / ntn) * BM, n0 = (L % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int m = m0 + (wave * IA + i) * 8 + (lane >> 3);
+      if (m < a.M) {
+        const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+        iy0[i] = y * a.sy;
+        ix0[i] = x * a.sx;
+        pix[i] = ((b * a.Hi + iy0[i]) * a.Wi + ix0[i]) * a.Ci;
+      } else {
+        iy0[i] = -(1 << 20);
+        ix0[i] = 0;
+        pix[i] = 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) wbase[i] = a.W + (long)(n0 + (wave * IB + i) * 8) * ldw;
+  };
+  auto stage_next = [&]() {
+    if (cg >= total) return;
+    const int slot = cg % NS;
+    const int t = ck / cpt, c0 = (ck - t * cpt) << 6;
+    const int dy = (int)((a.tdy >> (4 * t)) & 15) - 8, dx = (int)((a.tdx >> (4 * t)) & 15) - 8;
+    const int toff = (dy * a.Wi + dx) * a.Ci + c0;
+    char* As = lds + slot * STAGE;
+    char* Bs = As + BM * 128;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int iy = iy0[j] + dy, ix = ix0[j] + dx + gpx[j];
+      const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+      const void* src = ok ? (const void*)(a.X + (long)(pix[j] + toff) + gca[j]) : (const void*)cv_zero_page;
+      cv_glds16(src, As + (wave * IA + j) * 1024);
+    }
+    const long k0 = (long)t * cpt * 64 + c0;
+#pragma unroll
+    for (int j = 0; j < IB; ++j) cv_glds16s(wbase[j] + k0, woff[(wave * IB + j) & 1], Bs + (wave * IB + j) * 1024);
+    ++cg;
+    if (++ck == KT) {
+      ck = 0;
+      if (++cj < my_tiles) cursor_tile(cj);
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  cursor_tile(0);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) stage_next();
+
+  float* red = (float*)(lds + NS * STAGE);                  // EPI 1: [WGM][BN] statistics scratch
+  int jt = 0, kin = 0;
+  for (int g = 0; g < total; ++g) {
+    const int ahead = total - 1 - g;
+    cv_wait_stage<G, NS>(ahead < NS - 2 ? ahead : NS - 2);
+    cv_bar();
+    stage_next();
+    const char* As = lds + (g % NS) * STAGE;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      cv_s16x8 fa[MI], fb[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = cv_frag(As, wm * WM + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = cv_frag(Bs, wn * WN + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb[j], (bf16x8_t)fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (++kin != KT) continue;
+
+    // ---- epilogue of tile jt (same math as conv_igemm_kernel; image in ring slot g % NS)
+    kin = 0;
+    const int L = xcd_remap(jt * P + wg, tiles);
+    const int tm = L / ntn, tn = L % ntn;
+    const int m0 = tm * BM, n0 = tn * BN;
+    char* ot = lds + (g % NS) * STAGE;
+    auto ot_chunk = [&](int row, int chunk) -> char* {
+      return ot + row * (BN * 2) + ((chunk ^ ((CPR == 8 ? row >> 1 : row) & (CPR - 1))) << 4);
+    };
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    cv_bar();                                             // every wave is done reading the slot
+    bool rv[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * WM + 16 * i + (lane & 15);
+      rv[i] = m0 + row < a.M;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        u16x4 out;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          out[r] = f2bf(acc[i][j][r]);
+          if constexpr (EPI == 1) acc[i][j][r] = rv[i] ? bf2f(out[r]) : 0.f;
+        }
+        const int col = wn * WN + 16 * j + 4 * (lane >> 4);
+        *(u16x4*)(ot_chunk(row, col >> 3) + (col & 7) * 2) = out;
+      }
+    }
+    if constexpr (EPI == 1) {
+      const int nrows = min(BM, a.M - m0);
+      float cs[NJ][4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = 0.f;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) v += acc[i][j][r];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
+        }
+      __syncthreads();
+      float mean[NJ][4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
+          float sum = 0.f;
+#pragma unroll
+          for (int w = 0; w < WGM; ++w) sum += red[w * BN + c];
+          mean[j][r] = sum / (float)nrows;
+          float q = 0.f;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const float d = acc[i][j][r] - mean[j][r];
+            q += rv[i] ? d * d : 0.f;
+          }
+          cs[j][r] = q;
+        }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = cs[j][r];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
+        }
+      __syncthreads();
+      if (wm == 0 && (lane & 15) == 0) {
+        const long tiles_m = (a.M + BM - 1) / BM;
+        float* pm = a.part + (long)tm * a.Co;
+        float* pq = a.part + (tiles_m + tm) * (long)a.Co;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
+            float q = 0.f;
+#pragma unroll
+            for (int w = 0; w < WGM; ++w) q += red[w * BN + c];
+            pm[n0 + c] = mean[j][r];
+            pq[n0 + c] = q;
+          }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    const int cc = tid % CPR;
+    float bmu[8], bis[8], bfa[8], bfb[8], s1[8], s2[8];
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = n0 + cc * 8 + e;
+        bmu[e] = a.bnstat[c];
+        bis[e] = a.bnstat[a.Co + c];
+        bfa[e] = a.bnstat[2 * a.Co + c];
+        bfb[e] = a.bnstat[3 * a.Co + c];
+        s1[e] = 0.f;
+        s2[e] = 0.f;
+      }
+    }
+#pragma unroll 4
+    for (int row = tid / CPR; row < BM; row += RPP) {
+      const int m = m0 + row;
+      if (m >= a.M) break;
+      const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+      const long yo = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+      bf16_t* yp = a.Y + yo;
+      u16x8 v = *(const u16x8*)ot_chunk(row, cc);
+      if (a.accumulate) {
+        const u16x8 old = *(const u16x8*)yp;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(old[e]));
+      }
+      if constexpr (EPI == 2) {
+        const u16x8 xv = *(const u16x8*)(a.bnx + yo);
+        const u16x8 yv = a.bny ? *(const u16x8*)(a.bny + yo) : u16x8(0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xf = bf2f(xv[e]);
+          const bool on = a.bny ? bf2f(yv[e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
+          if (!on) v[e] = 0;
+          const float d = bf2f(v[e]);
+          s1[e] += d;
+          s2[e] += d * (xf - bmu[e]) * bis[e];
+        }
+      }
+      *(u16x8*)yp = v;
+    }
+    if constexpr (EPI == 2) {
+      float* r1 = (float*)ot;
+      float* r2 = r1 + RPP * BN;
+      __syncthreads();                                    // every lane is done reading the image
+      const int slot = tid / CPR;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        r1[slot * BN + cc * 8 + e] = s1[e];
+        r2[slot * BN + cc * 8 + e] = s2[e];
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += 64 * NW) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll 8
+        for (int q = 0; q < RPP; ++q) {
+          t1 += r1[q * BN + c];
+          t2 += r2[q * BN + c];
+        }
+        float* pp = a.bnp + (long)(a.bntile0 + tm) * a.Co + n0 + c;
+        pp[0] = t1;
+        pp[a.bnp2] = t2;
+      }
+    }
+    ++jt;
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int WPC, bool WITH_BN = false>
+static int cs_launch(const ConvArgs& a, int epi, int cus, hipStream_t s) {
+  const long tiles = (long)ceil_div(a.M, BM) * (a.Co / BN);
+  if (tiles > (1L << 30)) return 5;
+  const int P = (int)std::min<long>(tiles, (long)cus * WPC);
+  if (epi == 1)
+    conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, 1><<<P, 64 * WGM * WGN, 0, s>>>(a, P);
+  else if (epi == 2) {
+    if constexpr (WITH_BN) conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, 2><<<P, 64 * WGM * WGN, 0, s>>>(a, P);
+    else return 6;
+  } else
+    conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, 0><<<P, 64 * WGM * WGN, 0, s>>>(a, P);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+// ------------------------------------------------------------------------------------------
 // Weight gradient: dW[co][t * Ci + c] = sum_m dY[m][co] * X[pixel(m) + tap_t][c]
 // a "TN" GEMM whose reduction runs over the pixels (the row index of both NHWC operands):
 //   * BK = 32 pixels per stage; both tiles are staged row-major ([pixel][channel], as in memory)
@@ -596,6 +919,8 @@ using namespace ct;
 //   0: 256x64  4w NS3      1: 256x128 8w NS3      2: 128x128 4w NS4      3: 128x64 4w NS4
 //   4: 256x64  4w NS2 x2   5: 128x128 4w NS2 x2   6: 256x64  8w NS3      7: 128x64 4w NS2 x2
 //   8: 128x64  4w NS2 x3   9: 64x128  4w NS2 x3
+// streamed persistent (conv_stream_kernel; workgroups per CU, ring slots):
+//  10: 128x128 4w NS4 x1  11: 128x128 4w NS2 x2  12: 128x64 4w NS3 x2  13: 64x128 4w NS3 x2
 // -1 = pick by shape: short reductions (<= 4 K-steps of 64) want two workgroups per CU so one
 // tile's epilogue overlaps another's loads; long ones want the deeper ring.
 extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
@@ -609,8 +934,23 @@ extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
 }
 
 extern "C" int ct_conv_igemm_tile_m(int cfg) {
-  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : (cfg == 9 ? 64 : 128);
+  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : ((cfg == 9 || cfg == 13) ? 64 : 128);
 }
+
+static int g_cv_stream_cus = 0;      // test / probe override of the streamed kernels' CU count
+
+static int cv_cu_count() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    return v;
+  }();
+  return g_cv_stream_cus > 0 ? g_cv_stream_cus : n;
+}
+
+// streamed conv kernels: workgroups = cus x (workgroups per CU); 0 restores the device's CU count
+extern "C" void ct_conv_stream_set_cus(int cus) { g_cv_stream_cus = cus > 0 ? cus : 0; }
 
 // Y = implicit-GEMM conv (see the file comment).  `taps` = T (dy, dx) pairs in [-8, 7].
 // Returns nonzero (launching nothing) on an unsupported shape.
@@ -675,13 +1015,17 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   }
   const int epi = bn ? 2 : (part ? 1 : 0);
   cfg = ct_conv_igemm_rows(cfg, Co, M, T * a.cpt);
-  if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9) && Co % 128) return 2;
+  if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9 || cfg == 10 || cfg == 11 || cfg == 13) && Co % 128) return 2;
   if (epi == 2) {
     // the default (shape-picked) configurations only: the others are not instantiated with EPI 2
     switch (cfg) {
       case 5: return cv_launch<128, 128, 2, 2, 2, 2, true>(a, epi, stream);
       case 8: return cv_launch<128, 64, 2, 2, 2, 3, true>(a, epi, stream);
       case 9: return cv_launch<64, 128, 1, 4, 2, 3, true>(a, epi, stream);
+      case 10: return cs_launch<128, 128, 2, 2, 4, 1, true>(a, epi, cv_cu_count(), stream);
+      case 11: return cs_launch<128, 128, 2, 2, 2, 2, true>(a, epi, cv_cu_count(), stream);
+      case 12: return cs_launch<128, 64, 2, 2, 3, 2, true>(a, epi, cv_cu_count(), stream);
+      case 13: return cs_launch<64, 128, 1, 4, 3, 2, true>(a, epi, cv_cu_count(), stream);
       default: return 6;
     }
   }
@@ -696,6 +1040,10 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
     case 7: return cv_launch<128, 64, 2, 2, 2, 2>(a, epi, stream);
     case 8: return cv_launch<128, 64, 2, 2, 2, 3>(a, epi, stream);
     case 9: return cv_launch<64, 128, 1, 4, 2, 3>(a, epi, stream);
+    case 10: return cs_launch<128, 128, 2, 2, 4, 1>(a, epi, cv_cu_count(), stream);
+    case 11: return cs_launch<128, 128, 2, 2, 2, 2>(a, epi, cv_cu_count(), stream);
+    case 12: return cs_launch<128, 64, 2, 2, 3, 2>(a, epi, cv_cu_count(), stream);
+    case 13: return cs_launch<64, 128, 1, 4, 3, 2>(a, epi, cv_cu_count(), stream);
     default: return 6;
   }
 }

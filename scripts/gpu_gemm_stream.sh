@@ -12,4 +12,12 @@ tail -3 "$O/tests.txt"
 timeout -k 10 300 python -u bench/gemm_stream_probe.py --rounds 5 --iters 20 > "$O/probe.jsonl" 2> "$O/probe.md"
 rc=$?
 tail -12 "$O/probe.md"
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+# BERT-large A/B: hipBLASLt forward / dgrad GEMMs vs every site on the streamed kernel (two rounds)
+for r in 1 2; do
+  for v in "" all; do
+    CLOUDTIK_AMD_STREAM_GEMM=$v timeout -k 10 240 python -u bench.py --model bert-large --steps 20 --warmup 5 \
+      > "$O/bert_stream_${v:-off}_$r.json" 2> "$O/bert_stream_${v:-off}_$r.err" || exit $?
+    echo "stream=${v:-off} round $r: $(grep -o '"ms_per_step": [0-9.]*' "$O/bert_stream_${v:-off}_$r.json")"
+  done
+done

@@ -277,3 +277,74 @@ def test_dgrad_weight_cache_matches_direct_transposes():
         torch.testing.assert_close(full, wt.reshape(4, -1) * scale)
         torch.testing.assert_close(sub, torch.stack([wt[:, 0, 0, :], wt[:, 2, 1, :]], 1).reshape(4, -1) * scale)
     assert cache.get(w, full_rs) is None        # outside a backward pass nothing is cached
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [10, 11, 12, 13])
+@pytest.mark.parametrize("ci,co,H,k,s,cus", [(64, 256, 20, 3, 1, 7), (64, 128, 15, 3, 2, 3), (256, 128, 12, 1, 1, 5),
+                                             (128, 256, 9, 1, 2, 0)])
+def test_streamed_conv_kernels_match_fp32_reference(cuda, monkeypatch, cfg, ci, co, H, k, s, cus):
+    """conv.hip conv_stream_kernel (cfg 10-13): forward + BatchNorm tile statistics, data gradient
+    (stride-2 phase plans included) plain and accumulated, with few persistent workgroups
+    (``cus`` x per-CU count) so every workgroup streams several tiles and the DMA ring runs
+    across tile boundaries (tiles mixing in-image rows and the zero-padded tail of M)."""
+    from cloudtik_amd import ops
+    C = ops.require_native()
+    monkeypatch.setattr(CV, "_CFG", cfg)
+    C.conv_stream_set_cus(cus)
+    try:
+        torch.manual_seed(ci + co + H + cfg)
+        pad = k // 2
+        x = _nhwc(torch.randn(5, ci, H, H, device=cuda).to(torch.bfloat16))
+        w = _nhwc((torch.randn(co, ci, k, k, device=cuda) * (2.0 / (ci * k * k)) ** 0.5).to(torch.bfloat16))
+        xr = x.float().requires_grad_()
+        ref = F.conv2d(xr, w.float(), stride=s, padding=pad)
+        dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
+        ref.backward(dy.float())
+        y, mean, var = CV.conv_fwd(x, w, (s, s), (pad, pad), stats=True)
+        assert _rel(y, ref) < 1e-2
+        yb = y.float()
+        torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(var, yb.var((0, 2, 3), unbiased=False), rtol=1e-3, atol=1e-6)
+        if ci % 128 == 0 or cfg == 12:            # dgrad output channels = ci
+            dx = CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad))
+            assert _rel(dx, xr.grad) < 1e-2
+            other = _nhwc(torch.randn(x.shape, device=cuda).to(torch.bfloat16))
+            acc = CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad), out=other.clone(), accumulate=True)
+            assert _rel(acc, xr.grad + other.float()) < 1e-2
+    finally:
+        C.conv_stream_set_cus(0)
+
+
+@pytest.mark.gpu
+def test_streamed_conv_bn_backward_epilogue(cuda, monkeypatch):
+    """EPI 2 (BatchNorm + ReLU backward reduction in the data-gradient epilogue) on the streamed
+    128 x 64 kernel with 3 persistent workgroups per CU slot: the gradients equal the separate
+    reduction pass."""
+    from cloudtik_amd import ops
+    from cloudtik_amd.models.resnet import Bottleneck
+    C = ops.require_native()
+    monkeypatch.setattr(CV, "_CFG", 12)
+    C.conv_stream_set_cus(3)
+    try:
+        torch.manual_seed(2)
+        kw = dict(device=cuda, dtype=torch.bfloat16)
+        blk = torch.nn.Sequential(Bottleneck(64, 64, 2, downsample=True, **kw),
+                                  Bottleneck(256, 64, 1, downsample=False, **kw)).to(memory_format=torch.channels_last)
+        x0 = _nhwc(torch.randn(4, 64, 20, 20, device=cuda).to(torch.bfloat16))
+
+        def run(fuse):
+            monkeypatch.setattr(CV, "BN_BWD_FUSE", fuse)
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = blk(x)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+            return x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
+
+        gx1, gp1 = run(True)
+        gx0, gp0 = run(False)
+        assert _rel(gx1, gx0) < 1e-2
+        for a, b in zip(gp1, gp0):
+            assert _rel(a, b) < 1e-2
+    finally:
+        C.conv_stream_set_cus(0)
