@@ -286,18 +286,19 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
 
 
 _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
-_WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256)}
+_WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128)}
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
 WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
 
 
 def wgrad_plan(M: int, co: int, nn: int, cfg: int):
-    """(splits, rows per split): about 2048 workgroups, each split a multiple of 32 pixels
+    """(splits, rows per split): about 2048 workgroups, each split a multiple of the stage depth
     and at least 256 deep, the fp32 partials capped at PARTIAL_BYTES."""
     bm, bn = _WG_TILES[cfg]
     tiles = (co // bm) * (nn // bn)
     splits = max(1, min(WGRAD_BLOCKS // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
-    rows = ((M + splits - 1) // splits + 31) // 32 * 32
+    q = 64 if cfg >= 4 else 32                     # pixels per stage of the configuration
+    rows = ((M + splits - 1) // splits + q - 1) // q * q
     return (M + rows - 1) // rows, rows
 
 

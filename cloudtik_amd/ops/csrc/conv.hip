@@ -753,9 +753,11 @@ __device__ __forceinline__ cv_s16x8 wg_frag(const char* img, int col0, int lane)
   return cv_s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BMC, int BNC, int WGM, int WGN, int NS>
+template <int BMC, int BNC, int WGM, int WGN, int NS, int BK = 32>
 __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs a) {
-  constexpr int NW = WGM * WGN, BK = 32;
+  // BK pixels per stage (32 or 64: one or two MFMA k-steps per barrier)
+  constexpr int NW = WGM * WGN;
+  static_assert(BK == 32 || BK == 64, "wgrad stage depth");
   constexpr int ROWA = BMC * 2, ROWB = BNC * 2, LPA = ROWA / 16, LPB = ROWB / 16;
   constexpr int TA = BK * ROWA, TB = BK * ROWB, STG = TA + TB;
   constexpr int GA = TA / (1024 * NW), GB = TB / (1024 * NW), G = GA + GB;
@@ -848,16 +850,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
     if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
     const char* As = lds + (kt % NS) * STG;
     const char* Bs = As + TA;
-    cv_s16x8 fa[MI], fb[NJ];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = wg_frag<ROWA>(As, wm * WM + 16 * i, lane);
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      cv_s16x8 fa[MI], fb[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) fb[j] = wg_frag<ROWB>(Bs, wn * WN + 16 * j, lane);
+      for (int i = 0; i < MI; ++i) fa[i] = wg_frag<ROWA>(As + ks * 32 * ROWA, wm * WM + 16 * i, lane);
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int j = 0; j < NJ; ++j) fb[j] = wg_frag<ROWB>(Bs + ks * 32 * ROWB, wn * WN + 16 * j, lane);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb[j], (bf16x8_t)fa[i], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb[j], (bf16x8_t)fa[i], acc[i][j], 0, 0, 0);
+    }
   }
   // acc[i][j][r] = dW[c0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]
   float* P = a.P + (long)split * a.Co * a.NN;
@@ -870,11 +875,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
   }
 }
 
-template <int BMC, int BNC, int WGM, int WGN, int NS>
+template <int BMC, int BNC, int WGM, int WGN, int NS, int BK = 32>
 static int wg_launch(const WgradArgs& a, int splits, hipStream_t s) {
   const long blocks = (long)(a.Co / BMC) * (a.NN / BNC) * splits;
   if (blocks > (1L << 30)) return 5;
-  conv_wgrad_kernel<BMC, BNC, WGM, WGN, NS><<<(int)blocks, 64 * WGM * WGN, 0, s>>>(a);
+  conv_wgrad_kernel<BMC, BNC, WGM, WGN, NS, BK><<<(int)blocks, 64 * WGM * WGN, 0, s>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
@@ -1097,7 +1102,8 @@ __global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restric
 }
 
 // wgrad tile configurations: 0 = 64x64 (4 waves 2x2), 1 = 64x128 (2x2), 2 = 128x128 (2x2),
-// 3 = 128x256 (8 waves 2x4); -1 = the largest that divides (Co, T*Ci)
+// 3 = 128x256 (8 waves 2x4); 4 / 5 / 6 = cfg 0 / 1 / 2 with 64-pixel stages (two MFMA k-steps per
+// barrier); -1 = the largest that divides (Co, T*Ci)
 extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   if (cfg >= 0) return cfg;
   // per-shape probe over every ResNet-50 conv (profiles/r3/conv_wgrad_cfg.md): the 8-wave
@@ -1139,12 +1145,17 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
-  if ((cfg >= 2 && Co % 128) || (cfg == 3 && a.NN % 256) || (cfg >= 1 && a.NN % 128)) return 2;
+  const int tile = cfg >= 4 ? cfg - 4 : cfg;
+  if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
+  if (cfg >= 4 && rows_per_split % 64) return 2;
   switch (cfg) {
     case 0: return wg_launch<64, 64, 2, 2, 4>(a, splits, stream);
     case 1: return wg_launch<64, 128, 2, 2, 4>(a, splits, stream);
     case 2: return wg_launch<128, 128, 2, 2, 4>(a, splits, stream);
     case 3: return wg_launch<128, 256, 2, 4, 4>(a, splits, stream);
+    case 4: return wg_launch<64, 64, 2, 2, 4, 64>(a, splits, stream);
+    case 5: return wg_launch<64, 128, 2, 2, 4, 64>(a, splits, stream);
+    case 6: return wg_launch<128, 128, 2, 2, 3, 64>(a, splits, stream);
     default: return 6;
   }
 }

@@ -348,3 +348,25 @@ def test_streamed_conv_bn_backward_epilogue(cuda, monkeypatch):
             assert _rel(a, b) < 1e-2
     finally:
         C.conv_stream_set_cus(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wcfg", [4, 5, 6])
+@pytest.mark.parametrize("ci,co,H,k,s", [(128, 128, 15, 3, 2), (128, 128, 12, 1, 1), (64, 256, 10, 3, 1)])
+def test_wgrad_64_pixel_stages_match_fp32_reference(cuda, monkeypatch, wcfg, ci, co, H, k, s):
+    """conv_wgrad_kernel with 64-pixel stages (two MFMA k-steps per barrier; wgrad cfg 4-6),
+    including splits that end inside a stage."""
+    bm, bn = CV._WG_TILES[wcfg]
+    if co % bm or (k * k * ci) % bn:
+        pytest.skip("tile does not divide the weight gradient")
+    monkeypatch.setattr(CV, "_WG_CFG", wcfg)
+    torch.manual_seed(ci + co + wcfg)
+    pad = k // 2
+    x = _nhwc(torch.randn(3, ci, H, H, device=cuda).to(torch.bfloat16))
+    w = _nhwc((torch.randn(co, ci, k, k, device=cuda) * 0.1).to(torch.bfloat16))
+    wr = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wr, stride=s, padding=pad)
+    dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
+    ref.backward(dy.float())
+    dw = CV.conv_wgrad(dy, x, w.shape, (s, s), (pad, pad))
+    assert _rel(dw, wr.grad) < 1e-2
