@@ -111,15 +111,22 @@ def main():
         per = []
         for c in cfgs:
             CV._CFG = c
+            # forward (Co = co) and data gradient (Co = ci) are timed independently: a
+            # configuration may fit one and not the other
             try:
                 tf = timeit(lambda: CV.conv_fwd(x, w, (s, s), (pad, pad)))
+            except RuntimeError:
+                tf = None
+            try:
                 td = timeit(lambda: CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad)))
             except RuntimeError:
+                td = None
+            if tf is None and td is None:
                 continue
-            per.append(f"c{c}:{tf:.0f}/{td:.0f}")
-            if best_f is None or tf < best_f[0]:
+            per.append(f"c{c}:{'-' if tf is None else f'{tf:.0f}'}/{'-' if td is None else f'{td:.0f}'}")
+            if tf is not None and (best_f is None or tf < best_f[0]):
                 best_f = (tf, c)
-            if best_d is None or td < best_d[0]:
+            if td is not None and (best_d is None or td < best_d[0]):
                 best_d = (td, c)
             if c == -1:
                 auto_f, auto_d = tf, td

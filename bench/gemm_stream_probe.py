@@ -10,11 +10,14 @@ calls per round; the median and min over ``--rounds`` rounds are reported, cdna_
 """
 import argparse
 import json
+import os
 import statistics
 import sys
 
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timeit(fn, iters):

@@ -932,9 +932,15 @@ extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
   // measured on MI355X over every ResNet-50 shape at batch 256 (bench/conv_igemm_probe.py,
   // profiles/r3/conv_igemm.md): small tiles with 2-3 workgroups per CU win everywhere; the
   // 1-workgroup configurations (deeper ring) never do
-  (void)M;
+  // r4: the streamed 128 x 128 kernel (cfg 11, two persistent workgroups per CU) wins on the
+  // large-M layers (every ResNet-50 launch with M >= 200704 output rows and Co % 128 == 0:
+  // l2.c1a fwd 145 -> 128 us, dgrad 197 -> 169; l2.c2 dgrad 96 -> 85) and loses on the
+  // 50176-row layer-3/4 launches (profiles/r4/conv_stream_probe.md)
   (void)KT;
-  if (cfg < 0) cfg = Co % 128 ? 8 : (Co == 128 ? 9 : 5);
+  if (cfg < 0) {
+    if (Co % 128 == 0 && M >= 150000) return 11;
+    cfg = Co % 128 ? 8 : (Co == 128 ? 9 : 5);
+  }
   return cfg;
 }
 
@@ -1111,8 +1117,10 @@ extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   // 128 x 128, then 64 x 128 for 64-channel outputs (l1.c1 163 -> 128 us)
   if (Co % 128 == 0 && NN % 256 == 0) return 3;
   if (Co % 128 == 0 && NN % 128 == 0) return 2;
-  if (NN % 128 == 0) return 1;
-  return 0;
+  // the 64-wide tiles serve the layer-1 shapes (802816-pixel reductions): 64-pixel stages win
+  // there (l1.c2 301 -> 289 us, l1.c3 156 -> 142, l1.c1 128 -> 118; profiles/r4/conv_stream_probe.md)
+  if (NN % 128 == 0) return 5;
+  return 4;
 }
 
 // workspace: n fp32 + ceil(n / 1024) tickets, zeroed here

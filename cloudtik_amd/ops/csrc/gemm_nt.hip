@@ -614,7 +614,7 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
 struct NtStream {
   int nk;            // K-tiles per output tile
   int total_k;       // K-tiles of this workgroup's whole stream
-  int tiles_n, tiles, P, wg;
+  int tiles_n, tiles, P, wg, my_tiles;
   __device__ __forceinline__ void tile_origin(int j, long& m0, long& n0) const {
     const int L = xcd_remap(j * P + wg, tiles);
     m0 = (long)(L / tiles_n) * NT_BM;
@@ -622,60 +622,90 @@ struct NtStream {
   }
 };
 
-// DMA cursor: the (output tile, K-tile, slot) of the next half to stage, advanced one slot per
-// staging call (the phases issue halves in stream order).  Wave-uniform, lives in SGPRs.
-struct NtCursor {
-  int j, k, slot, G;
-  long m0, n0;
+// K-tile cursor of the stream: output tile j of this workgroup, K-tile k inside it, with the
+// tile's operand bases (recomputed only when the cursor crosses into the next tile) and the
+// K offsets (A: k0 elements; B: k0 for NT, k0 * ldb for NN).  Wave-uniform: SGPRs.
+struct NtKCur {
+  int j, k;
+  long ka, kb;
+  const bf16_t* arow;   // A + m0 * lda
+  const bf16_t* brow;   // NT: B + n0 * ldb; NN: B + n0
+};
+
+// per-wave staging offsets (elements) of the two pieces a wave stages per half, fixed for the
+// whole kernel: A rows of piece i in A0 (A1: + 64 rows), B rows of piece i in B0 (B1: + 32)
+struct NtSOff {
+  long pa[2], pb[2];
+  long a64, b32;
 };
 
 template <int LAY>
-__device__ __forceinline__ void nt_stage_cursor(const NtCtx& c, const NtStream& st, NtCursor& cur) {
-  using Ly = NtLay<LAY>;
-  static_assert(!Ly::AT, "streamed kernel: NT / NN layouts only");
-  if (cur.G < st.total_k) {
-    char* dst = c.lds + (cur.G & 1) * NT_BUF + cur.slot * NT_HALF;
-    const long k0 = (long)cur.k * NT_BK;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int piece = c.wave * 2 + i;
-      const bf16_t* base;
-      unsigned off;
-      if (cur.slot == 0 || cur.slot == 3) {
-        base = c.A + (cur.m0 + ((piece >> 3) << 7) + (cur.slot == 3 ? 64 : 0) + (piece & 7) * 8) * c.lda + k0;
-        off = i ? c.offa1 : c.offa0;
-      } else if constexpr (!Ly::BT) {
-        base = c.B + (cur.n0 + ((piece >> 2) << 6) + (cur.slot == 2 ? 32 : 0) + (piece & 3) * 8) * c.ldb + k0;
-        off = i ? c.offb1 : c.offb0;
-      } else {
-        base = c.B + (k0 + piece * 4) * c.ldb + cur.n0 + (cur.slot == 2 ? 32 : 0);
-        off = c.offb0;
-      }
-      nt_glds16s(base, off, dst + piece * 1024);
-    }
-  }
-  // advance: slot -> K-tile -> output tile
-  if (++cur.slot == 4) {
-    cur.slot = 0;
-    ++cur.G;
-    if (++cur.k == st.nk) {
-      cur.k = 0;
-      ++cur.j;
-      if (cur.G < st.total_k) st.tile_origin(cur.j, cur.m0, cur.n0);
-    }
+__device__ __forceinline__ void nt_kcur_set(const NtCtx& c, const NtStream& st, NtKCur& q, int j) {
+  q.j = j;
+  q.k = 0;
+  q.ka = 0;
+  q.kb = 0;
+  if (j < st.my_tiles) {
+    long m0, n0;
+    st.tile_origin(j, m0, n0);
+    q.arow = c.A + m0 * c.lda;
+    q.brow = NtLay<LAY>::BT ? c.B + n0 : c.B + n0 * c.ldb;
   }
 }
 
+template <int LAY>
+__device__ __forceinline__ void nt_kcur_next(const NtCtx& c, const NtStream& st, NtKCur& q) {
+  if (++q.k == st.nk) {
+    nt_kcur_set<LAY>(c, st, q, q.j + 1);
+  } else {
+    q.ka += NT_BK;
+    q.kb += NtLay<LAY>::BT ? NT_BK * c.ldb : NT_BK;
+  }
+}
+
+// stage half SLOT (0 A0, 1 B0, 2 B1, 3 A1) of the K-tile at cursor q into buffer buf
+template <int LAY, int SLOT>
+__device__ __forceinline__ void nt_stage_kt(const NtCtx& c, const NtSOff& so, const NtKCur& q, char* buf) {
+  using Ly = NtLay<LAY>;
+  static_assert(!Ly::AT, "streamed kernel: NT / NN layouts only");
+  char* dst = buf + SLOT * NT_HALF;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = c.wave * 2 + i;
+    const bf16_t* base;
+    unsigned off;
+    if constexpr (SLOT == 0 || SLOT == 3) {
+      base = q.arow + so.pa[i] + (SLOT == 3 ? so.a64 : 0) + q.ka;
+      off = i ? c.offa1 : c.offa0;
+    } else {
+      base = q.brow + so.pb[i] + (SLOT == 2 ? so.b32 : 0) + q.kb;
+      off = Ly::BT ? c.offb0 : (i ? c.offb1 : c.offb0);
+    }
+    nt_glds16s(base, off, dst + piece * 1024);
+  }
+}
+
+// one K-tile of the stream: phases 0 / 1 stage B1 / A1 of K-tile t + 1 (cursor q1), phases 2 / 3
+// A0 / B0 of K-tile t + 2 (cursor q2) -- the one-tile kernel's half order (nt_stage_v), with
+// every slot a compile-time constant
 template <int POS, int LAY>
-__device__ __forceinline__ void nt_ktile_stream(const NtCtx& c, const NtStream& st, NtCursor& cur, int t,
-                                                f32x4 (&acc)[8][4], nt_s16x8 (&fa)[2][4][2], nt_s16x8 (&fb)[2][2][2]) {
+__device__ __forceinline__ void nt_ktile_stream(const NtCtx& c, const NtSOff& so, const NtKCur& q1,
+                                                const NtKCur& q2, int t, f32x4 (&acc)[8][4],
+                                                nt_s16x8 (&fa)[2][4][2], nt_s16x8 (&fb)[2][2][2]) {
   const char* buf = c.lds + (t & 1) * NT_BUF;
+  char* nbuf = c.lds + ((t + 1) & 1) * NT_BUF;
+  char* cbuf = c.lds + (t & 1) * NT_BUF;
   using P = NtPlan<POS>;
-#define NT_SPHASE_TAIL(Q, I0, J0, FA, FB)                          \
-  if constexpr (P::issue(Q)) nt_stage_cursor<LAY>(c, st, cur);     \
-  nt_vm<P::wait(Q)>();                                             \
-  nt_mma_begin();                                                  \
-  nt_quad<I0, J0>(acc, FA, FB);                                    \
+#define NT_SPHASE_TAIL(Q, I0, J0, FA, FB)                                                  \
+  if constexpr (P::issue(Q)) {                                                             \
+    if constexpr (Q == 0) nt_stage_kt<LAY, 2>(c, so, q1, nbuf);                            \
+    else if constexpr (Q == 1) nt_stage_kt<LAY, 3>(c, so, q1, nbuf);                       \
+    else if constexpr (Q == 2) nt_stage_kt<LAY, 0>(c, so, q2, cbuf);                       \
+    else nt_stage_kt<LAY, 1>(c, so, q2, cbuf);                                             \
+  }                                                                                        \
+  nt_vm<P::wait(Q)>();                                                                     \
+  nt_mma_begin();                                                                          \
+  nt_quad<I0, J0>(acc, FA, FB);                                                            \
   nt_mma_end();
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -708,7 +738,7 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_stream_kernel(NtArgs a,
   const int wg = blockIdx.x;
   const int my_tiles = wg < tiles ? (tiles - wg + P - 1) / P : 0;
   const int nk = a.K / NT_BK;
-  NtStream st{nk, my_tiles * nk, tiles_n, tiles, P, wg};
+  NtStream st{nk, my_tiles * nk, tiles_n, tiles, P, wg, my_tiles};
   if (my_tiles == 0) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -722,31 +752,54 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_stream_kernel(NtArgs a,
     c.offb0 = nt_lane_off(a.ldb, 0, lane);
     c.offb1 = nt_lane_off(a.ldb, 1, lane);
   }
-  NtCursor cur{0, 0, 0, 0, 0, 0};
-  st.tile_origin(0, cur.m0, cur.n0);
-  long m0 = cur.m0, n0 = cur.n0;      // origin of the tile being multiplied
-  int jt = 0, kin = 0;
+  NtSOff so;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wave * 2 + i;
+    so.pa[i] = (long)(((piece >> 3) << 7) + (piece & 7) * 8) * a.lda;
+    so.pb[i] = NtLay<LAY>::BT ? (long)piece * 4 * a.ldb : (long)(((piece >> 2) << 6) + (piece & 3) * 8) * a.ldb;
+  }
+  so.a64 = 64 * a.lda;
+  so.b32 = NtLay<LAY>::BT ? 32 : 32 * a.ldb;
 
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  long m0, n0;                          // origin of the tile being multiplied
+  st.tile_origin(0, m0, n0);
   NtEpiPre<4> epre;
   nt_preload_bias<EPI, 4>(a, n0 + wc * 64 + (lane >> 4) * 4, epre);
   nt_s16x8 fa[2][4][2];
   nt_s16x8 fb[2][2][2];
 
-  // prologue: the first K-tile and half of the second (six halves), as in the one-tile kernel
-#pragma unroll
-  for (int v = 0; v < 6; ++v) nt_stage_cursor<LAY>(c, st, cur);
-  if (st.total_k > 1) nt_vm<8>(); else nt_vm<4>();
+  // prologue: all of K-tile 0 and A0 + B0 of K-tile 1 (the one-tile kernel's halves -6 .. -1)
+  NtKCur q1, q2;
+  nt_kcur_set<LAY>(c, st, q1, 0);
+  nt_stage_kt<LAY, 0>(c, so, q1, lds);
+  nt_stage_kt<LAY, 1>(c, so, q1, lds);
+  nt_stage_kt<LAY, 2>(c, so, q1, lds);
+  nt_stage_kt<LAY, 3>(c, so, q1, lds);
+  nt_kcur_next<LAY>(c, st, q1);                          // K-tile 1
+  if (st.total_k > 1) {
+    nt_stage_kt<LAY, 0>(c, so, q1, lds + NT_BUF);
+    nt_stage_kt<LAY, 1>(c, so, q1, lds + NT_BUF);
+    nt_vm<8>();
+  } else {
+    nt_vm<4>();
+  }
+  q2 = q1;
+  nt_kcur_next<LAY>(c, st, q2);                          // K-tile 2
   nt_bar();
   if (wr == 1) nt_bar();                                 // group 1 runs one barrier behind
 
   // after each K-tile: when an output tile is complete, store it (the next tile's DMAs are
   // already in flight), clear the accumulators and load the next tile's bias
+  int jt = 0, kin = 0;
   auto finish_k = [&]() {
+    q1 = q2;
+    nt_kcur_next<LAY>(c, st, q2);
     if (++kin != nk) return;
     const long emrow = m0 + wr * 128 + (lane & 15), encol = n0 + wc * 64 + (lane >> 4) * 4;
     nt_epilogue<EPI, false, 4>(a, acc, emrow, encol, lane, 0, epre);
@@ -765,15 +818,15 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_stream_kernel(NtArgs a,
   const int T = st.total_k;
   int t = 0;
   for (; t < T - 2; ++t) {
-    nt_ktile_stream<0, LAY>(c, st, cur, t, acc, fa, fb);
+    nt_ktile_stream<0, LAY>(c, so, q1, q2, t, acc, fa, fb);
     finish_k();
   }
   if (T >= 2) {
-    nt_ktile_stream<1, LAY>(c, st, cur, t, acc, fa, fb);
+    nt_ktile_stream<1, LAY>(c, so, q1, q2, t, acc, fa, fb);
     finish_k();
     ++t;
   }
-  nt_ktile_stream<2, LAY>(c, st, cur, t, acc, fa, fb);
+  nt_ktile_stream<2, LAY>(c, so, q1, q2, t, acc, fa, fb);
   finish_k();
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 }

@@ -105,11 +105,20 @@ _STREAM_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _STREAM_SIT
                  else {t for t in _STREAM_SITES.split(",") if t})
 
 
+# The same sites through the one-tile MFMA kernel (gemm_nt / gemm_nn: one 256 x 256 tile per
+# workgroup); CLOUDTIK_AMD_ONETILE_GEMM takes the same site list.
+_ONETILE_SITES = os.environ.get("CLOUDTIK_AMD_ONETILE_GEMM", "")
+_ONETILE_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _ONETILE_SITES == "all"
+                  else {t for t in _ONETILE_SITES.split(",") if t})
+
+
 def _stream_mm(site, A, B, b_kn, bias=None, out=None):
     """A [M,K] . B^T (b_kn False: B [N,K]) or A . B (b_kn True: B [K,N]) [+ bias], or
-    ``out += A . B`` when ``out`` is given.  None when the site is not routed or the shape
-    is outside the kernel's tiling (M, N multiples of 256, K of 64)."""
-    if site not in _STREAM_SITES:
+    ``out += A . B`` when ``out`` is given, on the in-tree MFMA kernel the site is routed to
+    (streamed or one-tile).  None when the site is not routed or the shape is outside the
+    kernels' tiling (M, N multiples of 256, K of 64)."""
+    stream = site in _STREAM_SITES
+    if not stream and site not in _ONETILE_SITES:
         return None
     M, K = A.shape
     N = B.shape[1] if b_kn else B.shape[0]
@@ -119,9 +128,14 @@ def _stream_mm(site, A, B, b_kn, bias=None, out=None):
         return None
     acc = out is not None
     D = out if acc else torch.empty(M, N, device=A.device, dtype=A.dtype)
-    if not _C().gemm_nt_stream(A, B, D, bias, b_kn, 0, acc):
-        return None
-    return D
+    C = _C()
+    if stream:
+        ok = C.gemm_nt_stream(A, B, D, bias, b_kn, 0, acc)
+    elif b_kn:
+        ok = bias is None and C.gemm_nn(A, B, D, 0, acc, None, None, None)
+    else:
+        ok = C.gemm_nt(A, B, D, 5 if bias is not None else 0, acc, bias, None, None)
+    return D if ok else None
 
 
 def _flat(p) -> bool:

@@ -13,4 +13,8 @@ tail -3 "$O/tests.txt"
 timeout -k 10 600 python -u bench/conv_igemm_probe.py --cfgs=-1,5,8,9,10,11,12,13 > "$O/probe.md" 2> "$O/probe.err"
 rc=$?
 tail -30 "$O/probe.md"
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+  timeout -k 10 240 python -u bench.py --model resnet50 --steps 20 --warmup 5 > "$O/rn_$r.json" 2> "$O/rn_$r.err" || exit $?
+  echo "resnet50 round $r: $(grep -o '"ms_per_step": [0-9.]*' "$O/rn_$r.json")"
+done

@@ -402,7 +402,8 @@ def test_wgrad_splitk_accumulate(cuda, N, K):
 
 @pytest.mark.parametrize("p,fused,fused_fwd,stream", [(0.0, False, False, False), (0.1, False, False, False),
                                                      (0.1, True, False, False), (0.1, False, True, False),
-                                                     (0.1, True, True, False), (0.1, True, True, True)])
+                                                     (0.1, True, True, False), (0.1, True, True, True),
+                                                     (0.1, True, True, "onetile")])
 def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, stream, monkeypatch):
     """Hand-scheduled block backward == composed-op autograd (same dropout streams); `fused`
     routes the FFN dgrad through the MFMA GEMM with the dGELU + bias-gradient epilogue,
@@ -413,8 +414,10 @@ def test_bert_layer_blocks_match_composed(cuda, p, fused, fused_fwd, stream, mon
     monkeypatch.setattr(T, "_FUSED_FFN_DGRAD", fused)
     monkeypatch.setattr(T, "_FUSED_FFN_FWD", fused_fwd)
     stream_sites = []
-    if stream:                             # every plain fwd / dgrad GEMM through the streamed kernel
-        monkeypatch.setattr(T, "_STREAM_SITES", {"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"})
+    if stream:                             # every plain fwd / dgrad GEMM through an in-tree kernel
+        sites = {"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"}
+        monkeypatch.setattr(T, "_STREAM_SITES", set() if stream == "onetile" else sites)
+        monkeypatch.setattr(T, "_ONETILE_SITES", sites if stream == "onetile" else set())
         orig_stream = T._stream_mm
         def spy_stream(site, *a, **k):
             r = orig_stream(site, *a, **k)
