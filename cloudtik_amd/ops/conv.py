@@ -119,7 +119,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride=(1, 1), padding=(0, 0), ou
     C = _C()
     part = None
     if stats or partials:
-        bm = C.conv_igemm_tile_m(_CFG, co, geo[11], len(taps) // 2 * (x.shape[1] // 64))
+        # one (mean, M2) partial per wave row block of the tile (conv.hip cv_wave_stats)
+        bm = C.conv_igemm_part_rows(_CFG, co, geo[11], len(taps) // 2 * max(1, x.shape[1] // 64))
         tiles = (geo[11] + bm - 1) // bm
         # + room for the first-level merge of the BatchNorm finalize (batchnorm.hip)
         part = torch.empty((tiles + (tiles + 63) // 64) * 2 * co, device=x.device, dtype=torch.float32)

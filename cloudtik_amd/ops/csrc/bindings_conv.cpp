@@ -14,6 +14,7 @@ int ct_conv_igemm_bn(const void*, int, int, int, const void*, void*, int, int, i
                      int, hipStream_t);
 int ct_conv_igemm_rows(int, int, int, int);
 int ct_conv_igemm_tile_m(int);
+int ct_conv_igemm_part_rows(int);
 void ct_conv_stream_set_cus(int);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
 int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
@@ -49,9 +50,9 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
   float* pp = nullptr;
   if (part.has_value() && part->defined()) {
     const int cfg_r = ct_conv_igemm_rows((int)cfg, Co, (int)M, T * (cw / 64));
-    const int bm = ct_conv_igemm_tile_m(cfg_r);
+    const int pr = ct_conv_igemm_part_rows(cfg_r);     // rows per statistics partial
     TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() &&
-                part->numel() >= (M + bm - 1) / bm * 2 * Co, "conv_igemm: part buffer");
+                part->numel() >= (M + pr - 1) / pr * 2 * Co, "conv_igemm: part buffer");
     pp = part->data_ptr<float>();
   }
   const int rc = ct_conv_igemm(X.data_ptr(), Hi, Wi, Ci, W.data_ptr(), Y.data_ptr(), (int)geo[0], (int)geo[1],
@@ -111,6 +112,10 @@ int64_t conv_igemm_tile_m(int64_t cfg, int64_t Co, int64_t M, int64_t KT) {
   return ct_conv_igemm_tile_m(ct_conv_igemm_rows((int)cfg, (int)Co, (int)M, (int)KT));
 }
 
+int64_t conv_igemm_part_rows(int64_t cfg, int64_t Co, int64_t M, int64_t KT) {
+  return ct_conv_igemm_part_rows(ct_conv_igemm_rows((int)cfg, (int)Co, (int)M, (int)KT));
+}
+
 void bn_partials_finalize(at::Tensor part, int64_t rows_per_tile, int64_t M, at::Tensor mean, at::Tensor var) {
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(), "bn_partials_finalize");
   const int C = (int)mean.numel();
@@ -165,6 +170,7 @@ void register_conv(pybind11::module& m) {
   m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
   m.def("conv_stream_set_cus", [](int64_t cus) { ct_conv_stream_set_cus((int)cus); },
         "streamed conv kernels: persistent workgroups = cus x per-CU count (0: the device's CUs)");
+  m.def("conv_igemm_part_rows", &conv_igemm_part_rows, "rows per BatchNorm-statistics partial (EPI 1)");
   m.def("conv_igemm_tile_m", &conv_igemm_tile_m, "rows per tile of the chosen conv configuration");
   m.def("bn_partials_finalize", &bn_partials_finalize, "Chan merge of per-tile (mean, M2) -> mean, var");
 }

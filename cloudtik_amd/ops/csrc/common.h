@@ -58,6 +58,23 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Sum over each 16-lane DPP row (lanes 16k .. 16k + 15), broadcast to the row's lanes: four
+// VALU adds with DPP operand swizzles (quad_perm 1032, quad_perm 2301, row_half_mirror,
+// row_mirror) instead of four LDS-routed __shfl_xor permutes, each waiting on LDS latency.
+// The MFMA 16x16 output layout keeps a fragment's 16 rows in one DPP row, so this is the
+// column sum of a fragment.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);     // quad_perm [2,3,0,1]: quad sums
+  v += dpp_mov<0x141>(v);    // row_half_mirror: 8-lane sums
+  v += dpp_mov<0x140>(v);    // row_mirror: 16-lane sums
+  return v;
+}
+
 // Block-wide sum; `scratch` must hold blockDim.x/64 floats. Result broadcast to all threads.
 __device__ __forceinline__ float block_sum(float v, float* scratch) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;

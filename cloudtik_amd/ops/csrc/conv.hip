@@ -66,6 +66,22 @@ struct ConvArgs {
 
 __device__ __forceinline__ int cv_swz(int r) { return (r >> 1) & 7; }
 
+// q = n / d, r = n % d for 0 <= n < 2^24, d > 0: the float quotient is within one of the exact
+// one; one correction each way makes it exact (~10 VALU instead of a ~40-instruction integer
+// division sequence)
+__device__ __forceinline__ void cv_divmod(int n, int d, float inv_d, int& q, int& r) {
+  q = (int)((float)n * inv_d);
+  r = n - q * d;
+  if (r >= d) {
+    ++q;
+    r -= d;
+  }
+  if (r < 0) {
+    --q;
+    r += d;
+  }
+}
+
 __device__ __forceinline__ void cv_glds16(const void* g, const char* lds_wave_base) {
   const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(cv_lds_void*)lds_wave_base);
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
@@ -94,6 +110,13 @@ __device__ __forceinline__ void cv_bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, never for
+// vector memory -- __syncthreads() would emit vmcnt(0) and drain the LDS-DMA stages in flight
+__device__ __forceinline__ void cs_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  cv_bar();
+}
+
 template <int N>
 __device__ __forceinline__ void cv_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -109,6 +132,45 @@ __device__ __forceinline__ void cv_wait_stage(int rem) {
     if (rem >= 1) { cv_vm<G>(); return; }
   }
   cv_vm<0>();
+}
+
+// BatchNorm statistics of one wave's rows (EPI 1): the column mean and M2 (sum of squared
+// deviations from that mean, two passes over the registers) of the bf16 outputs in the wave's
+// WM rows, written as the partials of a WM-row block: means [blocks][Co] then M2 [blocks][Co],
+// block = global row / WM (what bn_finalize / bn_partials_finalize merge with Chan's formula).
+// Column sums over a 16-row fragment are DPP row sums: no LDS, no workgroup barrier.
+template <int MI, int NJ, int WM>
+__device__ __forceinline__ void cv_wave_stats(const ConvArgs& a, const f32x4 (&acc)[MI][NJ], const bool (&rv)[MI],
+                                              int row0, int col0, int lane) {
+  const int nrows = min(WM, a.M - row0);
+  if (nrows <= 0) return;
+  const float inv = 1.f / (float)nrows;
+  const long blocks = ((long)a.M + WM - 1) / WM, pb = row0 / WM;
+  float* pm = a.part + pb * a.Co + col0 + 4 * (lane >> 4);
+  float* pq = a.part + (blocks + pb) * a.Co + col0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    f32x4 mv, qv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) v += acc[i][j][r];
+      const float mean = row16_sum(v) * inv;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const float d = acc[i][j][r] - mean;
+        q += rv[i] ? d * d : 0.f;
+      }
+      mv[r] = mean;
+      qv[r] = row16_sum(q);
+    }
+    if ((lane & 15) == 0) {
+      *(f32x4*)(pm + 16 * j) = mv;
+      *(f32x4*)(pq + 16 * j) = qv;
+    }
+  }
 }
 
 template <int BM, int BN, int WGM, int WGN, int NS, int MINB, int EPI>
@@ -221,9 +283,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   // bytes and a wave writes whole rows: 8-byte stores of the MFMA layout (4 channels of 16
   // rows per instruction) made the epilogue store-issue-bound.
   constexpr int OROW = BN * 2 + 16;                // padded LDS row: 2-way at most on the b64 writes
-  static_assert(BM * OROW + WGM * BN * 4 <= NS * STAGE, "epilogue LDS");
+  static_assert(BM * OROW <= NS * STAGE, "epilogue LDS");
   char* ot = lds;
-  float* red = (float*)(lds + BM * OROW);          // [WGM][BN] statistics scratch
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   cv_bar();                                        // every wave is done reading the ring
   bool rv[MI];
@@ -242,73 +303,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
       *(u16x4*)(ot + row * OROW + (wn * WN + 16 * j + 4 * (lane >> 4)) * 2) = out;
     }
   }
-  if constexpr (EPI == 1) {
-    // per-tile column mean and M2 from the registers (two passes: numerically like Welford)
-    const int nrows = min(BM, a.M - m0);
-    float cs[NJ][4];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) v += acc[i][j][r];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
-      }
-    __syncthreads();
-    float mean[NJ][4];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
-        float sum = 0.f;
-#pragma unroll
-        for (int w = 0; w < WGM; ++w) sum += red[w * BN + c];
-        mean[j][r] = sum / (float)nrows;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const float d = acc[i][j][r] - mean[j][r];
-          q += rv[i] ? d * d : 0.f;
-        }
-        cs[j][r] = q;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = cs[j][r];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
-      }
-    __syncthreads();
-    if (wm == 0 && (lane & 15) == 0) {
-      // part = means [tiles_m][Co], then M2 [tiles_m][Co] (the layout bn_finalize_kernel reads)
-      const long tiles_m = (a.M + BM - 1) / BM;
-      float* pm = a.part + (long)tm * a.Co;
-      float* pq = a.part + (tiles_m + tm) * (long)a.Co;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
-          float q = 0.f;
-#pragma unroll
-          for (int w = 0; w < WGM; ++w) q += red[w * BN + c];
-          pm[n0 + c] = mean[j][r];
-          pq[n0 + c] = q;
-        }
-    }
-  }
+  if constexpr (EPI == 1) cv_wave_stats<MI, NJ, WM>(a, acc, rv, m0 + wm * WM, n0 + wn * WN, lane);
   __syncthreads();
   // coalesced copy-out: row-major 16-B chunks, BN / 8 lanes per row
   constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;
@@ -330,11 +325,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
       s2[e] = 0.f;
     }
   }
+  // row -> output pixel by float-reciprocal division with an exact integer fix-up
+  // (straight-line, so the unrolled rows keep their loads in flight together)
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)a.Wr;
 #pragma unroll 4
   for (int row = tid / CPR; row < BM; row += RPP) {
     const int m = m0 + row;
     if (m >= a.M) break;
-    const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+    int b, rem, y, x;
+    cv_divmod(m, HW, inv_hw, b, rem);
+    cv_divmod(rem, a.Wr, inv_w, y, x);
     const long yo = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
     bf16_t* yp = a.Y + yo;
     u16x8 v = *(const u16x8*)(ot + row * OROW + cc * 16);
@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int IA = BM / (8 * NW), IB = BN / (8 * NW), G = IA + IB;
   constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;         // copy-out: 16-B chunks per row, rows per pass
-  constexpr int REDB = EPI == 1 ? WGM * BN * 4 : 16;
+  constexpr int REDB = 16;
   static_assert(IA * 8 * NW == BM && IB * 8 * NW == BN, "tile / wave mismatch");
   static_assert(NS >= 2 && NS <= 4 && WPC * (NS * STAGE + REDB) <= 160 * 1024, "LDS ring");
   static_assert(BM * BN * 2 <= STAGE && (CPR == 8 || CPR == 16), "epilogue image in one ring slot");
@@ -502,7 +502,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) stage_next();
 
-  float* red = (float*)(lds + NS * STAGE);                  // EPI 1: [WGM][BN] statistics scratch
   int jt = 0, kin = 0;
   for (int g = 0; g < total; ++g) {
     const int ahead = total - 1 - g;
@@ -554,76 +553,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
         *(u16x4*)(ot_chunk(row, col >> 3) + (col & 7) * 2) = out;
       }
     }
-    if constexpr (EPI == 1) {
-      const int nrows = min(BM, a.M - m0);
-      float cs[NJ][4];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = 0.f;
-#pragma unroll
-          for (int i = 0; i < MI; ++i) v += acc[i][j][r];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
-        }
-      __syncthreads();
-      float mean[NJ][4];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
-          float sum = 0.f;
-#pragma unroll
-          for (int w = 0; w < WGM; ++w) sum += red[w * BN + c];
-          mean[j][r] = sum / (float)nrows;
-          float q = 0.f;
-#pragma unroll
-          for (int i = 0; i < MI; ++i) {
-            const float d = acc[i][j][r] - mean[j][r];
-            q += rv[i] ? d * d : 0.f;
-          }
-          cs[j][r] = q;
-        }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = cs[j][r];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          if ((lane & 15) == 0) red[wm * BN + wn * WN + 16 * j + 4 * (lane >> 4) + r] = v;
-        }
-      __syncthreads();
-      if (wm == 0 && (lane & 15) == 0) {
-        const long tiles_m = (a.M + BM - 1) / BM;
-        float* pm = a.part + (long)tm * a.Co;
-        float* pq = a.part + (tiles_m + tm) * (long)a.Co;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int c = wn * WN + 16 * j + 4 * (lane >> 4) + r;
-            float q = 0.f;
-#pragma unroll
-            for (int w = 0; w < WGM; ++w) q += red[w * BN + c];
-            pm[n0 + c] = mean[j][r];
-            pq[n0 + c] = q;
-          }
-      }
-    }
+    if constexpr (EPI == 1) cv_wave_stats<MI, NJ, WM>(a, acc, rv, m0 + wm * WM, n0 + wn * WN, lane);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();
+    cs_sync();
     const int cc = tid % CPR;
     float bmu[8], bis[8], bfa[8], bfb[8], s1[8], s2[8];
     if constexpr (EPI == 2) {
@@ -638,11 +573,16 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
         s2[e] = 0.f;
       }
     }
+    // row -> output pixel by float-reciprocal division with an exact integer fix-up
+    // (straight-line, so the unrolled rows keep their loads in flight together)
+    const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)a.Wr;
 #pragma unroll 4
     for (int row = tid / CPR; row < BM; row += RPP) {
       const int m = m0 + row;
       if (m >= a.M) break;
-      const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+      int b, rem, y, x;
+      cv_divmod(m, HW, inv_hw, b, rem);
+      cv_divmod(rem, a.Wr, inv_w, y, x);
       const long yo = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
       bf16_t* yp = a.Y + yo;
       u16x8 v = *(const u16x8*)ot_chunk(row, cc);
@@ -669,14 +609,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
     if constexpr (EPI == 2) {
       float* r1 = (float*)ot;
       float* r2 = r1 + RPP * BN;
-      __syncthreads();                                    // every lane is done reading the image
+      cs_sync();                                    // every lane is done reading the image
       const int slot = tid / CPR;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         r1[slot * BN + cc * 8 + e] = s1[e];
         r2[slot * BN + cc * 8 + e] = s2[e];
       }
-      __syncthreads();
+      cs_sync();
       for (int c = tid; c < BN; c += 64 * NW) {
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll 8
@@ -944,6 +884,11 @@ extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
   return cfg;
 }
 
+// rows per BatchNorm-statistics partial (EPI 1 writes one per wave row block: BM / WGM)
+extern "C" int ct_conv_igemm_part_rows(int cfg) {
+  return cfg == 6 ? 32 : 64;
+}
+
 extern "C" int ct_conv_igemm_tile_m(int cfg) {
   return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : ((cfg == 9 || cfg == 13) ? 64 : 128);
 }
@@ -1004,7 +949,9 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
                            int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M, int T,
                            const int* taps, int accumulate, float* part, int cfg, const ConvBnBwd* bn,
                            hipStream_t stream) {
-  if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT) return 1;
+  // (M < 2^24: the epilogue's float-reciprocal row division, cv_divmod)
+  if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || M >= (1 << 24) || T <= 0 || T > CV_MAXT)
+    return 1;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 7) || ldy % 4) return 3;
   const int pixchunk = Ci == 8;            // the stem: NHWC8 input, 8 pixels per K-step
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
