@@ -173,6 +173,75 @@ __device__ __forceinline__ void cv_wave_stats(const ConvArgs& a, const f32x4 (&a
   }
 }
 
+// ---- copy-out of the epilogue (both conv kernels).  Thread tid owns 16-B chunk cc = tid % CPR
+// of rows tid / CPR + k * RPP, k < NR.  cv_out_prefetch computes the rows' output addresses and
+// issues every global load the copy-out needs (the old Y of an accumulate, the BatchNorm input /
+// output of EPI 2) BEFORE the tile goes through LDS, so their latency overlaps the LDS re-lay
+// instead of being paid row by row (the compiler cannot hoist them over the previous row's Y
+// store: the pointers may alias).
+template <int NR>
+struct CvOut {
+  long yo[NR];
+  bool ok[NR];
+  u16x8 old[NR], xv[NR], yv[NR];
+};
+
+template <int BM, int CPR, int RPP, int EPI>
+__device__ __forceinline__ void cv_out_prefetch(const ConvArgs& a, CvOut<BM / RPP>& o, int m0, int n0, int tid) {
+  constexpr int NR = BM / RPP;
+  const int HW = a.Hr * a.Wr;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)a.Wr;
+  const int cc = tid % CPR;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const int m = m0 + tid / CPR + k * RPP;
+    o.ok[k] = m < a.M;
+    int b, rem, y, x;
+    cv_divmod(o.ok[k] ? m : m0, HW, inv_hw, b, rem);
+    cv_divmod(rem, a.Wr, inv_w, y, x);
+    o.yo[k] = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+  }
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    if (!o.ok[k]) continue;
+    if (a.accumulate) o.old[k] = *(const u16x8*)(a.Y + o.yo[k]);
+    if constexpr (EPI == 2) {
+      o.xv[k] = *(const u16x8*)(a.bnx + o.yo[k]);
+      if (a.bny) o.yv[k] = *(const u16x8*)(a.bny + o.yo[k]);
+    }
+  }
+}
+
+// the stores (+ accumulate, + EPI 2 mask and per-thread sums s1 / s2 of its 8 channels);
+// chunk(row) = the LDS address of this thread's 16-B chunk of tile row `row`
+template <int BM, int CPR, int RPP, int EPI, typename ChunkFn>
+__device__ __forceinline__ void cv_out_store(const ConvArgs& a, CvOut<BM / RPP>& o, ChunkFn chunk, int tid,
+                                             const float (&bfa)[8], const float (&bfb)[8], const float (&bmu)[8],
+                                             const float (&bis)[8], float (&s1)[8], float (&s2)[8]) {
+  constexpr int NR = BM / RPP;
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    if (!o.ok[k]) continue;
+    u16x8 v = *(const u16x8*)chunk(tid / CPR + k * RPP);
+    if (a.accumulate) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(o.old[k][e]));
+    }
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xf = bf2f(o.xv[k][e]);
+        const bool on = a.bny ? bf2f(o.yv[k][e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
+        if (!on) v[e] = 0;
+        const float d = bf2f(v[e]);
+        s1[e] += d;
+        s2[e] += d * (xf - bmu[e]) * bis[e];
+      }
+    }
+    *(u16x8*)(a.Y + o.yo[k]) = v;
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN, int NS, int MINB, int EPI>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WGM * WGN;
@@ -284,6 +353,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   // rows per instruction) made the epilogue store-issue-bound.
   constexpr int OROW = BN * 2 + 16;                // padded LDS row: 2-way at most on the b64 writes
   static_assert(BM * OROW <= NS * STAGE, "epilogue LDS");
+  constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;
+  const int cc = tid % CPR;
+  CvOut<BM / RPP> co;
+  cv_out_prefetch<BM, CPR, RPP, EPI>(a, co, m0, n0, tid);
   char* ot = lds;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   cv_bar();                                        // every wave is done reading the ring
@@ -305,59 +378,28 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   }
   if constexpr (EPI == 1) cv_wave_stats<MI, NJ, WM>(a, acc, rv, m0 + wm * WM, n0 + wn * WN, lane);
   __syncthreads();
-  // coalesced copy-out: row-major 16-B chunks, BN / 8 lanes per row
-  constexpr int CPR = BN / 8, RPP = (64 * NW) / CPR;
-  const int cc = tid % CPR;
+  // coalesced copy-out: row-major 16-B chunks, BN / 8 lanes per row.
   // EPI 2: the BatchNorm backward's reduction pass rides on the copy-out.  This thread's 8
   // channels are fixed over its rows: it masks dy with the ReLU mask recomputed from the
   // BatchNorm input (what bn_bwd_reduce_kernel mode 2 does), stores the masked dy' and sums
   // dy' and dy' * xhat -- the separate pass re-reading dy and x goes away.
   float bmu[8], bis[8], bfa[8], bfb[8], s1[8], s2[8];
-  if constexpr (EPI == 2) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+  for (int e = 0; e < 8; ++e) {
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+    if constexpr (EPI == 2) {
       const int c = n0 + cc * 8 + e;
       bmu[e] = a.bnstat[c];
       bis[e] = a.bnstat[a.Co + c];
       bfa[e] = a.bnstat[2 * a.Co + c];
       bfb[e] = a.bnstat[3 * a.Co + c];
-      s1[e] = 0.f;
-      s2[e] = 0.f;
+    } else {
+      bmu[e] = bis[e] = bfa[e] = bfb[e] = 0.f;
     }
   }
-  // row -> output pixel by float-reciprocal division with an exact integer fix-up
-  // (straight-line, so the unrolled rows keep their loads in flight together)
-  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)a.Wr;
-#pragma unroll 4
-  for (int row = tid / CPR; row < BM; row += RPP) {
-    const int m = m0 + row;
-    if (m >= a.M) break;
-    int b, rem, y, x;
-    cv_divmod(m, HW, inv_hw, b, rem);
-    cv_divmod(rem, a.Wr, inv_w, y, x);
-    const long yo = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
-    bf16_t* yp = a.Y + yo;
-    u16x8 v = *(const u16x8*)(ot + row * OROW + cc * 16);
-    if (a.accumulate) {
-      const u16x8 old = *(const u16x8*)yp;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(old[e]));
-    }
-    if constexpr (EPI == 2) {
-      const u16x8 xv = *(const u16x8*)(a.bnx + yo);
-      const u16x8 yv = a.bny ? *(const u16x8*)(a.bny + yo) : u16x8(0);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xf = bf2f(xv[e]);
-        const bool on = a.bny ? bf2f(yv[e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
-        if (!on) v[e] = 0;
-        const float d = bf2f(v[e]);
-        s1[e] += d;
-        s2[e] += d * (xf - bmu[e]) * bis[e];
-      }
-    }
-    *(u16x8*)yp = v;
-  }
+  cv_out_store<BM, CPR, RPP, EPI>(a, co, [&](int row) { return ot + row * OROW + cc * 16; }, tid, bfa, bfb, bmu,
+                                  bis, s1, s2);
   if constexpr (EPI == 2) {
     // column sums over the tile: [RPP][BN] per set in the (now free) LDS, then one thread per
     // column adds the RPP row slots
@@ -534,6 +576,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
     auto ot_chunk = [&](int row, int chunk) -> char* {
       return ot + row * (BN * 2) + ((chunk ^ ((CPR == 8 ? row >> 1 : row) & (CPR - 1))) << 4);
     };
+    CvOut<BM / RPP> co;
+    cv_out_prefetch<BM, CPR, RPP, EPI>(a, co, m0, n0, tid);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     cv_bar();                                             // every wave is done reading the slot
     bool rv[MI];
@@ -561,51 +605,22 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
     cs_sync();
     const int cc = tid % CPR;
     float bmu[8], bis[8], bfa[8], bfb[8], s1[8], s2[8];
-    if constexpr (EPI == 2) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = 0.f;
+      s2[e] = 0.f;
+      if constexpr (EPI == 2) {
         const int c = n0 + cc * 8 + e;
         bmu[e] = a.bnstat[c];
         bis[e] = a.bnstat[a.Co + c];
         bfa[e] = a.bnstat[2 * a.Co + c];
         bfb[e] = a.bnstat[3 * a.Co + c];
-        s1[e] = 0.f;
-        s2[e] = 0.f;
+      } else {
+        bmu[e] = bis[e] = bfa[e] = bfb[e] = 0.f;
       }
     }
-    // row -> output pixel by float-reciprocal division with an exact integer fix-up
-    // (straight-line, so the unrolled rows keep their loads in flight together)
-    const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)a.Wr;
-#pragma unroll 4
-    for (int row = tid / CPR; row < BM; row += RPP) {
-      const int m = m0 + row;
-      if (m >= a.M) break;
-      int b, rem, y, x;
-      cv_divmod(m, HW, inv_hw, b, rem);
-      cv_divmod(rem, a.Wr, inv_w, y, x);
-      const long yo = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
-      bf16_t* yp = a.Y + yo;
-      u16x8 v = *(const u16x8*)ot_chunk(row, cc);
-      if (a.accumulate) {
-        const u16x8 old = *(const u16x8*)yp;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(old[e]));
-      }
-      if constexpr (EPI == 2) {
-        const u16x8 xv = *(const u16x8*)(a.bnx + yo);
-        const u16x8 yv = a.bny ? *(const u16x8*)(a.bny + yo) : u16x8(0);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xf = bf2f(xv[e]);
-          const bool on = a.bny ? bf2f(yv[e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
-          if (!on) v[e] = 0;
-          const float d = bf2f(v[e]);
-          s1[e] += d;
-          s2[e] += d * (xf - bmu[e]) * bis[e];
-        }
-      }
-      *(u16x8*)yp = v;
-    }
+    cv_out_store<BM, CPR, RPP, EPI>(a, co, [&](int row) { return ot_chunk(row, cc); }, tid, bfa, bfb, bmu, bis, s1,
+                                    s2);
     if constexpr (EPI == 2) {
       float* r1 = (float*)ot;
       float* r2 = r1 + RPP * BN;
