@@ -287,6 +287,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
 
 
 _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
+# 1x1 stride-1 weight gradients with 256-multiple channel counts on the TN GEMM kernel
+_TN_WGRAD_1X1 = os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "1") == "1"
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128)}
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
 WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
@@ -315,6 +317,21 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=(1, 1), paddin
             taps += [r - padding[0], s - padding[1]]
     nn = R * S * ci
     M = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    if (_TN_WGRAD_1X1 and R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(padding) == (0, 0)
+            and co % 256 == 0 and ci % 256 == 0 and M % 64 == 0
+            and dy.is_contiguous(memory_format=torch.channels_last)
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        # a 1x1 stride-1 weight gradient IS the linear one, dW = dY^T X over the pixel rows: the
+        # 256 x 256 TN MFMA GEMM with split-K (ops.linear.wgrad_accumulate) instead of the
+        # 128-wide implicit-GEMM tiles
+        from cloudtik_amd.ops.linear import wgrad_accumulate
+        if out is None or not accumulate:
+            out = out.zero_() if out is not None else torch.zeros(
+                w_shape, device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+        g2 = out.permute(0, 2, 3, 1).reshape(co, ci)
+        if g2.data_ptr() == out.data_ptr() and g2.is_contiguous():
+            wgrad_accumulate(g2, dy.permute(0, 2, 3, 1).reshape(M, co), x.permute(0, 2, 3, 1).reshape(M, ci))
+            return out
     C = _C()
     cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
     splits, rows = wgrad_plan(M, co, nn, cfg)

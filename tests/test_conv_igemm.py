@@ -370,3 +370,24 @@ def test_wgrad_64_pixel_stages_match_fp32_reference(cuda, monkeypatch, wcfg, ci,
     ref.backward(dy.float())
     dw = CV.conv_wgrad(dy, x, w.shape, (s, s), (pad, pad))
     assert _rel(dw, wr.grad) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tn", [False, True])
+def test_1x1_wgrad_on_tn_gemm(cuda, monkeypatch, tn):
+    """1x1 stride-1 weight gradients with 256-multiple channels go through the linear TN GEMM
+    (split-K): fresh and accumulated into an existing gradient, vs fp32."""
+    monkeypatch.setattr(CV, "_TN_WGRAD_1X1", tn)
+    torch.manual_seed(7)
+    x = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).to(torch.bfloat16))
+    w = _nhwc((torch.randn(512, 256, 1, 1, device=cuda) * 0.05).to(torch.bfloat16))
+    wr = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wr)
+    dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
+    ref.backward(dy.float())
+    dw = CV.conv_wgrad(dy, x, w.shape)
+    assert dw.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(dw, wr.grad) < 1e-2
+    base = _nhwc(torch.randn(w.shape, device=cuda).to(torch.bfloat16))
+    dw2 = CV.conv_wgrad(dy, x, w.shape, out=base.clone(), accumulate=True)
+    assert _rel(dw2, wr.grad + base.float()) < 1e-2
