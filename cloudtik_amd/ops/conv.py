@@ -326,8 +326,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=(1, 1), paddin
         # 128-wide implicit-GEMM tiles
         from cloudtik_amd.ops.linear import wgrad_accumulate
         if out is None or not accumulate:
-            out = out.zero_() if out is not None else torch.zeros(
-                w_shape, device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
+            out = (out if out is not None else torch.empty(
+                w_shape, device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)).zero_()
         g2 = out.permute(0, 2, 3, 1).reshape(co, ci)
         if g2.data_ptr() == out.data_ptr() and g2.is_contiguous():
             wgrad_accumulate(g2, dy.permute(0, 2, 3, 1).reshape(M, co), x.permute(0, 2, 3, 1).reshape(M, ci))

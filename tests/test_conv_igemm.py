@@ -378,8 +378,13 @@ def test_1x1_wgrad_on_tn_gemm(cuda, monkeypatch, tn):
     """1x1 stride-1 weight gradients with 256-multiple channels go through the linear TN GEMM
     (split-K): fresh and accumulated into an existing gradient, vs fp32."""
     monkeypatch.setattr(CV, "_TN_WGRAD_1X1", tn)
+    import importlib
+    L = importlib.import_module("cloudtik_amd.ops.linear")     # (ops.linear is also a function)
+    calls = []
+    orig = L.wgrad_accumulate
+    monkeypatch.setattr(L, "wgrad_accumulate", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
     torch.manual_seed(7)
-    x = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).to(torch.bfloat16))
+    x = _nhwc(torch.randn(4, 256, 16, 16, device=cuda).to(torch.bfloat16))     # 1024 pixel rows
     w = _nhwc((torch.randn(512, 256, 1, 1, device=cuda) * 0.05).to(torch.bfloat16))
     wr = w.float().requires_grad_()
     ref = F.conv2d(x.float(), wr)
@@ -391,3 +396,4 @@ def test_1x1_wgrad_on_tn_gemm(cuda, monkeypatch, tn):
     base = _nhwc(torch.randn(w.shape, device=cuda).to(torch.bfloat16))
     dw2 = CV.conv_wgrad(dy, x, w.shape, out=base.clone(), accumulate=True)
     assert _rel(dw2, wr.grad + base.float()) < 1e-2
+    assert len(calls) == (2 if tn else 0)
