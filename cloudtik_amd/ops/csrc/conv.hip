@@ -62,6 +62,8 @@ struct ConvArgs {
   float* bnp;           // per-tile sums of dy' and dy' * xhat: rows [bntile0 + tm][Co], the
   long bnp2;            //   second set bnp2 floats further
   int bntile0;
+  int dense_out;        // the output grid IS the row grid (every forward, every stride-1 data
+                        //   gradient): output row = m * ldy, no pixel arithmetic
 };
 
 __device__ __forceinline__ int cv_swz(int r) { return (r >> 1) & 7; }
@@ -196,10 +198,14 @@ __device__ __forceinline__ void cv_out_prefetch(const ConvArgs& a, CvOut<BM / RP
   for (int k = 0; k < NR; ++k) {
     const int m = m0 + tid / CPR + k * RPP;
     o.ok[k] = m < a.M;
-    int b, rem, y, x;
-    cv_divmod(o.ok[k] ? m : m0, HW, inv_hw, b, rem);
-    cv_divmod(rem, a.Wr, inv_w, y, x);
-    o.yo[k] = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+    if (a.dense_out) {
+      o.yo[k] = (long)(o.ok[k] ? m : m0) * a.ldy + n0 + cc * 8;
+    } else {
+      int b, rem, y, x;
+      cv_divmod(o.ok[k] ? m : m0, HW, inv_hw, b, rem);
+      cv_divmod(rem, a.Wr, inv_w, y, x);
+      o.yo[k] = ((long)(b * a.Ho + y * a.oys + a.oy0) * a.Wo + x * a.oxs + a.ox0) * a.ldy + n0 + cc * 8;
+    }
   }
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
@@ -272,7 +278,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
     gca[j] = (unsigned)gc * 8u;                    // element offset of the chunk
     gpx[j] = a.pixchunk ? gc : 0;                  // stem: the chunk is a pixel step along x
     if (m < a.M) {
-      const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+      int b, rem, y, x;
+      cv_divmod(m, HW, 1.f / (float)HW, b, rem);
+      cv_divmod(rem, a.Wr, 1.f / (float)a.Wr, y, x);
       iy0[j] = y * a.sy;
       ix0[j] = x * a.sx;
       pix[j] = ((b * a.Hi + iy0[j]) * a.Wi + ix0[j]) * a.Ci;
@@ -496,7 +504,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
     for (int i = 0; i < IA; ++i) {
       const int m = m0 + (wave * IA + i) * 8 + (lane >> 3);
       if (m < a.M) {
-        const int b = m / HW, rem = m - b * HW, y = rem / a.Wr, x = rem - y * a.Wr;
+        int b, rem, y, x;
+        cv_divmod(m, HW, 1.f / (float)HW, b, rem);
+        cv_divmod(rem, a.Wr, 1.f / (float)a.Wr, y, x);
         iy0[i] = y * a.sy;
         ix0[i] = x * a.sx;
         pix[i] = ((b * a.Hi + iy0[i]) * a.Wi + ix0[i]) * a.Ci;
@@ -972,6 +982,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
              Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk,
              nullptr, nullptr, nullptr, nullptr, 0, 0};
+  a.dense_out = (Ho == Hr && Wo == Wr && oys == 1 && oxs == 1 && oy0 == 0 && ox0 == 0) ? 1 : 0;
   if (bn) {
     a.bnx = (const bf16_t*)bn->bnx;
     a.bny = (const bf16_t*)bn->bny;
