@@ -210,12 +210,15 @@ class BnBwdLink:
     identity and version are recorded so a gradient that autograd summed with another consumer's
     (or modified) is never paired with stale partials."""
 
-    __slots__ = ("x", "stat", "mode", "pending")
+    __slots__ = ("x", "stat", "mode", "mask", "pending")
 
-    def __init__(self, x: torch.Tensor, stat: torch.Tensor, mode: int):
+    def __init__(self, x: torch.Tensor, stat: torch.Tensor, mode: int, mask: Optional[torch.Tensor] = None):
         self.x = x
         self.stat = stat
-        self.mode = mode            # 2: mask recomputed from x; 1: mask read from the BN output
+        # 2: mask recomputed from x; 1: mask read from the BN output; 3: the forward's ReLU
+        # bitmask (`mask`, uint8, one byte per 8 channels)
+        self.mode = mode
+        self.mask = mask
         self.pending = None
 
     def take(self, dy: torch.Tensor):
@@ -240,7 +243,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
     empty_phase = any(not rs for _, _, _, rs in phases)
     C = _C()
     bn_plan = None
-    if bn is not None and (bn.mode == 2 or bn_y is not None) and not (accumulate and empty_phase) \
+    if bn is not None and (bn.mode in (2, 3) or bn_y is not None) and not (accumulate and empty_phase) \
             and bn.x.shape == tuple(x_shape) and co % 64 == 0:
         tiles = []
         for _, (Hr, Wr), taps, rs in phases:
@@ -271,7 +274,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
         geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
         if bn_plan is not None:
             part, rows = bn_plan
-            if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, bn_y if bn.mode == 1 else None,
+            msrc = bn.mask if bn.mode == 3 else (bn_y if bn.mode == 1 else None)
+            if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, msrc,
                                bn.stat, part, tile0, rows):
                 bm = C.conv_igemm_tile_m(_CFG, ci, geo[11], len(taps) // 2 * (co // 64))
                 tile0 += (geo[11] + bm - 1) // bm

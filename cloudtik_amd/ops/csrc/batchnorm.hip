@@ -203,8 +203,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ res,
                                                        const float* __restrict__ a,
                                                        const float* __restrict__ b,
-                                                       bf16_t* __restrict__ y, long total_vec,
-                                                       int CV, int relu) {
+                                                       bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                       long total_vec, int CV, int relu) {
   const long stride = (long)gridDim.x * blockDim.x;
   const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const bool fixed = bn_fixed_cv(CV);
@@ -224,24 +224,30 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
       if (v >= total_vec) break;
       if (!fixed) { const int cv = (int)(v % CV); bn_load8(a, cv, av); bn_load8(b, cv, bv); }
       u16x8 o;
+      uint32_t bits = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = bn_pre(bf2f(xv[u][j]), av[j], bv[j], bf2f(rv[u][j]));
         if (relu) t = fmaxf(t, 0.f);
         o[j] = f2bf(t);
+        bits |= (o[j] != 0 && !(o[j] & 0x8000u) ? 1u : 0u) << j;     // y > 0
       }
       reinterpret_cast<u16x8*>(y)[v] = o;
+      if (mask) mask[v] = (uint8_t)bits;
     }
   }
 }
 
 // ReLU mask source for the backward: mode 0 = no ReLU, 1 = read y (fused residual add),
-// 2 = recompute the pre-activation from x and the forward affine (a, b): no y read at all
+// 2 = recompute the pre-activation from x and the forward affine (a, b): no y read at all,
+// 3 = the forward's bitmask (one byte per 8-channel vector, bit j = y > 0: what a BN +
+// residual + ReLU forward writes beside y, 1/16 of y's bytes)
 struct BnMask {
   int mode;
   const bf16_t* y;
   const float* fa;
   const float* fb;
+  const uint8_t* m;
 };
 
 // forward affine of channel vector cv (mode 2 only)
@@ -250,11 +256,12 @@ __device__ __forceinline__ void bn_mask_coef(const BnMask& mk, int cv, float (&f
 }
 
 __device__ __forceinline__ void bn_mask8(const BnMask& mk, const u16x8& yv, const u16x8& xv, const float (&fa)[8],
-                                         const float (&fb)[8], bool (&on)[8]) {
+                                         const float (&fb)[8], uint32_t mb, bool (&on)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (mk.mode == 0) on[j] = true;
     else if (mk.mode == 1) on[j] = bf2f(yv[j]) > 0.f;
+    else if (mk.mode == 3) on[j] = (mb >> j) & 1u;
     else on[j] = bf2f(f2bf(bn_pre(bf2f(xv[j]), fa[j], fb[j], 0.f))) > 0.f;
   }
 }
@@ -284,6 +291,7 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
     int r = r0 + rl;
     for (; r + (U - 1) * L.RPI < r1; r += U * L.RPI) {
       u16x8 g[U], xv[U], yv[U];
+      uint32_t mb[U];
       size_t o[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -291,11 +299,12 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
         g[u] = reinterpret_cast<const u16x8*>(dy)[o[u]];
         xv[u] = reinterpret_cast<const u16x8*>(x)[o[u]];
         yv[u] = mk.mode == 1 ? reinterpret_cast<const u16x8*>(mk.y)[o[u]] : u16x8(0);
+        mb[u] = mk.mode == 3 ? mk.m[o[u]] : 0u;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         bool on[8];
-        bn_mask8(mk, yv[u], xv[u], fa, fb, on);
+        bn_mask8(mk, yv[u], xv[u], fa, fb, mb[u], on);
         u16x8 od;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -312,8 +321,9 @@ __global__ __launch_bounds__(BN_RT) void bn_bwd_reduce_kernel(
       const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
       const u16x8 xv = reinterpret_cast<const u16x8*>(x)[o];
       const u16x8 yv = mk.mode == 1 ? reinterpret_cast<const u16x8*>(mk.y)[o] : u16x8(0);
+      const uint32_t mb = mk.mode == 3 ? mk.m[o] : 0u;
       bool on[8];
-      bn_mask8(mk, yv, xv, fa, fb, on);
+      bn_mask8(mk, yv, xv, fa, fb, mb, on);
       u16x8 od;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -386,6 +396,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
   for (long v0 = blockIdx.x * (long)blockDim.x + threadIdx.x; v0 < total_vec; v0 += BN_EW * stride) {
     u16x8 g[BN_EW], xv[BN_EW], yv[BN_EW];
+    uint32_t mb[BN_EW];
 #pragma unroll
     for (int u = 0; u < BN_EW; ++u) {
       const long v = v0 + u * stride;
@@ -393,6 +404,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       g[u] = in ? reinterpret_cast<const u16x8*>(dy)[v] : u16x8(0);
       xv[u] = in ? reinterpret_cast<const u16x8*>(x)[v] : u16x8(0);
       yv[u] = (in && mk.mode == 1) ? reinterpret_cast<const u16x8*>(mk.y)[v] : u16x8(0);
+      mb[u] = (in && mk.mode == 3) ? mk.m[v] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < BN_EW; ++u) {
@@ -404,7 +416,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         bn_mask_coef(mk, cv, fa, fb);
       }
       bool on[8];
-      bn_mask8(mk, yv[u], xv[u], fa, fb, on);
+      bn_mask8(mk, yv[u], xv[u], fa, fb, mb[u], on);
       u16x8 o, od;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -576,7 +588,7 @@ static int bn_target_blocks() {
 // workspace: part = float[2 * 2048 * C]; stat = float[4 * C] (save_mean, save_invstd, a, b)
 extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma, const void* beta,
                                float* run_mean, float* run_var, void* y, float* part, float* stat,
-                               int M, int C, float eps, float momentum, int relu,
+                               int M, int C, float eps, float momentum, int relu, void* mask,
                                hipStream_t stream) {
   if (C % 8 || C / 8 > BN_RT || M <= 0) return -1;
   BnLayout L = bn_layout(M, C, bn_target_blocks());
@@ -589,7 +601,7 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
                                                            stat + C, stat + 2 * C, stat + 3 * C);
   const long tv = (long)M * (C / 8);
   BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, stat + 2 * C, stat + 3 * C,
-                 (bf16_t*)y, tv, C / 8, relu);
+                 (bf16_t*)y, (uint8_t*)mask, tv, C / 8, relu);
   return 0;
 }
 
@@ -640,7 +652,7 @@ __global__ __launch_bounds__(256) void bn_partials_merge_kernel(const float* __r
 extern "C" int ct_bn_fwd_train_given(const void* x, const void* res, const void* gamma, const void* beta,
                                      float* run_mean, float* run_var, void* y, const float* part, int tiles,
                                      int rows_per_tile, float* stat, int M, int C, float eps, float momentum,
-                                     int relu, hipStream_t stream) {
+                                     int relu, void* mask, hipStream_t stream) {
   if (C % 8 || M <= 0 || tiles <= 0 || (long)tiles * rows_per_tile < M) return -1;
   if (tiles > 2 * BN_MERGE_GROUP) {
     // merge groups of tiles first, into the tail of the partial buffer (means at
@@ -660,7 +672,7 @@ extern "C" int ct_bn_fwd_train_given(const void* x, const void* res, const void*
                                                            stat + C, stat + 2 * C, stat + 3 * C);
   const long tv = (long)M * (C / 8);
   BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, stat + 2 * C, stat + 3 * C,
-                 (bf16_t*)y, tv, C / 8, relu);
+                 (bf16_t*)y, (uint8_t*)mask, tv, C / 8, relu);
   return 0;
 }
 
@@ -699,7 +711,8 @@ extern "C" int ct_bn_apply(const void* x, const void* res, const float* a, const
                            int M, int C, int relu, hipStream_t stream) {
   if (C % 8) return -1;
   const long tv = (long)M * (C / 8);
-  BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, a, b, (bf16_t*)y, tv, C / 8, relu);
+  BN_EW_DISPATCH(bn_apply_kernel, tv, (const bf16_t*)x, (const bf16_t*)res, a, b, (bf16_t*)y, (uint8_t*)nullptr, tv,
+                 C / 8, relu);
   return 0;
 }
 
@@ -709,15 +722,17 @@ extern "C" int ct_bn_apply(const void* x, const void* res, const float* a, const
 extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const void* gamma, const float* stat,
                          void* dx, void* dres, void* dgamma, void* dbeta, int param_flags, float* part,
                          float* coef, int M, int C, int relu_mode, hipStream_t stream) {
-  if (C % 8 || C / 8 > BN_RT || M <= 0 || relu_mode < 0 || relu_mode > 2) return -1;
-  if (relu_mode == 1 && !y) return -2;
+  if (C % 8 || C / 8 > BN_RT || M <= 0 || relu_mode < 0 || relu_mode > 3) return -1;
+  if ((relu_mode == 1 || relu_mode == 3) && !y) return -2;
   BnLayout L = bn_layout(M, C, bn_target_blocks());
   const int nblk = bn_nblk(L);
-  const BnMask mk{relu_mode, (const bf16_t*)y, stat + 2 * C, stat + 3 * C};
+  // relu_mode 3: `y` is the forward's ReLU bitmask
+  const BnMask mk{relu_mode, relu_mode == 1 ? (const bf16_t*)y : nullptr, stat + 2 * C, stat + 3 * C,
+                  relu_mode == 3 ? (const uint8_t*)y : nullptr};
   // BN + residual add + ReLU: the reduction pass writes the masked gradient (= the residual
   // branch's gradient, returned as dres) and the apply pass reads it back instead of dy and y:
   // 7 instead of 8 activation-sized passes over the biggest ResNet tensors
-  bf16_t* dm = (relu_mode == 1 && dres) ? (bf16_t*)dres : nullptr;
+  bf16_t* dm = ((relu_mode == 1 || relu_mode == 3) && dres) ? (bf16_t*)dres : nullptr;
   if (bn_unroll() == 8)
     bn_bwd_reduce_kernel<8><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dy, mk, (const bf16_t*)x, stat, stat + C, L,
                                                         part, part + (size_t)2048 * C, dm);
@@ -735,7 +750,7 @@ extern "C" int ct_bn_bwd(const void* dy, const void* y, const void* x, const voi
         (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C, coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
   if (dm) {
-    const BnMask none{0, nullptr, nullptr, nullptr};
+    const BnMask none{0, nullptr, nullptr, nullptr, nullptr};
     BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dm, none, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
                    (bf16_t*)dx, (bf16_t*)nullptr, tv, C / 8);
   } else {
@@ -786,7 +801,7 @@ extern "C" int ct_bn_bwd_given(const void* dym, const void* x, const void* gamma
         q1, q2, G, M, C, (const bf16_t*)gamma, stat, stat + C, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C,
         coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
-  const BnMask none{0, nullptr, nullptr, nullptr};
+  const BnMask none{0, nullptr, nullptr, nullptr, nullptr};
   BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dym, none, (const bf16_t*)x, coef, coef + C, coef + 2 * C,
                  (bf16_t*)dx, (bf16_t*)nullptr, tv, C / 8);
   return hipGetLastError() == hipSuccess ? 0 : 7;

@@ -39,10 +39,10 @@ int ct_clip_coef(const float*, float*, float, float, hipStream_t);
 int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, const float*, int, int,
                 float, hipStream_t);
 int ct_bn_fwd_train(const void*, const void*, const void*, const void*, float*, float*, void*, float*,
-                    float*, int, int, float, float, int, hipStream_t);
+                    float*, int, int, float, float, int, void*, hipStream_t);
 int ct_bn_apply(const void*, const void*, const float*, const float*, void*, int, int, int, hipStream_t);
 int ct_bn_fwd_train_given(const void*, const void*, const void*, const void*, float*, float*, void*, const float*, int,
-                          int, float*, int, int, float, float, int, hipStream_t);
+                          int, float*, int, int, float, float, int, void*, hipStream_t);
 int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
                          int, int, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
@@ -440,10 +440,20 @@ static void check_nhwc(const at::Tensor& x, const char* name) {
 }
 static int64_t nhwc_rows(const at::Tensor& x) { return x.numel() / x.size(1); }
 
-// returns (y, stat) with stat = float[4C]: save_mean, save_invstd, a, b (y = x * a + b ...)
+// optional ReLU bitmask output of the training forwards: uint8, one byte per 8 channels
+static void* mask_ptr(const c10::optional<at::Tensor>& mask, const at::Tensor& x) {
+  if (!mask.has_value() || !mask->defined()) return nullptr;
+  TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+              mask->numel() * 8 == x.numel(), "ReLU mask: uint8 [numel / 8]");
+  return mask->data_ptr();
+}
+
+// returns (y, stat) with stat = float[4C]: save_mean, save_invstd, a, b (y = x * a + b ...);
+// mask_out (optional, uint8 [numel / 8]) receives the ReLU bitmask (bit j of byte v: y > 0)
 std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma,
                                      at::Tensor beta, at::Tensor run_mean, at::Tensor run_var,
-                                     double eps, double momentum, bool relu) {
+                                     double eps, double momentum, bool relu,
+                                     c10::optional<at::Tensor> mask_out) {
   check_nhwc(x, "x");
   const int C = x.size(1);
   const long M = nhwc_rows(x);
@@ -457,7 +467,7 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
   int rc = ct_bn_fwd_train(x.data_ptr(), optr(res), gamma.data_ptr(), beta.data_ptr(),
                            run_mean.data_ptr<float>(), run_var.data_ptr<float>(), y.data_ptr(),
                            part.data_ptr<float>(), stat.data_ptr<float>(), (int)M, C, (float)eps,
-                           (float)momentum, relu ? 1 : 0, cur_stream());
+                           (float)momentum, relu ? 1 : 0, mask_ptr(mask_out, x), cur_stream());
   TORCH_CHECK(rc == 0, "bn_fwd_train: unsupported C=", C);
   return {y, stat};
 }
@@ -466,7 +476,8 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
 // part = means [tiles][C] then M2 [tiles][C], tiles = ceil(M / rows_per_tile)
 std::vector<at::Tensor> bn_fwd_train_given(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma,
                                            at::Tensor beta, at::Tensor run_mean, at::Tensor run_var, at::Tensor part,
-                                           int64_t rows_per_tile, double eps, double momentum, bool relu) {
+                                           int64_t rows_per_tile, double eps, double momentum, bool relu,
+                                           c10::optional<at::Tensor> mask_out) {
   check_nhwc(x, "x");
   const int C = x.size(1);
   const long M = nhwc_rows(x);
@@ -482,7 +493,8 @@ std::vector<at::Tensor> bn_fwd_train_given(at::Tensor x, c10::optional<at::Tenso
   int rc = ct_bn_fwd_train_given(x.data_ptr(), optr(res), gamma.data_ptr(), beta.data_ptr(),
                                  run_mean.data_ptr<float>(), run_var.data_ptr<float>(), y.data_ptr(),
                                  part.data_ptr<float>(), (int)tiles, (int)rows_per_tile, stat.data_ptr<float>(),
-                                 (int)M, C, (float)eps, (float)momentum, relu ? 1 : 0, cur_stream());
+                                 (int)M, C, (float)eps, (float)momentum, relu ? 1 : 0, mask_ptr(mask_out, x),
+                                 cur_stream());
   TORCH_CHECK(rc == 0, "bn_fwd_train_given: unsupported C=", C);
   return {y, stat};
 }
@@ -535,7 +547,8 @@ at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, a
 }
 
 // returns (dx, dres, dgamma, dbeta).  relu_mode: 0 no ReLU, 1 mask from y (forward had a
-// residual), 2 mask recomputed from x and the forward's (a, b) -- y may be undefined then.
+// residual), 2 mask recomputed from x and the forward's (a, b) -- y may be undefined then,
+// 3 y is the forward's ReLU bitmask (uint8 [numel / 8]).
 std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, at::Tensor gamma,
                                at::Tensor stat, int64_t relu_mode, bool need_dres,
                                c10::optional<at::Tensor> dgamma_acc, c10::optional<at::Tensor> dbeta_acc) {
@@ -546,11 +559,15 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::T
   const long M = nhwc_rows(x);
   TORCH_CHECK(C <= 2048 && stat.numel() == 4 * (long)C, "bn_bwd: stat must be float[4C], C <= 2048");
   CHECK_F32(stat);
-  TORCH_CHECK(relu_mode >= 0 && relu_mode <= 2, "bn_bwd: relu_mode 0/1/2");
+  TORCH_CHECK(relu_mode >= 0 && relu_mode <= 3, "bn_bwd: relu_mode 0/1/2/3");
   if (relu_mode == 1) {
     TORCH_CHECK(y.has_value() && y->defined(), "bn_bwd: relu_mode 1 needs y");
     check_nhwc(*y, "y");
     TORCH_CHECK(y->sizes() == x.sizes(), "bn_bwd: y shape");
+  }
+  if (relu_mode == 3) {
+    TORCH_CHECK(y.has_value() && y->defined(), "bn_bwd: relu_mode 3 needs the mask");
+    mask_ptr(y, x);
   }
   TORCH_CHECK(dyc.sizes() == x.sizes(), "bn_bwd: dy shape");
   auto dx = at::empty_like(x);
@@ -566,7 +583,8 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> y, at::T
   auto dgamma = acc ? *dgamma_acc : at::empty_like(gamma), dbeta = acc ? *dbeta_acc : at::empty_like(gamma);
   auto coef = at::empty({3 * (long)C}, x.options().dtype(at::kFloat));
   auto part = at::empty({2 * 2048 * (long)C}, x.options().dtype(at::kFloat));
-  int rc = ct_bn_bwd(dyc.data_ptr(), relu_mode == 1 ? y->data_ptr() : nullptr, x.data_ptr(), gamma.data_ptr(),
+  int rc = ct_bn_bwd(dyc.data_ptr(), (relu_mode == 1 || relu_mode == 3) ? y->data_ptr() : nullptr, x.data_ptr(),
+                     gamma.data_ptr(),
                      stat.data_ptr<float>(), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
                      dgamma.data_ptr(), dbeta.data_ptr(),
                      (gamma.scalar_type() == at::kFloat ? 1 : 0) | (acc ? 2 : 0), part.data_ptr<float>(),
@@ -642,9 +660,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_into", &sumsq_into);
   m.def("clip_coef", &clip_coef);
   m.def("xent_fwd", &xent_fwd);
-  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_train", &bn_fwd_train, pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("gamma"),
+        pybind11::arg("beta"), pybind11::arg("run_mean"), pybind11::arg("run_var"), pybind11::arg("eps"),
+        pybind11::arg("momentum"), pybind11::arg("relu"), pybind11::arg("mask_out") = pybind11::none());
   m.def("bn_apply", &bn_apply);
-  m.def("bn_fwd_train_given", &bn_fwd_train_given);
+  m.def("bn_fwd_train_given", &bn_fwd_train_given, pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("gamma"),
+        pybind11::arg("beta"), pybind11::arg("run_mean"), pybind11::arg("run_var"), pybind11::arg("part"),
+        pybind11::arg("rows_per_tile"), pybind11::arg("eps"), pybind11::arg("momentum"), pybind11::arg("relu"),
+        pybind11::arg("mask_out") = pybind11::none());
   m.def("bn_fwd_train_pool", &bn_fwd_train_pool);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd);

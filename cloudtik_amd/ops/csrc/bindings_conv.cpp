@@ -10,8 +10,8 @@ extern "C" {
 int ct_conv_igemm(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
                   int, int, int, int, const int*, int, float*, int, hipStream_t);
 int ct_conv_igemm_bn(const void*, int, int, int, const void*, void*, int, int, int, int, int, int, int, int, int, int,
-                     int, int, int, int, const int*, int, int, const void*, const void*, const float*, float*, long,
-                     int, hipStream_t);
+                     int, int, int, int, const int*, int, int, const void*, const void*, const void*, const float*,
+                     float*, long, int, hipStream_t);
 int ct_conv_igemm_rows(int, int, int, int);
 int ct_conv_igemm_tile_m(int);
 int ct_conv_igemm_part_rows(int);
@@ -79,10 +79,16 @@ bool conv_igemm_bn(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t
   // the BatchNorm input must share Y's memory layout exactly (same shape, both NHWC-dense)
   TORCH_CHECK(Y.dim() == 4 && Y.is_contiguous(at::MemoryFormat::ChannelsLast) && bnx.sizes() == Y.sizes() &&
               bnx.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm_bn: bnx / Y layout");
+  // bny: the BatchNorm output (bf16, Y's layout) or its ReLU bitmask (uint8, one byte per 8
+  // channels of every pixel: Y.numel() / 8 bytes)
   const bool has_y = bny.has_value() && bny->defined();
-  if (has_y)
+  const bool is_mask = has_y && bny->scalar_type() == at::kByte;
+  if (is_mask) {
+    TORCH_CHECK(bny->is_cuda() && bny->is_contiguous() && bny->numel() * 8 == Y.numel(), "conv_igemm_bn: bny mask");
+  } else if (has_y) {
     TORCH_CHECK(bny->is_cuda() && bny->scalar_type() == at::kBFloat16 && bny->sizes() == Y.sizes() &&
                 bny->is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm_bn: bny / Y layout");
+  }
   const int Ci = (int)X.size(1), Hi = (int)X.size(2), Wi = (int)X.size(3);
   const int T = (int)taps.size() / 2, Co = (int)W.size(0);
   TORCH_CHECK(Ci % 64 == 0 && W.size(1) == (int64_t)T * Ci, "conv_igemm_bn: W columns != taps * Ci");
@@ -103,7 +109,8 @@ bool conv_igemm_bn(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t
   const int rc = ct_conv_igemm_bn(X.data_ptr(), Hi, Wi, Ci, W.data_ptr(), Y.data_ptr(), (int)geo[0], (int)geo[1],
                                   (int)geo[2], (int)geo[3], (int)geo[4], (int)geo[5], (int)geo[6], (int)geo[7],
                                   (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), accumulate ? 1 : 0,
-                                  (int)cfg, bnx.data_ptr(), has_y ? bny->data_ptr() : nullptr, stat.data_ptr<float>(), part.data_ptr<float>(), rows * Co,
+                                  (int)cfg, bnx.data_ptr(), (has_y && !is_mask) ? bny->data_ptr() : nullptr,
+                                  is_mask ? bny->data_ptr() : nullptr, stat.data_ptr<float>(), part.data_ptr<float>(), rows * Co,
                                   (int)tile0, at::hip::getCurrentHIPStream().stream());
   return rc == 0;
 }

@@ -62,6 +62,7 @@ struct ConvArgs {
   float* bnp;           // per-tile sums of dy' and dy' * xhat: rows [bntile0 + tm][Co], the
   long bnp2;            //   second set bnp2 floats further
   int bntile0;
+  const uint8_t* bnm;   // EPI 2: the BatchNorm's ReLU bitmask (byte per 8 channels), or null
   int dense_out;        // the output grid IS the row grid (every forward, every stride-1 data
                         //   gradient): output row = m * ldy, no pixel arithmetic
 };
@@ -186,6 +187,7 @@ struct CvOut {
   long yo[NR];
   bool ok[NR];
   u16x8 old[NR], xv[NR], yv[NR];
+  uint32_t mb[NR];
 };
 
 template <int BM, int CPR, int RPP, int EPI>
@@ -213,7 +215,8 @@ __device__ __forceinline__ void cv_out_prefetch(const ConvArgs& a, CvOut<BM / RP
     if (a.accumulate) o.old[k] = *(const u16x8*)(a.Y + o.yo[k]);
     if constexpr (EPI == 2) {
       o.xv[k] = *(const u16x8*)(a.bnx + o.yo[k]);
-      if (a.bny) o.yv[k] = *(const u16x8*)(a.bny + o.yo[k]);
+      if (a.bnm) o.mb[k] = a.bnm[o.yo[k] >> 3];
+      else if (a.bny) o.yv[k] = *(const u16x8*)(a.bny + o.yo[k]);
     }
   }
 }
@@ -237,7 +240,8 @@ __device__ __forceinline__ void cv_out_store(const ConvArgs& a, CvOut<BM / RPP>&
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xf = bf2f(o.xv[k][e]);
-        const bool on = a.bny ? bf2f(o.yv[k][e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f;
+        const bool on = a.bnm ? ((o.mb[k] >> e) & 1u) != 0
+                        : (a.bny ? bf2f(o.yv[k][e]) > 0.f : bf2f(f2bf(__builtin_fmaf(xf, bfa[e], bfb[e]))) > 0.f);
         if (!on) v[e] = 0;
         const float d = bf2f(v[e]);
         s1[e] += d;
@@ -939,6 +943,7 @@ extern "C" void ct_conv_stream_set_cus(int cus) { g_cv_stream_cus = cus > 0 ? cu
 struct ConvBnBwd {
   const void* bnx;
   const void* bny;
+  const void* bnm;
   const float* bnstat;
   float* bnp;
   long bnp2;
@@ -962,10 +967,11 @@ extern "C" int ct_conv_igemm(const void* X, int Hi, int Wi, int Ci, const void* 
 extern "C" int ct_conv_igemm_bn(const void* X, int Hi, int Wi, int Ci, const void* W, void* Y, int Hr, int Wr, int sy,
                                 int sx, int Ho, int Wo, int oys, int oxs, int oy0, int ox0, int ldy, int Co, int M,
                                 int T, const int* taps, int accumulate, int cfg, const void* bnx, const void* bny,
-                                const float* bnstat, float* bnp, long bnp2, int tile0, hipStream_t stream) {
+                                const void* bnm, const float* bnstat, float* bnp, long bnp2, int tile0,
+                                hipStream_t stream) {
   if (!bnx || !bnstat || !bnp || ((uintptr_t)bnx & 15) || ((uintptr_t)bny & 15) || ((uintptr_t)Y & 15) || ldy % 8)
     return 8;
-  const ConvBnBwd bn{bnx, bny, bnstat, bnp, bnp2, tile0};
+  const ConvBnBwd bn{bnx, bny, bnm, bnstat, bnp, bnp2, tile0};
   return conv_igemm_impl(X, Hi, Wi, Ci, W, Y, Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, taps,
                          accumulate, nullptr, cfg, &bn, stream);
 }
@@ -986,6 +992,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   if (bn) {
     a.bnx = (const bf16_t*)bn->bnx;
     a.bny = (const bf16_t*)bn->bny;
+    a.bnm = (const uint8_t*)bn->bnm;
     a.bnstat = bn->bnstat;
     a.bnp = bn->bnp;
     a.bnp2 = bn->bnp2;

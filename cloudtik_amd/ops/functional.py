@@ -1,6 +1,8 @@
 """Autograd front-ends for the HIP op library (GPU) with reference fallbacks (CPU)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -210,28 +212,35 @@ def cross_entropy_fused(x, W, b, labels, V=None, ignore_index=-100, label_smooth
 
 
 # ----------------------------------------------------------------------------- batchnorm
+# BN + residual + ReLU keeps a ReLU bitmask for its backward instead of re-reading y
+_BN_RELU_BITMASK = os.environ.get("CLOUDTIK_AMD_BN_RELU_BITMASK", "1") == "1"
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, run_mean, run_var, relu, momentum, eps):
+        has_res = residual is not None
+        # ReLU mask for the backward: without a residual it is recomputed from x and the
+        # forward's affine coefficients (stat), so y is neither saved nor re-read; with one the
+        # forward also writes a bitmask (1 byte per 8 channels, 1/16 of y) that the backward
+        # reads instead of y (mode 3; mode 1 = read y itself)
+        mode = 0 if not relu else ((3 if _BN_RELU_BITMASK and x.numel() % 8 == 0 else 1) if has_res else 2)
+        mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8) if mode == 3 else None
         given = getattr(x, "_ct_bn_part", None)
         if given is not None:
             # statistics already reduced per tile by the conv that produced x (ops/conv.py)
             y, stat = _C().bn_fwd_train_given(x, residual, gamma, beta, run_mean, run_var, given[0], given[1],
-                                              eps, momentum, relu)
+                                              eps, momentum, relu, mask)
         else:
-            y, stat = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu)
-        has_res = residual is not None
-        # ReLU mask for the backward: without a residual it is recomputed from x and the
-        # forward's affine coefficients (stat), so y is neither saved nor re-read
-        mode = 0 if not relu else (1 if has_res else 2)
-        ctx.save_for_backward(x, y if mode == 1 else None, gamma, stat)
+            y, stat = _C().bn_fwd_train(x, residual, gamma, beta, run_mean, run_var, eps, momentum, relu, mask)
+        ctx.save_for_backward(x, y if mode == 1 else mask, gamma, stat)
         ctx.params = (gamma, beta)
         ctx.cfg = (mode, has_res)
         ctx.bn_link = None
         if mode != 0 and x.dim() == 4:
             # a conv consuming y may run our backward reduction in its dgrad epilogue (ops/conv.py)
             from cloudtik_amd.ops.conv import BnBwdLink
-            ctx.bn_link = BnBwdLink(x, stat, mode)
+            ctx.bn_link = BnBwdLink(x, stat, mode, mask)
             y._ct_bn_bwd = ctx.bn_link
         return y
 

@@ -153,8 +153,8 @@ def test_bottleneck_matches_miopen_path(cuda, down, stride, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("down,stride", [(True, 2), (False, 1)])
-def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, monkeypatch):
+@pytest.mark.parametrize("down,stride,bitmask", [(True, 2, True), (False, 1, True), (False, 1, False)])
+def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, bitmask, monkeypatch):
     """conv.hip EPI 2: the BatchNorm + ReLU backward reduction done in the consuming conv's
     data-gradient epilogue gives the gradients of the separate reduction pass, and actually runs:
     bn1 -> conv2 (incl. the stride-2 phase plan) and bn2 -> conv3 (mask recomputed from x), and
@@ -162,6 +162,8 @@ def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, monkeypatch
     accumulates into the residual gradient."""
     from cloudtik_amd import ops
     from cloudtik_amd.models.resnet import Bottleneck
+    from cloudtik_amd.ops import functional as FN
+    monkeypatch.setattr(FN, "_BN_RELU_BITMASK", bitmask)      # residual BN: ReLU bitmask vs y
     torch.manual_seed(1)
     cin = 64 if down else 256
     kw = dict(device=cuda, dtype=torch.bfloat16)

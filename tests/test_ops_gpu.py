@@ -538,6 +538,16 @@ def test_batchnorm_repeat_and_relu_modes(cuda, C):
         d2 = C_.bn_bwd(dy, None, x, g, stat, 2, False, None, None)
         d1 = C_.bn_bwd(dy, y, x, g, stat, 1, False, None, None)
         assert torch.equal(d1[0], d2[0]) and torch.equal(d1[2], d2[2]) and torch.equal(d1[3], d2[3])
+        # with a residual: the forward's ReLU bitmask (mode 3) == reading y (mode 1), bit for bit
+        res = torch.randn_like(x)
+        mask = torch.empty(x.numel() // 8, device=cuda, dtype=torch.uint8)
+        yr, statr = C_.bn_fwd_train(x, res, g, b, rm.clone(), rv.clone(), 1e-5, 0.1, True, mask)
+        assert torch.equal(mask.view(-1, 1).bitwise_and(1 << torch.arange(8, device=cuda, dtype=torch.uint8)) != 0,
+                           (yr.permute(0, 2, 3, 1).reshape(-1, 8) > 0))
+        m1 = C_.bn_bwd(dy, yr, x, g, statr, 1, True, None, None)
+        m3 = C_.bn_bwd(dy, mask, x, g, statr, 3, True, None, None)
+        for a_, b_ in zip(m1, m3):
+            assert torch.equal(a_, b_)
         outs.append((y, stat, rm.clone()))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1])
