@@ -605,45 +605,55 @@ extern "C" int ct_bn_fwd_train(const void* x, const void* res, const void* gamma
   return 0;
 }
 
-// First-level Chan merge of per-tile (mean, M2) partials: block (g, cb) merges tiles
+// First-level merge of per-block (mean, M2) partials: block (g, cb) merges partials
 // [g * GROUP, (g + 1) * GROUP) of channels [64 cb, 64 cb + 64) -- one lane per channel, the 4
-// waves take interleaved tiles and are merged through LDS -- into one (mean, M2) partial of
-// GROUP * rows_per_tile rows.  The conv epilogue emits one partial per 128-row tile (6272 for a
-// ResNet-50 layer-1 conv); the single-block-per-64-channels finalize read them serially.
+// waves take interleaved partials and are combined through LDS -- into one (mean, M2) partial
+// of GROUP * rows_per_tile rows.  The conv epilogue emits one partial per 64-row wave block
+// (12544 for a ResNet-50 layer-1 conv); the single-block-per-64-channels finalize would read
+// them serially.
 constexpr int BN_MERGE_GROUP = 64;
+// Two passes over the group's partials (they stay in cache) instead of a sequential Chan merge:
+// mean_g = sum(n_t mean_t) / sum(n_t), then M2_g = sum(M2_t + n_t (mean_t - mean_g)^2) -- no
+// division inside the loop (the dependent divisions of the sequential merge made it
+// latency-bound: 52 launches, 0.47 ms per ResNet-50 step).
 __global__ __launch_bounds__(256) void bn_partials_merge_kernel(const float* __restrict__ pmean,
                                                                const float* __restrict__ pm2, int tiles,
                                                                int rows_per_tile, int M, int C,
                                                                float* __restrict__ omean, float* __restrict__ om2) {
-  __shared__ float sn[4][64], sm[4][64], sq[4][64];
+  __shared__ float sn[4][64], ss[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + lane, g = blockIdx.x;
   const int t0 = g * BN_MERGE_GROUP, t1 = min(tiles, t0 + BN_MERGE_GROUP);
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < C) {
+  const bool live = c < C;
+  float n = 0.f, s = 0.f;
+  if (live) {
+#pragma unroll 4
     for (int t = t0 + w; t < t1; t += 4) {
-      const float nb = (float)min(rows_per_tile, M - t * rows_per_tile);
-      const float mb = pmean[(size_t)t * C + c], qb = pm2[(size_t)t * C + c];
-      const float nn = n + nb, d = mb - mean;
-      mean += d * nb / nn;
-      m2 += qb + d * d * n * nb / nn;
-      n = nn;
+      const float nb = (float)max(0, min(rows_per_tile, M - t * rows_per_tile));
+      n += nb;
+      s += nb * pmean[(size_t)t * C + c];
     }
   }
-  sn[w][lane] = n; sm[w][lane] = mean; sq[w][lane] = m2;
+  sn[w][lane] = n;
+  ss[w][lane] = s;
   __syncthreads();
-  if (w != 0 || c >= C) return;
-#pragma unroll
-  for (int k = 1; k < 4; ++k) {
-    const float nb = sn[k][lane];
-    if (nb <= 0.f) continue;
-    const float nn = n + nb, d = sm[k][lane] - mean;
-    mean += d * nb / nn;
-    m2 += sq[k][lane] + d * d * n * nb / nn;
-    n = nn;
+  const float ng = sn[0][lane] + sn[1][lane] + sn[2][lane] + sn[3][lane];
+  const float mg = ng > 0.f ? (ss[0][lane] + ss[1][lane] + ss[2][lane] + ss[3][lane]) / ng : 0.f;
+  float q = 0.f;
+  if (live) {
+#pragma unroll 4
+    for (int t = t0 + w; t < t1; t += 4) {
+      const float nb = (float)max(0, min(rows_per_tile, M - t * rows_per_tile));
+      const float d = pmean[(size_t)t * C + c] - mg;
+      q += pm2[(size_t)t * C + c] + nb * d * d;
+    }
   }
-  omean[(size_t)g * C + c] = mean;
-  om2[(size_t)g * C + c] = m2;
+  __syncthreads();                                    // ss reuse
+  ss[w][lane] = q;
+  __syncthreads();
+  if (w != 0 || !live) return;
+  omean[(size_t)g * C + c] = mg;
+  om2[(size_t)g * C + c] = ss[0][lane] + ss[1][lane] + ss[2][lane] + ss[3][lane];
 }
 
 // Training forward whose statistics were produced by the PRODUCER of x: per-tile means
