@@ -199,6 +199,7 @@ _DGRAD_W_CACHE = os.environ.get("CLOUDTIK_AMD_CONV_DGRAD_WCACHE", "1") == "1"
 
 
 BN_BWD_FUSE = os.environ.get("CLOUDTIK_AMD_CONV_BN_BWD_FUSE", "1") == "1"
+_DGRAD_ZFILL = os.environ.get("CLOUDTIK_AMD_CONV_DGRAD_ZFILL", "1") == "1"
 
 
 class BnBwdLink:
@@ -253,11 +254,16 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
                 tiles.append((m + bm - 1) // bm)
         rows = sum(tiles)
         bn_plan = (torch.empty(2 * rows * ci, device=dy.device, dtype=torch.float32), rows)
+    live = [ph for ph in phases if ph[3]]
+    # a 1x1 stride-2 data gradient (the downsample convs) writes only the (even, even) pixels:
+    # the kernel stores the three odd-parity zeros beside each of them instead of a zero-fill
+    # pass over the whole gradient first (conv.hip accumulate mode 2)
+    zfill = (_DGRAD_ZFILL and not accumulate and bn_plan is None and len(live) == 1 and live[0][0] == (0, 0)
+             and tuple(stride) == (2, 2) and live[0][1] == (H // 2, W // 2) and H % 2 == 0 and W % 2 == 0
+             and ci % 8 == 0)
     if out is None:
         out = torch.empty((N, ci, H, W), device=dy.device, dtype=dy.dtype, memory_format=torch.channels_last)
-        if empty_phase and not accumulate:
-            out.zero_()
-    elif empty_phase and not accumulate:
+    if empty_phase and not accumulate and not zfill:
         out.zero_()
     wt = w.permute(1, 2, 3, 0)                      # [Ci, R, S, Co]
     sh, sw = stride
@@ -283,7 +289,12 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
             if tile0:
                 raise RuntimeError("conv_igemm_bn rejected a later phase of a supported data gradient")
             bn_plan = None                          # configuration without the fused epilogue
-        if not C.conv_igemm(dy, wm, out, geo, taps, accumulate, None, _CFG):
+        if not C.conv_igemm(dy, wm, out, geo, taps, 2 if zfill else int(accumulate), None, _CFG):
+            if zfill:                               # shape the zero-filling mode refuses
+                out.zero_()
+                zfill = False
+                if C.conv_igemm(dy, wm, out, geo, taps, 0, None, _CFG):
+                    continue
             raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)} w{tuple(w.shape)}")
     if bn_plan is not None:
         bn.pending = (bn_plan[0], tile0, bn_plan[1], out.data_ptr(), out._version)

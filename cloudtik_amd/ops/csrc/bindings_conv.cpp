@@ -28,7 +28,7 @@ int ct_splitk_reduce_wide(const float*, int, long, void*, int, float*, hipStream
 // geo = {Hr, Wr, sy, sx, Ho, Wo, oys, oxs, oy0, ox0, ldy, M}; taps = {dy0, dx0, dy1, dx1, ...}.
 // part (optional, fp32 [tiles, 2, Co]) receives per-tile BatchNorm (mean, M2) of Y.
 bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> geo, std::vector<int64_t> taps,
-                bool accumulate, c10::optional<at::Tensor> part, int64_t cfg) {
+                int64_t accumulate, c10::optional<at::Tensor> part, int64_t cfg) {
   TORCH_CHECK(X.is_cuda() && W.is_cuda() && Y.is_cuda(), "conv_igemm: GPU tensors");
   TORCH_CHECK(X.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 && Y.scalar_type() == at::kBFloat16,
               "conv_igemm: bf16 tensors");
@@ -57,7 +57,7 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
   }
   const int rc = ct_conv_igemm(X.data_ptr(), Hi, Wi, Ci, W.data_ptr(), Y.data_ptr(), (int)geo[0], (int)geo[1],
                                (int)geo[2], (int)geo[3], (int)geo[4], (int)geo[5], (int)geo[6], (int)geo[7],
-                               (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), accumulate ? 1 : 0, pp,
+                               (int)geo[8], (int)geo[9], (int)geo[10], Co, (int)M, T, tp.data(), (int)accumulate, pp,
                                (int)cfg, at::hip::getCurrentHIPStream().stream());
   return rc == 0;
 }

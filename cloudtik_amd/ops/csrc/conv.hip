@@ -50,7 +50,8 @@ struct ConvArgs {
   int sy, sx;           // input pixel = (y * sy + dy_t, x * sx + dx_t)
   int Ho, Wo, oys, oxs, oy0, ox0, ldy;   // output pixel = (y * oys + oy0, x * oxs + ox0), row stride ldy
   int Co, M, T;
-  int accumulate;
+  int accumulate;        // 1: Y += result; 2: the 1x1 stride-2 data gradient -- also write the zeros
+                         //   of the three odd-parity pixels of each written one (no zero-fill pass)
   unsigned long long tdy, tdx;           // 16 taps x 4 bits, biased by 8
   int cpt;              // K-steps (of 64 weight columns) per tap: Ci / 64, or 1 in pixel-chunk mode
   int pixchunk;         // stem mode: Ci = 8, the 8 chunks of a K-step are 8 consecutive pixels
@@ -212,7 +213,7 @@ __device__ __forceinline__ void cv_out_prefetch(const ConvArgs& a, CvOut<BM / RP
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
     if (!o.ok[k]) continue;
-    if (a.accumulate) o.old[k] = *(const u16x8*)(a.Y + o.yo[k]);
+    if (a.accumulate == 1) o.old[k] = *(const u16x8*)(a.Y + o.yo[k]);
     if constexpr (EPI == 2) {
       o.xv[k] = *(const u16x8*)(a.bnx + o.yo[k]);
       if (a.bnm) o.mb[k] = a.bnm[o.yo[k] >> 3];
@@ -232,7 +233,7 @@ __device__ __forceinline__ void cv_out_store(const ConvArgs& a, CvOut<BM / RPP>&
   for (int k = 0; k < NR; ++k) {
     if (!o.ok[k]) continue;
     u16x8 v = *(const u16x8*)chunk(tid / CPR + k * RPP);
-    if (a.accumulate) {
+    if (a.accumulate == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(o.old[k][e]));
     }
@@ -249,6 +250,12 @@ __device__ __forceinline__ void cv_out_store(const ConvArgs& a, CvOut<BM / RPP>&
       }
     }
     *(u16x8*)(a.Y + o.yo[k]) = v;
+    if (a.accumulate == 2) {
+      const long ld = a.ldy, ldr = (long)a.Wo * a.ldy;
+      *(u16x8*)(a.Y + o.yo[k] + ld) = u16x8(0);
+      *(u16x8*)(a.Y + o.yo[k] + ldr) = u16x8(0);
+      *(u16x8*)(a.Y + o.yo[k] + ldr + ld) = u16x8(0);
+    }
   }
 }
 
@@ -984,6 +991,10 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || M >= (1 << 24) || T <= 0 || T > CV_MAXT)
     return 1;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 7) || ldy % 4) return 3;
+  // zero-filling mode: exactly the (even, even) phase of a stride-2 output grid, 16-B rows
+  if (accumulate == 2 && (Ho != 2 * Hr || Wo != 2 * Wr || oys != 2 || oxs != 2 || oy0 || ox0 || bn ||
+                          ((uintptr_t)Y & 15) || ldy % 8))
+    return 9;
   const int pixchunk = Ci == 8;            // the stem: NHWC8 input, 8 pixels per K-step
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
              Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk,
