@@ -29,6 +29,7 @@
 // (applications/ai/quickstart/models/image_recognition/pytorch/common/main.py:276-296).
 #include "common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace ct {
 
@@ -902,6 +903,8 @@ using namespace ct;
 //   8: 128x64  4w NS2 x3   9: 64x128  4w NS2 x3
 // streamed persistent (conv_stream_kernel; workgroups per CU, ring slots):
 //  10: 128x128 4w NS4 x1  11: 128x128 4w NS2 x2  12: 128x64 4w NS3 x2  13: 64x128 4w NS3 x2
+// 8 waves (2 x 4, 64 x 32 per wave: twice the waves per CU to hide LDS / memory latency):
+//  14: 128x128 8w NS2 x2 (one tile per workgroup)   15: the same, streamed
 // -1 = pick by shape: short reductions (<= 4 K-steps of 64) want two workgroups per CU so one
 // tile's epilogue overlaps another's loads; long ones want the deeper ring.
 extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
@@ -912,8 +915,18 @@ extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
   // large-M layers (every ResNet-50 launch with M >= 200704 output rows and Co % 128 == 0:
   // l2.c1a fwd 145 -> 128 us, dgrad 197 -> 169; l2.c2 dgrad 96 -> 85) and loses on the
   // 50176-row layer-3/4 launches (profiles/r4/conv_stream_probe.md)
+  // r4, later: the 8-wave 128 x 128 tiles (cfg 14 one-tile, 15 streamed: twice the waves per CU
+  // to hide LDS and memory latency) beat the 4-wave ones on every Co % 128 == 0 shape: one-tile
+  // below 400000 rows (l3.c2 fwd 77 -> 73 us, l4.c2s2 dgrad 127 -> 116), streamed above
+  // (l1.c3 fwd 115 -> 112; profiles/r4/conv_cfg_8wave.md).  CLOUDTIK_AMD_CONV_RULE=1: the rule
+  // before that.
+  static const int rule = [] {
+    const char* e = std::getenv("CLOUDTIK_AMD_CONV_RULE");
+    return e ? std::atoi(e) : 2;
+  }();
   (void)KT;
   if (cfg < 0) {
+    if (rule >= 2 && Co % 128 == 0) return M >= 400000 ? 15 : 14;
     if (Co % 128 == 0 && M >= 150000) return 11;
     cfg = Co % 128 ? 8 : (Co == 128 ? 9 : 5);
   }
@@ -926,7 +939,7 @@ extern "C" int ct_conv_igemm_part_rows(int cfg) {
 }
 
 extern "C" int ct_conv_igemm_tile_m(int cfg) {
-  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : ((cfg == 9 || cfg == 13) ? 64 : 128);
+  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : ((cfg == 9 || cfg == 13) ? 64 : 128);   // 14, 15: 128
 }
 
 static int g_cv_stream_cus = 0;      // test / probe override of the streamed kernels' CU count
@@ -1017,7 +1030,9 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   }
   const int epi = bn ? 2 : (part ? 1 : 0);
   cfg = ct_conv_igemm_rows(cfg, Co, M, T * a.cpt);
-  if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9 || cfg == 10 || cfg == 11 || cfg == 13) && Co % 128) return 2;
+  if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9 || cfg == 10 || cfg == 11 || cfg == 13 || cfg == 14 ||
+       cfg == 15) && Co % 128)
+    return 2;
   if (epi == 2) {
     // the default (shape-picked) configurations only: the others are not instantiated with EPI 2
     switch (cfg) {
@@ -1028,6 +1043,8 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
       case 11: return cs_launch<128, 128, 2, 2, 2, 2, true>(a, epi, cv_cu_count(), stream);
       case 12: return cs_launch<128, 64, 2, 2, 3, 2, true>(a, epi, cv_cu_count(), stream);
       case 13: return cs_launch<64, 128, 1, 4, 3, 2, true>(a, epi, cv_cu_count(), stream);
+      case 14: return cv_launch<128, 128, 2, 4, 2, 2, true>(a, epi, stream);
+      case 15: return cs_launch<128, 128, 2, 4, 2, 2, true>(a, epi, cv_cu_count(), stream);
       default: return 6;
     }
   }
@@ -1046,6 +1063,8 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
     case 11: return cs_launch<128, 128, 2, 2, 2, 2>(a, epi, cv_cu_count(), stream);
     case 12: return cs_launch<128, 64, 2, 2, 3, 2>(a, epi, cv_cu_count(), stream);
     case 13: return cs_launch<64, 128, 1, 4, 3, 2>(a, epi, cv_cu_count(), stream);
+    case 14: return cv_launch<128, 128, 2, 4, 2, 2>(a, epi, stream);
+    case 15: return cs_launch<128, 128, 2, 4, 2, 2>(a, epi, cv_cu_count(), stream);
     default: return 6;
   }
 }

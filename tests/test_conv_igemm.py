@@ -282,11 +282,12 @@ def test_dgrad_weight_cache_matches_direct_transposes():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [10, 11, 12, 13])
+@pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("ci,co,H,k,s,cus", [(64, 256, 20, 3, 1, 7), (64, 128, 15, 3, 2, 3), (256, 128, 12, 1, 1, 5),
                                              (128, 256, 9, 1, 2, 0)])
 def test_streamed_conv_kernels_match_fp32_reference(cuda, monkeypatch, cfg, ci, co, H, k, s, cus):
-    """conv.hip conv_stream_kernel (cfg 10-13): forward + BatchNorm tile statistics, data gradient
+    """conv.hip conv_stream_kernel (cfg 10-13, 15) and the 8-wave one-tile kernel (cfg 14): forward
+    + BatchNorm tile statistics, data gradient
     (stride-2 phase plans included) plain and accumulated, with few persistent workgroups
     (``cus`` x per-CU count) so every workgroup streams several tiles and the DMA ring runs
     across tile boundaries (tiles mixing in-image rows and the zero-padded tail of M)."""
@@ -308,7 +309,7 @@ def test_streamed_conv_kernels_match_fp32_reference(cuda, monkeypatch, cfg, ci, 
         yb = y.float()
         torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(var, yb.var((0, 2, 3), unbiased=False), rtol=1e-3, atol=1e-6)
-        if ci % 128 == 0 or cfg == 12:            # dgrad output channels = ci
+        if ci % 128 == 0 or cfg == 12:            # dgrad output channels = ci (cfg 12: any multiple of 64)
             dx = CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad))
             assert _rel(dx, xr.grad) < 1e-2
             other = _nhwc(torch.randn(x.shape, device=cuda).to(torch.bfloat16))
