@@ -905,6 +905,8 @@ using namespace ct;
 //  10: 128x128 4w NS4 x1  11: 128x128 4w NS2 x2  12: 128x64 4w NS3 x2  13: 64x128 4w NS3 x2
 // 8 waves (2 x 4, 64 x 32 per wave: twice the waves per CU to hide LDS / memory latency):
 //  14: 128x128 8w NS2 x2 (one tile per workgroup)   15: the same, streamed
+//  16: 128x64 8w (4 x 2, 32 x 32 per wave) NS2 x2    17: 128x64 8w NS3 x2, streamed (no EPI 2:
+//      its reduction scratch does not fit a ring slot)
 // -1 = pick by shape: short reductions (<= 4 K-steps of 64) want two workgroups per CU so one
 // tile's epilogue overlaps another's loads; long ones want the deeper ring.
 extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
@@ -935,7 +937,7 @@ extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
 
 // rows per BatchNorm-statistics partial (EPI 1 writes one per wave row block: BM / WGM)
 extern "C" int ct_conv_igemm_part_rows(int cfg) {
-  return cfg == 6 ? 32 : 64;
+  return (cfg == 6 || cfg == 16 || cfg == 17) ? 32 : 64;
 }
 
 extern "C" int ct_conv_igemm_tile_m(int cfg) {
@@ -1045,6 +1047,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
       case 13: return cs_launch<64, 128, 1, 4, 3, 2, true>(a, epi, cv_cu_count(), stream);
       case 14: return cv_launch<128, 128, 2, 4, 2, 2, true>(a, epi, stream);
       case 15: return cs_launch<128, 128, 2, 4, 2, 2, true>(a, epi, cv_cu_count(), stream);
+      case 16: return cv_launch<128, 64, 4, 2, 2, 2, true>(a, epi, stream);
       default: return 6;
     }
   }
@@ -1065,6 +1068,8 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
     case 13: return cs_launch<64, 128, 1, 4, 3, 2>(a, epi, cv_cu_count(), stream);
     case 14: return cv_launch<128, 128, 2, 4, 2, 2>(a, epi, stream);
     case 15: return cs_launch<128, 128, 2, 4, 2, 2>(a, epi, cv_cu_count(), stream);
+    case 16: return cv_launch<128, 64, 4, 2, 2, 2>(a, epi, stream);
+    case 17: return cs_launch<128, 64, 4, 2, 3, 2>(a, epi, cv_cu_count(), stream);
     default: return 6;
   }
 }
@@ -1119,7 +1124,8 @@ __global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restric
 
 // wgrad tile configurations: 0 = 64x64 (4 waves 2x2), 1 = 64x128 (2x2), 2 = 128x128 (2x2),
 // 3 = 128x256 (8 waves 2x4); 4 / 5 / 6 = cfg 0 / 1 / 2 with 64-pixel stages (two MFMA k-steps per
-// barrier); -1 = the largest that divides (Co, T*Ci)
+// barrier); 7 / 8 = cfg 4 with a 2 / 3-slot ring (more workgroups per CU); -1 = the largest that
+// divides (Co, T*Ci)
 extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   if (cfg >= 0) return cfg;
   // per-shape probe over every ResNet-50 conv (profiles/r3/conv_wgrad_cfg.md): the 8-wave
@@ -1130,7 +1136,7 @@ extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   // the 64-wide tiles serve the layer-1 shapes (802816-pixel reductions): 64-pixel stages win
   // there (l1.c2 301 -> 289 us, l1.c3 156 -> 142, l1.c1 128 -> 118; profiles/r4/conv_stream_probe.md)
   if (NN % 128 == 0) return 5;
-  return 4;
+  return 8;                        // 64 x 64, 64-pixel stages, 3-slot ring (l1.c3 145 -> 137 us)
 }
 
 // workspace: n fp32 + ceil(n / 1024) tickets, zeroed here
@@ -1163,7 +1169,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
-  const int tile = cfg >= 4 ? cfg - 4 : cfg;
+  const int tile = cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg);
   if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
   if (cfg >= 4 && rows_per_split % 64) return 2;
   switch (cfg) {
@@ -1174,6 +1180,8 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     case 4: return wg_launch<64, 64, 2, 2, 4, 64>(a, splits, stream);
     case 5: return wg_launch<64, 128, 2, 2, 4, 64>(a, splits, stream);
     case 6: return wg_launch<128, 128, 2, 2, 3, 64>(a, splits, stream);
+    case 7: return wg_launch<64, 64, 2, 2, 2, 64>(a, splits, stream);
+    case 8: return wg_launch<64, 64, 2, 2, 3, 64>(a, splits, stream);
     default: return 6;
   }
 }

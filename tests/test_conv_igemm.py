@@ -282,7 +282,7 @@ def test_dgrad_weight_cache_matches_direct_transposes():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("ci,co,H,k,s,cus", [(64, 256, 20, 3, 1, 7), (64, 128, 15, 3, 2, 3), (256, 128, 12, 1, 1, 5),
                                              (128, 256, 9, 1, 2, 0)])
 def test_streamed_conv_kernels_match_fp32_reference(cuda, monkeypatch, cfg, ci, co, H, k, s, cus):
@@ -309,7 +309,7 @@ def test_streamed_conv_kernels_match_fp32_reference(cuda, monkeypatch, cfg, ci, 
         yb = y.float()
         torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(var, yb.var((0, 2, 3), unbiased=False), rtol=1e-3, atol=1e-6)
-        if ci % 128 == 0 or cfg == 12:            # dgrad output channels = ci (cfg 12: any multiple of 64)
+        if ci % 128 == 0 or cfg in (12, 16, 17):  # dgrad output channels = ci (64-wide tiles: any multiple of 64)
             dx = CV.conv_dgrad(dy, w, x.shape, (s, s), (pad, pad))
             assert _rel(dx, xr.grad) < 1e-2
             other = _nhwc(torch.randn(x.shape, device=cuda).to(torch.bfloat16))
@@ -354,7 +354,7 @@ def test_streamed_conv_bn_backward_epilogue(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wcfg", [4, 5, 6])
+@pytest.mark.parametrize("wcfg", [4, 5, 6, 7, 8])
 @pytest.mark.parametrize("ci,co,H,k,s", [(128, 128, 15, 3, 2), (128, 128, 12, 1, 1), (64, 256, 10, 3, 1)])
 def test_wgrad_64_pixel_stages_match_fp32_reference(cuda, monkeypatch, wcfg, ci, co, H, k, s):
     """conv_wgrad_kernel with 64-pixel stages (two MFMA k-steps per barrier; wgrad cfg 4-6),
