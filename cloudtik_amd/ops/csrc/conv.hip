@@ -1124,15 +1124,18 @@ __global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restric
 
 // wgrad tile configurations: 0 = 64x64 (4 waves 2x2), 1 = 64x128 (2x2), 2 = 128x128 (2x2),
 // 3 = 128x256 (8 waves 2x4); 4 / 5 / 6 = cfg 0 / 1 / 2 with 64-pixel stages (two MFMA k-steps per
-// barrier); 7 / 8 = cfg 4 with a 2 / 3-slot ring (more workgroups per CU); -1 = the largest that
-// divides (Co, T*Ci)
+// barrier); 7 / 8 = cfg 4 with a 2 / 3-slot ring (more workgroups per CU); 9 / 10 = 128x128 on 8
+// waves (2x4), 32-pixel stages x 4 slots / 64-pixel x 2; -1 = the largest that divides (Co, T*Ci)
 extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   if (cfg >= 0) return cfg;
   // per-shape probe over every ResNet-50 conv (profiles/r3/conv_wgrad_cfg.md): the 8-wave
   // 128 x 256 tile wins wherever it divides (l4.c2 357 -> 146 us, l3.c2 183 -> 111 us), then
   // 128 x 128, then 64 x 128 for 64-channel outputs (l1.c1 163 -> 128 us)
-  if (Co % 128 == 0 && NN % 256 == 0) return 3;
-  if (Co % 128 == 0 && NN % 128 == 0) return 2;
+  // r4: the 8-wave 128 x 128 tile (cfg 9) beats the 4-wave one everywhere and the 8-wave
+  // 128 x 256 one for 128-channel outputs (l2.c2 185 -> 130 us, l2.c3 90 -> 69;
+  // profiles/r4/conv_cfg_8wave.md)
+  if (Co % 128 == 0 && NN % 256 == 0 && Co >= 256) return 3;
+  if (Co % 128 == 0 && NN % 128 == 0) return 9;
   // the 64-wide tiles serve the layer-1 shapes (802816-pixel reductions): 64-pixel stages win
   // there (l1.c2 301 -> 289 us, l1.c3 156 -> 142, l1.c1 128 -> 118; profiles/r4/conv_stream_probe.md)
   if (NN % 128 == 0) return 5;
@@ -1169,9 +1172,9 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
-  const int tile = cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg);
+  const int tile = cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg));
   if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
-  if (cfg >= 4 && rows_per_split % 64) return 2;
+  if (cfg >= 4 && cfg != 9 && rows_per_split % 64) return 2;
   switch (cfg) {
     case 0: return wg_launch<64, 64, 2, 2, 4>(a, splits, stream);
     case 1: return wg_launch<64, 128, 2, 2, 4>(a, splits, stream);
@@ -1182,6 +1185,8 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     case 6: return wg_launch<128, 128, 2, 2, 3, 64>(a, splits, stream);
     case 7: return wg_launch<64, 64, 2, 2, 2, 64>(a, splits, stream);
     case 8: return wg_launch<64, 64, 2, 2, 3, 64>(a, splits, stream);
+    case 9: return wg_launch<128, 128, 2, 4, 4>(a, splits, stream);
+    case 10: return wg_launch<128, 128, 2, 4, 2, 64>(a, splits, stream);
     default: return 6;
   }
 }
