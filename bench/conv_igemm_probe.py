@@ -97,7 +97,7 @@ def main():
         mi_w = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [pad, pad], [1, 1], False,
                                                                   [0, 0], 1, [False, True, False]))
         wper = []
-        for c in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
+        for c in (-1, 2, 3, 9, 11):
             CV._WG_CFG = c
             try:
                 wper.append((timeit(lambda: CV.conv_wgrad(dy, x, w.shape, (s, s), (pad, pad))), c))

@@ -305,7 +305,7 @@ _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
 # 1x1 stride-1 weight gradients with 256-multiple channel counts on the TN GEMM kernel
 _TN_WGRAD_1X1 = os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "1") == "1"
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128),
-             7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128)}
+             7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256)}
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
 WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
 

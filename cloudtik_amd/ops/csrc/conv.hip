@@ -907,6 +907,7 @@ using namespace ct;
 //  14: 128x128 8w NS2 x2 (one tile per workgroup)   15: the same, streamed
 //  16: 128x64 8w (4 x 2, 32 x 32 per wave) NS2 x2    17: 128x64 8w NS3 x2, streamed (no EPI 2:
 //      its reduction scratch does not fit a ring slot)
+//  18: 256x128 16w (4 x 4, 64 x 32 per wave) NS2 x1
 // -1 = pick by shape: short reductions (<= 4 K-steps of 64) want two workgroups per CU so one
 // tile's epilogue overlaps another's loads; long ones want the deeper ring.
 extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
@@ -941,7 +942,7 @@ extern "C" int ct_conv_igemm_part_rows(int cfg) {
 }
 
 extern "C" int ct_conv_igemm_tile_m(int cfg) {
-  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6) ? 256 : ((cfg == 9 || cfg == 13) ? 64 : 128);   // 14, 15: 128
+  return (cfg == 0 || cfg == 1 || cfg == 4 || cfg == 6 || cfg == 18) ? 256 : ((cfg == 9 || cfg == 13) ? 64 : 128);
 }
 
 static int g_cv_stream_cus = 0;      // test / probe override of the streamed kernels' CU count
@@ -1033,7 +1034,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   const int epi = bn ? 2 : (part ? 1 : 0);
   cfg = ct_conv_igemm_rows(cfg, Co, M, T * a.cpt);
   if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9 || cfg == 10 || cfg == 11 || cfg == 13 || cfg == 14 ||
-       cfg == 15) && Co % 128)
+       cfg == 15 || cfg == 18) && Co % 128)
     return 2;
   if (epi == 2) {
     // the default (shape-picked) configurations only: the others are not instantiated with EPI 2
@@ -1048,6 +1049,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
       case 14: return cv_launch<128, 128, 2, 4, 2, 2, true>(a, epi, stream);
       case 15: return cs_launch<128, 128, 2, 4, 2, 2, true>(a, epi, cv_cu_count(), stream);
       case 16: return cv_launch<128, 64, 4, 2, 2, 2, true>(a, epi, stream);
+      case 18: return cv_launch<256, 128, 4, 4, 2, 1, true>(a, epi, stream);
       default: return 6;
     }
   }
@@ -1070,6 +1072,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
     case 15: return cs_launch<128, 128, 2, 4, 2, 2>(a, epi, cv_cu_count(), stream);
     case 16: return cv_launch<128, 64, 4, 2, 2, 2>(a, epi, stream);
     case 17: return cs_launch<128, 64, 4, 2, 3, 2>(a, epi, cv_cu_count(), stream);
+    case 18: return cv_launch<256, 128, 4, 4, 2, 1>(a, epi, stream);
     default: return 6;
   }
 }
@@ -1125,7 +1128,8 @@ __global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restric
 // wgrad tile configurations: 0 = 64x64 (4 waves 2x2), 1 = 64x128 (2x2), 2 = 128x128 (2x2),
 // 3 = 128x256 (8 waves 2x4); 4 / 5 / 6 = cfg 0 / 1 / 2 with 64-pixel stages (two MFMA k-steps per
 // barrier); 7 / 8 = cfg 4 with a 2 / 3-slot ring (more workgroups per CU); 9 / 10 = 128x128 on 8
-// waves (2x4), 32-pixel stages x 4 slots / 64-pixel x 2; -1 = the largest that divides (Co, T*Ci)
+// waves (2x4), 32-pixel stages x 4 slots / 64-pixel x 2; 11 = 128x256 on 16 waves (4x4), 64-pixel
+// stages x 2; -1 = the largest that divides (Co, T*Ci)
 extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   if (cfg >= 0) return cfg;
   // per-shape probe over every ResNet-50 conv (profiles/r3/conv_wgrad_cfg.md): the 8-wave
@@ -1172,7 +1176,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
-  const int tile = cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg));
+  const int tile = cfg == 11 ? 3 : (cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg)));
   if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
   if (cfg >= 4 && cfg != 9 && rows_per_split % 64) return 2;
   switch (cfg) {
@@ -1187,6 +1191,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     case 8: return wg_launch<64, 64, 2, 2, 3, 64>(a, splits, stream);
     case 9: return wg_launch<128, 128, 2, 4, 4>(a, splits, stream);
     case 10: return wg_launch<128, 128, 2, 4, 2, 64>(a, splits, stream);
+    case 11: return wg_launch<128, 256, 4, 4, 2, 64>(a, splits, stream);
     default: return 6;
   }
 }

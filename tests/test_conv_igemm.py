@@ -282,7 +282,7 @@ def test_dgrad_weight_cache_matches_direct_transposes():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("cfg", [10, 11, 12, 13, 14, 15, 16, 17, 18])
 @pytest.mark.parametrize("ci,co,H,k,s,cus", [(64, 256, 20, 3, 1, 7), (64, 128, 15, 3, 2, 3), (256, 128, 12, 1, 1, 5),
                                              (128, 256, 9, 1, 2, 0)])
 def test_streamed_conv_kernels_match_fp32_reference(cuda, monkeypatch, cfg, ci, co, H, k, s, cus):
@@ -354,8 +354,9 @@ def test_streamed_conv_bn_backward_epilogue(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wcfg", [4, 5, 6, 7, 8, 9, 10])
-@pytest.mark.parametrize("ci,co,H,k,s", [(128, 128, 15, 3, 2), (128, 128, 12, 1, 1), (64, 256, 10, 3, 1)])
+@pytest.mark.parametrize("wcfg", [4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("ci,co,H,k,s", [(128, 128, 15, 3, 2), (128, 128, 12, 1, 1), (64, 256, 10, 3, 1),
+                                         (128, 256, 9, 3, 1)])
 def test_wgrad_64_pixel_stages_match_fp32_reference(cuda, monkeypatch, wcfg, ci, co, H, k, s):
     """conv_wgrad_kernel with 64-pixel stages (two MFMA k-steps per barrier; wgrad cfg 4-6),
     including splits that end inside a stage."""
