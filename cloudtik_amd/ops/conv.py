@@ -26,6 +26,7 @@ main.py:276-296); tests compare against ``F.conv2d`` in fp32.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import List, Optional, Tuple
 
@@ -268,37 +269,81 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
     wt = w.permute(1, 2, 3, 0)                      # [Ci, R, S, Co]
     sh, sw = stride
     tile0 = 0
-    for (a, b), (Hr, Wr), taps, rs in phases:
-        if not rs:
-            continue
-        wm = _DGRAD_W.get(w, rs) if _DGRAD_W_CACHE else None
-        if wm is None:
-            if len(rs) == R * S:
-                wm = wt.reshape(ci, -1).contiguous()
-            else:
-                wm = torch.stack([wt[:, r, s, :] for r, s in rs], 1).reshape(ci, -1).contiguous()
-        geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
-        if bn_plan is not None:
-            part, rows = bn_plan
-            msrc = bn.mask if bn.mode == 3 else (bn_y if bn.mode == 1 else None)
-            if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, msrc,
-                               bn.stat, part, tile0, rows):
-                bm = C.conv_igemm_tile_m(_CFG, ci, geo[11], len(taps) // 2 * (co // 64))
-                tile0 += (geo[11] + bm - 1) // bm
-                continue
-            if tile0:
-                raise RuntimeError("conv_igemm_bn rejected a later phase of a supported data gradient")
-            bn_plan = None                          # configuration without the fused epilogue
-        if not C.conv_igemm(dy, wm, out, geo, taps, 2 if zfill else int(accumulate), None, _CFG):
-            if zfill:                               # shape the zero-filling mode refuses
-                out.zero_()
-                zfill = False
-                if C.conv_igemm(dy, wm, out, geo, taps, 0, None, _CFG):
-                    continue
-            raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)} w{tuple(w.shape)}")
+    # the output phases of a strided data gradient write disjoint pixels (and disjoint rows of
+    # the BatchNorm partials): launched on parallel streams, the short launches overlap instead
+    # of each draining the GPU in turn
+    cur = torch.cuda.current_stream() if dy.is_cuda else None
+    streams = _phase_streams(dy.device, len(live) - 1) if (cur is not None and _PHASE_STREAMS and len(live) > 1
+                                                           and not zfill) else []
+    # every phase's weight matrix first, on this stream (the batched gather of the dgrad weight
+    # cache may launch here), then the side streams join it
+    mats = [_dgrad_weights(w, wt, rs, R, S, ci) for _, _, _, rs in live]
+    for st in streams:
+        st.wait_stream(cur)
+    for i, ((a, b), (Hr, Wr), taps, rs) in enumerate(live):
+        st = streams[i - 1] if i > 0 and streams else None
+        with (torch.cuda.stream(st) if st is not None else contextlib.nullcontext()):
+            tile0 = _dgrad_phase(C, dy, mats[i], ci, co, N, H, W, Hr, Wr, a, b, sh, sw, taps, out, accumulate,
+                                 bn, bn_y, bn_plan, tile0, zfill)
+        if tile0 is None:                           # the fused epilogue was declined: plain from here on
+            bn_plan = None
+            tile0 = 0
+    if streams:
+        for st in streams:
+            cur.wait_stream(st)
+        for t in (dy, out) + ((bn_plan[0],) if bn_plan is not None else ()):
+            for st in streams:
+                t.record_stream(st)
     if bn_plan is not None:
         bn.pending = (bn_plan[0], tile0, bn_plan[1], out.data_ptr(), out._version)
     return out
+
+
+_PHASE_STREAMS = os.environ.get("CLOUDTIK_AMD_CONV_PHASE_STREAMS", "0") == "1"
+_PHASE_STREAM_POOL = {}
+
+
+def _phase_streams(device, n):
+    pool = _PHASE_STREAM_POOL.setdefault(device, [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Stream(device=device))
+    return pool[:n]
+
+
+def _dgrad_weights(w, wt, rs, R, S, ci):
+    """[Ci, taps * Co] weight matrix of one data-gradient phase (taps rs, flipped)."""
+    wm = _DGRAD_W.get(w, rs) if _DGRAD_W_CACHE else None
+    if wm is None:
+        if len(rs) == R * S:
+            wm = wt.reshape(ci, -1).contiguous()
+        else:
+            wm = torch.stack([wt[:, r, s, :] for r, s in rs], 1).reshape(ci, -1).contiguous()
+    return wm
+
+
+def _dgrad_phase(C, dy, wm, ci, co, N, H, W, Hr, Wr, a, b, sh, sw, taps, out, accumulate, bn, bn_y, bn_plan, tile0,
+                 zfill):
+    """One output phase of conv_dgrad; returns the next BatchNorm-partial row, or None when the
+    fused BN-backward epilogue was declined on the first phase."""
+    geo = [Hr, Wr, 1, 1, H, W, sh, sw, a, b, ci, N * Hr * Wr]
+    if bn_plan is not None:
+        part, rows = bn_plan
+        msrc = bn.mask if bn.mode == 3 else (bn_y if bn.mode == 1 else None)
+        if C.conv_igemm_bn(dy, wm, out, geo, taps, accumulate, _CFG, bn.x, msrc, bn.stat, part, tile0, rows):
+            bm = C.conv_igemm_tile_m(_CFG, ci, geo[11], len(taps) // 2 * (co // 64))
+            return tile0 + (geo[11] + bm - 1) // bm
+        if tile0:
+            raise RuntimeError("conv_igemm_bn rejected a later phase of a supported data gradient")
+        if not C.conv_igemm(dy, wm, out, geo, taps, int(accumulate), None, _CFG):
+            raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)}")
+        return None                                 # configuration without the fused epilogue
+    if not C.conv_igemm(dy, wm, out, geo, taps, 2 if zfill else int(accumulate), None, _CFG):
+        if zfill:                                   # shape the zero-filling mode refuses
+            out.zero_()
+            if C.conv_igemm(dy, wm, out, geo, taps, 0, None, _CFG):
+                return tile0
+        raise RuntimeError(f"conv_igemm (dgrad) rejected dy{tuple(dy.shape)}")
+    return tile0
 
 
 _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
