@@ -64,6 +64,39 @@ __device__ __forceinline__ bf16x8_t gload_frag(const bf16_t* p, bool valid) {
 __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+// Store a 64-wide row held as two 32x32 MFMA accumulators in the "row on the lane" layout:
+// lane (r, hh) holds columns d = 8 g + 4 hh .. + 3 of row r (A0: d < 32, A1: d + 32).  A
+// v_permlane32_swap of the (g, g + 1) pair between the lane halves leaves each lane 8
+// consecutive columns (hh = 0: block g, hh = 1: block g + 1), so the row goes out as 16-byte
+// stores, 4 per lane instead of 8 of 8 bytes (the store tail of these short kernels is
+// issue-bound).  Every lane must take part (the swap); `valid` only gates the stores.
+__device__ __forceinline__ void store_row64(bf16_t* p, const f32x16& A0, const f32x16& A1, float mul, int hh,
+                                            bool valid) {
+  u16x8 ov[4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+      const f32x16& A = t ? A1 : A0;
+      const int g0 = 2 * gp, g1 = g0 + 1;
+      const u16x4 x = {f2bf(A[4 * g0] * mul), f2bf(A[4 * g0 + 1] * mul), f2bf(A[4 * g0 + 2] * mul),
+                       f2bf(A[4 * g0 + 3] * mul)};
+      const u16x4 y = {f2bf(A[4 * g1] * mul), f2bf(A[4 * g1 + 1] * mul), f2bf(A[4 * g1 + 2] * mul),
+                       f2bf(A[4 * g1 + 3] * mul)};
+      const uint2 xv = __builtin_bit_cast(uint2, x), yv = __builtin_bit_cast(uint2, y);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(xv.x, yv.x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(xv.y, yv.y, false, false);
+      // s*[0] = the new x (hh = 1 lanes: the partner's y), s*[1] = the new y
+      const uint4 v = {s0[0], s1[0], s0[1], s1[1]};
+      ov[2 * t + gp] = __builtin_bit_cast(u16x8, v);
+    }
+  if (!valid) return;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) *reinterpret_cast<u16x8*>(p + 32 * t + 8 * (2 * gp + hh)) = ov[2 * t + gp];
+}
+
 __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
   return x;
@@ -146,8 +179,36 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   }                                                                                  \
   if (tid < 64) kbias_lds[(buf_) * 64 + tid] = stB;
 
+  // Sk <= 128 (BERT phase 1): both K/V tiles are loaded up front (a second staging set; the
+  // accumulators are not live yet, so it costs no occupancy) and sit in the two LDS buffers
+  // before the first MFMA -- one memory latency per workgroup instead of two in series, and
+  // no barrier inside the loop
+  const bool resident = nt == 2;
   FWD_GLOAD(0);
-  FWD_SWRITE(0);
+  if (resident) {
+    u16x8 k1[2], v1[2];
+    float b1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = 64 + srow + 32 * i;
+      const bool ok = key < a.Sk;
+      k1[i] = ok ? *reinterpret_cast<const u16x8*>(kp + (key * (int)a.k_ss + sch * 8)) : u16x8(0);
+      v1[i] = ok ? *reinterpret_cast<const u16x8*>(vp + (key * (int)a.v_ss + sch * 8)) : u16x8(0);
+    }
+    if (tid < 64) {
+      const int kk = 64 + tid;
+      b1 = kk < a.Sk ? (kbp ? kbp[kk] * LOG2E : 0.f) : -INFINITY;
+    }
+    FWD_SWRITE(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<u16x8*>(smem + 16384 + swz(srow + 32 * i, sch)) = k1[i];
+      *reinterpret_cast<u16x8*>(smem + 16384 + 8192 + swz(srow + 32 * i, sch)) = v1[i];
+    }
+    if (tid < 64) kbias_lds[64 + tid] = b1;
+  } else {
+    FWD_SWRITE(0);
+  }
   __syncthreads();
 
   const int trow = (lane >> 2) & 3;
@@ -155,7 +216,7 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
 
   for (int kt = 0; kt < nt; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nt) { FWD_GLOAD(kt + 1); }
+    if (!resident && kt + 1 < nt) { FWD_GLOAD(kt + 1); }
     const char* Kb = smem + buf * 16384;
     const char* Vb = Kb + 8192;
     f32x16 S0, S1;
@@ -248,23 +309,18 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
         O0 = mfma32(a0, pf[t][s2], O0);
         O1 = mfma32(a1, pf[t][s2], O1);
       }
-    if (kt + 1 < nt) { FWD_SWRITE(buf ^ 1); }
-    __syncthreads();
+    if (!resident) {
+      if (kt + 1 < nt) { FWD_SWRITE(buf ^ 1); }
+      __syncthreads();
+    }
   }
 #undef FWD_GLOAD
 #undef FWD_SWRITE
   l += __shfl_xor(l, 32, 64);
   const float inv = l > 0.f ? (DROP ? a.inv_keep : 1.f) / l : 0.f;
+  bf16_t* op = a.o + b * a.o_sb + h * a.o_sh + (long)(qvalid ? qi : 0) * a.o_ss;
+  store_row64(op, O0, O1, inv, hh, qvalid);
   if (qvalid) {
-    bf16_t* op = a.o + b * a.o_sb + h * a.o_sh + (long)qi * a.o_ss;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * hh;
-      u16x4 v0 = {f2bf(O0[4 * g] * inv), f2bf(O0[4 * g + 1] * inv), f2bf(O0[4 * g + 2] * inv), f2bf(O0[4 * g + 3] * inv)};
-      u16x4 v1 = {f2bf(O1[4 * g] * inv), f2bf(O1[4 * g + 1] * inv), f2bf(O1[4 * g + 2] * inv), f2bf(O1[4 * g + 3] * inv)};
-      *reinterpret_cast<u16x4*>(op + d) = v0;
-      *reinterpret_cast<u16x4*>(op + 32 + d) = v1;
-    }
     if (hh == 0 && a.lse) a.lse[(long)bh * a.Sq + qi] = l > 0.f ? m + log2f(l) : INFINITY;
   }
 }
@@ -717,21 +773,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   }
 #undef BWD_PREFETCH
 #undef BWD_STAGE
-  if (kvalid) {
-    bf16_t* dkp = a.dk + b * a.dk_sb + h * a.dk_sh + (long)key_l * a.dk_ss;
-    bf16_t* dvp = a.dv + b * a.dv_sb + h * a.dv_sh + (long)key_l * a.dv_ss;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * hh;
-      u16x4 k0v = {f2bf(dK0[4 * g] * a.scale), f2bf(dK0[4 * g + 1] * a.scale), f2bf(dK0[4 * g + 2] * a.scale), f2bf(dK0[4 * g + 3] * a.scale)};
-      u16x4 k1v = {f2bf(dK1[4 * g] * a.scale), f2bf(dK1[4 * g + 1] * a.scale), f2bf(dK1[4 * g + 2] * a.scale), f2bf(dK1[4 * g + 3] * a.scale)};
-      u16x4 v0v = {f2bf(dV0[4 * g]), f2bf(dV0[4 * g + 1]), f2bf(dV0[4 * g + 2]), f2bf(dV0[4 * g + 3])};
-      u16x4 v1v = {f2bf(dV1[4 * g]), f2bf(dV1[4 * g + 1]), f2bf(dV1[4 * g + 2]), f2bf(dV1[4 * g + 3])};
-      *reinterpret_cast<u16x4*>(dkp + d) = k0v;
-      *reinterpret_cast<u16x4*>(dkp + 32 + d) = k1v;
-      *reinterpret_cast<u16x4*>(dvp + d) = v0v;
-      *reinterpret_cast<u16x4*>(dvp + 32 + d) = v1v;
-    }
+  {
+    const long kl = kvalid ? key_l : 0;
+    store_row64(a.dk + b * a.dk_sb + h * a.dk_sh + kl * a.dk_ss, dK0, dK1, a.scale, hh, kvalid);
+    store_row64(a.dv + b * a.dv_sb + h * a.dv_sh + kl * a.dv_ss, dV0, dV1, 1.f, hh, kvalid);
   }
 }
 
@@ -806,6 +851,8 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
   if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0) return -1;
   if (p_drop > 0.f && (Sk % 2)) return -2;
   if (!fits32(Sq, qs[1]) || !fits32(Sk, ks[1]) || !fits32(Sk, vs[1]) || !fits32(Sq, os[1])) return -5;
+  // 16-byte output stores (attn_fwd_d64_kernel's epilogue)
+  if (((uintptr_t)o & 15) || os[0] % 8 || os[1] % 8 || os[2] % 8) return -7;
   AttnFwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
   a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
@@ -864,6 +911,7 @@ extern "C" int ct_attn_fwd_relbias(const void* q, const long* qs, const void* k,
   if (B <= 0 || H <= 0 || Sq <= 0 || Sk <= 0 || relb_len <= 0) return -1;
   if (relb_len > kRelBiasMax) return -4;
   if (!fits32(Sq, qs[1]) || !fits32(Sk, ks[1]) || !fits32(Sk, vs[1]) || !fits32(Sq, os[1])) return -5;
+  if (((uintptr_t)o & 15) || os[0] % 8 || os[1] % 8 || os[2] % 8) return -7;   // 16-byte output stores
   AttnFwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (bf16_t*)o;
   a.q_sb = qs[0]; a.q_ss = qs[1]; a.q_sh = qs[2];
@@ -895,6 +943,10 @@ extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const l
   if (p_drop > 0.f && (Sk % 2)) return -2;
   if (!fits32(Sq, qs[1]) || !fits32(Sk, ks[1]) || !fits32(Sk, vs[1]) || !fits32(Sq, os[1]) ||
       !fits32(Sq, dos[1]) || !fits32(Sq, dqs[1])) return -5;
+  // 16-byte dK / dV stores (store_row64)
+  if (((uintptr_t)dk & 15) || ((uintptr_t)dv & 15) || dks[0] % 8 || dks[1] % 8 || dks[2] % 8 || dvs[0] % 8 ||
+      dvs[1] % 8 || dvs[2] % 8)
+    return -7;
   const long rows = (long)B * H * Sq;
   AttnBwdArgs a;
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.dO = (const bf16_t*)dO;
