@@ -97,7 +97,7 @@ def main():
         mi_w = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [pad, pad], [1, 1], False,
                                                                   [0, 0], 1, [False, True, False]))
         wper = []
-        for c in (-1, 2, 3, 9, 11):
+        for c in [int(v) for v in os.environ.get("WCFGS", "-1,2,3,9,11").split(",")]:
             CV._WG_CFG = c
             try:
                 wper.append((timeit(lambda: CV.conv_wgrad(dy, x, w.shape, (s, s), (pad, pad))), c))

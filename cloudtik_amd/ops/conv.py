@@ -353,6 +353,9 @@ _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64
              7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256)}
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
 WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
+# the same target for the tiles narrower than 128 x 256 (cfg 3 / 11 keep WGRAD_BLOCKS): at 256
+# workgroups the 64-wide 4-wave tiles run one wave per SIMD (l1.c2 299 us, 187 at 512)
+WGRAD_BLOCKS_SMALL = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS_SMALL", "256"))
 
 
 def wgrad_plan(M: int, co: int, nn: int, cfg: int):
@@ -360,7 +363,8 @@ def wgrad_plan(M: int, co: int, nn: int, cfg: int):
     and at least 256 deep, the fp32 partials capped at PARTIAL_BYTES."""
     bm, bn = _WG_TILES[cfg]
     tiles = (co // bm) * (nn // bn)
-    splits = max(1, min(WGRAD_BLOCKS // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
+    blocks = WGRAD_BLOCKS if cfg in (3, 11) else WGRAD_BLOCKS_SMALL
+    splits = max(1, min(blocks // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
     q = 64 if cfg >= 4 and cfg != 9 else 32        # pixels per stage of the configuration
     rows = ((M + splits - 1) // splits + q - 1) // q * q
     return (M + rows - 1) // rows, rows

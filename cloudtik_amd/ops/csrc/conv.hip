@@ -1138,7 +1138,16 @@ extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   // r4: the 8-wave 128 x 128 tile (cfg 9) beats the 4-wave one everywhere and the 8-wave
   // 128 x 256 one for 128-channel outputs (l2.c2 185 -> 130 us, l2.c3 90 -> 69;
   // profiles/r4/conv_cfg_8wave.md)
-  if (Co % 128 == 0 && NN % 256 == 0 && Co >= 256) return 3;
+  // CLOUDTIK_AMD_WGRAD_RULE=2: the 16-wave 128 x 256 tile with 64-pixel stages (cfg 11) instead
+  // of cfg 3.  Faster alone on every 256+-channel shape it divides (l3.c2 110 -> 91 us, l4.c2
+  // 146 -> 123, l3.down 101 -> 85) but SLOWER in the ResNet-50 step (22.79 -> 23.06 ms): a
+  // 1024-thread workgroup on the gradient side stream cannot share a CU with the data-gradient
+  // kernels it is meant to overlap (profiles/r4/conv_wgrad_split.md)
+  static const int rule = [] {
+    const char* e = std::getenv("CLOUDTIK_AMD_WGRAD_RULE");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (Co % 128 == 0 && NN % 256 == 0 && Co >= 256) return rule >= 2 ? 11 : 3;
   if (Co % 128 == 0 && NN % 128 == 0) return 9;
   // the 64-wide tiles serve the layer-1 shapes (802816-pixel reductions): 64-pixel stages win
   // there (l1.c2 301 -> 289 us, l1.c3 156 -> 142, l1.c1 128 -> 118; profiles/r4/conv_stream_probe.md)
