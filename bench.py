@@ -32,6 +32,7 @@ the ratio), ``--device cpu --model tiny`` (gloo plumbing check).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -537,8 +538,18 @@ def run_one(build, args, rank, world, device, kind):
     import torch
     step, close, info = build(args, rank, world, device, kind)
     bucketer = info.pop("bucketer", None)
-    elapsed, per_rank, loss, step_ms, audit = timed(step, args, rank, world, device,
-                                                    audit=info["unit"] == "images/s", bucketer=bucketer)
+    prio = None
+    if device.type == "cuda" and os.environ.get("CLOUDTIK_AMD_COMPUTE_PRIO", "0") == "1":
+        # the step's own stream at the highest priority: the gradient side stream (and RCCL's
+        # streams) keep the default one, so their workgroups yield CU slots to the critical path
+        lo, hi = torch.cuda.Stream.priority_range()
+        prio = torch.cuda.Stream(device=device, priority=min(lo, hi))
+        prio.wait_stream(torch.cuda.current_stream())
+    with (torch.cuda.stream(prio) if prio is not None else contextlib.nullcontext()):
+        elapsed, per_rank, loss, step_ms, audit = timed(step, args, rank, world, device,
+                                                        audit=info["unit"] == "images/s", bucketer=bucketer)
+    if prio is not None:
+        torch.cuda.current_stream().wait_stream(prio)
     del bucketer
     host_ms = audit.pop("host_issue_ms_mean", None) if audit else None
     host_arr = audit.pop("host_ms", None) if audit else None

@@ -280,14 +280,23 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
     mats = [_dgrad_weights(w, wt, rs, R, S, ci) for _, _, _, rs in live]
     for st in streams:
         st.wait_stream(cur)
-    for i, ((a, b), (Hr, Wr), taps, rs) in enumerate(live):
-        st = streams[i - 1] if i > 0 and streams else None
-        with (torch.cuda.stream(st) if st is not None else contextlib.nullcontext()):
-            tile0 = _dgrad_phase(C, dy, mats[i], ci, co, N, H, W, Hr, Wr, a, b, sh, sw, taps, out, accumulate,
-                                 bn, bn_y, bn_plan, tile0, zfill)
-        if tile0 is None:                           # the fused epilogue was declined: plain from here on
-            bn_plan = None
-            tile0 = 0
+    # or: the phases' tiles in ONE grid (conv.hip conv_igemm_phases_kernel)
+    batch = _PHASE_BATCH and not streams and len(live) > 1 and dy.is_cuda
+    if batch:
+        C.conv_batch_begin()
+    try:
+        for i, ((a, b), (Hr, Wr), taps, rs) in enumerate(live):
+            st = streams[i - 1] if i > 0 and streams else None
+            with (torch.cuda.stream(st) if st is not None else contextlib.nullcontext()):
+                tile0 = _dgrad_phase(C, dy, mats[i], ci, co, N, H, W, Hr, Wr, a, b, sh, sw, taps, out, accumulate,
+                                     bn, bn_y, bn_plan, tile0, zfill)
+            if tile0 is None:                       # the fused epilogue was declined: plain from here on
+                bn_plan = None
+                tile0 = 0
+    finally:
+        if batch:
+            C.conv_batch_end()
+
     if streams:
         for st in streams:
             cur.wait_stream(st)
@@ -300,6 +309,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape, stride=(1, 1), paddin
 
 
 _PHASE_STREAMS = os.environ.get("CLOUDTIK_AMD_CONV_PHASE_STREAMS", "0") == "1"
+# the output phases of a strided data gradient as one launch (one grid over all their tiles)
+_PHASE_BATCH = os.environ.get("CLOUDTIK_AMD_CONV_PHASE_BATCH", "0") == "1"
 _PHASE_STREAM_POOL = {}
 
 

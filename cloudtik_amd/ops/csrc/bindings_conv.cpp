@@ -16,6 +16,8 @@ int ct_conv_igemm_rows(int, int, int, int);
 int ct_conv_igemm_tile_m(int);
 int ct_conv_igemm_part_rows(int);
 void ct_conv_stream_set_cus(int);
+void ct_conv_batch_begin();
+int ct_conv_batch_end(hipStream_t);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
 int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
                   int, int, hipStream_t);
@@ -175,6 +177,13 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
   m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
   m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
+  m.def("conv_batch_begin", []() { ct_conv_batch_begin(); },
+        "queue the following one-tile conv launches (same configuration, <= 4) for one grid");
+  m.def("conv_batch_end", []() {
+          const int rc = ct_conv_batch_end(at::hip::getCurrentHIPStream().stream());
+          TORCH_CHECK(rc == 0, "conv_batch_end: launch failed (", rc, ")");
+        },
+        "launch the queued conv launches as one grid");
   m.def("conv_stream_set_cus", [](int64_t cus) { ct_conv_stream_set_cus((int)cus); },
         "streamed conv kernels: persistent workgroups = cus x per-CU count (0: the device's CUs)");
   m.def("conv_igemm_part_rows", &conv_igemm_part_rows, "rows per BatchNorm-statistics partial (EPI 1)");

@@ -260,8 +260,10 @@ __device__ __forceinline__ void cv_out_store(const ConvArgs& a, CvOut<BM / RPP>&
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS, int MINB, int EPI>
-__global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvArgs a) {
+// One output tile (L = tile index, N-tiles fastest) of conv_igemm_kernel; also the body of
+// conv_igemm_phases_kernel, which runs several launches' tiles in one grid.
+template <int BM, int BN, int WGM, int WGN, int NS, int EPI>
+__device__ __forceinline__ void conv_igemm_tile(const ConvArgs& a, const int L) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
   constexpr int STAGE = (BM + BN) * 128;
@@ -271,7 +273,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
   __shared__ __attribute__((aligned(1024))) char lds[NS * STAGE];   // the only LDS object
 
   const int ntn = a.Co / BN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = L / ntn, tn = L % ntn;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: weight bases in SGPRs
@@ -446,6 +447,33 @@ __global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvAr
       p[a.bnp2] = t2;
     }
   }
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int MINB, int EPI>
+__global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_kernel(ConvArgs a) {
+  conv_igemm_tile<BM, BN, WGM, WGN, NS, EPI>(a, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Up to four launches of one configuration in ONE grid: the output phases of a strided data
+// gradient (4 / 2 / 2 / 1 taps for a 3x3 stride-2 conv), each a short launch of a few hundred
+// tiles that left the chip draining between them.  Phase i owns tiles [start[i], start[i+1]);
+// its arguments are read from the kernel-argument segment at a wave-uniform index.
+constexpr int CV_MAXPH = 4;
+struct ConvPhases {
+  ConvArgs a[CV_MAXPH];
+  int start[CV_MAXPH];
+  int n;
+};
+
+template <int BM, int BN, int WGM, int WGN, int NS, int MINB, int EPI>
+__global__ void __launch_bounds__(64 * WGM * WGN, MINB) conv_igemm_phases_kernel(ConvPhases p) {
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  int ph = 0;
+#pragma unroll
+  for (int i = 1; i < CV_MAXPH; ++i)
+    if (i < p.n && L >= p.start[i]) ph = i;
+  ph = __builtin_amdgcn_readfirstlane(ph);
+  conv_igemm_tile<BM, BN, WGM, WGN, NS, EPI>(p.a[ph], L - p.start[ph]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -879,10 +907,47 @@ __global__ void bn_partials_finalize_kernel(const float* __restrict__ part, int 
   var_out[c] = (float)(m2 / n);
 }
 
+// conv_batch_begin() .. conv_batch_end(): the one-tile launches issued in between are collected
+// (same configuration, at most CV_MAXPH) and run as ONE conv_igemm_phases_kernel grid
+struct CvBatch {
+  bool on = false;
+  int n = 0, cfg = -1, epi = -1, bm = 0, bn = 0;
+  ConvArgs a[CV_MAXPH];
+  int (*launch)(const ConvPhases&, int, long, hipStream_t) = nullptr;
+};
+static thread_local CvBatch g_cv_batch;
+
+template <int BM, int BN, int WGM, int WGN, int NS, int MINB, bool WITH_BN>
+static int cv_phases_launch(const ConvPhases& p, int epi, long tiles, hipStream_t s) {
+  if (epi == 2) {
+    if constexpr (WITH_BN)
+      conv_igemm_phases_kernel<BM, BN, WGM, WGN, NS, MINB, 2><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(p);
+    else
+      return 6;
+  } else if (epi == 0) {
+    conv_igemm_phases_kernel<BM, BN, WGM, WGN, NS, MINB, 0><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(p);
+  } else {
+    return 6;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
 template <int BM, int BN, int WGM, int WGN, int NS, int MINB, bool WITH_BN = false>
-static int cv_launch(const ConvArgs& a, int epi, hipStream_t s) {
+static int cv_launch(const ConvArgs& a, int epi, hipStream_t s, int cfg = -1) {
   const long tiles = (long)ceil_div(a.M, BM) * (a.Co / BN);
   if (tiles > (1L << 30)) return 5;
+  CvBatch& B = g_cv_batch;
+  if (B.on && cfg >= 0 && epi != 1) {
+    // queued: validated here, launched by conv_batch_end
+    if (B.n == CV_MAXPH || (B.n && (B.cfg != cfg || B.epi != epi))) return 10;
+    B.cfg = cfg;
+    B.epi = epi;
+    B.bm = BM;
+    B.bn = BN;
+    B.launch = &cv_phases_launch<BM, BN, WGM, WGN, NS, MINB, true>;
+    B.a[B.n++] = a;
+    return 0;
+  }
   if (epi == 1)
     conv_igemm_kernel<BM, BN, WGM, WGN, NS, MINB, 1><<<(int)tiles, 64 * WGM * WGN, 0, s>>>(a);
   else if (epi == 2) {
@@ -1046,7 +1111,7 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
       case 11: return cs_launch<128, 128, 2, 2, 2, 2, true>(a, epi, cv_cu_count(), stream);
       case 12: return cs_launch<128, 64, 2, 2, 3, 2, true>(a, epi, cv_cu_count(), stream);
       case 13: return cs_launch<64, 128, 1, 4, 3, 2, true>(a, epi, cv_cu_count(), stream);
-      case 14: return cv_launch<128, 128, 2, 4, 2, 2, true>(a, epi, stream);
+      case 14: return cv_launch<128, 128, 2, 4, 2, 2, true>(a, epi, stream, 14);
       case 15: return cs_launch<128, 128, 2, 4, 2, 2, true>(a, epi, cv_cu_count(), stream);
       case 16: return cv_launch<128, 64, 4, 2, 2, 2, true>(a, epi, stream);
       case 18: return cv_launch<256, 128, 4, 4, 2, 1, true>(a, epi, stream);
@@ -1068,13 +1133,52 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
     case 11: return cs_launch<128, 128, 2, 2, 2, 2>(a, epi, cv_cu_count(), stream);
     case 12: return cs_launch<128, 64, 2, 2, 3, 2>(a, epi, cv_cu_count(), stream);
     case 13: return cs_launch<64, 128, 1, 4, 3, 2>(a, epi, cv_cu_count(), stream);
-    case 14: return cv_launch<128, 128, 2, 4, 2, 2>(a, epi, stream);
+    case 14: return cv_launch<128, 128, 2, 4, 2, 2, true>(a, epi, stream, 14);
     case 15: return cs_launch<128, 128, 2, 4, 2, 2>(a, epi, cv_cu_count(), stream);
     case 16: return cv_launch<128, 64, 4, 2, 2, 2>(a, epi, stream);
     case 17: return cs_launch<128, 64, 4, 2, 3, 2>(a, epi, cv_cu_count(), stream);
     case 18: return cv_launch<256, 128, 4, 4, 2, 1>(a, epi, stream);
     default: return 6;
   }
+}
+
+// conv_batch_begin / conv_batch_end (see CvBatch).  A configuration the batch cannot hold (not
+// a one-tile 8-wave 128 x 128 launch, or a second configuration) is launched directly as usual;
+// end returns nonzero if a queued launch failed.
+extern "C" void ct_conv_batch_begin() {
+  g_cv_batch.on = true;
+  g_cv_batch.n = 0;
+  g_cv_batch.cfg = g_cv_batch.epi = -1;
+}
+
+extern "C" int ct_conv_batch_end(hipStream_t stream) {
+  CvBatch& B = g_cv_batch;
+  B.on = false;
+  if (!B.n) return 0;
+  ConvPhases p{};
+  // the longest reductions first: their tiles are dispatched early, the short ones fill the tail
+  int order[CV_MAXPH];
+  for (int i = 0; i < B.n; ++i) order[i] = i;
+  for (int i = 1; i < B.n; ++i)
+    for (int j = i; j > 0 && B.a[order[j]].T > B.a[order[j - 1]].T; --j) std::swap(order[j], order[j - 1]);
+  long tiles = 0;
+  for (int i = 0; i < B.n; ++i) {
+    p.a[i] = B.a[order[i]];
+    p.start[i] = (int)tiles;
+    tiles += (long)ceil_div(p.a[i].M, B.bm) * (p.a[i].Co / B.bn);
+  }
+  for (int i = B.n; i < CV_MAXPH; ++i) p.start[i] = (int)tiles;
+  p.n = B.n;
+  const int n = B.n;
+  B.n = 0;
+  if (tiles > (1L << 30)) return 5;
+  if (n == 1) {
+    // one launch: the plain kernel (same tile code)
+    if (B.epi == 2) conv_igemm_kernel<128, 128, 2, 4, 2, 2, 2><<<(int)tiles, 512, 0, stream>>>(p.a[0]);
+    else conv_igemm_kernel<128, 128, 2, 4, 2, 2, 0><<<(int)tiles, 512, 0, stream>>>(p.a[0]);
+    return hipGetLastError() == hipSuccess ? 0 : 7;
+  }
+  return B.launch(p, B.epi, tiles, stream);
 }
 
 extern "C" int ct_bn_partials_finalize(const float* part, int tiles, int rows_per_tile, int M, int C, float* mean,

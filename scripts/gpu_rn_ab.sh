@@ -7,7 +7,7 @@ mkdir -p "$O"
 cd "$R"
 for r in 1 2 3; do
   for v in "$A" "$B"; do
-    env "$VAR=$v" timeout -k 10 240 python -u bench.py --model resnet50 --steps 20 --warmup 5 > "$O/rn_${v}_$r.json" 2> "$O/rn_${v}_$r.err" || exit $?
+    env "$VAR=$v" timeout -k 10 240 python -u bench.py --model ${MODEL:-resnet50} --steps 20 --warmup 5 > "$O/rn_${v}_$r.json" 2> "$O/rn_${v}_$r.err" || exit $?
     echo "$VAR=$v round $r: $(grep -o '"ms_per_step": [0-9.]*' "$O/rn_${v}_$r.json")"
   done
 done

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--title", default="")
+    ap.add_argument("--gaps", type=int, default=0, help="list the N largest idle-gap kinds of the main stream")
     a = ap.parse_args()
     rows = []
     with open(a.csv) as f:
@@ -66,6 +67,27 @@ def main():
                           sorted(per_stream.items(), key=lambda kv: -kv[1]))
         print(f"Per stream kernel time per step: {parts}; wall time with >= 1 kernel running "
               f"{cover / a.steps / 1e3:.2f} ms per step.\n")
+    if len(per_stream) > 1 or a.gaps:
+        # idle gaps of the busiest stream (the main one): where it waits on the host or on an
+        # event of another stream
+        main = max(per_stream.items(), key=lambda kv: kv[1])[0]
+        ms = [r for r in win if r[3] == main]
+        gaps = [(ms[i + 1][0] - ms[i][1], ms[i][2], ms[i + 1][2]) for i in range(len(ms) - 1)]
+        tot_gap = sum(g for g, _, _ in gaps if g > 0) / 1e3 / a.steps
+        big = sorted([g for g in gaps if g[0] > 5000], key=lambda g: -g[0])
+        print(f"Stream {main}: {tot_gap / 1e3:.2f} ms idle per step between its kernels; "
+              f"{sum(g for g, _, _ in big) / 1e3 / a.steps / 1e3:.2f} ms of it in {len(big) / a.steps:.0f} gaps > 5 us "
+              f"per step.\n")
+        if a.gaps:
+            agg = defaultdict(lambda: [0.0, 0])
+            for g, b, n in big:
+                k = (b[:60], n[:60])
+                agg[k][0] += g / 1e3 / a.steps
+                agg[k][1] += 1
+            print("| gap before | gap after | us/step | count/step |\n|---|---|---:|---:|")
+            for (b, n), (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:a.gaps]:
+                print(f"| `{b}` | `{n}` | {t:.0f} | {c / a.steps:.1f} |")
+            print()
     print("| kernel | ms/step | calls/step | % busy |\n|---|---:|---:|---:|")
     for n, t in sorted(tot.items(), key=lambda kv: -kv[1])[:a.top]:
         short = n if len(n) <= 100 else n[:97] + "..."

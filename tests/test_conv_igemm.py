@@ -401,3 +401,60 @@ def test_1x1_wgrad_on_tn_gemm(cuda, monkeypatch, tn):
     dw2 = CV.conv_wgrad(dy, x, w.shape, out=base.clone(), accumulate=True)
     assert _rel(dw2, wr.grad + base.float()) < 1e-2
     assert len(calls) == (2 if tn else 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci,co,H", [(128, 128, 15), (256, 64, 14), (128, 256, 8)])
+def test_strided_dgrad_phases_in_one_grid(cuda, monkeypatch, ci, co, H):
+    """conv.hip conv_igemm_phases_kernel: the output phases of a 3x3 stride-2 data gradient
+    queued (conv_batch_begin / end) and run as one grid match the fp32 reference, plain and
+    accumulating."""
+    from cloudtik_amd import ops
+    C = ops.require_native()
+    ends = {"n": 0}
+    orig = C.conv_batch_end
+
+    def counted():
+        ends["n"] += 1
+        return orig()
+
+    monkeypatch.setattr(C, "conv_batch_end", counted)
+    monkeypatch.setattr(CV, "_PHASE_BATCH", True)
+    torch.manual_seed(ci + co + H)
+    x = _nhwc(torch.randn(3, ci, H, H, device=cuda).to(torch.bfloat16))
+    w = _nhwc((torch.randn(co, ci, 3, 3, device=cuda) * (2.0 / (ci * 9)) ** 0.5).to(torch.bfloat16))
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    ref = F.conv2d(xr, wr, stride=2, padding=1)
+    dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
+    ref.backward(dy.float())
+    dx = CV.conv_dgrad(dy, w, x.shape, (2, 2), (1, 1))
+    assert _rel(dx, xr.grad) < 1e-2
+    other = _nhwc(torch.randn(x.shape, device=cuda).to(torch.bfloat16))
+    acc = CV.conv_dgrad(dy, w, x.shape, (2, 2), (1, 1), out=other.clone(), accumulate=True)
+    assert _rel(acc, xr.grad + other.float()) < 1e-2
+    assert ends["n"] == 2
+
+
+@pytest.mark.gpu
+def test_strided_dgrad_phases_in_one_grid_bn_epilogue(cuda, monkeypatch):
+    """The one-grid phases with the fused BatchNorm-backward epilogue (EPI 2: per-phase partial
+    rows) give the gradients of the per-phase launches: a 128-wide stride-2 bottleneck."""
+    from cloudtik_amd.models.resnet import Bottleneck
+    torch.manual_seed(5)
+    kw = dict(device=cuda, dtype=torch.bfloat16)
+    blk = Bottleneck(256, 128, 2, downsample=True, **kw).to(memory_format=torch.channels_last)
+    x0 = _nhwc(torch.randn(4, 256, 18, 18, device=cuda).to(torch.bfloat16))
+
+    def run(batch):
+        monkeypatch.setattr(CV, "_PHASE_BATCH", batch)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+        return x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
+
+    gx1, gp1 = run(True)
+    gx0, gp0 = run(False)
+    assert _rel(gx1, gx0) < 1e-2
+    for a, b in zip(gp1, gp0):
+        assert _rel(a, b) < 1e-2
