@@ -47,13 +47,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--cfgs", default="-1", help="conv configurations to time (comma list; -1 = auto)")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
     a = ap.parse_args()
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    want = set(a.shapes.split(",")) if a.shapes else None
     C = ops.require_native()
     dev = torch.device("cuda")
-    print("| conv | fwd EPI0 hot / cold us | fwd EPI1 (stats) hot / cold us | dgrad EPI0 hot / cold us | "
-          "dgrad EPI2 (BN bwd) hot / cold us |")
-    print("|---|---:|---:|---:|---:|")
+    print("| conv | cfg | fwd EPI0 hot / cold us | fwd EPI1 (stats) hot / cold us | dgrad EPI0 hot / cold us | "
+          "dgrad EPI2 (BN bwd) hot / cold us | dgrad EPI2 bitmask + accumulate (the residual input) hot / cold us |")
+    print("|---|---|---:|---:|---:|---:|---:|")
     for name, ci, co, H, k, s in SHAPES:
+        if want and name not in want:
+            continue
         pad = k // 2
         xbytes = a.batch * ci * H * H * 2
         ncopy = max(2, math.ceil(600e6 / xbytes))
@@ -64,25 +70,43 @@ def main():
         gamma = torch.ones(ci, device=dev, dtype=torch.bfloat16)
         beta = torch.zeros(ci, device=dev, dtype=torch.bfloat16)
         rm, rv = torch.zeros(ci, device=dev), torch.ones(ci, device=dev)
-        links = []
+        links, links3, outs = [], [], []
         for x in xs:                       # x = the output of a BN + ReLU whose input is xb
             xb = x
             _, stat = C.bn_fwd_train(xb, None, gamma, beta, rm, rv, 1e-5, 0.1, True)
             links.append(CV.BnBwdLink(xb, stat, 2))
-        r = {}
-        for tag, sel in (("hot", lambda L: L[:1]), ("cold", lambda L: L)):
-            r[("f0", tag)] = timeit([lambda x=x: CV.conv_fwd(x, w, (s, s), (pad, pad)) for x in sel(xs)], a.iters)
-            r[("f1", tag)] = timeit([lambda x=x: CV.conv_fwd(x, w, (s, s), (pad, pad), partials=True)
-                                     for x in sel(xs)], a.iters)
-            r[("d0", tag)] = timeit([lambda dy=dy: CV.conv_dgrad(dy, w, xs[0].shape, (s, s), (pad, pad))
-                                     for dy in sel(dys)], a.iters)
-            pairs = list(zip(sel(dys), sel(links)))
-            r[("d2", tag)] = timeit([lambda dy=dy, L=L: CV.conv_dgrad(dy, w, xs[0].shape, (s, s), (pad, pad), bn=L)
-                                     for dy, L in pairs], a.iters)
-        cell = lambda k: f"{r[(k, 'hot')]:.1f} / {r[(k, 'cold')]:.1f}"
-        print(f"| {name} {ci}->{co} {H}x{H} k{k} | {cell('f0')} | {cell('f1')} | {cell('d0')} | {cell('d2')} |",
-              flush=True)
-        del xs, dys, links
+            # the residual BN + ReLU of the ResNet block input: bitmask (mode 3), and the data
+            # gradient accumulates into the residual branch's gradient
+            mask = torch.empty(xb.numel() // 8, device=dev, dtype=torch.uint8)
+            _, stat3 = C.bn_fwd_train(xb, None, gamma, beta, rm, rv, 1e-5, 0.1, True, mask)
+            links3.append(CV.BnBwdLink(xb, stat3, 3, mask))
+            outs.append(torch.zeros_like(xb))
+        for cfg in cfgs:
+            CV._CFG = cfg
+            r = {}
+            for tag, sel in (("hot", lambda L: L[:1]), ("cold", lambda L: L)):
+              try:
+                r[("f0", tag)] = timeit([lambda x=x: CV.conv_fwd(x, w, (s, s), (pad, pad)) for x in sel(xs)], a.iters)
+                r[("f1", tag)] = timeit([lambda x=x: CV.conv_fwd(x, w, (s, s), (pad, pad), partials=True)
+                                         for x in sel(xs)], a.iters)
+                r[("d0", tag)] = timeit([lambda dy=dy: CV.conv_dgrad(dy, w, xs[0].shape, (s, s), (pad, pad))
+                                         for dy in sel(dys)], a.iters)
+                pairs = list(zip(sel(dys), sel(links)))
+                r[("d2", tag)] = timeit([lambda dy=dy, L=L: CV.conv_dgrad(dy, w, xs[0].shape, (s, s), (pad, pad),
+                                                                          bn=L)
+                                         for dy, L in pairs], a.iters)
+                trip = list(zip(sel(dys), sel(links3), sel(outs)))
+                r[("d3", tag)] = timeit([lambda dy=dy, L=L, o=o: CV.conv_dgrad(dy, w, xs[0].shape, (s, s), (pad, pad),
+                                                                               out=o, accumulate=True, bn=L,
+                                                                               bn_y=o)
+                                         for dy, L, o in trip], a.iters)
+              except RuntimeError:          # a configuration this shape's fwd or dgrad rejects
+                pass
+            cell = lambda k: (f"{r[(k, 'hot')]:.1f} / {r[(k, 'cold')]:.1f}" if (k, 'cold') in r else "-")
+            print(f"| {name} {ci}->{co} {H}x{H} k{k} | {cfg} | {cell('f0')} | {cell('f1')} | {cell('d0')} | "
+                  f"{cell('d2')} | {cell('d3')} |", flush=True)
+        CV._CFG = -1
+        del xs, dys, links, links3, outs
         torch.cuda.empty_cache()
 
 

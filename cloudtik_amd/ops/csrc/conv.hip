@@ -698,19 +698,36 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
   }
 }
 
+// Workgroups of `kernel` that fit on one CU (registers, LDS), at most `want`.  A persistent grid
+// sized for more than fit runs its surplus workgroups only after the first ones have walked all
+// their tiles: twice the time (the 8-wave streamed kernel with the BatchNorm-backward epilogue
+// needs 157 VGPRs, so 3 waves per SIMD, not the 4 of two 8-wave workgroups per CU).
+template <typename K>
+static int cs_resident(K kernel, int threads, int want) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, threads, 0) != hipSuccess || n <= 0) return want;
+  return std::min(n, want);
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int WPC, int EPI>
+static int cs_go(const ConvArgs& a, long tiles, int cus, hipStream_t s) {
+  constexpr int threads = 64 * WGM * WGN;
+  static const int per_cu = cs_resident(conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, EPI>, threads, WPC);
+  const int P = (int)std::min<long>(tiles, (long)cus * per_cu);
+  conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, EPI><<<P, threads, 0, s>>>(a, P);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
 template <int BM, int BN, int WGM, int WGN, int NS, int WPC, bool WITH_BN = false>
 static int cs_launch(const ConvArgs& a, int epi, int cus, hipStream_t s) {
   const long tiles = (long)ceil_div(a.M, BM) * (a.Co / BN);
   if (tiles > (1L << 30)) return 5;
-  const int P = (int)std::min<long>(tiles, (long)cus * WPC);
-  if (epi == 1)
-    conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, 1><<<P, 64 * WGM * WGN, 0, s>>>(a, P);
-  else if (epi == 2) {
-    if constexpr (WITH_BN) conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, 2><<<P, 64 * WGM * WGN, 0, s>>>(a, P);
+  if (epi == 1) return cs_go<BM, BN, WGM, WGN, NS, WPC, 1>(a, tiles, cus, s);
+  if (epi == 2) {
+    if constexpr (WITH_BN) return cs_go<BM, BN, WGM, WGN, NS, WPC, 2>(a, tiles, cus, s);
     else return 6;
-  } else
-    conv_stream_kernel<BM, BN, WGM, WGN, NS, WPC, 0><<<P, 64 * WGM * WGN, 0, s>>>(a, P);
-  return hipGetLastError() == hipSuccess ? 0 : 7;
+  }
+  return cs_go<BM, BN, WGM, WGN, NS, WPC, 0>(a, tiles, cus, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1097,7 +1114,16 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   const int epi = bn ? 2 : (part ? 1 : 0);
+  const bool autocfg = cfg < 0;
   cfg = ct_conv_igemm_rows(cfg, Co, M, T * a.cpt);
+  // the 8-wave streamed kernel's BatchNorm-backward variant holds one workgroup per CU (157
+  // VGPRs): the one-tile kernel at two per CU is faster there (l2.c1a dgrad 521 -> 281 us,
+  // profiles/r4/conv_epi2_occupancy.md)
+  static const bool epi2_stream = [] {
+    const char* e = std::getenv("CLOUDTIK_AMD_CONV_EPI2_STREAM");
+    return e && std::atoi(e) == 1;
+  }();
+  if (autocfg && epi == 2 && cfg == 15 && !epi2_stream) cfg = 14;
   if ((cfg == 1 || cfg == 2 || cfg == 5 || cfg == 9 || cfg == 10 || cfg == 11 || cfg == 13 || cfg == 14 ||
        cfg == 15 || cfg == 18) && Co % 128)
     return 2;
