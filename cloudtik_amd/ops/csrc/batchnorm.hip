@@ -20,6 +20,7 @@
 // Channels are the contiguous dimension: a thread owns 8 channels (one 16-byte vector) and
 // walks rows, so every load is a full coalesced 16-byte-per-lane access.
 #include "common.h"
+#include <algorithm>
 #include <stdlib.h>
 
 namespace ct {
@@ -659,12 +660,25 @@ __global__ __launch_bounds__(256) void bn_partials_merge_kernel(const float* __r
 // Training forward whose statistics were produced by the PRODUCER of x: per-tile means
 // [tiles][C] and M2 [tiles][C] over rows_per_tile rows each (the implicit-GEMM conv epilogue,
 // conv.hip).  Only the finalize and the apply pass run: x is read once instead of twice.
+// Up to this many per-tile partials the finalize kernels (16 row lanes x 64 channels, loads 8
+// deep) read them directly: a first-level merge / sum launch plus its dependent-launch gap costs
+// more than the finalize's few extra loads (the layer-4 BatchNorms of ResNet-50: 196 forward
+// partials, 98 backward tiles).  CLOUDTIK_AMD_BN_DIRECT_TILES=0: the merge above 128 partials
+// and the backward sum always, as before.
+static int bn_direct_tiles() {
+  static int n = [] {
+    const char* e = getenv("CLOUDTIK_AMD_BN_DIRECT_TILES");
+    return e ? atoi(e) : 256;
+  }();
+  return n;
+}
+
 extern "C" int ct_bn_fwd_train_given(const void* x, const void* res, const void* gamma, const void* beta,
                                      float* run_mean, float* run_var, void* y, const float* part, int tiles,
                                      int rows_per_tile, float* stat, int M, int C, float eps, float momentum,
                                      int relu, void* mask, hipStream_t stream) {
   if (C % 8 || M <= 0 || tiles <= 0 || (long)tiles * rows_per_tile < M) return -1;
-  if (tiles > 2 * BN_MERGE_GROUP) {
+  if (tiles > std::max(2 * BN_MERGE_GROUP, bn_direct_tiles())) {
     // merge groups of tiles first, into the tail of the partial buffer (means at
     // part + 2 tiles C, then the M2 rows): the finalize then reads at most 2 * GROUP partials
     const int groups = ceil_div(tiles, BN_MERGE_GROUP);
@@ -800,15 +814,22 @@ extern "C" int ct_bn_bwd_given(const void* dym, const void* x, const void* gamma
   float* q1 = work;
   float* q2 = work + (size_t)G * C;
   float* coef = q2 + (size_t)G * C;
-  bn_bwd_partials_sum_kernel<<<dim3(G, ceil_div(C, 256)), 256, 0, stream>>>(p1, p1 + p2off, tiles, C, q1, q2);
+  int nq = G;
+  if (tiles <= bn_direct_tiles()) {            // the finalize sums the tile partials itself
+    q1 = const_cast<float*>(p1);
+    q2 = const_cast<float*>(p1) + p2off;
+    nq = tiles;
+  } else {
+    bn_bwd_partials_sum_kernel<<<dim3(G, ceil_div(C, 256)), 256, 0, stream>>>(p1, p1 + p2off, tiles, C, q1, q2);
+  }
   const int acc = (param_flags >> 1) & 1;
   if (param_flags & 1)
     bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
-        q1, q2, G, M, C, (const bf16_t*)gamma, stat, stat + C, (float*)dgamma, (float*)dbeta, coef, coef + C,
+        q1, q2, nq, M, C, (const bf16_t*)gamma, stat, stat + C, (float*)dgamma, (float*)dbeta, coef, coef + C,
         coef + 2 * C, acc);
   else
     bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
-        q1, q2, G, M, C, (const bf16_t*)gamma, stat, stat + C, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C,
+        q1, q2, nq, M, C, (const bf16_t*)gamma, stat, stat + C, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C,
         coef + 2 * C, acc);
   const long tv = (long)M * (C / 8);
   const BnMask none{0, nullptr, nullptr, nullptr, nullptr};
