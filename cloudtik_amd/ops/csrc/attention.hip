@@ -867,13 +867,15 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
   a.relb = nullptr; a.relb_sh = 0; a.relb_len = 0; a.rel_base = 0;
   dim3 grid((Sq + 127) / 128, B * H);
   const bool drop = p_drop > 0.f;
-  // default: 3 waves/SIMD with dropout (168 VGPRs since the keep bits are packed into one
-  // register, no spills; 74-75 vs 77-78 us per BERT-large layer), 2 without (62 vs 64 us)
+  // default: 2 waves/SIMD.  (r3: 3 with dropout, 168 VGPRs, 74-75 vs 77-78 us per BERT-large
+  // layer; since both K/V tiles of an S <= 128 item load up front the 3-wave build spills one
+  // register and the BERT-large step is 0.03-0.06 ms faster at 2 in three interleaved rounds:
+  // 72.63 / 72.60 / 72.36 vs 72.57 / 72.55 / 72.34 ms)
   static const int wpe_env = [] {
     const char* e = getenv("CLOUDTIK_AMD_ATTN_FWD_WPE");
     return e ? atoi(e) : 0;
   }();
-  const int wpe = (wpe_env >= 1 && wpe_env <= 3) ? wpe_env : (p_drop > 0.f ? 3 : 2);
+  const int wpe = (wpe_env >= 1 && wpe_env <= 3) ? wpe_env : 2;
   static const int pipe = [] {
     // opt-in: measured slower than the one-item kernel on BERT-large shapes (B 256, S 128,
     // p 0.1: 75.5 us persistent / 84.9 us one item per workgroup vs 65.9 us;
