@@ -435,23 +435,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 // BN output is never written (nor read back by the pool): the BN backward recomputes its ReLU
 // mask from x (mode 2), and the pool backward needs only the argmax, kept as one byte per
 // element (window position kh*3+kw; ties go to the first maximum in row-major window order,
-// as PyTorch's kernel does).  One thread = one output pixel x 8 channels.
+// as PyTorch's kernel does).
+// Block = one output row (n, oh); thread = (ow, 8-channel chunk) items of that row.  The item's
+// chunk is fixed per thread when CV divides the block (ResNet: CV = 8) and the column advances
+// by a constant per iteration: no per-item 64-bit division / modulo (the grid-stride form spent
+// its time there, 2.4-2.9 TB/s).
 __global__ __launch_bounds__(256) void bn_apply_pool_kernel(const bf16_t* __restrict__ x, const float* __restrict__ a,
                                                             const float* __restrict__ b, bf16_t* __restrict__ y,
                                                             uint8_t* __restrict__ arg, int N, int H, int W, int CV,
                                                             int OH, int OW) {
-  const long total = (long)N * OH * OW * CV;
-  const long stride = (long)gridDim.x * blockDim.x;
+  const int n = blockIdx.x / OH, oh = blockIdx.x - n * OH;
+  const int items = OW * CV;
   const bool fixed = bn_fixed_cv(CV);
   float av[8], bv[8];
   if (fixed) { bn_load8(a, threadIdx.x % CV, av); bn_load8(b, threadIdx.x % CV, bv); }
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total; v += stride) {
-    const int cv = (int)(v % CV);
-    long t = v / CV;
-    const int ow = (int)(t % OW); t /= OW;
-    const int oh = (int)(t % OH);
-    const int n = (int)(t / OH);
-    if (!fixed) { bn_load8(a, cv, av); bn_load8(b, cv, bv); }
+  const long orow = ((long)n * OH + oh) * OW * CV;
+  const int cv0 = threadIdx.x % CV, ow0 = threadIdx.x / CV, ostep = blockDim.x / CV;
+  for (int i = threadIdx.x, k = 0; i < items; i += blockDim.x, ++k) {
+    int ow = ow0 + k * ostep, cv = cv0;
+    if (!fixed) {
+      ow = i / CV;
+      cv = i - ow * CV;
+      bn_load8(a, cv, av);
+      bn_load8(b, cv, bv);
+    }
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -460,11 +467,12 @@ __global__ __launch_bounds__(256) void bn_apply_pool_kernel(const bf16_t* __rest
     for (int kh = 0; kh < 3; ++kh) {
       const int h = 2 * oh - 1 + kh;
       if (h < 0 || h >= H) continue;
+      const long rbase = ((long)n * H + h) * W;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         const int w = 2 * ow - 1 + kw;
         if (w < 0 || w >= W) continue;
-        const u16x8 xv = reinterpret_cast<const u16x8*>(x)[(((long)n * H + h) * W + w) * CV + cv];
+        const u16x8 xv = reinterpret_cast<const u16x8*>(x)[(rbase + w) * CV + cv];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           // compare the bf16-rounded activation: the pooled value is the BN output as stored
@@ -477,38 +485,43 @@ __global__ __launch_bounds__(256) void bn_apply_pool_kernel(const bf16_t* __rest
     uint64_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { o[j] = f2bf(best[j]); packed |= (uint64_t)bi[j] << (8 * j); }
-    reinterpret_cast<u16x8*>(y)[v] = o;
-    reinterpret_cast<uint64_t*>(arg)[v] = packed;
+    reinterpret_cast<u16x8*>(y)[orow + i] = o;
+    reinterpret_cast<uint64_t*>(arg)[orow + i] = packed;
   }
 }
 
 // dx[n,h,w,c] = sum of dy over the (<= 4) pooling windows whose argmax is (h, w): a gather, so
-// no zero-fill and no atomics; one thread = one input pixel x 8 channels.
+// no zero-fill and no atomics.  Block = one input row (n, h) (its <= 2 window rows are
+// block-uniform); thread = (w, 8-channel chunk) items of that row.
 __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy,
                                                              const uint8_t* __restrict__ arg,
                                                              bf16_t* __restrict__ dx, int N, int H, int W, int CV,
                                                              int OH, int OW) {
-  const long total = (long)N * H * W * CV;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total; v += stride) {
-    const int cv = (int)(v % CV);
-    long t = v / CV;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+  const int n = blockIdx.x / H, h = blockIdx.x - n * H;
+  const int items = W * CV;
+  // windows o with 2o-1 <= h <= 2o+1
+  const int oh0 = h >> 1, oh1 = min((h + 1) >> 1, OH - 1);
+  const long xrow = ((long)n * H + h) * W * CV;
+  const bool fixed = bn_fixed_cv(CV);
+  const int cv0 = threadIdx.x % CV, w0 = threadIdx.x / CV, wstep = blockDim.x / CV;
+  for (int i = threadIdx.x, k = 0; i < items; i += blockDim.x, ++k) {
+    int w = w0 + k * wstep, cv = cv0;
+    if (!fixed) {
+      w = i / CV;
+      cv = i - w * CV;
+    }
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    // windows o with 2o-1 <= h <= 2o+1
-    const int oh0 = h >> 1, oh1 = min((h + 1) >> 1, OH - 1);
     const int ow0 = w >> 1, ow1 = min((w + 1) >> 1, OW - 1);
     for (int oh = oh0; oh <= oh1; ++oh) {
       const int kh = h - (2 * oh - 1);
       if (kh < 0 || kh > 2) continue;
+      const long obase = ((long)n * OH + oh) * OW;
       for (int ow = ow0; ow <= ow1; ++ow) {
         const int kw = w - (2 * ow - 1);
         if (kw < 0 || kw > 2) continue;
-        const long o = (((long)n * OH + oh) * OW + ow) * CV + cv;
+        const long o = (obase + ow) * CV + cv;
         const uint64_t packed = reinterpret_cast<const uint64_t*>(arg)[o];
         const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
         const uint8_t pos = (uint8_t)(kh * 3 + kw);
@@ -520,7 +533,7 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
     u16x8 out;
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = f2bf(acc[j]);
-    reinterpret_cast<u16x8*>(dx)[v] = out;
+    reinterpret_cast<u16x8*>(dx)[xrow + i] = out;
   }
 }
 
@@ -715,18 +728,18 @@ extern "C" int ct_bn_fwd_train_pool(const void* x, const void* gamma, const void
                                                            (const bf16_t*)gamma, (const bf16_t*)beta,
                                                            eps, momentum, run_mean, run_var, stat,
                                                            stat + C, stat + 2 * C, stat + 3 * C);
-  const long tv = (long)N * OH * OW * (C / 8);
-  bn_apply_pool_kernel<<<ew_grid(tv, 1), 256, 0, stream>>>((const bf16_t*)x, stat + 2 * C, stat + 3 * C, (bf16_t*)y,
-                                                           (uint8_t*)arg, N, H, W, C / 8, OH, OW);
+  if ((long)N * OH >= (1L << 31)) return -1;
+  bn_apply_pool_kernel<<<N * OH, 256, 0, stream>>>((const bf16_t*)x, stat + 2 * C, stat + 3 * C, (bf16_t*)y,
+                                                   (uint8_t*)arg, N, H, W, C / 8, OH, OW);
   return 0;
 }
 
 extern "C" int ct_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, int OH,
                                  int OW, hipStream_t stream) {
   if (C % 8 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
-  const long tv = (long)N * H * W * (C / 8);
-  maxpool3s2_bwd_kernel<<<ew_grid(tv, 1), 256, 0, stream>>>((const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, N, H,
-                                                            W, C / 8, OH, OW);
+  if ((long)N * H >= (1L << 31)) return -1;
+  maxpool3s2_bwd_kernel<<<N * H, 256, 0, stream>>>((const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, N, H, W,
+                                                   C / 8, OH, OW);
   return 0;
 }
 
