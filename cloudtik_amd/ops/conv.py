@@ -161,6 +161,25 @@ class _DgradWeights:
             return wti.reshape(ci, -1).contiguous()
         return torch.stack([wti[:, r, q, :] for r, q in rs], 1).reshape(ci, -1).contiguous()
 
+    @staticmethod
+    def _tiles(keys, slices, device):
+        """The 64 x 64 transpose tiles of every key for conv.hip dgrad_wgather_kernel (int32
+        [tiles, 10]), or None when a key's channel counts are not multiples of 64."""
+        rows = []
+        for key in keys:
+            soff, (co, ci, R, S), rs = key
+            if co % 64 or ci % 64 or co // 64 > 255 or ci // 64 > 255:
+                return None
+            doff = slices[key][0]
+            taps = [(r, q) for r in range(R) for q in range(S)] if len(rs) == R * S else list(rs)
+            T = len(taps)
+            for t, (r, q) in enumerate(taps):
+                for a in range(co // 64):
+                    for b in range(ci // 64):
+                        rows.append([soff >> 16, soff & 0xFFFF, doff >> 16, doff & 0xFFFF, co, ci, R * S * ci,
+                                     (r * S + q) * ci, t, T | (a << 16) | (b << 24)])
+        return torch.tensor(rows, dtype=torch.int32).to(device) if rows else None
+
     def get(self, w: torch.Tensor, rs) -> Optional[torch.Tensor]:
         task = torch._C._current_graph_task_id()
         if task == -1 or not w.is_contiguous(memory_format=torch.channels_last):
@@ -184,6 +203,8 @@ class _DgradWeights:
                 parts.append(idx.view(-1))
                 off += idx.numel()
             g["idx"] = torch.cat(parts)
+            g["desc"] = self._tiles(g["keys"], slices, w.device) if (
+                _DGRAD_WGATHER and w.is_cuda and w.dtype == torch.bfloat16) else None
             if g["flat"].numel() < 2 ** 31:
                 # 4-byte indices: the gather reads one index per element (a ResNet-50 pass: 25M
                 # elements, 100 MB of indices instead of 200 MB)
@@ -192,7 +213,10 @@ class _DgradWeights:
             g["slices"] = slices
             g["task"] = None
         if g["task"] != task:
-            torch.index_select(g["flat"], 0, g["idx"], out=g["buf"])
+            if g.get("desc") is not None:
+                _C().dgrad_wgather(g["flat"], g["buf"], g["desc"])
+            else:
+                torch.index_select(g["flat"], 0, g["idx"], out=g["buf"])
             g["task"] = task
         off, shape = g["slices"][key]
         n = shape[0] * shape[1]
@@ -201,6 +225,8 @@ class _DgradWeights:
 
 _DGRAD_W = _DgradWeights()
 _DGRAD_W_CACHE = os.environ.get("CLOUDTIK_AMD_CONV_DGRAD_WCACHE", "1") == "1"
+# the batched refresh as tiled transposes (conv.hip dgrad_wgather_kernel) instead of an element gather
+_DGRAD_WGATHER = os.environ.get("CLOUDTIK_AMD_CONV_DGRAD_WGATHER", "1") == "1"
 
 
 BN_BWD_FUSE = os.environ.get("CLOUDTIK_AMD_CONV_BN_BWD_FUSE", "1") == "1"

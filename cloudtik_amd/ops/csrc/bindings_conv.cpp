@@ -18,6 +18,7 @@ int ct_conv_igemm_part_rows(int);
 void ct_conv_stream_set_cus(int);
 void ct_conv_batch_begin();
 int ct_conv_batch_end(hipStream_t);
+int ct_dgrad_wgather(const void*, void*, const int*, int, hipStream_t);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
 int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
                   int, int, hipStream_t);
@@ -177,6 +178,15 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
   m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
   m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
+  m.def("dgrad_wgather", [](at::Tensor src, at::Tensor dst, at::Tensor desc) {
+          TORCH_CHECK(src.is_cuda() && dst.is_cuda() && desc.is_cuda(), "dgrad_wgather: CUDA tensors");
+          TORCH_CHECK(src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kBFloat16, "dgrad_wgather: bf16");
+          TORCH_CHECK(desc.scalar_type() == at::kInt && desc.is_contiguous() && desc.dim() == 2 && desc.size(1) == 10,
+                      "dgrad_wgather: desc int32 [tiles, 10]");
+          TORCH_CHECK(ct_dgrad_wgather(src.data_ptr(), dst.data_ptr(), desc.data_ptr<int>(), (int)desc.size(0),
+                                       at::hip::getCurrentHIPStream().stream()) == 0, "dgrad_wgather launch");
+        },
+        "data-gradient weight matrices of many convs by 64x64 tiled transposes (desc: 10 ints per tile)");
   m.def("conv_batch_begin", []() { ct_conv_batch_begin(); },
         "queue the following one-tile conv launches (same configuration, <= 4) for one grid");
   m.def("conv_batch_end", []() {

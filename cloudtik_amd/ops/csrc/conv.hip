@@ -1168,6 +1168,49 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
   }
 }
 
+// ---- data-gradient weight matrices of many convs in one launch (ops/conv.py _DgradWeights):
+// dst[ci][t][co] = src[co][r_t][s_t][ci] (channels_last weights [Co][R][S][Ci] -> the dgrad
+// operand [Ci][taps * Co]).  One workgroup = one 64 x 64 (co, ci) tile of one tap of one conv,
+// described by 8 ints: src offset (elements), dst offset, Co, Ci, R * S * Ci (src row stride),
+// tap source offset (r * S + s) * Ci, tap index t, number of taps T, and its first (co0, ci0).
+// Transposed through LDS: 16-B reads along ci, 16-B writes along co (the element gather it
+// replaces read one 2-B element per 64-B line, plus an index per element).
+__global__ __launch_bounds__(256) void dgrad_wgather_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                                            const int* __restrict__ desc) {
+  __shared__ unsigned short tile[64][64 + 8];
+  const int* d = desc + (long)blockIdx.x * 10;
+  const long soff = (long)d[0] * 65536 + d[1];   // offsets as (hi, lo) pairs of 16 bits
+  const long doff = (long)d[2] * 65536 + d[3];
+  const int Co = d[4], Ci = d[5], srow = d[6], tapoff = d[7], t = d[8], T = d[9] & 0xFFFF;
+  const int co0 = (d[9] >> 16) & 0xFF, ci0b = (d[9] >> 24) & 0xFF;
+  const int cob = co0 * 64, cib = ci0b * 64;
+  const int tid = threadIdx.x;
+  // load: 64 co rows x 64 ci (8 chunks of 8 per row): 512 chunks, 2 per thread
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = tid + 256 * k, row = c >> 3, ch = c & 7;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(src + soff + (long)(cob + row) * srow + tapoff + cib + ch * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[row][ch * 8 + e] = v[e];
+  }
+  __syncthreads();
+  // store: 64 ci rows x 64 co (8 chunks of 8 per row) at dst[ci][t][co]
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = tid + 256 * k, row = c >> 3, ch = c & 7;
+    u16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[ch * 8 + e][row];
+    *reinterpret_cast<u16x8*>(dst + doff + ((long)(cib + row) * T + t) * Co + cob + ch * 8) = v;
+  }
+}
+
+extern "C" int ct_dgrad_wgather(const void* src, void* dst, const int* desc, int ntiles, hipStream_t stream) {
+  if (ntiles <= 0) return 0;
+  dgrad_wgather_kernel<<<ntiles, 256, 0, stream>>>((const bf16_t*)src, (bf16_t*)dst, desc);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
 // conv_batch_begin / conv_batch_end (see CvBatch).  A configuration the batch cannot hold (not
 // a one-tile 8-wave 128 x 128 launch, or a second configuration) is launched directly as usual;
 // end returns nonzero if a queued launch failed.

@@ -458,3 +458,62 @@ def test_strided_dgrad_phases_in_one_grid_bn_epilogue(cuda, monkeypatch):
     assert _rel(gx1, gx0) < 1e-2
     for a, b in zip(gp1, gp0):
         assert _rel(a, b) < 1e-2
+
+
+def _emulate_wgather(flat, n_out, desc):
+    """conv.hip dgrad_wgather_kernel's index math on the CPU (one 64 x 64 tile per desc row)."""
+    out = torch.full((n_out,), float("nan"))
+    for d in desc.tolist():
+        soff, doff = d[0] * 65536 + d[1], d[2] * 65536 + d[3]
+        co, ci, srow, tapoff, t = d[4], d[5], d[6], d[7], d[8]
+        T, a, b = d[9] & 0xFFFF, (d[9] >> 16) & 0xFF, (d[9] >> 24) & 0xFF
+        cos = torch.arange(a * 64, a * 64 + 64)
+        cis = torch.arange(b * 64, b * 64 + 64)
+        src = soff + cos[:, None] * srow + tapoff + cis[None, :]             # [co, ci]
+        dst = doff + (cis[None, :] * T + t) * co + cos[:, None]
+        out[dst.reshape(-1)] = flat[src.reshape(-1)]
+    return out
+
+
+def test_dgrad_weight_tiles_match_index_gather():
+    """_DgradWeights._tiles: the transpose tiles (what the HIP kernel does with them, emulated)
+    rebuild the same [Ci, taps * Co] matrices as the element gather, full and phase tap sets."""
+    torch.manual_seed(4)
+    flat = torch.randn(200000)
+    w1 = flat[128:128 + 64 * 128 * 9].view(64, 3, 3, 128).permute(0, 3, 1, 2)     # [64, 128, 3, 3]
+    o2 = 128 + 64 * 128 * 9
+    w2 = flat[o2:o2 + 128 * 64].view(128, 1, 1, 64).permute(0, 3, 1, 2)          # [128, 64, 1, 1]
+    keys = {}
+    for w, rs in ((w1, [(r, q) for r in range(3) for q in range(3)]), (w1, [(0, 1), (2, 1)]), (w2, [(0, 0)])):
+        keys[(w.storage_offset(), tuple(w.shape), tuple(rs))] = CV._DgradWeights._index(w, rs)
+    slices, off, parts = {}, 0, []
+    for k, idx in keys.items():
+        slices[k] = (off, idx.shape)
+        parts.append(idx.view(-1))
+        off += idx.numel()
+    ref = torch.index_select(flat, 0, torch.cat(parts))
+    desc = CV._DgradWeights._tiles(keys, slices, torch.device("cpu"))
+    assert desc is not None and desc.shape[1] == 10
+    got = _emulate_wgather(flat, off, desc)
+    torch.testing.assert_close(got, ref)
+
+
+@pytest.mark.gpu
+def test_dgrad_wgather_kernel_matches_index_gather(cuda):
+    torch.manual_seed(6)
+    flat = torch.randn(300000, device=cuda).to(torch.bfloat16)
+    w1 = flat[256:256 + 128 * 64 * 9].view(128, 3, 3, 64).permute(0, 3, 1, 2)
+    keys = {}
+    for rs in ([(r, q) for r in range(3) for q in range(3)], [(1, 1)], [(0, 0), (0, 2), (2, 0), (2, 2)]):
+        keys[(w1.storage_offset(), tuple(w1.shape), tuple(rs))] = CV._DgradWeights._index(w1, rs)
+    slices, off, parts = {}, 0, []
+    for k, idx in keys.items():
+        slices[k] = (off, idx.shape)
+        parts.append(idx.view(-1))
+        off += idx.numel()
+    ref = torch.index_select(flat, 0, torch.cat(parts))
+    desc = CV._DgradWeights._tiles(keys, slices, flat.device)
+    out = torch.full((off,), float("nan"), device=cuda, dtype=torch.bfloat16)
+    from cloudtik_amd import ops
+    ops.require_native().dgrad_wgather(flat, out, desc)
+    assert torch.equal(out, ref)
