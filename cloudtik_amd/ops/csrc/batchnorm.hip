@@ -537,6 +537,99 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
   }
 }
 
+// The stem backward in one pass over the pool's input grid: the max-pool gradient gather (as
+// maxpool3s2_bwd_kernel), the ReLU mask recomputed from the BatchNorm input x (y = relu(a x + b)
+// as the forward rounded it), the masked gradient dy' stored, and the BatchNorm-backward sums
+// of dy' and dy' * xhat per channel for this block's row -- partial row n * H + h of p1 / p2
+// (what bn_bwd_given finalizes).  Replaces the separate reduction pass that re-read dy and x
+// (bn_bwd_reduce_kernel over 256 x 112 x 112 x 64).  Requires CV | 256 (fixed chunk per thread).
+constexpr int MPB_ROWS = 4;   // input rows per workgroup of maxpool3s2_bwd_bn_kernel
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_bn_kernel(const bf16_t* __restrict__ dy,
+                                                                const uint8_t* __restrict__ arg,
+                                                                const bf16_t* __restrict__ x,
+                                                                const float* __restrict__ stat,
+                                                                bf16_t* __restrict__ dx, float* __restrict__ p1,
+                                                                float* __restrict__ p2, int N, int H, int W, int CV,
+                                                                int OH, int OW) {
+  __shared__ float r1[4][256], r2[4][256];
+  const int HB = (H + MPB_ROWS - 1) / MPB_ROWS;
+  const int n = blockIdx.x / HB, h0 = (blockIdx.x - n * HB) * MPB_ROWS;
+  const int items = W * CV, C = CV * 8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cv0 = threadIdx.x % CV, w0 = threadIdx.x / CV, wstep = blockDim.x / CV;
+  float mu[8], is[8], fa[8], fb[8], s1[8], s2[8];
+  bn_load8(stat, cv0, mu);
+  bn_load8(stat + C, cv0, is);
+  bn_load8(stat + 2 * C, cv0, fa);
+  bn_load8(stat + 3 * C, cv0, fb);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (int h = h0; h < min(H, h0 + MPB_ROWS); ++h) {
+    const int oh0 = h >> 1, oh1 = min((h + 1) >> 1, OH - 1);
+    const long xrow = ((long)n * H + h) * W * CV;
+    for (int i = threadIdx.x, k = 0; i < items; i += blockDim.x, ++k) {
+      const int w = w0 + k * wstep;
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      const int ow0 = w >> 1, ow1 = min((w + 1) >> 1, OW - 1);
+      const u16x8 xv = reinterpret_cast<const u16x8*>(x)[xrow + i];
+      for (int oh = oh0; oh <= oh1; ++oh) {
+        const int kh = h - (2 * oh - 1);
+        if (kh < 0 || kh > 2) continue;
+        const long obase = ((long)n * OH + oh) * OW;
+        for (int ow = ow0; ow <= ow1; ++ow) {
+          const int kw = w - (2 * ow - 1);
+          if (kw < 0 || kw > 2) continue;
+          const long o = (obase + ow) * CV + cv0;
+          const uint64_t packed = reinterpret_cast<const uint64_t*>(arg)[o];
+          const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
+          const uint8_t pos = (uint8_t)(kh * 3 + kw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (((packed >> (8 * j)) & 0xFF) == pos) acc[j] += bf2f(g[j]);
+        }
+      }
+      u16x8 out;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xf = bf2f(xv[j]);
+        const bool on = bf2f(f2bf(bn_pre(xf, fa[j], fb[j], 0.f))) > 0.f;
+        out[j] = on ? f2bf(acc[j]) : (unsigned short)0;
+        const float d = bf2f(out[j]);
+        s1[j] += d;
+        s2[j] += d * (xf - mu[j]) * is[j];
+      }
+      reinterpret_cast<u16x8*>(dx)[xrow + i] = out;
+    }
+  }
+  // per-channel sums: lanes of one wave holding the same chunk (lane % CV) folded by xor
+  // shuffles, then the 4 waves through LDS
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    for (int m = CV; m < 64; m <<= 1) {
+      s1[j] += __shfl_xor(s1[j], m, 64);
+      s2[j] += __shfl_xor(s2[j], m, 64);
+    }
+  }
+  if (lane < CV) {                                // CV <= 32: every chunk in every wave
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r1[wave][lane * 8 + j] = s1[j];
+      r2[wave][lane * 8 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  const long prow = (long)blockIdx.x * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {   // chunk c >> 3 is lane c >> 3 of every wave
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { t1 += r1[q][c]; t2 += r2[q][c]; }
+    p1[prow + c] = t1;
+    p2[prow + c] = t2;
+  }
+}
+
 inline BnLayout bn_layout(int M, int C, int target_blocks) {
   BnLayout L;
   L.M = M; L.C = C; L.CV = C / 8;
@@ -741,6 +834,25 @@ extern "C" int ct_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int 
   maxpool3s2_bwd_kernel<<<N * H, 256, 0, stream>>>((const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, N, H, W,
                                                    C / 8, OH, OW);
   return 0;
+}
+
+// partial rows (= workgroups) of ct_maxpool3s2_bwd_bn
+extern "C" long ct_maxpool3s2_bwd_bn_rows(int N, int H) { return (long)N * ((H + MPB_ROWS - 1) / MPB_ROWS); }
+
+// maxpool3s2_bwd + the stem BatchNorm's backward reduction (maxpool3s2_bwd_bn_kernel): dxm = the
+// masked gradient, part = float[2 * N * H * C] (p1 rows then p2 rows), stat = the forward's float[4C]
+extern "C" int ct_maxpool3s2_bwd_bn(const void* dy, const void* arg, const void* x, const float* stat, void* dxm,
+                                    float* part, int N, int H, int W, int C, int OH, int OW, hipStream_t stream) {
+  if (C % 8 || 256 % (C / 8) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  // one partial row per workgroup (MPB_ROWS input rows); C <= 256 (CV <= 32 chunks, folded
+  // inside each wave)
+  if (C / 8 > 32) return -1;
+  const long rows = (long)N * ((H + MPB_ROWS - 1) / MPB_ROWS);
+  if (rows >= (1L << 31)) return -1;
+  maxpool3s2_bwd_bn_kernel<<<(int)rows, 256, 0, stream>>>((const bf16_t*)dy, (const uint8_t*)arg,
+                                                          (const bf16_t*)x, stat, (bf16_t*)dxm, part,
+                                                          part + rows * C, N, H, W, C / 8, OH, OW);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
 // inference-mode forward with given affine coefficients a, b (float[C] each)

@@ -46,6 +46,9 @@ int ct_bn_fwd_train_given(const void*, const void*, const void*, const void*, fl
 int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
                          int, int, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
+int ct_maxpool3s2_bwd_bn(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
+                         int, hipStream_t);
+long ct_maxpool3s2_bwd_bn_rows(int, int);
 int ct_bn_bwd_given(const void*, const void*, const void*, const float*, void*, void*, void*, int, const float*, long,
                     int, float*, int, int, hipStream_t);
 int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, void*, void*, void*, void*, int,
@@ -535,6 +538,29 @@ at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W) {
   return dx;
 }
 
+// stem backward: the max-pool gradient gather + the BatchNorm's ReLU mask and backward sums in one
+// pass; returns the masked gradient (at x's shape) and fills part (float[2 * rows * C]: p1 rows
+// then p2 rows, rows = maxpool3s2_bwd_bn_rows(N, H) tiles) for bn_bwd_given
+at::Tensor maxpool3s2_bwd_bn(at::Tensor dy, at::Tensor arg, at::Tensor x, at::Tensor stat, at::Tensor part) {
+  at::Tensor dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dyc, "dy");
+  check_nhwc(x, "x");
+  CHECK_F32(stat);
+  CHECK_F32(part);
+  const int N = dyc.size(0), C = dyc.size(1), OH = dyc.size(2), OW = dyc.size(3);
+  const int H = x.size(2), W = x.size(3);
+  TORCH_CHECK(x.size(0) == N && x.size(1) == C && stat.numel() == 4 * (long)C, "maxpool3s2_bwd_bn: shapes");
+  TORCH_CHECK(arg.scalar_type() == at::kByte && arg.is_contiguous() && arg.numel() == dyc.numel(),
+              "maxpool3s2_bwd_bn: argmax bytes");
+  TORCH_CHECK(part.is_contiguous() && part.numel() >= 2L * ct_maxpool3s2_bwd_bn_rows(N, H) * C,
+              "maxpool3s2_bwd_bn: part buffer");
+  auto dxm = at::empty_like(x);
+  int rc = ct_maxpool3s2_bwd_bn(dyc.data_ptr(), arg.data_ptr(), x.data_ptr(), stat.data_ptr<float>(), dxm.data_ptr(),
+                                part.data_ptr<float>(), N, H, W, C, OH, OW, cur_stream());
+  TORCH_CHECK(rc == 0, "maxpool3s2_bwd_bn: unsupported shape");
+  return dxm;
+}
+
 at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor a, at::Tensor b, bool relu) {
   check_nhwc(x, "x");
   const int C = x.size(1);
@@ -642,6 +668,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_p2p(m);
   register_lt(m);
   register_conv(m);
+  m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
+  m.def("maxpool3s2_bwd_bn_rows", [](int64_t N, int64_t H) { return (int64_t)ct_maxpool3s2_bwd_bn_rows((int)N, (int)H); });
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);

@@ -292,6 +292,11 @@ def _bn_param_grads(wp, bp, gamma, x, stat, dy, y, mode, has_res):
     return tuple(_C().bn_bwd(dy, y, x, gamma, stat, mode, has_res, None, None))
 
 
+# the stem backward's pool gather and BatchNorm reduction in one kernel (batchnorm.hip
+# maxpool3s2_bwd_bn_kernel)
+_STEM_POOL_BN_FUSE = os.environ.get("CLOUDTIK_AMD_STEM_POOL_BN_FUSE", "0") == "1"
+
+
 class _BNReLUPoolFn(torch.autograd.Function):
     """ResNet stem ``maxpool3x3/s2/p1(relu(bn(x)))`` (batchnorm.hip ``bn_apply_pool_kernel``):
     the full-resolution BN output is never materialised; the backward gathers the pooled
@@ -308,8 +313,26 @@ class _BNReLUPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dyp):
         x, gamma, stat, arg = ctx.saved_tensors
-        dy = _C().maxpool3s2_bwd(dyp, arg, x.shape[2], x.shape[3])
         wp, bp = ctx.params
+        if _STEM_POOL_BN_FUSE and x.shape[1] in (8, 16, 32, 64, 128, 256):
+            # pool gradient, ReLU mask and the BN-backward sums in one pass (partials per block
+            # of input rows), then the finalize + apply of bn_bwd_given: x is not re-read for a
+            # reduction
+            rows = _C().maxpool3s2_bwd_bn_rows(x.shape[0], x.shape[2])
+            part = torch.empty(2 * rows * x.shape[1], device=x.device, dtype=torch.float32)
+            dym = _C().maxpool3s2_bwd_bn(dyp, arg, x, stat, part)
+            flat = all(p is not None and p.grad is not None and getattr(p, "_ct_flat_grad", False)
+                       and p.grad.is_contiguous() and p.grad.dtype == gamma.dtype for p in (wp, bp))
+            if flat:
+                dx, _, _ = _C().bn_bwd_given(dym, x, gamma, stat, part, rows, rows, wp.grad, bp.grad)
+                for p in (wp, bp):
+                    cb = getattr(p, "_ct_grad_ready", None)
+                    if cb is not None:
+                        cb(p)
+                return dx, None, None, None, None, None, None
+            dx, dg, db = _C().bn_bwd_given(dym, x, gamma, stat, part, rows, rows, None, None)
+            return dx, dg, db, None, None, None, None
+        dy = _C().maxpool3s2_bwd(dyp, arg, x.shape[2], x.shape[3])
         dx, _, dg, db = _bn_param_grads(wp, bp, gamma, x, stat, dy, None, 2, False)
         return dx, dg, db, None, None, None, None
 
