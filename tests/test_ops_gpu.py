@@ -220,9 +220,13 @@ def test_batchnorm_act(cuda, C, HW, res):
 
 @pytest.mark.parametrize("HW", [112, 37])
 @pytest.mark.parametrize("shift", [0.5, -1.0])      # -1.0: most activations ReLU to 0 -> many ties
-def test_bn_relu_maxpool_stem(cuda, HW, shift):
-    """Fused ResNet stem (bn_apply_pool_kernel + maxpool3s2_bwd_kernel) vs the unfused native
-    BN + PyTorch max_pool2d on the same bf16 tensors, and vs an fp32 reference."""
+@pytest.mark.parametrize("bwd_fuse", [False, True])  # maxpool3s2_bwd_bn_kernel (pool grad + BN sums)
+def test_bn_relu_maxpool_stem(cuda, HW, shift, bwd_fuse, monkeypatch):
+    """Fused ResNet stem (bn_apply_pool_kernel + maxpool3s2_bwd_kernel, or the one-pass pool
+    gradient + BatchNorm-backward reduction) vs the unfused native BN + PyTorch max_pool2d on the
+    same bf16 tensors, and vs an fp32 reference."""
+    from cloudtik_amd.ops import functional as FN
+    monkeypatch.setattr(FN, "_STEM_POOL_BN_FUSE", bwd_fuse)
     torch.manual_seed(1)
     N, C = 4, 64
     x0 = (torch.randn(N, C, HW, HW, device=cuda) + shift).bfloat16().contiguous(memory_format=torch.channels_last)
