@@ -100,9 +100,19 @@ class Bottleneck(nn.Module):
             # epilogue absorbs that branch's gradient
             st = self.training and not self.bn1.frozen      # BatchNorm statistics from the conv epilogues
             out, x = igemm.conv2d(x, self.conv1, keep_input=True, bn_stats=st)
-            idt = self.down_bn(igemm.conv2d(x, self.down, bn_stats=st)) if self.down is not None else x
+            d = igemm.conv2d(x, self.down, bn_stats=st) if self.down is not None else None
             out = self.bn2(igemm.conv2d(self.bn1(out), self.conv2, bn_stats=st))
-            return self.bn3(igemm.conv2d(out, self.conv3, bn_stats=st), residual=idt)
+            c3 = igemm.conv2d(out, self.conv3, bn_stats=st)
+            b3, bd = self.bn3, getattr(self, "down_bn", None)
+            if (d is not None and st and b3.relu and not bd.relu and not bd.frozen
+                    and (b3.eps, b3.momentum) == (bd.eps, bd.momentum)):
+                # bn3(conv3) + down_bn(down) + ReLU in one apply pass: the downsample branch's
+                # BatchNorm output is never written (ops.functional._BNAddBNActFn)
+                return ops.batch_norm_add_bn_act(c3, b3.weight, b3.bias, b3.running_mean, b3.running_var,
+                                                 d, bd.weight, bd.bias, bd.running_mean, bd.running_var,
+                                                 momentum=b3.momentum, eps=b3.eps)
+            idt = bd(d) if d is not None else x
+            return b3(c3, residual=idt)
         # MIOpen path (CLOUDTIK_AMD_CONV_IGEMM=0, CPU): 1x1 convs as NHWC GEMMs, conv1's dgrad
         # GEMM absorbs the residual branch's gradient (ops/conv1x1.py)
         out, x = conv1x1(x, self.conv1, keep_input=True)

@@ -239,6 +239,43 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// y = relu(x * a[c] + b[c] + bf16(x2 * a2[c] + b2[c])) + the ReLU bitmask: a BatchNorm + residual
+// + ReLU whose residual is itself a BatchNorm output (the ResNet downsample branch) -- that
+// residual is never written and read back.  Rounds the inner BatchNorm output to bf16 first, so
+// y is bit-identical to bn_apply(x2) followed by bn_apply(x, res).
+__global__ __launch_bounds__(256) void bn_apply2_kernel(const bf16_t* __restrict__ x, const float* __restrict__ a,
+                                                        const float* __restrict__ b, const bf16_t* __restrict__ x2,
+                                                        const float* __restrict__ a2, const float* __restrict__ b2,
+                                                        bf16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                        long total_vec, int CV) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const bool fixed = bn_fixed_cv(CV);
+  float av[8], bv[8], a2v[8], b2v[8];
+  if (fixed) {
+    const int cv = threadIdx.x % CV;
+    bn_load8(a, cv, av); bn_load8(b, cv, bv); bn_load8(a2, cv, a2v); bn_load8(b2, cv, b2v);
+  }
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec; v += stride) {
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
+    const u16x8 x2v = reinterpret_cast<const u16x8*>(x2)[v];
+    if (!fixed) {
+      const int cv = (int)(v % CV);
+      bn_load8(a, cv, av); bn_load8(b, cv, bv); bn_load8(a2, cv, a2v); bn_load8(b2, cv, b2v);
+    }
+    u16x8 o;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float r = bf2f(f2bf(bn_pre(bf2f(x2v[j]), a2v[j], b2v[j], 0.f)));
+      const float t = fmaxf(bn_pre(bf2f(xv[j]), av[j], bv[j], r), 0.f);
+      o[j] = f2bf(t);
+      bits |= (o[j] != 0 && !(o[j] & 0x8000u) ? 1u : 0u) << j;
+    }
+    reinterpret_cast<u16x8*>(y)[v] = o;
+    mask[v] = (uint8_t)bits;
+  }
+}
+
 // ReLU mask source for the backward: mode 0 = no ReLU, 1 = read y (fused residual add),
 // 2 = recompute the pre-activation from x and the forward affine (a, b): no y read at all,
 // 3 = the forward's bitmask (one byte per 8-channel vector, bit j = y > 0: what a BN +
@@ -777,6 +814,46 @@ static int bn_direct_tiles() {
     return e ? atoi(e) : 256;
   }();
   return n;
+}
+
+// merge (when many) + finalize of producer partials into stat = float[4C]
+static void bn_given_finalize(const float* part, int tiles, int rows_per_tile, const void* gamma, const void* beta,
+                              float* run_mean, float* run_var, float* stat, int M, int C, float eps, float momentum,
+                              hipStream_t stream) {
+  if (tiles > std::max(2 * BN_MERGE_GROUP, bn_direct_tiles())) {
+    const int groups = ceil_div(tiles, BN_MERGE_GROUP);
+    float* om = const_cast<float*>(part) + (size_t)2 * tiles * C;
+    bn_partials_merge_kernel<<<dim3(groups, ceil_div(C, 64)), 256, 0, stream>>>(
+        part, part + (size_t)tiles * C, tiles, rows_per_tile, M, C, om, om + (size_t)groups * C);
+    part = om;
+    tiles = groups;
+    rows_per_tile *= BN_MERGE_GROUP;
+  }
+  BnLayout L{M, C, C / 8, 1, rows_per_tile};
+  bn_finalize_kernel<<<ceil_div(C, 64), 1024, 0, stream>>>(part, part + (size_t)tiles * C, tiles, L,
+                                                           (const bf16_t*)gamma, (const bf16_t*)beta,
+                                                           eps, momentum, run_mean, run_var, stat,
+                                                           stat + C, stat + 2 * C, stat + 3 * C);
+}
+
+// Two BatchNorms with producer partials, y = relu(bn(x) + bn2(x2)) + bitmask (bn_apply2_kernel)
+extern "C" int ct_bn_fwd_train_given2(const void* x, const void* gamma, const void* beta, float* run_mean,
+                                      float* run_var, const float* part, int tiles, int rows_per_tile, float* stat,
+                                      const void* x2, const void* gamma2, const void* beta2, float* run_mean2,
+                                      float* run_var2, const float* part2, int tiles2, int rows_per_tile2,
+                                      float* stat2, void* y, void* mask, int M, int C, float eps, float momentum,
+                                      hipStream_t stream) {
+  if (C % 8 || M <= 0 || tiles <= 0 || tiles2 <= 0 || (long)tiles * rows_per_tile < M ||
+      (long)tiles2 * rows_per_tile2 < M || !mask)
+    return -1;
+  bn_given_finalize(part, tiles, rows_per_tile, gamma, beta, run_mean, run_var, stat, M, C, eps, momentum, stream);
+  bn_given_finalize(part2, tiles2, rows_per_tile2, gamma2, beta2, run_mean2, run_var2, stat2, M, C, eps, momentum,
+                    stream);
+  const long tv = (long)M * (C / 8);
+  bn_apply2_kernel<<<ew_grid(tv, 1), 256, 0, stream>>>((const bf16_t*)x, stat + 2 * C, stat + 3 * C,
+                                                       (const bf16_t*)x2, stat2 + 2 * C, stat2 + 3 * C, (bf16_t*)y,
+                                                       (uint8_t*)mask, tv, C / 8);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
 extern "C" int ct_bn_fwd_train_given(const void* x, const void* res, const void* gamma, const void* beta,

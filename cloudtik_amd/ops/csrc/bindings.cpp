@@ -46,6 +46,9 @@ int ct_bn_fwd_train_given(const void*, const void*, const void*, const void*, fl
 int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
                          int, int, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
+int ct_bn_fwd_train_given2(const void*, const void*, const void*, float*, float*, const float*, int, int, float*,
+                           const void*, const void*, const void*, float*, float*, const float*, int, int, float*,
+                           void*, void*, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd_bn(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
                          int, hipStream_t);
 long ct_maxpool3s2_bwd_bn_rows(int, int);
@@ -502,6 +505,40 @@ std::vector<at::Tensor> bn_fwd_train_given(at::Tensor x, c10::optional<at::Tenso
   return {y, stat};
 }
 
+// y = relu(bn(x) + bn2(x2)) with both BatchNorms' statistics from their producers' partials (the
+// ResNet downsample block: bn3(conv3) + down_bn(down)): returns (y, mask bytes, stat, stat2)
+std::vector<at::Tensor> bn_fwd_train_given2(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor run_mean,
+                                            at::Tensor run_var, at::Tensor part, int64_t rows_per_tile,
+                                            at::Tensor x2, at::Tensor gamma2, at::Tensor beta2,
+                                            at::Tensor run_mean2, at::Tensor run_var2, at::Tensor part2,
+                                            int64_t rows_per_tile2, double eps, double momentum) {
+  check_nhwc(x, "x");
+  check_nhwc(x2, "x2");
+  TORCH_CHECK(x2.sizes() == x.sizes() && x2.strides() == x.strides(), "bn_fwd_train_given2: x2 layout");
+  const int C = x.size(1);
+  const long M = nhwc_rows(x);
+  for (const at::Tensor* t : {&gamma, &beta, &run_mean, &run_var, &gamma2, &beta2, &run_mean2, &run_var2})
+    TORCH_CHECK(t->numel() == C, "bn_fwd_train_given2: per-channel tensors");
+  CHECK_F32(run_mean); CHECK_F32(run_var); CHECK_F32(run_mean2); CHECK_F32(run_var2);
+  CHECK_IN(part); CHECK_F32(part); CHECK_IN(part2); CHECK_F32(part2);
+  const long tiles = (M + rows_per_tile - 1) / rows_per_tile, tiles2 = (M + rows_per_tile2 - 1) / rows_per_tile2;
+  TORCH_CHECK(part.numel() >= 2 * (tiles + (tiles > 128 ? (tiles + 63) / 64 : 0)) * C &&
+              part2.numel() >= 2 * (tiles2 + (tiles2 > 128 ? (tiles2 + 63) / 64 : 0)) * C,
+              "bn_fwd_train_given2: part buffers");
+  auto y = at::empty_like(x);
+  auto mask = at::empty({x.numel() / 8}, x.options().dtype(at::kByte));
+  auto stat = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
+  auto stat2 = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_fwd_train_given2(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr<float>(),
+                                  run_var.data_ptr<float>(), part.data_ptr<float>(), (int)tiles, (int)rows_per_tile,
+                                  stat.data_ptr<float>(), x2.data_ptr(), gamma2.data_ptr(), beta2.data_ptr(),
+                                  run_mean2.data_ptr<float>(), run_var2.data_ptr<float>(), part2.data_ptr<float>(),
+                                  (int)tiles2, (int)rows_per_tile2, stat2.data_ptr<float>(), y.data_ptr(),
+                                  mask.data_ptr(), (int)M, C, (float)eps, (float)momentum, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_fwd_train_given2: unsupported C=", C);
+  return {y, mask, stat, stat2};
+}
+
 // ResNet stem: returns (y_pool [N, C, OH, OW] channels_last, argmax bytes [N, OH, OW, C] uint8, stat)
 std::vector<at::Tensor> bn_fwd_train_pool(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor run_mean,
                                           at::Tensor run_var, double eps, double momentum) {
@@ -669,6 +706,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_lt(m);
   register_conv(m);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
+  m.def("bn_fwd_train_given2", &bn_fwd_train_given2);
   m.def("maxpool3s2_bwd_bn_rows", [](int64_t N, int64_t H) { return (int64_t)ct_maxpool3s2_bwd_bn_rows((int)N, (int)H); });
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

@@ -277,6 +277,82 @@ class _BNActFn(torch.autograd.Function):
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None
 
 
+# BN(x) + BN2(x2) + ReLU in one apply pass when both statistics come from conv epilogues
+_BN_ADD_BN_FUSE = os.environ.get("CLOUDTIK_AMD_BN_ADD_BN_FUSE", "1") == "1"
+
+
+class _BNAddBNActFn(torch.autograd.Function):
+    """``relu(bn(x) + bn2(x2))`` -- a ResNet downsample block's ``bn3(conv3) + down_bn(down)``
+    -- with the downsample BatchNorm's output never materialised (batchnorm.hip
+    ``bn_apply2_kernel``): forward and gradients are those of ``_BNActFn(x2, relu=False)`` feeding
+    ``_BNActFn(x, residual=..., relu=True)`` (bitmask mode), which it replaces."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, run_mean, run_var, x2, gamma2, beta2, run_mean2, run_var2, momentum, eps):
+        g1, g2 = x._ct_bn_part, x2._ct_bn_part
+        y, mask, stat, stat2 = _C().bn_fwd_train_given2(x, gamma, beta, run_mean, run_var, g1[0], g1[1],
+                                                         x2, gamma2, beta2, run_mean2, run_var2, g2[0], g2[1],
+                                                         eps, momentum)
+        ctx.save_for_backward(x, mask, gamma, stat, x2, gamma2, stat2)
+        ctx.params = (gamma, beta, gamma2, beta2)
+        from cloudtik_amd.ops.conv import BnBwdLink
+        ctx.bn_link = BnBwdLink(x, stat, 3, mask)
+        y._ct_bn_bwd = ctx.bn_link
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, gamma, stat, x2, gamma2, stat2 = ctx.saved_tensors
+        wp, bp, wp2, bp2 = ctx.params
+
+        def flat_ok(w, b, g):
+            return all(p is not None and p.grad is not None and getattr(p, "_ct_flat_grad", False)
+                       and p.grad.is_contiguous() and p.grad.dtype == g.dtype for p in (w, b))
+
+        def ready(*ps):
+            for p in ps:
+                cb = getattr(p, "_ct_grad_ready", None)
+                if cb is not None:
+                    cb(p)
+
+        f1, f2 = flat_ok(wp, bp, gamma), flat_ok(wp2, bp2, gamma2)
+        given = ctx.bn_link.take(dy)
+        dg = db = dg2 = db2 = None
+        if given is not None and dy.is_contiguous(memory_format=torch.channels_last):
+            part, tiles, rows = given
+            dym = dy                                   # already ReLU-masked by the conv epilogue
+            dx, dg, db = _C().bn_bwd_given(dym, x, gamma, stat, part, tiles, rows,
+                                           wp.grad if f1 else None, bp.grad if f1 else None)
+        else:
+            dx, dym, dg, db = _C().bn_bwd(dy, mask, x, gamma, stat, 3, True,
+                                          wp.grad if f1 else None, bp.grad if f1 else None)
+        if f1:
+            dg = db = None
+            ready(wp, bp)
+        # the downsample BatchNorm (no ReLU) sees the masked gradient, as the residual input did
+        dx2, _, dg2, db2 = _C().bn_bwd(dym, None, x2, gamma2, stat2, 0, False,
+                                       wp2.grad if f2 else None, bp2.grad if f2 else None)
+        if f2:
+            dg2 = db2 = None
+            ready(wp2, bp2)
+        return dx, dg, db, None, None, dx2, dg2, db2, None, None, None, None
+
+
+def batch_norm_add_bn_act(x, weight, bias, running_mean, running_var, x2, weight2, bias2, running_mean2,
+                          running_var2, momentum=0.1, eps=1e-5):
+    """``relu(bn(x) + bn2(x2))`` in training mode; one apply pass when both inputs carry conv
+    epilogue statistics (``_ct_bn_part``), else the two-step form."""
+    if (_BN_ADD_BN_FUSE and _native(x) and x.dim() == 4 and x2.shape == x.shape
+            and getattr(x, "_ct_bn_part", None) is not None and getattr(x2, "_ct_bn_part", None) is not None
+            and x.stride() == x2.stride() and x.numel() % 8 == 0):
+        return _BNAddBNActFn.apply(x, weight, bias, running_mean, running_var, x2, weight2, bias2, running_mean2,
+                                   running_var2, float(momentum), float(eps))
+    idt = batch_norm_act(x2, weight2, bias2, running_mean2, running_var2, relu=False, training=True,
+                         momentum=momentum, eps=eps)
+    return batch_norm_act(x, weight, bias, running_mean, running_var, residual=idt, relu=True, training=True,
+                          momentum=momentum, eps=eps)
+
+
 def _bn_param_grads(wp, bp, gamma, x, stat, dy, y, mode, has_res):
     """BN backward shared by the BN(+ReLU)(+pool) autograd functions: accumulates the affine
     gradients straight into the flat gradient buffer when the parameters live there."""

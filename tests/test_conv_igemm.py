@@ -517,3 +517,55 @@ def test_dgrad_wgather_kernel_matches_index_gather(cuda):
     from cloudtik_amd import ops
     ops.require_native().dgrad_wgather(flat, out, desc)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("follow", [True, False])   # an identity block after it: its conv1 EPI 2 link
+def test_downsample_bn_pair_in_one_apply(cuda, monkeypatch, follow):
+    """ops.functional._BNAddBNActFn: bn3(conv3) + down_bn(down) + ReLU in one apply pass gives
+    the same output (bit-exact) and gradients as the two BatchNorm passes it replaces, with
+    the backward reduction from the next block's conv epilogue or from its own pass."""
+    from cloudtik_amd.models.resnet import Bottleneck
+    from cloudtik_amd.ops import functional as FN
+    torch.manual_seed(8)
+    kw = dict(device=cuda, dtype=torch.bfloat16)
+    mods = [Bottleneck(128, 64, 2, downsample=True, **kw)]
+    if follow:
+        mods.append(Bottleneck(256, 64, 1, downsample=False, **kw))
+    blk = torch.nn.Sequential(*mods).to(memory_format=torch.channels_last)
+    for m in blk.modules():                       # non-trivial affine parameters
+        if hasattr(m, "running_mean"):
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    x0 = _nhwc(torch.randn(4, 128, 18, 18, device=cuda).to(torch.bfloat16))
+    calls = {"n": 0}
+    orig = FN._BNAddBNActFn.apply
+
+    def counted(*a):
+        calls["n"] += 1
+        return orig(*a)
+
+    monkeypatch.setattr(FN._BNAddBNActFn, "apply", counted)
+    state = {k: v.clone() for k, v in blk.state_dict().items()}
+
+    def run(fuse):
+        monkeypatch.setattr(FN, "_BN_ADD_BN_FUSE", fuse)
+        blk.load_state_dict(state)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+        rs = [m.running_mean.clone() for m in blk.modules() if hasattr(m, "running_mean")]
+        return y.detach(), x.grad.float(), [p.grad.float().clone() for p in blk.parameters()], rs
+
+    y1, gx1, gp1, rs1 = run(True)
+    assert calls["n"] == 1
+    y0, gx0, gp0, rs0 = run(False)
+    assert calls["n"] == 1
+    assert torch.equal(y1, y0)
+    for a, b in zip(rs1, rs0):
+        assert torch.equal(a, b)
+    assert _rel(gx1, gx0) < 1e-3
+    for a, b in zip(gp1, gp0):
+        assert _rel(a, b) < 1e-3
