@@ -690,6 +690,44 @@ inline int ew_grid(long work, int ew) {
 
 using namespace ct;
 
+namespace ct {
+// dx = a dm + k x + z and dx2 = a2 dm + k2 x2 + z2 from ONE read of the (already ReLU-masked)
+// gradient dm: the two BatchNorms of a ResNet downsample block's residual sum (bn3, down_bn)
+__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(
+    const bf16_t* __restrict__ dm, const bf16_t* __restrict__ x, const float* __restrict__ ca,
+    const float* __restrict__ c1, const float* __restrict__ c0, const bf16_t* __restrict__ x2,
+    const float* __restrict__ ca2, const float* __restrict__ c12, const float* __restrict__ c02,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dx2, long total_vec, int CV) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const bool fixed = bn_fixed_cv(CV);
+  float aa[8], kk[8], zz[8], a2[8], k2[8], z2[8];
+  if (fixed) {
+    const int cv = threadIdx.x % CV;
+    bn_load8(ca, cv, aa); bn_load8(c1, cv, kk); bn_load8(c0, cv, zz);
+    bn_load8(ca2, cv, a2); bn_load8(c12, cv, k2); bn_load8(c02, cv, z2);
+  }
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < total_vec; v += stride) {
+    const u16x8 g = reinterpret_cast<const u16x8*>(dm)[v];
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[v];
+    const u16x8 x2v = reinterpret_cast<const u16x8*>(x2)[v];
+    if (!fixed) {
+      const int cv = (int)(v % CV);
+      bn_load8(ca, cv, aa); bn_load8(c1, cv, kk); bn_load8(c0, cv, zz);
+      bn_load8(ca2, cv, a2); bn_load8(c12, cv, k2); bn_load8(c02, cv, z2);
+    }
+    u16x8 o, o2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = bf2f(g[j]);
+      o[j] = f2bf(aa[j] * d + kk[j] * bf2f(xv[j]) + zz[j]);
+      o2[j] = f2bf(a2[j] * d + k2[j] * bf2f(x2v[j]) + z2[j]);
+    }
+    reinterpret_cast<u16x8*>(dx)[v] = o;
+    reinterpret_cast<u16x8*>(dx2)[v] = o2;
+  }
+}
+}  // namespace ct
+
 extern "C" int ct_bn_max_blocks() { return 2048; }
 
 // vectors per thread per iteration of the apply kernels (CLOUDTIK_AMD_BN_EW: 1, 2 or 4)
@@ -1008,6 +1046,61 @@ __global__ __launch_bounds__(256) void bn_bwd_partials_sum_kernel(const float* _
 // BatchNorm (+ ReLU) backward whose reduction was done by the producer of dy (conv.hip EPI 2):
 // dym = the already-masked gradient, p1 / p2 = per-tile sums [tiles][C] (p2 = p1 + p2off).
 // work = float[2 * ceil(tiles / 64) * C + 3 * C] scratch.
+// The two BatchNorm backwards of a ResNet downsample block's residual sum relu(bn(x) + bn2(x2)):
+// dym = the masked gradient (the conv epilogue's), p1 / p2 = bn's per-tile sums from that epilogue;
+// bn2's sums come from its own reduction pass over dym and x2; then ONE apply pass writes dx and
+// dx2 (bn_bwd_apply2_kernel).  param_flags as ct_bn_bwd_given (both parameter pairs alike);
+// work = float[2 * ceil(tiles / 64) * C + 3 * C], part2 = float[2 * 2048 * C], coef2 = float[3C].
+extern "C" int ct_bn_bwd_given_pair(const void* dym, const void* x, const void* gamma, const float* stat,
+                                    const float* p1, long p2off, int tiles, const void* x2, const void* gamma2,
+                                    const float* stat2, void* dx, void* dx2, void* dgamma, void* dbeta,
+                                    void* dgamma2, void* dbeta2, int param_flags, float* work, float* part2,
+                                    float* coef2, int M, int C, hipStream_t stream) {
+  if (C % 8 || C / 8 > BN_RT || C > 2048 || M <= 0 || tiles <= 0) return -1;
+  const int G = (tiles + 63) / 64;
+  float* q1 = work;
+  float* q2 = work + (size_t)G * C;
+  float* coef = q2 + (size_t)G * C;
+  int nq = G;
+  if (tiles <= bn_direct_tiles()) {
+    q1 = const_cast<float*>(p1);
+    q2 = const_cast<float*>(p1) + p2off;
+    nq = tiles;
+  } else {
+    bn_bwd_partials_sum_kernel<<<dim3(G, ceil_div(C, 256)), 256, 0, stream>>>(p1, p1 + p2off, tiles, C, q1, q2);
+  }
+  BnLayout L = bn_layout(M, C, bn_target_blocks());
+  const int nblk = bn_nblk(L);
+  const BnMask none{0, nullptr, nullptr, nullptr, nullptr};
+  if (bn_unroll() == 8)
+    bn_bwd_reduce_kernel<8><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dym, none, (const bf16_t*)x2, stat2,
+                                                        stat2 + C, L, part2, part2 + (size_t)2048 * C, nullptr);
+  else
+    bn_bwd_reduce_kernel<4><<<nblk, BN_RT, 0, stream>>>((const bf16_t*)dym, none, (const bf16_t*)x2, stat2,
+                                                        stat2 + C, L, part2, part2 + (size_t)2048 * C, nullptr);
+  const int acc = (param_flags >> 1) & 1;
+  if (param_flags & 1) {
+    bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
+        q1, q2, nq, M, C, (const bf16_t*)gamma, stat, stat + C, (float*)dgamma, (float*)dbeta, coef, coef + C,
+        coef + 2 * C, acc);
+    bn_bwd_finalize_kernel<float><<<ceil_div(C, 64), 1024, 0, stream>>>(
+        part2, part2 + (size_t)2048 * C, nblk, M, C, (const bf16_t*)gamma2, stat2, stat2 + C, (float*)dgamma2,
+        (float*)dbeta2, coef2, coef2 + C, coef2 + 2 * C, acc);
+  } else {
+    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
+        q1, q2, nq, M, C, (const bf16_t*)gamma, stat, stat + C, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C,
+        coef + 2 * C, acc);
+    bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
+        part2, part2 + (size_t)2048 * C, nblk, M, C, (const bf16_t*)gamma2, stat2, stat2 + C, (bf16_t*)dgamma2,
+        (bf16_t*)dbeta2, coef2, coef2 + C, coef2 + 2 * C, acc);
+  }
+  const long tv = (long)M * (C / 8);
+  bn_bwd_apply2_kernel<<<ew_grid(tv, 1), 256, 0, stream>>>((const bf16_t*)dym, (const bf16_t*)x, coef, coef + C,
+                                                           coef + 2 * C, (const bf16_t*)x2, coef2, coef2 + C,
+                                                           coef2 + 2 * C, (bf16_t*)dx, (bf16_t*)dx2, tv, C / 8);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
 extern "C" int ct_bn_bwd_given(const void* dym, const void* x, const void* gamma, const float* stat, void* dx,
                                void* dgamma, void* dbeta, int param_flags, const float* p1, long p2off, int tiles,
                                float* work, int M, int C, hipStream_t stream) {

@@ -52,6 +52,9 @@ int ct_bn_fwd_train_given2(const void*, const void*, const void*, float*, float*
 int ct_maxpool3s2_bwd_bn(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
                          int, hipStream_t);
 long ct_maxpool3s2_bwd_bn_rows(int, int);
+int ct_bn_bwd_given_pair(const void*, const void*, const void*, const float*, const float*, long, int, const void*,
+                         const void*, const float*, void*, void*, void*, void*, void*, void*, int, float*, float*,
+                         float*, int, int, hipStream_t);
 int ct_bn_bwd_given(const void*, const void*, const void*, const float*, void*, void*, void*, int, const float*, long,
                     int, float*, int, int, hipStream_t);
 int ct_bn_bwd(const void*, const void*, const void*, const void*, const float*, void*, void*, void*, void*, int,
@@ -539,6 +542,51 @@ std::vector<at::Tensor> bn_fwd_train_given2(at::Tensor x, at::Tensor gamma, at::
   return {y, mask, stat, stat2};
 }
 
+// backward of bn_fwd_train_given2 with the masked gradient and bn's partials from the consuming
+// conv's epilogue: [dx, dx2, dgamma, dbeta, dgamma2, dbeta2] (accumulated into the *_acc targets,
+// all four or none, when given)
+std::vector<at::Tensor> bn_bwd_given_pair(at::Tensor dym, at::Tensor x, at::Tensor gamma, at::Tensor stat,
+                                          at::Tensor part, int64_t tiles, int64_t rows, at::Tensor x2,
+                                          at::Tensor gamma2, at::Tensor stat2,
+                                          c10::optional<at::Tensor> dgamma_acc, c10::optional<at::Tensor> dbeta_acc,
+                                          c10::optional<at::Tensor> dgamma2_acc,
+                                          c10::optional<at::Tensor> dbeta2_acc) {
+  check_nhwc(x, "x");
+  check_nhwc(x2, "x2");
+  check_nhwc(dym, "dym");
+  const int C = x.size(1);
+  const long M = nhwc_rows(x);
+  TORCH_CHECK(dym.sizes() == x.sizes() && dym.strides() == x.strides() && x2.sizes() == x.sizes() &&
+              x2.strides() == x.strides(), "bn_bwd_given_pair: layouts");
+  TORCH_CHECK(C <= 2048 && stat.numel() == 4 * (long)C && stat2.numel() == 4 * (long)C, "bn_bwd_given_pair: stat");
+  CHECK_F32(stat); CHECK_F32(stat2); CHECK_F32(part);
+  TORCH_CHECK(tiles > 0 && tiles <= rows && part.numel() >= 2 * rows * C, "bn_bwd_given_pair: part buffer");
+  TORCH_CHECK(gamma2.scalar_type() == gamma.scalar_type(), "bn_bwd_given_pair: parameter dtypes");
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined();
+  for (const auto* t : {&dbeta_acc, &dgamma2_acc, &dbeta2_acc})
+    TORCH_CHECK((t->has_value() && (*t)->defined()) == acc, "bn_bwd_given_pair: accumulate targets: all or none");
+  if (acc) {
+    for (const auto* t : {&dgamma_acc, &dbeta_acc, &dgamma2_acc, &dbeta2_acc})
+      TORCH_CHECK((*t)->is_contiguous() && (*t)->numel() == C && (*t)->scalar_type() == gamma.scalar_type(),
+                  "bn_bwd_given_pair: bad accumulate target");
+  }
+  auto dx = at::empty_like(x), dx2 = at::empty_like(x2);
+  auto dg = acc ? *dgamma_acc : at::empty_like(gamma), db = acc ? *dbeta_acc : at::empty_like(gamma);
+  auto dg2 = acc ? *dgamma2_acc : at::empty_like(gamma2), db2 = acc ? *dbeta2_acc : at::empty_like(gamma2);
+  const long G = (tiles + 63) / 64;
+  auto work = at::empty({2 * G * C + 3 * (long)C}, x.options().dtype(at::kFloat));
+  auto part2 = at::empty({2 * 2048 * (long)C}, x.options().dtype(at::kFloat));
+  auto coef2 = at::empty({3 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_bwd_given_pair(dym.data_ptr(), x.data_ptr(), gamma.data_ptr(), stat.data_ptr<float>(),
+                                part.data_ptr<float>(), rows * C, (int)tiles, x2.data_ptr(), gamma2.data_ptr(),
+                                stat2.data_ptr<float>(), dx.data_ptr(), dx2.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                                dg2.data_ptr(), db2.data_ptr(),
+                                (gamma.scalar_type() == at::kFloat ? 1 : 0) | (acc ? 2 : 0), work.data_ptr<float>(),
+                                part2.data_ptr<float>(), coef2.data_ptr<float>(), (int)M, C, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_bwd_given_pair: unsupported C=", C);
+  return {dx, dx2, dg, db, dg2, db2};
+}
+
 // ResNet stem: returns (y_pool [N, C, OH, OW] channels_last, argmax bytes [N, OH, OW, C] uint8, stat)
 std::vector<at::Tensor> bn_fwd_train_pool(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor run_mean,
                                           at::Tensor run_var, double eps, double momentum) {
@@ -707,6 +755,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
   m.def("bn_fwd_train_given2", &bn_fwd_train_given2);
+  m.def("bn_bwd_given_pair", &bn_bwd_given_pair);
   m.def("maxpool3s2_bwd_bn_rows", [](int64_t N, int64_t H) { return (int64_t)ct_maxpool3s2_bwd_bn_rows((int)N, (int)H); });
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

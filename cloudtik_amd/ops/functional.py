@@ -279,6 +279,8 @@ class _BNActFn(torch.autograd.Function):
 
 # BN(x) + BN2(x2) + ReLU in one apply pass when both statistics come from conv epilogues
 _BN_ADD_BN_FUSE = os.environ.get("CLOUDTIK_AMD_BN_ADD_BN_FUSE", "1") == "1"
+# ... and its two BatchNorm backwards with one apply pass over the masked gradient
+_BN_PAIR_BWD = os.environ.get("CLOUDTIK_AMD_BN_PAIR_BWD", "1") == "1"
 
 
 class _BNAddBNActFn(torch.autograd.Function):
@@ -318,6 +320,17 @@ class _BNAddBNActFn(torch.autograd.Function):
         f1, f2 = flat_ok(wp, bp, gamma), flat_ok(wp2, bp2, gamma2)
         given = ctx.bn_link.take(dy)
         dg = db = dg2 = db2 = None
+        if (_BN_PAIR_BWD and given is not None and dy.is_contiguous(memory_format=torch.channels_last)
+                and f1 == f2 and gamma.dtype == gamma2.dtype):
+            # both BatchNorm backwards with ONE apply pass over the masked gradient
+            part, tiles, rows = given
+            acc = [wp.grad, bp.grad, wp2.grad, bp2.grad] if f1 else [None] * 4
+            dx, dx2, dg, db, dg2, db2 = _C().bn_bwd_given_pair(dy, x, gamma, stat, part, tiles, rows, x2, gamma2,
+                                                               stat2, *acc)
+            if f1:
+                ready(wp, bp, wp2, bp2)
+                return dx, None, None, None, None, dx2, None, None, None, None, None, None
+            return dx, dg, db, None, None, dx2, dg2, db2, None, None, None, None
         if given is not None and dy.is_contiguous(memory_format=torch.channels_last):
             part, tiles, rows = given
             dym = dy                                   # already ReLU-masked by the conv epilogue

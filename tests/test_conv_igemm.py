@@ -172,13 +172,18 @@ def test_bn_backward_reduction_in_dgrad_epilogue(cuda, down, stride, bitmask, mo
     x0 = _nhwc(torch.randn(4, cin, 20, 20, device=cuda).to(torch.bfloat16))
     C = ops.require_native()
     calls = {"n": 0}
-    orig = C.bn_bwd_given
+    orig, orig_pair = C.bn_bwd_given, C.bn_bwd_given_pair
 
     def counted(*a):
         calls["n"] += 1
         return orig(*a)
 
+    def counted_pair(*a):                        # a downsample block's bn3 + down_bn, fused
+        calls["n"] += 1
+        return orig_pair(*a)
+
     monkeypatch.setattr(C, "bn_bwd_given", counted)
+    monkeypatch.setattr(C, "bn_bwd_given_pair", counted_pair)
 
     def run(fuse):
         monkeypatch.setattr(CV, "BN_BWD_FUSE", fuse)
