@@ -548,10 +548,15 @@ def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and max(conv.padding) <= 7)
 
 
+_STEM_NHWC8_KERNEL = os.environ.get("CLOUDTIK_AMD_STEM_NHWC8_KERNEL", "1") == "1"
+
+
 def to_nhwc8(x: torch.Tensor) -> torch.Tensor:
     """[N, C<=8, H, W] -> NHWC with the channels zero-padded to 8 (16 bytes per pixel), returned
     as the logical [N, 8, H, W] channels_last view the kernels take."""
     n, c, h, w = x.shape
+    if x.is_cuda and x.dtype == torch.bfloat16 and _STEM_NHWC8_KERNEL:
+        return _C().to_nhwc8(x)                     # one pass (conv.hip to_nhwc8_kernel)
     return F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous().permute(0, 3, 1, 2)
 
 

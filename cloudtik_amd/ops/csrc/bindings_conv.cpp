@@ -19,6 +19,7 @@ void ct_conv_stream_set_cus(int);
 void ct_conv_batch_begin();
 int ct_conv_batch_end(hipStream_t);
 int ct_dgrad_wgather(const void*, void*, const int*, int, hipStream_t);
+int ct_to_nhwc8(const void*, void*, int, int, int, int, long, long, long, long, hipStream_t);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
 int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
                   int, int, hipStream_t);
@@ -178,6 +179,17 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
   m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
   m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
+  m.def("to_nhwc8", [](at::Tensor x) {
+          TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) <= 8,
+                      "to_nhwc8: [N, C <= 8, H, W] bf16 CUDA tensor");
+          const long N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+          auto y = at::empty({N, 8, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+          TORCH_CHECK(ct_to_nhwc8(x.data_ptr(), y.data_ptr(), (int)N, (int)C, (int)H, (int)W, x.stride(0), x.stride(1),
+                                  x.stride(2), x.stride(3), at::hip::getCurrentHIPStream().stream()) == 0,
+                      "to_nhwc8 launch");
+          return y;
+        },
+        "[N, C<=8, H, W] bf16 -> channels_last [N, 8, H, W] zero-padded, one pass");
   m.def("dgrad_wgather", [](at::Tensor src, at::Tensor dst, at::Tensor desc) {
           TORCH_CHECK(src.is_cuda() && dst.is_cuda() && desc.is_cuda(), "dgrad_wgather: CUDA tensors");
           TORCH_CHECK(src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kBFloat16, "dgrad_wgather: bf16");

@@ -1211,6 +1211,33 @@ extern "C" int ct_dgrad_wgather(const void* src, void* dst, const int* desc, int
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
+// ---- stem input: [N, C <= 8, H, W] (NCHW, or any strides) bf16 -> NHWC with the channels
+// zero-padded to 8 (16 bytes per pixel), in one pass: one thread per pixel reads its C values
+// (pixel-contiguous across the wave for NCHW) and writes one 16-B chunk (the pad-then-copy form
+// wrote the 205 MB ResNet-50 batch twice)
+__global__ __launch_bounds__(256) void to_nhwc8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long npix,
+                                                       int C, int H, int W, long sn, long sc, long sh, long sw) {
+  const long p = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const long hw = (long)H * W;
+  const long n = p / hw, r = p - n * hw;
+  const int h = (int)(r / W), w = (int)(r - (long)h * W);
+  const bf16_t* src = x + n * sn + h * sh + w * sw;
+  u16x8 v = u16x8(0);
+  for (int c = 0; c < C; ++c) v[c] = reinterpret_cast<const unsigned short*>(src)[c * sc];
+  reinterpret_cast<u16x8*>(y)[p] = v;
+}
+
+extern "C" int ct_to_nhwc8(const void* x, void* y, int N, int C, int H, int W, long sn, long sc, long sh, long sw,
+                           hipStream_t stream) {
+  if (C < 1 || C > 8) return 1;
+  const long npix = (long)N * H * W;
+  if (npix <= 0) return 0;
+  to_nhwc8_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, npix, C, H, W,
+                                                                      sn, sc, sh, sw);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
 // conv_batch_begin / conv_batch_end (see CvBatch).  A configuration the batch cannot hold (not
 // a one-tile 8-wave 128 x 128 launch, or a second configuration) is launched directly as usual;
 // end returns nonzero if a queued launch failed.

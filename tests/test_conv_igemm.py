@@ -574,3 +574,17 @@ def test_downsample_bn_pair_in_one_apply(cuda, monkeypatch, follow):
     assert _rel(gx1, gx0) < 1e-3
     for a, b in zip(gp1, gp0):
         assert _rel(a, b) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cl", [False, True])
+def test_to_nhwc8_kernel(cuda, cl):
+    """conv.hip to_nhwc8_kernel: [N, 3, H, W] (NCHW or channels_last) -> zero-padded NHWC8 in one
+    pass equals the pad-then-copy form."""
+    x = torch.randn(3, 3, 17, 23, device=cuda).to(torch.bfloat16)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    got = CV.to_nhwc8(x)
+    ref = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 5)).contiguous().permute(0, 3, 1, 2)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, ref)
