@@ -23,6 +23,20 @@ from cloudtik_amd import ops
 from cloudtik_amd.ops import conv as igemm
 from cloudtik_amd.ops.conv1x1 import conv1x1, conv3x3
 
+import os
+
+# the downsample branch's conv on its own stream, concurrent with conv1 -> conv2 -> conv3 of the
+# block (its autograd backward then runs on that stream too, beside the main branch's)
+_DOWN_STREAM = os.environ.get("CLOUDTIK_AMD_RESNET_DOWN_STREAM", "0") == "1"
+_DOWN_STREAMS = {}
+
+
+def _down_stream(device):
+    s = _DOWN_STREAMS.get(device)
+    if s is None:
+        s = _DOWN_STREAMS[device] = torch.cuda.Stream(device=device)
+    return s
+
 
 class BatchNormAct(nn.Module):
     """BatchNorm2d (+ optional residual add) (+ optional ReLU), NHWC, fused on GPU."""
@@ -100,9 +114,24 @@ class Bottleneck(nn.Module):
             # epilogue absorbs that branch's gradient
             st = self.training and not self.bn1.frozen      # BatchNorm statistics from the conv epilogues
             out, x = igemm.conv2d(x, self.conv1, keep_input=True, bn_stats=st)
-            d = igemm.conv2d(x, self.down, bn_stats=st) if self.down is not None else None
+            side = None
+            if self.down is not None and _DOWN_STREAM and x.is_cuda:
+                cur = torch.cuda.current_stream(x.device)
+                side = _down_stream(x.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    d = igemm.conv2d(x, self.down, bn_stats=st)
+                x.record_stream(side)
+            else:
+                d = igemm.conv2d(x, self.down, bn_stats=st) if self.down is not None else None
             out = self.bn2(igemm.conv2d(self.bn1(out), self.conv2, bn_stats=st))
             c3 = igemm.conv2d(out, self.conv3, bn_stats=st)
+            if side is not None:
+                cur.wait_stream(side)
+                d.record_stream(cur)
+                part = getattr(d, "_ct_bn_part", None)
+                if part is not None:
+                    part[0].record_stream(cur)
             b3, bd = self.bn3, getattr(self, "down_bn", None)
             if (d is not None and st and b3.relu and not bd.relu and not bd.frozen
                     and (b3.eps, b3.momentum) == (bd.eps, bd.momentum)):

@@ -588,3 +588,33 @@ def test_to_nhwc8_kernel(cuda, cl):
     ref = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 5)).contiguous().permute(0, 3, 1, 2)
     assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_downsample_branch_on_side_stream(cuda, monkeypatch):
+    """models.resnet: the downsample conv on its own stream (forward, and so its backward)
+    gives the outputs and gradients of the single-stream block."""
+    from cloudtik_amd.models import resnet as RN
+    torch.manual_seed(9)
+    kw = dict(device=cuda, dtype=torch.bfloat16)
+    blk = torch.nn.Sequential(RN.Bottleneck(128, 64, 2, downsample=True, **kw),
+                              RN.Bottleneck(256, 64, 1, downsample=False, **kw)).to(memory_format=torch.channels_last)
+    x0 = _nhwc(torch.randn(4, 128, 18, 18, device=cuda).to(torch.bfloat16))
+    state = {k: v.clone() for k, v in blk.state_dict().items()}
+
+    def run(side):
+        monkeypatch.setattr(RN, "_DOWN_STREAM", side)
+        blk.load_state_dict(state)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = blk(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+        torch.cuda.synchronize()
+        return y.detach(), x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
+
+    y1, gx1, gp1 = run(True)
+    y0, gx0, gp0 = run(False)
+    assert torch.equal(y1, y0)
+    assert _rel(gx1, gx0) < 1e-3
+    for a, b in zip(gp1, gp0):
+        assert _rel(a, b) < 1e-3
