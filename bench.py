@@ -240,6 +240,8 @@ def build_bert(args, rank, world, device, kind):
 
     ops.manual_seed(1234 + rank)
     torch.manual_seed(1234)
+    from cloudtik_amd.ops.linear import prefer_wgrad_stream
+    prefer_wgrad_stream(False)          # GEMM-bound backward: weight gradients in line
     cfg = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "tiny": BertConfig.tiny}[kind]()
     if args.no_dropout:
         cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = 0.0
@@ -291,6 +293,8 @@ def build_resnet(args, rank, world, device, kind):
     from cloudtik_amd.train.optim import FusedSGD, FlatParamSpace
 
     torch.manual_seed(1234)
+    from cloudtik_amd.ops.linear import prefer_wgrad_stream
+    prefer_wgrad_stream(True)           # memory-bound backward: weight gradients beside it
     if args.conv_benchmark:
         torch.backends.cudnn.benchmark = True
     tiny = kind == "tiny"

@@ -27,7 +27,8 @@ _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 # backward pass (filling the CUs the dgrad GEMM's last wave leaves idle).  Consumers of the
 # gradients -- the bucketed all-reduce and the optimizer -- order themselves after this
 # stream via ``grad_stream_event()`` / ``sync_grad_stream()``.
-_WGRAD_STREAM = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM", "1") == "1"
+_WGRAD_STREAM_ENV = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM")
+_WGRAD_STREAM = (_WGRAD_STREAM_ENV or "1") == "1"
 # weight-gradient GEMMs through the MFMA kernel's TN layout (csrc/gemm_nt.hip, ct_gemm_tn2)
 # instead of hipBLASLt's batched split-K GEMM: 13-17 % faster per BERT-large layer
 # (bench/gemm_tn2_probe.py); "blas" restores hipBLASLt
@@ -53,6 +54,17 @@ def grad_stream():
 def set_wgrad_stream(enabled: bool) -> None:
     global _WGRAD_STREAM
     _WGRAD_STREAM = bool(enabled)
+
+
+def prefer_wgrad_stream(enabled: bool) -> bool:
+    """A model's default for the weight-gradient side stream, unless CLOUDTIK_AMD_WGRAD_STREAM
+    pins it.  Worth it where the backward's critical path is memory-bound (ResNet-50: BatchNorm
+    passes; the side stream saves 2.0 ms of 24.0 per step), not where it is two compute-bound
+    GEMM streams competing for the matrix cores (BERT-large: 71.3 ms with it, 70.6 without;
+    profiles/r4/bert_rejected_r4.md).  Returns the setting in force."""
+    if _WGRAD_STREAM_ENV is None:
+        set_wgrad_stream(enabled)
+    return _WGRAD_STREAM
 
 
 def sync_grad_stream() -> None:
