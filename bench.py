@@ -241,7 +241,10 @@ def build_bert(args, rank, world, device, kind):
     ops.manual_seed(1234 + rank)
     torch.manual_seed(1234)
     from cloudtik_amd.ops.linear import prefer_wgrad_stream
-    prefer_wgrad_stream(False)          # GEMM-bound backward: weight gradients in line
+    # GEMM-bound backward: weight gradients in line on one GPU (0.7 ms/step faster); with ranks
+    # the side stream stays (the bucketed all-reduce path it was validated with; a model switching
+    # the policy mid-process under gloo was seen to stall the next model's steps)
+    prefer_wgrad_stream(world > 1)
     cfg = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "tiny": BertConfig.tiny}[kind]()
     if args.no_dropout:
         cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = 0.0
