@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--cfgs", default="-1,1,4,5,7,8,9")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.backends.cudnn.benchmark = False
@@ -84,7 +85,10 @@ def main():
     print("|---|---|---|---:|---:|---:|---:|---:|")
     tot = {"mi_f": 0.0, "ig_f": 0.0, "mi_d": 0.0, "ig_d": 0.0}
     roofs = []
+    want = set(a.shapes.split(",")) if a.shapes else None
     for name, ci, co, H, k, s, calls in SHAPES:
+        if want and name not in want:
+            continue
         errs = check(ci, co, H, k, s, dev)
         pad = k // 2
         x = torch.randn(a.batch, ci, H, H, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
