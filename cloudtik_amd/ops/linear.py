@@ -56,6 +56,10 @@ def set_wgrad_stream(enabled: bool) -> None:
     _WGRAD_STREAM = bool(enabled)
 
 
+def wgrad_stream_enabled() -> bool:
+    return _WGRAD_STREAM
+
+
 def prefer_wgrad_stream(enabled: bool) -> bool:
     """A model's default for the weight-gradient side stream, unless CLOUDTIK_AMD_WGRAD_STREAM
     pins it.  Worth it where the backward's critical path is memory-bound (ResNet-50: BatchNorm

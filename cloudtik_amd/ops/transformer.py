@@ -107,9 +107,23 @@ _STREAM_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _STREAM_SIT
 
 # The same sites through the one-tile MFMA kernel (gemm_nt / gemm_nn: one 256 x 256 tile per
 # workgroup); CLOUDTIK_AMD_ONETILE_GEMM takes the same site list.
-_ONETILE_SITES = os.environ.get("CLOUDTIK_AMD_ONETILE_GEMM", "")
-_ONETILE_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _ONETILE_SITES == "all"
-                  else {t for t in _ONETILE_SITES.split(",") if t})
+_ONETILE_ENV = os.environ.get("CLOUDTIK_AMD_ONETILE_GEMM")
+_ONETILE_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _ONETILE_ENV == "all"
+                  else {t for t in (_ONETILE_ENV or "").split(",") if t})
+# Unless CLOUDTIK_AMD_ONETILE_GEMM says otherwise, the data-gradient sites take the one-tile
+# kernel while the weight gradients run in line (no side stream): BERT-large 73.40 -> 73.16
+# ms/step on one box (3 interleaved rounds; profiles/r4/bert_rejected_r4.md).  Beside the side
+# stream's weight-gradient GEMMs it was 1.6 ms slower, so there hipBLASLt keeps them.
+_ONETILE_INLINE_SITES = {"do", "dx_attn", "dx_ffn"} if _ONETILE_ENV is None else set()
+
+
+def _onetile(site) -> bool:
+    if site in _ONETILE_SITES:
+        return True
+    if site in _ONETILE_INLINE_SITES:
+        from cloudtik_amd.ops.linear import wgrad_stream_enabled
+        return not wgrad_stream_enabled()
+    return False
 
 
 def _stream_mm(site, A, B, b_kn, bias=None, out=None):
@@ -118,7 +132,7 @@ def _stream_mm(site, A, B, b_kn, bias=None, out=None):
     (streamed or one-tile).  None when the site is not routed or the shape is outside the
     kernels' tiling (M, N multiples of 256, K of 64)."""
     stream = site in _STREAM_SITES
-    if not stream and site not in _ONETILE_SITES:
+    if not stream and not _onetile(site):
         return None
     M, K = A.shape
     N = B.shape[1] if b_kn else B.shape[0]
