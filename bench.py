@@ -240,11 +240,8 @@ def build_bert(args, rank, world, device, kind):
 
     ops.manual_seed(1234 + rank)
     torch.manual_seed(1234)
-    from cloudtik_amd.ops.linear import prefer_wgrad_stream
-    # GEMM-bound backward: weight gradients in line on one GPU (0.7 ms/step faster); with ranks
-    # the side stream stays (the bucketed all-reduce path it was validated with; a model switching
-    # the policy mid-process under gloo was seen to stall the next model's steps)
-    prefer_wgrad_stream(world > 1)
+    # weight-gradient routing: the model's own (in line: BertForPreTraining), the same at
+    # every world size
     cfg = {"bert-large": BertConfig.large, "bert-base": BertConfig.base, "tiny": BertConfig.tiny}[kind]()
     if args.no_dropout:
         cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = 0.0
@@ -296,8 +293,8 @@ def build_resnet(args, rank, world, device, kind):
     from cloudtik_amd.train.optim import FusedSGD, FlatParamSpace
 
     torch.manual_seed(1234)
-    from cloudtik_amd.ops.linear import prefer_wgrad_stream
-    prefer_wgrad_stream(True)           # memory-bound backward: weight gradients beside it
+    # weight gradients on the side stream beside the memory-bound backward: the model's own
+    # routing (models/resnet.py)
     if args.conv_benchmark:
         torch.backends.cudnn.benchmark = True
     tiny = kind == "tiny"
@@ -418,6 +415,70 @@ def build_resnet_eager(args, rank, world, device, kind):
     return step, (lambda: None), info
 
 
+# ------------------------------------------------------------------ GPU telemetry
+class GpuTelemetry:
+    """Clock / power / temperature of this rank's GPU (amdgpu sysfs), sampled right before
+    and after a timed region and every ``period`` s inside it by a daemon thread (a sysfs
+    read costs microseconds and never touches the GPU queue).  An MFMA-bound step's speed
+    follows the clock the chip holds under load, so a slow box and a regression can be told
+    apart from the JSON line alone."""
+
+    def __init__(self, device, period=0.25):
+        self.dev_dir = None
+        self.period = period
+        self._samples = []
+        self._stop = None
+        self._thread = None
+        if device.type != "cuda":
+            return
+        try:
+            import torch
+            from cloudtik_amd.core.node.metrics import pci_device_dir
+            p = torch.cuda.get_device_properties(device)
+            self.dev_dir = pci_device_dir(getattr(p, "pci_domain_id", 0), p.pci_bus_id, p.pci_device_id)
+        except Exception:  # noqa: BLE001 - telemetry is informational
+            self.dev_dir = None
+
+    def snapshot(self):
+        if self.dev_dir is None:
+            return {}
+        try:
+            from cloudtik_amd.core.node.metrics import gpu_clock_snapshot
+            return gpu_clock_snapshot(self.dev_dir)
+        except Exception as e:  # noqa: BLE001
+            return {"error": repr(e)[:120]}
+
+    def start(self):
+        import threading
+        self.before = self.snapshot()
+        self._samples = []
+        if self.dev_dir is None:
+            return
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.wait(self.period):
+                self._samples.append(self.snapshot())
+        self._thread = threading.Thread(target=loop, daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=2)
+            self._thread = None
+        out = {"before": self.before, "after": self.snapshot()}
+        during = {}
+        for key in ("sclk_mhz", "mclk_mhz", "power_w", "temp_junction_c", "temp_edge_c", "temp_mem_c"):
+            vals = [s[key] for s in self._samples if isinstance(s.get(key), (int, float))]
+            if vals:
+                during[key] = {"mean": round(sum(vals) / len(vals), 1), "min": min(vals), "max": max(vals)}
+        if during:
+            during["samples"] = len(self._samples)
+            out["during"] = during
+        return out
+
+
 # ------------------------------------------------------------------ timing
 def kernel_audit(step, device):
     """One extra UNTIMED step under torch.profiler: how many GPU kernels ran, and how many of
@@ -483,6 +544,8 @@ def timed(step, args, rank, world, device, audit=False, bucketer=None):
     cuda = device.type == "cuda"
     events = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if cuda else []
     stamps = []
+    tele = GpuTelemetry(device)
+    tele.start()
     t0 = time.perf_counter()
     loss = None
     if cuda:
@@ -499,6 +562,7 @@ def timed(step, args, rank, world, device, audit=False, bucketer=None):
     barrier()
     sync()
     el = time.perf_counter() - t0
+    telemetry = tele.stop()
     if cuda:
         step_ms = [events[i].elapsed_time(events[i + 1]) for i in range(args.steps)]
     else:
@@ -510,10 +574,10 @@ def timed(step, args, rank, world, device, audit=False, bucketer=None):
         out = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(out, t)
         per_rank = [float(o.item()) for o in out]
-    info = {}
+    info = {"gpu_telemetry": telemetry} if telemetry.get("before") or telemetry.get("after") else {}
     if host:
         # a host issue time close to the GPU step time means the step is launch / host bound
-        info = dict(host_issue_ms_mean=round(sum(host) / len(host), 3), host_ms=[round(h, 3) for h in host])
+        info.update(host_issue_ms_mean=round(sum(host) / len(host), 3), host_ms=[round(h, 3) for h in host])
     if dist.is_initialized() and world > 1:
         # every rank's per-step GPU times (the max over ranks is the headline; a straggler
         # rank or step shows up here)
@@ -562,6 +626,7 @@ def run_one(build, args, rank, world, device, kind):
     host_arr = audit.pop("host_ms", None) if audit else None
     info["per_rank_step_ms"] = audit.pop("per_rank_step_ms", None) if audit else None
     info["bucket_timeline"] = audit.pop("bucket_timeline", None) if audit else None
+    info["gpu_telemetry"] = audit.pop("gpu_telemetry", None) if audit else None
     if audit and rank == 0:
         print(f"[bench] {info['model']} kernel audit (one untimed step): {json.dumps(audit)}", file=sys.stderr)
     plan = info.pop("plan", None)
@@ -660,6 +725,7 @@ def main():
                "host_issue_ms_per_step": head.get("host_issue_ms"),
                "step_ms": head["step_ms"], "host_ms": head.get("host_ms"),
                "per_rank_step_ms": head.get("per_rank_step_ms"), "bucket_timeline": head.get("bucket_timeline"),
+               "gpu_telemetry": head.get("gpu_telemetry"),
                "env": {k: envinfo.get(k) for k in ("gpu", "rccl", "nccl_env", "rank0_cpus", "tunableop",
                                                    "distinct_devices", "world_size_seen_by_collective")
                        if envinfo.get(k) is not None},
@@ -686,6 +752,8 @@ def main():
                 out[f"{key}_per_rank_step_ms"] = r["per_rank_step_ms"]
             if r.get("bucket_timeline"):
                 out[f"{key}_bucket_timeline"] = r["bucket_timeline"]
+            if r.get("gpu_telemetry"):
+                out[f"{key}_gpu_telemetry"] = r["gpu_telemetry"]
             if "hip_graph" in r:
                 out[f"{key}_hip_graph"] = r["hip_graph"]
             if r.get("audit"):

@@ -11,12 +11,12 @@ from cloudtik_amd.train.optim import FlatParamSpace
 dev = torch.device("cuda")
 grads = []
 for side in (False, True):
-    L.set_wgrad_stream(side)
     ops.manual_seed(5)
     torch.manual_seed(5)
     cfg = BertConfig.base()
     cfg.hidden_dropout_prob = cfg.attention_probs_dropout_prob = 0.0
     m = BertForPreTraining(cfg, device=dev, dtype=torch.bfloat16)
+    L.use_wgrad_side_stream(m, side)
     named = list(m.named_parameters())
     space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
     batch = synthetic_pretraining_batch(cfg, 32, 128, 20, device=dev, generator=torch.Generator().manual_seed(1))

@@ -117,6 +117,76 @@ def gpu_metrics(root: str = DRM_ROOT) -> List[Dict[str, Any]]:
     return gpus
 
 
+def _dpm_current_mhz(path: str) -> Optional[int]:
+    """The active level of an amdgpu ``pp_dpm_*`` table ("1: 2100Mhz *")."""
+    for line in (_read(path) or "").splitlines():
+        if line.rstrip().endswith("*"):
+            tok = line.split(":", 1)[-1].strip().split()[0].lower()
+            try:
+                return int(float(tok.replace("mhz", "")))
+            except ValueError:
+                return None
+    return None
+
+
+def pci_device_dir(domain: int, bus: int, device: int, root: str = DRM_ROOT) -> Optional[str]:
+    """sysfs directory of the GPU at PCI ``domain:bus:device.0``
+    (``torch.cuda.get_device_properties`` gives the three numbers), or None.  Looked up
+    through the amdgpu DRM cards (a container may not expose /sys/bus/pci); when exactly
+    one AMD card is visible and nothing matches, that card."""
+    want = f"{bus:02x}:{device:02x}.0"
+    d = f"/sys/bus/pci/devices/{domain:04x}:{want}"
+    if os.path.isdir(d):
+        return d
+    cards = amd_gpu_cards(root)
+    for card in cards:
+        dev = os.path.realpath(os.path.join(card, "device"))
+        if os.path.basename(dev).endswith(want):
+            return dev
+    if len(cards) == 1:
+        return os.path.realpath(os.path.join(cards[0], "device"))
+    return None
+
+
+def gpu_clock_snapshot(dev: Optional[str] = None, root: str = DRM_ROOT) -> Dict[str, Any]:
+    """Clock / power / temperature of one GPU right now, from amdgpu sysfs: the state that
+    decides an MFMA-bound benchmark's speed on a given box (the chip lowers its clock under
+    load; MI355X_MICROARCH.md 'DVFS give-back').  ``dev`` is the PCI device directory (default:
+    the first AMD card).  Keys absent when the driver does not expose them."""
+    if dev is None:
+        cards = amd_gpu_cards(root)
+        if not cards:
+            return {}
+        dev = os.path.realpath(os.path.join(cards[0], "device"))
+    out: Dict[str, Any] = {"pci": os.path.basename(os.path.realpath(dev))}
+    s = _dpm_current_mhz(os.path.join(dev, "pp_dpm_sclk"))
+    m = _dpm_current_mhz(os.path.join(dev, "pp_dpm_mclk"))
+    if s is not None:
+        out["sclk_mhz"] = s
+    if m is not None:
+        out["mclk_mhz"] = m
+    hw = sorted(glob.glob(os.path.join(dev, "hwmon", "hwmon*")))
+    if hw:
+        h = hw[0]
+        pw = _read_int(os.path.join(h, "power1_average")) or _read_int(os.path.join(h, "power1_input"))
+        if pw is not None:
+            out["power_w"] = round(pw / 1e6, 1)
+        cap = _read_int(os.path.join(h, "power1_cap"))
+        if cap:
+            out["power_cap_w"] = round(cap / 1e6, 1)
+        for f in sorted(glob.glob(os.path.join(h, "freq*_input"))):
+            lab = (_read(f.replace("_input", "_label")) or os.path.basename(f)[:-6]).lower()
+            v = _read_int(f)
+            if v is not None:
+                out[f"{lab}_mhz"] = int(v / 1e6)
+        for f in sorted(glob.glob(os.path.join(h, "temp*_input"))):
+            lab = (_read(f.replace("_input", "_label")) or os.path.basename(f)[:-6]).lower()
+            v = _read_int(f)
+            if v is not None:
+                out[f"temp_{lab}_c"] = v / 1000.0
+    return out
+
+
 class NodeMetricsCollector:
     def __init__(self, drm_root: str = DRM_ROOT):
         self.drm_root = drm_root

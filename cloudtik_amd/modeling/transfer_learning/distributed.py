@@ -31,11 +31,48 @@ from typing import Any, Dict, Optional
 SPEC = "job.json"
 
 
+_LOCAL_HOSTS = {"localhost", "127.0.0.1", "::1"}
+
+
+def _host_names(hosts: Optional[str], hostfile: Optional[str]):
+    names = []
+    for item in (hosts or "").split(","):
+        h = item.strip().split(":")[0]
+        if h:
+            names.append(h)
+    if hostfile:
+        with open(hostfile) as f:
+            for line in f:
+                line = line.split("#", 1)[0].strip()
+                if line:
+                    names.append(line.split()[0].split(":")[0])
+    return names
+
+
+def spans_hosts(nnodes: int, hosts: Optional[str], hostfile: Optional[str]) -> bool:
+    """Whether a launch would put ranks on more than this host."""
+    import socket
+    if nnodes > 1:
+        return True
+    local = _LOCAL_HOSTS | {socket.gethostname(), socket.getfqdn()}
+    names = set(_host_names(hosts, hostfile))
+    return bool(names - local) or len(names) > 1
+
+
 def fit_distributed(model, dataset, train_kwargs: Dict[str, Any], nnodes: int = 1, nproc_per_node: int = 1,
                     hosts: Optional[str] = None, hostfile: Optional[str] = None, shared_dir: Optional[str] = None,
                     launcher: Optional[str] = None, master_port: int = 29500, env: Optional[dict] = None):
+    """Train ``model`` on ``dataset`` over ranks started by ``run_command``.  The job directory
+    (model export, ``datasets.pkl``, the trained model and history written by rank 0) must be
+    readable by every rank: a job that spans hosts needs ``shared_dir`` on a filesystem all of
+    them mount.  ``datasets.pkl`` is a cloudpickle that every rank LOADS (executes): keep
+    ``shared_dir`` writable only by trusted users."""
     import cloudpickle
     from cloudtik_amd.runner import run_command
+    if shared_dir is None and spans_hosts(nnodes, hosts, hostfile):
+        raise ValueError("a distributed job that spans hosts needs shared_dir= (a directory every host mounts): "
+                         "the ranks on other hosts read the job files from it and rank 0 writes the trained "
+                         "model there")
     root = shared_dir or tempfile.mkdtemp(prefix="cloudtik-tl-")
     job = os.path.join(root, f"tl_job_{time.strftime('%Y%m%d-%H%M%S')}_{os.getpid()}")
     os.makedirs(job)

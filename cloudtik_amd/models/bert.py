@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from cloudtik_amd.ops.linear import use_wgrad_side_stream
 from cloudtik_amd import ops
 
 
@@ -184,6 +185,9 @@ class BertForPreTraining(nn.Module):
         self.mlm_decoder_bias = _param(cfg.padded_vocab, fill=0.0, **kw)
         self.nsp_weight = _param(2, H, std=std, **kw)
         self.nsp_bias = _param(2, fill=0.0, **kw)
+        # GEMM-bound backward: weight gradients in line, not on the side stream (the model's
+        # own routing, the same at every world size; ops/linear.py use_wgrad_side_stream)
+        use_wgrad_side_stream(self, False)
 
     def mlm_loss(self, seq, masked_lm_positions=None, masked_lm_ids=None, masked_lm_labels=None):
         cfg = self.cfg

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from cloudtik_amd.ops.linear import use_wgrad_side_stream
 from cloudtik_amd import ops
 from cloudtik_amd.ops import conv as igemm
 from cloudtik_amd.ops.conv1x1 import conv1x1, conv3x3
@@ -133,8 +134,8 @@ class Bottleneck(nn.Module):
                 if part is not None:
                     part[0].record_stream(cur)
             b3, bd = self.bn3, getattr(self, "down_bn", None)
-            if (d is not None and st and b3.relu and not bd.relu and not bd.frozen
-                    and (b3.eps, b3.momentum) == (bd.eps, bd.momentum)):
+            if (d is not None and st and b3.relu and not bd.relu and not bd.frozen and not b3.frozen
+                    and b3.momentum is not None and (b3.eps, b3.momentum) == (bd.eps, bd.momentum)):
                 # bn3(conv3) + down_bn(down) + ReLU in one apply pass: the downsample branch's
                 # BatchNorm output is never written (ops.functional._BNAddBNActFn)
                 return ops.batch_norm_add_bn_act(c3, b3.weight, b3.bias, b3.running_mean, b3.running_var,
@@ -181,6 +182,9 @@ class ResNet(nn.Module):
         self.fc = fc.to(dtype)
         if device is not None and torch.device(device).type == "cuda":
             self.to(memory_format=torch.channels_last)
+        # memory-bound backward (BatchNorm passes): weight gradients on the side stream beside
+        # it (ops/linear.py use_wgrad_side_stream)
+        use_wgrad_side_stream(self, True)
 
     def stem(self, x):
         y = igemm.stem_conv(x, self.conv1)

@@ -168,9 +168,13 @@ class _DgradWeights:
         rows = []
         for key in keys:
             soff, (co, ci, R, S), rs = key
-            if co % 64 or ci % 64 or co // 64 > 255 or ci // 64 > 255:
+            # T | a << 16 | b << 24 must stay a non-negative int32 (b < 128), and the kernel
+            # moves 16-B pieces: both offsets must be multiples of 8 elements
+            if co % 64 or ci % 64 or co // 64 > 255 or ci // 64 > 127:
                 return None
             doff = slices[key][0]
+            if soff % 8 or doff % 8:
+                return None
             taps = [(r, q) for r in range(R) for q in range(S)] if len(rs) == R * S else list(rs)
             T = len(taps)
             for t, (r, q) in enumerate(taps):
@@ -461,9 +465,9 @@ def _weight_grad(wp, dy, x, w_shape, stride, padding):
     side stream (returns None: autograd never sees it, the data-parallel bucketer is told through
     ``_ct_grad_ready``); otherwise it is returned for AccumulateGrad."""
     from cloudtik_amd.ops.conv1x1 import _SIDE_WGRAD, _flat_target
-    from cloudtik_amd.ops.linear import side_grad_stream
+    from cloudtik_amd.ops.linear import side_grad_stream, wgrad_side
     target = _flat_target(wp) if _SIDE_WGRAD else None
-    side = side_grad_stream() if target is not None else None
+    side = side_grad_stream() if (target is not None and wgrad_side(wp)) else None
     if target is None or not target.is_contiguous(memory_format=torch.channels_last) or target.dtype != dy.dtype:
         return conv_wgrad(dy, x, w_shape, stride, padding)
     if side is None:
@@ -555,7 +559,9 @@ def to_nhwc8(x: torch.Tensor) -> torch.Tensor:
     """[N, C<=8, H, W] -> NHWC with the channels zero-padded to 8 (16 bytes per pixel), returned
     as the logical [N, 8, H, W] channels_last view the kernels take."""
     n, c, h, w = x.shape
-    if x.is_cuda and x.dtype == torch.bfloat16 and _STEM_NHWC8_KERNEL:
+    # the kernel is not differentiable: an input that needs a gradient takes the autograd path
+    if (x.is_cuda and x.dtype == torch.bfloat16 and _STEM_NHWC8_KERNEL
+            and not (x.requires_grad and torch.is_grad_enabled())):
         return _C().to_nhwc8(x)                     # one pass (conv.hip to_nhwc8_kernel)
     return F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous().permute(0, 3, 1, 2)
 

@@ -73,8 +73,8 @@ def _weight_grad(wp, dy, x, w, pad):
     stream is on, it is computed there and added into the buffer (returns None: autograd
     never sees it, so the data-parallel bucketer is told via ``_ct_grad_ready``); otherwise
     it is returned for AccumulateGrad."""
-    from cloudtik_amd.ops.linear import side_grad_stream
-    target = _flat_target(wp) if _SIDE_WGRAD else None
+    from cloudtik_amd.ops.linear import side_grad_stream, wgrad_side
+    target = _flat_target(wp) if (_SIDE_WGRAD and wgrad_side(wp)) else None
     side = side_grad_stream() if target is not None else None
     if side is None:
         return _conv_bwd(dy, x, w, [False, True, False], pad)[1]

@@ -26,9 +26,14 @@ _SPLITK_MAX = int(os.environ.get("CLOUDTIK_AMD_WGRAD_SPLITK", "8"))
 # slices of the flat gradient buffer, so they can run concurrently with the dgrad chain of the
 # backward pass (filling the CUs the dgrad GEMM's last wave leaves idle).  Consumers of the
 # gradients -- the bucketed all-reduce and the optimizer -- order themselves after this
-# stream via ``grad_stream_event()`` / ``sync_grad_stream()``.
+# stream via ``sync_grad_stream()``.
+#
+# The choice is a property of each weight (``param._ct_wgrad_side``, set per model by
+# ``use_wgrad_side_stream``), read by the backward that produces its gradient: two models in
+# one process keep their own routing, and nothing a model builder does changes another
+# model's backward.  CLOUDTIK_AMD_WGRAD_STREAM (0 / 1) pins it for every model.
 _WGRAD_STREAM_ENV = os.environ.get("CLOUDTIK_AMD_WGRAD_STREAM")
-_WGRAD_STREAM = (_WGRAD_STREAM_ENV or "1") == "1"
+_DEFAULT_SIDE = (_WGRAD_STREAM_ENV or "1") == "1"
 # weight-gradient GEMMs through the MFMA kernel's TN layout (csrc/gemm_nt.hip, ct_gemm_tn2)
 # instead of hipBLASLt's batched split-K GEMM: 13-17 % faster per BERT-large layer
 # (bench/gemm_tn2_probe.py); "blas" restores hipBLASLt
@@ -41,8 +46,9 @@ _streams = {}
 
 
 def grad_stream():
-    """The side stream used for weight-gradient GEMMs on the current device (or None)."""
-    if not _WGRAD_STREAM or not torch.cuda.is_available():
+    """The side stream used for weight-gradient GEMMs on the current device (or None
+    without a GPU).  Created on first use; cached per device."""
+    if not torch.cuda.is_available():
         return None
     dev = torch.cuda.current_device()
     s = _streams.get(dev)
@@ -51,24 +57,25 @@ def grad_stream():
     return s
 
 
-def set_wgrad_stream(enabled: bool) -> None:
-    global _WGRAD_STREAM
-    _WGRAD_STREAM = bool(enabled)
+def use_wgrad_side_stream(params, enabled: Optional[bool]) -> bool:
+    """A model's weight-gradient routing: ``params`` (an ``nn.Module`` or an iterable of
+    parameters) get their gradients on the side stream when ``enabled`` (None: the process
+    default), unless CLOUDTIK_AMD_WGRAD_STREAM pins it.  Worth it where the backward's
+    critical path is memory-bound (ResNet-50: BatchNorm passes; the side stream saves 2.0 ms
+    of 24.0 per step), not where it is two compute-bound GEMM streams competing for the
+    matrix cores (BERT-large: 71.3 ms with it, 70.6 without; profiles/r4/bert_rejected_r4.md).
+    Returns the setting in force."""
+    val = _DEFAULT_SIDE if (_WGRAD_STREAM_ENV is not None or enabled is None) else bool(enabled)
+    it = params.parameters() if hasattr(params, "parameters") else params
+    for p in it:
+        p._ct_wgrad_side = val
+    return val
 
 
-def wgrad_stream_enabled() -> bool:
-    return _WGRAD_STREAM
-
-
-def prefer_wgrad_stream(enabled: bool) -> bool:
-    """A model's default for the weight-gradient side stream, unless CLOUDTIK_AMD_WGRAD_STREAM
-    pins it.  Worth it where the backward's critical path is memory-bound (ResNet-50: BatchNorm
-    passes; the side stream saves 2.0 ms of 24.0 per step), not where it is two compute-bound
-    GEMM streams competing for the matrix cores (BERT-large: 71.3 ms with it, 70.6 without;
-    profiles/r4/bert_rejected_r4.md).  Returns the setting in force."""
-    if _WGRAD_STREAM_ENV is None:
-        set_wgrad_stream(enabled)
-    return _WGRAD_STREAM
+def wgrad_side(p) -> bool:
+    """Whether parameter ``p``'s weight gradient goes to the side stream."""
+    v = getattr(p, "_ct_wgrad_side", None)
+    return _DEFAULT_SIDE if v is None else bool(v)
 
 
 def sync_grad_stream() -> None:
@@ -109,10 +116,10 @@ def side_grad_stream():
 
 
 def wgrad_on_side_stream(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
-                         dbias: Optional[torch.Tensor] = None) -> bool:
+                         dbias: Optional[torch.Tensor] = None, enabled: bool = True) -> bool:
     """Issue ``g += dy2^T x2`` (and ``dbias += column sums of dy2``) on the gradient side
-    stream; False if disabled."""
-    s = side_grad_stream() if g.is_cuda else None
+    stream; False (nothing issued) when ``enabled`` is False or there is no GPU."""
+    s = side_grad_stream() if (g.is_cuda and enabled) else None
     if s is None:
         return False
     cur = torch.cuda.current_stream()
@@ -241,7 +248,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             g = Wp.grad
             if g is not None and getattr(Wp, "_ct_flat_grad", False) and g.dtype == dy.dtype:
-                if not wgrad_on_side_stream(g, dy2, x2):
+                if not wgrad_on_side_stream(g, dy2, x2, enabled=wgrad_side(Wp)):
                     wgrad_accumulate(g, dy2, x2)
                 cb = getattr(Wp, "_ct_grad_ready", None)
                 if cb is not None:

@@ -25,7 +25,7 @@ import os
 
 import torch
 
-from cloudtik_amd.ops.linear import wgrad_accumulate, wgrad_on_side_stream
+from cloudtik_amd.ops.linear import wgrad_accumulate, wgrad_on_side_stream, wgrad_side
 
 
 def _C():
@@ -117,22 +117,21 @@ _ONETILE_SITES = ({"qkv", "wo", "ffn2", "do", "dx_attn", "dx_ffn"} if _ONETILE_E
 _ONETILE_INLINE_SITES = {"do", "dx_attn", "dx_ffn"} if _ONETILE_ENV is None else set()
 
 
-def _onetile(site) -> bool:
+def _onetile(site, side: bool) -> bool:
+    """``side``: whether this layer's weight gradients run on the side stream (the weight's
+    own routing, ops.linear.wgrad_side)."""
     if site in _ONETILE_SITES:
         return True
-    if site in _ONETILE_INLINE_SITES:
-        from cloudtik_amd.ops.linear import wgrad_stream_enabled
-        return not wgrad_stream_enabled()
-    return False
+    return site in _ONETILE_INLINE_SITES and not side
 
 
-def _stream_mm(site, A, B, b_kn, bias=None, out=None):
+def _stream_mm(site, A, B, b_kn, bias=None, out=None, side=True):
     """A [M,K] . B^T (b_kn False: B [N,K]) or A . B (b_kn True: B [K,N]) [+ bias], or
     ``out += A . B`` when ``out`` is given, on the in-tree MFMA kernel the site is routed to
     (streamed or one-tile).  None when the site is not routed or the shape is outside the
     kernels' tiling (M, N multiples of 256, K of 64)."""
     stream = site in _STREAM_SITES
-    if not stream and not _onetile(site):
+    if not stream and not _onetile(site, side):
         return None
     M, K = A.shape
     N = B.shape[1] if b_kn else B.shape[0]
@@ -168,7 +167,7 @@ def _wgrad(p, dy2, x2, bias=None):
     parameter), its gradient -- the column sums of dy2 -- comes out of the same GEMM."""
     if _flat(p):
         db = bias.grad if bias is not None else None
-        if not wgrad_on_side_stream(p.grad, dy2, x2, db):
+        if not wgrad_on_side_stream(p.grad, dy2, x2, db, enabled=wgrad_side(p)):
             wgrad_accumulate(p.grad, dy2, x2, db)
         _ready(p)
         if bias is not None:
@@ -232,7 +231,7 @@ class _AttnBlockFn(torch.autograd.Function):
         _ready(*[p for p, f in ((g1, fg1), (b1, fb1), (bo, fbo)) if f])
         o2 = o.view(B * S, H)
         dWo = _wgrad(Wo, da, o2)
-        do = _stream_mm("do", da, Wo, True)
+        do = _stream_mm("do", da, Wo, True, side=wgrad_side(Wo))
         if do is None:
             do = torch.mm(da, Wo)
         do = do.view(B, S, nh, D)
@@ -249,7 +248,7 @@ class _AttnBlockFn(torch.autograd.Function):
             if fbq:
                 _ready(bqkv)
             dWqkv = _wgrad(Wqkv, dqkv, x2)
-        dx = _stream_mm("dx_attn", dqkv, Wqkv, True, out=ds)
+        dx = _stream_mm("dx_attn", dqkv, Wqkv, True, out=ds, side=wgrad_side(Wqkv))
         if dx is None:
             dx = ds.addmm_(dqkv, Wqkv)    # residual grad fused: in-place beta=1 epilogue, no C copy
         return (dx.view(B, S, H), dWqkv, None if fbq else dbq, dWo, None if fbo else dbo,
@@ -304,7 +303,7 @@ class _FFNBlockFn(torch.autograd.Function):
         if fb1f:
             _ready(b1f)
         dW1 = _wgrad(W1, dz, x2)
-        dx = _stream_mm("dx_ffn", dz, W1, True, out=ds)
+        dx = _stream_mm("dx_ffn", dz, W1, True, out=ds, side=wgrad_side(W1))
         if dx is None:
             dx = ds.addmm_(dz, W1)
         return (dx.view(B, S, H), dW1, None if fb1f else db1f, dW2, None if fb2f else db2f,

@@ -95,6 +95,7 @@ class GradBucketer:
         self._reported = set()
         self._works = []
         self._enabled = True
+        self._side = None
         self._hooks = []
         # bucket timeline (CUDA, opt-in per step): an event where each bucket's collective is
         # issued and one where backward ended (finish() entry) -> launch times relative to it
@@ -161,10 +162,18 @@ class GradBucketer:
             self._launch(self._next)
             self._next += 1
 
+    def _uses_side_stream(self) -> bool:
+        """Whether any weight of this space gets its gradient on the side stream (the
+        model's routing, ops.linear.use_wgrad_side_stream)."""
+        if self._side is None:
+            from cloudtik_amd.ops.linear import wgrad_side
+            self._side = self.space.grad.is_cuda and any(wgrad_side(p) for p in self.space.params)
+        return self._side
+
     def _launch(self, b):
         from cloudtik_amd.ops.linear import grad_stream
         self.space.flush_grads()            # deferred conv-weight grads -> flat buffer
-        side = grad_stream()
+        side = grad_stream() if self._uses_side_stream() else None
         if self.p2p is not None and self._p2p_fits(b):
             # the one-shot kernel spins until the slowest rank reaches this bucket: give it
             # its own stream so weight-gradient GEMMs queued on the side stream (and the

@@ -155,7 +155,13 @@ class KafkaRuntime(ConfiguredRuntime):
 
 # ----------------------------------------------------------------------------- Redis
 class RedisRuntime(ConfiguredRuntime):
+    """``cluster_mode``: ``replication`` (workers replicate the head; with ``sentinel.enabled``
+    a sentinel on every node fails the master over) or ``sharding`` (a Redis Cluster: the head
+    bootstraps the slots, every worker meets it and takes a master share or a replica role --
+    runtime/redis_cluster.py)."""
     spec = SPEC_BY_NAME["redis"]
+    members_env = "REDIS_MEMBERS"
+    quorum_members = False
 
     def files(self, c):
         cfg = c["cfg"]
@@ -169,32 +175,109 @@ class RedisRuntime(ConfiguredRuntime):
             lines.append(f"replicaof {c['head_ip']} {port}")
         elif mode == "sharding":
             lines += ["cluster-enabled yes", f"cluster-config-file {os.path.join(c['dir'], 'data', 'nodes.conf')}",
-                      "cluster-node-timeout 5000"]
+                      "cluster-node-timeout 5000", f"cluster-announce-ip {c['ip']}"]
         lines += [f"{k} {v}" for k, v in _extra(cfg).items()]
-        return {os.path.join(c["dir"], "redis.conf"): "\n".join(lines) + "\n"}
+        out = {os.path.join(c["dir"], "redis.conf"): "\n".join(lines) + "\n"}
+        if mode == "replication" and (cfg.get("sentinel") or {}).get("enabled"):
+            from cloudtik_amd.runtime.replication import redis_sentinel_conf
+            out[os.path.join(c["dir"], "sentinel.conf")] = redis_sentinel_conf(c)
+        return out
 
     def configure_steps(self, head):
         return [f"mkdir -p $RUNTIME_PATH/redis/data $RUNTIME_PATH/redis/logs"]
 
+    def start_steps(self, head):
+        import sys
+        c = self.ctx(head, self.node_env(head))
+        cfg = c["cfg"]
+        mode = cfg.get("cluster_mode", "none")
+        port = int(cfg.get("port", 6379))
+        steps = super().start_steps(head)
+        if mode == "replication" and (cfg.get("sentinel") or {}).get("enabled"):
+            steps.append(f"redis-sentinel {c['dir']}/sentinel.conf --daemonize yes")
+        elif mode == "sharding":
+            seeds = [c["head_ip"]] + [ip for _, ip in c["members"] if ip != c["ip"]]
+            steps.append(f"{sys.executable} -m cloudtik_amd.runtime.redis_cluster join --node-ip {c['ip']} "
+                         f"--port {port} --seeds {','.join(seeds)}"
+                         f" --replicas-per-master {int((cfg.get('sharding') or {}).get('replicas_per_master', 0))}"
+                         f" --marker {c['dir']}/data/.cluster-initialized" + (" --head" if head else ""))
+        return steps
+
+    def stop_steps(self, head):
+        steps = super().stop_steps(head)
+        if (self.runtime_config or {}).get("cluster_mode") == "replication" and \
+                ((self.runtime_config or {}).get("sentinel") or {}).get("enabled"):
+            sp = int(((self.runtime_config or {}).get("sentinel") or {}).get("port", 26379))
+            steps.append(f"redis-cli -p {sp} shutdown || true")
+        return steps
+
 
 # ----------------------------------------------------------------------------- MongoDB
 class MongoDBRuntime(ConfiguredRuntime):
+    """``cluster_mode``: ``replication`` (one replica set: the head initiates it, workers are
+    added from the primary) or ``sharding`` (config-server replica set + mongos router on the
+    head, the workers grouped into shard replica sets of ``shard_size`` members;
+    runtime/replication.py)."""
     spec = SPEC_BY_NAME["mongodb"]
+    members_env = "MONGODB_MEMBERS"
+    quorum_members = False
+
+    @staticmethod
+    def _mongod(c, port, db, log, extra=None):
+        conf = {"storage": {"dbPath": os.path.join(c["dir"], db)},
+                "net": {"port": port, "bindIp": "0.0.0.0"},
+                "systemLog": {"destination": "file", "path": os.path.join(c["dir"], "logs", log), "logAppend": True},
+                "processManagement": {"fork": True}}
+        conf.update(extra or {})
+        return conf
 
     def files(self, c):
-        cfg = c["cfg"]
-        conf = {"storage": {"dbPath": os.path.join(c["dir"], "data")},
-                "net": {"port": int(cfg.get("port", 27017)), "bindIp": "0.0.0.0"},
-                "systemLog": {"destination": "file", "path": os.path.join(c["dir"], "logs", "mongod.log"),
-                              "logAppend": True},
-                "processManagement": {"fork": True}}
-        if cfg.get("cluster_mode", "none") == "replication":
-            conf["replication"] = {"replSetName": cfg.get("replication_set_name") or f"{c['cluster']}-rs"}
         import yaml
+        cfg = c["cfg"]
+        mode = cfg.get("cluster_mode", "none")
+        port = int(cfg.get("port", 27017))
+        if mode == "sharding":
+            cfg_port = int(cfg.get("config_server_port", 27019))
+            shard_port = int(cfg.get("shard_server_port", 27018))
+            if c["head"]:
+                cfg_rs = f"{c['cluster']}-cfg"
+                cs = self._mongod(c, cfg_port, "data-cfg", "mongod-cfg.log",
+                                  {"replication": {"replSetName": cfg_rs}, "sharding": {"clusterRole": "configsvr"}})
+                mongos = {"net": {"port": port, "bindIp": "0.0.0.0"},
+                          "systemLog": {"destination": "file", "path": os.path.join(c["dir"], "logs", "mongos.log"),
+                                        "logAppend": True},
+                          "processManagement": {"fork": True},
+                          "sharding": {"configDB": f"{cfg_rs}/{c['head_ip']}:{cfg_port}"}}
+                return {os.path.join(c["dir"], "mongod-cfg.conf"): yaml.safe_dump(cs, sort_keys=False),
+                        os.path.join(c["dir"], "mongos.conf"): yaml.safe_dump(mongos, sort_keys=False)}
+            from cloudtik_amd.runtime.replication import mongo_shard_layout
+            layout = mongo_shard_layout(c["members"], cfg.get("shard_size", 1), c["cluster"])
+            rs = next((s["name"] for s in layout if c["ip"] in s["members"]), f"{c['cluster']}-shard0")
+            conf = self._mongod(c, shard_port, "data", "mongod.log",
+                                {"replication": {"replSetName": rs}, "sharding": {"clusterRole": "shardsvr"}})
+            return {os.path.join(c["dir"], "mongod.conf"): yaml.safe_dump(conf, sort_keys=False)}
+        conf = self._mongod(c, port, "data", "mongod.log")
+        if mode == "replication":
+            conf["replication"] = {"replSetName": cfg.get("replication_set_name") or f"{c['cluster']}-rs"}
         return {os.path.join(c["dir"], "mongod.conf"): yaml.safe_dump(conf, sort_keys=False)}
 
     def configure_steps(self, head):
-        return ["mkdir -p $RUNTIME_PATH/mongodb/data $RUNTIME_PATH/mongodb/logs"]
+        return ["mkdir -p $RUNTIME_PATH/mongodb/data $RUNTIME_PATH/mongodb/data-cfg $RUNTIME_PATH/mongodb/logs"]
+
+    def start_steps(self, head):
+        from cloudtik_amd.runtime.replication import mongodb_bootstrap_steps
+        c = self.ctx(head, self.node_env(head))
+        if c["cfg"].get("cluster_mode", "none") == "sharding" and head:
+            steps = [f"mongod --fork --config {c['dir']}/mongod-cfg.conf"]
+        else:
+            steps = super().start_steps(head)
+        return steps + mongodb_bootstrap_steps(c)
+
+    def stop_steps(self, head):
+        if head and (self.runtime_config or {}).get("cluster_mode") == "sharding":
+            return ["pkill -f 'mongos --config' || true",
+                    "mongod --shutdown --dbpath $RUNTIME_PATH/mongodb/data-cfg || true"]
+        return super().stop_steps(head)
 
 
 # ----------------------------------------------------------------------------- Consul
@@ -251,17 +334,27 @@ class CoreDNSRuntime(ConfiguredRuntime):
 
 # ----------------------------------------------------------------------------- MySQL / PostgreSQL
 class MySQLRuntime(ConfiguredRuntime):
+    """``cluster_mode``: ``replication`` (GTID source on the head, every worker a replica of
+    it) or ``group_replication`` (single- or multi-primary group bootstrapped by the head);
+    runtime/replication.py issues the replication statements after the server is up."""
     spec = SPEC_BY_NAME["mysql"]
+    members_env = "MYSQL_MEMBERS"
+    quorum_members = False
 
     def files(self, c):
         cfg = c["cfg"]
+        mode = cfg.get("cluster_mode", "none")
+        port = int(cfg.get("port", 3306))
         lines = ["[mysqld]", f"server-id = {c['seq']}", "bind-address = 0.0.0.0",
-                 f"port = {int(cfg.get('port', 3306))}", "max_connections = 1000"]
-        if cfg.get("cluster_mode", "none") in ("replication", "group_replication"):
+                 f"port = {port}", "max_connections = 1000", f"report_host = {c['ip']}"]
+        if mode in ("replication", "group_replication"):
             lines += ["log_bin = mysql-bin", "binlog_format = ROW", "gtid_mode = ON",
                       "enforce_gtid_consistency = ON", "log_replica_updates = ON"]
-            if not c["head"]:
-                lines.append("read_only = ON")
+            if mode == "replication" and not c["head"]:
+                lines += ["read_only = ON", "super_read_only = ON", "skip_replica_start = OFF"]
+            if mode == "group_replication":
+                from cloudtik_amd.runtime.replication import mysql_group_conf
+                lines += mysql_group_conf(c, port)
         return {os.path.join(c["dir"], "conf.d", "cloudtik.cnf"): "\n".join(lines) + "\n"}
 
     def configure_steps(self, head):
@@ -270,17 +363,42 @@ class MySQLRuntime(ConfiguredRuntime):
                 "[ -d /etc/mysql/mysql.conf.d ] && sudo cp $RUNTIME_PATH/mysql/conf.d/cloudtik.cnf "
                 "/etc/mysql/mysql.conf.d/zz-cloudtik.cnf || true"]
 
+    def _clustered(self) -> bool:
+        return (self.runtime_config or {}).get("cluster_mode", "none") in ("replication", "group_replication")
+
+    def start_steps(self, head):
+        from cloudtik_amd.runtime.replication import mysql_bootstrap_steps
+        if not head and not self._clustered():
+            return []
+        c = self.ctx(head, self.node_env(head))
+        return ["sudo service mysql start"] + mysql_bootstrap_steps(c)
+
+    def stop_steps(self, head):
+        return ["sudo service mysql stop"] if (head or self._clustered()) else []
+
 
 class PostgresRuntime(ConfiguredRuntime):
+    """``cluster_mode: replication``: streaming replication from the head; a worker's data
+    directory is replaced by a base backup of the primary before its server starts (so it comes
+    up as a hot standby, not a second primary); with ``repmgr.enabled`` the nodes register with
+    repmgr and ``repmgrd`` promotes a standby when the primary fails (runtime/replication.py)."""
     spec = SPEC_BY_NAME["postgres"]
 
+    def _data_dir(self, cfg):
+        return cfg.get("data_dir") or f"/var/lib/postgresql/{self.spec.version}/main"
+
     def files(self, c):
+        from cloudtik_amd.runtime.replication import postgres_repmgr_enabled, repmgr_conf
         cfg = c["cfg"]
         repl = cfg.get("cluster_mode", "none") == "replication"
+        repmgr = postgres_repmgr_enabled(cfg)
         conf = [f"listen_addresses = '*'", f"port = {int(cfg.get('port', 5432))}", "max_connections = 500"]
         if repl:
             conf += ["wal_level = replica", "max_wal_senders = 16", "max_replication_slots = 16",
-                     "hot_standby = on", f"archive_mode = {'on' if cfg.get('archive_mode') else 'off'}"]
+                     "hot_standby = on", "wal_keep_size = 2048", "wal_log_hints = on",
+                     f"archive_mode = {'on' if cfg.get('archive_mode') else 'off'}"]
+            if repmgr:
+                conf.append("shared_preload_libraries = 'repmgr'")
             if not c["head"]:
                 user = cfg.get("replication_user", "repl_user")
                 conf.append(f"primary_conninfo = 'host={c['head_ip']} port={int(cfg.get('port', 5432))} "
@@ -288,8 +406,11 @@ class PostgresRuntime(ConfiguredRuntime):
         hba = ["host all all 0.0.0.0/0 scram-sha-256"]
         if repl:
             hba.append("host replication all 0.0.0.0/0 scram-sha-256")
-        return {os.path.join(c["dir"], "conf.d", "cloudtik.conf"): "\n".join(conf) + "\n",
-                os.path.join(c["dir"], "conf.d", "pg_hba.cloudtik.conf"): "\n".join(hba) + "\n"}
+        out = {os.path.join(c["dir"], "conf.d", "cloudtik.conf"): "\n".join(conf) + "\n",
+               os.path.join(c["dir"], "conf.d", "pg_hba.cloudtik.conf"): "\n".join(hba) + "\n"}
+        if repmgr:
+            out[os.path.join(c["dir"], "repmgr.conf")] = repmgr_conf(c, self._data_dir(cfg))
+        return out
 
     def configure_steps(self, head):
         # packaged server: include dir conf.d + hba rules appended once
@@ -299,6 +420,22 @@ class PostgresRuntime(ConfiguredRuntime):
                 "(sudo grep -q cloudtik-hba $d/pg_hba.conf || (echo '# cloudtik-hba' | sudo tee -a $d/pg_hba.conf "
                 ">/dev/null && sudo tee -a $d/pg_hba.conf < $RUNTIME_PATH/postgres/conf.d/pg_hba.cloudtik.conf "
                 ">/dev/null)); done; true"]
+
+    def _replicated(self) -> bool:
+        return (self.runtime_config or {}).get("cluster_mode", "none") == "replication"
+
+    def start_steps(self, head):
+        from cloudtik_amd.runtime.replication import postgres_bootstrap_steps, postgres_pre_start_steps
+        if not head and not self._replicated():
+            return []
+        c = self.ctx(head, self.node_env(head))
+        return postgres_pre_start_steps(c) + ["sudo service postgresql start"] + postgres_bootstrap_steps(c)
+
+    def stop_steps(self, head):
+        if not head and not self._replicated():
+            return []
+        steps = ["pkill -f 'repmgrd -f' || true"] if (self.runtime_config or {}).get("repmgr") else []
+        return steps + ["sudo service postgresql stop"]
 
 
 # ----------------------------------------------------------------------------- Prometheus / Grafana
@@ -336,27 +473,78 @@ class GrafanaRuntime(ConfiguredRuntime):
 
 
 # ----------------------------------------------------------------------------- HAProxy
-class HAProxyRuntime(ConfiguredRuntime):
+class DiscoveryBackedRuntime(ConfiguredRuntime):
+    """A load balancer / gateway whose backends come from service discovery when
+    ``backend.config_mode`` is ``dynamic`` (the default once a ``backend.selector`` is given):
+    a pull job (runtime/gateway_discovery.py) started as a service daemon on every node that
+    runs the gateway updates it as services come and go."""
+
+    discovery_class = ""
+
+    def dynamic(self, cfg) -> bool:
+        backend = cfg.get("backend") or {}
+        mode = backend.get("config_mode") or ("dynamic" if backend.get("selector") else "static")
+        return mode == "dynamic"
+
+    def discovery_config(self, c) -> Dict[str, Any]:
+        cfg = c["cfg"]
+        backend = cfg.get("backend") or {}
+        selector = backend.get("selector") or {"clusters": [c["cluster"]], "tags": ["cloudtik-f-load-balancer"]}
+        consul = cfg.get("consul_address") or f"{c['head_ip']}:8500"
+        return {"service_selector": selector, "consul_address": consul, "interval": backend.get("interval", 15)}
+
+    def _discovery_files(self, c) -> Dict[str, str]:
+        if not self.dynamic(c["cfg"]):
+            return {}
+        return {os.path.join(c["dir"], "discovery.json"): json.dumps(self.discovery_config(c), indent=1)}
+
+    def start_steps(self, head):
+        steps = super().start_steps(head)
+        c = self.ctx(head, self.node_env(head))
+        if self.dynamic(c["cfg"]):
+            steps.append(f"cloudtik node service-daemon start {self.name}-discovery "
+                         f"--service-class cloudtik_amd.runtime.gateway_discovery.{self.discovery_class} "
+                         f"config_file={os.path.join(c['dir'], 'discovery.json')}")
+        return steps
+
+    def stop_steps(self, head):
+        steps = []
+        if self.dynamic(self.runtime_config or {}):
+            steps.append(f"cloudtik node service-daemon stop {self.name}-discovery")
+        return steps + super().stop_steps(head)
+
+
+class HAProxyRuntime(DiscoveryBackedRuntime):
+    """Static backends (``backend.servers``) or dynamic ones: the runtime API socket is
+    opened and the backend gets a pool of server slots that the discovery job fills
+    (``DiscoverHAProxyBackends``)."""
     spec = SPEC_BY_NAME["haproxy"]
+    discovery_class = "DiscoverHAProxyBackends"
+    API_PORT = 19999
 
     def files(self, c):
+        from cloudtik_amd.runtime.gateway_discovery import haproxy_config
         cfg = c["cfg"]
-        port = int(cfg.get("port", 80))
-        mode = "http" if cfg.get("protocol", "http") == "http" else "tcp"
         backend = cfg.get("backend") or {}
-        servers = backend.get("servers") or []
-        lines = ["global", "    maxconn 20000", "defaults", f"    mode {mode}", "    timeout connect 5s",
-                 "    timeout client 60s", "    timeout server 60s",
-                 "frontend cloudtik", f"    bind *:{port}", "    default_backend cloudtik-servers",
-                 "backend cloudtik-servers", "    balance roundrobin"]
-        # role-aware routing: probe the runtime's health check (runtime/common/health_check.py),
-        # e.g. health_check_port 9201 + health_check_path /primary sends traffic to the primary only
-        hc_port = backend.get("health_check_port")
-        if hc_port:
-            lines.append(f"    option httpchk GET {backend.get('health_check_path', '/')}")
-        for i, s in enumerate(servers):
-            lines.append(f"    server s{i} {s} check" + (f" port {int(hc_port)}" if hc_port else ""))
-        return {os.path.join(c["dir"], "haproxy.cfg"): "\n".join(lines) + "\n"}
+        dyn = self.dynamic(cfg)
+        text = haproxy_config(int(cfg.get("port", 80)), cfg.get("protocol", "http"),
+                              [] if dyn else list(backend.get("servers") or []),
+                              backend.get("health_check_port"), backend.get("health_check_path", "/"),
+                              api_port=self.API_PORT if dyn else None)
+        out = {os.path.join(c["dir"], "haproxy.cfg"): text}
+        out.update(self._discovery_files(c))
+        return out
+
+    def discovery_config(self, c):
+        cfg = c["cfg"]
+        backend = cfg.get("backend") or {}
+        d = super().discovery_config(c)
+        d.update(backend_name="cloudtik-servers", api_addresses=[f"127.0.0.1:{self.API_PORT}"],
+                 conf_path=os.path.join(c["dir"], "haproxy.cfg"),
+                 haproxy={"port": int(cfg.get("port", 80)), "protocol": cfg.get("protocol", "http"),
+                          "health_check_port": backend.get("health_check_port"),
+                          "health_check_path": backend.get("health_check_path", "/"), "api_port": self.API_PORT})
+        return d
 
     def configure_steps(self, head):
         return ["mkdir -p $RUNTIME_PATH/haproxy/logs",

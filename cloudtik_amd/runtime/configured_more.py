@@ -19,7 +19,7 @@ from typing import Any, Dict, List
 import yaml
 
 from cloudtik_amd.runtime.catalog import SPEC_BY_NAME
-from cloudtik_amd.runtime.configured import ConfiguredRuntime, _extra, _props, parse_members
+from cloudtik_amd.runtime.configured import DiscoveryBackedRuntime, ConfiguredRuntime, _extra, _props, parse_members
 
 
 def _node_memory_mb(cfg: Dict[str, Any]) -> int:
@@ -293,11 +293,14 @@ class ElasticsearchRuntime(ConfiguredRuntime):
 
 
 # ----------------------------------------------------------------------------- NGINX
-class NginxRuntime(ConfiguredRuntime):
-    """Web server (``config_mode: web``) or load balancer over static backends (``backend.
-    servers`` with ``route_path`` per service)."""
+class NginxRuntime(DiscoveryBackedRuntime):
+    """Web server (``config_mode: web``), load balancer over static backends (``backend.
+    services`` with ``route_path`` per service), or over discovered services
+    (``backend.config_mode: dynamic`` / a ``backend.selector``: ``DiscoverNginxBackends``
+    rewrites nginx.conf and reloads when they change)."""
 
     spec = SPEC_BY_NAME["nginx"]
+    discovery_class = "DiscoverNginxBackends"
 
     def files(self, c):
         cfg = c["cfg"]
@@ -318,7 +321,17 @@ class NginxRuntime(ConfiguredRuntime):
         if not services:
             lines += [f"    root {cfg.get('web_root', os.path.join(c['dir'], 'html'))};"]
         lines += ["  }", "}"]
-        return {os.path.join(c["dir"], "nginx.conf"): "\n".join(lines) + "\n"}
+        out = {os.path.join(c["dir"], "nginx.conf"): "\n".join(lines) + "\n"}
+        out.update(self._discovery_files(c))
+        return out
+
+    def discovery_config(self, c):
+        d = super().discovery_config(c)
+        conf = os.path.join(c["dir"], "nginx.conf")
+        d.update(conf_path=conf, port=int(c["cfg"].get("port", 80)),
+                 balance=(c["cfg"].get("backend") or {}).get("balance"),
+                 reload_cmd=f"[ -d /etc/nginx ] && sudo cp {conf} /etc/nginx/nginx.conf; sudo nginx -s reload")
+        return d
 
     def configure_steps(self, head):
         return ["mkdir -p $RUNTIME_PATH/nginx/html",
@@ -326,8 +339,11 @@ class NginxRuntime(ConfiguredRuntime):
 
 
 # ----------------------------------------------------------------------------- Kong / APISIX
-class KongRuntime(ConfiguredRuntime):
+class KongRuntime(DiscoveryBackedRuntime):
+    """Kong on Postgres; discovered services become upstreams / services / routes through
+    the admin API (``DiscoverKongBackends``)."""
     spec = SPEC_BY_NAME["kong"]
+    discovery_class = "DiscoverKongBackends"
 
     def files(self, c):
         cfg = c["cfg"]
@@ -336,7 +352,14 @@ class KongRuntime(ConfiguredRuntime):
                 "pg_password": db["password"], "pg_database": db.get("name", "kong"),
                 "proxy_listen": "0.0.0.0:8000", "admin_listen": f"{c['ip']}:8001"}
         conf.update(_extra(cfg))
-        return {os.path.join(c["dir"], "kong.conf"): "".join(f"{k} = {v}\n" for k, v in conf.items())}
+        out = {os.path.join(c["dir"], "kong.conf"): "".join(f"{k} = {v}\n" for k, v in conf.items())}
+        out.update(self._discovery_files(c))
+        return out
+
+    def discovery_config(self, c):
+        d = super().discovery_config(c)
+        d["admin_url"] = f"http://{c['ip']}:8001"
+        return d
 
     def configure_steps(self, head):
         # migrations once, on the head (kong migrations bootstrap is idempotent)
@@ -344,8 +367,11 @@ class KongRuntime(ConfiguredRuntime):
             (["kong migrations bootstrap -c $RUNTIME_PATH/kong/kong.conf >/dev/null 2>&1 || true"] if head else [])
 
 
-class APISIXRuntime(ConfiguredRuntime):
+class APISIXRuntime(DiscoveryBackedRuntime):
+    """APISIX on etcd; discovered services become upstreams + routes through the admin API
+    (``DiscoverAPISIXBackends``)."""
     spec = SPEC_BY_NAME["apisix"]
+    discovery_class = "DiscoverAPISIXBackends"
 
     def files(self, c):
         cfg = c["cfg"]
@@ -357,7 +383,15 @@ class APISIXRuntime(ConfiguredRuntime):
                                                         "key": cfg.get("admin_key", "cloudtik-apisix")}],
                                          "allow_admin": ["0.0.0.0/0"]},
                                "etcd": {"host": etcd, "prefix": f"/apisix/{c['cluster']}"}}}
-        return {os.path.join(c["dir"], "conf", "config.yaml"): yaml.safe_dump(conf, sort_keys=False)}
+        out = {os.path.join(c["dir"], "conf", "config.yaml"): yaml.safe_dump(conf, sort_keys=False)}
+        out.update(self._discovery_files(c))
+        return out
+
+    def discovery_config(self, c):
+        d = super().discovery_config(c)
+        d.update(admin_url="http://127.0.0.1:9180/apisix/admin", admin_key=c["cfg"].get("admin_key", "cloudtik-apisix"),
+                 balance=(c["cfg"].get("backend") or {}).get("balance"))
+        return d
 
     members_env = "APISIX_ETCD_MEMBERS"
     quorum_members = False

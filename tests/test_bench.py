@@ -39,3 +39,14 @@ def test_bench_single_process_eager_impl():
     r = _run("--gpus", "1", "--impl", "eager")
     assert r["world_size"] == 1 and r["config"]["impl"] == "eager"
     assert r["value"] > 0 and r["resnet50_images_per_sec"] > 0
+
+
+def test_bench_eight_ranks_one_node_layout():
+    """The N = 8 launch of the driver's scaling run, rehearsed on gloo: 8 ranks, one JSON
+    line, the max over 8 ranks, both halves through the same bucketed data-parallel path."""
+    r = _run("--gpus", "8")
+    assert r["world_size"] == 8 and r["env"]["world_size_seen_by_collective"] == 8
+    assert len(r["per_rank_ms_per_step"]) == 8 and len(r["resnet50_per_rank_ms_per_step"]) == 8
+    assert r["ms_per_step"] >= max(r["per_rank_ms_per_step"]) * 0.999
+    assert r["config"]["parallelism"] == "dp8" and r["config"]["global_batch"] == 32
+    assert r["value"] > 0 and r["resnet50_images_per_sec"] > 0

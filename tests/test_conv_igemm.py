@@ -7,7 +7,7 @@ logic (forward taps, stride-1 data-gradient taps, stride-2 phase decomposition) 
 
 GPU: the HIP kernels against an fp32 reference: forward (+ BatchNorm tile statistics), data
 gradient (plain and accumulated into a residual gradient), weight gradient (split-K slabs,
-both reduce paths), and a ResNet-50 bottleneck fwd + bwd against the MIOpen path."""
+both reduce paths), and a ResNet-50 bottleneck fwd + bwd against an fp32 PyTorch block."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -127,29 +127,65 @@ def test_wide_reduce_many_slabs(cuda):
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-1)
 
 
+def _fp32_bottleneck(blk, x, train=True):
+    """The same bottleneck in plain fp32 PyTorch (F.conv2d + F.batch_norm in training mode +
+    ReLU, v1.5 stride on the 3x3) with the block's weights cast up: the oracle."""
+    def bn(t, m):
+        return F.batch_norm(t, m.running_mean.float().clone(), m.running_var.float().clone(), m.weight,
+                            m.bias, training=train, momentum=m.momentum, eps=m.eps)
+
+    o = F.relu(bn(F.conv2d(x, blk.conv1.weight), blk.bn1))
+    o = F.relu(bn(F.conv2d(o, blk.conv2.weight, stride=blk.conv2.stride, padding=1), blk.bn2))
+    o = bn(F.conv2d(o, blk.conv3.weight), blk.bn3)
+    idt = bn(F.conv2d(x, blk.down.weight, stride=blk.down.stride), blk.down_bn) if blk.down is not None else x
+    return F.relu(o + idt)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("down,stride", [(True, 1), (True, 2), (False, 1)])
-def test_bottleneck_matches_miopen_path(cuda, down, stride, monkeypatch):
+def test_bottleneck_matches_fp32_reference(cuda, down, stride, monkeypatch):
+    """A ResNet-50 bottleneck on the in-tree kernels (implicit-GEMM MFMA convs, BatchNorm
+    statistics from the conv epilogues, fused BN-apply / BN-backward / downsample-pair passes)
+    forward + backward against the fp32 PyTorch block (F.conv2d / F.batch_norm) with the same
+    weights: output, input gradient and every parameter gradient."""
     from cloudtik_amd.models.resnet import Bottleneck
     torch.manual_seed(0)
     cin = 64 if down else 256
     blk = Bottleneck(cin, 64, stride, downsample=down, device=cuda, dtype=torch.bfloat16).to(
         memory_format=torch.channels_last)
+    with torch.no_grad():                        # non-trivial affine BatchNorms (bn3 is zero-init)
+        for m in (blk.bn1, blk.bn2, blk.bn3) + ((blk.down_bn,) if down else ()):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.2, 0.2)
     x0 = _nhwc(torch.randn(4, cin, 16, 16, device=cuda).to(torch.bfloat16))
+    coef = None
 
     def run(enabled):
+        nonlocal coef
         monkeypatch.setattr(CV, "ENABLED", enabled)
         blk.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_()
         y = blk(x)
-        (y.float() * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
-        return y.detach().float(), x.grad.float(), [p.grad.float().clone() for p in blk.parameters()]
+        if coef is None:
+            coef = torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)
+        (y.float() * coef).sum().backward()
+        return [y.detach().float(), x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
 
-    y1, gx1, gp1 = run(True)
-    y0, gx0, gp0 = run(False)
-    assert _rel(y1, y0) < 2e-2 and _rel(gx1, gx0) < 3e-2
-    for a, b in zip(gp1, gp0):
-        assert _rel(a, b) < 3e-2
+    import copy
+    rb = copy.deepcopy(blk).float()              # fp32 copies of the weights, own gradients
+    ours = run(True)
+    stock = run(False)                           # MIOpen / PyTorch bf16: what bf16 costs anyway
+    rb.zero_grad(set_to_none=True)
+    xr = x0.float().clone().requires_grad_()
+    yr = _fp32_bottleneck(rb, xr)
+    (yr * coef.float()).sum().backward()
+    ref = [yr.detach(), xr.grad] + [p.grad for p in rb.parameters()]
+    names = ["y", "x.grad"] + [n for n, _ in blk.named_parameters()]
+    for n, a, s_, r in zip(names, ours, stock, ref):
+        e_ours, e_stock = _rel(a, r), _rel(s_, r)
+        # the in-tree kernels are at most 1.5x the stock bf16 path's distance from fp32 (and
+        # within 2 % wherever bf16 itself is that close)
+        assert e_ours < max(2e-2, 1.5 * e_stock), (n, e_ours, e_stock)
 
 
 @pytest.mark.gpu

@@ -1,5 +1,5 @@
 """Data-parallel gradient reduction (parallel.GradBucketer) against single-process
-full-batch gradients, over gloo with 2 and 4 ranks: several buckets, an unused parameter,
+full-batch gradients, over gloo with 2, 4 and 8 ranks (8 = one MI355X node): several buckets, an unused parameter,
 ``no_sync`` gradient accumulation over 2 micro-batches, bf16 gradients with fp32 reduction,
 and the optimizer step that follows (reference semantics: DDP averaging,
 ssd-resnet34 distributed.py:13-48, transfer-learning trainer.py:215-219)."""
@@ -106,7 +106,7 @@ def _reference():
 
 
 @pytest.mark.parametrize("world,accum,fp32_reduce", [(2, 1, False), (2, 2, False), (4, 2, False), (2, 2, True),
-                                                     (4, 1, True)])
+                                                     (4, 1, True), (8, 1, False), (8, 2, True)])
 def test_gradbucketer_matches_full_batch(world, accum, fp32_reduce, device="cpu"):
     port = _port()
     ctx = mp.get_context("spawn")

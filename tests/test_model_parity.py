@@ -147,3 +147,64 @@ def test_bert_native_kernels_match_hf_fp32():
         a, r = og[mine].grad.float().cpu().reshape(-1), hg[theirs].grad.reshape(-1)
         cos = torch.nn.functional.cosine_similarity(a, r, dim=0).item()
         assert cos > 0.99, (mine, cos)
+
+
+@pytest.mark.gpu
+def test_bert_bench_routing_matches_hf_fp32():
+    """The headline configuration's exact kernel routing -- parameters in a FlatParamSpace,
+    weight gradients in line (the model's own routing, no side stream), FFN1 + bias-GELU and
+    FFN dgrad + dGELU fused MFMA GEMMs, the data-gradient sites on the one-tile MFMA kernel,
+    MFMA attention, fused LayerNorm -- against the fp32 Hugging Face model with identical
+    weights.  The kernels are asserted to have run (torch.profiler)."""
+    import re
+    from torch.profiler import ProfilerActivity, profile
+    from cloudtik_amd.benchmarks.eager import dense_mlm_labels
+    from cloudtik_amd.models.bert import synthetic_pretraining_batch
+    from cloudtik_amd.ops.linear import wgrad_side
+    from cloudtik_amd.train.optim import FlatParamSpace
+    hf, ours, cfg = _hf_and_ours(V=1024, H=256, L=2, NH=4, I=1024, maxpos=128)
+    ours = ours.to("cuda", torch.bfloat16).train()
+    assert not any(wgrad_side(p) for p in ours.parameters())          # in line, as in bench.py
+    named = list(ours.named_parameters())
+    space = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+    B, S, P = 8, 128, 20
+    b = synthetic_pretraining_batch(cfg, B, S, P, generator=torch.Generator().manual_seed(3))
+    b["attention_mask"][1, 100:] = 0
+    labels = dense_mlm_labels(b, S)
+    out = hf(input_ids=b["input_ids"], token_type_ids=b["token_type_ids"], attention_mask=b["attention_mask"],
+             labels=labels, next_sentence_label=b["next_sentence_labels"])
+    out.loss.backward()
+    space.grad.zero_()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        loss = ours(**{k: v.cuda() for k, v in b.items()})
+        loss.backward()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+    joined = "\n".join(names)
+    for pat in (r"gemm_nt_kernel<1, false, 0, 0",          # FFN1 + bias + erf-GELU (+ pre-activation)
+                r"gemm_nt_kernel<2, (true|false), 0, 2",   # FFN dgrad + dGELU (+ bias grad)
+                r"gemm_nt_kernel<0, false, 0, 2",          # one-tile data-gradient sites (NN)
+                r"gemm_nt_kernel<\d, false, 0, 1",         # MFMA weight gradients (TN)
+                r"attn_fwd", r"attn_bwd", r"ln_fwd", r"ln_bwd"):
+        assert re.search(pat, joined), (pat, sorted(set(names))[:40])
+    assert abs(loss.item() - out.loss.item()) < 2e-2 * out.loss.item()
+    hg = dict(hf.named_parameters())
+    og = dict(ours.named_parameters())
+    q, p = "bert.layers.{}.", "bert.encoder.layer.{}."
+    pairs = [("bert.layers.0.ffn1_weight", hg["bert.encoder.layer.0.intermediate.dense.weight"].grad),
+             ("bert.layers.1.ffn2_weight", hg["bert.encoder.layer.1.output.dense.weight"].grad),
+             ("bert.layers.1.out_weight", hg["bert.encoder.layer.1.attention.output.dense.weight"].grad),
+             ("bert.layers.0.qkv_weight", torch.cat([hg[p.format(0) + f"attention.self.{n}.weight"].grad
+                                                     for n in ("query", "key", "value")])),
+             ("bert.layers.0.qkv_bias", torch.cat([hg[p.format(0) + f"attention.self.{n}.bias"].grad
+                                                   for n in ("query", "key", "value")])),
+             ("bert.layers.0.ffn1_bias", hg["bert.encoder.layer.0.intermediate.dense.bias"].grad),
+             ("bert.layers.1.ln2_weight", hg["bert.encoder.layer.1.output.LayerNorm.weight"].grad),
+             ("mlm_dense_weight", hg["cls.predictions.transform.dense.weight"].grad),
+             ("bert.position_embeddings", hg["bert.embeddings.position_embeddings.weight"].grad)]
+    for mine, ref in pairs:
+        a = og[mine].grad.float().cpu().reshape(-1)[: ref.numel()]
+        r = ref.reshape(-1)
+        cos = torch.nn.functional.cosine_similarity(a, r, dim=0).item()
+        rel = ((a - r).norm() / r.norm()).item()
+        assert cos > 0.99 and rel < 0.15, (mine, cos, rel)

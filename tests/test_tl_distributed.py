@@ -37,3 +37,14 @@ def test_run_command_api_launches_every_rank(tmp_path, monkeypatch):
     assert run_command(["python", str(script)], nproc_per_node=3, launcher="local", no_python=True) == 0
     assert sorted(p.name for p in tmp_path.iterdir() if p.name.startswith("r")) == ["r0", "r1", "r2"]
     assert (tmp_path / "r2").read_text() == "3"
+
+
+def test_multi_host_job_without_shared_dir_is_refused_up_front():
+    """A job whose ranks land on other hosts cannot read a local temp dir: refused before
+    anything is exported or launched (advisor r4)."""
+    import pytest
+    from cloudtik_amd.modeling.transfer_learning.distributed import fit_distributed, spans_hosts
+    assert not spans_hosts(1, None, None) and not spans_hosts(1, "localhost:2", None)
+    assert spans_hosts(2, None, None) and spans_hosts(1, "10.0.0.1:4,10.0.0.2:4", None)
+    with pytest.raises(ValueError, match="shared_dir"):
+        fit_distributed(object(), [], {}, nnodes=2, nproc_per_node=1)

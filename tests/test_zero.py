@@ -98,7 +98,8 @@ def _worker(rank, world, port, kind, dtype, out):
 
 
 @pytest.mark.parametrize("kind,world,dtype", [("lamb", 2, torch.float32), ("adamw", 4, torch.float32),
-                                              ("sgd", 2, torch.float32), ("lamb", 4, torch.bfloat16)])
+                                              ("sgd", 2, torch.float32), ("lamb", 4, torch.bfloat16),
+                                              ("lamb", 8, torch.float32)])
 def test_zero1_matches_unsharded(kind, world, dtype):
     port = _port()
     ctx = mp.get_context("spawn")
