@@ -63,11 +63,14 @@ def parse(argv=None):
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--max-pred", type=int, default=76,
                     help="masked-LM slots per sequence (reference phase-1: max_predictions_per_seq=76)")
-    ap.add_argument("--bucket-mb", type=float, default=64.0, help="BERT gradient bucket (MiB)")
-    ap.add_argument("--rn-bucket-mb", type=float, default=8.0,
-                    help="ResNet-50 gradient bucket (MiB): its 51 MB of bf16 gradients would be ONE "
-                         "64 MiB bucket, all-reduced only after the whole backward; 8 MiB gives 7 "
-                         "buckets that overlap the backward of the earlier stages")
+    ap.add_argument("--bucket-mb", default="auto",
+                    help="BERT gradient bucket (MiB), or auto: the size measured on this node for this "
+                         "world size by bench/comm_bench.py --write-tuning (parallel/comm_tuning.py), "
+                         "64 MiB when never measured")
+    ap.add_argument("--rn-bucket-mb", default="auto",
+                    help="ResNet-50 gradient bucket (MiB) or auto (measured, else 8 MiB): its 51 MB of "
+                         "bf16 gradients would be ONE 64 MiB bucket, all-reduced only after the whole "
+                         "backward; 8 MiB gives 7 buckets that overlap the backward of the earlier stages")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="native path: fp32 = bf16 per-backward grads reduced / accumulated in fp32")
     ap.add_argument("--zero", action="store_true",
@@ -181,6 +184,15 @@ def setup_tunableop(mode, rank):
         tn.set_max_tuning_iterations(30)
 
 
+def resolve_bucket_mb(value, world: int, default: float) -> float:
+    """``--bucket-mb`` value: a number, or ``auto`` = the bucket measured for this world size
+    (parallel/comm_tuning.py), else ``default``."""
+    if str(value).lower() != "auto":
+        return float(value)
+    from cloudtik_amd.parallel.comm_tuning import bucket_mb
+    return bucket_mb(world, default)
+
+
 def bucket_plan(ddp):
     """Gradient-bucket plan of a GradBucketer: count, sizes, collective, wire dtype."""
     esize = ddp.space.grad.element_size() if not ddp.fp32 else 4
@@ -256,7 +268,7 @@ def build_bert(args, rank, world, device, kind):
     sched = LinearWarmupPolyDecayScheduler(opt, start_warmup_steps=0, warmup_steps=0,
                                            total_steps=13700, end_learning_rate=0.0, degree=1.0)
     broadcast_flat_params(space)
-    ddp = GradBucketer(space, bucket_mb=args.bucket_mb,
+    ddp = GradBucketer(space, bucket_mb=resolve_bucket_mb(args.bucket_mb, world, 64.0),
                        reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
                        mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale
@@ -306,7 +318,7 @@ def build_resnet(args, rank, world, device, kind):
     opt = FusedSGD(space, lr=0.1, momentum=0.9, weight_decay=1e-4,
                    no_decay=lambda n: n.endswith("bias") or ".bn" in n or n.startswith("bn"))
     broadcast_flat_params(space)
-    ddp = GradBucketer(space, bucket_mb=args.rn_bucket_mb,
+    ddp = GradBucketer(space, bucket_mb=resolve_bucket_mb(args.rn_bucket_mb, world, 8.0),
                        reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
                        mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale

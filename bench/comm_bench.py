@@ -53,6 +53,10 @@ def parse(argv=None):
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-p2p", action="store_true")
+    ap.add_argument("--write-tuning", nargs="?", const="", default=None, metavar="PATH",
+                    help="store the recommended bucket and P2P crossover for this world size in the "
+                         "tuning file the data-parallel path reads (parallel/comm_tuning.py; default "
+                         "path when given without a value)")
     ap.add_argument("--plateau", type=float, default=0.8,
                     help="recommended bucket = smallest size reaching this fraction of the peak busbw")
     return ap.parse_args(argv)
@@ -221,6 +225,12 @@ def main():
                 out["rccl"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
             except Exception:  # noqa: BLE001
                 pass
+        if args.write_tuning is not None and cuda:
+            from cloudtik_amd.parallel import comm_tuning
+            gpu = torch.cuda.get_device_properties(device).name
+            comm_tuning.record(world, out["recommended_bucket_bytes"], out["p2p_crossover_bytes"],
+                               p=args.write_tuning or None, rccl=out["rccl"], gpu=gpu)
+            out["tuning_written"] = args.write_tuning or comm_tuning.path()
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

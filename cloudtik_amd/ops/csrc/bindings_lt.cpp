@@ -303,8 +303,8 @@ static bool gemm_nt_impl(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, 
                       aux->size(1) == N, "gemm_nt: aux");
   if (hd) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->is_contiguous() && dbias->numel() == N,
                       "gemm_nt: dbias");
-  TORCH_CHECK(epi != 1 || (hb && ha), "gemm_nt: epilogue 1 needs bias and aux");
-  TORCH_CHECK(epi != 2 || ha, "gemm_nt: epilogue 2 needs aux");
+  TORCH_CHECK((epi != 1 && epi != 6) || (hb && ha), "gemm_nt: epilogues 1 / 6 need bias and aux");
+  TORCH_CHECK((epi != 2 && epi != 7) || ha, "gemm_nt: epilogues 2 / 7 need aux");
   int rc = ct_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0), (int)M,
                       (int)N, (int)K, (int)epi, accumulate ? 1 : 0, hb ? bias->data_ptr() : nullptr,
                       ha ? aux->data_ptr() : nullptr, ha ? aux->stride(0) : 0,

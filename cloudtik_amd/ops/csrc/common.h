@@ -149,6 +149,40 @@ __device__ __forceinline__ void gelu2_batch(const f32x2 (&x)[NP], f32x2 (&y)[NP]
   }
 }
 
+// gelu(x) and gelu'(x) of NP packed pairs in one pass: the two share the erf term and the
+// Gaussian exp (the derivative adds one FMA per element).  The FFN1 forward epilogue stores
+// gelu'(x) instead of x, so the FFN data-gradient epilogue is a multiply (gemm_nt.hip EPI 6/7).
+template <int NP>
+__device__ __forceinline__ void gelu2_batch_both(const f32x2 (&x)[NP], f32x2 (&y)[NP], f32x2 (&g)[NP]) {
+  const float kE = -0.5f * 1.4426950408889634f;
+  f32x2 d[NP], e[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const f32x2 ax = {fabsf(x[p][0]), fabsf(x[p][1])};
+    d[p] = __builtin_elementwise_fma(ax, (f32x2)(0.3275911f * 0.70710678118654752f), (f32x2)(1.f));
+    e[p] = x[p] * (x[p] * kE);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    d[p] = f32x2{__builtin_amdgcn_rcpf(d[p][0]), __builtin_amdgcn_rcpf(d[p][1])};
+    e[p] = f32x2{__builtin_amdgcn_exp2f(e[p][0]), __builtin_amdgcn_exp2f(e[p][1])};
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const f32x2 t = d[p];
+    f32x2 q = __builtin_elementwise_fma(t, (f32x2)(1.061405429f), (f32x2)(-1.453152027f));
+    q = __builtin_elementwise_fma(q, t, (f32x2)(1.421413741f));
+    q = __builtin_elementwise_fma(q, t, (f32x2)(-0.284496736f));
+    q = __builtin_elementwise_fma(q, t, (f32x2)(0.254829592f));
+    q = q * t;
+    const f32x2 ea = __builtin_elementwise_fma(-q, e[p], (f32x2)(1.f));          // erf(|x| / sqrt 2)
+    const f32x2 s = {copysignf(ea[0], x[p][0]), copysignf(ea[1], x[p][1])};
+    const f32x2 cdf = __builtin_elementwise_fma(s, (f32x2)(0.5f), (f32x2)(0.5f));
+    g[p] = __builtin_elementwise_fma(x[p] * 0.3989422804014327f, e[p], cdf);
+    y[p] = x[p] * cdf;
+  }
+}
+
 // Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): consecutive logical tiles land on the same XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

@@ -43,8 +43,12 @@ constexpr int NT_ROWB = NT_BK * 2;        // 128 B per LDS image row
 constexpr int NT_HALF = 128 * NT_ROWB;    // 16 KiB: 128 rows of one operand
 constexpr int NT_BUF = 4 * NT_HALF;       // 64 KiB per K-tile buffer
 
+// EPI 6 / 7 are the derivative-storing pair: the FFN1 forward keeps gelu'(x W1^T + b1) (bf16) as
+// its aux output instead of the pre-activation, and the FFN data gradient multiplies by it --
+// the dGELU's transcendental work (exp + rcp per element) moves out of the VALU-bound backward
+// epilogue into the forward one, which is store-bound and computes the same exp / erf terms anyway.
 enum { NT_EPI_PLAIN = 0, NT_EPI_BIAS_GELU_AUX = 1, NT_EPI_DGELU_BGRAD = 2, NT_EPI_F32_SLAB = 3, NT_EPI_NONE = 4,
-       NT_EPI_BIAS = 5 };
+       NT_EPI_BIAS = 5, NT_EPI_BIAS_GELU_DAUX = 6, NT_EPI_MUL_AUX_BGRAD = 7 };
 
 struct NtArgs {
   const bf16_t* A;
@@ -60,6 +64,7 @@ struct NtArgs {
                         // possible: the first (K / 64) % splits slices get one K-tile more)
   int M, N, K;
   int accumulate;       // EPI 0: D += result
+  int stagger;          // NT / NN one-tile grid: H column-half tiles at each end (0 = none), below
 };
 
 __device__ __forceinline__ int nt_swz(int r) { return (r >> 1) & 7; }
@@ -173,6 +178,7 @@ struct NtCtx {
   int wave, lane, ra, rb;
   unsigned offa0, offa1, offb0, offb1;   // per-lane staging offsets (NT: by piece parity; TN: A / B)
   int biasw;                             // BIASG: this wave owns bias rows 2 wc, 2 wc + 1 (else -1)
+  int half;                              // 0 full tile; 1 / 2: only the B0 / B1 column halves
 };
 
 // Bias gradient inside the weight-gradient GEMM (TN): db[m] = sum_k A[k][m] is one more MFMA per
@@ -295,7 +301,7 @@ __device__ __forceinline__ void nt_ktile(const NtCtx& c, int t, f32x4 (&acc)[8][
   if constexpr (DMA && P::issue(Q)) nt_stage_v<LAY>(c, 4 * t + Q);                   \
   if constexpr (WAIT) nt_vm<P::wait(Q)>();                                           \
   if constexpr (BAR) nt_mma_begin(); else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
-  nt_quad<I0, J0>(acc, FA, FB);                                                      \
+  if (c.half != (J0 == 0 ? 2 : 1)) nt_quad<I0, J0>(acc, FA, FB);                     \
   if constexpr (BIASG && (Q == 0 || Q == 2)) nt_quad_bias<Q, I0>(accb, FA, c.biasw); \
   if constexpr (BAR) nt_mma_end(); else __builtin_amdgcn_sched_barrier(0);
   // ---- q0: B0 + A0 fragments
@@ -358,7 +364,8 @@ struct NtEpiPre {
 
 template <int EPI, int NJ>
 __device__ __forceinline__ void nt_preload_bias(const NtArgs& a, long ncol, NtEpiPre<NJ>& pre) {
-  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_BIAS) {
+  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_BIAS ||
+                EPI == NT_EPI_BIAS_GELU_DAUX) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) pre.bias[j] = a.bias ? *(const u16x4*)(a.bias + ncol + j * 16) : u16x4(0);
   }
@@ -366,7 +373,7 @@ __device__ __forceinline__ void nt_preload_bias(const NtArgs& a, long ncol, NtEp
 
 template <int EPI, int NJ>
 __device__ __forceinline__ void nt_preload_z(const NtArgs& a, long mrow, long ncol, NtEpiPre<NJ>& pre) {
-  if constexpr (EPI == NT_EPI_DGELU_BGRAD) {
+  if constexpr (EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_MUL_AUX_BGRAD) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -376,7 +383,7 @@ __device__ __forceinline__ void nt_preload_z(const NtArgs& a, long mrow, long nc
 
 template <int EPI, bool BGRAD, int NJ>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[8][NJ], long mrow, long ncol,
-                                            int lane, int split, NtEpiPre<NJ>& pre) {
+                                            int lane, int split, NtEpiPre<NJ>& pre, int half = 0) {
   static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
   if constexpr (EPI == NT_EPI_NONE) {
     // timing diagnostic (CLOUDTIK_AMD_GEMM_DIAG=4): the K loop without the epilogue's memory
@@ -398,7 +405,8 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
     return;
   }
   float bv[NJ][4] = {};
-  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_BIAS) {
+  if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_BIAS ||
+                EPI == NT_EPI_BIAS_GELU_DAUX) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -444,7 +452,43 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
       // of 1742 VALU instructions and 6 instead of 260 hazard s_nop per wave epilogue).  Same
       // time measured (301 vs 302 us for BERT-large FFN1): the epilogue writes h and z, 2 x
       // 268 MB, at ~5 TB/s -- it is store-bandwidth bound once every CU reaches it together.
-      if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) {
+      if constexpr (EPI == NT_EPI_BIAS_GELU_DAUX) {
+        // h = gelu(x), aux = gelu'(x), x = acc + bias
+        f32x2 xv[2 * NJ], gv[2 * NJ], dv[2 * NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            xv[2 * j + h] = f32x2{acc[i][j][2 * h], acc[i][j][2 * h + 1]} + f32x2{bv[j][2 * h], bv[j][2 * h + 1]};
+        gelu2_batch_both<2 * NJ>(xv, gv, dv);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              pre[j][2 * h + e] = f2bf(dv[2 * j + h][e]);
+              out[j][2 * h + e] = f2bf(gv[2 * j + h][e]);
+            }
+      } else if constexpr (EPI == NT_EPI_MUL_AUX_BGRAD) {
+        // dz = dh * gelu'(z): the derivative was stored by the forward (EPI 6)
+        u16x4 z[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) z[j] = zq[i & 1][j];
+        if (i + 2 < 8) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) zq[i & 1][j] = *(const u16x4*)(a.aux + (m + 32) * a.ldaux + ncol + j * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float gg = acc[i][j][r] * bf2f(z[j][r]);
+            out[j][r] = f2bf(gg);
+            if constexpr (BGRAD) cs[2 * j + (r >> 1)][r & 1] += gg;
+          }
+        }
+      } else if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) {
         f32x2 xv[2 * NJ], gv[2 * NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
@@ -485,17 +529,20 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
 #pragma unroll
     for (int j = 0; j < NJ; j += 2) {
       const long n = scol + j * 16;
+      if (half == (j < NJ / 2 ? 2 : 1)) continue;       // the other WG's column half
       *(u16x8*)(a.D + m * a.ldd + n) = nt_pair_swap(out[j], out[j + 1]);
-      if constexpr (EPI == NT_EPI_BIAS_GELU_AUX) *(u16x8*)(a.aux + m * a.ldaux + n) = nt_pair_swap(pre[j], pre[j + 1]);
+      if constexpr (EPI == NT_EPI_BIAS_GELU_AUX || EPI == NT_EPI_BIAS_GELU_DAUX)
+        *(u16x8*)(a.aux + m * a.ldaux + n) = nt_pair_swap(pre[j], pre[j + 1]);
     }
   }
-  if constexpr (EPI == NT_EPI_DGELU_BGRAD && BGRAD) {
+  if constexpr ((EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_MUL_AUX_BGRAD) && BGRAD) {
     // column sums: reduce the 16 rows held by lanes sharing (lane >> 4), then one atomic per
     // column per wave (vector-memory float atomics)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        if (half == (j < NJ / 2 ? 2 : 1)) continue;
         float v = cs[2 * j + (r >> 1)][r & 1];
         v += __shfl_xor(v, 1);
         v += __shfl_xor(v, 2);
@@ -517,7 +564,27 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * NT_BUF];    // 128 KiB, the only LDS object
   const int tiles_n = a.N / NT_BN;
   const int tiles = (a.M / NT_BM) * tiles_n;
-  int L = xcd_remap(blockIdx.x, gridDim.x);
+  // Staggered grid (NT / NN, a.stagger = H > 0): the first 2H blocks alternate a full tile and
+  // the B0 column half of one of tiles H .. 2H-1, and H blocks at the end do their B1 halves.
+  // The half tiles (about half the time of a full one) put half of the CUs of the first round
+  // half a tile out of phase with the other half for the rest of the grid, so their epilogues
+  // -- store- or VALU-bound with the matrix cores idle -- no longer all hit HBM at once; the
+  // total work is unchanged.  Dispatch order only decides how well it staggers, never what
+  // is computed.
+  int v = blockIdx.x, half = 0;
+  if constexpr (!SPLIT) {
+    const int H = a.stagger;
+    if (H > 0) {
+      if (v < 2 * H) {
+        half = v & 1;
+        v = (v & 1) ? H + (v >> 1) : (v >> 1);
+      } else if (v >= tiles) {
+        half = 2;
+        v = H + (v - tiles);
+      }
+    }
+  }
+  int L = xcd_remap(v, SPLIT ? gridDim.x : tiles);
   const int split = SPLIT ? L / tiles : 0;
   L -= split * tiles;
   const int tm = L / tiles_n, tn = L % tiles_n;
@@ -533,7 +600,7 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   const int nk = kt_q + (split < kt_r ? 1 : 0);
   const long kfirst = SPLIT ? (long)(split * kt_q + min(split, kt_r)) * NT_BK : 0L;
   NtCtx c{a.A, a.B, a.lda, a.ldb, m0, n0, kfirst, lds, wave, lane, wr * 64, wc * 32,
-          0, 0, 0, 0, (BIASG && tn == 0) ? 2 * wc : -1};
+          0, 0, 0, 0, (BIASG && tn == 0) ? 2 * wc : -1, half};
   f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   if constexpr (Ly::AT) {
     c.offa0 = c.offa1 = tn_lane_off(a.lda, wave, lane, true);
@@ -587,7 +654,7 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 
   // acc[i][j][r] = D[m0 + wr*128 + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
-  nt_epilogue<EPI, BGRAD, 4>(a, acc, emrow, encol, lane, split, epre);
+  nt_epilogue<EPI, BGRAD, 4>(a, acc, emrow, encol, lane, split, epre, half);
   if constexpr (BIASG) {
     // accb[t] row block 2 wc + t: every column holds the row sum; lanes 0-15 hold rows 0-15
     if (c.biasw >= 0 && lane < 16) {
@@ -743,7 +810,7 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_stream_kernel(NtArgs a,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  NtCtx c{a.A, a.B, a.lda, a.ldb, 0, 0, 0, lds, wave, lane, wr * 64, wc * 32, 0, 0, 0, 0, -1};
+  NtCtx c{a.A, a.B, a.lda, a.ldb, 0, 0, 0, lds, wave, lane, wr * 64, wc * 32, 0, 0, 0, 0, -1, 0};
   c.offa0 = nt_lane_off(a.lda, 0, lane);
   c.offa1 = nt_lane_off(a.lda, 1, lane);
   if constexpr (NtLay<LAY>::BT) {
@@ -874,7 +941,9 @@ extern "C" int ct_gemm_nt_stream(const void* A, long lda, const void* B, long ld
 
 // D[M,N] = A[M,K] . B[N,K]^T (row-major, K-contiguous operands) with epilogue `epi`:
 //   0: plain (accumulate: D += result); 1: aux = result + bias, D = gelu(aux);
-//   2: D = result * gelu'(aux [+ bias]), dbias += column sums (bias, dbias may be null).
+//   2: D = result * gelu'(aux [+ bias]), dbias += column sums (bias, dbias may be null);
+//   6: D = gelu(result + bias), aux = gelu'(result + bias);
+//   7: D = result * aux, dbias += column sums (dbias may be null).
 // Returns nonzero (and launches nothing) when the shape / alignment is not supported.
 extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void* D, long ldd, int M, int N, int K,
                           int epi, int accumulate, const void* bias, void* aux, long ldaux, float* dbias, int b_kn,
@@ -882,14 +951,22 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   if (M <= 0 || N <= 0 || K <= 0 || M % NT_BM || N % NT_BN || K % NT_BK) return 1;
   if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < (b_kn ? N : K) || ldd < N) return 2;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 15)) return 3;
-  if (epi == 1 && (!bias || !aux || ((uintptr_t)bias & 7))) return 4;
+  if ((epi == 1 || epi == 6) && (!bias || !aux || ((uintptr_t)bias & 7))) return 4;
   if (epi == 5 && (!bias || ((uintptr_t)bias & 7))) return 4;
-  if ((epi == 1 || epi == 2) && (!aux || ((uintptr_t)aux & 15) || ldaux % 8 || ldaux < N)) return 4;
+  if ((epi == 1 || epi == 2 || epi == 6 || epi == 7) && (!aux || ((uintptr_t)aux & 15) || ldaux % 8 || ldaux < N))
+    return 4;
   if (bias && ((uintptr_t)bias & 7)) return 4;
-  const long blocks = (long)(M / NT_BM) * (N / NT_BN);
-  if (blocks > (1L << 30)) return 5;
+  const long tiles = (long)(M / NT_BM) * (N / NT_BN);
+  if (tiles > (1L << 30)) return 5;
+  // stagger half of the first round's CUs by half a tile when the grid has >= 2 rounds
+  // (CLOUDTIK_AMD_GEMM_STAGGER: -1 auto (default), 0 off, H > 0 forces H half-tile pairs)
+  static const int stag_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_STAGGER"); return e ? atoi(e) : -1; }();
+  int H = 0;
+  if (stag_env > 0) H = (int)std::min<long>(stag_env, tiles / 2);
+  else if (stag_env < 0 && tiles >= 2L * nt_cu_count()) H = nt_cu_count() / 2;
+  const long blocks = tiles + H;
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias, nullptr,
-           nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, accumulate};
+           nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, accumulate, H};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
   if (diag == 4) {
     if (b_kn) gemm_nt_kernel<NT_EPI_NONE, false, 0, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
@@ -915,6 +992,11 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
       else NT_LAUNCH(2, false);
       break;
     case 5: NT_LAUNCH(5, false); break;
+    case 6: NT_LAUNCH(6, false); break;
+    case 7:
+      if (dbias) NT_LAUNCH(7, true);
+      else NT_LAUNCH(7, false);
+      break;
     default: return 6;
   }
 #undef NT_LAUNCH

@@ -22,6 +22,7 @@
 // Dynamic hyper-parameters (lr, grad scale, bias corrections) are read from a device array
 // so a hipGraph-captured step picks up the scheduler's new values at replay.
 #include "common.h"
+#include <cstdlib>
 
 namespace ct {
 
@@ -48,6 +49,134 @@ __device__ __forceinline__ void store4(float* p, long i, f32x4 v) { *reinterpret
 __device__ __forceinline__ void store4(bf16_t* p, long i, f32x4 v) {
   u16x4 o = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
   *reinterpret_cast<u16x4*>(p + i) = o;
+}
+
+// 8 consecutive elements as one 16-byte (bf16) or two 16-byte (fp32) accesses
+__device__ __forceinline__ void load8(const float* p, long i, float (&o)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p + i), b = *reinterpret_cast<const f32x4*>(p + i + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
+}
+__device__ __forceinline__ void load8(const bf16_t* p, long i, float (&o)[8]) {
+  const u16x8 v = *reinterpret_cast<const u16x8*>(p + i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f(v[j]);
+}
+__device__ __forceinline__ void store8(float* p, long i, const float (&v)[8]) {
+  *reinterpret_cast<f32x4*>(p + i) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + i + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void store8(bf16_t* p, long i, const float (&v)[8]) {
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+  *reinterpret_cast<u16x8*>(p + i) = o;
+}
+
+// LAMB over a segment with every load of the thread's share issued before any math: U chunks
+// of 8 elements per thread (a whole 8K segment in one pass at U = 4, 256 threads).  The
+// one-vec4-per-iteration form kept a single 56-byte load group in flight per thread and ran at
+// 3.4-3.8 TB/s (profiles/r4/pmc_bert-large_r4late.md); segments are 64-element multiples, so a
+// chunk that starts inside the segment ends inside it.
+constexpr int LAMB_U = 4;
+
+template <typename GT>
+__global__ __launch_bounds__(256) void lamb_stage1_v8_kernel(
+    const GT* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ w, OptSegs segs, const float* __restrict__ tensor_wd,
+    const float* __restrict__ dyn, float beta1, float beta2, float eps, int bias_corr,
+    float* __restrict__ seg_part) {
+  __shared__ float scratch[8];
+  const int s = blockIdx.x;
+  const long start = segs.seg_start[s];
+  const int len = segs.seg_len[s];
+  const float wd = tensor_wd[segs.seg_tensor[s]];
+  const float gs = dyn[1];
+  const float bc1 = bias_corr ? dyn[2] : 1.f, bc2 = bias_corr ? dyn[3] : 1.f;
+  float w2 = 0.f, u2 = 0.f;
+  for (int i0 = threadIdx.x * 8; i0 < len; i0 += 256 * 8 * LAMB_U) {
+    float gv[LAMB_U][8], mv[LAMB_U][8], vv[LAMB_U][8], wv[LAMB_U][8];
+#pragma unroll
+    for (int u = 0; u < LAMB_U; ++u) {
+      const int i = i0 + u * 256 * 8;
+      if (i < len) {
+        const long k = start + i;
+        load8(g, k, gv[u]);
+        load8(m, k, mv[u]);
+        load8(v, k, vv[u]);
+        load8(w, k, wv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < LAMB_U; ++u) {
+      const int i = i0 + u * 256 * 8;
+      if (i < len) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gr = gv[u][j] * gs;
+          mv[u][j] = beta1 * mv[u][j] + (1.f - beta1) * gr;
+          vv[u][j] = beta2 * vv[u][j] + (1.f - beta2) * gr * gr;
+          const float up = (mv[u][j] * bc1) / (sqrtf(vv[u][j] * bc2) + eps) + wd * wv[u][j];
+          w2 += wv[u][j] * wv[u][j];
+          u2 += up * up;
+        }
+        const long k = start + i;
+        store8(m, k, mv[u]);
+        store8(v, k, vv[u]);
+      }
+    }
+  }
+  w2 = block_sum(w2, scratch);
+  u2 = block_sum(u2, scratch);
+  if (threadIdx.x == 0) { seg_part[2 * s] = w2; seg_part[2 * s + 1] = u2; }
+}
+
+template <typename PT>
+__global__ __launch_bounds__(256) void lamb_stage2_v8_kernel(
+    const float* __restrict__ m, const float* __restrict__ v, float* __restrict__ w,
+    PT* __restrict__ w_model, OptSegs segs, const float* __restrict__ tensor_wd,
+    const float* __restrict__ tensor_part, const float* __restrict__ dyn, float eps, int bias_corr,
+    int trust_all) {
+  const int s = blockIdx.x;
+  const long start = segs.seg_start[s];
+  const int len = segs.seg_len[s];
+  const int t = segs.seg_tensor[s];
+  const float wd = tensor_wd[t];
+  const float lr = dyn[0];
+  const float bc1 = bias_corr ? dyn[2] : 1.f, bc2 = bias_corr ? dyn[3] : 1.f;
+  float ratio = 1.f;
+  if (wd != 0.f || trust_all) {
+    const float wn = sqrtf(tensor_part[2 * t]), un = sqrtf(tensor_part[2 * t + 1]);
+    ratio = (wn > 0.f && un > 0.f) ? wn / un : 1.f;
+  }
+  const float step = lr * ratio;
+  for (int i0 = threadIdx.x * 8; i0 < len; i0 += 256 * 8 * LAMB_U) {
+    float mv[LAMB_U][8], vv[LAMB_U][8], wv[LAMB_U][8];
+#pragma unroll
+    for (int u = 0; u < LAMB_U; ++u) {
+      const int i = i0 + u * 256 * 8;
+      if (i < len) {
+        const long k = start + i;
+        load8(m, k, mv[u]);
+        load8(v, k, vv[u]);
+        load8(w, k, wv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < LAMB_U; ++u) {
+      const int i = i0 + u * 256 * 8;
+      if (i < len) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float up = (mv[u][j] * bc1) / (sqrtf(vv[u][j] * bc2) + eps) + wd * wv[u][j];
+          wv[u][j] -= step * up;
+        }
+        const long k = start + i;
+        store8(w, k, wv[u]);
+        if (w_model) store8(w_model, k, wv[u]);
+      }
+    }
+  }
 }
 
 template <typename GT>
@@ -232,15 +361,26 @@ extern "C" int ct_lamb(const void* g, int gdt, float* m, float* v, float* w, voi
                        float beta1, float beta2, float eps, int bias_corr, int trust_all,
                        float* seg_part, float* tensor_part, int stage, hipStream_t stream) {
   OptSegs segs{seg_tensor, seg_start, seg_len};
+  // the 8-element form needs 16-byte aligned bases (segments start at 64-element multiples)
+  static const bool v8_env = [] { const char* e = getenv("CLOUDTIK_AMD_LAMB_V8"); return !e || atoi(e) != 0; }();
+  const bool v8 = v8_env && !(((uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)w | (uintptr_t)w_model) & 15);
   if (stage & 1) {
-    if (gdt == 1)
+    if (v8 && gdt == 1)
+      lamb_stage1_v8_kernel<bf16_t><<<nseg, 256, 0, stream>>>((const bf16_t*)g, m, v, w, segs, tensor_wd, dyn, beta1, beta2, eps, bias_corr, seg_part);
+    else if (v8)
+      lamb_stage1_v8_kernel<float><<<nseg, 256, 0, stream>>>((const float*)g, m, v, w, segs, tensor_wd, dyn, beta1, beta2, eps, bias_corr, seg_part);
+    else if (gdt == 1)
       lamb_stage1_kernel<bf16_t><<<nseg, 256, 0, stream>>>((const bf16_t*)g, m, v, w, segs, tensor_wd, dyn, beta1, beta2, eps, bias_corr, seg_part);
     else
       lamb_stage1_kernel<float><<<nseg, 256, 0, stream>>>((const float*)g, m, v, w, segs, tensor_wd, dyn, beta1, beta2, eps, bias_corr, seg_part);
     seg_to_tensor_kernel<<<ceil_div(T, 4), 256, 0, stream>>>(seg_part, tensor_first_seg, T, tensor_part);
   }
   if (stage & 2) {
-    if (pdt == 1)
+    if (v8 && pdt == 1)
+      lamb_stage2_v8_kernel<bf16_t><<<nseg, 256, 0, stream>>>(m, v, w, (bf16_t*)w_model, segs, tensor_wd, tensor_part, dyn, eps, bias_corr, trust_all);
+    else if (v8)
+      lamb_stage2_v8_kernel<float><<<nseg, 256, 0, stream>>>(m, v, w, (float*)w_model, segs, tensor_wd, tensor_part, dyn, eps, bias_corr, trust_all);
+    else if (pdt == 1)
       lamb_stage2_kernel<bf16_t><<<nseg, 256, 0, stream>>>(m, v, w, (bf16_t*)w_model, segs, tensor_wd, tensor_part, dyn, eps, bias_corr, trust_all);
     else
       lamb_stage2_kernel<float><<<nseg, 256, 0, stream>>>(m, v, w, (float*)w_model, segs, tensor_wd, tensor_part, dyn, eps, bias_corr, trust_all);

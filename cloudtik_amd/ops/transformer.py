@@ -47,17 +47,26 @@ _FUSED_FFN_DGRAD = os.environ.get("CLOUDTIK_AMD_FUSED_FFN_DGRAD", "1") == "1"
 _FUSED_FFN_FWD = os.environ.get("CLOUDTIK_AMD_FUSED_FFN_FWD", "1") == "1"
 
 
+# The FFN1 forward keeps gelu'(z) (bf16) for backward instead of z itself (gemm_nt.hip EPI 6):
+# the forward epilogue computes the erf / exp terms anyway and is store-bound, and the FFN
+# data-gradient epilogue becomes a multiply (EPI 7) instead of ~2,150 VALU instructions per wave
+# of dGELU (profiles/r3/gemm_epilogue_cost.md).  0 = keep z (EPI 1 / EPI 2).
+_STORE_DGELU = os.environ.get("CLOUDTIK_AMD_FFN_STORE_DGELU", "1") == "1"
+
+
 def _fused_ffn1(C, x2, W1, b1f):
-    """(zb, h): zb = x2 W1^T + b1f (kept), h = gelu(zb).  None when unsupported."""
+    """(aux, h, kind): h = gelu(x2 W1^T + b1f); aux = gelu'(x2 W1^T + b1f) (kind "dgelu") or
+    the biased pre-activation itself (kind "z").  None when unsupported."""
     T, H = x2.shape
     F = W1.shape[0]
     if T % 256 or F % 256 or H % 64 or b1f.dtype != torch.bfloat16:
         return None
-    zb = torch.empty(T, F, device=x2.device, dtype=x2.dtype)
-    h = torch.empty_like(zb)
-    if not C.gemm_nt(x2, W1, h, 1, False, b1f, zb, None):
+    aux = torch.empty(T, F, device=x2.device, dtype=x2.dtype)
+    h = torch.empty_like(aux)
+    epi = 6 if _STORE_DGELU else 1
+    if not C.gemm_nt(x2, W1, h, epi, False, b1f, aux, None):
         return None
-    return zb, h
+    return aux, h, ("dgelu" if epi == 6 else "z")
 
 
 # fp32 bias-gradient accumulators of the fused FFN dgrad, one per (device, width), kept
@@ -75,18 +84,18 @@ def _zeroed_acc(device, F):
     return t
 
 
-def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f):
-    """dz = (df @ W2) * gelu'(z [+ b1f]); db1f += column sums of dz (b1f None: z already
-    holds the bias).  W2 [H, F] is read in place as the [K, N] operand (gemm_nn: no transposed
-    copy); the fp32 column sums land in db1f through the split-K reduce kernel (one slab).
-    None when unsupported."""
+def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f, dgelu=False):
+    """dz = (df @ W2) * gelu'(z [+ b1f]) -- or, ``dgelu``, (df @ W2) * z with z already holding
+    gelu'(.) (EPI 7); db1f += column sums of dz (b1f None: z already holds the bias).  W2 [H, F]
+    is read in place as the [K, N] operand (gemm_nn: no transposed copy); the fp32 column sums
+    land in db1f through the split-K reduce kernel (one slab).  None when unsupported."""
     T, F = z.shape
     if T % 256 or F % 256 or df.shape[1] % 64:
         return None
     dz = torch.empty_like(z)
     direct = db1f.dtype == torch.bfloat16 and db1f.is_contiguous()
     db = _zeroed_acc(z.device, F) if direct else torch.zeros(F, device=z.device, dtype=torch.float32)
-    if not C.gemm_nn(df, W2, dz, 2, False, b1f, z, db):
+    if not C.gemm_nn(df, W2, dz, 7 if dgelu else 2, False, None if dgelu else b1f, z, db):
         return None
     if direct:
         C.splitk_reduce_clear(db.view(1, F), db1f, True)
@@ -263,8 +272,9 @@ class _FFNBlockFn(torch.autograd.Function):
         B, S, H = x1.shape
         x2 = x1.reshape(B * S, H)
         fused = _fused_ffn1(C, x2, W1, b1f) if _FUSED_FFN_FWD else None
+        kind = None
         if fused is not None:
-            z, h = fused                        # z includes the bias
+            z, h, kind = fused                  # z includes the bias, or is gelu'(z + b1)
         else:
             z = torch.mm(x2, W1.t())
             h = C.bias_act_fwd(z, b1f, 1)
@@ -274,7 +284,7 @@ class _FFNBlockFn(torch.autograd.Function):
         y, s, mean, rstd = C.layernorm_fwd(f, b2f, x2, g2, b2, eps, False, p_hid, seed_h, off_h)
         ctx.save_for_backward(x2, z, h, s, mean, rstd)
         ctx.params = (W1, b1f, W2, b2f, g2, b2)
-        ctx.cfg = (B, S, H, p_hid, seed_h, off_h, fused is not None)
+        ctx.cfg = (B, S, H, p_hid, seed_h, off_h, kind)
         return y.view(B, S, H)
 
     @staticmethod
@@ -282,8 +292,9 @@ class _FFNBlockFn(torch.autograd.Function):
         C = _C()
         x2, z, h, s, mean, rstd = ctx.saved_tensors
         W1, b1f, W2, b2f, g2, b2 = ctx.params
-        B, S, H, p_hid, seed_h, off_h, z_biased = ctx.cfg
-        zbias = None if z_biased else b1f       # the bias gelu' still has to add to z
+        B, S, H, p_hid, seed_h, off_h, kind = ctx.cfg
+        dgelu = kind == "dgelu"                 # z holds gelu'(pre-activation) itself
+        zbias = None if kind is not None else b1f   # the bias gelu' still has to add to z
         dy2 = dy.reshape(B * S, H).contiguous()
         dg2, fg2 = _vec_grad_out(g2)
         db2, fb2 = _vec_grad_out(b2)
@@ -296,8 +307,11 @@ class _FFNBlockFn(torch.autograd.Function):
         _ready(*[p for p, f in ((g2, fg2), (b2, fb2), (b2f, fb2f)) if f])
         dW2 = _wgrad(W2, df, h)
         db1f, fb1f = _vec_grad_out(b1f)
-        dz = _fused_ffn_dgrad(C, df.contiguous(), W2, z, zbias, db1f) if _FUSED_FFN_DGRAD else None
-        if dz is None:
+        dz = _fused_ffn_dgrad(C, df.contiguous(), W2, z, zbias, db1f, dgelu) if _FUSED_FFN_DGRAD else None
+        if dz is None and dgelu:
+            dz = torch.mm(df, W2).mul_(z)
+            db1f.add_(dz.float().sum(0).to(db1f.dtype))
+        elif dz is None:
             dh = torch.mm(df, W2)
             dz = C.bias_act_bwd_into(dh, z, zbias, 1, db1f, True)
         if fb1f:

@@ -113,7 +113,10 @@ class P2PAllReducer:
 
 
 def from_env(group=None) -> Optional[P2PAllReducer]:
-    """``CLOUDTIK_P2P_ALLREDUCE_BYTES=<n>`` (> 0) enables the one-shot path for buckets up to n bytes.
+    """``CLOUDTIK_P2P_ALLREDUCE_BYTES=<n>`` (> 0) enables the one-shot path for buckets up to n bytes
+    (0 disables it); unset, the crossover measured on this node at this world size
+    (``parallel/comm_tuning.py``, written by ``bench/comm_bench.py --write-tuning``) decides, and
+    with no measurement the path stays off.
 
     The decision is COLLECTIVE: every rank contributes (hostname, n, GPU available) and the
     path is enabled only if all ranks agree and share one host, so either every rank builds a
@@ -121,8 +124,13 @@ def from_env(group=None) -> Optional[P2PAllReducer]:
     foreign IPC handles and never leaves ranks waiting in a barrier the others skipped."""
     if not dist.is_initialized():
         return None
-    n = int(os.environ.get("CLOUDTIK_P2P_ALLREDUCE_BYTES", "0") or 0)
     world = dist.get_world_size(group)
+    env = os.environ.get("CLOUDTIK_P2P_ALLREDUCE_BYTES")
+    if env is not None and env != "":
+        n = int(env)
+    else:
+        from cloudtik_amd.parallel.comm_tuning import p2p_bytes
+        n = p2p_bytes(world)
     mine = (socket.gethostname(), n, bool(torch.cuda.is_available()))
     votes: List = [None] * world
     dist.all_gather_object(votes, mine, group=group)

@@ -59,6 +59,43 @@ def test_gemm_nt_bias_gelu_aux():
     _close(h, _gelu(z))
 
 
+def test_gemm_nt_bias_gelu_stores_derivative():
+    """EPI 6: h = gelu(z), aux = gelu'(z) (the FFN1 forward's derivative-storing epilogue)."""
+    C = _C()
+    M, N, K = 1024, 512, 256
+    A, B, bias = _rand(M, K, seed=14), _rand(N, K, scale=K ** -0.5, seed=15), _rand(N, scale=0.5, seed=16)
+    h = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    g = torch.empty_like(h)
+    assert C.gemm_nt(A, B, h, 6, False, bias, g, None)
+    z = A.float() @ B.float().t() + bias.float()
+    _close(h, _gelu(z))
+    _close(g, _gelu_grad(z))
+    assert (g.float() - _gelu_grad(z)).abs().max().item() < 1.5e-2     # bf16 rounding of values <= 1.13
+
+
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_mul_aux_bgrad(b_kn):
+    """EPI 7: dz = (A . B) * aux, dbias += column sums (the FFN data gradient with the stored
+    gelu'), both operand layouts; agrees with EPI 2 on the same pre-activation."""
+    C = _C()
+    M, N, K = 1024, 768, 320
+    A = _rand(M, K, seed=17)
+    B = _rand(K, N, seed=18, scale=K ** -0.5) if b_kn else _rand(N, K, seed=18, scale=K ** -0.5)
+    mm = C.gemm_nn if b_kn else C.gemm_nt
+    ref_ab = A.float() @ (B.float() if b_kn else B.float().t())
+    z = _rand(M, N, seed=19)
+    g = _gelu_grad(z.float()).to(torch.bfloat16)
+    dz = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    db = torch.full((N,), -0.5, device="cuda", dtype=torch.float32)
+    assert mm(A, B, dz, 7, False, None, g, db)
+    ref = ref_ab * g.float()
+    _close(dz, ref)
+    torch.testing.assert_close(db, ref.sum(0) - 0.5, rtol=2e-3, atol=2e-2 * max(1.0, ref.abs().sum(0).max().item() / M))
+    dz2 = torch.empty_like(dz)
+    assert mm(A, B, dz2, 2, False, None, z, None)                       # the recomputing epilogue
+    assert (dz.float() - dz2.float()).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())
+
+
 def test_gemm_nt_dgelu_bgrad():
     C = _C()
     M, N, K = 1024, 512, 320
@@ -243,3 +280,36 @@ def test_gemm_nt_stream_refuses_unsupported():
     A, B = _rand(300, 64), _rand(256, 64)
     D = torch.empty(300, 256, device="cuda", dtype=torch.bfloat16)
     assert not C.gemm_nt_stream(A, B, D, None, False, 0)
+
+
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_staggered_grid_covers_every_tile(b_kn):
+    """>= 2 rounds of tiles (8192 x 4096: 512 tiles on 256 CUs) launch the staggered grid: 128
+    full / column-half pairs first, the other column halves last.  Every epilogue kind must
+    still write every tile exactly once (plain, accumulate, bias-GELU + gelu', x gelu' + bias
+    grad)."""
+    C = _C()
+    M, N, K = 8192, 4096, 128
+    mm = C.gemm_nn if b_kn else C.gemm_nt
+    A = _rand(M, K, seed=31)
+    B = _rand(K, N, seed=32, scale=K ** -0.5) if b_kn else _rand(N, K, seed=32, scale=K ** -0.5)
+    ref = A.float() @ (B.float() if b_kn else B.float().t())
+    D = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert mm(A, B, D, 0, False, None, None, None)
+    _close(D, ref)
+    base = _rand(M, N, seed=33)
+    D2 = base.clone()
+    assert mm(A, B, D2, 0, True, None, None, None)
+    _close(D2, ref + base.float())
+    bias = _rand(N, scale=0.5, seed=34)
+    h, g = torch.full_like(D, float("nan")), torch.full_like(D, float("nan"))
+    assert mm(A, B, h, 6, False, bias, g, None)
+    z = ref + bias.float()
+    _close(h, _gelu(z))
+    _close(g, _gelu_grad(z))
+    db = torch.zeros(N, device="cuda", dtype=torch.float32)
+    dz = torch.full_like(D, float("nan"))
+    assert mm(A, B, dz, 7, False, None, g, db)
+    want = ref * g.float()
+    _close(dz, want)
+    torch.testing.assert_close(db, want.sum(0), rtol=3e-3, atol=5e-2 * max(1.0, want.abs().sum(0).max().item() / M))

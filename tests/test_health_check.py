@@ -3,11 +3,23 @@ runtime/common/health_check.py + xinetd health-check services): role probes for 
 Postgres / Redis / HDFS from canned CLI output, the xinetd HTTP responder, and the xinetd
 runtime rendering one service per runtime with a health_check_port."""
 import io
-
-from test_configured_runtimes import _render
+import os
 
 from cloudtik_amd.core import runtime_factory as rf
 from cloudtik_amd.runtime.common.health_check import check, respond
+
+
+def _render(name, rc, env, head=False, monkeypatch=None, tmp_path=None):
+    """Render one runtime's files on a node with ``env`` (same helper as
+    tests/test_configured_runtimes.py, kept local: no test module imports another)."""
+    rt = rf.get_runtime(name, rc)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("RUNTIME_PATH", str(tmp_path))
+    if rt.spec.home_env:
+        monkeypatch.setenv(rt.spec.home_env, str(tmp_path / name))
+    out = rt.render(head)
+    return {os.path.relpath(p, tmp_path): open(p).read() for p in out}
 
 
 def runner(outputs):

@@ -181,8 +181,8 @@ def test_bert_bench_routing_matches_hf_fp32():
         torch.cuda.synchronize()
     names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
     joined = "\n".join(names)
-    for pat in (r"gemm_nt_kernel<1, false, 0, 0",          # FFN1 + bias + erf-GELU (+ pre-activation)
-                r"gemm_nt_kernel<2, (true|false), 0, 2",   # FFN dgrad + dGELU (+ bias grad)
+    for pat in (r"gemm_nt_kernel<[16], false, 0, 0",       # FFN1 + bias + erf-GELU (+ gelu' or pre-activation)
+                r"gemm_nt_kernel<[27], (true|false), 0, 2",  # FFN dgrad x gelu' (+ bias grad)
                 r"gemm_nt_kernel<0, false, 0, 2",          # one-tile data-gradient sites (NN)
                 r"gemm_nt_kernel<\d, false, 0, 1",         # MFMA weight gradients (TN)
                 r"attn_fwd", r"attn_bwd", r"ln_fwd", r"ln_bwd"):

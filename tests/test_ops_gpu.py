@@ -189,6 +189,33 @@ def test_fused_optimizers_match_torch_path(cuda, name):
     assert _rel(outs[0], outs[1]) < 2e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_lamb_large_tensors_match_cpu(cuda, dtype):
+    """LAMB's 8-wide kernels over multi-segment tensors (3M weights: 367 full 8K segments and a
+    partial one, every per-thread chunk of a segment used) against the CPU implementation."""
+    from cloudtik_amd.train.optim import FlatParamSpace, FusedLAMB
+
+    def make(dev):
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(1024, 2936), torch.nn.LayerNorm(2936), torch.nn.Linear(2936, 40))
+        return m.to(dev).to(dtype)
+
+    outs = []
+    for dev in (cuda, "cpu"):
+        m = make(dev)
+        named = list(m.named_parameters())
+        sp = FlatParamSpace([p for _, p in named], names=[n for n, _ in named])
+        opt = FusedLAMB(sp, lr=1e-2, weight_decay=0.01, no_decay=lambda n: n.endswith("bias"), space=sp)
+        for it in range(2):
+            g = torch.Generator().manual_seed(7 + it)
+            x = torch.randn(32, 1024, generator=g).to(dev).to(dtype)
+            m(x).float().pow(2).mean().backward()
+            opt.step()
+            opt.zero_grad()
+        outs.append(sp.shard_params.detach().float().cpu())
+    assert _rel(outs[0], outs[1]) < (1e-5 if dtype == torch.float32 else 2e-2)
+
+
 @pytest.mark.parametrize("C,HW", [(64, 56), (256, 14), (2048, 7)])
 @pytest.mark.parametrize("res", [False, True])
 def test_batchnorm_act(cuda, C, HW, res):
