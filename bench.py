@@ -493,23 +493,32 @@ class GpuTelemetry:
 
 # ------------------------------------------------------------------ timing
 def kernel_audit(step, device):
-    """One extra UNTIMED step under torch.profiler: how many GPU kernels ran, and how many of
-    them are MIOpen's naive convolution fallbacks (ConvDirectNaive*: 25-200 ms per call; a
-    correctly installed solver db never selects them).  {} if profiling is unavailable."""
+    """One extra UNTIMED step: which path every convolution took (exact: the route counters of
+    ops/conv.py -- ``library_conv_calls`` > 0 means a convolution fell back to MIOpen), and how
+    many GPU kernels torch.profiler saw.  The profiler count is a LOWER bound on ROCm: roctracer
+    drops activity records (169-216 seen per ResNet-50 step against rocprofv3's 568,
+    profiles/r5/audit_probe.md), so rocprofv3 is the kernel-count authority.  {} if disabled."""
     import torch
     if device.type != "cuda" or os.environ.get("CLOUDTIK_BENCH_AUDIT", "1") == "0":
         return {}
+    from cloudtik_amd.ops import conv as CV
+    before = dict(CV.ROUTES)
+    out = {}
     try:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CUDA]) as prof:
             step()
             torch.cuda.synchronize()
         names = [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+        naive = sorted({n for n in names if "naive" in n.lower()})
+        out.update(kernels_seen_by_torch_profiler=len(names),
+                   naive_conv_launches_seen=sum("naive" in n.lower() for n in names), naive_conv_kernels=naive[:8])
     except Exception as e:  # noqa: BLE001
-        return {"error": repr(e)[:200]}
-    naive = sorted({n for n in names if "naive" in n.lower()})
-    return {"kernels_per_step": len(names), "naive_conv_launches": sum("naive" in n.lower() for n in names),
-            "naive_conv_kernels": naive[:8]}
+        out["profiler_error"] = repr(e)[:200]
+    out.update(igemm_conv_calls=CV.ROUTES["igemm"] - before["igemm"],
+               library_conv_calls=CV.ROUTES["library"] - before["library"],
+               kernel_count_authority="rocprofv3 --kernel-trace (torch.profiler undercounts on ROCm)")
+    return out
 
 
 def bucket_timeline(step, bucketer, device):

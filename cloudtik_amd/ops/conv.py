@@ -529,13 +529,20 @@ class ConvFn(torch.autograd.Function):
 
 BN_STATS = os.environ.get("CLOUDTIK_AMD_CONV_BN_STATS", "1") == "1"
 
+# forward convolutions by route since import: "igemm" = the in-tree MFMA kernels (stem
+# included), "library" = the module's own forward (MIOpen).  bench.py's ResNet audit reads the
+# delta over one step -- an exact count, unlike a kernel trace taken in-process.
+ROUTES = {"igemm": 0, "library": 0}
+
 
 def conv2d(x: torch.Tensor, conv: torch.nn.Conv2d, keep_input: bool = False, bn_stats: bool = False):
     """``conv(x)`` on the implicit-GEMM kernels when eligible, else ``conv(x)``; with
     ``keep_input`` returns ``(conv(x), x_alias)`` (see ConvFn); ``bn_stats``: the output feeds a
     training-mode BatchNorm, so the epilogue also reduces its statistics."""
     if conv.bias is not None or not eligible(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups):
+        ROUTES["library"] += 1
         return (conv(x), x) if keep_input else conv(x)
+    ROUTES["igemm"] += 1
     return ConvFn.apply(x, conv.weight, tuple(conv.stride), tuple(conv.padding), keep_input,
                         bool(bn_stats and BN_STATS))
 
@@ -641,5 +648,7 @@ class StemFn(torch.autograd.Function):
 def stem_conv(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
     """``conv(x)`` for the image-batch stem on the kernels' pixel-chunk mode when eligible."""
     if not stem_eligible(x, conv):
+        ROUTES["library"] += 1
         return conv(x)
+    ROUTES["igemm"] += 1
     return StemFn.apply(to_nhwc8(x), conv.weight, tuple(conv.stride), tuple(conv.padding))

@@ -65,6 +65,7 @@ struct NtArgs {
   int M, N, K;
   int accumulate;       // EPI 0: D += result
   int stagger;          // NT / NN one-tile grid: H column-half tiles at each end (0 = none), below
+  int group_m;          // NT / NN: M-tiles walked per N-tile in the XCD tile order (1 = row-major)
 };
 
 __device__ __forceinline__ int nt_swz(int r) { return (r >> 1) & 7; }
@@ -587,7 +588,20 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_kernel(NtArgs a) {
   int L = xcd_remap(v, SPLIT ? gridDim.x : tiles);
   const int split = SPLIT ? L / tiles : 0;
   L -= split * tiles;
-  const int tm = L / tiles_n, tn = L % tiles_n;
+  // tile order of the blocks that share an XCD (consecutive L): a.group_m > 1 walks group_m
+  // M-tiles for each N-tile (a group_m x (32 / group_m) block of tiles runs at once per XCD,
+  // instead of 2 M-rows x every N-tile), so fewer distinct A / B panels stream into each XCD's
+  // 4 MiB L2 per round
+  int tm, tn;
+  if (!SPLIT && a.group_m > 1) {
+    const int gsz = a.group_m * tiles_n;
+    const int g = L / gsz, r = L - g * gsz;
+    tm = g * a.group_m + r % a.group_m;
+    tn = r / a.group_m;
+  } else {
+    tm = L / tiles_n;
+    tn = L % tiles_n;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: staging bases in SGPRs
   const int wr = wave >> 2, wc = wave & 3;
@@ -959,14 +973,20 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   const long tiles = (long)(M / NT_BM) * (N / NT_BN);
   if (tiles > (1L << 30)) return 5;
   // stagger half of the first round's CUs by half a tile when the grid has >= 2 rounds
-  // (CLOUDTIK_AMD_GEMM_STAGGER: -1 auto (default), 0 off, H > 0 forces H half-tile pairs)
-  static const int stag_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_STAGGER"); return e ? atoi(e) : -1; }();
+  // (CLOUDTIK_AMD_GEMM_STAGGER: -1 auto, 0 off (default), H > 0 forces H half-tile pairs).
+  // Off by default: BERT-large 73.06 / 72.96 ms/step without it, 77.23 / 77.25 with the auto
+  // stagger (same box, interleaved; profiles/r5/SUMMARY.md) -- the half tiles stage every
+  // operand and keep every barrier, so they cost nearly a full tile, and the grid grows by H.
+  static const int stag_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_STAGGER"); return e ? atoi(e) : 0; }();
   int H = 0;
   if (stag_env > 0) H = (int)std::min<long>(stag_env, tiles / 2);
   else if (stag_env < 0 && tiles >= 2L * nt_cu_count()) H = nt_cu_count() / 2;
   const long blocks = tiles + H;
+  // CLOUDTIK_AMD_GEMM_GROUP_M: M-tiles per N-tile in the tile order (must divide M / 256)
+  static const int gm_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_GROUP_M"); return e ? atoi(e) : 1; }();
+  const int gm = (gm_env > 1 && (M / NT_BM) % gm_env == 0) ? gm_env : 1;
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias, nullptr,
-           nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, accumulate, H};
+           nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, accumulate, H, gm};
   static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_DIAG"); return e ? atoi(e) : 0; }();
   if (diag == 4) {
     if (b_kn) gemm_nt_kernel<NT_EPI_NONE, false, 0, 2><<<(int)blocks, NT_THREADS, 0, stream>>>(a);

@@ -74,10 +74,11 @@ __device__ __forceinline__ void store8(bf16_t* p, long i, const float (&v)[8]) {
 }
 
 // LAMB over a segment with every load of the thread's share issued before any math: U chunks
-// of 8 elements per thread (a whole 8K segment in one pass at U = 4, 256 threads).  The
-// one-vec4-per-iteration form kept a single 56-byte load group in flight per thread and ran at
-// 3.4-3.8 TB/s (profiles/r4/pmc_bert-large_r4late.md); segments are 64-element multiples, so a
-// chunk that starts inside the segment ends inside it.
+// of 8 elements per thread (a whole 8K segment in one pass at U = 4, 256 threads); segments are
+// 64-element multiples, so a chunk that starts inside the segment ends inside it.  Opt-in
+// (CLOUDTIK_AMD_LAMB_V8=1): in the BERT-large step stage 1 took 1.386 ms against 1.257 for the
+// one-vec4-per-iteration kernel and stage 2 the same 1.13 ms (profiles/r5/steady_bert_large_head_r5a.md)
+// -- the two passes are HBM-bound as they are, more bytes in flight per thread buy nothing.
 constexpr int LAMB_U = 4;
 
 template <typename GT>
@@ -362,7 +363,7 @@ extern "C" int ct_lamb(const void* g, int gdt, float* m, float* v, float* w, voi
                        float* seg_part, float* tensor_part, int stage, hipStream_t stream) {
   OptSegs segs{seg_tensor, seg_start, seg_len};
   // the 8-element form needs 16-byte aligned bases (segments start at 64-element multiples)
-  static const bool v8_env = [] { const char* e = getenv("CLOUDTIK_AMD_LAMB_V8"); return !e || atoi(e) != 0; }();
+  static const bool v8_env = [] { const char* e = getenv("CLOUDTIK_AMD_LAMB_V8"); return e && atoi(e) != 0; }();
   const bool v8 = v8_env && !(((uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)w | (uintptr_t)w_model) & 15);
   if (stage & 1) {
     if (v8 && gdt == 1)

@@ -8,7 +8,7 @@ cd "$R"
 timeout -k 10 400 python -u -m pytest tests/test_gemm_nt_gpu.py tests/test_model_parity.py tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > "$O/tests.txt" 2>&1 \
  && tail -1 "$O/tests.txt" \
  && bash "$R/scripts/gpu_ab_cfgs.sh" "$TAG/ab" 2 bert-large "new:" "nostag:CLOUDTIK_AMD_GEMM_STAGGER=0" \
-      "old_ffn:CLOUDTIK_AMD_FFN_STORE_DGELU=0,CLOUDTIK_AMD_GEMM_STAGGER=0,CLOUDTIK_AMD_LAMB_V8=0"
+      "old_ffn:CLOUDTIK_AMD_FFN_STORE_DGELU=0;CLOUDTIK_AMD_GEMM_STAGGER=0;CLOUDTIK_AMD_LAMB_V8=0"
 rc=$?
 [ $rc -eq 0 ] || { grep -E "FAIL|Error" "$O/tests.txt" | head; }
 exit $rc

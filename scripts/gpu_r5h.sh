@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG=${1:-r5h}
+O="$R/gpurun_out/$TAG"
+mkdir -p "$O"
+cd "$R"
+timeout -k 10 600 python -u -m pytest tests/test_gemm_nt_gpu.py tests/test_ops_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread > "$O/tests.txt" 2>&1 \
+ && tail -1 "$O/tests.txt" \
+ && bash "$R/scripts/gpu_ab_cfgs.sh" "$TAG/ab" 2 bert-large "base:" "gm4:CLOUDTIK_AMD_GEMM_GROUP_M=4" "gm8:CLOUDTIK_AMD_GEMM_GROUP_M=8"
+rc=$?
+[ $rc -eq 0 ] || { grep -E "FAIL|Error" "$O/tests.txt" | head; }
+exit $rc

@@ -282,12 +282,29 @@ def test_gemm_nt_stream_refuses_unsupported():
     assert not C.gemm_nt_stream(A, B, D, None, False, 0)
 
 
+@pytest.mark.parametrize("knob", ["CLOUDTIK_AMD_GEMM_STAGGER=-1", "CLOUDTIK_AMD_GEMM_GROUP_M=4"])
+def test_gemm_staggered_grid_covers_every_tile_subprocess(knob):
+    """The opt-in tile orders -- the staggered grid (CLOUDTIK_AMD_GEMM_STAGGER=-1: 128 full /
+    column-half pairs first, the other column halves last, on a >= 2-round grid) and the
+    grouped-M order (CLOUDTIK_AMD_GEMM_GROUP_M=4) -- still write every tile exactly once for
+    every epilogue kind: the test below in a child process with the knob on (the library reads
+    it once per process)."""
+    import os
+    import subprocess
+    import sys
+    k, v = knob.split("=")
+    env = dict(os.environ, **{k: v})
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", __file__, "-k", "staggered_grid_covers_every_tile and not subprocess",
+                        "-p", "no:cacheprovider"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("b_kn", [False, True])
 def test_gemm_staggered_grid_covers_every_tile(b_kn):
-    """>= 2 rounds of tiles (8192 x 4096: 512 tiles on 256 CUs) launch the staggered grid: 128
-    full / column-half pairs first, the other column halves last.  Every epilogue kind must
-    still write every tile exactly once (plain, accumulate, bias-GELU + gelu', x gelu' + bias
-    grad)."""
+    """>= 2 rounds of tiles (8192 x 4096: 512 tiles on 256 CUs); with the stagger on (the
+    subprocess test above) 128 full / column-half pairs come first and the other column halves
+    last.  Every epilogue kind must write every tile exactly once (plain, accumulate,
+    bias-GELU + gelu', x gelu' + bias grad)."""
     C = _C()
     M, N, K = 8192, 4096, 128
     mm = C.gemm_nn if b_kn else C.gemm_nt

@@ -216,6 +216,18 @@ def test_fused_lamb_large_tensors_match_cpu(cuda, dtype):
     assert _rel(outs[0], outs[1]) < (1e-5 if dtype == torch.float32 else 2e-2)
 
 
+def test_fused_lamb_v8_kernels_subprocess():
+    """The opt-in 8-wide LAMB kernels (CLOUDTIK_AMD_LAMB_V8=1, read once per process) pass the
+    same large-tensor check in a child process."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, CLOUDTIK_AMD_LAMB_V8="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", __file__, "-k", "fused_lamb_large_tensors_match_cpu",
+                        "-p", "no:cacheprovider"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("C,HW", [(64, 56), (256, 14), (2048, 7)])
 @pytest.mark.parametrize("res", [False, True])
 def test_batchnorm_act(cuda, C, HW, res):
