@@ -348,6 +348,16 @@ __device__ __forceinline__ u16x8 nt_pair_swap(u16x4 x, u16x4 y) {
   return __builtin_bit_cast(u16x8, v);
 }
 
+// inverse of nt_pair_swap (the lane swap is an involution): 8 consecutive columns loaded in the
+// store layout -> this lane's 4 columns of blocks j (x) and j + 1 (y) in the MFMA layout
+__device__ __forceinline__ void nt_pair_unswap(u16x8 v, u16x4& x, u16x4& y) {
+  const uint4 w = __builtin_bit_cast(uint4, v);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(w.x, w.z, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(w.y, w.w, false, false);
+  x = __builtin_bit_cast(u16x4, uint2{r0[0], r1[0]});
+  y = __builtin_bit_cast(u16x4, uint2{r0[1], r1[1]});
+}
+
 // epilogue over one wave's accumulators: acc[i][j][r] holds D[mrow + 16i][ncol + 16j + r]
 // (ncol includes this lane's 4 (lane >> 4)); math in that layout, stores after the swap.
 // EPI 3 (fp32 split-K slab, row stride N): the lane's 4 columns are one 16-B store already.
@@ -419,11 +429,25 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
   // column of this lane's 16-B chunk after the swap, relative to block 0 of the pair
   const int g = lane >> 4;
   const long scol = (ncol - 4 * g) + 16 * (g & 1) + 8 * (g >> 1);
-  // dGELU: the pre-activation rows are loaded two rows ahead of their use (a ring of two
-  // row buffers, compile-time indexed in the unrolled row loop; rows 0 and 1 by
-  // nt_preload_z); loaded at the row itself, every row waited a full memory latency
-  auto& zq = pre.z;
-  nt_preload_z<EPI, NJ>(a, mrow, ncol, pre);
+  // The tensor the epilogue reads (EPI 2 / 7: aux; EPI 0 accumulating: D itself) is loaded for
+  // all 8 row blocks up front, as 16-byte pieces in the store layout (full 64-byte row
+  // segments), then turned into the MFMA layout (nt_pair_unswap): one memory latency per tile
+  // instead of one per row block (a two-row-ahead ring of 8-byte loads before: the EPI 7
+  // epilogue cost 19.6 us per tile-round against 14.6 for EPI 6, profiles/r5/gemm_epilogue_probe.md).
+  // The fragment registers of the K loop are dead here, so the 64 VGPRs come free.
+  constexpr bool RD = EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_MUL_AUX_BGRAD || EPI == NT_EPI_PLAIN;
+  u16x8 zin[RD ? 8 : 1][NJ / 2];
+  if constexpr (RD) {
+    const bool rd = EPI != NT_EPI_PLAIN || a.accumulate;
+    const bf16_t* src = EPI == NT_EPI_PLAIN ? a.D : a.aux;
+    const long ld = EPI == NT_EPI_PLAIN ? a.ldd : a.ldaux;
+    if (rd) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int p = 0; p < NJ / 2; ++p) zin[i][p] = *(const u16x8*)(src + (mrow + i * 16) * ld + scol + p * 32);
+    }
+  }
 
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -438,9 +462,10 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
     } else if constexpr (EPI == NT_EPI_PLAIN) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const long n = ncol + j * 16;
         if (a.accumulate) {
-          const u16x4 old = *(const u16x4*)(a.D + m * a.ldd + n);
+          u16x4 old, old2;
+          nt_pair_unswap(zin[i][j >> 1], old, old2);
+          if (j & 1) old = old2;
 #pragma unroll
           for (int r = 0; r < 4; ++r) out[j][r] = f2bf(acc[i][j][r] + bf2f(old[r]));
         } else {
@@ -475,11 +500,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
         // dz = dh * gelu'(z): the derivative was stored by the forward (EPI 6)
         u16x4 z[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) z[j] = zq[i & 1][j];
-        if (i + 2 < 8) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) zq[i & 1][j] = *(const u16x4*)(a.aux + (m + 32) * a.ldaux + ncol + j * 16);
-        }
+        for (int p = 0; p < NJ / 2; ++p) nt_pair_unswap(zin[i][p], z[2 * p], z[2 * p + 1]);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
 #pragma unroll
@@ -511,11 +532,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
         // BERT-large FFN dgrad)
         u16x4 z[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) z[j] = zq[i & 1][j];
-        if (i + 2 < 8) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) zq[i & 1][j] = *(const u16x4*)(a.aux + (m + 32) * a.ldaux + ncol + j * 16);
-        }
+        for (int p = 0; p < NJ / 2; ++p) nt_pair_unswap(zin[i][p], z[2 * p], z[2 * p + 1]);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
 #pragma unroll
@@ -982,8 +999,10 @@ extern "C" int ct_gemm_nt(const void* A, long lda, const void* B, long ldb, void
   if (stag_env > 0) H = (int)std::min<long>(stag_env, tiles / 2);
   else if (stag_env < 0 && tiles >= 2L * nt_cu_count()) H = nt_cu_count() / 2;
   const long blocks = tiles + H;
-  // CLOUDTIK_AMD_GEMM_GROUP_M: M-tiles per N-tile in the tile order (must divide M / 256)
-  static const int gm_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_GROUP_M"); return e ? atoi(e) : 1; }();
+  // CLOUDTIK_AMD_GEMM_GROUP_M: M-tiles per N-tile in the tile order (must divide M / 256).
+  // Default 4: BERT-large 72.68 -> 72.43 ms/step (2 interleaved rounds, one box; 8: 73.08;
+  // profiles/r5/SUMMARY.md)
+  static const int gm_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_GROUP_M"); return e ? atoi(e) : 4; }();
   const int gm = (gm_env > 1 && (M / NT_BM) % gm_env == 0) ? gm_env : 1;
   NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, dbias, nullptr,
            nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, accumulate, H, gm};

@@ -282,7 +282,7 @@ def test_gemm_nt_stream_refuses_unsupported():
     assert not C.gemm_nt_stream(A, B, D, None, False, 0)
 
 
-@pytest.mark.parametrize("knob", ["CLOUDTIK_AMD_GEMM_STAGGER=-1", "CLOUDTIK_AMD_GEMM_GROUP_M=4"])
+@pytest.mark.parametrize("knob", ["CLOUDTIK_AMD_GEMM_STAGGER=-1", "CLOUDTIK_AMD_GEMM_GROUP_M=1"])
 def test_gemm_staggered_grid_covers_every_tile_subprocess(knob):
     """The opt-in tile orders -- the staggered grid (CLOUDTIK_AMD_GEMM_STAGGER=-1: 128 full /
     column-half pairs first, the other column halves last, on a >= 2-round grid) and the
