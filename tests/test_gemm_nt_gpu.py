@@ -284,11 +284,11 @@ def test_gemm_nt_stream_refuses_unsupported():
 
 @pytest.mark.parametrize("knob", ["CLOUDTIK_AMD_GEMM_STAGGER=-1", "CLOUDTIK_AMD_GEMM_GROUP_M=1"])
 def test_gemm_staggered_grid_covers_every_tile_subprocess(knob):
-    """The opt-in tile orders -- the staggered grid (CLOUDTIK_AMD_GEMM_STAGGER=-1: 128 full /
-    column-half pairs first, the other column halves last, on a >= 2-round grid) and the
-    grouped-M order (CLOUDTIK_AMD_GEMM_GROUP_M=4) -- still write every tile exactly once for
-    every epilogue kind: the test below in a child process with the knob on (the library reads
-    it once per process)."""
+    """The non-default tile orders -- the staggered grid (CLOUDTIK_AMD_GEMM_STAGGER=-1: 128 full /
+    column-half pairs first, the other column halves last, on a >= 2-round grid) and the plain
+    row-major order (CLOUDTIK_AMD_GEMM_GROUP_M=1; the default walks 4 M-tiles per N-tile) --
+    still write every tile exactly once for every epilogue kind: the test below in a child
+    process with the knob set (the library reads it once per process)."""
     import os
     import subprocess
     import sys
