@@ -64,6 +64,17 @@ __device__ __forceinline__ bf16x8_t gload_frag(const bf16_t* p, bool valid) {
 __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+typedef __attribute__((address_space(3))) void at_lds_void;
+// global_load_lds_dwordx4: lane l's 16 bytes at sbase + voff land at LDS wave_base + 16 l (one
+// 1 KB wave instruction, no staging registers).  sbase must be wave-uniform.  The compiler does
+// not count these in vmcnt: callers wait with s_waitcnt vmcnt(0) before the barrier.
+__device__ __forceinline__ void at_glds16s(const void* sbase, unsigned voff, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(at_lds_void*)lds_wave_base);
+  const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)sbase) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)sbase >> 32)) << 32);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
+               : "memory", "m0");
+}
 // Store a 64-wide row held as two 32x32 MFMA accumulators in the "row on the lane" layout:
 // lane (r, hh) holds columns d = 8 g + 4 hh .. + 3 of row r (A0: d < 32, A1: d + 32).  A
 // v_permlane32_swap of the (g, g + 1) pair between the lane halves leaves each lane 8
@@ -124,7 +135,14 @@ constexpr int kRelBiasMax = 4096;   // LDS floats for one head's relative-offset
 // workgroup).  The compiler's default budget (236 VGPR + 32 AGPR) allowed ONE resident
 // workgroup per CU, so a workgroup's Q/K/V loads never overlapped another's MFMAs; at 2 the
 // kernel fits in ~170 VGPRs without spills.
-template <bool DROP, bool CAUSAL, bool REL = false, int WPE = 2>
+// GL: K/V tiles go global -> LDS by global_load_lds (at_glds16s) instead of through the
+// stK/stV (+ k1/v1) staging registers: wave w DMAs rows 16 w .. 16 w + 15 of the K and the V
+// tile (two 1 KB wave instructions each).  Lane l lands at physical chunk l & 7 of row
+// 16 w + 8 i + (l >> 3), so it fetches logical chunk (l & 7) ^ rev3(((row >> 1) & 7)) =
+// (l & 7) ^ rev3((4 i + (l >> 4)) & 7) -- the same swizzled image the register path writes.
+// Keys past Sk read key Sk - 1 (finite data; their -inf key bias zeroes them), so no load is
+// out of bounds and no zero fill is needed.
+template <bool DROP, bool CAUSAL, bool REL = false, int WPE = 2, bool GL = false>
 __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   // [buf][K,V][64 rows][128 B] then [buf][64] fp32 log2-domain key bias (-inf past Sk)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 64 * 128 + 2 * 64 * 4];
@@ -184,6 +202,26 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   // before the first MFMA -- one memory latency per workgroup instead of two in series, and
   // no barrier inside the loop
   const bool resident = nt == 2;
+#define FWD_GLDS(kt_, buf_)                                                                    \
+  _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                           \
+    const int row_ = 16 * w + 8 * i_ + (lane >> 3);                                            \
+    const unsigned key_ = (unsigned)min((kt_) * 64 + row_, a.Sk - 1);                          \
+    const unsigned c_ = (unsigned)((lane & 7) ^ rev3((4 * i_ + (lane >> 4)) & 7));             \
+    char* dst_ = smem + (buf_) * 16384 + (16 * w + 8 * i_) * 128;                              \
+    at_glds16s(kp, (key_ * (unsigned)a.k_ss + c_ * 8u) * 2u, dst_);                            \
+    at_glds16s(vp, (key_ * (unsigned)a.v_ss + c_ * 8u) * 2u, dst_ + 8192);                     \
+  }
+  if constexpr (GL) {
+    FWD_GLDS(0, 0);
+    if (resident) {
+      FWD_GLDS(1, 1);
+      if (tid < 128) stB = tid < a.Sk ? (kbp ? kbp[tid] * LOG2E : 0.f) : -INFINITY;
+    } else if (tid < 64) {
+      stB = tid < a.Sk ? (kbp ? kbp[tid] * LOG2E : 0.f) : -INFINITY;
+    }
+    if (tid < (resident ? 128 : 64)) kbias_lds[tid] = stB;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
   FWD_GLOAD(0);
   if (resident) {
     u16x8 k1[2], v1[2];
@@ -209,6 +247,7 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
   } else {
     FWD_SWRITE(0);
   }
+  }
   __syncthreads();
 
   const int trow = (lane >> 2) & 3;
@@ -216,7 +255,18 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
 
   for (int kt = 0; kt < nt; ++kt) {
     const int buf = kt & 1;
-    if (!resident && kt + 1 < nt) { FWD_GLOAD(kt + 1); }
+    if (!resident && kt + 1 < nt) {
+      if constexpr (GL) {
+        // buf ^ 1 was last read in tile kt - 1, which ended with a barrier
+        FWD_GLDS(kt + 1, buf ^ 1);
+        if (tid < 64) {
+          const int kk = (kt + 1) * 64 + tid;
+          stB = kk < a.Sk ? (kbp ? kbp[kk] * LOG2E : 0.f) : -INFINITY;
+        }
+      } else {
+        FWD_GLOAD(kt + 1);
+      }
+    }
     const char* Kb = smem + buf * 16384;
     const char* Vb = Kb + 8192;
     f32x16 S0, S1;
@@ -310,12 +360,18 @@ __global__ __launch_bounds__(256, WPE) void attn_fwd_d64_kernel(AttnFwdArgs a) {
         O1 = mfma32(a1, pf[t][s2], O1);
       }
     if (!resident) {
-      if (kt + 1 < nt) { FWD_SWRITE(buf ^ 1); }
+      if constexpr (GL) {
+        if (kt + 1 < nt && tid < 64) kbias_lds[(buf ^ 1) * 64 + tid] = stB;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (kt + 1 < nt) { FWD_SWRITE(buf ^ 1); }
+      }
       __syncthreads();
     }
   }
 #undef FWD_GLOAD
 #undef FWD_SWRITE
+#undef FWD_GLDS
   l += __shfl_xor(l, 32, 64);
   const float inv = l > 0.f ? (DROP ? a.inv_keep : 1.f) / l : 0.f;
   bf16_t* op = a.o + b * a.o_sb + h * a.o_sh + (long)(qvalid ? qi : 0) * a.o_ss;
@@ -875,7 +931,11 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
     const char* e = getenv("CLOUDTIK_AMD_ATTN_FWD_WPE");
     return e ? atoi(e) : 0;
   }();
-  const int wpe = (wpe_env >= 1 && wpe_env <= 3) ? wpe_env : 2;
+  static const int gl = [] {
+    const char* e = getenv("CLOUDTIK_AMD_ATTN_FWD_GLDS");
+    return e ? atoi(e) : 1;
+  }();
+  const int wpe = (wpe_env >= 1 && wpe_env <= 4) ? wpe_env : (gl ? 3 : 2);
   static const int pipe = [] {
     // opt-in: measured slower than the one-item kernel on BERT-large shapes (B 256, S 128,
     // p 0.1: 75.5 us persistent / 84.9 us one item per workgroup vs 65.9 us;
@@ -893,12 +953,16 @@ extern "C" int ct_attn_fwd(const void* q, const long* qs, const void* k, const l
     else attn_fwd_pipe_kernel<false, false><<<g1, 256, 0, stream>>>(a);
     return 0;
   }
-#define CT_ATTN_FWD(W)                                                                          \
-  if (drop && causal) attn_fwd_d64_kernel<true, true, false, W><<<grid, 256, 0, stream>>>(a);    \
-  else if (drop) attn_fwd_d64_kernel<true, false, false, W><<<grid, 256, 0, stream>>>(a);        \
-  else if (causal) attn_fwd_d64_kernel<false, true, false, W><<<grid, 256, 0, stream>>>(a);      \
-  else attn_fwd_d64_kernel<false, false, false, W><<<grid, 256, 0, stream>>>(a);
-  if (wpe == 3) { CT_ATTN_FWD(3) } else if (wpe == 1) { CT_ATTN_FWD(1) } else { CT_ATTN_FWD(2) }
+#define CT_ATTN_FWD(W, G)                                                                          \
+  if (drop && causal) attn_fwd_d64_kernel<true, true, false, W, G><<<grid, 256, 0, stream>>>(a);    \
+  else if (drop) attn_fwd_d64_kernel<true, false, false, W, G><<<grid, 256, 0, stream>>>(a);        \
+  else if (causal) attn_fwd_d64_kernel<false, true, false, W, G><<<grid, 256, 0, stream>>>(a);      \
+  else attn_fwd_d64_kernel<false, false, false, W, G><<<grid, 256, 0, stream>>>(a);
+  if (gl) {
+    if (wpe == 4) { CT_ATTN_FWD(4, true) } else if (wpe == 3) { CT_ATTN_FWD(3, true) } else { CT_ATTN_FWD(2, true) }
+  } else {
+    if (wpe == 3) { CT_ATTN_FWD(3, false) } else if (wpe == 1) { CT_ATTN_FWD(1, false) } else { CT_ATTN_FWD(2, false) }
+  }
 #undef CT_ATTN_FWD
   return 0;
 }
