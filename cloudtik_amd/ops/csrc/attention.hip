@@ -45,6 +45,12 @@ __device__ __forceinline__ int rev3(int x) { return ((x & 1) << 2) | (x & 2) | (
 // byte offset of 16-byte chunk c of `row` inside a [rows][64 x bf16] LDS tile
 __device__ __forceinline__ int swz(int row, int c) { return row * 128 + ((c ^ rev3((row >> 1) & 7)) << 4); }
 __device__ __forceinline__ int swz_e(int row, int col) { return swz(row, col >> 3) + ((col & 7) << 1); }
+// 8-byte chunk XOR of key row `key` in the backward's dS^T image ([keys][32 q], 64-byte rows).
+// Writes (ds_write_b64, 16-lane groups over 32 banks): 16 consecutive keys hit distinct
+// (parity, chunk) slots.  Transposing reads (32-lane halves over 64 banks, 8 consecutive rows
+// 8a .. 8a + 7, 4 chunks each): rows r and r + 4 share a 64-byte window and their chunk sets
+// differ in bit 2.
+__device__ __forceinline__ int dsw(int key) { return ((key >> 1) & 7) ^ (key & 4); }
 
 __device__ __forceinline__ bf16x8_t lds_b128(const char* p) {
   return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const u16x8*>(p));
@@ -771,12 +777,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
       dK0 = mfma32(aq0, dsf[s2], dK0);
       dK1 = mfma32(aq1, dsf[s2], dK1);
     }
-    // dS^T -> LDS [128 keys][32 q] (64-byte rows, 8-byte chunks XOR ((key >> 1) & 7)):
+    // dS^T -> LDS [128 keys][32 q] (64-byte rows, 8-byte chunks XOR dsw(key), below):
     // each lane owns one key row and 4 runs of 4 consecutive queries -> 4 ds_write_b64
     {
       const int key = w * 32 + r;
       char* rowp = dSt + key * 64;
-      const int sw = (key >> 1) & 7;
+      const int sw = dsw(key);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = 2 * g + hh;     // 8-byte chunk = queries 8g + 4hh .. +3
@@ -790,13 +796,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     // dQ[q][d] = sum over the 128 keys of dS[q][key] K[key][d], 16x16x32 MFMAs issued as
     // (K^T fragment, dS fragment): the lane ends up with 4 consecutive d of one query.  Both
     // fragments (8 consecutive keys per lane) come from transposing reads of [key][.] images.
+    // The key rows a lane reads are a permutation of the natural 8 fg + 4 j + fq (bits 2 and 3
+    // swapped: 16 (fg >> 1) + 8 j + 4 (fg & 1) + fq), the same for both operands, so the sum
+    // over keys is unchanged: each 32-lane half of a transposing read then covers 8
+    // consecutive rows, whose swizzled chunks of K (swz) and of dS^T (dsw) fill all 64 banks
+    // (with the natural order rows r and r + 8 of K shared banks: a 2-way conflict on every
+    // K^T read).
     f32x4 dq0 = {0.f, 0.f, 0.f, 0.f}, dq1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const int kr0 = 32 * ks + 8 * fg + fq, kr1 = kr0 + 4;
+      const int kr0 = 32 * ks + 16 * (fg >> 1) + 4 * (fg & 1) + fq, kr1 = kr0 + 8;
       const int qc = (dq_q0 >> 2) + fp;        // 8-byte chunk of queries dq_q0 + 4 fp .. + 3
-      const bf16x8_t sf = cat_tr(lds_tr(dSt + kr0 * 64 + ((qc ^ ((kr0 >> 1) & 7)) << 3)),
-                                 lds_tr(dSt + kr1 * 64 + ((qc ^ ((kr1 >> 1) & 7)) << 3)));
+      const bf16x8_t sf = cat_tr(lds_tr(dSt + kr0 * 64 + ((qc ^ dsw(kr0)) << 3)),
+                                 lds_tr(dSt + kr1 * 64 + ((qc ^ dsw(kr1)) << 3)));
       const bf16x8_t kf0 = cat_tr(lds_tr(Ks + swz_e(kr0, dq_d0 + 4 * fp)), lds_tr(Ks + swz_e(kr1, dq_d0 + 4 * fp)));
       const bf16x8_t kf1 = cat_tr(lds_tr(Ks + swz_e(kr0, dq_d0 + 16 + 4 * fp)),
                                   lds_tr(Ks + swz_e(kr1, dq_d0 + 16 + 4 * fp)));
