@@ -598,7 +598,7 @@ struct AttnBwdArgs {
   uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
 };
 
-template <bool DROP, bool CAUSAL>
+template <bool DROP, bool CAUSAL, bool MULTI>
 __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   // LDS: Q tiles 2 x 4K | dO tiles 2 x 4K | K block 16K | V block 16K | dS^T 2 x 8K | lse, delta 2 x 256 B
   // The per-q-tile inputs (Q, dO, lse, delta) and dS^T are double-buffered, so one barrier per
@@ -653,7 +653,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   const int trow = (lane >> 2) & 3;
   const int tcol = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
   const int nq = (a.Sq + 31) / 32;
-  const bool single_block = gridDim.x == 1;
+  // MULTI: Sk > 128, several key blocks per (batch, head) -> dQ summed by fp32 atomics
+  constexpr bool single_block = !MULTI;
   // 16-byte dQ stores need 8-element strides and a 16-byte aligned base
   const bool dq16 = ((a.dq_ss | a.dq_sb | a.dq_sh) & 7) == 0 && (((uintptr_t)a.dq) & 15) == 0;
   // this wave's share of the tile's dQ: queries 16 (w & 1) .. +16, d 32 (w >> 1) .. +32
@@ -792,6 +793,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     }
     __syncthreads();   // the ONLY barrier of the tile: dS^T complete; this tile's Q / dO / lse /
                        // delta buffers free; tile t+1's staged buffers visible
+    // tile qt + 2's inputs into the buffers tile qt released at this barrier (staging after the
+    // dQ stores instead measured slower: its vmcnt wait then covers those stores too)
     if (qt + 2 < nq) BWD_STAGE(buf);
     // dQ[q][d] = sum over the 128 keys of dS[q][key] K[key][d], 16x16x32 MFMAs issued as
     // (K^T fragment, dS fragment): the lane ends up with 4 consecutive d of one query.  Both
@@ -827,15 +830,35 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
       const uint4 v = {s0[0], s1[0], s0[1], s1[1]};
       const int d = dq_d0 + 16 * (fg & 1) + 8 * (fg >> 1);
       *reinterpret_cast<uint4*>(dqbase + q * (int)a.dq_ss + d) = v;
+    } else if (!single_block) {
+      // Sk > 128: the wave's [16 q][32 d] fp32 share goes through LDS so that each atomic
+      // wave-instruction adds two contiguous 128-byte row segments (the memory-side atomic
+      // unit's full-rate shape) instead of 16 rows x 4 scattered dwords (~10x slower: the
+      // backward took 883 us at B 32, S 512 before, 326 after).  Scratch: this wave's own key
+      // rows of the OTHER dS^T buffer (tile qt - 1's, read by every wave's dQ before this
+      // tile's barrier; rewritten only by this wave, at tile qt + 1); 128-byte rows, 16-byte
+      // chunks XOR (q & 7).  Every lane takes part; rows past Sq only skip their atomics.
+      char* xw = dSs + (buf ^ 1) * 8192 + w * 2048;
+      const int xq = lane & 15;
+      *reinterpret_cast<f32x4*>(xw + xq * 128 + ((fg ^ (xq & 7)) << 4)) = dq0;
+      *reinterpret_cast<f32x4*>(xw + xq * 128 + (((4 + fg) ^ (xq & 7)) << 4)) = dq1;
+      __builtin_amdgcn_wave_barrier();
+      const int xd = lane & 31;
+      float* accp = a.dq_acc + ((long)bh * a.Sq + qb + dq_q0) * 64 + dq_d0 + xd;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int qr = 2 * i + (lane >> 5);
+        const float val = *reinterpret_cast<const float*>(xw + qr * 128 + (((xd >> 2) ^ (qr & 7)) << 4) + ((xd & 3) << 2)) * a.scale;
+        if (qb + dq_q0 + qr < a.Sq) atomicAdd(accp + qr * 64, val);
+      }
+      __builtin_amdgcn_wave_barrier();
     } else if (q < a.Sq) {
 #pragma unroll
       for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int d = dq_d0 + 16 * t2 + 4 * fg + rr;
-          const float val = (t2 ? dq1[rr] : dq0[rr]) * a.scale;
-          if (single_block) dqbase[q * (int)a.dq_ss + d] = f2bf(val);
-          else atomicAdd(a.dq_acc + ((long)bh * a.Sq + q) * 64 + d, val);
+          dqbase[q * (int)a.dq_ss + d] = f2bf((t2 ? dq1[rr] : dq0[rr]) * a.scale);
         }
     }
   }
@@ -1048,13 +1071,16 @@ extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const l
   dim3 grid(nkb, B * H);
   // causal masking is a template parameter (as in the forward): no per-element test of a
   // runtime flag in the non-causal (BERT) kernel
-  if (p_drop > 0.f) {
-    if (causal) attn_bwd_d64_kernel<true, true><<<grid, 256, 0, stream>>>(a);
-    else attn_bwd_d64_kernel<true, false><<<grid, 256, 0, stream>>>(a);
-  } else {
-    if (causal) attn_bwd_d64_kernel<false, true><<<grid, 256, 0, stream>>>(a);
-    else attn_bwd_d64_kernel<false, false><<<grid, 256, 0, stream>>>(a);
+#define CT_ATTN_BWD(M)                                                                   \
+  if (p_drop > 0.f) {                                                                    \
+    if (causal) attn_bwd_d64_kernel<true, true, M><<<grid, 256, 0, stream>>>(a);         \
+    else attn_bwd_d64_kernel<true, false, M><<<grid, 256, 0, stream>>>(a);               \
+  } else {                                                                               \
+    if (causal) attn_bwd_d64_kernel<false, true, M><<<grid, 256, 0, stream>>>(a);        \
+    else attn_bwd_d64_kernel<false, false, M><<<grid, 256, 0, stream>>>(a);              \
   }
+  if (nkb > 1) { CT_ATTN_BWD(true) } else { CT_ATTN_BWD(false) }
+#undef CT_ATTN_BWD
   if (nkb > 1)
     attn_dq_convert_kernel<<<(int)((rows * 64 + 255) / 256), 256, 0, stream>>>(
         dq_acc, (bf16_t*)dq, dqs[0], dqs[1], dqs[2], B, H, Sq);
