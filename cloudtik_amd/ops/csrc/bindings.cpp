@@ -11,7 +11,7 @@
 extern "C" {
 int ct_layernorm_fwd(const void*, const void*, const void*, const void*, const void*, void*, void*,
                      float*, float*, int, int, float, int, float, uint64_t, uint64_t, hipStream_t);
-int ct_layernorm_bwd_grid(int M);
+int ct_layernorm_bwd_grid(int M, int N);
 int ct_layernorm_bwd(const void*, const void*, const void*, const float*, const float*,
                      const void*, void*, void*, float*, void*, void*, void*, int, int, int, int,
                      int, float, uint64_t, uint64_t, hipStream_t);
@@ -132,7 +132,7 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor s, at::Tensor ga
   auto dgamma = at::empty_like(gamma);
   at::Tensor dbeta = has_beta ? at::empty_like(gamma) : at::Tensor();
   at::Tensor dbias = has_bias ? at::empty_like(gamma) : at::Tensor();
-  const int grid = ct_layernorm_bwd_grid(M);
+  const int grid = ct_layernorm_bwd_grid(M, N);
   auto part = at::empty({3 * (long)grid * N}, s.options().dtype(at::kFloat));
   int rc = ct_layernorm_bwd(dy.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
                             rstd.data_ptr<float>(), optr(dextra), ds.data_ptr(),
@@ -161,7 +161,7 @@ std::vector<at::Tensor> layernorm_bwd_into(at::Tensor dy, at::Tensor s, at::Tens
   if (dbias.has_value() && dbias->defined()) { CHECK_IN(*dbias); TORCH_CHECK(dbias->numel() == N && dbias->scalar_type() == dgamma.scalar_type()); }
   auto ds = at::empty_like(s);
   at::Tensor dx = need_dx ? at::empty_like(s) : at::Tensor();
-  const int grid = ct_layernorm_bwd_grid(M);
+  const int grid = ct_layernorm_bwd_grid(M, N);
   auto part = at::empty({3 * (long)grid * N}, s.options().dtype(at::kFloat));
   int rc = ct_layernorm_bwd(dy.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
                             rstd.data_ptr<float>(), nullptr, ds.data_ptr(),

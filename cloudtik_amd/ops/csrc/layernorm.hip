@@ -114,9 +114,11 @@ struct LnBwdArgs {
 // prologue); off when the consumer computes them instead (the projection's weight-gradient
 // GEMM sums its dY operand with an all-ones MFMA: ops/transformer.py) -- 16 fewer registers
 // and adds per row, a third fewer partials
+// 3 waves / SIMD up to N = 1024 (MAXV 2); wider rows (N <= 2048) keep more registers at 2
+// (1 with the bias gradient) -- at 3 they spilled 20-550 VGPRs
 template <int MAXV, bool RMS, bool EXTRA, bool DBIAS>
-__global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
-  __shared__ float red[4][512];
+__global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_kernel(LnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[4][512];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
   const int N = a.N, nvec = N >> 3;
@@ -205,25 +207,33 @@ __global__ __launch_bounds__(256, 3) void ln_bwd_kernel(LnBwdArgs a) {
       }
     }
   }
-  // reduce the block's waves through LDS, 512 columns at a time
+  // reduce the block's waves through LDS, 512 columns at a time.  A lane's 8 columns go in as
+  // two 16-byte stores whose halves swap when bit 2 of the column group is set: the 8 lanes of
+  // a ds_write_b128 group then cover all 32 banks (scalar stores at a 32-byte lane stride were
+  // 8-way conflicted: 2.06 M conflict cycles per BERT-large step); the column-order reads
+  // undo the swap and stay conflict-free.
   const int nparts = want_dbias ? 3 : 2;
   for (int base = 0; base < N; base += 512) {
     for (int pass = 0; pass < nparts; ++pass) {
 #pragma unroll
       for (int i = 0; i < MAXV; ++i) {
         const int c = lane + i * 64;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = c * 8 + j;
-          if (c < nvec && col >= base && col < base + 512)
-            red[wid][col - base] = pass == 0 ? dg[i][j] : (pass == 1 ? db[i][j] : dbi[DBIAS ? i : 0][j]);
+        const int cl = c - (base >> 3);
+        if (c < nvec && cl >= 0 && cl < 64) {
+          const float* src = pass == 0 ? dg[i] : (pass == 1 ? db[i] : dbi[DBIAS ? i : 0]);
+          const int hs = (cl >> 2) & 1;
+          float* rw = red[wid] + cl * 8;
+          *reinterpret_cast<f32x4*>(rw + 4 * hs) = f32x4{src[0], src[1], src[2], src[3]};
+          *reinterpret_cast<f32x4*>(rw + 4 * (hs ^ 1)) = f32x4{src[4], src[5], src[6], src[7]};
         }
       }
       __syncthreads();
       float* dst = pass == 0 ? a.dg_part : (pass == 1 ? a.db_part : a.dbias_part);
       for (int col = threadIdx.x; col < 512 && base + col < N; col += blockDim.x) {
+        const int cl = col >> 3, j = col & 7;
+        const int idx = cl * 8 + 4 * ((j >> 2) ^ ((cl >> 2) & 1)) + (j & 3);
         float t = 0.f;
-        for (int w = 0; w < wpb; ++w) t += red[w][col];
+        for (int w = 0; w < wpb; ++w) t += red[w][idx];
         if (dst) dst[(size_t)blockIdx.x * N + base + col] = t;
       }
       __syncthreads();
@@ -347,20 +357,22 @@ extern "C" int ct_layernorm_fwd(const void* x, const void* bias, const void* res
   return 0;
 }
 
-extern "C" int ct_layernorm_bwd_grid(int M) {
-  // 768 blocks x 4 waves = 3 waves per SIMD on 256 CUs (the kernel's VGPR budget allows 3)
+extern "C" int ct_layernorm_bwd_grid(int M, int N) {
+  // 768 blocks x 4 waves = 3 waves per SIMD on 256 CUs (the kernel's VGPR budget allows 3
+  // for N <= 1024, 2 above)
+  const int cap = N > 1024 ? 512 : 768;
   const int grid = ceil_div(M, 4);
-  return grid > 768 ? 768 : grid;
+  return grid > cap ? cap : grid;
 }
 
-// Workspace: part = float[3 * grid * N] (grid = ct_layernorm_bwd_grid(M)).
+// Workspace: part = float[3 * grid * N] (grid = ct_layernorm_bwd_grid(M, N)).
 extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, const float* mean,
                                 const float* rstd, const void* dextra, void* ds, void* dx,
                                 float* part, void* dgamma, void* dbeta, void* dbias, int M, int N,
                                 int rms, int param_fp32, int accumulate, float p_drop,
                                 uint64_t seed, uint64_t offset, hipStream_t stream) {
   if (N % 8 != 0 || N > 2048 || M <= 0) return -1;
-  const int grid = ct_layernorm_bwd_grid(M);
+  const int grid = ct_layernorm_bwd_grid(M, N);
   LnBwdArgs a;
   a.dy = (const bf16_t*)dy; a.s = (const bf16_t*)s; a.gamma = (const bf16_t*)g; a.mean = mean;
   a.rstd = rstd; a.dextra = (const bf16_t*)dextra; a.ds = (bf16_t*)ds; a.dx = (bf16_t*)dx;
