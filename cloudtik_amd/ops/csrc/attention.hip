@@ -598,21 +598,32 @@ struct AttnBwdArgs {
   uint32_t thr16; float inv_keep; uint32_t hash_base; int causal;
 };
 
-template <bool DROP, bool CAUSAL, bool MULTI>
+// GL (single key block and Sq <= 128 only): every LDS tile arrives by global_load_lds -- K, V
+// and the first two Q / dO tiles in the prologue, tile t + 2's Q / dO at the top of tile t into
+// a THREE-deep ring (the slot tile t - 1 released at its barrier), waited for by a counted
+// vmcnt just before tile t + 1's barrier: one and a half tiles of compute cover each load
+// (the register-staged form gives half a tile and stalls on it: 47 % of wave cycles parked in
+// s_waitcnt / barrier).  lse and delta = rowsum(dO * O) are computed for all (<= 128) rows
+// once in the prologue instead of per tile, so the loop issues no register-destined loads.
+template <bool DROP, bool CAUSAL, bool MULTI, bool GL = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
-  // LDS: Q tiles 2 x 4K | dO tiles 2 x 4K | K block 16K | V block 16K | dS^T 2 x 8K | lse, delta 2 x 256 B
-  // The per-q-tile inputs (Q, dO, lse, delta) and dS^T are double-buffered, so one barrier per
-  // q-tile orders everything: tile t+2 is staged into the buffers tile t has just released, and
-  // dQ needs no cross-wave reduction (each wave owns 16 queries x 32 d of the tile's dQ and sums
-  // over all 128 keys itself).
-  __shared__ __attribute__((aligned(16))) char smem[8192 + 8192 + 16384 + 16384 + 16384 + 512];
+  // LDS: Q tiles R x 4K | dO tiles R x 4K | K block 16K | V block 16K | dS^T 2 x 8K | lse, delta
+  // (R = 2 register-staged: 2 x 32 rows each; R = 3 with GL: all <= 128 rows each)
+  // The per-q-tile inputs (Q, dO, lse, delta) and dS^T are multi-buffered, so one barrier per
+  // q-tile orders everything: tile t+2 is staged into the buffers tile t (t - 1 with GL) has
+  // released, and dQ needs no cross-wave reduction (each wave owns 16 queries x 32 d of the
+  // tile's dQ and sums over all 128 keys itself).
+  static_assert(!(GL && MULTI), "GL: single key block only");
+  constexpr int QR = GL ? 3 : 2;
+  constexpr int QB = QR * 4096;
+  __shared__ __attribute__((aligned(16))) char smem[2 * QB + 16384 + 16384 + 16384 + (GL ? 1024 : 512)];
   char* Qs = smem;
-  char* dOs = smem + 8192;
-  char* Ks = smem + 16384;
-  char* Vs = smem + 32768;
-  char* dSs = smem + 49152;
-  float* lse_s = reinterpret_cast<float*>(smem + 65536);      // [2][32]
-  float* delta_s = lse_s + 64;                                // [2][32]
+  char* dOs = smem + QB;
+  char* Ks = smem + 2 * QB;
+  char* Vs = Ks + 16384;
+  char* dSs = Vs + 16384;
+  float* lse_s = reinterpret_cast<float*>(dSs + 16384);       // [2][32] or [128]
+  float* delta_s = lse_s + (GL ? 128 : 64);                   // [2][32] or [128]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
@@ -626,6 +637,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   // K and V blocks (128 keys) into LDS: row reads give the B operands of S = Q K^T and
   // dP = dO V^T (re-read per q-tile instead of pinning 32 VGPRs), transposed reads of K
   // give dQ's operand
+  if constexpr (GL) {
+    // wave w DMAs rows 32 w + 8 i + (lane >> 3); lane l lands at physical chunk l & 7, so it
+    // fetches logical chunk (l & 7) ^ rev3(((row >> 1) & 7)) = (l & 7) ^ rev3((4 i + (l >> 4)) & 7).
+    // Rows past Sk read row Sk - 1 (finite; their -inf key bias zeroes them)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 32 * w + 8 * i + (lane >> 3);
+      const unsigned key = (unsigned)min(k0 + row, a.Sk - 1);
+      const unsigned c = (unsigned)((lane & 7) ^ rev3((4 * i + (lane >> 4)) & 7));
+      at_glds16s(kp, (key * (unsigned)a.k_ss + c * 8u) * 2u, Ks + (32 * w + 8 * i) * 128);
+      at_glds16s(vp, (key * (unsigned)a.v_ss + c * 8u) * 2u, Vs + (32 * w + 8 * i) * 128);
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i;
@@ -636,6 +660,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     const u16x8 vv = ok ? *reinterpret_cast<const u16x8*>(vp + (long)key * a.v_ss + ch * 8) : u16x8(0);
     *reinterpret_cast<u16x8*>(Ks + swz(row, ch)) = kv;
     *reinterpret_cast<u16x8*>(Vs + swz(row, ch)) = vv;
+  }
   }
   const int krow = w * 32 + r;   // this lane's key row inside the block
   float kb2 = 0.f;
@@ -694,22 +719,66 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
     dd_ += __shfl_xor(dd_, 4, 64);                                                          \
     if (pch == 0) delta_s[(buf_) * 32 + prow] = dd_;                                        \
   }
+  // GL: Q / dO tile t (32 rows) into ring slot `slot_`: wave w DMAs rows 8 w + (lane >> 3) of
+  // each (one 1 KB instruction per operand); rows past Sq read row Sq - 1 (finite; their
+  // +inf lse zeroes every product they enter)
+#define BWD_GLDS(qb_, slot_)                                                                \
+  {                                                                                         \
+    const unsigned q_ = (unsigned)min((qb_) + 8 * w + (lane >> 3), a.Sq - 1);               \
+    const unsigned c_ = (unsigned)((lane & 7) ^ rev3((4 * w + (lane >> 4)) & 7));           \
+    at_glds16s(qbase, (q_ * (unsigned)a.q_ss + c_ * 8u) * 2u, Qs + (slot_) * 4096 + w * 1024); \
+    at_glds16s(dobase, (q_ * (unsigned)a.do_ss + c_ * 8u) * 2u, dOs + (slot_) * 4096 + w * 1024); \
+  }
+  if constexpr (GL) {
+    BWD_GLDS(0, 0);
+    if (nq > 1) BWD_GLDS(32, 1);
+    // lse and delta of all rows: thread (row tid >> 1, half tid & 1) dots 32 d of dO and O
+    {
+      const int row = tid >> 1, hf = tid & 1;
+      float dd = 0.f;
+      if (row < a.Sq) {
+        const bf16_t* dr = dobase + row * (int)a.do_ss + 32 * hf;
+        const bf16_t* orow = obase + row * (int)a.o_ss + 32 * hf;
+        u16x8 dv[4], ov[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dv[j] = *reinterpret_cast<const u16x8*>(dr + 8 * j);
+          ov[j] = *reinterpret_cast<const u16x8*>(orow + 8 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dd += bf2f(dv[j][e]) * bf2f(ov[j][e]);
+      }
+      dd += __shfl_xor(dd, 1, 64);
+      if (hf == 0 && row < 128) delta_s[row] = dd;
+      if (tid < 128) lse_s[tid] = tid < a.Sq ? a.lse[(long)bh * a.Sq + tid] : INFINITY;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
   BWD_PREFETCH(0);
   BWD_STAGE(0);
   if (nq > 1) {
     BWD_PREFETCH(32);
     BWD_STAGE(1);
   }
+  }
   __syncthreads();
 
+  int slot = 0;      // GL: ring slot of tile qt
   for (int qt = 0; qt < nq; ++qt) {
     const int qb = qt * 32;
     const int buf = qt & 1;
-    if (qt + 2 < nq) BWD_PREFETCH(qb + 64);
-    const char* Qt = Qs + buf * 4096;
-    const char* dOt = dOs + buf * 4096;
-    const float* lse_t = lse_s + buf * 32;
-    const float* delta_t = delta_s + buf * 32;
+    if constexpr (GL) {
+      // slot of tile qt + 2 == slot of tile qt - 1 (released at tile qt - 1's barrier)
+      if (qt + 2 < nq) { const int s2 = slot == 0 ? 2 : slot - 1; BWD_GLDS(qb + 64, s2); }
+    } else {
+      if (qt + 2 < nq) BWD_PREFETCH(qb + 64);
+    }
+    const char* Qt = Qs + (GL ? slot : buf) * 4096;
+    const char* dOt = dOs + (GL ? slot : buf) * 4096;
+    const float* lse_t = lse_s + (GL ? qb : buf * 32);
+    const float* delta_t = delta_s + (GL ? qb : buf * 32);
     char* dSt = dSs + buf * 8192;
     f32x16 S, dP;
 #pragma unroll
@@ -791,11 +860,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
         *reinterpret_cast<u16x4*>(rowp + ((c ^ sw) << 3)) = v;
       }
     }
+    if constexpr (GL) {
+      // tile qt + 1's DMA (issued a tile and a half ago) must have landed before this barrier;
+      // only tile qt + 2's two pieces may stay in flight
+      if (qt + 2 < nq) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      slot = slot == 2 ? 0 : slot + 1;
+    }
     __syncthreads();   // the ONLY barrier of the tile: dS^T complete; this tile's Q / dO / lse /
                        // delta buffers free; tile t+1's staged buffers visible
     // tile qt + 2's inputs into the buffers tile qt released at this barrier (staging after the
     // dQ stores instead measured slower: its vmcnt wait then covers those stores too)
-    if (qt + 2 < nq) BWD_STAGE(buf);
+    if constexpr (!GL) {
+      if (qt + 2 < nq) BWD_STAGE(buf);
+    }
     // dQ[q][d] = sum over the 128 keys of dS[q][key] K[key][d], 16x16x32 MFMAs issued as
     // (K^T fragment, dS fragment): the lane ends up with 4 consecutive d of one query.  Both
     // fragments (8 consecutive keys per lane) come from transposing reads of [key][.] images.
@@ -864,6 +942,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_d64_kernel(AttnBwdArgs a) {
   }
 #undef BWD_PREFETCH
 #undef BWD_STAGE
+#undef BWD_GLDS
   {
     const long kl = kvalid ? key_l : 0;
     store_row64(a.dk + b * a.dk_sb + h * a.dk_sh + kl * a.dk_ss, dK0, dK1, a.scale, hh, kvalid);
@@ -1071,15 +1150,21 @@ extern "C" int ct_attn_bwd(const void* q, const long* qs, const void* k, const l
   dim3 grid(nkb, B * H);
   // causal masking is a template parameter (as in the forward): no per-element test of a
   // runtime flag in the non-causal (BERT) kernel
-#define CT_ATTN_BWD(M)                                                                   \
+#define CT_ATTN_BWD(M, G)                                                                \
   if (p_drop > 0.f) {                                                                    \
-    if (causal) attn_bwd_d64_kernel<true, true, M><<<grid, 256, 0, stream>>>(a);         \
-    else attn_bwd_d64_kernel<true, false, M><<<grid, 256, 0, stream>>>(a);               \
+    if (causal) attn_bwd_d64_kernel<true, true, M, G><<<grid, 256, 0, stream>>>(a);      \
+    else attn_bwd_d64_kernel<true, false, M, G><<<grid, 256, 0, stream>>>(a);            \
   } else {                                                                               \
-    if (causal) attn_bwd_d64_kernel<false, true, M><<<grid, 256, 0, stream>>>(a);        \
-    else attn_bwd_d64_kernel<false, false, M><<<grid, 256, 0, stream>>>(a);              \
+    if (causal) attn_bwd_d64_kernel<false, true, M, G><<<grid, 256, 0, stream>>>(a);     \
+    else attn_bwd_d64_kernel<false, false, M, G><<<grid, 256, 0, stream>>>(a);           \
   }
-  if (nkb > 1) { CT_ATTN_BWD(true) } else { CT_ATTN_BWD(false) }
+  static const int bwd_gl = [] {
+    const char* e = getenv("CLOUDTIK_AMD_ATTN_BWD_GL");
+    return e ? atoi(e) : 1;
+  }();
+  if (nkb > 1) { CT_ATTN_BWD(true, false) }
+  else if (bwd_gl && Sq <= 128) { CT_ATTN_BWD(false, true) }
+  else { CT_ATTN_BWD(false, false) }
 #undef CT_ATTN_BWD
   if (nkb > 1)
     attn_dq_convert_kernel<<<(int)((rows * 64 + 255) / 256), 256, 0, stream>>>(

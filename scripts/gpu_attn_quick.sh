@@ -7,8 +7,10 @@ cd "$R"
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_ops_gpu.py tests/test_model_parity.py -k "attention or attn or bert" > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
 tail -1 "$OUT/tests.log"
 for rep in 1 2; do
+for v in ${AB_VALUES:-1}; do
 for shape in "--S 128 --B 256 --p 0.1" "--S 128 --B 256 --p 0.0" "--S 512 --B 32 --p 0.1"; do
-  timeout -k 10 120 python3 bench/attn_kernel_probe.py $shape 2>&1 | grep -v amdgpu.ids || exit 1
+  env ${AB_VAR:-AB_NONE}=$v timeout -k 10 120 python3 bench/attn_kernel_probe.py $shape 2>&1 | grep -v amdgpu.ids | sed "s/^/${AB_VAR:-}=$v /" || exit 1
+done
 done
 done
 cd /tmp && export TMPDIR=/tmp
