@@ -27,6 +27,7 @@ int ct_embed3_bwd(const int64_t*, const int64_t*, const void*, float*, float*, f
 int ct_cast(const void*, int, void*, int, long, float, int, hipStream_t);
 int ct_splitk_reduce(const float*, int, long, void*, int, hipStream_t);
 int ct_splitk_reduce_clear(float*, int, long, void*, int, hipStream_t);
+int ct_splitk_reduce2(const float*, int, long, void*, const float*, int, long, void*, int, hipStream_t);
 int ct_lamb(const void*, int, float*, float*, float*, void*, int, const int*, const long*,
             const int*, int, const int*, int, const float*, const float*, float, float, float, int,
             int, float*, float*, int, hipStream_t);
@@ -272,6 +273,16 @@ void splitk_reduce(at::Tensor partials, at::Tensor g, bool accumulate) {
 }
 
 // the same, and the partials are zeroed once read (persistent accumulation buffers)
+// two (partials, g) reductions in one launch (see ct_splitk_reduce2)
+void splitk_reduce2(at::Tensor p1, at::Tensor g1, at::Tensor p2, at::Tensor g2, bool accumulate) {
+  for (auto* t : {&p1, &p2}) { CHECK_IN(*t); TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() >= 2); }
+  for (auto* t : {&g1, &g2}) { CHECK_IN(*t); CHECK_BF16(*t); TORCH_CHECK(t->numel() % 8 == 0, "splitk_reduce2: numel % 8"); }
+  TORCH_CHECK(p1[0].numel() == g1.numel() && p2[0].numel() == g2.numel(), "splitk_reduce2: shape mismatch");
+  TORCH_CHECK(ct_splitk_reduce2(p1.data_ptr<float>(), (int)p1.size(0), g1.numel(), g1.data_ptr(),
+                                p2.data_ptr<float>(), (int)p2.size(0), g2.numel(), g2.data_ptr(),
+                                accumulate ? 1 : 0, cur_stream()) == 0);
+}
+
 void splitk_reduce_clear(at::Tensor partials, at::Tensor g, bool accumulate) {
   CHECK_IN(partials); CHECK_F32(partials); CHECK_IN(g); CHECK_BF16(g);
   TORCH_CHECK(partials.dim() >= 2 && partials[0].numel() == g.numel(), "splitk_reduce_clear: shape mismatch");
@@ -769,6 +780,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_into", &cast_into);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("splitk_reduce_clear", &splitk_reduce_clear);
+  m.def("splitk_reduce2", &splitk_reduce2);
   m.def("lamb_step", &lamb_step);
   m.def("adam_step", &adam_step);
   m.def("sgd_step", &sgd_step);

@@ -351,6 +351,51 @@ extern "C" int ct_splitk_reduce(const float* P, int S, long n, void* g, int accu
   return 0;
 }
 
+// Two independent reductions in ONE launch (vectors [0, nv) of the first pair, then the second
+// pair's): a weight gradient's fp32 slabs and its bias's [S][N] column-sum partials, which were
+// two back-to-back launches per weight-gradient site (the bias one a few microseconds of launch
+// for a few KB of data).
+struct Reduce2 { const float* P[2]; int S[2]; long nv[2]; bf16_t* g[2]; };
+
+__global__ void __launch_bounds__(256) splitk_reduce2_kernel(Reduce2 r, int accumulate) {
+  const long nt = r.nv[0] + r.nv[1];
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < nt; t += (long)gridDim.x * blockDim.x) {
+    const int k = t < r.nv[0] ? 0 : 1;
+    const long v = k ? t - r.nv[0] : t;
+    const long n = r.nv[k] * 8;
+    const float* P = r.P[k];
+    bf16_t* g = r.g[k];
+    float acc[8];
+    if (accumulate) {
+      const u16x8 gv = *reinterpret_cast<const u16x8*>(g + v * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = bf2f(gv[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    }
+#pragma unroll 4
+    for (int s = 0; s < r.S[k]; ++s) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(P + s * n + v * 8);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(P + s * n + v * 8 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { acc[j] += a[j]; acc[4 + j] += b[j]; }
+    }
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+    *reinterpret_cast<u16x8*>(g + v * 8) = o;
+  }
+}
+
+extern "C" int ct_splitk_reduce2(const float* P, int S, long n, void* g, const float* P2, int S2, long n2,
+                                 void* g2, int accumulate, hipStream_t stream) {
+  if (n % 8 || n2 % 8) return -1;
+  Reduce2 r{{P, P2}, {S, S2}, {n / 8, n2 / 8}, {(bf16_t*)g, (bf16_t*)g2}};
+  splitk_reduce2_kernel<<<grid_for(r.nv[0] + r.nv[1]), 256, 0, stream>>>(r, accumulate);
+  return 0;
+}
+
 extern "C" int ct_splitk_reduce_clear(float* P, int S, long n, void* g, int accumulate, hipStream_t stream) {
   if (n % 8) return -1;
   const long nv = n / 8;

@@ -200,11 +200,13 @@ def wgrad_accumulate(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
         ok = (C.gemm_tn2_bias(dy2c, x2c, out, S, S == 1, bP) if fuse_bias
               else C.gemm_tn2(dy2c, x2c, out, S, S == 1))
         if ok:
-            if S > 1:
+            if S > 1 and fuse_bias:
+                C.splitk_reduce2(out, g, bP, dbias, True)     # slabs + bias partials, one launch
+            elif S > 1:
                 C.splitk_reduce(out, g, True)
-            if fuse_bias:
+            elif fuse_bias:
                 C.splitk_reduce(bP, dbias, True)
-            elif dbias is not None:
+            if dbias is not None and not fuse_bias:
                 _bias_colsum(dbias, dy2)
             return
     if dbias is not None:

@@ -629,3 +629,18 @@ def test_xent_kernel_matches_fp32(cuda, V, ld, smooth):
     g = (logp.exp() - smooth / V - (1 - smooth) * onehot) * scale * valid[:, None].float()
     torch.testing.assert_close(buf.float()[:, :V], g, rtol=2e-2, atol=2e-4)
     assert buf.float()[:, V:].abs().max().item() == 0.0 if ld > V else True
+
+
+def test_splitk_reduce2_matches_two_reductions(cuda):
+    """One launch reducing a weight gradient's fp32 slabs and its bias partials (+= into bf16)."""
+    torch.manual_seed(3)
+    C = ops.require_native()
+    P1 = torch.randn(5, 384, 256, device=cuda)
+    P2 = torch.randn(5, 384, device=cuda)
+    g1 = torch.randn(384, 256, device=cuda).bfloat16()
+    g2 = torch.randn(384, device=cuda).bfloat16()
+    r1 = (g1.float() + P1.sum(0)).bfloat16()
+    r2 = (g2.float() + P2.sum(0)).bfloat16()
+    C.splitk_reduce2(P1, g1, P2, g2, True)
+    assert _rel(g1, r1) < 1e-2 and _rel(g2, r2) < 1e-2
+    assert (g1.float() - r1.float()).abs().max().item() <= 0.0625
