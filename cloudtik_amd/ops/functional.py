@@ -255,8 +255,10 @@ class _BNActFn(torch.autograd.Function):
         if given is not None and dy.is_contiguous(memory_format=torch.channels_last):
             # dy arrives ReLU-masked with its reduction done by the conv's dgrad epilogue
             part, tiles, rows = given
+            from cloudtik_amd.ops.conv import flush_deferred_wgrads
             if flat:
                 dx, _, _ = _C().bn_bwd_given(dy, x, gamma, stat, part, tiles, rows, wp.grad, bp.grad)
+                flush_deferred_wgrads()         # the producing conv's weight gradient (ops/conv.py)
                 for p in (wp, bp):
                     cb = getattr(p, "_ct_grad_ready", None)
                     if cb is not None:
@@ -264,6 +266,7 @@ class _BNActFn(torch.autograd.Function):
                 # with a residual add the masked dy IS the residual branch's gradient
                 return dx, None, None, (dy if has_res else None), None, None, None, None, None
             dx, dg, db = _C().bn_bwd_given(dy, x, gamma, stat, part, tiles, rows, None, None)
+            flush_deferred_wgrads()
             return dx, dg, db, (dy if has_res else None), None, None, None, None, None
         if flat:
             # accumulate straight into the flat gradient buffer (no AccumulateGrad kernels)
@@ -327,6 +330,8 @@ class _BNAddBNActFn(torch.autograd.Function):
             acc = [wp.grad, bp.grad, wp2.grad, bp2.grad] if f1 else [None] * 4
             dx, dx2, dg, db, dg2, db2 = _C().bn_bwd_given_pair(dy, x, gamma, stat, part, tiles, rows, x2, gamma2,
                                                                stat2, *acc)
+            from cloudtik_amd.ops.conv import flush_deferred_wgrads
+            flush_deferred_wgrads()
             if f1:
                 ready(wp, bp, wp2, bp2)
                 return dx, None, None, None, None, dx2, None, None, None, None, None, None
@@ -336,6 +341,8 @@ class _BNAddBNActFn(torch.autograd.Function):
             dym = dy                                   # already ReLU-masked by the conv epilogue
             dx, dg, db = _C().bn_bwd_given(dym, x, gamma, stat, part, tiles, rows,
                                            wp.grad if f1 else None, bp.grad if f1 else None)
+            from cloudtik_amd.ops.conv import flush_deferred_wgrads
+            flush_deferred_wgrads()
         else:
             dx, dym, dg, db = _C().bn_bwd(dy, mask, x, gamma, stat, 3, True,
                                           wp.grad if f1 else None, bp.grad if f1 else None)
