@@ -15,6 +15,10 @@ from __future__ import annotations
 
 import math
 
+import os
+import sys
+import time
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -242,14 +246,28 @@ class ResNetTrainStep:
     def __init__(self, model, optimizer, bucketer=None, scheduler=None):
         self.model, self.opt, self.ddp, self.sched = model, optimizer, bucketer, scheduler
 
+    # CLOUDTIK_AMD_STEP_PHASES=<ms>: print the host time of each phase of any step slower than
+    # that (a diagnostic for host-side stalls, e.g. in collective waits)
+    _PHASES = float(os.environ.get("CLOUDTIK_AMD_STEP_PHASES", "0") or 0)
+
     def __call__(self, x, y):
+        t = [time.perf_counter()] if self._PHASES else None
         logits = self.model(x)
         loss = F.cross_entropy(logits.float(), y)
+        t and t.append(time.perf_counter())
         loss.backward()
+        t and t.append(time.perf_counter())
         if self.ddp is not None:
             self.ddp.finish()
+        t and t.append(time.perf_counter())
         self.opt.step()
         if self.sched is not None:
             self.sched.step()
         self.opt.zero_grad()
+        if t:
+            t.append(time.perf_counter())
+            if (t[-1] - t[0]) * 1e3 > self._PHASES:
+                ph = ", ".join(f"{n} {(b - a) * 1e3:.1f}" for n, a, b in
+                               zip(("forward", "backward", "finish", "optimizer"), t, t[1:]))
+                print(f"[step phases ms] {ph}", file=sys.stderr, flush=True)
         return loss

@@ -34,6 +34,9 @@ Design (MI355X):
 from __future__ import annotations
 
 import contextlib
+import os
+import sys
+import time
 from typing import List, Optional
 
 import torch
@@ -284,12 +287,19 @@ class GradBucketer:
             # a barrier that timed out in an earlier (finished) kernel means some rank's
             # gradients were never reduced: fatal, never a silent divergence of the ranks
             self.p2p.check()
+        diag = float(os.environ.get("CLOUDTIK_AMD_STEP_PHASES", "0") or 0)
+        waits = []
         for w, dst, buf in self._works:
             if w is not None:
+                t0 = time.perf_counter() if diag else 0.0
                 w.wait()
+                if diag:
+                    waits.append(round((time.perf_counter() - t0) * 1e3, 1))
             if dst is not None:
                 buf.record_stream(torch.cuda.current_stream()) if buf.is_cuda else None
                 dst.copy_(buf)
+        if diag and sum(waits) > diag:
+            print(f"[bucket waits ms] {waits} ({len(self.buckets)} buckets)", file=sys.stderr, flush=True)
         self._works.clear()
         self._reset()
 
