@@ -43,11 +43,14 @@ for M, N in ((32768, 4096), (4096, 4096), (2048, 4096)):
     dz = torch.empty_like(h)
     db = torch.zeros(N, device=dev)
     t7 = timeit(lambda: C.gemm_nn(x, w2, dz, 7, False, None, g, db))
+    t7n = timeit(lambda: C.gemm_nn(x, w2, dz, 7, False, None, g, None))     # no bias-gradient sums
+    db16 = torch.zeros(16, N, device=x.device, dtype=torch.float32)
+    t7r = timeit(lambda: C.gemm_nn(x, w2, dz, 7, False, None, g, db16))     # sums spread over 16 rows
     t0 = timeit(lambda: C.gemm_nt(x, w, h, 0, False, None, None, None))
     # data gradient accumulated into the residual gradient (the NN dgrad sites): D += A . B
     tacc = timeit(lambda: C.gemm_nn(x, w2, dz, 0, True, None, None, None))
     rounds = max(1, -(-tiles // 256))
-    out[f"{M}x{N}"] = {"tiles": tiles, "rounds": rounds, "epi6_us": round(t6, 1), "epi7_us": round(t7, 1),
+    out[f"{M}x{N}"] = {"tiles": tiles, "rounds": rounds, "epi6_us": round(t6, 1), "epi7_us": round(t7, 1), "epi7_nobgrad_us": round(t7n, 1), "epi7_rows16_us": round(t7r, 1),
                        "plain_us": round(t0, 1), "acc_nn_us": round(tacc, 1),
                        "acc_nn_per_round": round(tacc / rounds, 2), "epi6_per_round": round(t6 / rounds, 2),
                        "epi7_per_round": round(t7 / rounds, 2), "plain_per_round": round(t0 / rounds, 2)}

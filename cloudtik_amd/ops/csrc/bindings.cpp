@@ -35,7 +35,7 @@ int ct_adam(const void*, int, float*, float*, float*, void*, int, const int*, co
             const int*, int, const float*, const float*, float, float, float, int, hipStream_t);
 int ct_sgd(const void*, int, float*, float*, void*, int, const int*, const long*, const int*, int,
            const float*, const float*, float, float, int, int, hipStream_t);
-int ct_sumsq(const void*, int, long, float*, hipStream_t);
+int ct_sumsq(const void*, int, long, float*, float*, hipStream_t);
 int ct_clip_coef(const float*, float*, float, float, hipStream_t);
 int ct_xent_fwd(const void*, void*, int, int, const int64_t*, float*, float*, const float*, int, int,
                 float, hipStream_t);
@@ -343,7 +343,8 @@ void sgd_step(at::Tensor g, c10::optional<at::Tensor> buf, at::Tensor w, c10::op
 void sumsq_into(at::Tensor x, at::Tensor out) {
   CHECK_IN(x); CHECK_IN(out); CHECK_F32(out);
   TORCH_CHECK(x.numel() % 4 == 0, "sumsq: numel % 4");
-  ct_sumsq(x.data_ptr(), dt_code(x), x.numel(), out.data_ptr<float>(), cur_stream());
+  auto part = at::empty({2048}, out.options());
+  ct_sumsq(x.data_ptr(), dt_code(x), x.numel(), out.data_ptr<float>(), part.data_ptr<float>(), cur_stream());
 }
 
 void clip_coef(at::Tensor sumsq, at::Tensor dyn, double base_scale, double max_norm) {

@@ -283,7 +283,7 @@ double lt_bmm_tuned(at::Tensor A, at::Tensor B, at::Tensor D, bool trans_a, bool
 }
 
 extern "C" int ct_gemm_nt(const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*,
-                          void*, long, float*, int, hipStream_t);
+                          void*, long, float*, int, hipStream_t, int);
 
 // shared checks + launch of gemm_nt / gemm_nn (b_kn: B stored [K, N])
 static bool gemm_nt_impl(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, bool accumulate,
@@ -301,14 +301,18 @@ static bool gemm_nt_impl(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, 
                       "gemm_nt: bias");
   if (ha) TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && rowmajor_ok(*aux) && aux->size(0) == M &&
                       aux->size(1) == N, "gemm_nt: aux");
-  if (hd) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->is_contiguous() && dbias->numel() == N,
-                      "gemm_nt: dbias");
+  // dbias: [N], or [R][N] with R a power of two (the epilogue spreads its column-sum atomics over
+  // the R rows; the caller reduces them)
+  const long drows = hd && N > 0 ? dbias->numel() / N : 1;
+  if (hd) TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->is_contiguous() && dbias->numel() == drows * N &&
+                      drows >= 1 && (drows & (drows - 1)) == 0, "gemm_nt: dbias must be [N] or [2^k, N] fp32");
   TORCH_CHECK((epi != 1 && epi != 6) || (hb && ha), "gemm_nt: epilogues 1 / 6 need bias and aux");
   TORCH_CHECK((epi != 2 && epi != 7) || ha, "gemm_nt: epilogues 2 / 7 need aux");
   int rc = ct_gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0), (int)M,
                       (int)N, (int)K, (int)epi, accumulate ? 1 : 0, hb ? bias->data_ptr() : nullptr,
                       ha ? aux->data_ptr() : nullptr, ha ? aux->stride(0) : 0,
-                      hd ? dbias->data_ptr<float>() : nullptr, b_kn ? 1 : 0, at::hip::getCurrentHIPStream().stream());
+                      hd ? dbias->data_ptr<float>() : nullptr, b_kn ? 1 : 0, at::hip::getCurrentHIPStream().stream(),
+                      (int)drows);
   return rc == 0;
 }
 

@@ -328,10 +328,12 @@ __global__ __launch_bounds__(256) void sgd_kernel(
   }
 }
 
-// sum of squares over [n] (grad-norm clipping); out must be zeroed; float atomics per block
+// sum of squares over [n] (grad-norm clipping): per-block partials, then one block adds their
+// sum to *out (one atomic: up to 2048 blocks adding into one address serialise at the memory
+// side, ~0.2 us each)
 template <typename GT>
 __global__ __launch_bounds__(256) void sumsq_kernel(const GT* __restrict__ x, long n,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ part) {
   __shared__ float scratch[8];
   float acc = 0.f;
   for (long i = (blockIdx.x * (long)blockDim.x + threadIdx.x) * 4; i < n;
@@ -340,7 +342,16 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const GT* __restrict__ x, lo
     acc += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
   }
   acc = block_sum(acc, scratch);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void sumsq_finish_kernel(const float* __restrict__ part, int g,
+                                                           float* __restrict__ out) {
+  __shared__ float scratch[8];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < g; i += blockDim.x) acc += part[i];
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0) atomicAdd(out, acc);     // += : callers may sum several tensors
 }
 
 // dyn[1] = base_scale * min(1, max_norm / (sqrt(sumsq)*base_scale + 1e-6))
@@ -417,12 +428,14 @@ extern "C" int ct_sgd(const void* g, int gdt, float* buf, float* w, void* w_mode
   return 0;
 }
 
-extern "C" int ct_sumsq(const void* x, int dt, long n, float* out, hipStream_t stream) {
+// part: float[2048] scratch
+extern "C" int ct_sumsq(const void* x, int dt, long n, float* out, float* part, hipStream_t stream) {
   long g = (n / 4 + 255) / 256;
   if (g > 2048) g = 2048;
   if (g < 1) g = 1;
-  if (dt == 1) sumsq_kernel<bf16_t><<<(int)g, 256, 0, stream>>>((const bf16_t*)x, n, out);
-  else sumsq_kernel<float><<<(int)g, 256, 0, stream>>>((const float*)x, n, out);
+  if (dt == 1) sumsq_kernel<bf16_t><<<(int)g, 256, 0, stream>>>((const bf16_t*)x, n, part);
+  else sumsq_kernel<float><<<(int)g, 256, 0, stream>>>((const float*)x, n, part);
+  sumsq_finish_kernel<<<1, 256, 0, stream>>>(part, (int)g, out);
   return 0;
 }
 

@@ -76,11 +76,17 @@ def _fused_ffn1(C, x2, W1, b1f):
 _DB_ACC = {}
 
 
-def _zeroed_acc(device, F):
-    key = (device, F)
+# rows of the fp32 bias-gradient accumulator: the fused dgrad epilogue spreads its column-sum
+# atomics over them (one address took every row half's atomic in turn: 52 us per BERT-large FFN
+# data gradient, csrc/gemm_nt.hip), the reduce sums them
+_DB_ROWS = int(os.environ.get("CLOUDTIK_AMD_DBIAS_ROWS", "16"))
+
+
+def _zeroed_acc(device, F, rows=1):
+    key = (device, F, rows)
     t = _DB_ACC.get(key)
     if t is None:
-        t = _DB_ACC[key] = torch.zeros(F, device=device, dtype=torch.float32)
+        t = _DB_ACC[key] = torch.zeros(rows, F, device=device, dtype=torch.float32)
     return t
 
 
@@ -94,13 +100,14 @@ def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f, dgelu=False):
         return None
     dz = torch.empty_like(z)
     direct = db1f.dtype == torch.bfloat16 and db1f.is_contiguous()
-    db = _zeroed_acc(z.device, F) if direct else torch.zeros(F, device=z.device, dtype=torch.float32)
+    rows = _DB_ROWS if direct else 1
+    db = _zeroed_acc(z.device, F, rows) if direct else torch.zeros(1, F, device=z.device, dtype=torch.float32)
     if not C.gemm_nn(df, W2, dz, 7 if dgelu else 2, False, None if dgelu else b1f, z, db):
         return None
     if direct:
-        C.splitk_reduce_clear(db.view(1, F), db1f, True)
+        C.splitk_reduce_clear(db, db1f, True)          # sums the rows and zeroes them for next time
     else:
-        db1f.add_(db)
+        db1f.add_(db[0])
     return dz
 
 

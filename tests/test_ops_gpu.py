@@ -643,3 +643,16 @@ def test_splitk_reduce2_matches_two_reductions(cuda):
     r2 = (g2.float() + P2.sum(0)).bfloat16()
     C.splitk_reduce2(P1, g1, P2, g2, True)
     assert _rel(g1, r1) < 1e-2 and _rel(g2, r2) < 1e-2
+
+
+@pytest.mark.parametrize("n", [4096, 3 * 2**20 + 64])
+def test_sumsq_into_matches_torch(cuda, n):
+    """Grad-norm clipping's sum of squares: per-block partials + one finishing block, added
+    (+=) into the output."""
+    torch.manual_seed(5)
+    C = ops.require_native()
+    x = torch.randn(n, device=cuda).bfloat16()
+    out = torch.full((1,), 2.0, device=cuda)
+    C.sumsq_into(x, out)
+    ref = 2.0 + (x.float() ** 2).sum().item()
+    assert abs(out.item() - ref) <= 1e-4 * ref
