@@ -190,11 +190,25 @@ __global__ __launch_bounds__(256) void embed3_bwd_seq_kernel(
   const int c = blockIdx.y * 256 + threadIdx.x;
   if (c >= N) return;
   float ps = 0.f, t0 = 0.f, t1 = 0.f;
+  // consecutive tokens of this position with the same id (every sequence's [CLS] at s = 0, the
+  // padding tail) are summed in a register and added once: B same-address atomics serialise at
+  // the memory side
+  long cur = -1;
+  float run = 0.f;
 #pragma unroll 8
   for (int b = 0; b < B; ++b) {
     const long t = (long)b * S + s;
     const float v = bf2f(g[t * N + c]);
-    if (dW) atomicAdd(dW + ids[t] * N + c, v);
+    if (dW) {
+      const long id = ids[t];
+      if (id != cur) {
+        if (cur >= 0) atomicAdd(dW + cur * N + c, run);
+        cur = id;
+        run = v;
+      } else {
+        run += v;
+      }
+    }
     ps += v;
     if (dT) {
       const long ti = tt ? tt[t] : 0;
@@ -205,6 +219,7 @@ __global__ __launch_bounds__(256) void embed3_bwd_seq_kernel(
       }
     }
   }
+  if (dW && cur >= 0) atomicAdd(dW + cur * N + c, run);
   if (dP) dP[(long)s * N + c] += ps;   // (s, c) belongs to this thread alone
   if (dT && nT <= 2) {
     atomicAdd(dT + c, t0);

@@ -81,6 +81,8 @@ def test_embedding3(cuda, T, B, S, H):
     Pe = torch.randn(P, H, device=cuda, dtype=torch.bfloat16, requires_grad=True)
     Te = torch.randn(T, H, device=cuda, dtype=torch.bfloat16, requires_grad=True)
     ids = torch.randint(0, V, (B, S), device=cuda)
+    ids[:, 0] = 7                       # one id at a position in every sequence ([CLS])
+    ids[: B // 2, -2:] = 0              # runs of one id down the batch (padding)
     tt = torch.randint(0, T, (B, S), device=cuda)
     y = ops.embedding3(ids, tt, W, Pe, Te)
     dy = torch.randn_like(y)
