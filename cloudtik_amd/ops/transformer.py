@@ -76,10 +76,13 @@ def _fused_ffn1(C, x2, W1, b1f):
 _DB_ACC = {}
 
 
-# rows of the fp32 bias-gradient accumulator: the fused dgrad epilogue spreads its column-sum
-# atomics over them (one address took every row half's atomic in turn: 52 us per BERT-large FFN
-# data gradient, csrc/gemm_nt.hip), the reduce sums them
-_DB_ROWS = int(os.environ.get("CLOUDTIK_AMD_DBIAS_ROWS", "16"))
+# rows of the fp32 bias-gradient accumulator: the fused dgrad epilogue can spread its column-sum
+# atomics over them (csrc/gemm_nt.hip), the reduce sums them.  Default 1: back to back in the
+# epilogue probe 16 rows took the FFN data gradient from 363 to 334 us (the same-address atomics
+# of consecutive launches queue up), but in the BERT-large step 16 rows ran 72.43 / 72.50 ms/step
+# against 72.28 / 72.33 with one (the atomics drain behind the next kernels; the 16-row reduce
+# adds a few us) -- profiles/r5/SUMMARY.md
+_DB_ROWS = int(os.environ.get("CLOUDTIK_AMD_DBIAS_ROWS", "1"))
 
 
 def _zeroed_acc(device, F, rows=1):
