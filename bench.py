@@ -688,9 +688,6 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.backends.cuda.matmul.allow_tf32 = False
-    if device.type == "cuda" and os.environ.get("CLOUDTIK_AMD_EARLY_SIDE_STREAM", "0") == "1":
-        from cloudtik_amd.ops.linear import grad_stream
-        grad_stream()                   # the weight-gradient side stream before any model runs
     if args.impl == "native" or args.compare_eager:
         setup_tunableop(args.tunableop, rank)
 
