@@ -220,7 +220,11 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_k
         const int c = lane + i * 64;
         const int cl = c - (base >> 3);
         if (c < nvec && cl >= 0 && cl < 64) {
-          const float* src = pass == 0 ? dg[i] : (pass == 1 ? db[i] : dbi[DBIAS ? i : 0]);
+          // select values, not a pointer: a runtime-chosen pointer into the register arrays
+          // put dg / db / dbi in scratch memory for the whole kernel (80 B/lane)
+          float src[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) src[j] = pass == 0 ? dg[i][j] : (pass == 1 ? db[i][j] : dbi[DBIAS ? i : 0][j]);
           const int hs = (cl >> 2) & 1;
           float* rw = red[wid] + cl * 8;
           *reinterpret_cast<f32x4*>(rw + 4 * hs) = f32x4{src[0], src[1], src[2], src[3]};

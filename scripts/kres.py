@@ -23,7 +23,8 @@ def main():
         if cur is None:
             continue
         for key, rx in (("vgpr", r"VGPRs: (\d+)"), ("agpr", r"AGPRs: (\d+)"), ("spill", r"VGPRs Spill: (\d+)"),
-                        ("occ", r"Occupancy \[waves/SIMD\]: (\d+)"), ("lds", r"LDS Size \[bytes/block\]: (\d+)")):
+                        ("occ", r"Occupancy \[waves/SIMD\]: (\d+)"), ("lds", r"LDS Size \[bytes/block\]: (\d+)"),
+                        ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)")):
             m = re.search(rx, line)
             if m:
                 cur[key] = int(m.group(1))
@@ -32,7 +33,7 @@ def main():
     for r, d in zip(rows, demangle):
         if pat in d:
             print(f"{r.get('vgpr', '?'):>4} v {r.get('agpr', '?'):>3} a spill {r.get('spill', '?'):>3} "
-                  f"occ {r.get('occ', '?')} lds {r.get('lds', '?'):>6}  {d[:150]}")
+                  f"scr {r.get('scratch', '?'):>4} occ {r.get('occ', '?')} lds {r.get('lds', '?'):>6}  {d[:140]}")
 
 
 if __name__ == "__main__":
