@@ -93,6 +93,11 @@ def _zeroed_acc(device, F, rows=1):
     return t
 
 
+# FFN1's bias gradient from the FFN1 weight-gradient GEMM (all-ones MFMA on its dz operand,
+# as the QKV one) instead of column-sum atomics in the FFN data-gradient epilogue
+_FFN_BGRAD_IN_WGRAD = os.environ.get("CLOUDTIK_AMD_FFN_BGRAD_IN_WGRAD", "0") == "1"
+
+
 def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f, dgelu=False):
     """dz = (df @ W2) * gelu'(z [+ b1f]) -- or, ``dgelu``, (df @ W2) * z with z already holding
     gelu'(.) (EPI 7); db1f += column sums of dz (b1f None: z already holds the bias).  W2 [H, F]
@@ -102,6 +107,8 @@ def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f, dgelu=False):
     if T % 256 or F % 256 or df.shape[1] % 64:
         return None
     dz = torch.empty_like(z)
+    if db1f is None:                                   # no bias-gradient sums in the epilogue
+        return dz if C.gemm_nn(df, W2, dz, 7 if dgelu else 2, False, None if dgelu else b1f, z, None) else None
     direct = db1f.dtype == torch.bfloat16 and db1f.is_contiguous()
     rows = _DB_ROWS if direct else 1
     db = _zeroed_acc(z.device, F, rows) if direct else torch.zeros(1, F, device=z.device, dtype=torch.float32)
@@ -317,7 +324,17 @@ class _FFNBlockFn(torch.autograd.Function):
         _ready(*[p for p, f in ((g2, fg2), (b2, fb2), (b2f, fb2f)) if f])
         dW2 = _wgrad(W2, df, h)
         db1f, fb1f = _vec_grad_out(b1f)
-        dz = _fused_ffn_dgrad(C, df.contiguous(), W2, z, zbias, db1f, dgelu) if _FUSED_FFN_DGRAD else None
+        bias_in_wgrad = _FFN_BGRAD_IN_WGRAD and dgelu and fb1f and _flat(W1)
+        dz = (_fused_ffn_dgrad(C, df.contiguous(), W2, z, zbias, None if bias_in_wgrad else db1f, dgelu)
+              if _FUSED_FFN_DGRAD else None)
+        if dz is not None and bias_in_wgrad:
+            dW1 = _wgrad(W1, dz, x2, bias=b1f)         # bias gradient fused into the wgrad GEMM
+            dx = _stream_mm("dx_ffn", dz, W1, True, out=ds, side=wgrad_side(W1))
+            if dx is None:
+                dx = ds.addmm_(dz, W1)
+            return (dx.view(B, S, H), dW1, None, dW2, None if fb2f else db2f,
+                    None if fg2 else dg2, None if fb2 else db2, None, None, None, None)
+        bias_in_wgrad = False
         if dz is None and dgelu:
             dz = torch.mm(df, W2).mul_(z)
             db1f.add_(dz.float().sum(0).to(db1f.dtype))
