@@ -45,7 +45,8 @@ sys.path.insert(0, REPO)
 
 # no published reference number exists (BASELINE.json "published": {}); vs_baseline = null
 BASELINE = {"bert-large": None, "resnet50": None}
-TUNE_FILE = os.path.join(REPO, "cloudtik_amd", "ops", "tunableop", "gfx950_tunableop.csv")
+TUNE_FILE = os.environ.get("CLOUDTIK_BENCH_TUNE_FILE") or os.path.join(REPO, "cloudtik_amd", "ops", "tunableop",
+                                                                         "gfx950_tunableop.csv")
 
 
 def parse(argv=None):
@@ -86,7 +87,8 @@ def parse(argv=None):
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto: RCCL on GPU, gloo on CPU; gloo on GPU lets several ranks share "
                          "one GPU (plumbing check of the GPU data-parallel path without RCCL)")
-    ap.add_argument("--tunableop", default="use", choices=["off", "use", "tune"],
+    ap.add_argument("--tunableop", default=os.environ.get("CLOUDTIK_BENCH_TUNABLEOP", "use"),
+                    choices=["off", "use", "tune"],
                     help="hipBLASLt solution selection via PyTorch TunableOp (results shipped in-tree)")
     return ap.parse_args(argv)
 
