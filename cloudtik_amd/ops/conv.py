@@ -395,12 +395,21 @@ _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
 # 1x1 stride-1 weight gradients with 256-multiple channel counts on the TN GEMM kernel
 _TN_WGRAD_1X1 = os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "1") == "1"
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128),
-             7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256)}
+             7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256), 12: (64, 576), 13: (64, 576)}
+# 3x3 / stride 1 / pad 1 weight gradients on the nine-tap kernel (conv.hip conv_wgrad3x3_kernel):
+# one workgroup owns 64 output x 64 input channels of all nine taps.  -1 = auto (cfg 12, a 3-slot
+# ring at one workgroup per CU; cfg 13, 2 slots at two per CU and twice the split-K workgroups,
+# where the channel tiles alone make 64+ workgroups), 0 = the per-tap tiles, 12 / 13 = forced.
+# Probe (bench/wgrad3x3_probe.py, batch 256): l1.c2 297 -> 95 us, l2.c2 130 -> 92, l3.c2 108 -> 79,
+# l4.c2 140 -> 72
+_WG3X3 = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3", "-1"))
+_WG3X3_MAXCI = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_MAXCI", "4096"))
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
 WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
 # the same target for the tiles narrower than 128 x 256 (cfg 3 / 11 keep WGRAD_BLOCKS): at 256
 # workgroups the 64-wide 4-wave tiles run one wave per SIMD (l1.c2 299 us, 187 at 512)
 WGRAD_BLOCKS_SMALL = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS_SMALL", "256"))
+WGRAD3X3_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_BLOCKS", "256"))
 
 
 def wgrad_plan(M: int, co: int, nn: int, cfg: int):
@@ -409,6 +418,8 @@ def wgrad_plan(M: int, co: int, nn: int, cfg: int):
     bm, bn = _WG_TILES[cfg]
     tiles = (co // bm) * (nn // bn)
     blocks = WGRAD_BLOCKS if cfg in (3, 11) else WGRAD_BLOCKS_SMALL
+    if cfg >= 12:                      # nine-tap kernel: cfg 13 runs two workgroups per CU
+        blocks = WGRAD3X3_BLOCKS * (2 if cfg == 13 else 1)
     splits = max(1, min(blocks // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
     q = 64 if cfg >= 4 and cfg != 9 else 32        # pixels per stage of the configuration
     rows = ((M + splits - 1) // splits + q - 1) // q * q
@@ -444,6 +455,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=(1, 1), paddin
             return out
     C = _C()
     cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
+    if (_WG_CFG < 0 and _WG3X3 != 0 and R == 3 and S == 3 and tuple(stride) == (1, 1)
+            and tuple(padding) == (1, 1) and ci % 64 == 0 and co % 64 == 0 and ci <= _WG3X3_MAXCI
+            and M * max(ci, co) * 2 < 2 ** 31):      # 32-bit buffer offsets
+        cfg = _WG3X3 if _WG3X3 > 0 else (13 if (co // 64) * (ci // 64) >= 64 else 12)
     splits, rows = wgrad_plan(M, co, nn, cfg)
     part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)
     if not C.conv_wgrad(dy, x, part, taps, [stride[0], stride[1], rows], splits, cfg):

@@ -101,6 +101,15 @@ __device__ __forceinline__ void cv_glds16s(const void* sbase, unsigned voff, con
                : "memory", "m0");
 }
 
+// LDS-DMA by buffer load: 32-bit per-lane byte offset into a buffer resource whose range check
+// returns zeros past num_records (inline asm: a compiler-visible LDS-DMA makes hipcc wait for it
+// before every later LDS read, which drains the ring)
+__device__ __forceinline__ void cv_bglds16(__amdgpu_buffer_rsrc_t r, unsigned voff, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(cv_lds_void*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r), "s"(la)
+               : "memory", "m0");
+}
+
 __device__ __forceinline__ cv_s16x8 cv_frag(const char* img, int r0, int ks, int lane) {
   const int row = r0 + (lane & 15);
   const int kc = ks * 4 + (lane >> 4);
@@ -905,6 +914,110 @@ static int wg_launch(const WgradArgs& a, int splits, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
+// Weight gradient of a 3x3 / stride 1 / pad 1 convolution with ALL NINE TAPS in one workgroup:
+// tile = 64 output channels x (9 taps x 64 input channels).  The generic kernel above gives each
+// tap its own 64 x 64 tile, so every 32-pixel stage moved 8 KB for 16 MFMAs per workgroup and
+// re-fetched dY once per tap: at ResNet-50's 64-channel layer-1 shape (802,816 pixels) it ran
+// at ~0.2 PF/s, latency-bound behind one barrier per tiny stage.  Here a stage is dY [32 px][64
+// co] (4 KB) + the nine shifted X tiles [32 px][64 ci] (36 KB): 36 MFMAs per wave per barrier,
+// dY fetched once.
+//   * wave w stages pixel rows 8 w .. 8 w + 7 of every tile (one 1 KB LDS-DMA per tile), so a
+//     lane tracks ONE pixel; the loads are buffer loads whose range check supplies the zeros:
+//     dY's range ends at the split's last row, X's at the tensor end, and a tap that leaves the
+//     image (four border masks per stage) gets an offset past the range.  Per tap that is one
+//     add and one select -- the 64-bit gather addressing of the first version spent ~140 VALU
+//     per stage and ran at 3,100 wave-cycles per 576-cycle MFMA stage;
+//   * for the MFMAs wave w owns input channels 16 w .. 16 w + 15 of all nine taps and all 64
+//     output channels: acc[4 co blocks][9 taps] = 144 accumulator registers;
+//   * fp32 partial slabs [split][Co][9 * Ci] as the generic kernel (same reduce).
+template <int NS>
+__global__ void __launch_bounds__(256, 2) conv_wgrad3x3_kernel(WgradArgs a) {
+  constexpr int BK = 32, TT = BK * 128, STG = 10 * TT;   // dY + 9 tap tiles, 4 KB each
+  static_assert(NS * STG <= 160 * 1024, "wgrad3x3 ring");
+  __shared__ __attribute__((aligned(1024))) char lds[NS * STG];
+  const int ci_tiles = a.Ci / 64, tiles = (a.Co / 64) * ci_tiles;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, tile = L % tiles;
+  const int c0 = (tile / ci_tiles) * 64, ci0 = (tile % ci_tiles) * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.Hi, W = a.Wi;
+  const int kbeg = split * a.rows_per_split;
+  const int kend = min(a.M, kbeg + a.rows_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const int r = wave * 8 + (lane >> 3);
+  const int chunk = ((lane & 7) ^ wg_swz<8>(r)) << 3;
+  const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc((void*)a.DY, 0, kend * a.Co * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.X, 0, a.M * a.Ci * 2, 0x00020000);
+  unsigned vdy = (unsigned)((kbeg + r) * a.Co + c0 + chunk) * 2u;
+  unsigned vx = (unsigned)((kbeg + r) * a.Ci + ci0 + chunk) * 2u;
+  const unsigned sdy = BK * a.Co * 2, sxs = BK * a.Ci * 2;
+  const int rowb = W * a.Ci * 2, colb = a.Ci * 2;
+  const int ay = BK / W, ax = BK - (BK / W) * W;     // per-stage pixel advance
+  int py, px;
+  {
+    const int rem = (kbeg + r) % (H * W);
+    py = rem / W;
+    px = rem - py * W;
+  }
+
+  auto stage = [&](int slot) {
+    char* S = lds + slot * STG + wave * 1024;
+    cv_bglds16(rdy, vdy, S);
+    const bool top = py > 0, bot = py < H - 1, lef = px > 0, rig = px < W - 1;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool ok = (dy < 0 ? top : (dy > 0 ? bot : true)) && (dx < 0 ? lef : (dx > 0 ? rig : true));
+      const unsigned off = vx + (unsigned)(dy * rowb + dx * colb);
+      cv_bglds16(rx, ok ? off : 0x80000000u, S + (1 + t) * TT);
+    }
+    vdy += sdy;
+    vx += sxs;
+    px += ax;
+    py += ay;
+    if (px >= W) { px -= W; ++py; }
+    while (py >= H) py -= H;
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = nk - 1 - kt;
+    cv_wait_stage<10, NS>(ahead < NS - 2 ? ahead : NS - 2);
+    cv_bar();
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS);
+    const char* As = lds + (kt % NS) * STG;
+    cv_s16x8 fa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = wg_frag<128>(As, 16 * i, lane);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const cv_s16x8 fb = wg_frag<128>(As + (1 + t) * TT, 16 * wave, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((bf16x8_t)fb, (bf16x8_t)fa[i], acc[i][t], 0, 0, 0);
+    }
+  }
+  // acc[i][t][q] = dW[c0 + 16 i + (lane & 15)][t * Ci + ci0 + 16 wave + 4 (lane >> 4) + q]
+  float* P = a.P + (long)split * a.Co * a.NN;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long row = c0 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      *(f32x4*)(P + row * a.NN + t * a.Ci + ci0 + 16 * wave + 4 * (lane >> 4)) = acc[i][t];
+  }
+}
+
 // Chan merge of per-tile (mean, M2) partials -> per-channel mean and biased variance, in
 // fp64 (tiles x channels is small).  One thread per channel.
 __global__ void bn_partials_finalize_kernel(const float* __restrict__ part, int tiles, int rows_per_tile, int M,
@@ -1329,7 +1442,8 @@ __global__ void __launch_bounds__(256) splitk_wide_kernel(const float* __restric
 // 3 = 128x256 (8 waves 2x4); 4 / 5 / 6 = cfg 0 / 1 / 2 with 64-pixel stages (two MFMA k-steps per
 // barrier); 7 / 8 = cfg 4 with a 2 / 3-slot ring (more workgroups per CU); 9 / 10 = 128x128 on 8
 // waves (2x4), 32-pixel stages x 4 slots / 64-pixel x 2; 11 = 128x256 on 16 waves (4x4), 64-pixel
-// stages x 2; -1 = the largest that divides (Co, T*Ci)
+// stages x 2; 12 / 13 = the nine-tap 3x3 kernel (64 co x 9 x 64 ci) with a 3 / 2-slot ring;
+// -1 = the largest that divides (Co, T*Ci)
 extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   if (cfg >= 0) return cfg;
   // per-shape probe over every ResNet-50 conv (profiles/r3/conv_wgrad_cfg.md): the 8-wave
@@ -1385,6 +1499,17 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
+  if (cfg == 12 || cfg == 13) {      // 3x3 / stride 1 / pad 1, all taps per workgroup
+    if (T != 9 || sy != 1 || sx != 1 || Hr != Hi || Wr != Wi || pixchunk || Ci % 64) return 2;
+    if ((long)M * Ci * 2 >= (1L << 31) || (long)M * Co * 2 >= (1L << 31)) return 5;   // 32-bit buffer offsets
+    for (int t = 0; t < 9; ++t)
+      if (taps[2 * t] != t / 3 - 1 || taps[2 * t + 1] != t % 3 - 1) return 4;
+    const long blocks = (long)(Co / 64) * (Ci / 64) * splits;
+    if (blocks > (1L << 30)) return 5;
+    if (cfg == 12) conv_wgrad3x3_kernel<3><<<(int)blocks, 256, 0, stream>>>(a);
+    else conv_wgrad3x3_kernel<2><<<(int)blocks, 256, 0, stream>>>(a);
+    return hipGetLastError() == hipSuccess ? 0 : 7;
+  }
   const int tile = cfg == 11 ? 3 : (cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg)));
   if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
   if (cfg >= 4 && cfg != 9 && rows_per_split % 64) return 2;
