@@ -396,20 +396,21 @@ _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
 _TN_WGRAD_1X1 = os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "1") == "1"
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128),
              7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256), 12: (64, 576), 13: (64, 576)}
-# 3x3 / stride 1 / pad 1 weight gradients on the nine-tap kernel (conv.hip conv_wgrad3x3_kernel):
+# 3x3 / stride 1 or 2 / pad 1 weight gradients on the nine-tap kernel (conv.hip conv_wgrad3x3_kernel):
 # one workgroup owns 64 output x 64 input channels of all nine taps.  -1 = auto (cfg 12, a 3-slot
 # ring at one workgroup per CU; cfg 13, 2 slots at two per CU and twice the split-K workgroups,
 # where the channel tiles alone make 64+ workgroups), 0 = the per-tap tiles, 12 / 13 = forced.
 # Probe (bench/wgrad3x3_probe.py, batch 256): l1.c2 297 -> 95 us, l2.c2 130 -> 92, l3.c2 108 -> 79,
 # l4.c2 140 -> 72
 _WG3X3 = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3", "-1"))
+_WG3X3_S2 = os.environ.get("CLOUDTIK_AMD_WGRAD3X3_S2", "1") == "1"
 _WG3X3_MAXCI = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_MAXCI", "4096"))
 PARTIAL_BYTES = 64 << 20           # cap of the fp32 split-K slabs per weight gradient
 WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split-K target workgroups
 # the same target for the tiles narrower than 128 x 256 (cfg 3 / 11 keep WGRAD_BLOCKS): at 256
 # workgroups the 64-wide 4-wave tiles run one wave per SIMD (l1.c2 299 us, 187 at 512)
 WGRAD_BLOCKS_SMALL = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS_SMALL", "256"))
-WGRAD3X3_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_BLOCKS", "256"))
+WGRAD3X3_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_BLOCKS", "128"))
 
 
 def wgrad_plan(M: int, co: int, nn: int, cfg: int):
@@ -455,9 +456,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=(1, 1), paddin
             return out
     C = _C()
     cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
-    if (_WG_CFG < 0 and _WG3X3 != 0 and R == 3 and S == 3 and tuple(stride) == (1, 1)
+    if (_WG_CFG < 0 and _WG3X3 != 0 and R == 3 and S == 3
+            and (tuple(stride) == (1, 1) or (_WG3X3_S2 and tuple(stride) == (2, 2)))
             and tuple(padding) == (1, 1) and ci % 64 == 0 and co % 64 == 0 and ci <= _WG3X3_MAXCI
-            and M * max(ci, co) * 2 < 2 ** 31):      # 32-bit buffer offsets
+            and max(x.numel(), dy.numel()) * 2 < 2 ** 31):      # 32-bit buffer offsets
         cfg = _WG3X3 if _WG3X3 > 0 else (13 if (co // 64) * (ci // 64) >= 64 else 12)
     splits, rows = wgrad_plan(M, co, nn, cfg)
     part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)

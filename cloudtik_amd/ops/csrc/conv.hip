@@ -914,7 +914,7 @@ static int wg_launch(const WgradArgs& a, int splits, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
-// Weight gradient of a 3x3 / stride 1 / pad 1 convolution with ALL NINE TAPS in one workgroup:
+// Weight gradient of a 3x3 / pad 1 convolution (stride 1 or 2) with ALL NINE TAPS in one workgroup:
 // tile = 64 output channels x (9 taps x 64 input channels).  The generic kernel above gives each
 // tap its own 64 x 64 tile, so every 32-pixel stage moved 8 KB for 16 MFMAs per workgroup and
 // re-fetched dY once per tap: at ResNet-50's 64-channel layer-1 shape (802,816 pixels) it ran
@@ -941,31 +941,37 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad3x3_kernel(WgradArgs a) {
   const int c0 = (tile / ci_tiles) * 64, ci0 = (tile % ci_tiles) * 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = a.Hi, W = a.Wi;
+  // output pixel grid Hr x Wr at stride sd (1 or 2) over the Hi x Wi input
+  const int Hi = a.Hi, Wi = a.Wi, Hr = a.Hr, Wr = a.Wr, sd = a.sy;
   const int kbeg = split * a.rows_per_split;
   const int kend = min(a.M, kbeg + a.rows_per_split);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   const int r = wave * 8 + (lane >> 3);
   const int chunk = ((lane & 7) ^ wg_swz<8>(r)) << 3;
+  const int nimg = a.M / (Hr * Wr);
   const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc((void*)a.DY, 0, kend * a.Co * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.X, 0, a.M * a.Ci * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.X, 0, nimg * Hi * Wi * a.Ci * 2, 0x00020000);
   unsigned vdy = (unsigned)((kbeg + r) * a.Co + c0 + chunk) * 2u;
-  unsigned vx = (unsigned)((kbeg + r) * a.Ci + ci0 + chunk) * 2u;
-  const unsigned sdy = BK * a.Co * 2, sxs = BK * a.Ci * 2;
-  const int rowb = W * a.Ci * 2, colb = a.Ci * 2;
-  const int ay = BK / W, ax = BK - (BK / W) * W;     // per-stage pixel advance
-  int py, px;
+  const unsigned sdy = BK * a.Co * 2, xcol = (unsigned)(ci0 + chunk) * 2u;
+  const int rowb = Wi * a.Ci * 2, colb = a.Ci * 2;
+  const int ay = BK / Wr, ax = BK - (BK / Wr) * Wr;   // per-stage pixel advance
+  int pb, py, px;
   {
-    const int rem = (kbeg + r) % (H * W);
-    py = rem / W;
-    px = rem - py * W;
+    const int m = kbeg + r;
+    pb = m / (Hr * Wr);
+    const int rem = m - pb * Hr * Wr;
+    py = rem / Wr;
+    px = rem - py * Wr;
   }
 
   auto stage = [&](int slot) {
     char* S = lds + slot * STG + wave * 1024;
     cv_bglds16(rdy, vdy, S);
-    const bool top = py > 0, bot = py < H - 1, lef = px > 0, rig = px < W - 1;
+    const int iy = sd * py, ix = sd * px;               // the centre tap's input pixel
+    const unsigned vx = (unsigned)(((pb * Hi + iy) * Wi + ix) * a.Ci) * 2u + xcol;
+    const bool top = iy > 0, bot = iy < Hi - 1, lef = ix > 0, rig = ix < Wi - 1;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int dy = t / 3 - 1, dx = t % 3 - 1;
@@ -974,11 +980,10 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad3x3_kernel(WgradArgs a) {
       cv_bglds16(rx, ok ? off : 0x80000000u, S + (1 + t) * TT);
     }
     vdy += sdy;
-    vx += sxs;
     px += ax;
     py += ay;
-    if (px >= W) { px -= W; ++py; }
-    while (py >= H) py -= H;
+    if (px >= Wr) { px -= Wr; ++py; }
+    while (py >= Hr) { py -= Hr; ++pb; }
   };
 
   f32x4 acc[4][9];
@@ -1499,9 +1504,11 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     a.tdx |= (unsigned long long)(dx + 8) << (4 * t);
   }
   cfg = ct_conv_wgrad_cfg(cfg, Co, a.NN);
-  if (cfg == 12 || cfg == 13) {      // 3x3 / stride 1 / pad 1, all taps per workgroup
-    if (T != 9 || sy != 1 || sx != 1 || Hr != Hi || Wr != Wi || pixchunk || Ci % 64) return 2;
-    if ((long)M * Ci * 2 >= (1L << 31) || (long)M * Co * 2 >= (1L << 31)) return 5;   // 32-bit buffer offsets
+  if (cfg == 12 || cfg == 13) {      // 3x3 / stride 1 or 2 / pad 1, all taps per workgroup
+    if (T != 9 || sy != sx || (sy != 1 && sy != 2) || Hr != (Hi - 1) / sy + 1 || Wr != (Wi - 1) / sx + 1 || pixchunk ||
+        Ci % 64)
+      return 2;
+    if ((long)M / (Hr * Wr) * Hi * Wi * Ci * 2 >= (1L << 31) || (long)M * Co * 2 >= (1L << 31)) return 5;   // 32-bit buffer offsets
     for (int t = 0; t < 9; ++t)
       if (taps[2 * t] != t / 3 - 1 || taps[2 * t + 1] != t % 3 - 1) return 4;
     const long blocks = (long)(Co / 64) * (Ci / 64) * splits;

@@ -119,22 +119,25 @@ def test_kernels_match_fp32_reference(cuda, ci, co, H, k, s):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [12, 13])
-@pytest.mark.parametrize("ci,co,H,n", [(64, 64, 14, 3), (128, 128, 7, 5), (64, 192, 11, 2), (256, 128, 9, 3), (64, 64, 5, 7)])
-def test_wgrad_3x3_nine_tap_kernel(cuda, monkeypatch, cfg, ci, co, H, n):
+@pytest.mark.parametrize("ci,co,H,n,s", [(64, 64, 14, 3, 1), (128, 128, 7, 5, 1), (64, 192, 11, 2, 1),
+                                         (256, 128, 9, 3, 1), (64, 64, 5, 7, 1), (128, 128, 14, 3, 2),
+                                         (64, 128, 15, 4, 2), (256, 64, 7, 6, 2)])
+def test_wgrad_3x3_nine_tap_kernel(cuda, monkeypatch, cfg, ci, co, H, n, s):
     """The all-taps 3x3 weight-gradient kernel (cfg 12 / 13) against the fp32 reference: image
-    borders (zero taps), split-K boundaries inside an image, several channel tiles."""
+    borders (zero taps), split-K boundaries inside an image, several channel tiles, stride 2
+    (even and odd input sizes)."""
     monkeypatch.setattr(CV, "_WG3X3", cfg)
     torch.manual_seed(ci + co + H + cfg)
     x = _nhwc(torch.randn(n, ci, H, H, device=cuda).to(torch.bfloat16))
     w = _nhwc(torch.randn(co, ci, 3, 3, device=cuda).to(torch.bfloat16))
     wr = w.float().requires_grad_()
-    ref = F.conv2d(x.float(), wr, padding=1)
+    ref = F.conv2d(x.float(), wr, stride=s, padding=1)
     dy = _nhwc(torch.randn(ref.shape, device=cuda).to(torch.bfloat16))
     ref.backward(dy.float())
-    dw = CV.conv_wgrad(dy, x, w.shape, (1, 1), (1, 1))
+    dw = CV.conv_wgrad(dy, x, w.shape, (s, s), (1, 1))
     assert _rel(dw, wr.grad) < 1e-2
     base = _nhwc(torch.randn(w.shape, device=cuda).to(torch.bfloat16))
-    dw2 = CV.conv_wgrad(dy, x, w.shape, (1, 1), (1, 1), out=base.clone(), accumulate=True)
+    dw2 = CV.conv_wgrad(dy, x, w.shape, (s, s), (1, 1), out=base.clone(), accumulate=True)
     assert _rel(dw2, wr.grad + base.float()) < 1e-2
 
 
