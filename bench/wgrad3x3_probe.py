@@ -1,4 +1,4 @@
-"""3x3 weight-gradient kernels on the ResNet-50 3x3 shapes (stride 1 and 2) (batch 256): total time of
+"""Conv weight-gradient kernels on ResNet-50 shapes (3x3 stride 1 / 2, narrow 1x1; batch 256): total time of
 ``ops.conv.conv_wgrad`` (kernel + split-K reduce) per configuration.  Run under
 ``rocprofv3 --kernel-trace --stats`` for the kernel / reduce split.
 
@@ -14,8 +14,13 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cloudtik_amd.ops import conv as CV  # noqa: E402
 
-SHAPES = {"l1": (64, 56, 1), "l2": (128, 28, 1), "l3": (256, 14, 1), "l4": (512, 7, 1),
-          "l2s2": (128, 56, 2), "l3s2": (256, 28, 2), "l4s2": (512, 14, 2)}
+# name: (ci, co, input H, kernel, stride)
+SHAPES = {"l1": (64, 64, 56, 3, 1), "l2": (128, 128, 28, 3, 1), "l3": (256, 256, 14, 3, 1), "l4": (512, 512, 7, 3, 1),
+          "l2s2": (128, 128, 56, 3, 2), "l3s2": (256, 256, 28, 3, 2), "l4s2": (512, 512, 14, 3, 2),
+          "l1c3": (64, 256, 56, 1, 1), "l1c1": (256, 64, 56, 1, 1), "l1c1a": (64, 64, 56, 1, 1),
+          "l2c3": (128, 512, 28, 1, 1), "l2c1": (512, 128, 28, 1, 1), "l3c1a": (512, 256, 28, 1, 1),
+          "l3c3": (256, 1024, 14, 1, 1), "l3c1": (1024, 256, 14, 1, 1), "l4c1a": (1024, 512, 14, 1, 1),
+          "l4c3": (512, 2048, 7, 1, 1), "l4c1": (2048, 512, 7, 1, 1)}
 
 
 def main():
@@ -27,15 +32,16 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda")
     for name in a.shapes.split(","):
-        c, H, st = SHAPES[name]
-        Ho = (H - 1) // st + 1
-        x = torch.randn(a.batch, c, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        dy = torch.randn(a.batch, c, Ho, Ho, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        shape = (c, c, 3, 3)
-        row = {"shape": name, "gflop": round(2 * a.batch * Ho * Ho * c * c * 9 / 1e9, 1)}
+        ci, co, H, k, st = SHAPES[name]
+        pad = k // 2
+        Ho = (H + 2 * pad - k) // st + 1
+        x = torch.randn(a.batch, ci, H, H, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dy = torch.randn(a.batch, co, Ho, Ho, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        shape = (co, ci, k, k)
+        row = {"shape": name, "gflop": round(2 * a.batch * Ho * Ho * co * ci * k * k / 1e9, 1)}
         for cfg in [int(v) for v in a.cfgs.split(",")]:
             CV._WG_CFG = cfg
-            fn = lambda: CV.conv_wgrad(dy, x, shape, (st, st), (1, 1))  # noqa: E731
+            fn = lambda: CV.conv_wgrad(dy, x, shape, (st, st), (pad, pad))  # noqa: E731
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()

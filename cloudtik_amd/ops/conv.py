@@ -393,7 +393,12 @@ def _dgrad_phase(C, dy, wm, ci, co, N, H, W, Hr, Wr, a, b, sh, sw, taps, out, ac
 
 _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
 # 1x1 stride-1 weight gradients with 256-multiple channel counts on the TN GEMM kernel
-_TN_WGRAD_1X1 = os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "1") == "1"
+# (2: every 256-multiple shape; 1: only where it beats the implicit-GEMM kernel's linear 1x1 mode
+# alone -- 32K-64K pixels and 1024+ output channels: l3.c3 57 vs 66 us, but l3.c1a at 200K pixels
+# 164 vs 88 us, l4.c3 47 vs 43 (bench/wgrad3x3_probe.py).  In the step rule 1 is SLOWER, 21.37 ->
+# 21.46 ms (profiles/r5/wgrad3x3.md): the TN GEMM's few large tiles leave the data gradients on the
+# main stream more of the chip; 0: never)
+_TN_WGRAD_1X1 = int(os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "2"))
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128),
              7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256), 12: (64, 576), 13: (64, 576)}
 # 3x3 / stride 1 or 2 / pad 1 weight gradients on the nine-tap kernel (conv.hip conv_wgrad3x3_kernel):
@@ -441,6 +446,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride=(1, 1), paddin
     M = dy.shape[0] * dy.shape[2] * dy.shape[3]
     if (_TN_WGRAD_1X1 and R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(padding) == (0, 0)
             and co % 256 == 0 and ci % 256 == 0 and M % 64 == 0
+            and (_TN_WGRAD_1X1 == 2 or (32768 < M <= 65536 and co >= 1024))
             and dy.is_contiguous(memory_format=torch.channels_last)
             and x.is_contiguous(memory_format=torch.channels_last)):
         # a 1x1 stride-1 weight gradient IS the linear one, dW = dY^T X over the pixel rows: the

@@ -784,7 +784,10 @@ __device__ __forceinline__ cv_s16x8 wg_frag(const char* img, int col0, int lane)
   return cv_s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BMC, int BNC, int WGM, int WGN, int NS, int BK = 32>
+// LIN: a 1x1 / stride-1 weight gradient, X row = pixel: both operands are linear in the pixel
+// index and stream by buffer loads (32-bit offsets, one add per row per stage; rows past the split
+// read zeros from the range check) instead of the per-row (b, y, x) gather
+template <int BMC, int BNC, int WGM, int WGN, int NS, int BK = 32, bool LIN = false>
 __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs a) {
   // BK pixels per stage (32 or 64: one or two MFMA k-steps per barrier)
   constexpr int NW = WGM * WGN;
@@ -839,9 +842,34 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
     xb[j] = rem - yb[j] * a.Wr;
   }
 
+  // LIN operand streams
+  __amdgpu_buffer_rsrc_t rdy, rx;
+  unsigned va[GA], vb[GB];
+  if constexpr (LIN) {
+    rdy = __builtin_amdgcn_make_buffer_rsrc((void*)a.DY, 0, kend * a.Co * 2, 0x00020000);
+    rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.X, 0, a.M * a.Ci * 2, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < GA; ++j) va[j] = (unsigned)((kbeg + ra[j]) * a.Co + (int)ga_off[j]) * 2u;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) vb[j] = (unsigned)((kbeg + rb[j]) * a.Ci + cib[j]) * 2u;
+  }
+
   auto stage = [&](int s, int slot) {
     char* As = lds + slot * STG;
     char* Bs = As + TA;
+    if constexpr (LIN) {
+#pragma unroll
+      for (int j = 0; j < GA; ++j) {
+        cv_bglds16(rdy, va[j], As + (wave * GA + j) * 1024);
+        va[j] += BK * a.Co * 2;
+      }
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        cv_bglds16(rx, vb[j], Bs + (wave * GB + j) * 1024);
+        vb[j] += BK * a.Ci * 2;
+      }
+      return;
+    }
     const int kb = kbeg + s * BK;
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
@@ -906,11 +934,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
   }
 }
 
-template <int BMC, int BNC, int WGM, int WGN, int NS, int BK = 32>
+template <int BMC, int BNC, int WGM, int WGN, int NS, int BK = 32, bool LIN = false>
 static int wg_launch(const WgradArgs& a, int splits, hipStream_t s) {
   const long blocks = (long)(a.Co / BMC) * (a.NN / BNC) * splits;
   if (blocks > (1L << 30)) return 5;
-  conv_wgrad_kernel<BMC, BNC, WGM, WGN, NS, BK><<<(int)blocks, 64 * WGM * WGN, 0, s>>>(a);
+  conv_wgrad_kernel<BMC, BNC, WGM, WGN, NS, BK, LIN><<<(int)blocks, 64 * WGM * WGN, 0, s>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
@@ -1520,6 +1548,21 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
   const int tile = cfg == 11 ? 3 : (cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg)));
   if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
   if (cfg >= 4 && cfg != 9 && rows_per_split % 64) return 2;
+  static const bool lin_on = [] {
+    const char* e = std::getenv("CLOUDTIK_AMD_WGRAD_LIN");
+    return !e || std::atoi(e) != 0;
+  }();
+  const bool lin = lin_on && T == 1 && taps[0] == 0 && taps[1] == 0 && sy == 1 && sx == 1 && Hr == Hi && Wr == Wi &&
+                   !pixchunk && (long)M * Co * 2 < (1L << 31) && (long)M * Ci * 2 < (1L << 31);
+  if (lin) {
+    switch (cfg) {
+      case 3: return wg_launch<128, 256, 2, 4, 4, 32, true>(a, splits, stream);
+      case 5: return wg_launch<64, 128, 2, 2, 4, 64, true>(a, splits, stream);
+      case 8: return wg_launch<64, 64, 2, 2, 3, 64, true>(a, splits, stream);
+      case 9: return wg_launch<128, 128, 2, 4, 4, 32, true>(a, splits, stream);
+      default: break;
+    }
+  }
   switch (cfg) {
     case 0: return wg_launch<64, 64, 2, 2, 4>(a, splits, stream);
     case 1: return wg_launch<64, 128, 2, 2, 4>(a, splits, stream);
