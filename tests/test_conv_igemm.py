@@ -446,7 +446,7 @@ def test_wgrad_64_pixel_stages_match_fp32_reference(cuda, monkeypatch, wcfg, ci,
 def test_1x1_wgrad_on_tn_gemm(cuda, monkeypatch, tn):
     """1x1 stride-1 weight gradients with 256-multiple channels go through the linear TN GEMM
     (split-K): fresh and accumulated into an existing gradient, vs fp32."""
-    monkeypatch.setattr(CV, "_TN_WGRAD_1X1", tn)
+    monkeypatch.setattr(CV, "_TN_WGRAD_1X1", 2 if tn else 0)
     import importlib
     L = importlib.import_module("cloudtik_amd.ops.linear")     # (ops.linear is also a function)
     calls = []
