@@ -643,14 +643,29 @@ def stem_weight(w: torch.Tensor) -> torch.Tensor:
     return wp.reshape(co, R * 64)
 
 
-def stem_fwd(x8: torch.Tensor, w: torch.Tensor, stride, padding) -> torch.Tensor:
+# the stem conv's epilogue reduces the BatchNorm statistics of its output per tile (EPI 1), so the
+# fused BN + ReLU + max-pool skips its statistics pass over the 112x112x64 activation
+_STEM_STATS = os.environ.get("CLOUDTIK_AMD_STEM_STATS", "1") == "1"
+
+
+def stem_fwd(x8: torch.Tensor, w: torch.Tensor, stride, padding, partials: bool = False) -> torch.Tensor:
+    """The stem conv; with ``partials`` the output carries its BatchNorm tile statistics as
+    ``_ct_bn_part`` (ops.batch_norm_relu_maxpool consumes them)."""
     n, _, H, W = x8.shape
     co, c, R, S = w.shape
     Ho, Wo = out_size(H, R, stride[0], padding[0]), out_size(W, S, stride[1], padding[1])
     out = torch.empty((n, co, Ho, Wo), device=x8.device, dtype=x8.dtype, memory_format=torch.channels_last)
     geo = [Ho, Wo, stride[0], stride[1], Ho, Wo, 1, 1, 0, 0, co, n * Ho * Wo]
-    if not _C().conv_igemm(x8, stem_weight(w), out, geo, _stem_taps(R, padding), False, None, _CFG):
+    C = _C()
+    part = bm = None
+    if partials:
+        bm = C.conv_igemm_part_rows(_CFG, co, geo[11], R)
+        tiles = (geo[11] + bm - 1) // bm
+        part = torch.empty((tiles + (tiles + 63) // 64) * 2 * co, device=x8.device, dtype=torch.float32)
+    if not C.conv_igemm(x8, stem_weight(w), out, geo, _stem_taps(R, padding), False, part, _CFG):
         raise RuntimeError(f"conv_igemm (stem) rejected x{tuple(x8.shape)} w{tuple(w.shape)}")
+    if partials:
+        out._ct_bn_part = (part, bm)
     return out
 
 
@@ -680,7 +695,7 @@ class StemFn(torch.autograd.Function):
         ctx.save_for_backward(x8)
         ctx.stride, ctx.padding, ctx.w_shape = stride, padding, tuple(w.shape)
         ctx.wp = w
-        return stem_fwd(x8, w, stride, padding)
+        return stem_fwd(x8, w, stride, padding, partials=_STEM_STATS)
 
     @staticmethod
     def backward(ctx, dy):

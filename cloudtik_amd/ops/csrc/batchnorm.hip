@@ -942,6 +942,22 @@ extern "C" int ct_bn_fwd_train_pool(const void* x, const void* gamma, const void
   return 0;
 }
 
+// The same with the statistics from the stem conv's epilogue partials (conv.hip EPI 1): no
+// statistics pass over the full-resolution conv output
+extern "C" int ct_bn_fwd_train_pool_given(const void* x, const void* gamma, const void* beta, float* run_mean,
+                                          float* run_var, void* y, void* arg, const float* part, int tiles,
+                                          int rows_per_tile, float* stat, int N, int H, int W, int C, int OH, int OW,
+                                          float eps, float momentum, hipStream_t stream) {
+  const int M = N * H * W;
+  if (C % 8 || M <= 0 || tiles <= 0 || (long)tiles * rows_per_tile < M || OH != (H - 1) / 2 + 1 ||
+      OW != (W - 1) / 2 + 1 || (long)N * OH >= (1L << 31))
+    return -1;
+  bn_given_finalize(part, tiles, rows_per_tile, gamma, beta, run_mean, run_var, stat, M, C, eps, momentum, stream);
+  bn_apply_pool_kernel<<<N * OH, 256, 0, stream>>>((const bf16_t*)x, stat + 2 * C, stat + 3 * C, (bf16_t*)y,
+                                                   (uint8_t*)arg, N, H, W, C / 8, OH, OW);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
 extern "C" int ct_maxpool3s2_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, int OH,
                                  int OW, hipStream_t stream) {
   if (C % 8 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;

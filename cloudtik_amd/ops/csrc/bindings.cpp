@@ -44,6 +44,8 @@ int ct_bn_fwd_train(const void*, const void*, const void*, const void*, float*, 
 int ct_bn_apply(const void*, const void*, const float*, const float*, void*, int, int, int, hipStream_t);
 int ct_bn_fwd_train_given(const void*, const void*, const void*, const void*, float*, float*, void*, const float*, int,
                           int, float*, int, int, float, float, int, void*, hipStream_t);
+int ct_bn_fwd_train_pool_given(const void*, const void*, const void*, float*, float*, void*, void*, const float*, int, int,
+                               float*, int, int, int, int, int, int, float, float, hipStream_t);
 int ct_bn_fwd_train_pool(const void*, const void*, const void*, float*, float*, void*, void*, float*, float*, int, int,
                          int, int, int, int, float, float, hipStream_t);
 int ct_maxpool3s2_bwd(const void*, const void*, void*, int, int, int, int, int, int, hipStream_t);
@@ -620,6 +622,34 @@ std::vector<at::Tensor> bn_fwd_train_pool(at::Tensor x, at::Tensor gamma, at::Te
   return {y, arg, stat};
 }
 
+// bn_fwd_train_pool with the statistics from the conv epilogue's per-tile partials (part, rows
+// per tile: conv_fwd(..., partials=True)); returns (y_pool, argmax bytes, stat)
+std::vector<at::Tensor> bn_fwd_train_pool_given(at::Tensor x, at::Tensor gamma, at::Tensor beta,
+                                                at::Tensor run_mean, at::Tensor run_var, at::Tensor part,
+                                                int64_t rows_per_tile, double eps, double momentum) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "bn_fwd_train_pool_given: 4-D NHWC input");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const long M = (long)N * H * W;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "bn_fwd_train_pool_given: C % 8 == 0, C <= 2048");
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && run_mean.numel() == C && run_var.numel() == C);
+  CHECK_F32(run_mean); CHECK_F32(run_var); CHECK_IN(part); CHECK_F32(part);
+  TORCH_CHECK(rows_per_tile > 0, "bn_fwd_train_pool_given: rows per tile");
+  const long tiles = (M + rows_per_tile - 1) / rows_per_tile;
+  TORCH_CHECK(part.numel() >= 2 * (tiles + (tiles > 128 ? (tiles + 63) / 64 : 0)) * C,
+              "bn_fwd_train_pool_given: part buffer");
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto arg = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  auto stat = at::empty({4 * (long)C}, x.options().dtype(at::kFloat));
+  int rc = ct_bn_fwd_train_pool_given(x.data_ptr(), gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr<float>(),
+                                      run_var.data_ptr<float>(), y.data_ptr(), arg.data_ptr(), part.data_ptr<float>(),
+                                      (int)tiles, (int)rows_per_tile, stat.data_ptr<float>(), N, H, W, C, OH, OW,
+                                      (float)eps, (float)momentum, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_fwd_train_pool_given: unsupported shape");
+  return {y, arg, stat};
+}
+
 // gradient of maxpool3x3/s2/p1 from the byte argmax: dx [N, C, H, W] channels_last
 at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W) {
   at::Tensor dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -797,6 +827,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("rows_per_tile"), pybind11::arg("eps"), pybind11::arg("momentum"), pybind11::arg("relu"),
         pybind11::arg("mask_out") = pybind11::none());
   m.def("bn_fwd_train_pool", &bn_fwd_train_pool);
+  m.def("bn_fwd_train_pool_given", &bn_fwd_train_pool_given);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_bwd_given", &bn_bwd_given);

@@ -401,7 +401,12 @@ class _BNReLUPoolFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, run_mean, run_var, momentum, eps):
-        y, arg, stat = _C().bn_fwd_train_pool(x, gamma, beta, run_mean, run_var, eps, momentum)
+        given = getattr(x, "_ct_bn_part", None)           # the stem conv's epilogue statistics
+        if given is not None:
+            y, arg, stat = _C().bn_fwd_train_pool_given(x, gamma, beta, run_mean, run_var, given[0], given[1],
+                                                        eps, momentum)
+        else:
+            y, arg, stat = _C().bn_fwd_train_pool(x, gamma, beta, run_mean, run_var, eps, momentum)
         ctx.save_for_backward(x, gamma, stat, arg)
         ctx.params = (gamma, beta)
         return y

@@ -310,6 +310,35 @@ def test_stem_kernels_match_fp32_reference(cuda):
     assert _rel(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("HW", [40, 112])
+def test_stem_epilogue_stats_feed_bn_relu_pool(cuda, HW):
+    """The stem conv's epilogue BatchNorm partials (EPI 1) -> BN + ReLU + max-pool without a
+    statistics pass (bn_fwd_train_pool_given): the same pooled output, argmax and running
+    statistics as the statistics-pass kernel, and batch statistics equal to the fp32 ones of the
+    bf16 conv output."""
+    from cloudtik_amd import ops
+    torch.manual_seed(HW)
+    x = torch.randn(2, 3, HW, HW, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = _nhwc((torch.randn(64, 3, 7, 7, device=cuda) * 0.1).to(torch.bfloat16))
+    x8 = CV.to_nhwc8(x)
+    y = CV.stem_fwd(x8, w, (2, 2), (3, 3), partials=True)
+    part, rows = y._ct_bn_part
+    g = (torch.rand(64, device=cuda) + 0.5).to(torch.bfloat16)
+    b = (torch.randn(64, device=cuda) * 0.1).to(torch.bfloat16)
+    rm1, rv1 = torch.zeros(64, device=cuda), torch.ones(64, device=cuda)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    C = ops.require_native()
+    yp1, arg1, st1 = C.bn_fwd_train_pool(y, g, b, rm1, rv1, 1e-5, 0.1)
+    yp2, arg2, st2 = C.bn_fwd_train_pool_given(y, g, b, rm2, rv2, part, rows, 1e-5, 0.1)
+    yf = y.float()
+    torch.testing.assert_close(st2[:64], yf.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rm2, rm1, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv2, rv1, rtol=1e-3, atol=1e-5)
+    assert (yp2.float() - yp1.float()).abs().max().item() <= 0.02 * yp1.float().abs().max().item()
+    assert (arg2 == arg1).float().mean().item() > 0.99
+
+
 def test_dgrad_weight_cache_matches_direct_transposes():
     """_DgradWeights: per-phase [Ci, taps*Co] matrices of channels_last weights living in one
     flat storage, built per key on first sight and by one batched gather from the next
