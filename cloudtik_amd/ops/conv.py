@@ -615,29 +615,53 @@ def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
 
 
 _STEM_NHWC8_KERNEL = os.environ.get("CLOUDTIK_AMD_STEM_NHWC8_KERNEL", "1") == "1"
+# pair-chunk stem mode (conv.hip pixchunk 2): the image padded to 4 channels, a 64-column K-step =
+# 2 filter rows x 8 pixels x 4 channels, so a 7x7 RGB stem takes 4 K-steps (57 % useful
+# columns) instead of 7 (33 %).  Needs stride 2 along x, an even image width and an odd x padding
+# (the 8-pixel window starts at x * 2 - pad - 1: even, 16-byte aligned)
+_STEM_PAIRS = os.environ.get("CLOUDTIK_AMD_STEM_PAIRS", "1") == "1"
 
 
-def to_nhwc8(x: torch.Tensor) -> torch.Tensor:
-    """[N, C<=8, H, W] -> NHWC with the channels zero-padded to 8 (16 bytes per pixel), returned
-    as the logical [N, 8, H, W] channels_last view the kernels take."""
+def stem_pairs(x_shape, w_shape, stride, padding) -> bool:
+    """Whether the stem conv takes the pair-chunk mode."""
+    co, c, R, S = w_shape
+    return (_STEM_PAIRS and c <= 4 and stride[1] == 2 and x_shape[3] % 2 == 0 and padding[1] % 2 == 1
+            and S + 1 <= 8 and padding[1] + 1 <= 8)
+
+
+def to_nhwc8(x: torch.Tensor, cp: int = 8) -> torch.Tensor:
+    """[N, C<=cp, H, W] -> NHWC with the channels zero-padded to cp (8: 16 bytes per pixel; 4: the
+    pair-chunk stem mode), returned as the logical [N, cp, H, W] channels_last view the kernels
+    take."""
     n, c, h, w = x.shape
     # the kernel is not differentiable: an input that needs a gradient takes the autograd path
     if (x.is_cuda and x.dtype == torch.bfloat16 and _STEM_NHWC8_KERNEL
             and not (x.requires_grad and torch.is_grad_enabled())):
-        return _C().to_nhwc8(x)                     # one pass (conv.hip to_nhwc8_kernel)
-    return F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous().permute(0, 3, 1, 2)
+        return _C().to_nhwc8(x, cp)                 # one pass (conv.hip to_nhwc8_kernel)
+    return F.pad(x.permute(0, 2, 3, 1), (0, cp - c)).contiguous().permute(0, 3, 1, 2)
 
 
-def _stem_taps(R, pad):
+def _stem_taps(R, pad, pairs=False):
     taps = []
+    if pairs:
+        for r in range(0, R, 2):               # kernel rows r, r + 1; pixels x*2 - pad - 1 .. + 7
+            taps += [r - pad[0], -pad[1] - 1]
+        return taps
     for r in range(R):
         taps += [r - pad[0], -pad[1]]          # the K-step's 8 pixels start at x*s - pad
     return taps
 
 
-def stem_weight(w: torch.Tensor) -> torch.Tensor:
-    """[Co, C, R, S] -> [Co, R * 64]: column r*64 + s*8 + c = w[co, c, r, s] (zero-padded)."""
+def stem_weight(w: torch.Tensor, pairs=False) -> torch.Tensor:
+    """[Co, C, R, S] -> [Co, R * 64]: column r*64 + s*8 + c = w[co, c, r, s] (zero-padded); pair
+    mode [Co, ceil(R / 2) * 64]: column = r*32 + (s + 1)*4 + c (the window's first pixel and the
+    channels past C are zero)."""
     co, c, R, S = w.shape
+    if pairs:
+        T = (R + 1) // 2
+        wp = torch.zeros(co, 2 * T, 8, 4, device=w.device, dtype=w.dtype)
+        wp[:, :R, 1:S + 1, :c] = w.permute(0, 2, 3, 1)
+        return wp.reshape(co, T * 64)
     wp = torch.zeros(co, R, 8, 8, device=w.device, dtype=w.dtype)
     wp[:, :, :S, :c] = w.permute(0, 2, 3, 1)
     return wp.reshape(co, R * 64)
@@ -649,20 +673,22 @@ _STEM_STATS = os.environ.get("CLOUDTIK_AMD_STEM_STATS", "1") == "1"
 
 
 def stem_fwd(x8: torch.Tensor, w: torch.Tensor, stride, padding, partials: bool = False) -> torch.Tensor:
-    """The stem conv; with ``partials`` the output carries its BatchNorm tile statistics as
-    ``_ct_bn_part`` (ops.batch_norm_relu_maxpool consumes them)."""
-    n, _, H, W = x8.shape
+    """The stem conv of an NHWC8 (or, pair mode, NHWC4) image batch; with ``partials`` the output
+    carries its BatchNorm tile statistics as ``_ct_bn_part`` (ops.batch_norm_relu_maxpool consumes
+    them)."""
+    n, cp, H, W = x8.shape
     co, c, R, S = w.shape
+    pairs = cp == 4
     Ho, Wo = out_size(H, R, stride[0], padding[0]), out_size(W, S, stride[1], padding[1])
     out = torch.empty((n, co, Ho, Wo), device=x8.device, dtype=x8.dtype, memory_format=torch.channels_last)
     geo = [Ho, Wo, stride[0], stride[1], Ho, Wo, 1, 1, 0, 0, co, n * Ho * Wo]
     C = _C()
     part = bm = None
     if partials:
-        bm = C.conv_igemm_part_rows(_CFG, co, geo[11], R)
+        bm = C.conv_igemm_part_rows(_CFG, co, geo[11], len(_stem_taps(R, padding, pairs)) // 2)
         tiles = (geo[11] + bm - 1) // bm
         part = torch.empty((tiles + (tiles + 63) // 64) * 2 * co, device=x8.device, dtype=torch.float32)
-    if not C.conv_igemm(x8, stem_weight(w), out, geo, _stem_taps(R, padding), False, part, _CFG):
+    if not C.conv_igemm(x8, stem_weight(w, pairs), out, geo, _stem_taps(R, padding, pairs), False, part, _CFG):
         raise RuntimeError(f"conv_igemm (stem) rejected x{tuple(x8.shape)} w{tuple(w.shape)}")
     if partials:
         out._ct_bn_part = (part, bm)
@@ -671,20 +697,26 @@ def stem_fwd(x8: torch.Tensor, w: torch.Tensor, stride, padding, partials: bool 
 
 def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding) -> torch.Tensor:
     co, c, R, S = w_shape
-    nn = R * 64
+    pairs = x8.shape[1] == 4
+    T = (R + 1) // 2 if pairs else R
+    nn = T * 64
     M = dy.shape[0] * dy.shape[2] * dy.shape[3]
     C = _C()
     cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
     splits, rows = wgrad_plan(M, co, nn, cfg)
     part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)
-    if not C.conv_wgrad(dy, x8, part, _stem_taps(R, padding), [stride[0], stride[1], rows], splits, cfg):
+    if not C.conv_wgrad(dy, x8, part, _stem_taps(R, padding, pairs), [stride[0], stride[1], rows], splits, cfg):
         raise RuntimeError(f"conv_wgrad (stem) rejected dy{tuple(dy.shape)} x{tuple(x8.shape)}")
     full = torch.empty(co * nn, device=dy.device, dtype=dy.dtype)
     if splits <= 16:
         C.splitk_reduce(part.view(splits, -1), full, False)
     else:
         C.splitk_reduce_wide(part, splits, full, False)
-    return full.view(co, R, 8, 8)[:, :, :S, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+    if pairs:
+        full = full.view(co, 2 * T, 8, 4)[:, :R, 1:S + 1, :c]
+    else:
+        full = full.view(co, R, 8, 8)[:, :, :S, :c]
+    return full.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
 
 
 class StemFn(torch.autograd.Function):
@@ -721,4 +753,5 @@ def stem_conv(x: torch.Tensor, conv: torch.nn.Conv2d) -> torch.Tensor:
         ROUTES["library"] += 1
         return conv(x)
     ROUTES["igemm"] += 1
-    return StemFn.apply(to_nhwc8(x), conv.weight, tuple(conv.stride), tuple(conv.padding))
+    cp = 4 if stem_pairs(x.shape, conv.weight.shape, tuple(conv.stride), tuple(conv.padding)) else 8
+    return StemFn.apply(to_nhwc8(x, cp), conv.weight, tuple(conv.stride), tuple(conv.padding))

@@ -19,7 +19,7 @@ void ct_conv_stream_set_cus(int);
 void ct_conv_batch_begin();
 int ct_conv_batch_end(hipStream_t);
 int ct_dgrad_wgather(const void*, void*, const int*, int, hipStream_t);
-int ct_to_nhwc8(const void*, void*, int, int, int, int, long, long, long, long, hipStream_t);
+int ct_to_nhwc8(const void*, void*, int, int, int, int, long, long, long, long, int, hipStream_t);
 int ct_bn_partials_finalize(const float*, int, int, int, int, float*, float*, hipStream_t);
 int ct_conv_wgrad(const void*, const void*, int, int, int, int, int, int, int, int, int, int, const int*, float*, int,
                   int, int, hipStream_t);
@@ -41,7 +41,7 @@ bool conv_igemm(at::Tensor X, at::Tensor W, at::Tensor Y, std::vector<int64_t> g
   TORCH_CHECK(geo.size() == 12 && taps.size() % 2 == 0, "conv_igemm: plan");
   const int Ci = (int)X.size(1), Hi = (int)X.size(2), Wi = (int)X.size(3);
   const int T = (int)taps.size() / 2, Co = (int)W.size(0);
-  const int cw = Ci == 8 ? 64 : Ci;           // stem (pixel-chunk) mode: 64 weight columns per tap
+  const int cw = (Ci == 8 || Ci == 4) ? 64 : Ci;   // stem (pixel-chunk) modes: 64 weight columns per tap
   TORCH_CHECK(W.size(1) == (int64_t)T * cw, "conv_igemm: W columns != taps * Ci");
   const long M = geo[11];
   // every output address the plan produces must lie inside Y (checked on the host before launch)
@@ -150,7 +150,7 @@ bool conv_wgrad(at::Tensor DY, at::Tensor X, at::Tensor P, std::vector<int64_t> 
   TORCH_CHECK(geo.size() == 3 && taps.size() % 2 == 0 && DY.size(0) == X.size(0), "conv_wgrad: plan");
   const int T = (int)taps.size() / 2, Ci = (int)X.size(1), Co = (int)DY.size(1);
   const long M = DY.size(0) * DY.size(2) * DY.size(3);
-  TORCH_CHECK(P.numel() >= splits * (long)Co * T * (Ci == 8 ? 64 : Ci), "conv_wgrad: partial buffer");
+  TORCH_CHECK(P.numel() >= splits * (long)Co * T * ((Ci == 8 || Ci == 4) ? 64 : Ci), "conv_wgrad: partial buffer");
   std::vector<int> tp(taps.begin(), taps.end());
   const int rc = ct_conv_wgrad(DY.data_ptr(), X.data_ptr(), (int)X.size(2), (int)X.size(3), Ci, (int)DY.size(2),
                                (int)DY.size(3), (int)geo[0], (int)geo[1], Co, (int)M, T, tp.data(),
@@ -179,17 +179,19 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad_cfg", &conv_wgrad_cfg, "wgrad tile configuration for (Co, T*Ci)");
   m.def("conv_igemm", &conv_igemm, "implicit-GEMM NHWC convolution (MFMA), optional BatchNorm tile statistics");
   m.def("conv_igemm_bn", &conv_igemm_bn, "conv data gradient + the BatchNorm+ReLU backward reduction in its epilogue");
-  m.def("to_nhwc8", [](at::Tensor x) {
-          TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) <= 8,
-                      "to_nhwc8: [N, C <= 8, H, W] bf16 CUDA tensor");
+  m.def("to_nhwc8", [](at::Tensor x, int64_t cp) {
+          TORCH_CHECK(cp == 8 || cp == 4, "to_nhwc8: 8 or 4 output channels");
+          TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) <= cp,
+                      "to_nhwc8: [N, C <= cp, H, W] bf16 CUDA tensor");
           const long N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-          auto y = at::empty({N, 8, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+          auto y = at::empty({N, cp, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
           TORCH_CHECK(ct_to_nhwc8(x.data_ptr(), y.data_ptr(), (int)N, (int)C, (int)H, (int)W, x.stride(0), x.stride(1),
-                                  x.stride(2), x.stride(3), at::hip::getCurrentHIPStream().stream()) == 0,
+                                  x.stride(2), x.stride(3), (int)cp, at::hip::getCurrentHIPStream().stream()) == 0,
                       "to_nhwc8 launch");
           return y;
         },
-        "[N, C<=8, H, W] bf16 -> channels_last [N, 8, H, W] zero-padded, one pass");
+        pybind11::arg("x"), pybind11::arg("cp") = 8,
+        "[N, C<=cp, H, W] bf16 -> channels_last [N, cp, H, W] zero-padded (cp = 8 or 4), one pass");
   m.def("dgrad_wgather", [](at::Tensor src, at::Tensor dst, at::Tensor desc) {
           TORCH_CHECK(src.is_cuda() && dst.is_cuda() && desc.is_cuda(), "dgrad_wgather: CUDA tensors");
           TORCH_CHECK(src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kBFloat16, "dgrad_wgather: bf16");

@@ -55,7 +55,9 @@ struct ConvArgs {
                          //   of the three odd-parity pixels of each written one (no zero-fill pass)
   unsigned long long tdy, tdx;           // 16 taps x 4 bits, biased by 8
   int cpt;              // K-steps (of 64 weight columns) per tap: Ci / 64, or 1 in pixel-chunk mode
-  int pixchunk;         // stem mode: Ci = 8, the 8 chunks of a K-step are 8 consecutive pixels
+  int pixchunk;         // stem modes: 1 = Ci 8, the 8 chunks of a K-step are 8 consecutive pixels;
+                        //   2 = Ci 4, chunk g = pixels (2 (g & 3), + 1) of kernel row (g >> 2): two
+                        //   filter rows x 8 pixels per K-step (a 7x7 RGB stem: 4 K-steps, not 7)
   // EPI 2 (data gradient feeding a BatchNorm + ReLU backward, mask recomputed from x):
   const bf16_t* bnx;    // the BatchNorm's input, at the same addresses as Y
   const bf16_t* bny;    // its output (ReLU mask source when it had a residual add), or null:
@@ -114,6 +116,20 @@ __device__ __forceinline__ cv_s16x8 cv_frag(const char* img, int r0, int ks, int
   const int row = r0 + (lane & 15);
   const int kc = ks * 4 + (lane >> 4);
   return *(const cv_lds_s16x8*)(img + row * 128 + ((kc ^ cv_swz(row)) << 4));
+}
+
+// a K-step chunk's element offset from its row's pixel and its pixel / row step (stem modes)
+template <class Args>
+__device__ __forceinline__ void cv_chunk_geo(const Args& a, int gc, unsigned& gca, int& gpx, int& gpy) {
+  if (a.pixchunk == 2) {
+    gpx = 2 * (gc & 3);
+    gpy = gc >> 2;
+    gca = (unsigned)((gpy * a.Wi + gpx) * 4);
+  } else {
+    gpx = a.pixchunk ? gc : 0;                     // stem: the chunk is a pixel step along x
+    gpy = 0;
+    gca = (unsigned)gc * 8u;                       // element offset of the chunk
+  }
 }
 
 __device__ __forceinline__ void cv_bar() {
@@ -290,15 +306,14 @@ __device__ __forceinline__ void conv_igemm_tile(const ConvArgs& a, const int L) 
   const int HW = a.Hr * a.Wr;
 
   // ---- per-lane gather descriptors: the A rows this lane stages (fixed for the whole K loop)
-  int pix[IA], iy0[IA], ix0[IA], gpx[IA];
+  int pix[IA], iy0[IA], ix0[IA], gpx[IA], gpy[IA];
   unsigned gca[IA];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
     const int row = (wave * IA + j) * 8 + (lane >> 3);
     const int m = m0 + row;
     const int gc = (lane & 7) ^ cv_swz(row);
-    gca[j] = (unsigned)gc * 8u;                    // element offset of the chunk
-    gpx[j] = a.pixchunk ? gc : 0;                  // stem: the chunk is a pixel step along x
+    cv_chunk_geo(a, gc, gca[j], gpx[j], gpy[j]);
     if (m < a.M) {
       int b, rem, y, x;
       cv_divmod(m, HW, 1.f / (float)HW, b, rem);
@@ -335,7 +350,7 @@ __device__ __forceinline__ void conv_igemm_tile(const ConvArgs& a, const int L) 
     char* Bs = As + BM * 128;
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
-      const int iy = iy0[j] + dy, ix = ix0[j] + dx + gpx[j];
+      const int iy = iy0[j] + dy + gpy[j], ix = ix0[j] + dx + gpx[j];
       const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
       const void* src = ok ? (const void*)(a.X + (long)(pix[j] + toff) + gca[j]) : (const void*)cv_zero_page;
       cv_glds16(src, As + (wave * IA + j) * 1024);
@@ -528,14 +543,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
   const int cpt = a.cpt;
 
   // tile-invariant parts of the gather: the lane's rows inside the tile and their swizzled chunk
-  int gpx[IA];
+  int gpx[IA], gpy[IA];
   unsigned gca[IA];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
     const int row = (wave * IA + j) * 8 + (lane >> 3);
     const int gc = (lane & 7) ^ cv_swz(row);
-    gca[j] = (unsigned)gc * 8u;
-    gpx[j] = a.pixchunk ? gc : 0;
+    cv_chunk_geo(a, gc, gca[j], gpx[j], gpy[j]);
   }
   unsigned woff[2];
 #pragma unroll
@@ -578,7 +592,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
     char* Bs = As + BM * 128;
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
-      const int iy = iy0[j] + dy, ix = ix0[j] + dx + gpx[j];
+      const int iy = iy0[j] + dy + gpy[j], ix = ix0[j] + dx + gpx[j];
       const bool ok = (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
       const void* src = ok ? (const void*)(a.X + (long)(pix[j] + toff) + gca[j]) : (const void*)cv_zero_page;
       cv_glds16(src, As + (wave * IA + j) * 1024);
@@ -757,7 +771,8 @@ struct WgradArgs {
   int Co, NN, M, T, rows_per_split;
   unsigned long long tdy, tdx;
   int Cw;               // weight columns per tap (= Ci, or 64 in pixel-chunk mode)
-  int pixchunk;         // stem: column c of a tap = pixel step c / 8, channel c % 8 (Ci = 8)
+  int pixchunk;         // stem: 1 = column c of a tap is pixel step c / 8, channel c % 8 (Ci = 8);
+                        //   2 = chunk g = c / 8 is pixels 2 (g & 3), + 1 of kernel row g >> 2 (Ci = 4)
 };
 
 template <int LPR>
@@ -823,7 +838,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
   }
   // B rows (gathered X): per instruction the lane's chunk column -> tap, channel; the pixel
   // (b, y, x) of its row is tracked incrementally
-  int rb[GB], bb[GB], yb[GB], xb[GB], dyb[GB], dxb[GB], cib[GB], pxb[GB];
+  int rb[GB], bb[GB], yb[GB], xb[GB], dyb[GB], dxb[GB], cib[GB], pxb[GB], pyb[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int r = (wave * GB + j) * RPB + lane / LPB;
@@ -832,7 +847,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
     const int t = n / a.Cw;
     const int c = n - t * a.Cw;
     cib[j] = a.pixchunk ? (c & 7) : c;
-    pxb[j] = a.pixchunk ? (c >> 3) : 0;
+    pxb[j] = a.pixchunk == 2 ? 2 * ((c >> 3) & 3) : (a.pixchunk ? (c >> 3) : 0);
+    pyb[j] = a.pixchunk == 2 ? (c >> 5) : 0;
     dyb[j] = (int)((a.tdy >> (4 * t)) & 15) - 8;
     dxb[j] = (int)((a.tdx >> (4 * t)) & 15) - 8;
     const int m = kbeg + r, HW = a.Hr * a.Wr;
@@ -880,7 +896,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, 1) conv_wgrad_kernel(WgradArgs
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const int m = kb + rb[j];
-      const int iy = yb[j] * a.sy + dyb[j], ix = xb[j] * a.sx + dxb[j] + pxb[j];
+      const int iy = yb[j] * a.sy + dyb[j] + pyb[j], ix = xb[j] * a.sx + dxb[j] + pxb[j];
       const bool ok = m < kend && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
       const void* src = ok ? (const void*)(a.X + ((long)(bb[j] * a.Hi + iy) * a.Wi + ix) * a.Ci + cib[j])
                            : (const void*)cv_zero_page;
@@ -1232,14 +1248,17 @@ static int conv_igemm_impl(const void* X, int Hi, int Wi, int Ci, const void* W,
                            const int* taps, int accumulate, float* part, int cfg, const ConvBnBwd* bn,
                            hipStream_t stream) {
   // (M < 2^24: the epilogue's float-reciprocal row division, cv_divmod)
-  if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || M >= (1 << 24) || T <= 0 || T > CV_MAXT)
+  if (Ci <= 0 || (Ci % 64 && Ci != 8 && Ci != 4) || Co <= 0 || Co % 64 || M <= 0 || M >= (1 << 24) || T <= 0 ||
+      T > CV_MAXT)
     return 1;
+  // pair mode: every 16-byte chunk starts at an even pixel of an even-width row
+  if (Ci == 4 && (Wi % 2 || sx % 2)) return 1;
   if (((uintptr_t)X & 15) || ((uintptr_t)W & 15) || ((uintptr_t)Y & 7) || ldy % 4) return 3;
   // zero-filling mode: exactly the (even, even) phase of a stride-2 output grid, 16-B rows
   if (accumulate == 2 && (Ho != 2 * Hr || Wo != 2 * Wr || oys != 2 || oxs != 2 || oy0 || ox0 || bn ||
                           ((uintptr_t)Y & 15) || ldy % 8))
     return 9;
-  const int pixchunk = Ci == 8;            // the stem: NHWC8 input, 8 pixels per K-step
+  const int pixchunk = Ci == 8 ? 1 : (Ci == 4 ? 2 : 0);   // the stem: NHWC8 / NHWC4 input
   ConvArgs a{(const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, part, Hi, Wi, Ci, Hr, Wr, sy, sx,
              Ho, Wo, oys, oxs, oy0, ox0, ldy, Co, M, T, accumulate, 0ull, 0ull, pixchunk ? 1 : Ci / 64, pixchunk,
              nullptr, nullptr, nullptr, nullptr, 0, 0};
@@ -1361,26 +1380,32 @@ extern "C" int ct_dgrad_wgather(const void* src, void* dst, const int* desc, int
 // zero-padded to 8 (16 bytes per pixel), in one pass: one thread per pixel reads its C values
 // (pixel-contiguous across the wave for NCHW) and writes one 16-B chunk (the pad-then-copy form
 // wrote the 205 MB ResNet-50 batch twice)
+template <int CP>
 __global__ __launch_bounds__(256) void to_nhwc8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long npix,
                                                        int C, int H, int W, long sn, long sc, long sh, long sw) {
+  typedef __attribute__((ext_vector_type(CP))) unsigned short vec_t;
   const long p = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (p >= npix) return;
   const long hw = (long)H * W;
   const long n = p / hw, r = p - n * hw;
   const int h = (int)(r / W), w = (int)(r - (long)h * W);
   const bf16_t* src = x + n * sn + h * sh + w * sw;
-  u16x8 v = u16x8(0);
+  vec_t v = vec_t(0);
   for (int c = 0; c < C; ++c) v[c] = reinterpret_cast<const unsigned short*>(src)[c * sc];
-  reinterpret_cast<u16x8*>(y)[p] = v;
+  reinterpret_cast<vec_t*>(y)[p] = v;
 }
 
+// CP = 8 (16 bytes per pixel) or 4 (8 bytes: the pair-chunk stem mode, C <= 4)
 extern "C" int ct_to_nhwc8(const void* x, void* y, int N, int C, int H, int W, long sn, long sc, long sh, long sw,
-                           hipStream_t stream) {
-  if (C < 1 || C > 8) return 1;
+                           int CP, hipStream_t stream) {
+  if (C < 1 || C > CP || (CP != 8 && CP != 4)) return 1;
   const long npix = (long)N * H * W;
   if (npix <= 0) return 0;
-  to_nhwc8_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, npix, C, H, W,
-                                                                      sn, sc, sh, sw);
+  const unsigned grid = (unsigned)((npix + 255) / 256);
+  if (CP == 8)
+    to_nhwc8_kernel<8><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, npix, C, H, W, sn, sc, sh, sw);
+  else
+    to_nhwc8_kernel<4><<<grid, 256, 0, stream>>>((const bf16_t*)x, (bf16_t*)y, npix, C, H, W, sn, sc, sh, sw);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
 
@@ -1518,11 +1543,13 @@ extern "C" int ct_splitk_reduce_wide(const float* P, int S, long n, void* out, i
 extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int Ci, int Hr, int Wr, int sy, int sx,
                              int Co, int M, int T, const int* taps, float* P, int splits, int rows_per_split, int cfg,
                              hipStream_t stream) {
-  if (Ci <= 0 || (Ci % 64 && Ci != 8) || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT || splits < 1)
+  if (Ci <= 0 || (Ci % 64 && Ci != 8 && Ci != 4) || Co <= 0 || Co % 64 || M <= 0 || T <= 0 || T > CV_MAXT ||
+      splits < 1)
     return 1;
+  if (Ci == 4 && (Wi % 2 || sx % 2)) return 1;
   if (rows_per_split % 32 || (long)rows_per_split * splits < M) return 2;
   if (((uintptr_t)DY & 15) || ((uintptr_t)X & 15) || ((uintptr_t)P & 15)) return 3;
-  const int pixchunk = Ci == 8, Cw = pixchunk ? 64 : Ci;
+  const int pixchunk = Ci == 8 ? 1 : (Ci == 4 ? 2 : 0), Cw = pixchunk ? 64 : Ci;
   WgradArgs a{(const bf16_t*)DY, (const bf16_t*)X, P, Hi, Wi, Ci, Hr, Wr, sy, sx, Co, T * Cw, M, T, rows_per_split,
               0ull, 0ull, Cw, pixchunk};
   for (int t = 0; t < T; ++t) {

@@ -290,8 +290,43 @@ def test_stem_pixel_chunk_plan_matches_conv2d():
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
 
 
+def test_stem_pair_chunk_plan_matches_conv2d():
+    """Pair mode: NHWC4 input, one K-step per two filter rows; chunk g = pixels 2 (g & 3), + 1 of
+    row g >> 2 (the kernel's cv_chunk_geo), the 8-pixel window starting at x * 2 - pad - 1."""
+    torch.manual_seed(4)
+    N, H, co = 2, 12, 64
+    x = torch.randn(N, 3, H, H)
+    w = torch.randn(co, 3, 7, 7)
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    assert CV.stem_pairs(x.shape, w.shape, (2, 2), (3, 3))
+    x4 = CV.to_nhwc8(x, 4)
+    assert x4.shape == (N, 4, H, H) and x4.is_contiguous(memory_format=torch.channels_last)
+    Wm = CV.stem_weight(w, pairs=True)                          # [co, 4 * 64]
+    taps = CV._stem_taps(7, (3, 3), pairs=True)
+    assert len(taps) == 8 and Wm.shape == (co, 256)
+    Ho = CV.out_size(H, 7, 2, 3)
+    xs = x4.permute(0, 2, 3, 1)
+    b = torch.arange(N).view(-1, 1, 1).expand(N, Ho, Ho).reshape(-1)
+    y = torch.arange(Ho).view(1, -1, 1).expand(N, Ho, Ho).reshape(-1)
+    xx = torch.arange(Ho).view(1, 1, -1).expand(N, Ho, Ho).reshape(-1)
+    cols = []
+    for t in range(4):
+        for g in range(8):
+            for pp in range(2):                                # the chunk's two pixels
+                iy = 2 * y + taps[2 * t] + (g >> 2)
+                ix = 2 * xx + taps[2 * t + 1] + 2 * (g & 3) + pp
+                ok = (iy >= 0) & (iy < H) & (ix >= 0) & (ix < H)
+                v = torch.zeros(b.numel(), 4)
+                v[ok] = xs[b[ok], iy[ok], ix[ok]]
+                cols.append(v)
+    out = (torch.cat(cols, 1) @ Wm.t()).view(N, Ho, Ho, co).permute(0, 3, 1, 2)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.gpu
-def test_stem_kernels_match_fp32_reference(cuda):
+@pytest.mark.parametrize("cp", [8, 4])
+def test_stem_kernels_match_fp32_reference(cuda, monkeypatch, cp):
+    monkeypatch.setattr(CV, "_STEM_PAIRS", cp == 4)
     torch.manual_seed(5)
     x = torch.randn(4, 3, 40, 40, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = _nhwc((torch.randn(64, 3, 7, 7, device=cuda) * 0.1).to(torch.bfloat16))
@@ -305,14 +340,16 @@ def test_stem_kernels_match_fp32_reference(cuda):
     assert CV.stem_eligible(x, conv)
     y = CV.stem_conv(x, conv)
     assert _rel(y, ref) < 1e-2
-    x8 = CV.to_nhwc8(x)
+    x8 = CV.to_nhwc8(x, cp)
+    y2 = CV.stem_fwd(x8, w, (2, 2), (3, 3))
+    assert _rel(y2, ref) < 1e-2
     dw = CV.stem_wgrad(dy, x8, w.shape, (2, 2), (3, 3))
     assert _rel(dw, wr.grad) < 1e-2
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("HW", [40, 112])
-def test_stem_epilogue_stats_feed_bn_relu_pool(cuda, HW):
+@pytest.mark.parametrize("HW,cp", [(40, 8), (112, 8), (112, 4)])
+def test_stem_epilogue_stats_feed_bn_relu_pool(cuda, HW, cp):
     """The stem conv's epilogue BatchNorm partials (EPI 1) -> BN + ReLU + max-pool without a
     statistics pass (bn_fwd_train_pool_given): the same pooled output, argmax and running
     statistics as the statistics-pass kernel, and batch statistics equal to the fp32 ones of the
@@ -321,7 +358,7 @@ def test_stem_epilogue_stats_feed_bn_relu_pool(cuda, HW):
     torch.manual_seed(HW)
     x = torch.randn(2, 3, HW, HW, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = _nhwc((torch.randn(64, 3, 7, 7, device=cuda) * 0.1).to(torch.bfloat16))
-    x8 = CV.to_nhwc8(x)
+    x8 = CV.to_nhwc8(x, cp)
     y = CV.stem_fwd(x8, w, (2, 2), (3, 3), partials=True)
     part, rows = y._ct_bn_part
     g = (torch.rand(64, device=cuda) + 0.5).to(torch.bfloat16)
@@ -667,14 +704,15 @@ def test_downsample_bn_pair_in_one_apply(cuda, monkeypatch, follow):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cl", [False, True])
-def test_to_nhwc8_kernel(cuda, cl):
-    """conv.hip to_nhwc8_kernel: [N, 3, H, W] (NCHW or channels_last) -> zero-padded NHWC8 in one
-    pass equals the pad-then-copy form."""
+@pytest.mark.parametrize("cp", [8, 4])
+def test_to_nhwc8_kernel(cuda, cl, cp):
+    """conv.hip to_nhwc8_kernel: [N, 3, H, W] (NCHW or channels_last) -> zero-padded NHWC8 / NHWC4
+    in one pass equals the pad-then-copy form."""
     x = torch.randn(3, 3, 17, 23, device=cuda).to(torch.bfloat16)
     if cl:
         x = x.contiguous(memory_format=torch.channels_last)
-    got = CV.to_nhwc8(x)
-    ref = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 5)).contiguous().permute(0, 3, 1, 2)
+    got = CV.to_nhwc8(x, cp)
+    ref = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, cp - 3)).contiguous().permute(0, 3, 1, 2)
     assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(got, ref)
 
