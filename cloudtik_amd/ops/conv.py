@@ -416,16 +416,21 @@ WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split
 # workgroups the 64-wide 4-wave tiles run one wave per SIMD (l1.c2 299 us, 187 at 512)
 WGRAD_BLOCKS_SMALL = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS_SMALL", "256"))
 WGRAD3X3_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_BLOCKS", "128"))
+STEM_WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_STEM_WGRAD_BLOCKS", "256"))
 
 
-def wgrad_plan(M: int, co: int, nn: int, cfg: int):
-    """(splits, rows per split): about 2048 workgroups, each split a multiple of the stage depth
-    and at least 256 deep, the fp32 partials capped at PARTIAL_BYTES."""
+def wgrad_plan(M: int, co: int, nn: int, cfg: int, blocks: Optional[int] = None):
+    """(splits, rows per split): about ``blocks`` workgroups (default: the per-configuration
+    target), each split a multiple of the stage depth and at least 256 deep, the fp32 partials
+    capped at PARTIAL_BYTES."""
     bm, bn = _WG_TILES[cfg]
     tiles = (co // bm) * (nn // bn)
+    given = blocks
     blocks = WGRAD_BLOCKS if cfg in (3, 11) else WGRAD_BLOCKS_SMALL
     if cfg >= 12:                      # nine-tap kernel: cfg 13 runs two workgroups per CU
         blocks = WGRAD3X3_BLOCKS * (2 if cfg == 13 else 1)
+    if given is not None:
+        blocks = given
     splits = max(1, min(blocks // max(1, tiles), M // 256, PARTIAL_BYTES // (co * nn * 4)))
     q = 64 if cfg >= 4 and cfg != 9 else 32        # pixels per stage of the configuration
     rows = ((M + splits - 1) // splits + q - 1) // q * q
@@ -703,7 +708,9 @@ def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding) -> 
     M = dy.shape[0] * dy.shape[2] * dy.shape[3]
     C = _C()
     cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
-    splits, rows = wgrad_plan(M, co, nn, cfg)
+    # the stem's weight gradient is the last kernel of the backward, on the main stream with the
+    # chip to itself: split it over more workgroups than the side-stream gradients
+    splits, rows = wgrad_plan(M, co, nn, cfg, STEM_WGRAD_BLOCKS)
     part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)
     if not C.conv_wgrad(dy, x8, part, _stem_taps(R, padding, pairs), [stride[0], stride[1], rows], splits, cfg):
         raise RuntimeError(f"conv_wgrad (stem) rejected dy{tuple(dy.shape)} x{tuple(x8.shape)}")
