@@ -658,3 +658,32 @@ def test_sumsq_into_matches_torch(cuda, n):
     C.sumsq_into(x, out)
     ref = 2.0 + (x.float() ** 2).sum().item()
     assert abs(out.item() - ref) <= 1e-4 * ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,tiles", [(64, 700), (128, 300), (256, 400), (192, 1000), (512, 130)])
+def test_bn_bwd_given_many_tile_partials(cuda, C, tiles):
+    """bn_bwd_given from producer per-tile sums (the conv data-gradient epilogue's): above the
+    direct-finalize limit the first-level partials sum (batchnorm.hip bn_bwd_partials_sum_kernel,
+    several tile rows per block below 256 channels) runs first.  dgamma / dbeta = column sums of
+    the partials, dx = the closed form, against fp32."""
+    torch.manual_seed(C + tiles)
+    N, H = 2, 16
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dym = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    mean = torch.randn(C, device=cuda) * 0.1
+    invstd = torch.rand(C, device=cuda) + 0.5
+    stat = torch.cat([mean, invstd, torch.zeros(2 * C, device=cuda)])
+    gamma = (torch.rand(C, device=cuda) + 0.5).to(torch.bfloat16)
+    p1 = torch.randn(tiles, C, device=cuda)
+    p2 = torch.randn(tiles, C, device=cuda)
+    part = torch.cat([p1.reshape(-1), p2.reshape(-1)])
+    dx, dg, db = ops.require_native().bn_bwd_given(dym, x, gamma, stat, part, tiles, tiles, None, None)
+    sdy, sdx = p1.sum(0), p2.sum(0)
+    torch.testing.assert_close(db.float(), sdy, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(dg.float(), sdx, rtol=2e-2, atol=5e-2)
+    M = N * H * H
+    a = gamma.float() * invstd
+    v = lambda t: t.view(1, -1, 1, 1)  # noqa: E731
+    ref_dx = v(a) * dym.float() - v(a * sdx / M * invstd) * (x.float() - v(mean)) - v(a * sdy / M)
+    assert ((dx.float() - ref_dx).norm() / ref_dx.norm()).item() < 1e-2
