@@ -129,9 +129,27 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
   const int c = blockIdx.x * 64 + lane;
   const bool live = c < L.C;
   const float R = (float)L.rows_per_blk;
+  // up to 256 partials (the direct case and every merged one) the wave's 16 rows of both
+  // arrays are loaded in ONE round before pass 1, so pass 2 needs no second memory round trip
+  constexpr int KR = 16;
+  const bool inreg = nblk <= 16 * KR;
+  float mv[KR], m2v[KR];
   // pass 1: sum of n_b * mean_b (every block but the last has R rows)
   float s = 0.f;
-  if (live) {
+  if (live && inreg) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int b = w + 16 * k;
+      mv[k] = b < nblk ? pmean[(size_t)b * L.C + c] : 0.f;
+      m2v[k] = b < nblk ? pm2[(size_t)b * L.C + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int b = w + 16 * k;
+      const float nb = b >= nblk ? 0.f : (b == nblk - 1 ? (float)(L.M - b * L.rows_per_blk) : R);
+      s += nb * mv[k];
+    }
+  } else if (live) {
 #pragma unroll 8
     for (int b = w; b < nblk; b += 16) {
       const float nb = b == nblk - 1 ? (float)(L.M - b * L.rows_per_blk) : R;
@@ -149,7 +167,15 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
   const float mean = lmean[lane];
   // pass 2: M2 = sum(M2_b + n_b (mean_b - mean)^2)
   float q = 0.f;
-  if (live) {
+  if (live && inreg) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int b = w + 16 * k;
+      const float nb = b >= nblk ? 0.f : (b == nblk - 1 ? (float)(L.M - b * L.rows_per_blk) : R);
+      const float d = mv[k] - mean;
+      q += m2v[k] + nb * d * d;
+    }
+  } else if (live) {
 #pragma unroll 8
     for (int b = w; b < nblk; b += 16) {
       const float nb = b == nblk - 1 ? (float)(L.M - b * L.rows_per_blk) : R;
@@ -807,13 +833,24 @@ __global__ __launch_bounds__(256) void bn_partials_merge_kernel(const float* __r
   const int c = blockIdx.y * 64 + lane, g = blockIdx.x;
   const int t0 = g * BN_MERGE_GROUP, t1 = min(tiles, t0 + BN_MERGE_GROUP);
   const bool live = c < C;
+  // the thread's BN_MERGE_GROUP / 4 rows of both arrays in one round of loads, kept in registers
+  // for the second pass
+  constexpr int KR = BN_MERGE_GROUP / 4;
+  float mv[KR], m2v[KR];
   float n = 0.f, s = 0.f;
   if (live) {
-#pragma unroll 4
-    for (int t = t0 + w; t < t1; t += 4) {
-      const float nb = (float)max(0, min(rows_per_tile, M - t * rows_per_tile));
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int t = t0 + w + 4 * k;
+      mv[k] = t < t1 ? pmean[(size_t)t * C + c] : 0.f;
+      m2v[k] = t < t1 ? pm2[(size_t)t * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int t = t0 + w + 4 * k;
+      const float nb = t < t1 ? (float)max(0, min(rows_per_tile, M - t * rows_per_tile)) : 0.f;
       n += nb;
-      s += nb * pmean[(size_t)t * C + c];
+      s += nb * mv[k];
     }
   }
   sn[w][lane] = n;
@@ -823,11 +860,12 @@ __global__ __launch_bounds__(256) void bn_partials_merge_kernel(const float* __r
   const float mg = ng > 0.f ? (ss[0][lane] + ss[1][lane] + ss[2][lane] + ss[3][lane]) / ng : 0.f;
   float q = 0.f;
   if (live) {
-#pragma unroll 4
-    for (int t = t0 + w; t < t1; t += 4) {
-      const float nb = (float)max(0, min(rows_per_tile, M - t * rows_per_tile));
-      const float d = pmean[(size_t)t * C + c] - mg;
-      q += pm2[(size_t)t * C + c] + nb * d * d;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int t = t0 + w + 4 * k;
+      const float nb = t < t1 ? (float)max(0, min(rows_per_tile, M - t * rows_per_tile)) : 0.f;
+      const float d = mv[k] - mg;
+      q += m2v[k] + nb * d * d;
     }
   }
   __syncthreads();                                    // ss reuse
