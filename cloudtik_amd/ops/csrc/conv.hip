@@ -1534,6 +1534,16 @@ extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   // the 64-wide tiles serve the layer-1 shapes (802816-pixel reductions): 64-pixel stages win
   // there (l1.c2 301 -> 289 us, l1.c3 156 -> 142, l1.c1 128 -> 118; profiles/r4/conv_stream_probe.md)
   if (NN % 128 == 0) return 5;
+  // 128 x 64 tiles where the output channels allow (layer-1 64 -> 256 1x1 convs: X re-read for
+  // 2 co tiles instead of 4).  Alone SLOWER (l1.c3 108 -> 124 us) but the step is faster beside
+  // the data gradients: 20.84 / 20.83 / 20.83 + 20.79 / 20.90 / 20.84 / 20.84 -> 20.80 / 20.76 /
+  // 20.73 + 20.77 / 20.78 / 20.76 / 20.75 ms (profiles/r5/SUMMARY.md); CLOUDTIK_AMD_WGRAD_TALL=0
+  // restores the 64 x 64 tiles
+  static const bool tall = [] {
+    const char* e = std::getenv("CLOUDTIK_AMD_WGRAD_TALL");
+    return !e || std::atoi(e) != 0;
+  }();
+  if (tall && Co % 128 == 0) return 14;
   return 8;                        // 64 x 64, 64-pixel stages, 3-slot ring (l1.c3 145 -> 137 us)
 }
 
@@ -1582,9 +1592,13 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     else conv_wgrad3x3_kernel<2><<<(int)blocks, 256, 0, stream>>>(a);
     return hipGetLastError() == hipSuccess ? 0 : 7;
   }
-  const int tile = cfg == 11 ? 3 : (cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg)));
-  if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
-  if (cfg >= 4 && cfg != 9 && rows_per_split % 64) return 2;
+  if (cfg == 14) {                   // 128 co x 64 columns (4 waves 2x2, 64-pixel stages x 3)
+    if (Co % 128 || rows_per_split % 64) return 2;
+  } else {
+    const int tile = cfg == 11 ? 3 : (cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg)));
+    if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
+    if (cfg >= 4 && cfg != 9 && rows_per_split % 64) return 2;
+  }
   static const bool lin_on = [] {
     const char* e = std::getenv("CLOUDTIK_AMD_WGRAD_LIN");
     return !e || std::atoi(e) != 0;
@@ -1597,6 +1611,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
       case 5: return wg_launch<64, 128, 2, 2, 4, 64, true>(a, splits, stream);
       case 8: return wg_launch<64, 64, 2, 2, 3, 64, true>(a, splits, stream);
       case 9: return wg_launch<128, 128, 2, 4, 4, 32, true>(a, splits, stream);
+      case 14: return wg_launch<128, 64, 2, 2, 3, 64, true>(a, splits, stream);
       default: break;
     }
   }
@@ -1613,6 +1628,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     case 9: return wg_launch<128, 128, 2, 4, 4>(a, splits, stream);
     case 10: return wg_launch<128, 128, 2, 4, 2, 64>(a, splits, stream);
     case 11: return wg_launch<128, 256, 4, 4, 2, 64>(a, splits, stream);
+    case 14: return wg_launch<128, 64, 2, 2, 3, 64>(a, splits, stream);
     default: return 6;
   }
 }
