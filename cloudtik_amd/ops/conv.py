@@ -417,7 +417,11 @@ WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS", "256"))   # split
 # workgroups the 64-wide 4-wave tiles run one wave per SIMD (l1.c2 299 us, 187 at 512)
 WGRAD_BLOCKS_SMALL = int(os.environ.get("CLOUDTIK_AMD_WGRAD_BLOCKS_SMALL", "256"))
 WGRAD3X3_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_WGRAD3X3_BLOCKS", "128"))
-STEM_WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_STEM_WGRAD_BLOCKS", "256"))
+# the stem's weight gradient is the last kernel of the backward, alone on the chip: small tiles,
+# many workgroups (bench/stem_wgrad_probe.py, NHWC4: the auto 64 x 128 tile at 256 workgroups
+# 418 us -> 64 x 64 at 1,024: 218 us)
+STEM_WGRAD_BLOCKS = int(os.environ.get("CLOUDTIK_AMD_STEM_WGRAD_BLOCKS", "1024"))
+STEM_WGRAD_CFG = int(os.environ.get("CLOUDTIK_AMD_STEM_WGRAD_CFG", "0"))
 
 
 def wgrad_plan(M: int, co: int, nn: int, cfg: int, blocks: Optional[int] = None):
@@ -708,7 +712,7 @@ def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding) -> 
     nn = T * 64
     M = dy.shape[0] * dy.shape[2] * dy.shape[3]
     C = _C()
-    cfg = C.conv_wgrad_cfg(_WG_CFG, co, nn)
+    cfg = C.conv_wgrad_cfg(_WG_CFG if _WG_CFG >= 0 else STEM_WGRAD_CFG, co, nn)
     # the stem's weight gradient is the last kernel of the backward, on the main stream with the
     # chip to itself: split it over more workgroups than the side-stream gradients
     splits, rows = wgrad_plan(M, co, nn, cfg, STEM_WGRAD_BLOCKS)
