@@ -191,8 +191,13 @@ class ResNet(nn.Module):
         use_wgrad_side_stream(self, True)
 
     def stem(self, x):
-        y = igemm.stem_conv(x, self.conv1)
         bn = self.bn1
+        if bn.relu and self.training and not bn.frozen:
+            # conv + BN + ReLU + max-pool with the BN backward folded into the conv weight gradient
+            out = ops.stem_block(x, self.conv1, bn)
+            if out is not None:
+                return out
+        y = igemm.stem_conv(x, self.conv1)
         if bn.relu and self.training and not bn.frozen:
             # BN + ReLU + 3x3/2 max-pool in one pass (the full-resolution activation is never
             # written; ops/functional.py batch_norm_relu_maxpool)

@@ -92,7 +92,7 @@ def set_rng_state(state):
 
 from .functional import (  # noqa: E402,F401
     layer_norm, bias_act, bias_gelu, dropout, embedding3, cross_entropy_fused, batch_norm_act,
-    batch_norm_relu_maxpool, batch_norm_add_bn_act,
+    batch_norm_relu_maxpool, batch_norm_add_bn_act, stem_block,
     ACT_NONE, ACT_GELU, ACT_RELU,
 )
 from .attention import attention, attention_packed, attention_relbias  # noqa: E402,F401

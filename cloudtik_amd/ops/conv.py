@@ -705,7 +705,10 @@ def stem_fwd(x8: torch.Tensor, w: torch.Tensor, stride, padding, partials: bool 
     return out
 
 
-def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding) -> torch.Tensor:
+def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding, fp32: bool = False,
+               blocks: Optional[int] = None) -> torch.Tensor:
+    """dW of the stem conv as channels_last [Co, C, R, S]: bf16, or (``fp32``) the fp32 sums
+    (ops.functional._StemBlockFn combines three of them)."""
     co, c, R, S = w_shape
     pairs = x8.shape[1] == 4
     T = (R + 1) // 2 if pairs else R
@@ -715,15 +718,18 @@ def stem_wgrad(dy: torch.Tensor, x8: torch.Tensor, w_shape, stride, padding) -> 
     cfg = C.conv_wgrad_cfg(_WG_CFG if _WG_CFG >= 0 else STEM_WGRAD_CFG, co, nn)
     # the stem's weight gradient is the last kernel of the backward, on the main stream with the
     # chip to itself: split it over more workgroups than the side-stream gradients
-    splits, rows = wgrad_plan(M, co, nn, cfg, STEM_WGRAD_BLOCKS)
+    splits, rows = wgrad_plan(M, co, nn, cfg, STEM_WGRAD_BLOCKS if blocks is None else blocks)
     part = torch.empty(splits * co * nn, device=dy.device, dtype=torch.float32)
     if not C.conv_wgrad(dy, x8, part, _stem_taps(R, padding, pairs), [stride[0], stride[1], rows], splits, cfg):
         raise RuntimeError(f"conv_wgrad (stem) rejected dy{tuple(dy.shape)} x{tuple(x8.shape)}")
-    full = torch.empty(co * nn, device=dy.device, dtype=dy.dtype)
-    if splits <= 16:
-        C.splitk_reduce(part.view(splits, -1), full, False)
+    if fp32:
+        full = part.view(splits, -1).sum(0)
     else:
-        C.splitk_reduce_wide(part, splits, full, False)
+        full = torch.empty(co * nn, device=dy.device, dtype=dy.dtype)
+        if splits <= 16:
+            C.splitk_reduce(part.view(splits, -1), full, False)
+        else:
+            C.splitk_reduce_wide(part, splits, full, False)
     if pairs:
         full = full.view(co, 2 * T, 8, 4)[:, :R, 1:S + 1, :c]
     else:

@@ -1202,6 +1202,7 @@ extern "C" int ct_bn_bwd_given(const void* dym, const void* x, const void* gamma
     bn_bwd_finalize_kernel<bf16_t><<<ceil_div(C, 64), 1024, 0, stream>>>(
         q1, q2, nq, M, C, (const bf16_t*)gamma, stat, stat + C, (bf16_t*)dgamma, (bf16_t*)dbeta, coef, coef + C,
         coef + 2 * C, acc);
+  if (dx == nullptr) return hipGetLastError() == hipSuccess ? 0 : 7;   // coefficients only (work + 2 G C)
   const long tv = (long)M * (C / 8);
   const BnMask none{0, nullptr, nullptr, nullptr, nullptr};
   BN_EW_DISPATCH(bn_bwd_apply_kernel, tv, (const bf16_t*)dym, none, (const bf16_t*)x, coef, coef + C, coef + 2 * C,

@@ -780,6 +780,35 @@ std::vector<at::Tensor> bn_bwd_given(at::Tensor dym, at::Tensor x, at::Tensor ga
   return {dx, dgamma, dbeta};
 }
 
+// The BatchNorm backward's per-channel results WITHOUT the apply pass: (dgamma, dbeta, coef) from
+// the producer's per-tile sums, coef = float[3C] = (ca, c1, c0) with dx = ca dym + c1 x + c0.  For
+// a BatchNorm whose input gradient only feeds a weight gradient (the ResNet stem: dW = ca G1 +
+// c1 G2 + c0 G0 over the conv's im2col columns, ops/functional.py _StemBlockFn).
+std::vector<at::Tensor> bn_bwd_coefs_given(int64_t M, at::Tensor gamma, at::Tensor stat, at::Tensor part,
+                                           int64_t tiles, int64_t rows, c10::optional<at::Tensor> dgamma_acc,
+                                           c10::optional<at::Tensor> dbeta_acc) {
+  const int C = (int)gamma.numel();
+  TORCH_CHECK(gamma.is_cuda() && C % 8 == 0 && C <= 2048 && stat.numel() == 4 * (long)C, "bn_bwd_coefs_given: stat");
+  CHECK_F32(stat);
+  CHECK_F32(part);
+  TORCH_CHECK(M > 0 && tiles > 0 && tiles <= rows && part.numel() >= 2 * rows * C, "bn_bwd_coefs_given: part buffer");
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined();
+  if (acc) {
+    TORCH_CHECK(dbeta_acc.has_value() && dbeta_acc->defined() && dgamma_acc->is_contiguous() &&
+                dbeta_acc->is_contiguous() && dgamma_acc->numel() == C && dbeta_acc->numel() == C &&
+                dgamma_acc->scalar_type() == gamma.scalar_type() && dbeta_acc->scalar_type() == gamma.scalar_type(),
+                "bn_bwd_coefs_given: bad accumulate targets");
+  }
+  auto dgamma = acc ? *dgamma_acc : at::empty_like(gamma), dbeta = acc ? *dbeta_acc : at::empty_like(gamma);
+  const long G = (tiles + 63) / 64;
+  auto work = at::empty({2 * G * C + 3 * (long)C}, gamma.options().dtype(at::kFloat));
+  int rc = ct_bn_bwd_given(nullptr, nullptr, gamma.data_ptr(), stat.data_ptr<float>(), nullptr, dgamma.data_ptr(),
+                           dbeta.data_ptr(), (gamma.scalar_type() == at::kFloat ? 1 : 0) | (acc ? 2 : 0),
+                           part.data_ptr<float>(), rows * C, (int)tiles, work.data_ptr<float>(), (int)M, C, cur_stream());
+  TORCH_CHECK(rc == 0, "bn_bwd_coefs_given: unsupported C=", C);
+  return {dgamma, dbeta, work.narrow(0, 2 * G * C, 3 * (long)C)};
+}
+
 void register_ext(pybind11::module& m);   // bindings_ext.cpp
 void register_graph(pybind11::module& m); // bindings_graph.cpp
 void register_deform(pybind11::module& m); // bindings_deform.cpp
@@ -831,6 +860,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_bwd_given", &bn_bwd_given);
+  m.def("bn_bwd_coefs_given", &bn_bwd_coefs_given);
   m.def("attn_fwd_relbias", &attn_fwd_relbias);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

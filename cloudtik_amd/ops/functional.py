@@ -438,6 +438,121 @@ class _BNReLUPoolFn(torch.autograd.Function):
         return dx, dg, db, None, None, None, None
 
 
+# the ResNet stem's BatchNorm backward folded into the stem conv's weight gradient (_StemBlockFn).
+# Opt-in: the backward's tail loses its apply pass, but G2 (as much MFMA work as the weight
+# gradient itself) then runs during the forward, where nothing else is on the side stream:
+# 20.44 / 20.46 / 20.46 -> 20.53 / 20.57 / 20.56 ms (profiles/r5/stem_pairs.md)
+_STEM_FOLD = os.environ.get("CLOUDTIK_AMD_STEM_FOLD", "0") == "1"
+
+
+def _stem_tap_colsum(x4, c, R, S, stride, padding):
+    """G0[ch, r, s] = sum over the batch and the output pixels of the input at tap (r, s): the
+    column sums of the stem conv's implicit im2col matrix (zero padding included), fp32."""
+    xs = x4.sum(0, dtype=torch.float32)[:c]                   # [c, H, W]
+    xp = torch.nn.functional.pad(xs, (padding[1], padding[1], padding[0], padding[0]))
+    cols = torch.nn.functional.unfold(xp.unsqueeze(0), (R, S), stride=stride)   # [1, c R S, L]
+    return cols.sum(-1).view(c, R, S)
+
+
+class _StemBlockFn(torch.autograd.Function):
+    """ResNet stem ``maxpool3x3/s2(relu(bn(conv7x7/s2(x))))`` with the BatchNorm backward folded
+    into the conv's weight gradient.  The stem conv's input needs no gradient, so the BatchNorm
+    input gradient dx = ca dym + c1 y + c0 (per-channel coefficients of the backward, dym the
+    masked pooled gradient, y the conv output) only feeds dW = sum_p dx (x) X, which splits into
+
+        dW = ca G1 + c1 G2 + c0 G0,   G1 = sum dym (x) X,  G2 = sum y (x) X,  G0 = sum X
+
+    G2 and G0 depend on the forward only: they run on the gradient side stream during the step.
+    The backward's tail is then the fused pool-gradient + BatchNorm-sums pass, the coefficient
+    finalize and G1 -- no BatchNorm apply pass over the 411 MB activation (with the old chain:
+    pool gradient, BatchNorm reduce, apply, weight gradient)."""
+
+    @staticmethod
+    def forward(ctx, x4, w, gamma, beta, run_mean, run_var, momentum, eps, stride, padding):
+        from cloudtik_amd.ops import conv as CV
+        from cloudtik_amd.ops.linear import grad_stream
+        y = CV.stem_fwd(x4, w, stride, padding, partials=True)
+        part, rows = y._ct_bn_part
+        yp, arg, stat = _C().bn_fwd_train_pool_given(y, gamma, beta, run_mean, run_var, part, rows, eps, momentum)
+        ctx.save_for_backward(x4, y, arg, stat, gamma)
+        ctx.cfg = (tuple(w.shape), stride, padding)
+        ctx.wp, ctx.params = w, (gamma, beta)
+        ctx.g = None
+        if ctx.needs_input_grad[1]:
+            side = grad_stream()
+            side.wait_stream(torch.cuda.current_stream())
+            co, c, R, S = w.shape
+            with torch.cuda.stream(side):
+                g2 = CV.stem_wgrad(y, x4, tuple(w.shape), stride, padding, fp32=True, blocks=256)
+                g0 = _stem_tap_colsum(x4, c, R, S, stride, padding)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            y.record_stream(side)
+            x4.record_stream(side)
+            ctx.g = (g2, g0, ev)
+        return yp
+
+    @staticmethod
+    def backward(ctx, dyp):
+        from cloudtik_amd.ops import conv as CV
+        x4, y, arg, stat, gamma = ctx.saved_tensors
+        wp, bp = ctx.params
+        w_shape, stride, padding = ctx.cfg
+        C = _C()
+        rows = C.maxpool3s2_bwd_bn_rows(y.shape[0], y.shape[2])
+        part = torch.empty(2 * rows * y.shape[1], device=y.device, dtype=torch.float32)
+        dym = C.maxpool3s2_bwd_bn(dyp.contiguous(memory_format=torch.channels_last), arg, y, stat, part)
+        M = y.numel() // y.shape[1]
+        flat = all(p is not None and p.grad is not None and getattr(p, "_ct_flat_grad", False)
+                   and p.grad.is_contiguous() and p.grad.dtype == gamma.dtype for p in (wp, bp))
+        dg, db, coef = C.bn_bwd_coefs_given(M, gamma, stat, part, rows, rows, wp.grad if flat else None,
+                                            bp.grad if flat else None)
+        if flat:
+            for p in (wp, bp):
+                cb = getattr(p, "_ct_grad_ready", None)
+                if cb is not None:
+                    cb(p)
+            dg = db = None
+        dw = None
+        if ctx.g is not None:
+            g2, g0, ev = ctx.g
+            g1 = CV.stem_wgrad(dym, x4, w_shape, stride, padding, fp32=True)
+            cur = torch.cuda.current_stream()
+            cur.wait_event(ev)
+            g2.record_stream(cur)
+            g0.record_stream(cur)
+            ca, c1, c0 = (t.view(-1, 1, 1, 1) for t in coef.view(3, -1))
+            dwf = ca * g1 + c1 * g2 + c0 * g0.unsqueeze(0)
+            dw = dwf.to(ctx.wp.dtype).contiguous(memory_format=torch.channels_last)
+            ctx.g = None
+            from cloudtik_amd.ops.conv1x1 import _flat_target
+            target = _flat_target(ctx.wp)
+            if target is not None:                    # straight into the flat gradient buffer
+                target.add_(dw)
+                cb = getattr(ctx.wp, "_ct_grad_ready", None)
+                if cb is not None:
+                    cb(ctx.wp)
+                dw = None
+        return None, dw, dg, db, None, None, None, None, None, None
+
+
+def stem_block(x, conv, bn):
+    """``max_pool2d(relu(bn(conv(x))), 3, 2, 1)`` for the ResNet stem in training, with the
+    BatchNorm backward folded into the conv weight gradient (_StemBlockFn) when the pieces are
+    on their native paths; None when not eligible (the caller composes the ops itself)."""
+    from cloudtik_amd.ops import conv as CV
+    w = conv.weight
+    if not (_STEM_FOLD and bn.training and _native(w) and CV.stem_eligible(x, conv)
+            and CV.stem_pairs(x.shape, w.shape, tuple(conv.stride), tuple(conv.padding))
+            and w.shape[0] in (8, 16, 32, 64, 128, 256) and bn.weight is not None and bn.bias is not None
+            and bn.running_mean is not None and bn.weight.dtype == torch.bfloat16):
+        return None
+    CV.ROUTES["igemm"] += 1
+    x4 = CV.to_nhwc8(x, 4)
+    return _StemBlockFn.apply(x4, w, bn.weight, bn.bias, bn.running_mean, bn.running_var, float(bn.momentum),
+                              float(bn.eps), tuple(conv.stride), tuple(conv.padding))
+
+
 def batch_norm_relu_maxpool(x, weight, bias, running_mean, running_var, training=True, momentum=0.1, eps=1e-5):
     """``max_pool2d(relu(BatchNorm(x)), 3, 2, 1)`` -- fused on GPU in training (NHWC bf16)."""
     if _native(x) and _bn_native_ok(x) and x.dim() == 4 and training:
