@@ -2,7 +2,7 @@
 ``ops.conv.conv_wgrad`` (kernel + split-K reduce) per configuration.  Run under
 ``rocprofv3 --kernel-trace --stats`` for the kernel / reduce split.
 
-    python bench/wgrad3x3_probe.py [--cfgs -1,13,15] [--shapes l1,l2] [--iters 20]
+    python bench/wgrad3x3_probe.py [--cfgs=-1,12,13] [--shapes l1,l2,l1c3] [--iters 20]
 """
 import argparse
 import json
