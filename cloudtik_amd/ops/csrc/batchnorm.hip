@@ -644,21 +644,27 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_bn_kernel(const bf16_t* __
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
       const int ow0 = w >> 1, ow1 = min((w + 1) >> 1, OW - 1);
       const u16x8 xv = reinterpret_cast<const u16x8*>(x)[xrow + i];
-      for (int oh = oh0; oh <= oh1; ++oh) {
-        const int kh = h - (2 * oh - 1);
-        if (kh < 0 || kh > 2) continue;
-        const long obase = ((long)n * OH + oh) * OW;
-        for (int ow = ow0; ow <= ow1; ++ow) {
-          const int kw = w - (2 * ow - 1);
-          if (kw < 0 || kw > 2) continue;
-          const long o = (obase + ow) * CV + cv0;
-          const uint64_t packed = reinterpret_cast<const uint64_t*>(arg)[o];
-          const u16x8 g = reinterpret_cast<const u16x8*>(dy)[o];
-          const uint8_t pos = (uint8_t)(kh * 3 + kw);
+      // the (at most 2 x 2) windows' loads all issued before use (as maxpool3s2_bwd_kernel)
+      uint64_t pk[4];
+      u16x8 gv[4];
+      uint8_t pos[4];
+      bool ok[4];
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (((packed >> (8 * j)) & 0xFF) == pos) acc[j] += bf2f(g[j]);
-        }
+      for (int q = 0; q < 4; ++q) {
+        const int oh = oh0 + (q >> 1), ow = ow0 + (q & 1);
+        const int kh = h - (2 * oh - 1), kw = w - (2 * ow - 1);
+        ok[q] = oh <= oh1 && ow <= ow1 && kh >= 0 && kh <= 2 && kw >= 0 && kw <= 2;
+        const long o = ok[q] ? (((long)n * OH + oh) * OW + ow) * CV + cv0 : 0;
+        pk[q] = ok[q] ? reinterpret_cast<const uint64_t*>(arg)[o] : 0ull;
+        gv[q] = ok[q] ? reinterpret_cast<const u16x8*>(dy)[o] : u16x8(0);
+        pos[q] = (uint8_t)(kh * 3 + kw);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!ok[q]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((pk[q] >> (8 * j)) & 0xFF) == pos[q]) acc[j] += bf2f(gv[q][j]);
       }
       u16x8 out;
 #pragma unroll

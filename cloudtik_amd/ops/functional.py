@@ -389,8 +389,10 @@ def _bn_param_grads(wp, bp, gamma, x, stat, dy, y, mode, has_res):
 
 
 # the stem backward's pool gather and BatchNorm reduction in one kernel (batchnorm.hip
-# maxpool3s2_bwd_bn_kernel)
-_STEM_POOL_BN_FUSE = os.environ.get("CLOUDTIK_AMD_STEM_POOL_BN_FUSE", "0") == "1"
+# maxpool3s2_bwd_bn_kernel): on by default since its window loads are issued together (the
+# separate 308 us reduce pass leaves the backward's tail: 20.56 / 20.60 / 20.57 -> 20.45 / 20.46
+# / 20.42 ms same box; before that change it measured neutral)
+_STEM_POOL_BN_FUSE = os.environ.get("CLOUDTIK_AMD_STEM_POOL_BN_FUSE", "1") == "1"
 
 
 class _BNReLUPoolFn(torch.autograd.Function):
