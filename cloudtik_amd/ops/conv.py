@@ -401,7 +401,7 @@ _WG_CFG = int(os.environ.get("CLOUDTIK_AMD_CONV_WGRAD_CFG", "-1"))
 _TN_WGRAD_1X1 = int(os.environ.get("CLOUDTIK_AMD_CONV1X1_TN_WGRAD", "2"))
 _WG_TILES = {0: (64, 64), 1: (64, 128), 2: (128, 128), 3: (128, 256), 4: (64, 64), 5: (64, 128), 6: (128, 128),
              7: (64, 64), 8: (64, 64), 9: (128, 128), 10: (128, 128), 11: (128, 256), 12: (64, 576), 13: (64, 576),
-             14: (128, 64)}
+             14: (128, 64), 15: (64, 256)}
 # 3x3 / stride 1 or 2 / pad 1 weight gradients on the nine-tap kernel (conv.hip conv_wgrad3x3_kernel):
 # one workgroup owns 64 output x 64 input channels of all nine taps.  -1 = auto (cfg 12, a 3-slot
 # ring at one workgroup per CU; cfg 13, 2 slots at two per CU and twice the split-K workgroups,

@@ -1531,6 +1531,14 @@ extern "C" int ct_conv_wgrad_cfg(int cfg, int Co, int NN) {
   }();
   if (Co % 128 == 0 && NN % 256 == 0 && Co >= 256) return rule >= 2 ? 11 : 3;
   if (Co % 128 == 0 && NN % 128 == 0) return 9;
+  // CLOUDTIK_AMD_WGRAD_WIDE=1: 64 x 256 tiles for 64-output-channel gradients with 256+ columns
+  // (layer-1 256 -> 64 1x1 convs: dY re-read for 1 column tile instead of 2).  Off: the step
+  // measured 20.44 / 20.38 / 20.40 -> 20.46 / 20.41 / 20.43 ms
+  static const bool wide = [] {
+    const char* e = std::getenv("CLOUDTIK_AMD_WGRAD_WIDE");
+    return e && std::atoi(e) != 0;
+  }();
+  if (wide && NN % 256 == 0) return 15;
   // the 64-wide tiles serve the layer-1 shapes (802816-pixel reductions): 64-pixel stages win
   // there (l1.c2 301 -> 289 us, l1.c3 156 -> 142, l1.c1 128 -> 118; profiles/r4/conv_stream_probe.md)
   if (NN % 128 == 0) return 5;
@@ -1594,6 +1602,8 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
   }
   if (cfg == 14) {                   // 128 co x 64 columns (4 waves 2x2, 64-pixel stages x 3)
     if (Co % 128 || rows_per_split % 64) return 2;
+  } else if (cfg == 15) {            // 64 co x 256 columns (4 waves 2x2, 64-pixel stages x 2)
+    if (a.NN % 256 || rows_per_split % 64) return 2;
   } else {
     const int tile = cfg == 11 ? 3 : (cfg >= 9 ? 2 : (cfg >= 7 ? 0 : (cfg >= 4 ? cfg - 4 : cfg)));
     if ((tile >= 2 && Co % 128) || (tile == 3 && a.NN % 256) || (tile >= 1 && a.NN % 128)) return 2;
@@ -1612,6 +1622,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
       case 8: return wg_launch<64, 64, 2, 2, 3, 64, true>(a, splits, stream);
       case 9: return wg_launch<128, 128, 2, 4, 4, 32, true>(a, splits, stream);
       case 14: return wg_launch<128, 64, 2, 2, 3, 64, true>(a, splits, stream);
+      case 15: return wg_launch<64, 256, 2, 2, 2, 64, true>(a, splits, stream);
       default: break;
     }
   }
@@ -1629,6 +1640,7 @@ extern "C" int ct_conv_wgrad(const void* DY, const void* X, int Hi, int Wi, int 
     case 10: return wg_launch<128, 128, 2, 4, 2, 64>(a, splits, stream);
     case 11: return wg_launch<128, 256, 4, 4, 2, 64>(a, splits, stream);
     case 14: return wg_launch<128, 64, 2, 2, 3, 64>(a, splits, stream);
+    case 15: return wg_launch<64, 256, 2, 2, 2, 64>(a, splits, stream);
     default: return 6;
   }
 }

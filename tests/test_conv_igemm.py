@@ -485,7 +485,7 @@ def test_streamed_conv_bn_backward_epilogue(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wcfg", [4, 5, 6, 7, 8, 9, 10, 11, 14])
+@pytest.mark.parametrize("wcfg", [4, 5, 6, 7, 8, 9, 10, 11, 14, 15])
 @pytest.mark.parametrize("ci,co,H,k,s", [(128, 128, 15, 3, 2), (128, 128, 12, 1, 1), (64, 256, 10, 3, 1),
                                          (128, 256, 9, 3, 1)])
 def test_wgrad_64_pixel_stages_match_fp32_reference(cuda, monkeypatch, wcfg, ci, co, H, k, s):
