@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import json
 import os
+import shlex
 from typing import Any, Dict, List, Optional, Tuple
 
 from cloudtik_amd.core import tags as T
@@ -197,7 +198,10 @@ class RedisRuntime(ConfiguredRuntime):
             steps.append(f"redis-sentinel {c['dir']}/sentinel.conf --daemonize yes")
         elif mode == "sharding":
             seeds = [c["head_ip"]] + [ip for _, ip in c["members"] if ip != c["ip"]]
-            steps.append(f"{sys.executable} -m cloudtik_amd.runtime.redis_cluster join --node-ip {c['ip']} "
+            # the join speaks RESP to every member: with requirepass set it must AUTH (the
+            # password goes by environment, not argv, so it stays out of the process table)
+            auth = f"REDIS_PASSWORD={shlex.quote(str(cfg['password']))} " if cfg.get("password") else ""
+            steps.append(f"{auth}{sys.executable} -m cloudtik_amd.runtime.redis_cluster join --node-ip {c['ip']} "
                          f"--port {port} --seeds {','.join(seeds)}"
                          f" --replicas-per-master {int((cfg.get('sharding') or {}).get('replicas_per_master', 0))}"
                          f" --marker {c['dir']}/data/.cluster-initialized" + (" --head" if head else ""))

@@ -78,12 +78,16 @@ class DiscoveryJob(PullJob):
     def discover(self) -> Dict[str, BackendService]:
         return backend_services_from_instances(self.query())
 
-    def changed(self, services: Dict[str, BackendService]) -> bool:
+    def pending(self, services: Dict[str, BackendService]) -> Optional[str]:
+        """The hash of ``services`` when it differs from the last one APPLIED, else None.  The
+        caller records it with ``commit`` only after every admin call / reload succeeded: a
+        failed apply (an admin API not up yet at the first pull) is retried on the next pull
+        even when the discovered set has not changed since."""
         h = json_hash({k: v.to_dict() for k, v in services.items()})
-        if h == self.last_hash:
-            return False
+        return None if h == self.last_hash else h
+
+    def commit(self, h: str) -> None:
         self.last_hash = h
-        return True
 
 
 # =============================================================================== HAProxy
@@ -259,8 +263,11 @@ class DiscoverHAProxyBackends(DiscoveryJob):
             logger.warning("haproxy discovery: no live servers for the selector")
         for api in self.apis:
             sync_haproxy_backend(api, self.backend, servers)
-        if self.changed(services) and self.render is not None:
-            self.render(servers)
+        h = self.pending(services)
+        if h is not None:
+            if self.render is not None:
+                self.render(servers)
+            self.commit(h)
 
 
 # =============================================================================== NGINX
@@ -302,15 +309,19 @@ class DiscoverNginxBackends(DiscoveryJob):
 
     def pull(self):
         services = self.discover()
-        if not self.changed(services):
+        h = self.pending(services)
+        if h is None:
             return
         text = nginx_conf(services, self.port, self.balance)
         tmp = self.conf_path + ".cloudtik-new"
         with open(tmp, "w") as f:
             f.write(text)
         os.replace(tmp, self.conf_path)
-        self.runner(self.reload_cmd)
+        r = self.runner(self.reload_cmd)
+        if getattr(r, "returncode", 0) not in (0, None):
+            raise RuntimeError(f"nginx reload failed (rc {r.returncode}): {self.reload_cmd}")
         self.reloads += 1
+        self.commit(h)
 
 
 # =============================================================================== admin-API gateways
@@ -346,7 +357,8 @@ class DiscoverKongBackends(DiscoveryJob):
 
     def pull(self):
         services = self.discover()
-        if not self.changed(services):
+        h = self.pending(services)
+        if h is None:
             return
         managed = {s["name"] for s in self._get_all(f"/services?tags={MANAGED_TAG}")}
         for name, svc in services.items():
@@ -367,6 +379,7 @@ class DiscoverKongBackends(DiscoveryJob):
             self.http("DELETE", f"{self.admin}/routes/{name}")
             self.http("DELETE", f"{self.admin}/services/{name}")
             self.http("DELETE", f"{self.admin}/upstreams/{name}")
+        self.commit(h)
 
 
 class DiscoverAPISIXBackends(DiscoveryJob):
@@ -396,7 +409,8 @@ class DiscoverAPISIXBackends(DiscoveryJob):
 
     def pull(self):
         services = self.discover()
-        if not self.changed(services):
+        h = self.pending(services)
+        if h is None:
             return
         for name, svc in services.items():
             self._call("PUT", f"/upstreams/{name}",
@@ -413,3 +427,4 @@ class DiscoverAPISIXBackends(DiscoveryJob):
             self._call("DELETE", f"/routes/{rid}")
         for uid in sorted(set(self._managed("upstreams")) - set(services)):
             self._call("DELETE", f"/upstreams/{uid}")
+        self.commit(h)

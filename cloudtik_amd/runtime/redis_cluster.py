@@ -76,8 +76,10 @@ class RedisClusterManager:
 
     def __init__(self, connect: Callable[[str, int], object], port: int = 6379,
                  replicas_per_master: int = 0, lock: Optional[Callable[[], contextlib.AbstractContextManager]] = None,
-                 wait: float = 30.0, poll: float = 0.2, migrate_timeout_ms: int = 5000):
+                 wait: float = 30.0, poll: float = 0.2, migrate_timeout_ms: int = 5000,
+                 password: Optional[str] = None):
         self.connect = connect
+        self.password = password or None      # MIGRATE authenticates to the target itself
         self.port = int(port)
         self.replicas = max(0, int(replicas_per_master))
         self.lock = lock or contextlib.nullcontext
@@ -169,7 +171,8 @@ class RedisClusterManager:
                     keys = src.execute("CLUSTER", "GETKEYSINSLOT", s, 100) or []
                     if not keys:
                         break
-                    src.execute("MIGRATE", dst_ip, self.port, "", 0, self.migrate_timeout_ms, "KEYS", *keys)
+                    auth = ("AUTH", self.password) if self.password else ()
+                    src.execute("MIGRATE", dst_ip, self.port, "", 0, self.migrate_timeout_ms, *auth, "KEYS", *keys)
                 dst.execute("CLUSTER", "SETSLOT", s, "NODE", dst_id)
                 src.execute("CLUSTER", "SETSLOT", s, "NODE", dst_id)
         return moved
@@ -241,7 +244,8 @@ def main(argv=None) -> int:
         return RespConnection(host, port, a.password or None, timeout=10, connect_retries=30).connect()
 
     cluster = os.environ.get("CLOUDTIK_CLUSTER", "cloudtik")
-    mgr = RedisClusterManager(connect, a.port, a.replicas_per_master, lock=_state_lock(f"{cluster}.redis.role"))
+    mgr = RedisClusterManager(connect, a.port, a.replicas_per_master, lock=_state_lock(f"{cluster}.redis.role"),
+                              password=a.password or None)
     role = mgr.join(a.node_ip, [s for s in a.seeds.split(",") if s], head=a.head)
     print(f"redis cluster: {a.node_ip} -> {role}")
     if a.marker:

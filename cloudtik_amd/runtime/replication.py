@@ -37,9 +37,10 @@ DEFAULT_PASSWORD = "cloudtik"
 
 
 def retry(cmd: str, tries: int = 60, delay: float = 2) -> str:
-    """bash: run ``cmd`` until it succeeds, at most ``tries`` times; fails after that."""
-    return (f"_ok=0; for _i in $(seq {tries}); do if ( {cmd} ); then _ok=1; break; fi; sleep {delay}; done; "
-            f"[ $_ok -eq 1 ]")
+    """bash: run ``cmd`` until it succeeds, at most ``tries`` times; fails after that.  One
+    brace group, so ``a && retry(b) && c`` chains as written."""
+    return (f"{{ _ok=0; for _i in $(seq {tries}); do if ( {cmd} ); then _ok=1; break; fi; sleep {delay}; done; "
+            f"[ $_ok -eq 1 ]; }}")
 
 
 def once(marker: str, cmd: str) -> str:
@@ -47,9 +48,12 @@ def once(marker: str, cmd: str) -> str:
     return f"[ -f {marker} ] || {{ {cmd} && touch {marker}; }}"
 
 
-def heredoc(prefix: str, body: str, tag: str = "CLOUDTIK_EOF") -> str:
-    """``prefix <<'TAG' ... TAG`` (quoted: no shell expansion inside the body)."""
-    return f"{prefix} <<'{tag}'\n{body.rstrip()}\n{tag}"
+def feed_stdin(prefix: str, body: str) -> str:
+    """bash: ``printf '%s\\n' '<body>' | prefix`` -- the body (SQL) on the command's stdin, single-
+    quoted so nothing in it is expanded.  One shell word, so the step composes with ``&&`` / ``;``
+    / ``( )`` anywhere on a line (a here-document would end only at a line holding its bare tag,
+    swallowing whatever the caller appends after it)."""
+    return f"printf '%s\\n' {shlex.quote(body.rstrip())} | {prefix}"
 
 
 def _sq(v: str) -> str:
@@ -80,7 +84,7 @@ def mysql_group_conf(c: Dict[str, Any], port: int) -> List[str]:
 
 
 def mysql_sql(body: str) -> str:
-    return heredoc("sudo mysql -uroot --protocol=socket", body)
+    return feed_stdin("sudo mysql -uroot --protocol=socket", body)
 
 
 def mysql_bootstrap_steps(c: Dict[str, Any]) -> List[str]:
@@ -138,7 +142,7 @@ PG_DATA = "$(ls -d /var/lib/postgresql/*/main 2>/dev/null | head -1)"
 
 def psql(body: str, host: Optional[str] = None, extra: str = "") -> str:
     h = f" -h {host}" if host else ""
-    return heredoc(f"sudo -u postgres psql -v ON_ERROR_STOP=1{h}{extra}", body)
+    return feed_stdin(f"sudo -u postgres psql -v ON_ERROR_STOP=1{h}{extra}", body)
 
 
 def repmgr_conf(c: Dict[str, Any], data_dir: str) -> str:
@@ -184,7 +188,7 @@ def postgres_pre_start_steps(c: Dict[str, Any]) -> List[str]:
         clone = (f"sudo -u postgres env PGPASSWORD={shlex.quote(pw)} pg_basebackup -h {c['head_ip']} -p {port} "
                  f"-U {user} -D \"$D\" -X stream -R")
     return [f"D={PG_DATA}; [ -n \"$D\" ] || exit 1; [ -f \"$D/standby.signal\" ] || {{ "
-            f"{retry(primary_up, tries=90, delay=2)} && sudo service postgresql stop; "
+            f"{retry(primary_up, tries=90, delay=2)} || exit 1; sudo service postgresql stop; "
             f"sudo rm -rf \"$D.cloudtik-old\" && sudo mv \"$D\" \"$D.cloudtik-old\" && "
             f"sudo install -d -o postgres -g postgres -m 700 \"$D\" && {clone} && "
             f"sudo chown -R postgres:postgres \"$D\"; }}"]

@@ -207,6 +207,49 @@ def test_kong_admin_objects_follow_services():
     assert len(kong.calls) == n
 
 
+def test_failed_apply_is_retried_on_the_next_pull():
+    """The admin API is not up yet at the first pull: the job must apply again on the next
+    pull even though the discovered set did not change (the hash is recorded only after a
+    successful apply)."""
+    src = Source([_inst("web", "10.0.0.2", 8080)])
+    kong = FakeKong()
+    down = {"n": 1}
+
+    def flaky(method, url, body=None, headers=None):
+        if down["n"] > 0:
+            down["n"] -= 1
+            raise ConnectionRefusedError("admin API not up")
+        return kong(method, url, body, headers)
+
+    job = GD.DiscoverKongBackends(query=src, http=flaky, admin_url="http://127.0.0.1:8001")
+    with pytest.raises(ConnectionRefusedError):
+        job.pull()
+    job.pull()                                                           # same services: retried
+    assert set(kong.objs["services"]) == {"web"}
+    n = len(kong.calls)
+    job.pull()
+    assert len(kong.calls) == n                                          # applied: now idle
+
+
+def test_nginx_failed_reload_is_retried(tmp_path):
+    src = Source([_inst("web", "10.0.0.2", 8080)])
+
+    class R:
+        def __init__(self, rc):
+            self.returncode = rc
+
+    rcs = [1, 0]
+    ran = []
+    job = GD.DiscoverNginxBackends(query=src, conf_path=str(tmp_path / "nginx.conf"),
+                                   runner=lambda cmd: ran.append(cmd) or R(rcs.pop(0)))
+    with pytest.raises(RuntimeError):
+        job.pull()
+    job.pull()
+    assert len(ran) == 2 and job.reloads == 1
+    job.pull()
+    assert len(ran) == 2
+
+
 class FakeAPISIX:
     def __init__(self):
         self.objs = {"upstreams": {}, "routes": {}}

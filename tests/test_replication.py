@@ -10,6 +10,10 @@ replaced by a recorder, per node role, and the recorded commands are checked.  T
 Cluster protocol (bootstrap, meet, role, re-shard with key migration) runs against an
 in-process fake cluster that implements the commands it uses."""
 import os
+import re
+import shlex
+import subprocess
+import time
 import zlib
 
 import pytest
@@ -41,7 +45,19 @@ def _start(name, rc, head, ip, monkeypatch, tmp_path, seq=None, members_env=None
     import cloudtik_amd.runtime.common.runtime_base as RB
     monkeypatch.setattr(RB.subprocess, "run", lambda cmd, env=None, **kw: ran.append(cmd[-1]) or R())
     rt.node_services("start", head)
-    return ran, files
+    RAW[:] = ran
+    return [_decode(c) for c in ran], files
+
+
+_REAL_RUN = subprocess.run    # _start patches subprocess.run (the module attribute) while it records
+RAW = []          # the undecoded commands of the last _start (for the bash checks)
+_FEED = re.compile(r"printf '%s\\n' ('(?:[^']|'\"'\"')*') \| ")
+
+
+def _decode(cmd):
+    """The SQL fed on stdin (``printf '%s\\n' <quoted> | mysql ...``) shown unquoted, so the
+    assertions below read the statements the server receives."""
+    return _FEED.sub(lambda m: shlex.split(m.group(1))[0] + "\n| ", cmd)
 
 
 # ------------------------------------------------------------------------------- MySQL
@@ -287,3 +303,175 @@ def test_redis_cluster_bootstrap_join_and_reshard(replicas, masters):
     # a restarted node does nothing (marker file) -- and the nodes view parses back
     view = RC.parse_nodes(nodes[0].execute("CLUSTER", "NODES"))
     assert sum(len(v.slots) for v in view) == RC.SLOTS
+
+
+# ------------------------------------------------------------------------------- the steps in bash
+_CASES = [
+    ("mysql", {"cluster_mode": "replication", "replication_password": "it's"}, "MYSQL_MEMBERS"),
+    ("mysql", {"cluster_mode": "group_replication"}, "MYSQL_MEMBERS"),
+    ("postgres", {"cluster_mode": "replication", "replication_password": "p'w"}, "POSTGRES_MEMBERS"),
+    ("postgres", {"cluster_mode": "replication", "repmgr": {"enabled": True}}, "POSTGRES_MEMBERS"),
+    ("mongodb", {"cluster_mode": "replication"}, "MONGODB_MEMBERS"),
+]
+
+
+@pytest.mark.parametrize("name,rc,menv", _CASES)
+def test_every_step_parses_in_bash(name, rc, menv, tmp_path, monkeypatch):
+    """Every generated start step is a complete bash program (``bash -n``): a step whose SQL
+    body or quoting runs past its own end would swallow the rest of the line."""
+    for head, ip, seq in ((True, HEAD, 1), (False, W[0], 2)):
+        _start(name, rc, head, ip, monkeypatch, tmp_path / f"{head}", seq=seq, members_env=menv)
+        assert RAW
+        for cmd in RAW:
+            r = _REAL_RUN(["bash", "-n", "-c", cmd], capture_output=True, text=True)
+            assert r.returncode == 0, (cmd, r.stderr)
+
+
+_STUBS = {
+    "sudo": 'if [ "$1" = -u ]; then shift 2; fi; exec "$@"',
+    "mysql": 'cat >> "$LOG"; echo "-- end" >> "$LOG"',
+    "psql": 'cat >> "$LOG"; echo "-- end" >> "$LOG"',
+    "mysqladmin": "exit 0", "pg_isready": "exit 0", "service": "exit 0", "pgrep": "exit 1",
+    "repmgr": 'echo "repmgr $*" >> "$LOG"', "repmgrd": 'echo "repmgrd $*" >> "$LOG"',
+    "createdb": "exit 0", "tee": "cat > /dev/null",
+}
+
+
+def _run_stubbed(cmds, tmp_path):
+    bind = tmp_path / "bin"
+    bind.mkdir()
+    for n, body in _STUBS.items():
+        (bind / n).write_text("#!/bin/bash\n" + body + "\n")
+        (bind / n).chmod(0o755)
+    log = tmp_path / "server.log"
+    env = dict(os.environ, PATH=f"{bind}:{os.environ['PATH']}", LOG=str(log))
+    for cmd in cmds:
+        r = _REAL_RUN(["bash", "-c", cmd], capture_output=True, text=True, env=env, timeout=60)
+        assert r.returncode == 0, (cmd, r.stderr)
+    return log.read_text() if log.exists() else ""
+
+
+def test_mysql_replica_steps_run(tmp_path, monkeypatch):
+    """The replica's steps executed by bash against stub binaries: the server receives the
+    user statements and then the CHANGE REPLICATION SOURCE, with a quote in the password kept
+    intact; a second run is a no-op (the marker)."""
+    rc = {"cluster_mode": "replication", "replication_password": "it's"}
+    _start("mysql", rc, False, W[0], monkeypatch, tmp_path / "w", seq=2, members_env="MYSQL_MEMBERS")
+    cmds = [c for c in RAW if not c.startswith("sudo service")]
+    got = _run_stubbed(cmds, tmp_path)
+    assert "IDENTIFIED BY 'it''s';" in got                      # SQL-escaped, shell-intact
+    assert got.index("CREATE USER IF NOT EXISTS") < got.index("CHANGE REPLICATION SOURCE TO")
+    assert got.rstrip().endswith("START REPLICA;\n-- end".rstrip())
+    marker = tmp_path / "w" / "mysql" / ".replication-initialized"
+    assert marker.exists()
+    (tmp_path / "server.log").unlink()
+    import shutil
+    shutil.rmtree(tmp_path / "bin")
+    assert _run_stubbed(cmds, tmp_path) == ""                  # re-run: nothing sent again
+
+
+def test_postgres_primary_steps_run(tmp_path, monkeypatch):
+    rc = {"cluster_mode": "replication", "repmgr": {"enabled": True}, "replication_password": "p'w"}
+    _start("postgres", rc, True, HEAD, monkeypatch, tmp_path / "h", members_env="POSTGRES_MEMBERS")
+    cmds = [c for c in RAW if not c.startswith("sudo service")]
+    got = _run_stubbed(cmds, tmp_path)
+    assert "CREATE ROLE repl_user WITH REPLICATION LOGIN PASSWORD 'p''w';" in got
+    assert "repmgr -f" in got and "primary register --force" in got and "repmgrd -f" in got
+
+
+# ------------------------------------------------------------------------------- Redis with a password
+def test_redis_sharding_join_passes_password(tmp_path, monkeypatch):
+    rc = {"cluster_mode": "sharding", "password": "pa ss"}
+    head, hf = _start("redis", rc, True, HEAD, monkeypatch, tmp_path / "h", members_env="REDIS_MEMBERS")
+    join = [c for c in head if "redis_cluster join" in c]
+    assert join and join[0].startswith("REDIS_PASSWORD='pa ss' ")        # env, not argv
+    assert "requirepass pa ss" in hf["redis/redis.conf"]
+
+
+def test_redis_reshard_migrate_authenticates():
+    """With a password the key migration carries ``AUTH <pw>`` (the target needs it)."""
+    fc = FakeCluster()
+    ips = [HEAD, W[0]]
+    nodes = [FakeNode(fc, ip) for ip in ips]
+    for i in range(50):
+        nodes[0].data[f"k{i}"] = i
+    sent = []
+    orig = FakeNode.execute
+
+    def spy(self, *args):
+        a = [str(x) for x in args]
+        if a[0] == "MIGRATE":
+            sent.append(a)
+            assert a[a.index("KEYS") - 2:a.index("KEYS")] == ["AUTH", "pw"]
+        return orig(self, *args)
+
+    FakeNode.execute = spy
+    try:
+        for i, ip in enumerate(ips):
+            RC.RedisClusterManager(fc.connect, wait=1, poll=0.01, password="pw").join(ip, ips, head=(i == 0))
+    finally:
+        FakeNode.execute = orig
+    assert sent and sum(len(n.data) for n in nodes) == 50
+
+
+def _state_server(tmp_path, password):
+    import socket
+    from cloudtik_amd.core.state.state_client import StateServer
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return StateServer(port=port, data_dir=str(tmp_path), password=password).start()
+
+
+def test_redis_cluster_against_native_resp_server(tmp_path, monkeypatch):
+    """Where redis_cluster.py and the in-tree RESP server (native/state_server) overlap:
+    (1) the join's connection authenticates with the password -- without it every probe is
+    refused (NOAUTH), which ``_alive`` must read as "not a live member" and not crash on;
+    (2) the cluster-wide role lock (``_state_lock``) is a real DistributedLock on the head's
+    state server: two concurrent role assignments never overlap."""
+    import threading
+    from cloudtik_amd.core import constants as C
+    from cloudtik_amd.core.state.resp import RespConnection, RespError
+    srv = _state_server(tmp_path, "s3cret")
+    try:
+        def conn(pw):
+            return lambda host, port: RespConnection(host, port, pw, timeout=5).connect()
+
+        # authenticated: the server answers (and refuses CLUSTER, which it does not implement)
+        ok = RC.RedisClusterManager(conn("s3cret"), port=srv.port)
+        with pytest.raises(RespError) as e:
+            ok.nodes("127.0.0.1")
+        assert "NOAUTH" not in str(e.value)
+        bad = RC.RedisClusterManager(conn(None), port=srv.port)
+        with pytest.raises(RespError) as e:
+            bad.nodes("127.0.0.1")
+        assert "NOAUTH" in str(e.value).upper()
+        assert not bad._alive("127.0.0.1")
+        with pytest.raises(RuntimeError, match="no live redis cluster member"):
+            bad.join("10.9.9.9", ["127.0.0.1"], head=False)
+
+        monkeypatch.setenv("CLOUDTIK_HEAD_IP", "127.0.0.1")
+        monkeypatch.setenv("CLOUDTIK_STATE_PASSWORD", "s3cret")
+        monkeypatch.setattr(C, "CLOUDTIK_DEFAULT_PORT", srv.port)
+        spans = []
+
+        def role(i):
+            with RC._state_lock("c1.redis.role")():
+                t0 = time.monotonic()
+                time.sleep(0.2)
+                spans.append((t0, time.monotonic()))
+
+        th = [threading.Thread(target=role, args=(i,)) for i in range(3)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(30)
+        spans.sort()
+        assert len(spans) == 3
+        assert all(spans[i][1] <= spans[i + 1][0] for i in range(2))     # mutually exclusive
+        from cloudtik_amd.core.state.lock import LOCK_NAMESPACE
+        chk = RespConnection("127.0.0.1", srv.port, "s3cret").connect()
+        assert chk.get(f"@namespace_{LOCK_NAMESPACE}:c1.redis.role") is None      # released
+    finally:
+        srv.stop()
