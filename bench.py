@@ -43,8 +43,12 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# no published reference number exists (BASELINE.json "published": {}); vs_baseline = null
+# no published reference number exists (BASELINE.json "published": {}): vs_baseline is the ratio
+# to the same-config stock PyTorch-ROCm eager step measured in the same run (--baseline-steps)
 BASELINE = {"bert-large": None, "resnet50": None}
+BASELINE_DESC = ("same-config stock PyTorch-ROCm eager step measured in this run after the native one "
+                 "(HF BertForPreTraining + SDPA + per-tensor LAMB / torchvision-style ResNet-50 + torch SGD, "
+                 "autocast bf16, stock DDP at world size > 1); BASELINE.json publishes no number")
 TUNE_FILE = os.environ.get("CLOUDTIK_BENCH_TUNE_FILE") or os.path.join(REPO, "cloudtik_amd", "ops", "tunableop",
                                                                          "gfx950_tunableop.csv")
 
@@ -57,7 +61,12 @@ def parse(argv=None):
     ap.add_argument("--model", default="all", choices=["all", "bert-large", "bert-base", "resnet50", "tiny"])
     ap.add_argument("--impl", default="native", choices=["native", "eager"])
     ap.add_argument("--compare-eager", action="store_true",
-                    help="also run the stock-PyTorch baseline of the same config and report the ratio")
+                    help="also run the stock-PyTorch baseline of the same config for the full K / W steps")
+    ap.add_argument("--baseline-steps", type=int, default=5,
+                    help="native runs: after the native halves, time this many steps of the same-config stock "
+                         "PyTorch-ROCm eager step (SURVEY.md section 6 item 3; BASELINE.json publishes no "
+                         "number) and report native / eager as vs_baseline; 0 = skip")
+    ap.add_argument("--baseline-warmup", type=int, default=2)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--batch", type=int, default=0, help="BERT per-GPU batch (default 256)")
     ap.add_argument("--rn-batch", type=int, default=0, help="ResNet-50 per-GPU batch (default 256)")
@@ -72,8 +81,12 @@ def parse(argv=None):
                     help="ResNet-50 gradient bucket (MiB) or auto (measured, else 8 MiB): its 51 MB of "
                          "bf16 gradients would be ONE 64 MiB bucket, all-reduced only after the whole "
                          "backward; 8 MiB gives 7 buckets that overlap the backward of the earlier stages")
-    ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
-                    help="native path: fp32 = bf16 per-backward grads reduced / accumulated in fp32")
+    ap.add_argument("--grad-dtype", default="auto", choices=["auto", "bf16", "fp32"],
+                    help="native path, gradient REDUCTION precision: fp32 = the bf16 per-backward "
+                         "gradients are summed across ranks in fp32 (the reference's DDP all-reduces "
+                         "fp32 gradients, run_pretrain_mlperf.py:688-691); bf16 = summed in bf16 (half "
+                         "the bytes on the wire); auto = fp32 at world size > 1 (at world size 1 nothing "
+                         "is reduced and the optimizer reads the bf16 gradients either way)")
     ap.add_argument("--zero", action="store_true",
                     help="ZeRO-1: reduce-scatter gradients, shard optimizer state, all-gather weights")
     ap.add_argument("--no-dropout", action="store_true")
@@ -188,11 +201,29 @@ def setup_tunableop(mode, rank):
 
 def resolve_bucket_mb(value, world: int, default: float) -> float:
     """``--bucket-mb`` value: a number, or ``auto`` = the bucket measured for this world size
-    (parallel/comm_tuning.py), else ``default``."""
+    (parallel/comm_tuning.py), else ``default``.  ``auto`` reads a per-node file, so the ranks
+    AGREE on rank 0's value before any bucket plan is built: ranks with different plans would
+    issue all-reduces of different sizes (a hang, or gradients summed across parameters)."""
     if str(value).lower() != "auto":
         return float(value)
     from cloudtik_amd.parallel.comm_tuning import bucket_mb
-    return bucket_mb(world, default)
+    mb = float(bucket_mb(world, default))
+    import torch.distributed as dist
+    if world > 1 and dist.is_initialized():
+        vals = [None] * dist.get_world_size()
+        dist.all_gather_object(vals, mb)
+        if len(set(vals)) > 1 and dist.get_rank() == 0:
+            print(f"[bench] note: per-node measured bucket sizes differ {vals}; every rank uses rank 0's "
+                  f"{vals[0]} MiB", file=sys.stderr)
+        mb = float(vals[0])
+    return mb
+
+
+def reduce_fp32(args, world: int) -> bool:
+    """Whether gradients are summed across ranks in fp32 (``--grad-dtype``)."""
+    if args.grad_dtype == "auto":
+        return world > 1
+    return args.grad_dtype == "fp32"
 
 
 def bucket_plan(ddp):
@@ -271,7 +302,7 @@ def build_bert(args, rank, world, device, kind):
                                            total_steps=13700, end_learning_rate=0.0, degree=1.0)
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=resolve_bucket_mb(args.bucket_mb, world, 64.0),
-                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
+                       reduce_dtype=torch.float32 if reduce_fp32(args, world) else None,
                        mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale
     B = args.batch or (256 if kind != "tiny" else 4)
@@ -321,7 +352,7 @@ def build_resnet(args, rank, world, device, kind):
                    no_decay=lambda n: n.endswith("bias") or ".bn" in n or n.startswith("bn"))
     broadcast_flat_params(space)
     ddp = GradBucketer(space, bucket_mb=resolve_bucket_mb(args.rn_bucket_mb, world, 8.0),
-                       reduce_dtype=torch.float32 if args.grad_dtype == "fp32" else None,
+                       reduce_dtype=torch.float32 if reduce_fp32(args, world) else None,
                        mode="reduce_scatter" if args.zero and world > 1 else "all_reduce")
     opt.grad_scale = ddp.grad_scale
     B = args.rn_batch or (256 if not tiny else 4)
@@ -533,7 +564,8 @@ def bucket_timeline(step, bucketer, device):
     try:
         step()
         torch.cuda.synchronize()
-        return [{"bucket": b, "bytes": n, "ms_vs_backward_end": t} for b, n, t in bucketer.timeline()]
+        return [{"bucket": b, "bytes": n, "ms_vs_backward_end": t, "done_ms_vs_backward_end": d,
+                 "host_wait_ms": w} for b, n, t, d, w in bucketer.timeline_full()]
     finally:
         bucketer.trace = False
 
@@ -711,10 +743,23 @@ def main():
     results = []
     for fam, kind in kinds:
         r = run_one(builders[(fam, args.impl)], args, rank, world, device, kind)
-        if args.compare_eager and args.impl == "native":
-            e = run_one(builders[(fam, "eager")], args, rank, world, device, kind)
-            r["eager_value"], r["eager_ms"] = e["value"], e["ms"]
         results.append(r)
+    # the stock-PyTorch baseline AFTER every native half (the native numbers are taken on a
+    # chip that has not yet run anything else); short unless --compare-eager
+    if args.impl == "native" and (args.compare_eager or args.baseline_steps > 0):
+        import copy
+        eargs = copy.copy(args)
+        if not args.compare_eager:
+            eargs.steps, eargs.warmup = args.baseline_steps, args.baseline_warmup
+        for (fam, kind), r in zip(kinds, results):
+            try:
+                e = run_one(builders[(fam, "eager")], eargs, rank, world, device, kind)
+                r["eager_value"], r["eager_ms"], r["eager_steps"] = e["value"], e["ms"], eargs.steps
+            except Exception as ex:  # noqa: BLE001 - the baseline never costs the headline
+                r["eager_error"] = repr(ex)[:300]
+                if rank == 0:
+                    print(f"[bench] eager baseline of {kind} failed: {ex!r}", file=sys.stderr)
+                break
 
     envinfo = environment(device, world)
     if device.type == "cuda" and args.tunableop != "off":
@@ -729,7 +774,9 @@ def main():
         cfg = {"model": head["model"], "global_batch": head["per_gpu_batch"] * world,
                "per_gpu_batch": head["per_gpu_batch"], "parallelism": f"dp{world}",
                "optimizer": head["optimizer"], "impl": head["impl"], "loss_last_step": round(head["loss"], 4),
-               "grad_dtype": args.grad_dtype if head["impl"] == "native" else "fp32 (autocast)",
+               "grad_dtype": ("bf16 grads, " + ("fp32" if reduce_fp32(args, world) else "bf16") + " cross-rank sum"
+                              if world > 1 else "bf16 (nothing reduced at world size 1)")
+               if head["impl"] == "native" else "fp32 (autocast)",
                "zero1": bool(args.zero and world > 1)}
         if "hip_graph" in head:
             cfg["hip_graph"] = head["hip_graph"]
@@ -739,7 +786,9 @@ def main():
         out = {"metric": head["metric"], "value": round(head["value"], 2), "unit": head["unit"],
                "n_gpus": n_dev, "world_size": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(head["ms"], 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": (round(head["value"] / base, 4) if base else None),
+               "vs_baseline": (round(head["value"] / base, 4) if base else
+                               round(head["value"] / head["eager_value"], 4) if head.get("eager_value") else None),
+               "baseline": (BASELINE_DESC if (not base and head.get("eager_value")) else None),
                "dtype": "bf16" if device.type == "cuda" else "fp32",
                "data": "synthetic (one resident random batch per rank, re-used every step; random-init weights)",
                "config": cfg,
@@ -764,7 +813,11 @@ def main():
             out["note"] = f"{world} ranks shared {n_dev} GPU(s): plumbing check, not a scaling point"
         if "eager_value" in head:
             out["eager_value"] = round(head["eager_value"], 2)
+            out["eager_ms_per_step"] = round(head["eager_ms"], 3)
+            out["eager_steps"] = head["eager_steps"]
             out["speedup_vs_eager"] = round(head["value"] / head["eager_value"], 3)
+        if "eager_error" in head:
+            out["eager_error"] = head["eager_error"]
         for r in results[1:]:
             key = "resnet50" if r["model"].startswith("resnet") else r["model"].replace("-", "_")
             out[f"{key}_images_per_sec" if r["unit"] == "images/s" else f"{key}_value"] = round(r["value"], 2)
@@ -790,7 +843,9 @@ def main():
                 out[f"{key}_kernel_audit"] = {k: v for k, v in r["audit"].items() if k != "naive_conv_kernels"}
             if "eager_value" in r:
                 out[f"{key}_eager_value"] = round(r["eager_value"], 2)
+                out[f"{key}_eager_ms_per_step"] = round(r["eager_ms"], 3)
                 out[f"{key}_speedup_vs_eager"] = round(r["value"] / r["eager_value"], 3)
+                out[f"{key}_vs_baseline"] = round(r["value"] / r["eager_value"], 4)
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

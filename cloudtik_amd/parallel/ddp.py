@@ -66,10 +66,10 @@ class GradBucketer:
         self.comm_dtype = comm_dtype
         # small buckets over the one-shot P2P kernel instead of RCCL (opt-in, parallel/p2p.py)
         self.p2p = None
+        self._comm_stream = None
         if self.world > 1 and space.grad.is_cuda and not self.zero:
             from cloudtik_amd.parallel.p2p import from_env
             self.p2p = from_env(group)
-            self._comm_stream = torch.cuda.Stream() if self.p2p is not None else None
         esize = space.grad.element_size()
         cap = max(1, int(bucket_mb * 1024 * 1024 / esize))
         self.buckets: List[tuple] = []
@@ -104,6 +104,8 @@ class GradBucketer:
         # issued and one where backward ended (finish() entry) -> launch times relative to it
         self.trace = False
         self._trace_ev: List = []
+        self._trace_done: List = []
+        self._trace_waits: List[float] = []
         self._trace_end = None
         if self.overlap:
             self._register_hooks()
@@ -173,30 +175,31 @@ class GradBucketer:
             self._side = self.space.grad.is_cuda and any(wgrad_side(p) for p in self.space.params)
         return self._side
 
+    def comm_stream(self):
+        """The stream the collectives are ordered on (CUDA, world > 1), created on first use."""
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(device=self.space.grad.device)
+        return self._comm_stream
+
     def _launch(self, b):
         from cloudtik_amd.ops.linear import grad_stream
         self.space.flush_grads()            # deferred conv-weight grads -> flat buffer
         side = grad_stream() if self._uses_side_stream() else None
-        if self.p2p is not None and self._p2p_fits(b):
-            # the one-shot kernel spins until the slowest rank reaches this bucket: give it
-            # its own stream so weight-gradient GEMMs queued on the side stream (and the
-            # main-stream dgrad chain) never wait behind that spin
-            comm = self._comm_stream
+        if side is not None or (self.p2p is not None and self._p2p_fits(b)):
+            # A stream of its own for the collective, waiting only for the two producers of
+            # this bucket's gradients: the main stream (bias / norm gradients, and the dgrad
+            # chain up to here) and the weight-gradient side stream.  Issued on the side stream
+            # itself (rounds 2-5), the collective's own work -- the one-shot P2P kernel's spin,
+            # gloo's device-to-host copy -- sat in that stream's queue, and the next layers'
+            # weight-gradient GEMMs queued behind it (profiles/r5/gloo_stall.md).
+            comm = self.comm_stream()
             comm.wait_stream(torch.cuda.current_stream())
             if side is not None:
                 comm.wait_stream(side)
             with torch.cuda.stream(comm):
                 self._launch_on_current(b)
             return
-        if side is not None:
-            # weight grads of this bucket were written on the side stream, bias / LayerNorm
-            # grads on the main one: issue the collective from the side stream after it has
-            # caught up with the main stream, so RCCL waits for both
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                self._launch_on_current(b)
-        else:
-            self._launch_on_current(b)
+        self._launch_on_current(b)
 
     def _launch_on_current(self, b):
         if self.trace and self.space.grad.is_cuda:
@@ -282,22 +285,34 @@ class GradBucketer:
             self._launch(self._next)
             self._next += 1
         sync_grad_stream()
-        if self.p2p is not None:
+        if self._comm_stream is not None:
             torch.cuda.current_stream().wait_stream(self._comm_stream)
+        if self.p2p is not None:
             # a barrier that timed out in an earlier (finished) kernel means some rank's
             # gradients were never reduced: fatal, never a silent divergence of the ranks
             self.p2p.check()
         diag = float(os.environ.get("CLOUDTIK_AMD_STEP_PHASES", "0") or 0)
+        timing = bool(diag) or self.trace
         waits = []
-        for w, dst, buf in self._works:
+        cuda = self.space.grad.is_cuda
+        for i, (w, dst, buf) in enumerate(self._works):
             if w is not None:
-                t0 = time.perf_counter() if diag else 0.0
+                t0 = time.perf_counter() if timing else 0.0
                 w.wait()
-                if diag:
-                    waits.append(round((time.perf_counter() - t0) * 1e3, 1))
+                if timing:
+                    waits.append(round((time.perf_counter() - t0) * 1e3, 3))
             if dst is not None:
                 buf.record_stream(torch.cuda.current_stream()) if buf.is_cuda else None
                 dst.copy_(buf)
+            if self.trace and cuda:
+                # the main stream has now waited for buckets 0..i: an event here is when the
+                # last of them finished on the GPU (relative to the end of backward: the
+                # reduction time the backward did NOT hide)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self._trace_done.append(ev)
+        if self.trace:
+            self._trace_waits = waits
         if diag and sum(waits) > diag:
             print(f"[bucket waits ms] {waits} ({len(self.buckets)} buckets)", file=sys.stderr, flush=True)
         self._works.clear()
@@ -313,16 +328,29 @@ class GradBucketer:
     def timeline(self):
         """After a traced step has finished on the GPU: [(bucket, bytes, ms)] -- when each
         bucket's collective was issued relative to the end of backward (negative = it
-        overlapped backward).  Clears the trace."""
+        overlapped backward).  Clears the trace (``timeline_full`` keeps the rest)."""
+        return [(b, n, t) for b, n, t, _, _ in self.timeline_full()]
+
+    def timeline_full(self):
+        """[(bucket, bytes, issued_ms, done_ms, host_wait_ms)]: issue and GPU completion of each
+        bucket's collective relative to the end of backward (done_ms > 0 is reduction time the
+        backward did not hide), and the host time ``finish()`` spent in the bucket's
+        ``wait()`` (near 0 on RCCL, whose wait only orders streams; the device-to-host copy
+        and the TCP transfer on gloo).  Clears the trace."""
         out = []
         if self._trace_end is not None:
             self._trace_end.synchronize()
             esize = 4 if self.fp32 else self.space.grad.element_size()
-            for b, ev in self._trace_ev:
+            for i, (b, ev) in enumerate(self._trace_ev):
                 ev.synchronize()
                 lo, hi, _ = self.buckets[b]
-                out.append((b, (hi - lo) * esize, round(self._trace_end.elapsed_time(ev), 3)))
-        self._trace_ev, self._trace_end = [], None
+                done = self._trace_done[i] if i < len(self._trace_done) else None
+                if done is not None:
+                    done.synchronize()
+                out.append((b, (hi - lo) * esize, round(self._trace_end.elapsed_time(ev), 3),
+                            round(self._trace_end.elapsed_time(done), 3) if done is not None else None,
+                            self._trace_waits[i] if i < len(self._trace_waits) else None))
+        self._trace_ev, self._trace_done, self._trace_waits, self._trace_end = [], [], [], None
         return out
 
     @property
