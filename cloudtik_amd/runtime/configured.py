@@ -444,36 +444,124 @@ class PostgresRuntime(ConfiguredRuntime):
 
 # ----------------------------------------------------------------------------- Prometheus / Grafana
 class PrometheusRuntime(ConfiguredRuntime):
+    """``scrape_scope`` local (default) / workspace / federation and ``service_discovery``
+    file / consul (auto: consul when the cluster runs it), runtime/monitoring_discovery.py.
+    File-based local scrape: the head's ``DiscoverLocalTargets`` pull job keeps
+    ``conf/local-targets.yaml`` current from the live nodes (``pull_services``, default every
+    node's exporter :9100 and training metrics :9500); federation from ``federation_targets``
+    is a static ``conf/federation-targets.yaml``."""
     spec = SPEC_BY_NAME["prometheus"]
     members_env = "PROMETHEUS_MEMBERS"
     quorum_members = False
 
+    @staticmethod
+    def _consul(cfg) -> bool:
+        if "use_consul" in cfg:
+            return bool(cfg["use_consul"])
+        return "consul" in [r.strip() for r in os.environ.get("CLOUDTIK_RUNTIMES", "").split(",")]
+
+    def _plan(self, c):
+        from cloudtik_amd.runtime import monitoring_discovery as MD
+        cfg = c["cfg"]
+        scope, sd = MD.resolve_discovery(cfg, self._consul(cfg))
+        return MD, scope, sd, os.path.join(c["home"], "conf")
+
     def files(self, c):
         import yaml
+        MD, scope, sd, conf_dir = self._plan(c)
         cfg = c["cfg"]
-        nodes = [c["head_ip"]] + [ip for _, ip in c["members"]]
-        scrape = [{"job_name": "cloudtik-nodes", "static_configs": [{"targets": [f"{ip}:9100" for ip in nodes],
-                                                                     "labels": {"cluster": c["cluster"]}}]},
-                  {"job_name": "cloudtik-training", "static_configs": [{"targets": [f"{ip}:9500" for ip in nodes]}]}]
-        for fed in cfg.get("federation_targets") or []:
-            scrape.append({"job_name": f"federate-{fed}", "honor_labels": True, "metrics_path": "/federate",
-                           "params": {"match[]": ['{job=~".+"}']}, "static_configs": [{"targets": [fed]}]})
-        conf = {"global": {"scrape_interval": "15s", "evaluation_interval": "15s"}, "scrape_configs": scrape}
-        return {os.path.join(c["home"], "prometheus.yml"): yaml.safe_dump(conf, sort_keys=False)}
+        consul = cfg.get("consul_address") or f"{c['head_ip']}:8500"
+        workspace = os.environ.get("CLOUDTIK_WORKSPACE", "default")
+        scrape = MD.scrape_configs(scope, sd, conf_dir, c["cluster"], workspace, consul, cfg.get("scrape_services"))
+        conf = {"global": {"scrape_interval": "30s", "evaluation_interval": "15s",
+                           "external_labels": {"monitor": "cloudtik"}}, "scrape_configs": scrape}
+        out = {os.path.join(c["home"], "prometheus.yml"): yaml.safe_dump(conf, sort_keys=False)}
+        if scope == "federation" and sd == "file":
+            out[os.path.join(conf_dir, "federation-targets.yaml")] = yaml.safe_dump(
+                MD.federation_targets_file(cfg.get("federation_targets") or []), sort_keys=False)
+        if self._pulls_local(c, scope, sd):
+            out[os.path.join(c["dir"], "local-targets.json")] = json.dumps(
+                {"interval": cfg.get("pull_interval", 15), "pull_services": cfg.get("pull_services") or
+                 MD.DEFAULT_PULL_SERVICES, "targets_file": os.path.join(conf_dir, "local-targets.yaml"),
+                 "state_address": f"{c['head_ip']}:{os.environ.get('CLOUDTIK_DEFAULT_PORT', '6789')}"}, indent=1)
+        return out
+
+    @staticmethod
+    def _pulls_local(c, scope, sd) -> bool:
+        # the file-based local scrape needs the live-node pull job, on the head (or on every
+        # Prometheus node with high_availability)
+        return sd == "file" and scope in ("local", "federation") and (
+            c["head"] or bool(c["cfg"].get("high_availability")))
+
+    def start_steps(self, head):
+        steps = super().start_steps(head)
+        c = self.ctx(head, self.node_env(head))
+        _, scope, sd, _ = self._plan(c)
+        if self._pulls_local(c, scope, sd):
+            steps.append("cloudtik node service-daemon start prometheus-local-targets "
+                         "--service-class cloudtik_amd.runtime.monitoring_discovery.DiscoverLocalTargets "
+                         f"config_file={os.path.join(c['dir'], 'local-targets.json')}")
+        return steps
+
+    def stop_steps(self, head):
+        return ["cloudtik node service-daemon stop prometheus-local-targets"] + super().stop_steps(head)
 
 
 class GrafanaRuntime(ConfiguredRuntime):
+    """``data_sources_scope`` (reference grafana/utils.py:95-110):
+
+    * ``local`` (default): this cluster's Prometheus as the default data source (provisioned);
+    * ``workspace``: every Prometheus server of the workspace, kept current by the
+      ``DiscoverDataSources`` pull job through the admin API (``data_sources_services``
+      narrows the service selector; needs Consul) -- runtime/monitoring_discovery.py;
+    * ``none``: only the static ``data_sources``."""
     spec = SPEC_BY_NAME["grafana"]
+
+    def _scope(self, cfg) -> str:
+        scope = cfg.get("data_sources_scope") or "local"
+        if scope not in ("none", "local", "workspace"):
+            raise ValueError(f"grafana.data_sources_scope must be none / local / workspace, not {scope!r}")
+        if scope == "workspace" and not PrometheusRuntime._consul(cfg):
+            raise ValueError("grafana.data_sources_scope 'workspace' needs a service discovery runtime (consul)")
+        return scope
 
     def files(self, c):
         import yaml
         cfg = c["cfg"]
-        sources = cfg.get("data_sources") or [{"name": "cloudtik-prometheus", "type": "prometheus",
-                                               "url": f"http://{c['head_ip']}:9090", "isDefault": True}]
+        scope = self._scope(cfg)
+        sources = [dict(s) for s in cfg.get("data_sources") or []]
+        if scope == "local" and not any(s.get("type") == "prometheus" for s in sources):
+            port = int((cfg.get("prometheus") or {}).get("port", 9090))
+            sources.append({"name": "cloudtik-prometheus", "type": "prometheus",
+                            "url": f"http://{c['head_ip']}:{port}", "isDefault": True})
         conf = {"apiVersion": 1, "datasources": [dict({"access": "proxy"}, **s) for s in sources]}
         # $GRAFANA_HOME/conf/provisioning is where a tarball install looks by default
-        return {os.path.join(c["home"], "conf", "provisioning", "datasources", "cloudtik.yaml"):
-                yaml.safe_dump(conf, sort_keys=False)}
+        out = {os.path.join(c["home"], "conf", "provisioning", "datasources", "cloudtik.yaml"):
+               yaml.safe_dump(conf, sort_keys=False)}
+        if scope == "workspace":
+            out[os.path.join(c["dir"], "data-sources.json")] = json.dumps(
+                {"interval": cfg.get("discovery_interval", 15),
+                 "admin_endpoint": f"http://127.0.0.1:{int(cfg.get('port', 3000))}",
+                 "service_selector": cfg.get("data_sources_services") or {},
+                 "consul_address": cfg.get("consul_address") or f"{c['head_ip']}:8500",
+                 "user": cfg.get("admin_user", "cloudtik"), "password": cfg.get("admin_password", "cloudtik")},
+                indent=1)
+        return out
+
+    def start_steps(self, head):
+        steps = super().start_steps(head)
+        c = self.ctx(head, self.node_env(head))
+        if self._scope(c["cfg"]) == "workspace":
+            steps.append("cloudtik node service-daemon start grafana-data-sources "
+                         "--service-class cloudtik_amd.runtime.monitoring_discovery.DiscoverDataSources "
+                         f"config_file={os.path.join(c['dir'], 'data-sources.json')}")
+        return steps
+
+    def stop_steps(self, head):
+        steps = []
+        if (self.runtime_config or {}).get("data_sources_scope") == "workspace":
+            steps.append("cloudtik node service-daemon stop grafana-data-sources")
+        return steps + super().stop_steps(head)
 
 
 # ----------------------------------------------------------------------------- HAProxy

@@ -43,8 +43,10 @@ RUNTIMES: Dict[str, Dict[str, Any]] = {
                           security="b", password="s", snapshot_repository="b", clustering="o"),
     "etcd": dict(port="port", peer_port="port"),
     "flink": dict(_METASTORE, config="o"),
-    "grafana": dict(port="port", high_availability="b", data_sources_scope="s", data_sources="a",
-                    data_sources_services="sel"),
+    "grafana": dict(port="port", high_availability="b",
+                    data_sources_scope={"enum": ["none", "local", "workspace"]}, data_sources="a",
+                    data_sources_services="sel", discovery_interval="i", consul_address="s", admin_user="s",
+                    admin_password="s"),
     "hadoop": dict(_sd("hdfs"), **_sd("minio"), hadoop_default_cluster="b", hdfs_namenode_uri="s",
                    minio_endpoint_uri="s", minio_storage="o", default_storage="s"),               # + default_storage
     "haproxy": dict(port="port", protocol="s", app_mode="s", high_availability="b", backend="o"),
@@ -72,8 +74,10 @@ RUNTIMES: Dict[str, Dict[str, Any]] = {
                      replication_slot="b", health_check_port="port", replication_synchronous="o", database="o",
                      repmgr="o"),
     "presto": dict(_METASTORE, config="o", catalogs="o"),
-    "prometheus": dict(port="port", high_availability="b", scrape_scope="s", scrape_services="sel",
-                       federation_targets="a"),
+    "prometheus": dict(port="port", high_availability="b",
+                       scrape_scope={"enum": ["local", "workspace", "federation"]}, scrape_services="sel",
+                       service_discovery={"enum": ["file", "consul"]}, federation_targets="a",
+                       pull_services="o", pull_interval="i", consul_address="s", use_consul="b"),
     "ray": dict(scaling="o"),
     "redis": dict(port="port", cluster_mode={"enum": ["none", "replication", "sharding"]}, password="s",
                   health_check_port="port", replication="o", sharding="o"),

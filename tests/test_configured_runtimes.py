@@ -120,11 +120,13 @@ def test_databases_and_observability(tmp_path, monkeypatch):
     p = FakeProvider()
     penv = rf.get_runtime("prometheus", {}).with_environment_variables({"runtime": {}}, p, "h")
     penv.update(CLOUDTIK_HEAD_IP="10.0.0.1")
-    prom = yaml.safe_load(_render("prometheus", {"federation_targets": ["10.9.0.1:9090"]}, penv, head=True,
-                                  monkeypatch=monkeypatch, tmp_path=tmp_path)["prometheus/prometheus.yml"])
-    targets = prom["scrape_configs"][0]["static_configs"][0]["targets"]
-    assert targets == ["10.0.0.1:9100", "10.0.0.12:9100", "10.0.0.13:9100", "10.0.0.14:9100", "10.0.0.19:9100"]
+    pf = _render("prometheus", {"scrape_scope": "federation", "federation_targets": ["10.9.0.1:9090"]}, penv,
+                 head=True, monkeypatch=monkeypatch, tmp_path=tmp_path)
+    prom = yaml.safe_load(pf["prometheus/prometheus.yml"])
+    # this cluster from the live-node targets file (no consul), the others through /federate
+    assert prom["scrape_configs"][0]["file_sd_configs"][0]["files"][0].endswith("conf/local-*targets.yaml")
     assert prom["scrape_configs"][-1]["metrics_path"] == "/federate"
+    assert yaml.safe_load(pf["prometheus/conf/federation-targets.yaml"])[0]["targets"] == ["10.9.0.1:9090"]
     graf = yaml.safe_load(_render("grafana", {}, {"CLOUDTIK_HEAD_IP": "10.0.0.1"}, head=True, monkeypatch=monkeypatch,
                                   tmp_path=tmp_path)["grafana/conf/provisioning/datasources/cloudtik.yaml"])
     assert graf["datasources"][0]["url"] == "http://10.0.0.1:9090"
