@@ -434,44 +434,156 @@ class BindRuntime(ConfiguredRuntime):
 
 
 # ----------------------------------------------------------------------------- Postgres poolers
-class PgBouncerRuntime(ConfiguredRuntime):
+def _cluster_runtimes() -> List[str]:
+    return [r.strip() for r in os.environ.get("CLOUDTIK_RUNTIMES", "").split(",") if r.strip()]
+
+
+class _PoolerRuntime(ConfiguredRuntime):
+    """``backend.config_mode`` static / local / dynamic (runtime/pooler_discovery.py): dynamic
+    starts a service daemon that rewrites the pooler's backends from the discovered Postgres
+    services and reloads it."""
+
+    static_key = "databases"
+    discovery_class = ""
+    conf_name = ""
+
+    def _backend(self, cfg) -> Dict[str, Any]:
+        return dict(cfg.get("backend") or {})
+
+    def mode(self, cfg) -> str:
+        from cloudtik_amd.runtime.pooler_discovery import resolve_config_mode
+        b = self._backend(cfg)
+        if self.static_key == "databases" and cfg.get("databases") and "databases" not in b:
+            b["databases"] = cfg["databases"]            # the older top-level form
+        return resolve_config_mode(b, _cluster_runtimes(), self.static_key)
+
+    def discovery_files(self, c) -> Dict[str, str]:
+        cfg = c["cfg"]
+        if self.mode(cfg) != "dynamic":
+            return {}
+        b = self._backend(cfg)
+        d = {"interval": b.get("interval", 15), "service_selector": b.get("service_selector") or {},
+             "consul_address": b.get("consul_address") or f"{c['head_ip']}:8500",
+             "conf_path": os.path.join(c["dir"], self.conf_name)}
+        if b.get("reload_cmd"):
+            d["reload_cmd"] = b["reload_cmd"]
+        d.update(self.extra_discovery(c))
+        return {os.path.join(c["dir"], "discovery.json"): json.dumps(d, indent=1)}
+
+    def extra_discovery(self, c) -> Dict[str, Any]:
+        return {}
+
+    def start_steps(self, head):
+        steps = super().start_steps(head)
+        c = self.ctx(head, self.node_env(head))
+        if self.mode(c["cfg"]) == "dynamic":
+            steps.append(f"cloudtik node service-daemon start {self.name}-discovery "
+                         f"--service-class cloudtik_amd.runtime.pooler_discovery.{self.discovery_class} "
+                         f"config_file={os.path.join(c['dir'], 'discovery.json')}")
+        return steps
+
+    def stop_steps(self, head):
+        steps = []
+        if self.mode(self.runtime_config or {}) == "dynamic":
+            steps.append(f"cloudtik node service-daemon stop {self.name}-discovery")
+        return steps + super().stop_steps(head)
+
+
+class PgBouncerRuntime(_PoolerRuntime):
+    """PgBouncer in front of Postgres.  static: ``backend.databases`` ({name: {host, port,
+    dbname, user, ...}} or ready ``host=.. port=..`` strings); local: every database of this
+    cluster's Postgres (head); dynamic: one entry per discovered Postgres service
+    (``DiscoverPgBouncerBackends``; ``backend.database`` gives the user / dbname / auth_user of
+    those entries)."""
     spec = SPEC_BY_NAME["pgbouncer"]
+    discovery_class = "DiscoverPgBouncerBackends"
+    conf_name = "pgbouncer.ini"
+
+    def _static_databases(self, cfg) -> Dict[str, Any]:
+        b = self._backend(cfg)
+        return dict(b.get("databases") or cfg.get("databases") or {})
 
     def files(self, c):
+        from cloudtik_amd.runtime.pooler_discovery import pgbouncer_ini
         cfg = c["cfg"]
-        host = cfg.get("postgres_host") or c["head_ip"]
-        dbs = cfg.get("databases") or {"*": f"host={host} port={int(cfg.get('postgres_port', 5432))}"}
-        text = "[databases]\n" + "".join(f"{k} = {v}\n" for k, v in dbs.items()) + (
-            "[pgbouncer]\nlisten_addr = 0.0.0.0\nlisten_port = 6432\nauth_type = md5\n"
-            "auth_file = /etc/pgbouncer/userlist.txt\n"
-            f"pool_mode = {cfg.get('pool_mode', 'transaction')}\n"
-            f"max_client_conn = {int(cfg.get('max_client_conn', 1000))}\n"
-            f"default_pool_size = {int(cfg.get('default_pool_size', 20))}\n")
-        return {os.path.join(c["dir"], "pgbouncer.ini"): text}
+        mode = self.mode(cfg)
+        pool = cfg.get("pool") or {}
+        if mode == "static":
+            dbs = self._static_databases(cfg)
+        elif mode == "local":
+            host = cfg.get("postgres_host") or c["head_ip"]
+            dbs = {"*": f"host={host} port={int(cfg.get('postgres_port', 5432))}"}
+        else:
+            dbs = self._static_databases(cfg)        # the job adds the discovered ones
+        settings = {"listen_addr": "0.0.0.0", "listen_port": int(cfg.get("port", 6432)), "auth_type": "md5",
+                    "auth_file": "/etc/pgbouncer/userlist.txt",
+                    "admin_users": cfg.get("admin_user", "cloudtik"),
+                    "pool_mode": pool.get("pool_mode", cfg.get("pool_mode", "transaction")),
+                    "max_client_conn": int(pool.get("max_client_conn", cfg.get("max_client_conn", 1000))),
+                    "default_pool_size": int(pool.get("default_pool_size", cfg.get("default_pool_size", 20))),
+                    "pidfile": os.path.join(c["dir"], "pgbouncer.pid")}
+        out = {os.path.join(c["dir"], "pgbouncer.ini"): pgbouncer_ini(dbs, settings)}
+        out.update(self.discovery_files(c))
+        return out
+
+    def extra_discovery(self, c):
+        cfg = c["cfg"]
+        b = self._backend(cfg)
+        return {"database": b.get("database") or {}, "static_databases": self._static_databases(cfg),
+                "reload_cmd": b.get("reload_cmd") or
+                f"([ -d /etc/pgbouncer ] && sudo cp {os.path.join(c['dir'], 'pgbouncer.ini')} /etc/pgbouncer/ || true) "
+                f"&& (kill -HUP $(cat {os.path.join(c['dir'], 'pgbouncer.pid')}) 2>/dev/null || "
+                "sudo systemctl reload pgbouncer)"}
 
     def configure_steps(self, head):
         return ["[ -d /etc/pgbouncer ] && sudo cp $RUNTIME_PATH/pgbouncer/pgbouncer.ini /etc/pgbouncer/ || true"]
 
 
-class PgpoolRuntime(ConfiguredRuntime):
-    """pgpool-II over the Postgres primary (head) and the replicas (workers): load-balanced
-    reads, streaming-replication mode."""
+class PgpoolRuntime(_PoolerRuntime):
+    """pgpool-II, streaming-replication mode with load-balanced reads.  static:
+    ``backend.servers`` (the first is the primary); local: this cluster's Postgres primary
+    (head) and replicas (workers); dynamic: the discovered Postgres servers, new ones appended
+    as backends by ``DiscoverPgpoolBackends`` and pgpool reloaded."""
 
     spec = SPEC_BY_NAME["pgpool"]
     members_env = "PGPOOL_BACKENDS"
     quorum_members = False
+    static_key = "servers"
+    discovery_class = "DiscoverPgpoolBackends"
+    conf_name = "pgpool.conf"
 
     def files(self, c):
+        from cloudtik_amd.runtime.pooler_discovery import pgpool_backend_lines
         cfg = c["cfg"]
-        backends = [c["head_ip"]] + [ip for _, ip in c["members"]]
-        lines = ["listen_addresses = '*'", "port = 6432", "backend_clustering_mode = 'streaming_replication'",
-                 "load_balance_mode = on", f"num_init_children = {int(cfg.get('num_init_children', 32))}",
-                 "sr_check_period = 10", f"sr_check_user = '{cfg.get('user', 'cloudtik')}'"]
-        for i, ip in enumerate(backends):
-            lines += [f"backend_hostname{i} = '{ip}'", f"backend_port{i} = 5432",
-                      f"backend_weight{i} = {0 if i == 0 and cfg.get('primary_no_reads') else 1}",
-                      f"backend_flag{i} = '{'ALWAYS_PRIMARY' if i == 0 else 'ALLOW_TO_FAILOVER'}'"]
-        return {os.path.join(c["dir"], "pgpool.conf"): "\n".join(lines) + "\n"}
+        mode = self.mode(cfg)
+        if mode == "static":
+            backends = []
+            for srv in self._backend(cfg)["servers"]:
+                h, _, p = str(srv).rpartition(":") if ":" in str(srv) else (str(srv), "", "5432")
+                backends.append((h, int(p or 5432)))
+        elif mode == "local":
+            backends = [(ip, 5432) for ip in [c["head_ip"]] + [ip for _, ip in c["members"]]]
+        else:
+            backends = []                            # filled by the discovery job
+        lines = ["listen_addresses = '*'", f"port = {int(cfg.get('port', 6432))}",
+                 "backend_clustering_mode = 'streaming_replication'", "load_balance_mode = on",
+                 f"num_init_children = {int(cfg.get('num_init_children', 32))}",
+                 f"max_pool = {int(cfg.get('max_pool', 4))}", "sr_check_period = 10",
+                 f"sr_check_user = '{cfg.get('user', 'cloudtik')}'", "health_check_period = 10",
+                 f"health_check_user = '{cfg.get('user', 'cloudtik')}'"]
+        for i, (ip, port) in enumerate(backends):
+            primary = i == 0 and mode != "dynamic"
+            lines += pgpool_backend_lines(i, ip, port, 0 if primary and cfg.get("primary_no_reads") else 1,
+                                          "ALWAYS_PRIMARY" if primary else "ALLOW_TO_FAILOVER")
+        out = {os.path.join(c["dir"], "pgpool.conf"): "\n".join(lines) + "\n"}
+        out.update(self.discovery_files(c))
+        return out
+
+    def extra_discovery(self, c):
+        b = self._backend(c["cfg"])
+        return {"reload_cmd": b.get("reload_cmd") or
+                f"([ -d /etc/pgpool2 ] && sudo cp {os.path.join(c['dir'], 'pgpool.conf')} /etc/pgpool2/pgpool.conf "
+                "|| true) && sudo pgpool reload"}
 
     def configure_steps(self, head):
         return ["[ -d /etc/pgpool2 ] && sudo cp $RUNTIME_PATH/pgpool/pgpool.conf /etc/pgpool2/pgpool.conf || true"]
