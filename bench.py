@@ -62,10 +62,12 @@ def parse(argv=None):
     ap.add_argument("--impl", default="native", choices=["native", "eager"])
     ap.add_argument("--compare-eager", action="store_true",
                     help="also run the stock-PyTorch baseline of the same config for the full K / W steps")
-    ap.add_argument("--baseline-steps", type=int, default=5,
+    ap.add_argument("--baseline-steps", type=int, default=-1,
                     help="native runs: after the native halves, time this many steps of the same-config stock "
                          "PyTorch-ROCm eager step (SURVEY.md section 6 item 3; BASELINE.json publishes no "
-                         "number) and report native / eager as vs_baseline; 0 = skip")
+                         "number) and report native / eager as vs_baseline; 0 = skip; -1 (default) = 5 at "
+                         "world size 1, skipped above (a stock-DDP failure on one rank would leave the others "
+                         "in a collective: the scaling runs never risk it)")
     ap.add_argument("--baseline-warmup", type=int, default=2)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
     ap.add_argument("--batch", type=int, default=0, help="BERT per-GPU batch (default 256)")
@@ -746,11 +748,12 @@ def main():
         results.append(r)
     # the stock-PyTorch baseline AFTER every native half (the native numbers are taken on a
     # chip that has not yet run anything else); short unless --compare-eager
-    if args.impl == "native" and (args.compare_eager or args.baseline_steps > 0):
+    base_steps = args.baseline_steps if args.baseline_steps >= 0 else (5 if world == 1 else 0)
+    if args.impl == "native" and (args.compare_eager or base_steps > 0):
         import copy
         eargs = copy.copy(args)
         if not args.compare_eager:
-            eargs.steps, eargs.warmup = args.baseline_steps, args.baseline_warmup
+            eargs.steps, eargs.warmup = base_steps, args.baseline_warmup
         for (fam, kind), r in zip(kinds, results):
             try:
                 e = run_one(builders[(fam, "eager")], eargs, rank, world, device, kind)
