@@ -93,7 +93,9 @@ def _worker(rank, port, kind, out):
                 opt.zero_grad()
                 losses.append(float(loss.detach()))
             ddp.remove()
-            res["fp32" if fp32 else "bf16"] = (g, losses)
+            # numpy, not a tensor: a tensor put on the queue is shared by file descriptor and
+            # the worker may be gone by the time the parent reads it
+            res["fp32" if fp32 else "bf16"] = (g.numpy(), losses)
         if rank == 0:
             out.put(res)
     finally:
@@ -117,6 +119,7 @@ def test_bf16_vs_fp32_gradient_reduction_at_world_8(kind):
         assert p.exitcode == 0
     g16, l16 = res["bf16"]
     g32, l32 = res["fp32"]
+    g16, g32 = torch.from_numpy(g16), torch.from_numpy(g32)
     rel = float((g16 - g32).norm() / g32.norm())
     assert rel <= 1e-2, rel
     # the trajectories: same start, then every step's loss within 2 % of the starting loss of
