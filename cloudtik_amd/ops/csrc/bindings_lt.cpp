@@ -353,6 +353,31 @@ bool gemm_nt_stream(at::Tensor A, at::Tensor B, at::Tensor D, c10::optional<at::
   return rc == 0;
 }
 
+extern "C" int ct_gemm_pp(const void*, long, const void*, long, void*, long, int, int, int, int, const void*, void*,
+                          long, int, int, hipStream_t);
+
+// Paired-tile persistent MFMA GEMM (gemm_pp.hip): D = A @ B^T with epilogue 0 (plain), 5 (+ bias)
+// or 6 (D = gelu(. + bias), aux = gelu'(. + bias)).  False when the shape is unsupported.
+bool gemm_pp(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> aux, int64_t wgs, int64_t eslots) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "gemm_pp: GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+              D.scalar_type() == at::kBFloat16, "gemm_pp: bf16 operands");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "gemm_pp: 2-D row-major operands");
+  const long M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && D.size(0) == M && D.size(1) == N, "gemm_pp: shape mismatch");
+  const bool hb = bias.has_value() && bias->defined();
+  const bool ha = aux.has_value() && aux->defined();
+  if (hb) TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                      "gemm_pp: bias");
+  if (ha) TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && rowmajor_ok(*aux) && aux->size(0) == M &&
+                      aux->size(1) == N, "gemm_pp: aux");
+  int rc = ct_gemm_pp(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0), (int)M, (int)N,
+                      (int)K, (int)epi, hb ? bias->data_ptr() : nullptr, ha ? aux->data_ptr() : nullptr,
+                      ha ? aux->stride(0) : 0, (int)wgs, (int)eslots, at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
 extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, float*,
                            hipStream_t);
 
@@ -396,6 +421,10 @@ void register_lt(pybind11::module& m) {
   m.def("gemm_nt_stream", &gemm_nt_stream, "streamed persistent MFMA GEMM A @ B^T / A @ B (+ bias)",
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("D"), pybind11::arg("bias") = pybind11::none(), pybind11::arg("b_kn") = false,
         pybind11::arg("wgs") = 0, pybind11::arg("accumulate") = false);
+  m.def("gemm_pp", &gemm_pp, "paired-tile persistent MFMA GEMM A @ B^T (epilogue of one tile beside another's K loop)",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("D"), pybind11::arg("epi") = 0,
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("aux") = pybind11::none(), pybind11::arg("wgs") = 0,
+        pybind11::arg("eslots") = 4);
   m.def("gemm_nn", &gemm_nn, "hand-written MFMA GEMM A @ B (B stored [K, N]) with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
   m.def("lt_bmm_tuned", &lt_bmm_tuned, "strided-batched hipBLASLt GEMM, algorithm picked by timing all solutions");
