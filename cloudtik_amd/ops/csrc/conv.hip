@@ -1166,7 +1166,8 @@ extern "C" int ct_conv_igemm_rows(int cfg, int Co, int M, int KT) {
   // to hide LDS and memory latency) beat the 4-wave ones on every Co % 128 == 0 shape: one-tile
   // below 400000 rows (l3.c2 fwd 77 -> 73 us, l4.c2s2 dgrad 127 -> 116), streamed above
   // (l1.c3 fwd 115 -> 112; profiles/r4/conv_cfg_8wave.md).  CLOUDTIK_AMD_CONV_RULE=1: the rule
-  // before that.
+  // before that.  r6: the 256 x 128 16-wave tiles (cfg 18), fastest alone on several layer-3/4
+  // shapes, cost 1 ms in the step (20.45 -> 21.5 ms, profiles/r6/conv_cfg_probe.md): rejected.
   static const int rule = [] {
     const char* e = std::getenv("CLOUDTIK_AMD_CONV_RULE");
     return e ? std::atoi(e) : 2;
