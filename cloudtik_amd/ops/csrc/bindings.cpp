@@ -15,6 +15,9 @@ int ct_layernorm_bwd_grid(int M, int N);
 int ct_layernorm_bwd(const void*, const void*, const void*, const float*, const float*,
                      const void*, void*, void*, float*, void*, void*, void*, int, int, int, int,
                      int, float, uint64_t, uint64_t, hipStream_t);
+int ct_layernorm_bwd2(const void*, const void*, const void*, const float*, const float*,
+                      const void*, void*, void*, float*, void*, void*, void*, int, int, int, int,
+                      int, float, uint64_t, uint64_t, int, const void*, hipStream_t);
 int ct_colsum(const float*, void*, int, int, int, int, hipStream_t);
 int ct_bias_act_fwd(const void*, const void*, void*, long, int, int, hipStream_t);
 int ct_bias_act_bwd_grid(long M);
@@ -99,7 +102,7 @@ static inline int dt_code(const at::Tensor& t) {
 std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> bias,
                                       c10::optional<at::Tensor> res, at::Tensor gamma,
                                       c10::optional<at::Tensor> beta, double eps, bool rms,
-                                      double p_drop, int64_t seed, int64_t offset) {
+                                      double p_drop, int64_t seed, int64_t offset, bool keep_sum) {
   CHECK_IN(x); CHECK_BF16(x); CHECK_IN(gamma); CHECK_BF16(gamma);
   const int N = x.size(-1);
   const int M = x.numel() / N;
@@ -108,7 +111,9 @@ std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> bi
   if (res.has_value() && res->defined()) { CHECK_IN(*res); CHECK_BF16(*res); TORCH_CHECK(res->numel() == x.numel()); }
   if (beta.has_value() && beta->defined()) { CHECK_IN(*beta); CHECK_BF16(*beta); TORCH_CHECK(beta->numel() == N); }
   auto y = at::empty_like(x);
-  const bool need_s = optr(bias) || optr(res) || p_drop > 0.0;
+  // keep_sum = false: the caller's backward runs from y (layernorm_bwd_into from_y), so the
+  // normalised input sum s is not written
+  const bool need_s = keep_sum && (optr(bias) || optr(res) || p_drop > 0.0);
   at::Tensor s = need_s ? at::empty_like(x) : at::Tensor();
   auto fo = x.options().dtype(at::kFloat);
   auto mean = at::empty({M}, fo);
@@ -155,7 +160,8 @@ std::vector<at::Tensor> layernorm_bwd_into(at::Tensor dy, at::Tensor s, at::Tens
                                            at::Tensor mean, at::Tensor rstd, bool rms,
                                            at::Tensor dgamma, c10::optional<at::Tensor> dbeta,
                                            c10::optional<at::Tensor> dbias, bool need_dx,
-                                           double p_drop, int64_t seed, int64_t offset) {
+                                           double p_drop, int64_t seed, int64_t offset,
+                                           c10::optional<at::Tensor> beta_y) {
   CHECK_IN(dy); CHECK_BF16(dy); CHECK_IN(s); CHECK_BF16(s); CHECK_IN(gamma); CHECK_IN(dgamma);
   const int N = s.size(-1);
   const int M = s.numel() / N;
@@ -166,12 +172,15 @@ std::vector<at::Tensor> layernorm_bwd_into(at::Tensor dy, at::Tensor s, at::Tens
   at::Tensor dx = need_dx ? at::empty_like(s) : at::Tensor();
   const int grid = ct_layernorm_bwd_grid(M, N);
   auto part = at::empty({3 * (long)grid * N}, s.options().dtype(at::kFloat));
-  int rc = ct_layernorm_bwd(dy.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
-                            rstd.data_ptr<float>(), nullptr, ds.data_ptr(),
-                            need_dx ? dx.data_ptr() : nullptr, part.data_ptr<float>(),
-                            dgamma.data_ptr(), optr_mut(dbeta), optr_mut(dbias), M, N, rms ? 1 : 0,
-                            dgamma.scalar_type() == at::kFloat ? 1 : 0, 1, (float)p_drop,
-                            (uint64_t)seed, (uint64_t)offset, cur_stream());
+  // beta_y given: s is the forward's OUTPUT y (its keep_sum = false form), xhat = (y - beta) / gamma
+  const bool from_y = beta_y.has_value() && beta_y->defined();
+  if (from_y) { CHECK_IN(*beta_y); CHECK_BF16(*beta_y); CHECK_BF16(gamma); TORCH_CHECK(beta_y->numel() == N && !rms); }
+  int rc = ct_layernorm_bwd2(dy.data_ptr(), s.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+                             rstd.data_ptr<float>(), nullptr, ds.data_ptr(),
+                             need_dx ? dx.data_ptr() : nullptr, part.data_ptr<float>(),
+                             dgamma.data_ptr(), optr_mut(dbeta), optr_mut(dbias), M, N, rms ? 1 : 0,
+                             dgamma.scalar_type() == at::kFloat ? 1 : 0, 1, (float)p_drop,
+                             (uint64_t)seed, (uint64_t)offset, from_y ? 1 : 0, optr(beta_y), cur_stream());
   TORCH_CHECK(rc == 0, "layernorm_bwd_into: unsupported shape N=", N);
   return {ds, dx};
 }
@@ -828,12 +837,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_train_given2", &bn_fwd_train_given2);
   m.def("bn_bwd_given_pair", &bn_bwd_given_pair);
   m.def("maxpool3s2_bwd_bn_rows", [](int64_t N, int64_t H) { return (int64_t)ct_maxpool3s2_bwd_bn_rows((int)N, (int)H); });
-  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_fwd", &layernorm_fwd, pybind11::arg("x"), pybind11::arg("bias"), pybind11::arg("res"),
+        pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"), pybind11::arg("rms"),
+        pybind11::arg("p_drop"), pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("keep_sum") = true);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("bias_act_bwd_into", &bias_act_bwd_into);
-  m.def("layernorm_bwd_into", &layernorm_bwd_into);
+  m.def("layernorm_bwd_into", &layernorm_bwd_into, pybind11::arg("dy"), pybind11::arg("s"), pybind11::arg("gamma"),
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("rms"), pybind11::arg("dgamma"),
+        pybind11::arg("dbeta"), pybind11::arg("dbias"), pybind11::arg("need_dx"), pybind11::arg("p_drop"),
+        pybind11::arg("seed"), pybind11::arg("offset"), pybind11::arg("beta_y") = pybind11::none());
   m.def("dropout_fwd", &dropout_fwd);
   m.def("embed3_fwd", &embed3_fwd);
   m.def("embed3_bwd", &embed3_bwd);

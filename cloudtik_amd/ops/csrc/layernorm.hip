@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwdArgs a) {
 
 struct LnBwdArgs {
   const bf16_t* dy; const bf16_t* s; const bf16_t* gamma; const float* mean; const float* rstd;
+  const bf16_t* beta;    // FROMY: s holds the forward's OUTPUT y; xhat = (y - beta) / gamma
   const bf16_t* dextra;  // optional extra gradient added to ds (e.g. a skip path)
   bf16_t* ds;            // grad wrt s (= grad of the residual input)
   bf16_t* dx;            // grad wrt x (after dropout backward); may alias nothing / be null
@@ -116,8 +117,12 @@ struct LnBwdArgs {
 // and adds per row, a third fewer partials
 // 3 waves / SIMD up to N = 1024 (MAXV 2); wider rows (N <= 2048) keep more registers at 2
 // (1 with the bias gradient) -- at 3 they spilled 20-550 VGPRs
-template <int MAXV, bool RMS, bool EXTRA, bool DBIAS>
-__global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_kernel(LnBwdArgs a) {
+// FROMY: the backward from the forward's output instead of its input (the "memory-efficient"
+// LayerNorm): xhat = (y - beta) / gamma.  The forward then writes no copy of its input sum s --
+// y is kept anyway (the next layer's input) -- a quarter of the forward's HBM bytes.  A channel
+// whose gamma is exactly 0 gets xhat 0 (its y carries no information about x).
+template <int MAXV, bool RMS, bool EXTRA, bool DBIAS, bool FROMY = false>
+__global__ __launch_bounds__(256, MAXV <= 2 ? ((FROMY && DBIAS) ? 2 : 3) : (DBIAS ? 1 : 2)) void ln_bwd_kernel(LnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][512];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
@@ -126,6 +131,18 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_k
   constexpr bool want_dbias = DBIAS;
   float dg[MAXV][8], db[MAXV][8], dbi[DBIAS ? MAXV : 1][8];
   u16x8 gb[MAXV];                    // gamma kept packed (bf16): 4 VGPRs per 8 columns
+  // FROMY: beta (bf16) and 1 / gamma (fp32, 0 where gamma is 0) per column in LDS, read per
+  // element -- in registers they pushed the kernel into spills at 3 waves / SIMD
+  __shared__ __attribute__((aligned(16))) unsigned short ybeta[FROMY ? 2048 : 8];
+  __shared__ __attribute__((aligned(16))) float yrg[FROMY ? 2048 : 4];
+  if constexpr (FROMY) {
+    for (int c = threadIdx.x; c < N; c += blockDim.x) {
+      ybeta[c] = a.beta[c];
+      const float gf = bf2f(a.gamma[c]);
+      yrg[c] = gf != 0.f ? 1.f / gf : 0.f;
+    }
+    __syncthreads();
+  }
   const u16x8* g8 = reinterpret_cast<const u16x8*>(a.gamma);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
@@ -152,7 +169,7 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_k
       ndv[i] = c < nvec ? dyr[c] : u16x8(0);
       if (EXTRA) nev[i] = c < nvec ? reinterpret_cast<const u16x8*>(a.dextra + (size_t)r * N)[c] : u16x8(0);
     }
-    nmean = RMS ? 0.f : a.mean[r];
+    nmean = (RMS || FROMY) ? 0.f : a.mean[r];
     nrstd = a.rstd[r];
   };
   prefetch(row);
@@ -171,13 +188,21 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_k
       if (c < nvec) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float xhat = (bf2f(csv[i][j]) - mean) * rstd;
           const float d = bf2f(cdv[i][j]);
           const float dgv = d * bf2f(gb[i][j]);
-          dg[i][j] += d * xhat;
           db[i][j] += d;
           s1 += dgv;
-          s2 += dgv * xhat;
+          if constexpr (FROMY) {
+            // u = y - beta = gamma * xhat: dy * gamma * xhat = dy * u needs no division, and the
+            // dgamma partials (sums of dy * u) are divided by gamma once, when written
+            const float u = bf2f(csv[i][j]) - bf2f(ybeta[8 * c + j]);
+            dg[i][j] += d * u;
+            s2 += d * u;
+          } else {
+            const float xhat = (bf2f(csv[i][j]) - mean) * rstd;
+            dg[i][j] += d * xhat;
+            s2 += dgv * xhat;
+          }
         }
       }
     }
@@ -193,7 +218,9 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_k
         u16x8 o, od;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float xhat = (bf2f(csv[i][j]) - mean) * rstd;
+          // FROMY: beta and 1 / gamma read per element (wider LDS reads held 12 more VGPRs)
+          const float xhat = FROMY ? (bf2f(csv[i][j]) - bf2f(ybeta[8 * c + j])) * yrg[8 * c + j]
+                                   : (bf2f(csv[i][j]) - mean) * rstd;
           const float dgv = bf2f(cdv[i][j]) * bf2f(gb[i][j]);
           float t = RMS ? rstd * (dgv - xhat * s2) : rstd * (dgv - s1 - xhat * s2);
           t += bf2f(ev[j]);
@@ -238,6 +265,7 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? 3 : (DBIAS ? 1 : 2)) void ln_bwd_k
         const int idx = cl * 8 + 4 * ((j >> 2) ^ ((cl >> 2) & 1)) + (j & 3);
         float t = 0.f;
         for (int w = 0; w < wpb; ++w) t += red[w][idx];
+        if (FROMY && pass == 0) t *= yrg[base + col];   // sums of dy * gamma * xhat -> of dy * xhat
         if (dst) dst[(size_t)blockIdx.x * N + base + col] = t;
       }
       __syncthreads();
@@ -370,14 +398,18 @@ extern "C" int ct_layernorm_bwd_grid(int M, int N) {
 }
 
 // Workspace: part = float[3 * grid * N] (grid = ct_layernorm_bwd_grid(M, N)).
-extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, const float* mean,
-                                const float* rstd, const void* dextra, void* ds, void* dx,
-                                float* part, void* dgamma, void* dbeta, void* dbias, int M, int N,
-                                int rms, int param_fp32, int accumulate, float p_drop,
-                                uint64_t seed, uint64_t offset, hipStream_t stream) {
+// from_y: `s` is the forward's output y and `beta` its beta (xhat = (y - beta) / gamma; mean unused)
+extern "C" int ct_layernorm_bwd2(const void* dy, const void* s, const void* g, const float* mean,
+                                 const float* rstd, const void* dextra, void* ds, void* dx,
+                                 float* part, void* dgamma, void* dbeta, void* dbias, int M, int N,
+                                 int rms, int param_fp32, int accumulate, float p_drop,
+                                 uint64_t seed, uint64_t offset, int from_y, const void* beta,
+                                 hipStream_t stream) {
   if (N % 8 != 0 || N > 2048 || M <= 0) return -1;
+  if (from_y && (rms || !beta)) return -2;        // the output form: LayerNorm with beta only
   const int grid = ct_layernorm_bwd_grid(M, N);
   LnBwdArgs a;
+  a.beta = (const bf16_t*)beta;
   a.dy = (const bf16_t*)dy; a.s = (const bf16_t*)s; a.gamma = (const bf16_t*)g; a.mean = mean;
   a.rstd = rstd; a.dextra = (const bf16_t*)dextra; a.ds = (bf16_t*)ds; a.dx = (bf16_t*)dx;
   a.dg_part = part; a.db_part = (rms || !dbeta) ? nullptr : part + (size_t)grid * N;
@@ -390,6 +422,8 @@ extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, co
 #define CT_LNB2(MV, DB)                                                                       \
     if (rms) { if (a.dextra) ln_bwd_kernel<MV, true, true, DB><<<grid, 256, 0, stream>>>(a);       \
                else ln_bwd_kernel<MV, true, false, DB><<<grid, 256, 0, stream>>>(a); }               \
+    else if (from_y) { if (a.dextra) ln_bwd_kernel<MV, false, true, DB, true><<<grid, 256, 0, stream>>>(a); \
+           else ln_bwd_kernel<MV, false, false, DB, true><<<grid, 256, 0, stream>>>(a); }            \
     else { if (a.dextra) ln_bwd_kernel<MV, false, true, DB><<<grid, 256, 0, stream>>>(a);          \
            else ln_bwd_kernel<MV, false, false, DB><<<grid, 256, 0, stream>>>(a); }
 #define CT_LNB(MV) case MV:                                                                   \
@@ -408,4 +442,13 @@ extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, co
   if (a.db_part) { parts[n] = a.db_part; outs[n++] = dbeta; }
   if (a.dbias_part) { parts[n] = a.dbias_part; outs[n++] = dbias; }
   return colsum_multi(parts, outs, n, grid, N, param_fp32, accumulate, stream);
+}
+
+extern "C" int ct_layernorm_bwd(const void* dy, const void* s, const void* g, const float* mean,
+                                const float* rstd, const void* dextra, void* ds, void* dx,
+                                float* part, void* dgamma, void* dbeta, void* dbias, int M, int N,
+                                int rms, int param_fp32, int accumulate, float p_drop,
+                                uint64_t seed, uint64_t offset, hipStream_t stream) {
+  return ct_layernorm_bwd2(dy, s, g, mean, rstd, dextra, ds, dx, part, dgamma, dbeta, dbias, M, N, rms, param_fp32,
+                           accumulate, p_drop, seed, offset, 0, nullptr, stream);
 }

@@ -96,6 +96,14 @@ def _zeroed_acc(device, F, rows=1):
 # FFN1's bias gradient from the FFN1 weight-gradient GEMM (all-ones MFMA on its dz operand,
 # as the QKV one) instead of column-sum atomics in the FFN data-gradient epilogue
 _FFN_BGRAD_IN_WGRAD = os.environ.get("CLOUDTIK_AMD_FFN_BGRAD_IN_WGRAD", "0") == "1"
+# LayerNorm backward from the block's OUTPUT y (xhat = (y - beta) / gamma; csrc/layernorm.hip
+# FROMY) instead of a saved copy of its input sum s: y is kept anyway as the next block's
+# input, so the forward writes one [tokens, hidden] tensor less (268 -> 201 MB per call on
+# BERT-large).  Off by default: measured on BERT-large (bench/ln_from_y_probe.py) the forward
+# gains 43.0 -> 34.8 us but the backward, which needs beta and 1 / gamma per element and drops
+# to 2 waves / SIMD to stay out of spills, loses 56.2 -> 65.2 us; the step is unchanged
+# (70.79 / 70.90 vs 70.86 / 70.94 ms, profiles/r6/SUMMARY.md).
+_LN_FROM_Y = os.environ.get("CLOUDTIK_AMD_LN_FROM_Y", "0") == "1"
 
 
 def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f, dgelu=False):
@@ -228,21 +236,25 @@ class _AttnBlockFn(torch.autograd.Function):
         a = _stream_mm("wo", o.view(B * S, H), Wo, False)
         if a is None:
             a = torch.mm(o.view(B * S, H), Wo.t())
-        y, s, mean, rstd = C.layernorm_fwd(a, bo, x2, g1, b1, eps, False, p_hid, seed_h, off_h)
-        ctx.save_for_backward(x2, qkv, o, lse, s, mean, rstd,
+        from_y = _LN_FROM_Y and b1 is not None
+        y, s, mean, rstd = C.layernorm_fwd(a, bo, x2, g1, b1, eps, False, p_hid, seed_h, off_h,
+                                           keep_sum=not from_y)
+        yv = y.view(B, S, H)
+        ctx.save_for_backward(x2, qkv, o, lse, yv if from_y else s, mean, rstd,
                               key_bias if key_bias is not None else torch.empty(0))
         ctx.params = (Wqkv, bqkv, Wo, bo, g1, b1)
         ctx.cfg = (B, S, H, nh, D, scale, p_attn, p_hid, seed_a, off_a, seed_h, off_h,
-                   key_bias is not None)
-        return y.view(B, S, H)
+                   key_bias is not None, from_y)
+        return yv
 
     @staticmethod
     def backward(ctx, dy):
         C = _C()
         x2, qkv, o, lse, s, mean, rstd, kb = ctx.saved_tensors
         Wqkv, bqkv, Wo, bo, g1, b1 = ctx.params
-        B, S, H, nh, D, scale, p_attn, p_hid, seed_a, off_a, seed_h, off_h, has_kb = ctx.cfg
+        B, S, H, nh, D, scale, p_attn, p_hid, seed_a, off_a, seed_h, off_h, has_kb, from_y = ctx.cfg
         dy2 = dy.reshape(B * S, H).contiguous()
+        s = s.view(B * S, H)
         dg1, fg1 = _vec_grad_out(g1)
         db1, fb1 = _vec_grad_out(b1)
         dbo, fbo = _vec_grad_out(bo)
@@ -251,7 +263,7 @@ class _AttnBlockFn(torch.autograd.Function):
         # backward: moving it into the projection's weight-gradient GEMM (all-ones MFMA) made the
         # LayerNorm pass 11 % faster but the GEMMs 1.5 ms per step slower
         ds, da = C.layernorm_bwd_into(dy2, s, g1, mean, rstd, False, dg1, db1, dbo, need_dx,
-                                      p_hid, seed_h, off_h)
+                                      p_hid, seed_h, off_h, beta_y=b1 if from_y else None)
         if not need_dx:
             da = ds
         _ready(*[p for p, f in ((g1, fg1), (b1, fb1), (bo, fbo)) if f])
@@ -298,18 +310,22 @@ class _FFNBlockFn(torch.autograd.Function):
         f = _stream_mm("ffn2", h, W2, False)
         if f is None:
             f = torch.mm(h, W2.t())
-        y, s, mean, rstd = C.layernorm_fwd(f, b2f, x2, g2, b2, eps, False, p_hid, seed_h, off_h)
-        ctx.save_for_backward(x2, z, h, s, mean, rstd)
+        from_y = _LN_FROM_Y and b2 is not None
+        y, s, mean, rstd = C.layernorm_fwd(f, b2f, x2, g2, b2, eps, False, p_hid, seed_h, off_h,
+                                           keep_sum=not from_y)
+        yv = y.view(B, S, H)
+        ctx.save_for_backward(x2, z, h, yv if from_y else s, mean, rstd)
         ctx.params = (W1, b1f, W2, b2f, g2, b2)
-        ctx.cfg = (B, S, H, p_hid, seed_h, off_h, kind)
-        return y.view(B, S, H)
+        ctx.cfg = (B, S, H, p_hid, seed_h, off_h, kind, from_y)
+        return yv
 
     @staticmethod
     def backward(ctx, dy):
         C = _C()
         x2, z, h, s, mean, rstd = ctx.saved_tensors
         W1, b1f, W2, b2f, g2, b2 = ctx.params
-        B, S, H, p_hid, seed_h, off_h, kind = ctx.cfg
+        B, S, H, p_hid, seed_h, off_h, kind, from_y = ctx.cfg
+        s = s.view(B * S, H)
         dgelu = kind == "dgelu"                 # z holds gelu'(pre-activation) itself
         zbias = None if kind is not None else b1f   # the bias gelu' still has to add to z
         dy2 = dy.reshape(B * S, H).contiguous()
@@ -318,7 +334,7 @@ class _FFNBlockFn(torch.autograd.Function):
         db2f, fb2f = _vec_grad_out(b2f)
         need_dx = p_hid > 0.0
         ds, df = C.layernorm_bwd_into(dy2, s, g2, mean, rstd, False, dg2, db2, db2f, need_dx,
-                                      p_hid, seed_h, off_h)
+                                      p_hid, seed_h, off_h, beta_y=b2 if from_y else None)
         if not need_dx:
             df = ds
         _ready(*[p for p, f in ((g2, fg2), (b2, fb2), (b2f, fb2f)) if f])

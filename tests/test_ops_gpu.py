@@ -43,6 +43,48 @@ def test_layernorm_fwd_bwd(cuda, N, fused):
         assert _rel(gk, xr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("N", [768, 1024])
+def test_layernorm_bwd_from_output(cuda, N):
+    """The output-based LayerNorm backward (xhat = (y - beta) / gamma, csrc/layernorm.hip FROMY;
+    what the BERT blocks run) against the fp32 reference, with gamma spread over [0.3, 1.7], beta
+    over [-1, 1], and one gamma exactly 0 (that channel: xhat 0, so its dgamma is 0)."""
+    C = ops.require_native()
+    torch.manual_seed(1)
+    M, p, eps = 333, 0.1, 1e-12
+    x = torch.randn(M, N, device=cuda).bfloat16()
+    res = torch.randn(M, N, device=cuda).bfloat16()
+    bias = (0.1 * torch.randn(N, device=cuda)).bfloat16()
+    g = (0.3 + 1.4 * torch.rand(N, device=cuda)).bfloat16()
+    g[5] = 0
+    b = (2 * torch.rand(N, device=cuda) - 1).bfloat16()
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    seed, off = 11, 4096
+    y, s, mean, rstd = C.layernorm_fwd(x, bias, res, g, b, eps, False, p, seed, off, keep_sum=False)
+    assert not s.defined() if hasattr(s, "defined") else s is None
+    outs = {}
+    for form in ("sum", "y"):
+        y2, s2, mean2, rstd2 = C.layernorm_fwd(x, bias, res, g, b, eps, False, p, seed, off, keep_sum=form == "sum")
+        assert torch.equal(y2, y)
+        dg, db, dbias = (torch.zeros(N, device=cuda) for _ in range(3))
+        ds, dx = C.layernorm_bwd_into(dy, y2 if form == "y" else s2, g, mean2, rstd2, False, dg, db, dbias, True,
+                                      p, seed, off, beta_y=b if form == "y" else None)
+        torch.cuda.synchronize()
+        outs[form] = (ds, dx, dg, db, dbias)
+    xs = [t.float().requires_grad_() for t in (x, g, b, res, bias)]
+    yr, _ = ref.layer_norm(xs[0], xs[1], xs[2], eps, xs[4], xs[3], p, seed, off)
+    yr.backward(dy.float())
+    keep = torch.ones(N, dtype=torch.bool, device=cuda)
+    keep[5] = False
+    ds, dx, dg, db, dbias = outs["y"]
+    assert torch.isfinite(ds.float()).all() and torch.isfinite(dx.float()).all()
+    assert _rel(ds, xs[3].grad) < 2e-2 and _rel(dx, xs[0].grad) < 2e-2
+    assert _rel(dg[keep], xs[1].grad[keep]) < 2e-2 and dg[5].item() == 0.0
+    assert _rel(db, xs[2].grad) < 2e-2 and _rel(dbias, xs[4].grad) < 2e-2
+    # and next to the saved-sum form, which the output form replaces
+    for a_, b_ in zip(outs["y"][:2], outs["sum"][:2]):
+        assert _rel(a_, b_) < 1e-2
+
+
 @pytest.mark.parametrize("act", [ops.ACT_GELU, ops.ACT_RELU])
 def test_bias_act(cuda, act):
     torch.manual_seed(0)
