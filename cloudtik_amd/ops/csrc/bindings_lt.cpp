@@ -378,6 +378,31 @@ bool gemm_pp(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, c10::optiona
   return rc == 0;
 }
 
+extern "C" int ct_gemm_w4(const void*, long, const void*, long, void*, long, int, int, int, int, int, const void*, void*,
+                          long, hipStream_t);
+
+// Four-wave MFMA GEMM (gemm_nt.hip gemm_w4_kernel): D = A @ B^T with epilogue 0 (plain), 5 (+ bias)
+// or 6 (D = gelu(. + bias), aux = gelu'(. + bias)).  False when the shape is unsupported.
+bool gemm_w4(at::Tensor A, at::Tensor B, at::Tensor D, int64_t epi, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> aux) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && D.is_cuda(), "gemm_w4: GPU tensors");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+              D.scalar_type() == at::kBFloat16, "gemm_w4: bf16 operands");
+  TORCH_CHECK(rowmajor_ok(A) && rowmajor_ok(B) && rowmajor_ok(D), "gemm_w4: 2-D row-major operands");
+  const long M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && D.size(0) == M && D.size(1) == N, "gemm_w4: shape mismatch");
+  const bool hb = bias.has_value() && bias->defined();
+  const bool ha = aux.has_value() && aux->defined();
+  if (hb) TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                      "gemm_w4: bias");
+  if (ha) TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && rowmajor_ok(*aux) && aux->size(0) == M &&
+                      aux->size(1) == N, "gemm_w4: aux");
+  int rc = ct_gemm_w4(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), D.data_ptr(), D.stride(0), (int)M, (int)N,
+                      (int)K, (int)epi, 0, hb ? bias->data_ptr() : nullptr, ha ? aux->data_ptr() : nullptr,
+                      ha ? aux->stride(0) : 0, at::hip::getCurrentHIPStream().stream());
+  return rc == 0;
+}
+
 extern "C" int ct_gemm_tn2(const void*, long, const void*, long, void*, long, int, int, long, int, int, float*,
                            hipStream_t);
 
@@ -425,6 +450,9 @@ void register_lt(pybind11::module& m) {
         pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("D"), pybind11::arg("epi") = 0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("aux") = pybind11::none(), pybind11::arg("wgs") = 0,
         pybind11::arg("eslots") = 4);
+  m.def("gemm_w4", &gemm_w4, "four-wave MFMA GEMM A @ B^T (128 x 128 per wave, AGPR-resident accumulators)",
+        pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("D"), pybind11::arg("epi") = 0,
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("aux") = pybind11::none());
   m.def("gemm_nn", &gemm_nn, "hand-written MFMA GEMM A @ B (B stored [K, N]) with fused epilogues");
   m.def("lt_matmul", &lt_matmul, "hipBLASLt matmul with epilogue (row-major semantics)");
   m.def("lt_bmm_tuned", &lt_bmm_tuned, "strided-batched hipBLASLt GEMM, algorithm picked by timing all solutions");

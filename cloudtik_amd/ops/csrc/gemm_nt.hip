@@ -394,7 +394,8 @@ __device__ __forceinline__ void nt_preload_z(const NtArgs& a, long mrow, long nc
   }
 }
 
-template <int EPI, bool BGRAD, int NJ>
+// ACC = false: the caller never accumulates into D (EPI 0), so no old-D registers are reserved
+template <int EPI, bool BGRAD, int NJ, bool ACC = true>
 __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[8][NJ], long mrow, long ncol,
                                             int lane, int split, NtEpiPre<NJ>& pre, int half = 0) {
   static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
@@ -437,7 +438,7 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
   // instead of one per row block (a two-row-ahead ring of 8-byte loads before: the EPI 7
   // epilogue cost 19.6 us per tile-round against 14.6 for EPI 6, profiles/r5/gemm_epilogue_probe.md).
   // The fragment registers of the K loop are dead here, so the 64 VGPRs come free.
-  constexpr bool RD = EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_MUL_AUX_BGRAD || EPI == NT_EPI_PLAIN;
+  constexpr bool RD = EPI == NT_EPI_DGELU_BGRAD || EPI == NT_EPI_MUL_AUX_BGRAD || (EPI == NT_EPI_PLAIN && ACC);
   u16x8 zin[RD ? 8 : 1][NJ / 2];
   if constexpr (RD) {
     const bool rd = EPI != NT_EPI_PLAIN || a.accumulate;
@@ -464,9 +465,9 @@ __device__ __forceinline__ void nt_epilogue(const NtArgs& a, const f32x4 (&acc)[
     } else if constexpr (EPI == NT_EPI_PLAIN) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        if (a.accumulate) {
+        if (ACC && a.accumulate) {
           u16x4 old, old2;
-          nt_pair_unswap(zin[i][j >> 1], old, old2);
+          nt_pair_unswap(zin[RD ? i : 0][RD ? (j >> 1) : 0], old, old2);
           if (j & 1) old = old2;
 #pragma unroll
           for (int r = 0; r < 4; ++r) out[j][r] = f2bf(acc[i][j][r] + bf2f(old[r]));
@@ -935,6 +936,171 @@ __global__ void __launch_bounds__(NT_THREADS, 1) gemm_nt_stream_kernel(NtArgs a,
   if (wr == 0) nt_bar();                                 // equal barrier counts for both groups
 }
 
+
+// nt_glds16s plus the wait states between v_readfirstlane and a VMEM instruction reading its SGPR
+// (s_nop 4, cdna_hip_programming.md §5.7 item 2): in the four-wave kernel hipcc keeps the staging
+// bases in VGPRs under SGPR pressure and re-reads them right before each DMA
+__device__ __forceinline__ void w4_glds16s(const void* sbase, unsigned voff, const char* lds_wave_base) {
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(nt_lds_void*)lds_wave_base);
+  const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)sbase) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)sbase >> 32)) << 32);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
+               : "memory", "m0");
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Four-wave variant (gemm_w4_kernel): the same 256 x 256 x 64 tile, LDS images, swizzles and
+// epilogues, but 4 waves of 128 x 128 each instead of 8 of 128 x 64.  Per K-tile a wave reads
+// 32 fragments for 128 MFMAs (0.25 per MFMA) where the 8-wave kernel reads 24 for 64 (0.375):
+// a third less LDS read traffic beside the LDS-DMA writes (profiles/r2/gemm_nt.md: the DMA
+// issue, not the schedule, is what costs the 8-wave kernel).  The 64 accumulator quads fill
+// all 256 AGPRs; through the builtin the register allocator rotated them through v_accvgpr
+// moves (92 per 128 MFMAs, r6 probe), so the MFMAs are inline asm with the accumulator bound
+// "+a": it stays in one AGPR quad for the whole kernel, dst == srcC.  One wave per SIMD, so
+// the wave interleaves its own fragment reads and DMA issue between MFMAs:
+//   K-tile t = two 32-deep k-steps; k-step 0 multiplies fragment set 0 while reading set 1
+//   (k-step 1 of the same LDS slot); then lgkmcnt(0) + vmcnt(0) + one barrier (stage t + 1 has
+//   landed, every wave is done reading slot t & 1); k-step 1 multiplies set 1 while issuing
+//   the DMA of stage t + 2 into slot t & 1 (front-loaded, one per MFMA) and reading set 0 of
+//   K-tile t + 1.  Two 64 KiB slots, one barrier per K-tile.
+// Hazards the compiler cannot see through the asm: the epilogue's AGPR reads wait out the last
+// MFMA (3 x s_nop 7 between sched_barriers), and the first k-step writes the accumulators with
+// srcC = 0 (a zeroing pass of v_accvgpr_write placed by the compiler next to the first MFMAs
+// broke the bias epilogues: profiles/r6/gemm_w4_four_wave.md).
+template <bool FIRST>
+__device__ __forceinline__ void w4_mfma(f32x4& c, const nt_s16x8& b, const nt_s16x8& a) {
+  if constexpr (FIRST)      // srcC = 0: the first k-step writes the accumulator (no zeroing pass)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(b), "v"(a));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+
+struct W4Frags {
+  nt_s16x8 a[8], b[8];
+};
+
+template <int DIAG, bool RD, bool DMA, bool FIRST = false>
+__device__ __forceinline__ void w4_kstep(f32x4 (&acc)[8][8], const W4Frags& cur, W4Frags& nxt, const char* rimg,
+                                         int ks, int wm, int wn, int lane, char* dimg,
+                                         const bf16_t* abase, const bf16_t* bbase, long lda, long ldb, long k0,
+                                         unsigned oa0, unsigned oa1, unsigned ob0, unsigned ob1, int wave) {
+  // 64 MFMAs in (i, j) order; DMA pieces after the first 16 (A pieces 0-7, B pieces 0-7), one
+  // fragment read after every third of the remaining 48
+#pragma unroll
+  for (int q = 0; q < 64; ++q) {
+    const int i = q >> 3, j = q & 7;
+    w4_mfma<FIRST>(acc[i][j], cur.b[j], cur.a[i]);
+    if constexpr (DIAG != 1 && DMA) {
+      if (q < 16) {
+        const int pc = q & 7;
+        if (q < 8) w4_glds16s(abase + 8 * pc * lda + k0, (pc & 1) ? oa1 : oa0, dimg + (8 * wave + pc) * 1024);
+        else w4_glds16s(bbase + 8 * pc * ldb + k0, (pc & 1) ? ob1 : ob0, dimg + 32768 + (8 * wave + pc) * 1024);
+      }
+    }
+    if (RD && q >= 16 && (q - 16) % 3 == 0 && (q - 16) / 3 < 16) {
+      // nt_frag with the row-block stride folded into immediates: the swizzle of row
+      // 128 w + 16 f + (lane & 15) does not depend on f
+      const int f = (q - 16) / 3;
+      const int lo = ((ks * 4 + (lane >> 4)) ^ (((lane & 15) >> 1) & 7)) << 4;
+      if (f < 8) nxt.a[f] = *(const nt_lds_s16x8*)(rimg + (wm * 128 + (lane & 15)) * NT_ROWB + lo + f * 16 * NT_ROWB);
+      else nxt.b[f - 8] = *(const nt_lds_s16x8*)(rimg + 32768 + (wn * 128 + (lane & 15)) * NT_ROWB + lo +
+                                                 (f - 8) * 16 * NT_ROWB);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// DIAG (timing only, wrong results): 1 = no DMA in the K loop, 2 = DMA issued, never waited for
+template <int EPI, bool BGRAD, int DIAG = 0>
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(NtArgs a) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * NT_BUF];    // 2 slots x (A 32 KiB | B 32 KiB)
+  const int tiles_n = a.N / NT_BN;
+  const int tiles = (a.M / NT_BM) * tiles_n;
+  const int L = xcd_remap(blockIdx.x, tiles);
+  int tm, tn;
+  if (a.group_m > 1) {
+    const int gsz = a.group_m * tiles_n;
+    const int g = L / gsz, r = L - g * gsz;
+    tm = g * a.group_m + r % a.group_m;
+    tn = r / a.group_m;
+  } else {
+    tm = L / tiles_n;
+    tn = L % tiles_n;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const long m0 = (long)tm * NT_BM, n0 = (long)tn * NT_BN;
+  const int nk = a.K / NT_BK;
+  // staging: wave w fills image rows 64 w .. 64 w + 63 of both operands (8 pieces of 8 rows)
+  const bf16_t* abase = a.A + (m0 + 64 * wave) * a.lda;
+  const bf16_t* bbase = a.B + (n0 + 64 * wave) * a.ldb;
+  const unsigned oa0 = nt_lane_off(a.lda, 0, lane), oa1 = nt_lane_off(a.lda, 1, lane);
+  const unsigned ob0 = nt_lane_off(a.ldb, 0, lane), ob1 = nt_lane_off(a.ldb, 1, lane);
+  auto stage = [&](int kt) {
+    char* img = lds + (kt & 1) * NT_BUF;
+    const long k0 = (long)kt * NT_BK;
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc)
+      w4_glds16s(abase + 8 * pc * a.lda + k0, (pc & 1) ? oa1 : oa0, img + (8 * wave + pc) * 1024);
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc)
+      w4_glds16s(bbase + 8 * pc * a.ldb + k0, (pc & 1) ? ob1 : ob0, img + 32768 + (8 * wave + pc) * 1024);
+  };
+
+  f32x4 acc[8][8];                                   // first written by the srcC = 0 k-step
+  const long emrow = m0 + wm * 128 + (lane & 15), encol = n0 + wn * 128 + (lane >> 4) * 4;
+  NtEpiPre<8> epre;
+  nt_preload_bias<EPI, 8>(a, encol, epre);
+
+  W4Frags s0, s1;
+  stage(0);
+  if (nk > 1) stage(1);
+  if (nk > 1) nt_vm<16>(); else nt_vm<0>();
+  nt_bar();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    s0.a[f] = nt_frag(lds, wm * 128 + 16 * f, 0, lane);
+    s0.b[f] = nt_frag(lds + 32768, wn * 128 + 16 * f, 0, lane);
+  }
+  // K-tile t: k-step 0 (set 0, reading set 1 from the same slot), the mid-tile wait + barrier,
+  // k-step 1 (set 1, DMA of stage t + 2, reading set 0 of K-tile t + 1).  The first K-tile
+  // starts the accumulators (srcC = 0), then the steady state, then the last two K-tiles
+  // without the DMA / the next-tile reads.
+#define W4_TILE(FIRST0, RD1, DMA1, WAITV)                                                          \
+  do {                                                                                               \
+    const char* img = lds + (t & 1) * NT_BUF;                                                        \
+    w4_kstep<DIAG, true, false, FIRST0>(acc, s0, s1, img, 1, wm, wn, lane, nullptr, abase, bbase,    \
+                                        a.lda, a.ldb, 0, oa0, oa1, ob0, ob1, wave);                  \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                               \
+    if constexpr (DIAG == 0 && WAITV) nt_vm<0>();                                                    \
+    nt_bar();                                                                                        \
+    w4_kstep<DIAG, RD1, DMA1>(acc, s1, s0, lds + ((t + 1) & 1) * NT_BUF, 0, wm, wn, lane,            \
+                              lds + (t & 1) * NT_BUF, abase, bbase, a.lda, a.ldb, (long)(t + 2) * NT_BK, \
+                              oa0, oa1, ob0, ob1, wave);                                             \
+  } while (0)
+  int t = 0;
+  if (nk == 1) {
+    W4_TILE(true, false, false, false);
+  } else {
+    if (nk == 2) W4_TILE(true, true, false, true);
+    else W4_TILE(true, true, true, true);
+    for (t = 1; t < nk - 2; ++t) W4_TILE(false, true, true, true);
+    if (nk >= 3) {
+      W4_TILE(false, true, false, true);
+      ++t;
+    }
+    W4_TILE(false, false, false, false);
+  }
+#undef W4_TILE
+  // the last MFMAs -> the epilogue's AGPR reads: the scheduler may not move the reads above
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  nt_epilogue<EPI, BGRAD, 8, false>(a, acc, emrow, encol, lane, 0, epre);
+}
+
 }  // namespace ct
 
 using namespace ct;
@@ -1078,5 +1244,36 @@ extern "C" int ct_gemm_tn2(const void* A, long lda, const void* B, long ldb, voi
     if (splits > 1) gemm_nt_kernel<NT_EPI_F32_SLAB, false, 0, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
     else gemm_nt_kernel<NT_EPI_PLAIN, false, 0, 1><<<(int)blocks, NT_THREADS, 0, stream>>>(a);
   }
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}
+
+// Four-wave GEMM (gemm_w4_kernel): D[M,N] = A[M,K] . B[N,K]^T with epilogue 0 (plain; accumulate:
+// D += result), 5 (+ bias) or 6 (D = gelu(. + bias), aux = gelu'(. + bias)).  Nonzero (nothing
+// launched) when unsupported.  CLOUDTIK_AMD_GEMM_W4_DIAG=1 / 2: timing diagnostics (no DMA / DMA
+// never waited for; wrong results).  Measured slower than gemm_nt_kernel: profiles/r6/gemm_w4_four_wave.md.
+extern "C" int ct_gemm_w4(const void* A, long lda, const void* B, long ldb, void* D, long ldd, int M, int N, int K,
+                          int epi, int accumulate, const void* bias, void* aux, long ldaux, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % NT_BM || N % NT_BN || K % NT_BK) return 1;
+  if (lda % 8 || ldb % 8 || ldd % 8 || lda < K || ldb < K || ldd < N) return 2;
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15) || ((uintptr_t)D & 15)) return 3;
+  if ((epi == 5 || epi == 6) && (!bias || ((uintptr_t)bias & 7))) return 4;
+  if (epi == 6 && (!aux || ((uintptr_t)aux & 15) || ldaux % 8 || ldaux < N)) return 4;
+  if (epi != 0 && epi != 5 && epi != 6) return 6;
+  if (accumulate) return 6;                           // (the accumulating epilogue is not instantiated)
+  const long tiles = (long)(M / NT_BM) * (N / NT_BN);
+  if (tiles > (1L << 30)) return 5;
+  static const int gm_env = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_GROUP_M"); return e ? atoi(e) : 4; }();
+  const int gm = (gm_env > 1 && (M / NT_BM) % gm_env == 0) ? gm_env : 1;
+  NtArgs a{(const bf16_t*)A, (const bf16_t*)B, (bf16_t*)D, (const bf16_t*)bias, (bf16_t*)aux, nullptr, nullptr,
+           nullptr, lda, ldb, ldd, ldaux, 0, M, N, K, 0, 0, gm, 1};
+  static const int diag = [] { const char* e = getenv("CLOUDTIK_AMD_GEMM_W4_DIAG"); return e ? atoi(e) : 0; }();
+  if (diag == 1 || diag == 2) {
+    if (diag == 1) gemm_w4_kernel<0, false, 1><<<(int)tiles, 256, 0, stream>>>(a);
+    else gemm_w4_kernel<0, false, 2><<<(int)tiles, 256, 0, stream>>>(a);
+    return 0;
+  }
+  if (epi == 5) gemm_w4_kernel<NT_EPI_BIAS, false><<<(int)tiles, 256, 0, stream>>>(a);
+  else if (epi == 6) gemm_w4_kernel<NT_EPI_BIAS_GELU_DAUX, false><<<(int)tiles, 256, 0, stream>>>(a);
+  else gemm_w4_kernel<NT_EPI_PLAIN, false><<<(int)tiles, 256, 0, stream>>>(a);
   return hipGetLastError() == hipSuccess ? 0 : 7;
 }
