@@ -94,13 +94,22 @@ __device__ __forceinline__ void cv_glds16(const void* g, const char* lds_wave_ba
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(la) : "memory", "m0");
 }
 
-// LDS-DMA addressed as a wave-uniform 64-bit base (SGPRs) + a per-lane 32-bit byte offset
+// LDS-DMA addressed as a wave-uniform 64-bit base (SGPRs) + a per-lane 32-bit byte offset.
+// PAD: 5 wait states between the M0 write and the load instead of 1, which also covers a base
+// SGPR that a VALU (v_readfirstlane / v_readlane of a spilled SGPR) wrote just before the
+// statement -- hipcc pads nothing inside asm (cdna_hip_programming.md §5.7 item 2).  The r6 audit
+// of the compiled kernels (profiles/r6/SUMMARY.md) found that pattern in the streamed kernel only.
+template <bool PAD = false>
 __device__ __forceinline__ void cv_glds16s(const void* sbase, unsigned voff, const char* lds_wave_base) {
   const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(cv_lds_void*)lds_wave_base);
   const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)sbase) |
                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)sbase >> 32)) << 32);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
-               : "memory", "m0");
+  if constexpr (PAD)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
+                 : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sb), "s"(la)
+                 : "memory", "m0");
 }
 
 // LDS-DMA by buffer load: 32-bit per-lane byte offset into a buffer resource whose range check
@@ -599,7 +608,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN, WPC) conv_stream_kernel(ConvAr
     }
     const long k0 = (long)t * cpt * 64 + c0;
 #pragma unroll
-    for (int j = 0; j < IB; ++j) cv_glds16s(wbase[j] + k0, woff[(wave * IB + j) & 1], Bs + (wave * IB + j) * 1024);
+    for (int j = 0; j < IB; ++j) cv_glds16s<true>(wbase[j] + k0, woff[(wave * IB + j) & 1], Bs + (wave * IB + j) * 1024);
     ++cg;
     if (++ck == KT) {
       ck = 0;

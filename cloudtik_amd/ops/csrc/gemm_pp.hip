@@ -330,6 +330,9 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(PpArgs a) {
         const long ncl = n0 + wc * 64 + (lane >> 4) * 4;
         float bv[4][4] = {};
         if constexpr (EPI != PP_EPI_PLAIN) {
+          // the hand-counted waits of the K loop have retired the asm bias loads by here; naming
+          // the registers keeps every consumer below this point (cdna_hip_programming.md §5.7 1(ii))
+          asm volatile("" : "+v"(braw[0]), "+v"(braw[1]), "+v"(braw[2]), "+v"(braw[3]));
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const u16x4 b4 = __builtin_bit_cast(u16x4, braw[j]);
