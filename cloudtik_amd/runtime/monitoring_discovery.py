@@ -276,7 +276,7 @@ class DiscoverDataSources(PullJob):
 
     def wanted(self) -> Dict[str, Dict[str, Any]]:
         out = {}
-        for inst in self.query():
+        for inst in sorted(self.query(), key=lambda i: (i["name"], i["host"], int(i["port"]))):
             meta = inst.get("meta") or {}
             name = data_source_name(inst["name"], meta.get("cloudtik-cluster"))
             if name in out:            # several servers of one cluster: the first (sorted) wins
@@ -287,7 +287,13 @@ class DiscoverDataSources(PullJob):
     def pull(self):
         want = self.wanted()
         have = {d["name"]: d for d in (self.http("GET", f"{self.admin}/api/datasources", None, self.headers) or [])}
-        for name in sorted(set(want) - set(have)):
+        for name in sorted(want):
+            old = have.get(name)
+            if old is not None:
+                if old.get("url") == want[name]["url"] or not (old.get("jsonData") or {}).get(AUTO_CREATED):
+                    continue            # up to date, or not ours
+                # ours, but the server moved: replace it
+                self.http("DELETE", f"{self.admin}/api/datasources/name/{name}", None, self.headers)
             self.http("POST", f"{self.admin}/api/datasources", want[name], self.headers)
             logger.info("grafana data source %s added: %s", name, want[name]["url"])
         for name, d in sorted(have.items()):

@@ -182,6 +182,13 @@ def test_grafana_data_sources_follow_prometheus_servers():
     n = len(g.calls)
     job.pull()
     assert [c[0] for c in g.calls[n:]] == ["GET"]                         # steady: only the listing
+    rows[0] = _svc("prometheus", "10.0.0.9", 9090, "c1")                  # c1's server moved
+    job.pull()
+    assert g.ds["prometheus-c1"]["url"] == "http://10.0.0.9:9090" and "manual" in g.ds
+    g.ds["manual"]["url"] = "http://y"
+    rows.append(_svc("manual", "10.2.0.1", 9090, None))                    # same name as a data source not ours
+    job.pull()
+    assert g.ds["manual"]["url"] == "http://y"                            # never replaced
 
 
 def test_grafana_scopes(tmp_path, monkeypatch):
