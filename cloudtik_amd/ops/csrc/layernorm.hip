@@ -17,6 +17,7 @@
 //     cross-row reduction = [grid x N] fp32 partials + one column-sum kernel (no atomics,
 //     bitwise reproducible).
 #include "common.h"
+#include <cstdlib>
 
 namespace ct {
 
@@ -121,7 +122,7 @@ struct LnBwdArgs {
 // LayerNorm): xhat = (y - beta) / gamma.  The forward then writes no copy of its input sum s --
 // y is kept anyway (the next layer's input) -- a quarter of the forward's HBM bytes.  A channel
 // whose gamma is exactly 0 gets xhat 0 (its y carries no information about x).
-template <int MAXV, bool RMS, bool EXTRA, bool DBIAS, bool FROMY = false>
+template <int MAXV, bool RMS, bool EXTRA, bool DBIAS, bool FROMY = false, bool PF2 = false>
 __global__ __launch_bounds__(256, MAXV <= 2 ? ((FROMY && DBIAS) ? 2 : 3) : (DBIAS ? 1 : 2)) void ln_bwd_kernel(LnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float red[4][512];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -151,34 +152,31 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? ((FROMY && DBIAS) ? 2 : 3) : (DBIA
 #pragma unroll
     for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; if (DBIAS) dbi[i][j] = 0.f; }
   }
-  // Software pipeline: the s / dy / dextra rows (and mean, rstd) of the NEXT row are in
-  // flight while this row's reductions and stores run -- the kernel is latency bound with
-  // one row per wave otherwise (measured 3.9 TB/s effective on MI355X before this change).
+  // Software pipeline: the s / dy / dextra rows (and mean, rstd) of later rows are in flight
+  // while this row's reductions and stores run -- the kernel is latency bound with one row per
+  // wave otherwise (measured 3.9 TB/s effective on MI355X before the first prefetch).
   const int stride = gridDim.x * wpb;
   int row = blockIdx.x * wpb + wid;
-  u16x8 nsv[MAXV], ndv[MAXV], nev[MAXV];
-  float nmean = 0.f, nrstd = 0.f;
-  auto prefetch = [&](int r) {
-    if (r >= a.M) return;
+  // Loads are unconditional (row and column clamped into range; the clamped copies are never
+  // used): with a branch around them the compiler's wait-count merge at the join waited for
+  // EVERY outstanding load (vmcnt(0)) before the first use, so rows prefetched further ahead
+  // were waited for too.
+  auto load = [&](u16x8 (&sv)[MAXV], u16x8 (&dv)[MAXV], u16x8 (&ev)[MAXV], float& mn, float& rs, int r) {
+    r = min(r, a.M - 1);
     const u16x8* sr = reinterpret_cast<const u16x8*>(a.s + (size_t)r * N);
     const u16x8* dyr = reinterpret_cast<const u16x8*>(a.dy + (size_t)r * N);
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
-      const int c = lane + i * 64;
-      nsv[i] = c < nvec ? sr[c] : u16x8(0);
-      ndv[i] = c < nvec ? dyr[c] : u16x8(0);
-      if (EXTRA) nev[i] = c < nvec ? reinterpret_cast<const u16x8*>(a.dextra + (size_t)r * N)[c] : u16x8(0);
+      const int c = min(lane + i * 64, nvec - 1);
+      sv[i] = sr[c];
+      dv[i] = dyr[c];
+      if (EXTRA) ev[i] = reinterpret_cast<const u16x8*>(a.dextra + (size_t)r * N)[c];
     }
-    nmean = (RMS || FROMY) ? 0.f : a.mean[r];
-    nrstd = a.rstd[r];
+    mn = (RMS || FROMY) ? 0.f : a.mean[r];
+    rs = a.rstd[r];
   };
-  prefetch(row);
-  for (; row < a.M; row += stride) {
-    u16x8 csv[MAXV], cdv[MAXV], cev[MAXV];
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i) { csv[i] = nsv[i]; cdv[i] = ndv[i]; if (EXTRA) cev[i] = nev[i]; }
-    const float mean = nmean, rstd = nrstd;
-    prefetch(row + stride);
+  auto process = [&](const u16x8 (&csv)[MAXV], const u16x8 (&cdv)[MAXV], const u16x8 (&cev)[MAXV],
+                     const float mean, const float rstd, const int row) {
     // pass 1: row sums; xhat and dy*gamma are recomputed in pass 2 from the raw bf16
     // registers instead of being kept live (keeps the kernel at 3 waves / SIMD)
     float s1 = 0.f, s2 = 0.f;
@@ -232,6 +230,36 @@ __global__ __launch_bounds__(256, MAXV <= 2 ? ((FROMY && DBIAS) ? 2 : 3) : (DBIA
         if (a.ds) reinterpret_cast<u16x8*>(a.ds + (size_t)row * N)[c] = o;
         if (a.dx) reinterpret_cast<u16x8*>(a.dx + (size_t)row * N)[c] = od;
       }
+    }
+  };
+  if constexpr (PF2) {
+    // two register sets that alternate: while row r is processed, row r + stride's loads are
+    // outstanding, and row r + 2 stride's are issued as soon as r's registers are free -- two
+    // rows in flight at the wait instead of one, for no more registers than load-then-copy
+    u16x8 sA[MAXV], dA[MAXV], eA[MAXV], sB[MAXV], dB[MAXV], eB[MAXV];
+    float mA = 0.f, rA = 0.f, mB = 0.f, rB = 0.f;
+    load(sA, dA, eA, mA, rA, row);
+    load(sB, dB, eB, mB, rB, row + stride);
+    while (row < a.M) {
+      process(sA, dA, eA, mA, rA, row);
+      load(sA, dA, eA, mA, rA, row + 2 * stride);
+      row += stride;
+      if (row >= a.M) break;
+      process(sB, dB, eB, mB, rB, row);
+      load(sB, dB, eB, mB, rB, row + 2 * stride);
+      row += stride;
+    }
+  } else {
+    u16x8 nsv[MAXV], ndv[MAXV], nev[MAXV];
+    float nmean = 0.f, nrstd = 0.f;
+    load(nsv, ndv, nev, nmean, nrstd, row);
+    for (; row < a.M; row += stride) {
+      u16x8 csv[MAXV], cdv[MAXV], cev[MAXV];
+#pragma unroll
+      for (int i = 0; i < MAXV; ++i) { csv[i] = nsv[i]; cdv[i] = ndv[i]; if (EXTRA) cev[i] = nev[i]; }
+      const float mean = nmean, rstd = nrstd;
+      load(nsv, ndv, nev, nmean, nrstd, row + stride);
+      process(csv, cdv, cev, mean, rstd, row);
     }
   }
   // reduce the block's waves through LDS, 512 columns at a time.  A lane's 8 columns go in as
@@ -419,11 +447,15 @@ extern "C" int ct_layernorm_bwd2(const void* dy, const void* s, const void* g, c
   a.scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed; a.offset = offset;
   const int mv = (N / 8 + 63) / 64;
+  // two rows in flight per wave (PF2) or one (CLOUDTIK_AMD_LN_BWD_PF2=0)
+  static const bool pf2 = [] { const char* e = getenv("CLOUDTIK_AMD_LN_BWD_PF2"); return !e || e[0] != '0'; }();
 #define CT_LNB2(MV, DB)                                                                       \
     if (rms) { if (a.dextra) ln_bwd_kernel<MV, true, true, DB><<<grid, 256, 0, stream>>>(a);       \
                else ln_bwd_kernel<MV, true, false, DB><<<grid, 256, 0, stream>>>(a); }               \
     else if (from_y) { if (a.dextra) ln_bwd_kernel<MV, false, true, DB, true><<<grid, 256, 0, stream>>>(a); \
            else ln_bwd_kernel<MV, false, false, DB, true><<<grid, 256, 0, stream>>>(a); }            \
+    else if (pf2) { if (a.dextra) ln_bwd_kernel<MV, false, true, DB, false, true><<<grid, 256, 0, stream>>>(a); \
+           else ln_bwd_kernel<MV, false, false, DB, false, true><<<grid, 256, 0, stream>>>(a); }     \
     else { if (a.dextra) ln_bwd_kernel<MV, false, true, DB><<<grid, 256, 0, stream>>>(a);          \
            else ln_bwd_kernel<MV, false, false, DB><<<grid, 256, 0, stream>>>(a); }
 #define CT_LNB(MV) case MV:                                                                   \

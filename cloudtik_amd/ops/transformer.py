@@ -99,11 +99,13 @@ _FFN_BGRAD_IN_WGRAD = os.environ.get("CLOUDTIK_AMD_FFN_BGRAD_IN_WGRAD", "0") == 
 # LayerNorm backward from the block's OUTPUT y (xhat = (y - beta) / gamma; csrc/layernorm.hip
 # FROMY) instead of a saved copy of its input sum s: y is kept anyway as the next block's
 # input, so the forward writes one [tokens, hidden] tensor less (268 -> 201 MB per call on
-# BERT-large).  Off by default: measured on BERT-large (bench/ln_from_y_probe.py) the forward
-# gains 43.0 -> 34.8 us but the backward, which needs beta and 1 / gamma per element and drops
-# to 2 waves / SIMD to stay out of spills, loses 56.2 -> 65.2 us; the step is unchanged
-# (70.79 / 70.90 vs 70.86 / 70.94 ms, profiles/r6/SUMMARY.md).
-_LN_FROM_Y = os.environ.get("CLOUDTIK_AMD_LN_FROM_Y", "0") == "1"
+# BERT-large).  On by default since the backward's loads became unconditional (clamped
+# addresses, so the compiler's wait counts no longer drain every prefetched row): BERT-large
+# (bench/ln_from_y_probe.py) forward 42 -> 35 us, backward 60 us either way, step 70.85 ->
+# 70.50 ms (3 interleaved rounds, profiles/r6/SUMMARY.md).  A channel whose gamma is exactly 0
+# gets xhat 0 there (its y carries no information about x), so its dgamma is 0: set
+# CLOUDTIK_AMD_LN_FROM_Y=0 for models that zero-initialise LayerNorm gammas.
+_LN_FROM_Y = os.environ.get("CLOUDTIK_AMD_LN_FROM_Y", "1") == "1"
 
 
 def _fused_ffn_dgrad(C, df, W2, z, b1f, db1f, dgelu=False):
