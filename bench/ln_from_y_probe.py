@@ -30,11 +30,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--p", type=float, default=0.1, help="hidden dropout probability")
     a = ap.parse_args()
     from cloudtik_amd import ops
     C = ops.require_native()
     dev = torch.device("cuda")
-    M, N, p = 32768, 1024, 0.1
+    M, N, p = 32768, 1024, a.p
     g = torch.Generator(device="cpu").manual_seed(0)
     mk = lambda *sh: torch.randn(*sh, generator=g).to(dev, torch.bfloat16)  # noqa: E731
     x, res, dy = mk(M, N), mk(M, N), mk(M, N)
