@@ -94,8 +94,10 @@ def _zeroed_acc(device, F, rows=1):
 
 
 # FFN1's bias gradient from the FFN1 weight-gradient GEMM (all-ones MFMA on its dz operand,
-# as the QKV one) instead of column-sum atomics in the FFN data-gradient epilogue
-_FFN_BGRAD_IN_WGRAD = os.environ.get("CLOUDTIK_AMD_FFN_BGRAD_IN_WGRAD", "0") == "1"
+# as the QKV one) instead of column-sum atomics in the FFN data-gradient epilogue.  On by
+# default: BERT-large 71.39 / 71.42 / 71.51 -> 71.34 / 71.33 / 71.43 ms/step (3 interleaved
+# rounds, profiles/r6/SUMMARY.md), and the bias gradient no longer depends on atomic order
+_FFN_BGRAD_IN_WGRAD = os.environ.get("CLOUDTIK_AMD_FFN_BGRAD_IN_WGRAD", "1") == "1"
 # LayerNorm backward from the block's OUTPUT y (xhat = (y - beta) / gamma; csrc/layernorm.hip
 # FROMY) instead of a saved copy of its input sum s: y is kept anyway as the next block's
 # input, so the forward writes one [tokens, hidden] tensor less (268 -> 201 MB per call on
