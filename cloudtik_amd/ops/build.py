@@ -114,7 +114,12 @@ def build_ops(force=False, jobs=None, verbose=True):
                 o = fu.result()
                 if verbose:
                     print("  built", os.path.basename(o), flush=True)
-    if tasks or force or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+    # the object set of the last link, next to the library: a source reverted to content built
+    # earlier maps to an OLDER cached object, which an mtime comparison would not relink
+    manifest = out + ".objs"
+    linked = open(manifest).read().split("\n") if os.path.exists(manifest) else None
+    stale = linked != [os.path.basename(o) for o in objs]
+    if tasks or force or stale or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
         link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
                 *[f"-L{p}" for p in lib], "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
                 "-ltorch_hip", "-ltorch_python",
@@ -124,6 +129,8 @@ def build_ops(force=False, jobs=None, verbose=True):
                 *[f"-Wl,-rpath,{p}" for p in lib if "torch" in p]]
         _run(link)
         os.replace(out + ".tmp", out)
+        with open(manifest, "w") as f:
+            f.write("\n".join(os.path.basename(o) for o in objs))
         if verbose:
             print("[cloudtik_amd.build] linked", out, flush=True)
     return out

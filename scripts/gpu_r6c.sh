@@ -4,7 +4,7 @@
 # r5 "mixed routing" stall configuration, gloo_stall.md), bucket waits > 50 ms printed.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O="$R/gpurun_out/r6c"; mkdir -p "$O"
+O="$R/gpurun_out/${TAG:-r6c}"; mkdir -p "$O"
 cd "$R"
 timeout -k 10 300 python -u -m pytest tests/test_ddp_gloo.py tests/test_bucket_ready_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > "$O/ddp_gpu.txt" 2>&1 || { tail -30 "$O/ddp_gpu.txt"; exit 1; }
 tail -1 "$O/ddp_gpu.txt"
