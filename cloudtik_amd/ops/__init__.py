@@ -36,6 +36,29 @@ except Exception as e:  # pragma: no cover - depends on build state
     _C_ERR = e
 
 
+def _check_build_current():
+    """The library must have been linked from the sources in this tree: a stale ``.so`` (sources
+    edited, or reverted, without a rebuild) would run other kernels than the ones the tree
+    shows.  Warns; ``CLOUDTIK_AMD_STRICT_BUILD=1`` raises instead."""
+    if _C is None:
+        return
+    try:
+        from .build import stale_sources
+        stale = stale_sources()
+    except Exception:  # noqa: BLE001 - a missing csrc dir (installed package) is not an error
+        return
+    if stale:
+        msg = ("cloudtik_amd: the in-tree HIP library was built from other sources than "
+               f"{', '.join(stale[:6])}{' ...' if len(stale) > 6 else ''}; run `python -m cloudtik_amd.ops.build`")
+        if os.environ.get("CLOUDTIK_AMD_STRICT_BUILD", "0") == "1":
+            raise RuntimeError(msg)
+        import warnings
+        warnings.warn(msg, RuntimeWarning, stacklevel=2)
+
+
+_check_build_current()
+
+
 def native_available() -> bool:
     return _C is not None
 

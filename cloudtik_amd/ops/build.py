@@ -61,6 +61,35 @@ def _hash(paths, flags):
     return h.hexdigest()[:16]
 
 
+def source_digest(d=None):
+    """{file name: sha1} of every source and header of the op library (path-independent, so
+    the GPU box, which sees the tree under another root, computes the same digest)."""
+    d = d or CSRC
+    out = {}
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".h", ".hpp", ".cuh")):
+            with open(os.path.join(d, f), "rb") as fh:
+                out[f] = hashlib.sha1(fh.read()).hexdigest()
+    return out
+
+
+def manifest_path():
+    return os.path.join(HERE, "_C" + EXT_SUFFIX) + ".objs"
+
+
+def stale_sources():
+    """Sources whose content differs from what the in-tree library was linked from (empty:
+    current), or None when the library has no manifest (built by an older build driver)."""
+    import json
+    try:
+        with open(manifest_path()) as f:
+            m = json.load(f)
+    except (OSError, ValueError):
+        return None
+    built, now = m.get("sources", {}), source_digest()
+    return sorted(f for f in set(built) | set(now) if built.get(f) != now.get(f))
+
+
 def _headers(d):
     return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp", ".cuh")))
 
@@ -116,8 +145,13 @@ def build_ops(force=False, jobs=None, verbose=True):
                     print("  built", os.path.basename(o), flush=True)
     # the object set of the last link, next to the library: a source reverted to content built
     # earlier maps to an OLDER cached object, which an mtime comparison would not relink
-    manifest = out + ".objs"
-    linked = open(manifest).read().split("\n") if os.path.exists(manifest) else None
+    import json
+    manifest = manifest_path()
+    try:
+        with open(manifest) as f:
+            linked = json.load(f).get("objs")
+    except (OSError, ValueError):
+        linked = None
     stale = linked != [os.path.basename(o) for o in objs]
     if tasks or force or stale or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
         link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
@@ -130,7 +164,7 @@ def build_ops(force=False, jobs=None, verbose=True):
         _run(link)
         os.replace(out + ".tmp", out)
         with open(manifest, "w") as f:
-            f.write("\n".join(os.path.basename(o) for o in objs))
+            json.dump({"objs": [os.path.basename(o) for o in objs], "sources": source_digest()}, f, indent=0)
         if verbose:
             print("[cloudtik_amd.build] linked", out, flush=True)
     return out
