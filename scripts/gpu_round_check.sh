@@ -11,6 +11,8 @@ cd "$R"
 H=$(mktemp -d /tmp/fresh.XXXXXX)
 export HOME=$H XDG_CACHE_HOME=$H/.cache
 unset MIOPEN_USER_DB_PATH
+# the shipped library must be the one built from these sources (no GPU touched by this check)
+python -c "from cloudtik_amd.ops.build import stale_sources as s; r = s(); assert r == [], r" || exit 1
 # the bench runs FIRST, as the first GPU process of a fresh box (the driver's condition)
 timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.log" 2> "$O/bench.err" \
  && tail -1 "$O/bench.log" | cut -c1-3000 \
