@@ -43,6 +43,9 @@ import torch
 import torch.distributed as dist
 
 
+_COMM_STREAMS = {}          # device -> the collectives' stream (GradBucketer.comm_stream)
+
+
 class GradBucketer:
     def __init__(self, space, group=None, bucket_mb: float = 64.0, overlap: bool = True,
                  comm_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None,
@@ -176,9 +179,16 @@ class GradBucketer:
         return self._side
 
     def comm_stream(self):
-        """The stream the collectives are ordered on (CUDA, world > 1), created on first use."""
+        """The stream the collectives are ordered on (CUDA, world > 1): ONE per device, shared
+        by every bucketer of the process (two models' bucketers used to hold a stream each;
+        the process group orders their collectives anyway, and every extra stream shares one
+        of the few hardware queues with the compute streams)."""
         if self._comm_stream is None:
-            self._comm_stream = torch.cuda.Stream(device=self.space.grad.device)
+            dev = self.space.grad.device
+            s = _COMM_STREAMS.get(dev)
+            if s is None:
+                s = _COMM_STREAMS[dev] = torch.cuda.Stream(device=dev)
+            self._comm_stream = s
         return self._comm_stream
 
     def _launch(self, b):
