@@ -29,6 +29,7 @@ run("plain")
 w = m.backbone.fpn.output[0].weight
 print("before opt: fpn weight CL", w.is_contiguous(memory_format=torch.channels_last), flush=True)
 opt = build_optimizer("sgd", m, 0.01, 1e-4, momentum=0.9)
+g = w.grad if w.grad is not None else getattr(w, "_ct_flat_view", None)   # flat-buffer view
 print("after opt: fpn weight CL", w.is_contiguous(memory_format=torch.channels_last),
-      "grad CL", w.grad.is_contiguous(memory_format=torch.channels_last), flush=True)
+      "grad CL", None if g is None else g.is_contiguous(memory_format=torch.channels_last), flush=True)
 run("flat-opt", opt, n=8)

@@ -122,6 +122,12 @@ class DLRM(nn.Module):
         F = len(cfg.table_sizes) + 1
         # dense layers first: their init must not depend on how many table rows this rank owns
         self.top = _mlp([E + F * (F - 1) // 2] + cfg.top_mlp, device)
+        # MLP weight gradients in line, not on the side stream: the GEMMs are small and the
+        # step is launch-bound, so the cross-stream events cost more than the overlap returns
+        # (1.20-1.32 vs 1.56-1.90 ms per 2048-sample step, 3 interleaved rounds;
+        # profiles/r6/SUMMARY.md)
+        from cloudtik_amd.ops.linear import use_wgrad_side_stream
+        use_wgrad_side_stream(list(self.bottom.parameters()) + list(self.top.parameters()), False)
         # tables are seeded per table so any sharding produces identical weights
         self.emb = EmbeddingBagCollection([cfg.table_sizes[t] for t in self.local_tables], E, device=device,
                                           sparse_lr=cfg.sparse_lr)
